@@ -1,0 +1,143 @@
+/*
+ * edverify.h -- C ABI of libplenum_edverify.so, the MI355X (gfx950) batched
+ * Ed25519 request-signature engine behind Plenum's client authenticator.
+ *
+ * What it replaces (reference interfaces, /root/reference):
+ *   stp_core/crypto/nacl_wrappers.py:232-242  Verifier.verify(signature, msg) -> bool
+ *   stp_core/crypto/nacl_wrappers.py:100-108  VerifyKey.verify(sig + msg) ->
+ *                                             libnacl.crypto_sign_open(sm, pk)
+ *   (libsodium 1.0.18 crypto_sign_open / crypto_sign_verify_detached:
+ *    int crypto_sign_verify_detached(const unsigned char *sig,
+ *        const unsigned char *m, unsigned long long mlen, const unsigned char *pk);
+ *    0 = accept, -1 = reject)
+ *   called once per request from NaclAuthNr.authenticate
+ *   (plenum/server/client_authn.py:99-102); here one call covers a batch.
+ *
+ *   plenum/server/quorums.py:15-32 + plenum/server/models.py:21-37
+ *   (Quorums thresholds, TrackedMsgs distinct-voter sets) -> edv_tally_*.
+ *
+ * Conventions
+ *   - Every function returns 0 on success or a negative EDV_E* code; the
+ *     message for the last failure on the calling thread is edv_last_error().
+ *     No C++ exception crosses this boundary.  A call either completes or
+ *     fails as a whole (no partial results).
+ *   - Host-pointer entry points (no _device suffix): the caller owns its
+ *     buffers; the library stages them through its own device buffers and
+ *     returns when the result is in the caller's buffer.
+ *   - _device entry points take device pointers and an optional hipStream_t
+ *     (NULL = the context's stream) and are asynchronous.
+ *   - Bitmasks: bit i of the mask is bit (i % 8) of byte (i / 8), i.e.
+ *     little-endian 64-bit words of wave ballots.  1 = libsodium returns 0.
+ *   - Threading: one context per GPU; calls on one context are serialised by
+ *     the caller (Plenum's node is single-threaded asyncio).
+ */
+#ifndef PLENUM_EDVERIFY_H
+#define PLENUM_EDVERIFY_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EDV_OK 0
+#define EDV_EINVAL -1   /* bad argument (NULL pointer, n too large, ...) */
+#define EDV_EHIP -2     /* HIP runtime error (message has the hipError string) */
+#define EDV_ENOMEM -3   /* device or host allocation failed */
+#define EDV_ENODEV -4   /* no gfx950 device / device index out of range */
+
+typedef struct edv_ctx edv_ctx;
+
+/* Library/version info. */
+const char *edv_version(void);
+const char *edv_last_error(void);
+int edv_device_count(void);
+
+/* Create a context bound to HIP device `device` (one stream, lazily grown
+ * device staging buffers).  Returns NULL on failure (see edv_last_error()). */
+edv_ctx *edv_create(int device);
+void edv_destroy(edv_ctx *ctx);
+/* Block until all work queued on the context stream has finished. */
+int edv_synchronize(edv_ctx *ctx);
+
+/* ---------------------------------------------------------------- verify */
+
+/* libsodium crypto_sign_verify_detached over a batch.
+ *   sig64   : n * 64 bytes (R || S per item)
+ *   pk32    : n * 32 bytes
+ *   msgs    : concatenated messages; item i is msgs[msg_off[i] .. msg_off[i+1])
+ *   msg_off : n + 1 offsets (msg_off[0] need not be 0)
+ *   accept_bits : (n + 7) / 8 bytes out.
+ * Replaces n calls of Verifier.verify (nacl_wrappers.py:232-242). */
+int edv_verify_batch(edv_ctx *ctx, const uint8_t *sig64, const uint8_t *pk32, const uint8_t *msgs,
+                     const uint64_t *msg_off, uint64_t n, uint8_t *accept_bits);
+
+/* libsodium crypto_sign_open semantics over a batch of signed messages
+ * sm_i = sm[sm_off[i] .. sm_off[i+1]): len < 64 -> reject, otherwise split
+ * at byte 64 (signature || message).  This is exactly what
+ * VerifyKey.verify(signature + msg) does (nacl_wrappers.py:100-108), so a
+ * base58-decoded signature of any length keeps the reference's behaviour. */
+int edv_sign_open_batch(edv_ctx *ctx, const uint8_t *sm, const uint64_t *sm_off, const uint8_t *pk32, uint64_t n,
+                        uint8_t *accept_bits);
+
+/* Device-resident verify (inputs already in HBM).  d_accept_words receives
+ * ceil(n / 64) little-endian uint64 words.  d_msgs must be readable up to the
+ * 4-byte-aligned word containing its last message byte. */
+int edv_verify_batch_device(edv_ctx *ctx, const void *d_sig64, const void *d_pk32, const void *d_msgs,
+                            const void *d_msg_off, uint64_t n, void *d_accept_words, void *stream);
+
+/* Kernel timing hooks for the roofline, measured with HIP events on the
+ * stream the kernels ran on.  The verify pipeline is three kernels per chunk
+ * of up to 2^20 items: hash (prechecks + SHA-512 + mod L), table (decode -A,
+ * [1..8](-A)), dsm ([h](-A) + [S]B, encode, compare, ballot).  For a
+ * multi-chunk launch hash/table cover the last chunk only.
+ * edv_last_kernel_ms returns the dsm time (the dominant kernel) or < 0. */
+int edv_last_phase_ms(edv_ctx *ctx, double *hash_ms, double *table_ms, double *dsm_ms);
+double edv_last_kernel_ms(edv_ctx *ctx);
+
+/* ------------------------------------------------- signing (synthetic load) */
+
+/* crypto_sign_seed_keypair for n seeds (32 bytes each): pk32_out n*32,
+ * sk64_out n*64 (= seed || pk).  Host pointers. */
+int edv_seed_keypair_batch(edv_ctx *ctx, const uint8_t *seeds32, uint64_t n, uint8_t *pk32_out, uint8_t *sk64_out);
+
+/* Deterministic Ed25519 signatures (crypto_sign_detached), device pointers:
+ * item i is signed with key d_sk64[key_idx[i]] over its message. */
+int edv_sign_batch_device(edv_ctx *ctx, const void *d_sk64, const void *d_key_idx, const void *d_msgs,
+                          const void *d_msg_off, uint64_t n, void *d_sig64_out, void *stream);
+
+/* Host-pointer convenience form of edv_sign_batch_device. */
+int edv_sign_batch(edv_ctx *ctx, const uint8_t *sk64, const uint32_t *key_idx, const uint8_t *msgs,
+                   const uint64_t *msg_off, uint64_t n, uint8_t *sig64_out);
+
+/* ------------------------------------------------------ quorum vote tally */
+
+/* Votes are (key, voter, phase) triples with an accept flag; the tally keeps
+ * the reference's distinct-voter set semantics (models.py:21-37: a duplicate
+ * vote counts once) and compares against Quorums(n_validators)
+ * (quorums.py:15-32: f = (n-1)//3 for n >= 4 else 0; prepare = n-f-1,
+ * commit = n-f).
+ *   d_key, d_voter, d_phase, d_valid : n_votes entries (uint32, uint8, uint8, uint8)
+ *   d_ballot : n_keys * n_validators * 2 bytes of scratch/output, zeroed here;
+ *              ballot[(k * 2 + phase) * n_validators + v] = 1 if a valid vote
+ *   d_counts : n_keys * 2 uint32 (distinct voters per key and phase)
+ *   d_quorum : n_keys bytes: bit0 = prepare quorum, bit1 = commit quorum. */
+int edv_tally_device(edv_ctx *ctx, const void *d_key, const void *d_voter, const void *d_phase, const void *d_valid,
+                     uint64_t n_votes, uint32_t n_keys, uint32_t n_validators, void *d_ballot, void *d_counts,
+                     void *d_quorum, void *stream);
+
+/* Second half of the tally alone: counts + quorum flags from a ballot array
+ * (used after an all-reduce(max) of ballots across GPUs). */
+int edv_tally_finish_device(edv_ctx *ctx, const void *d_ballot, uint32_t n_keys, uint32_t n_validators,
+                            void *d_counts, void *d_quorum, void *stream);
+
+/* Host-pointer convenience form of edv_tally_device. */
+int edv_tally(edv_ctx *ctx, const uint32_t *key, const uint8_t *voter, const uint8_t *phase, const uint8_t *valid,
+              uint64_t n_votes, uint32_t n_keys, uint32_t n_validators, uint32_t *counts_out, uint8_t *quorum_out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PLENUM_EDVERIFY_H */

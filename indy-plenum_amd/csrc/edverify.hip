@@ -1,0 +1,691 @@
+// edverify.hip -- libplenum_edverify.so: batched Ed25519 verification for
+// Plenum's request authenticator on MI355X (gfx950), behind the C ABI in
+// include/edverify.h.
+//
+// Kernels (one HIP stream per context):
+//   edv_verify_kernel   one lane per request: prechecks, SHA-512(R||A||M) mod L,
+//                       decode -A, [h](-A) + [S]B with signed radix-16 windows
+//                       (A multiples in a per-lane SoA scratch table, B
+//                       multiples in LDS), encode, byte compare with R, and a
+//                       wave ballot into the accept bitmask.
+//   edv_sign_kernel /
+//   edv_keypair_kernel  deterministic Ed25519 signer (synthetic request load).
+//   edv_tally_*         distinct-voter ballots -> counts -> quorum flags.
+#include <hip/hip_runtime.h>
+
+#include <mutex>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+#include <string>
+#include <vector>
+
+#include "../../include/edverify.h"
+#include "verify_core.h"
+
+using namespace edv;
+
+#define EDV_VERSION "plenum-edverify 0.1.0 (gfx950)"
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr uint64_t kMaxLanes = 1ull << 20;  // scratch lanes (grid-stride beyond)
+constexpr int kTableWords = 8 * 4 * 10;     // [1..8](-A) cached, u32 limbs
+
+thread_local std::string g_err;
+
+int set_err(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                      \
+  do {                                                                                     \
+    hipError_t e_ = (expr);                                                                \
+    if (e_ != hipSuccess) return set_err(EDV_EHIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+// ------------------------------------------------------------------ accessors
+
+// Per-lane cached multiples [1..8](-A), SoA per 256-lane block: word w of lane t
+// lives at region + (w * 256 + t) * 4, so every access is a coalesced
+// buffer_load/store with one VGPR (voffset) of addressing and the limb index in
+// the scalar offset.
+constexpr uint32_t kRegionBytes = kTableWords * kBlock * 4;
+struct DevTableA {
+  __amdgpu_buffer_rsrc_t rsrc;  // this block's region (wave-uniform)
+  uint32_t lane_off;            // threadIdx.x * 4
+  __device__ DevTableA(uint32_t* scratch, uint32_t block, uint32_t lane) {
+    rsrc = __builtin_amdgcn_make_buffer_rsrc((char*)scratch + (uint64_t)block * kRegionBytes, 0, kRegionBytes,
+                                             0x00020000);
+    lane_off = lane * 4;
+  }
+  __device__ void store(int j, const ge_cached& c) const {
+    const int off = lane_off + j * (40 * kBlock * 4);
+#pragma unroll
+    for (int l = 0; l < 10; ++l) {
+      __builtin_amdgcn_raw_buffer_store_b32(c.YplusX.v[l], rsrc, off, (0 + l) * kBlock * 4, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(c.YminusX.v[l], rsrc, off, (10 + l) * kBlock * 4, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(c.Z.v[l], rsrc, off, (20 + l) * kBlock * 4, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(c.T2d.v[l], rsrc, off, (30 + l) * kBlock * 4, 0);
+    }
+  }
+  __device__ void load(int j, ge_cached& c) const {
+    const int off = lane_off + j * (40 * kBlock * 4);
+#pragma unroll
+    for (int l = 0; l < 10; ++l) {
+      c.YplusX.v[l] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, off, (0 + l) * kBlock * 4, 0);
+      c.YminusX.v[l] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, off, (10 + l) * kBlock * 4, 0);
+      c.Z.v[l] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, off, (20 + l) * kBlock * 4, 0);
+      c.T2d.v[l] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, off, (30 + l) * kBlock * 4, 0);
+    }
+  }
+};
+
+struct LdsNiels {
+  const uint32_t* lds;  // 8 points * 30 words
+  __device__ void load(int j, ge_niels& n) const {
+    const uint32_t* p = lds + 30 * j;
+#pragma unroll
+    for (int l = 0; l < 10; ++l) {
+      n.ypx.v[l] = p[l];
+      n.ymx.v[l] = p[10 + l];
+      n.xy2d.v[l] = p[20 + l];
+    }
+  }
+};
+
+__device__ __forceinline__ void load_words(uint32_t* dst, const uint8_t* src, int nwords) {
+  // src is 16-byte aligned for the sig/pk arrays (64 / 32 byte records)
+  const uint4* s = (const uint4*)src;
+  for (int k = 0; k < nwords / 4; ++k) {
+    uint4 v = s[k];
+    dst[4 * k] = v.x;
+    dst[4 * k + 1] = v.y;
+    dst[4 * k + 2] = v.z;
+    dst[4 * k + 3] = v.w;
+  }
+}
+
+// ---------------------------------------------------------------- kernels
+
+// ---- split pipeline: hash -> table -> dsm (each kernel gets its own
+// register budget; intermediates are SoA in the context scratch).
+
+__global__ __launch_bounds__(kBlock) void edv_hash_kernel(const uint8_t* __restrict__ sig64,
+                                                         const uint8_t* __restrict__ pk32,
+                                                         const uint8_t* __restrict__ msgs,
+                                                         const uint64_t* __restrict__ msg_off, uint64_t n,
+                                                         uint32_t* __restrict__ h_soa, uint8_t* __restrict__ flags,
+                                                         uint64_t stride) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t sig[16], pk[8], h[8];
+  load_words(sig, sig64 + 64 * i, 16);
+  load_words(pk, pk32 + 32 * i, 8);
+  const uint64_t o0 = msg_off[i], o1 = msg_off[i + 1];
+  const bool ok = verify_phase_hash(h, sig, pk, msgs + o0, o1 - o0);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) h_soa[k * stride + i] = h[k];
+  flags[i] = ok ? 1 : 0;
+}
+
+__global__ __launch_bounds__(kBlock) void edv_table_kernel(const uint8_t* __restrict__ pk32, uint64_t n,
+                                                          uint32_t* __restrict__ table, uint8_t* __restrict__ flags,
+                                                          uint64_t stride) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t pk[8];
+  load_words(pk, pk32 + 32 * i, 8);
+  DevTableA ta(table, blockIdx.x, threadIdx.x);
+  const bool ok = verify_phase_table(pk, ta);
+  if (!ok) flags[i] = 0;
+}
+
+__global__ __launch_bounds__(kBlock) void edv_dsm_kernel(const uint8_t* __restrict__ sig64, uint64_t n,
+                                                        const uint32_t* __restrict__ h_soa,
+                                                        const uint8_t* __restrict__ flags,
+                                                        uint32_t* __restrict__ table, uint64_t stride,
+                                                        const uint32_t* __restrict__ btab,
+                                                        unsigned long long* __restrict__ accept_words) {
+  __shared__ uint32_t lds_b[8 * 30];
+  for (int t = threadIdx.x; t < 8 * 30; t += blockDim.x) lds_b[t] = btab[t];
+  __syncthreads();
+  const LdsNiels tb{lds_b};
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool ok = false;
+  if (i < n) {
+    uint32_t sig[16], h[8];
+    load_words(sig, sig64 + 64 * i, 16);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) h[k] = h_soa[k * stride + i];
+    const DevTableA ta(table, blockIdx.x, threadIdx.x);
+    ok = verify_phase_dsm(h, sig + 8, sig, ta, tb) && flags[i];
+  }
+  const unsigned long long b = __ballot(ok);
+  if ((threadIdx.x & 63) == 0 && i < n) accept_words[i >> 6] = b;
+}
+
+// Fixed-base comb: [x]B with x < 2^253, 64 madds over BASE_COMB (global).
+__device__ void ge_scalarmult_base(ge_p3& Q, const uint32_t x[8], const uint32_t* __restrict__ comb) {
+  uint32_t y[8];
+  sc_recode16(y, x);
+  ge_p3_0(Q);
+  ge_p1p1 t;
+  for (int i = 0; i < 64; ++i) {
+    const int e = recode_digit(y, i);
+    const int m = e < 0 ? -e : e;
+    ge_niels nb;
+    ge_niels_0(nb);
+    if (m != 0) {
+      const uint32_t* p = comb + (uint64_t)(i * 8 + m - 1) * 30;
+#pragma unroll
+      for (int l = 0; l < 10; ++l) {
+        nb.ypx.v[l] = p[l];
+        nb.ymx.v[l] = p[10 + l];
+        nb.xy2d.v[l] = p[20 + l];
+      }
+    }
+    if (e < 0) {
+      fe tmp = nb.ypx;
+      nb.ypx = nb.ymx;
+      nb.ymx = tmp;
+      fe_neg(nb.xy2d, nb.xy2d);
+    }
+    ge_madd(t, Q, nb);
+    ge_p1p1_to_p3_addlike(Q, t);
+  }
+}
+
+__device__ void clamp_reduce(uint32_t a_red[8], uint32_t a_clamped[8], const uint32_t az[16]) {
+  uint32_t wide[16];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) a_clamped[k] = az[k];
+  a_clamped[0] &= ~7u;
+  a_clamped[7] &= 0x3fffffffu;
+  a_clamped[7] |= 0x40000000u;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) wide[k] = k < 8 ? a_clamped[k] : 0u;
+  sc_reduce(a_red, wide);
+}
+
+__global__ __launch_bounds__(kBlock) void edv_keypair_kernel(const uint8_t* __restrict__ seeds, uint64_t n,
+                                                            const uint32_t* __restrict__ comb,
+                                                            uint8_t* __restrict__ pk_out, uint8_t* __restrict__ sk_out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t seed[8], az[16], a_red[8], a_cl[8], pk[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) seed[k] = ((const uint32_t*)(seeds + 32 * i))[k];
+  sha512_prefixed<8>(az, seed, nullptr, 0);
+  clamp_reduce(a_red, a_cl, az);
+  ge_p3 A;
+  ge_scalarmult_base(A, a_red, comb);
+  ge_p2 a2;
+  ge_p3_to_p2(a2, A);
+  ge_tobytes(pk, a2);
+  uint32_t* po = (uint32_t*)(pk_out + 32 * i);
+  uint32_t* so = (uint32_t*)(sk_out + 64 * i);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    po[k] = pk[k];
+    so[k] = seed[k];
+    so[8 + k] = pk[k];
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void edv_sign_kernel(const uint8_t* __restrict__ sk64,
+                                                         const uint32_t* __restrict__ key_idx,
+                                                         const uint8_t* __restrict__ msgs,
+                                                         const uint64_t* __restrict__ msg_off, uint64_t n,
+                                                         const uint32_t* __restrict__ comb,
+                                                         uint8_t* __restrict__ sig_out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t* sk = (const uint32_t*)(sk64 + 64 * (uint64_t)key_idx[i]);
+  uint32_t seed[8], pk[8], az[16], a_red[8], a_cl[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    seed[k] = sk[k];
+    pk[k] = sk[8 + k];
+  }
+  const uint8_t* m = msgs + msg_off[i];
+  const uint64_t mlen = msg_off[i + 1] - msg_off[i];
+  sha512_prefixed<8>(az, seed, nullptr, 0);
+  clamp_reduce(a_red, a_cl, az);
+  uint32_t nonce_full[16], nonce[8];
+  sha512_prefixed<8>(nonce_full, az + 8, m, mlen);
+  sc_reduce(nonce, nonce_full);
+  ge_p3 R;
+  ge_scalarmult_base(R, nonce, comb);
+  ge_p2 r2;
+  ge_p3_to_p2(r2, R);
+  uint32_t rb[8];
+  ge_tobytes(rb, r2);
+  uint32_t prefix[16], hram_full[16], hram[8], s[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    prefix[k] = rb[k];
+    prefix[8 + k] = pk[k];
+  }
+  sha512_prefixed<16>(hram_full, prefix, m, mlen);
+  sc_reduce(hram, hram_full);
+  sc_muladd(s, hram, a_cl, nonce);
+  uint32_t* so = (uint32_t*)(sig_out + 64 * i);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    so[k] = rb[k];
+    so[8 + k] = s[k];
+  }
+}
+
+__global__ void edv_tally_scatter_kernel(const uint32_t* __restrict__ key, const uint8_t* __restrict__ voter,
+                                         const uint8_t* __restrict__ phase, const uint8_t* __restrict__ valid,
+                                         uint64_t n_votes, uint32_t n_keys, uint32_t n_validators,
+                                         uint8_t* __restrict__ ballot) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_votes) return;
+  const uint32_t k = key[i], v = voter[i], ph = phase[i];
+  if (valid[i] && k < n_keys && v < n_validators && ph < 2) ballot[((uint64_t)k * 2 + ph) * n_validators + v] = 1;
+}
+
+__global__ void edv_tally_count_kernel(const uint8_t* __restrict__ ballot, uint32_t n_keys, uint32_t n_validators,
+                                       uint32_t q_prepare, uint32_t q_commit, uint32_t* __restrict__ counts,
+                                       uint8_t* __restrict__ quorum) {
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n_keys) return;
+  uint32_t c[2] = {0, 0};
+  for (int ph = 0; ph < 2; ++ph) {
+    const uint8_t* b = ballot + (k * 2 + ph) * n_validators;
+    for (uint32_t v = 0; v < n_validators; ++v) c[ph] += b[v] != 0;
+  }
+  counts[2 * k] = c[0];
+  counts[2 * k + 1] = c[1];
+  quorum[k] = (uint8_t)((c[0] >= q_prepare ? 1 : 0) | (c[1] >= q_commit ? 2 : 0));
+}
+
+uint64_t div_up(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
+
+}  // namespace
+
+// ------------------------------------------------------------------ context
+
+struct edv_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  uint32_t* d_btab_small = nullptr;
+  uint32_t* d_btab_comb = nullptr;
+  uint32_t* d_scratch = nullptr;  // per-lane A tables, kMaxLanes / kBlock regions
+  uint32_t* d_hsoa = nullptr;     // h words, SoA [8][kMaxLanes]
+  uint8_t* d_flags = nullptr;     // precheck / decode verdicts [kMaxLanes]
+  uint64_t scratch_lanes = 0;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // hash | table | dsm boundaries
+  bool timed = false;
+  // staging buffers for host-pointer calls
+  struct Buf {
+    void* p = nullptr;
+    size_t cap = 0;
+  } b_sig, b_pk, b_msg, b_off, b_bits, b_aux;
+};
+
+namespace {
+
+int ensure(edv_ctx::Buf& b, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  if (b.cap >= bytes) return 0;
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+  size_t want = bytes + bytes / 4 + 64;
+  hipError_t e = hipMalloc(&b.p, want);
+  if (e != hipSuccess) return set_err(EDV_ENOMEM, "hipMalloc(%zu): %s", want, hipGetErrorString(e));
+  b.cap = want;
+  return 0;
+}
+
+int set_device(edv_ctx* ctx) {
+  if (!ctx) return set_err(EDV_EINVAL, "null context");
+  HIP_TRY(hipSetDevice(ctx->device));
+  return 0;
+}
+
+hipStream_t pick_stream(edv_ctx* ctx, void* stream) { return stream ? (hipStream_t)stream : ctx->stream; }
+
+int launch_verify(edv_ctx* ctx, const void* d_sig, const void* d_pk, const void* d_msgs, const void* d_off, uint64_t n,
+                  void* d_words, hipStream_t st) {
+  if (n == 0) return 0;
+  const uint8_t* sig = (const uint8_t*)d_sig;
+  const uint8_t* pk = (const uint8_t*)d_pk;
+  const uint64_t* off = (const uint64_t*)d_off;
+  unsigned long long* words = (unsigned long long*)d_words;
+  const uint64_t chunk = ctx->scratch_lanes;  // multiple of 64
+  HIP_TRY(hipEventRecord(ctx->ev[0], st));
+  for (uint64_t c0 = 0; c0 < n; c0 += chunk) {
+    const uint64_t cn = (n - c0) < chunk ? (n - c0) : chunk;
+    const uint32_t grid = (uint32_t)div_up(cn, kBlock);
+    const bool last = c0 + cn >= n;
+    hipLaunchKernelGGL(edv_hash_kernel, dim3(grid), dim3(kBlock), 0, st, sig + 64 * c0, pk + 32 * c0,
+                       (const uint8_t*)d_msgs, off + c0, cn, ctx->d_hsoa, ctx->d_flags, chunk);
+    HIP_TRY(hipGetLastError());
+    if (last) HIP_TRY(hipEventRecord(ctx->ev[1], st));
+    hipLaunchKernelGGL(edv_table_kernel, dim3(grid), dim3(kBlock), 0, st, pk + 32 * c0, cn, ctx->d_scratch,
+                       ctx->d_flags, chunk);
+    HIP_TRY(hipGetLastError());
+    if (last) HIP_TRY(hipEventRecord(ctx->ev[2], st));
+    hipLaunchKernelGGL(edv_dsm_kernel, dim3(grid), dim3(kBlock), 0, st, sig + 64 * c0, cn, ctx->d_hsoa,
+                       ctx->d_flags, ctx->d_scratch, chunk, ctx->d_btab_small, words + c0 / 64);
+    HIP_TRY(hipGetLastError());
+  }
+  HIP_TRY(hipEventRecord(ctx->ev[3], st));
+  ctx->timed = true;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* edv_version(void) { return EDV_VERSION; }
+const char* edv_last_error(void) { return g_err.c_str(); }
+
+int edv_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+edv_ctx* edv_create(int device) {
+  int ndev = edv_device_count();
+  if (device < 0 || device >= ndev) {
+    set_err(EDV_ENODEV, "device %d out of range (%d HIP devices)", device, ndev);
+    return nullptr;
+  }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess || strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    set_err(EDV_ENODEV, "device %d is not gfx950 (%s)", device, prop.gcnArchName);
+    return nullptr;
+  }
+  edv_ctx* ctx = new edv_ctx();
+  ctx->device = device;
+  auto fail = [&](const char* what, hipError_t e) -> edv_ctx* {
+    set_err(EDV_EHIP, "%s: %s", what, hipGetErrorString(e));
+    edv_destroy(ctx);
+    return nullptr;
+  };
+  hipError_t e;
+  if ((e = hipSetDevice(device)) != hipSuccess) return fail("hipSetDevice", e);
+  if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess) return fail("hipStreamCreate", e);
+  for (int k = 0; k < 4; ++k)
+    if ((e = hipEventCreate(&ctx->ev[k])) != hipSuccess) return fail("hipEventCreate", e);
+  if ((e = hipMalloc(&ctx->d_btab_small, sizeof(BASE_SMALL_U32))) != hipSuccess) return fail("hipMalloc", e);
+  if ((e = hipMalloc(&ctx->d_btab_comb, sizeof(BASE_COMB_U32))) != hipSuccess) return fail("hipMalloc", e);
+  if ((e = hipMemcpy(ctx->d_btab_small, BASE_SMALL_U32, sizeof(BASE_SMALL_U32), hipMemcpyHostToDevice)) != hipSuccess)
+    return fail("hipMemcpy", e);
+  if ((e = hipMemcpy(ctx->d_btab_comb, BASE_COMB_U32, sizeof(BASE_COMB_U32), hipMemcpyHostToDevice)) != hipSuccess)
+    return fail("hipMemcpy", e);
+  ctx->scratch_lanes = kMaxLanes;
+  if ((e = hipMalloc(&ctx->d_scratch, ctx->scratch_lanes / kBlock * (uint64_t)kRegionBytes)) != hipSuccess)
+    return fail("hipMalloc(scratch)", e);
+  if ((e = hipMalloc(&ctx->d_hsoa, ctx->scratch_lanes * 8 * sizeof(uint32_t))) != hipSuccess)
+    return fail("hipMalloc(h)", e);
+  if ((e = hipMalloc(&ctx->d_flags, ctx->scratch_lanes)) != hipSuccess) return fail("hipMalloc(flags)", e);
+  return ctx;
+}
+
+void edv_destroy(edv_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  for (edv_ctx::Buf* b : {&ctx->b_sig, &ctx->b_pk, &ctx->b_msg, &ctx->b_off, &ctx->b_bits, &ctx->b_aux})
+    if (b->p) (void)hipFree(b->p);
+  if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
+  if (ctx->d_hsoa) (void)hipFree(ctx->d_hsoa);
+  if (ctx->d_flags) (void)hipFree(ctx->d_flags);
+  if (ctx->d_btab_small) (void)hipFree(ctx->d_btab_small);
+  if (ctx->d_btab_comb) (void)hipFree(ctx->d_btab_comb);
+  for (int k = 0; k < 4; ++k)
+    if (ctx->ev[k]) (void)hipEventDestroy(ctx->ev[k]);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+int edv_synchronize(edv_ctx* ctx) {
+  int r = set_device(ctx);
+  if (r) return r;
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int edv_verify_batch_device(edv_ctx* ctx, const void* d_sig64, const void* d_pk32, const void* d_msgs,
+                            const void* d_msg_off, uint64_t n, void* d_accept_words, void* stream) {
+  int r = set_device(ctx);
+  if (r) return r;
+  if (n && (!d_sig64 || !d_pk32 || !d_msgs || !d_msg_off || !d_accept_words))
+    return set_err(EDV_EINVAL, "null device pointer");
+  return launch_verify(ctx, d_sig64, d_pk32, d_msgs, d_msg_off, n, d_accept_words, pick_stream(ctx, stream));
+}
+
+int edv_last_phase_ms(edv_ctx* ctx, double* hash_ms, double* table_ms, double* dsm_ms) {
+  if (!ctx || !ctx->timed) return set_err(EDV_EINVAL, "no timed verify launch yet");
+  HIP_TRY(hipEventSynchronize(ctx->ev[3]));
+  float t[3] = {0.f, 0.f, 0.f};
+  for (int k = 0; k < 3; ++k) HIP_TRY(hipEventElapsedTime(&t[k], ctx->ev[k], ctx->ev[k + 1]));
+  if (hash_ms) *hash_ms = t[0];
+  if (table_ms) *table_ms = t[1];
+  if (dsm_ms) *dsm_ms = t[2];
+  return 0;
+}
+
+double edv_last_kernel_ms(edv_ctx* ctx) {
+  double d = -1.0;
+  if (edv_last_phase_ms(ctx, nullptr, nullptr, &d) != 0) return -1.0;
+  return d;
+}
+
+int edv_verify_batch(edv_ctx* ctx, const uint8_t* sig64, const uint8_t* pk32, const uint8_t* msgs,
+                     const uint64_t* msg_off, uint64_t n, uint8_t* accept_bits) {
+  int r = set_device(ctx);
+  if (r) return r;
+  if (n == 0) return 0;
+  if (!sig64 || !pk32 || !msg_off || !accept_bits) return set_err(EDV_EINVAL, "null pointer");
+  const uint64_t m0 = msg_off[0], m1 = msg_off[n];
+  if (m1 < m0) return set_err(EDV_EINVAL, "msg_off not monotone");
+  for (uint64_t i = 0; i < n; ++i)
+    if (msg_off[i + 1] < msg_off[i]) return set_err(EDV_EINVAL, "msg_off[%llu] decreasing", (unsigned long long)i);
+  const uint64_t mbytes = m1 - m0;
+  if (mbytes && !msgs) return set_err(EDV_EINVAL, "null msgs");
+  const uint64_t nwords = div_up(n, 64);
+  if ((r = ensure(ctx->b_sig, 64 * n)) || (r = ensure(ctx->b_pk, 32 * n)) || (r = ensure(ctx->b_msg, mbytes + 16)) ||
+      (r = ensure(ctx->b_off, 8 * (n + 1))) || (r = ensure(ctx->b_bits, 8 * nwords)))
+    return r;
+  hipStream_t st = ctx->stream;
+  // offsets rebased to 0 for the staged copy
+  std::vector<uint64_t> off(n + 1);
+  for (uint64_t i = 0; i <= n; ++i) off[i] = msg_off[i] - m0;
+  HIP_TRY(hipMemcpyAsync(ctx->b_sig.p, sig64, 64 * n, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(ctx->b_pk.p, pk32, 32 * n, hipMemcpyHostToDevice, st));
+  if (mbytes) HIP_TRY(hipMemcpyAsync(ctx->b_msg.p, msgs + m0, mbytes, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(ctx->b_off.p, off.data(), 8 * (n + 1), hipMemcpyHostToDevice, st));
+  if ((r = launch_verify(ctx, ctx->b_sig.p, ctx->b_pk.p, ctx->b_msg.p, ctx->b_off.p, n, ctx->b_bits.p, st))) return r;
+  std::vector<uint64_t> words(nwords);
+  HIP_TRY(hipMemcpyAsync(words.data(), ctx->b_bits.p, 8 * nwords, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  memcpy(accept_bits, words.data(), (n + 7) / 8);
+  if (n & 7) accept_bits[n / 8] &= (uint8_t)((1u << (n & 7)) - 1);
+  return 0;
+}
+
+int edv_sign_open_batch(edv_ctx* ctx, const uint8_t* sm, const uint64_t* sm_off, const uint8_t* pk32, uint64_t n,
+                        uint8_t* accept_bits) {
+  if (!ctx) return set_err(EDV_EINVAL, "null context");
+  if (n == 0) return 0;
+  if (!sm_off || !pk32 || !accept_bits) return set_err(EDV_EINVAL, "null pointer");
+  // crypto_sign_open: smlen < 64 -> reject; else sig = sm[0:64], m = sm[64:].
+  std::vector<uint8_t> sig(64 * n, 0), too_short(n, 0), msgs;
+  std::vector<uint64_t> off(n + 1, 0);
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint64_t a = sm_off[i], b = sm_off[i + 1];
+    if (b < a) return set_err(EDV_EINVAL, "sm_off[%llu] decreasing", (unsigned long long)i);
+    if (b - a < 64) {
+      too_short[i] = 1;
+    } else {
+      if (!sm) return set_err(EDV_EINVAL, "null sm");
+      memcpy(&sig[64 * i], sm + a, 64);
+      msgs.insert(msgs.end(), sm + a + 64, sm + b);
+    }
+    off[i + 1] = msgs.size();
+  }
+  int r = edv_verify_batch(ctx, sig.data(), pk32, msgs.data(), off.data(), n, accept_bits);
+  if (r) return r;
+  for (uint64_t i = 0; i < n; ++i)
+    if (too_short[i]) accept_bits[i / 8] &= (uint8_t)~(1u << (i % 8));
+  return 0;
+}
+
+int edv_seed_keypair_batch(edv_ctx* ctx, const uint8_t* seeds32, uint64_t n, uint8_t* pk32_out, uint8_t* sk64_out) {
+  int r = set_device(ctx);
+  if (r) return r;
+  if (n == 0) return 0;
+  if (!seeds32 || !pk32_out || !sk64_out) return set_err(EDV_EINVAL, "null pointer");
+  if ((r = ensure(ctx->b_sig, 64 * n)) || (r = ensure(ctx->b_pk, 32 * n)) || (r = ensure(ctx->b_aux, 32 * n))) return r;
+  hipStream_t st = ctx->stream;
+  HIP_TRY(hipMemcpyAsync(ctx->b_aux.p, seeds32, 32 * n, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(edv_keypair_kernel, dim3((uint32_t)div_up(n, kBlock)), dim3(kBlock), 0, st,
+                     (const uint8_t*)ctx->b_aux.p, n, ctx->d_btab_comb, (uint8_t*)ctx->b_pk.p, (uint8_t*)ctx->b_sig.p);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(pk32_out, ctx->b_pk.p, 32 * n, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(sk64_out, ctx->b_sig.p, 64 * n, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  return 0;
+}
+
+int edv_sign_batch_device(edv_ctx* ctx, const void* d_sk64, const void* d_key_idx, const void* d_msgs,
+                          const void* d_msg_off, uint64_t n, void* d_sig64_out, void* stream) {
+  int r = set_device(ctx);
+  if (r) return r;
+  if (n == 0) return 0;
+  if (!d_sk64 || !d_key_idx || !d_msgs || !d_msg_off || !d_sig64_out) return set_err(EDV_EINVAL, "null device pointer");
+  hipStream_t st = pick_stream(ctx, stream);
+  hipLaunchKernelGGL(edv_sign_kernel, dim3((uint32_t)div_up(n, kBlock)), dim3(kBlock), 0, st, (const uint8_t*)d_sk64,
+                     (const uint32_t*)d_key_idx, (const uint8_t*)d_msgs, (const uint64_t*)d_msg_off, n,
+                     ctx->d_btab_comb, (uint8_t*)d_sig64_out);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int edv_sign_batch(edv_ctx* ctx, const uint8_t* sk64, const uint32_t* key_idx, const uint8_t* msgs,
+                   const uint64_t* msg_off, uint64_t n, uint8_t* sig64_out) {
+  int r = set_device(ctx);
+  if (r) return r;
+  if (n == 0) return 0;
+  if (!sk64 || !key_idx || !msg_off || !sig64_out) return set_err(EDV_EINVAL, "null pointer");
+  uint32_t nkeys = 0;
+  for (uint64_t i = 0; i < n; ++i) nkeys = key_idx[i] + 1 > nkeys ? key_idx[i] + 1 : nkeys;
+  const uint64_t m0 = msg_off[0], mbytes = msg_off[n] - m0;
+  std::vector<uint64_t> off(n + 1);
+  for (uint64_t i = 0; i <= n; ++i) off[i] = msg_off[i] - m0;
+  if ((r = ensure(ctx->b_sig, 64 * n)) || (r = ensure(ctx->b_pk, 64 * (uint64_t)nkeys)) ||
+      (r = ensure(ctx->b_msg, mbytes + 16)) || (r = ensure(ctx->b_off, 8 * (n + 1))) || (r = ensure(ctx->b_aux, 4 * n)))
+    return r;
+  hipStream_t st = ctx->stream;
+  HIP_TRY(hipMemcpyAsync(ctx->b_pk.p, sk64, 64 * (uint64_t)nkeys, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(ctx->b_aux.p, key_idx, 4 * n, hipMemcpyHostToDevice, st));
+  if (mbytes) HIP_TRY(hipMemcpyAsync(ctx->b_msg.p, msgs + m0, mbytes, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(ctx->b_off.p, off.data(), 8 * (n + 1), hipMemcpyHostToDevice, st));
+  if ((r = edv_sign_batch_device(ctx, ctx->b_pk.p, ctx->b_aux.p, ctx->b_msg.p, ctx->b_off.p, n, ctx->b_sig.p, st)))
+    return r;
+  HIP_TRY(hipMemcpyAsync(sig64_out, ctx->b_sig.p, 64 * n, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  return 0;
+}
+
+static void quorum_thresholds(uint32_t nv, uint32_t* q_prepare, uint32_t* q_commit) {
+  // plenum/common/util.py:217-228 getMaxFailures; plenum/server/quorums.py:19-21
+  const uint32_t f = nv >= 4 ? (nv - 1) / 3 : 0;
+  *q_prepare = nv - f - 1;
+  *q_commit = nv - f;
+}
+
+int edv_tally_finish_device(edv_ctx* ctx, const void* d_ballot, uint32_t n_keys, uint32_t n_validators,
+                            void* d_counts, void* d_quorum, void* stream) {
+  int r = set_device(ctx);
+  if (r) return r;
+  if (n_keys == 0) return 0;
+  if (!d_ballot || !d_counts || !d_quorum || n_validators == 0) return set_err(EDV_EINVAL, "bad tally arguments");
+  uint32_t qp, qc;
+  quorum_thresholds(n_validators, &qp, &qc);
+  hipStream_t st = pick_stream(ctx, stream);
+  hipLaunchKernelGGL(edv_tally_count_kernel, dim3((uint32_t)div_up(n_keys, kBlock)), dim3(kBlock), 0, st,
+                     (const uint8_t*)d_ballot, n_keys, n_validators, qp, qc, (uint32_t*)d_counts, (uint8_t*)d_quorum);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int edv_tally_device(edv_ctx* ctx, const void* d_key, const void* d_voter, const void* d_phase, const void* d_valid,
+                     uint64_t n_votes, uint32_t n_keys, uint32_t n_validators, void* d_ballot, void* d_counts,
+                     void* d_quorum, void* stream) {
+  int r = set_device(ctx);
+  if (r) return r;
+  if (n_keys == 0) return 0;
+  if (!d_ballot || n_validators == 0 || n_validators > 255) return set_err(EDV_EINVAL, "bad tally arguments");
+  hipStream_t st = pick_stream(ctx, stream);
+  HIP_TRY(hipMemsetAsync(d_ballot, 0, (size_t)n_keys * 2 * n_validators, st));
+  if (n_votes) {
+    if (!d_key || !d_voter || !d_phase || !d_valid) return set_err(EDV_EINVAL, "null vote pointer");
+    hipLaunchKernelGGL(edv_tally_scatter_kernel, dim3((uint32_t)div_up(n_votes, kBlock)), dim3(kBlock), 0, st,
+                       (const uint32_t*)d_key, (const uint8_t*)d_voter, (const uint8_t*)d_phase,
+                       (const uint8_t*)d_valid, n_votes, n_keys, n_validators, (uint8_t*)d_ballot);
+    HIP_TRY(hipGetLastError());
+  }
+  return edv_tally_finish_device(ctx, d_ballot, n_keys, n_validators, d_counts, d_quorum, st);
+}
+
+int edv_tally(edv_ctx* ctx, const uint32_t* key, const uint8_t* voter, const uint8_t* phase, const uint8_t* valid,
+              uint64_t n_votes, uint32_t n_keys, uint32_t n_validators, uint32_t* counts_out, uint8_t* quorum_out) {
+  int r = set_device(ctx);
+  if (r) return r;
+  if (n_keys == 0) return 0;
+  if (!counts_out || !quorum_out) return set_err(EDV_EINVAL, "null output");
+  void *d_key = nullptr, *d_voter = nullptr, *d_phase = nullptr, *d_valid = nullptr, *d_ballot = nullptr,
+       *d_counts = nullptr, *d_quorum = nullptr;
+  auto cleanup = [&]() {
+    for (void* p : {d_key, d_voter, d_phase, d_valid, d_ballot, d_counts, d_quorum})
+      if (p) (void)hipFree(p);
+  };
+  hipStream_t st = ctx->stream;
+  const uint64_t nv = n_votes ? n_votes : 1;
+  hipError_t e = hipSuccess;
+  if ((e = hipMalloc(&d_key, 4 * nv)) || (e = hipMalloc(&d_voter, nv)) || (e = hipMalloc(&d_phase, nv)) ||
+      (e = hipMalloc(&d_valid, nv)) || (e = hipMalloc(&d_ballot, (size_t)n_keys * 2 * n_validators + 16)) ||
+      (e = hipMalloc(&d_counts, 8ull * n_keys)) || (e = hipMalloc(&d_quorum, n_keys))) {
+    cleanup();
+    return set_err(EDV_ENOMEM, "hipMalloc: %s", hipGetErrorString(e));
+  }
+  if (n_votes) {
+    if ((e = hipMemcpyAsync(d_key, key, 4 * n_votes, hipMemcpyHostToDevice, st)) ||
+        (e = hipMemcpyAsync(d_voter, voter, n_votes, hipMemcpyHostToDevice, st)) ||
+        (e = hipMemcpyAsync(d_phase, phase, n_votes, hipMemcpyHostToDevice, st)) ||
+        (e = hipMemcpyAsync(d_valid, valid, n_votes, hipMemcpyHostToDevice, st))) {
+      cleanup();
+      return set_err(EDV_EHIP, "hipMemcpyAsync: %s", hipGetErrorString(e));
+    }
+  }
+  r = edv_tally_device(ctx, d_key, d_voter, d_phase, d_valid, n_votes, n_keys, n_validators, d_ballot, d_counts,
+                       d_quorum, st);
+  if (!r) {
+    if ((e = hipMemcpyAsync(counts_out, d_counts, 8ull * n_keys, hipMemcpyDeviceToHost, st)) ||
+        (e = hipMemcpyAsync(quorum_out, d_quorum, n_keys, hipMemcpyDeviceToHost, st)) ||
+        (e = hipStreamSynchronize(st)))
+      r = set_err(EDV_EHIP, "tally copy-back: %s", hipGetErrorString(e));
+  }
+  cleanup();
+  return r;
+}
+
+}  // extern "C"

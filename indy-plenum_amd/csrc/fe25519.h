@@ -1,0 +1,313 @@
+// fe25519.h -- GF(2^255 - 19) arithmetic for gfx950 VALU.
+//
+// Part of the MI355X Ed25519 verify path that replaces libsodium's
+// crypto_sign_open (reached from stp_core/crypto/nacl_wrappers.py:108).
+//
+// Representation: 10 unsigned 32-bit limbs, radix 2^25.5 (widths 26,25,26,...),
+// value = sum v[k] * 2^ceil(25.5 k).  Products are 32x32->64 multiply-adds, which
+// hipcc lowers to v_mad_u64_u32 (measured half-rate on gfx950: 58.7 of 64
+// lane-ops/clk/CU, tools/microbench).  Carries use 64-bit shifts/adds only on
+// the accumulators.
+//
+// Bound classes (checked by tests/test_fe_bounds.py and, in the host self-test
+// build, by EDV_BOUND_CHECK assertions):
+//   C  "carried":  even limbs < 2^26, odd limbs <= 2^25 + 2^18   (mul/sq/carry output)
+//   L  "loose":    even <= 3*2^26, odd <= 3*2^25 + 2^18          (C+C, C+C+C, C+2p-C)
+//   W  "wide":     even <= 5*2^26, odd <= 5*2^25 + 2^18          (C+4p-L, ...)
+// fe_mul(h, f, g): f in W, g in L  (worst accumulator 2^62.87 < 2^64)
+// fe_sq(h, f):     f in L          (worst accumulator 2^62.13)
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define EDV_HD __host__ __device__ __forceinline__
+#define EDV_HDNI __host__ __device__ __forceinline__
+#else
+#define EDV_HD static inline
+#define EDV_HDNI static
+#endif
+
+#ifdef EDV_BOUND_CHECK
+#include <assert.h>
+#define EDV_ASSERT(x) assert(x)
+#else
+#define EDV_ASSERT(x) ((void)0)
+#endif
+
+namespace edv {
+
+struct fe {
+  uint32_t v[10];
+};
+
+constexpr uint32_t M26 = (1u << 26) - 1;
+constexpr uint32_t M25 = (1u << 25) - 1;
+EDV_HD constexpr int fe_width(int k) { return (k & 1) ? 25 : 26; }
+EDV_HD constexpr uint32_t fe_mask(int k) { return (k & 1) ? M25 : M26; }
+
+// 2p and 4p in this radix (limbwise >= any C / L value respectively).
+EDV_HD constexpr uint32_t two_p(int k) { return k == 0 ? (1u << 27) - 38 : ((k & 1) ? (1u << 26) - 2 : (1u << 27) - 2); }
+EDV_HD constexpr uint32_t four_p(int k) { return k == 0 ? (1u << 28) - 76 : ((k & 1) ? (1u << 27) - 4 : (1u << 28) - 4); }
+
+EDV_HD void fe_0(fe& h) {
+#pragma unroll
+  for (int k = 0; k < 10; ++k) h.v[k] = 0;
+}
+EDV_HD void fe_1(fe& h) {
+  fe_0(h);
+  h.v[0] = 1;
+}
+EDV_HD void fe_add(fe& h, const fe& f, const fe& g) {
+#pragma unroll
+  for (int k = 0; k < 10; ++k) h.v[k] = f.v[k] + g.v[k];
+}
+// h = f - g, for g in C (adds 2p).
+EDV_HD void fe_sub(fe& h, const fe& f, const fe& g) {
+#pragma unroll
+  for (int k = 0; k < 10; ++k) h.v[k] = f.v[k] + (two_p(k) - g.v[k]);
+}
+// h = f - g, for g in L (adds 4p); result class W when f in C.
+EDV_HD void fe_sub4(fe& h, const fe& f, const fe& g) {
+#pragma unroll
+  for (int k = 0; k < 10; ++k) h.v[k] = f.v[k] + (four_p(k) - g.v[k]);
+}
+EDV_HD void fe_neg(fe& h, const fe& f) {
+#pragma unroll
+  for (int k = 0; k < 10; ++k) h.v[k] = two_p(k) - f.v[k];
+}
+// Conditional move: h = b ? f : h   (b is 0 or 1; lowered to v_cndmask).
+EDV_HD void fe_cmov(fe& h, const fe& f, bool b) {
+#pragma unroll
+  for (int k = 0; k < 10; ++k) h.v[k] = b ? f.v[k] : h.v[k];
+}
+
+// 64-bit accumulator carry chain, final limbs in class C.
+EDV_HD void fe_carry64(fe& out, uint64_t h[10]) {
+#define EDV_C(k)                                 \
+  {                                              \
+    uint64_t c = h[k] >> fe_width(k);            \
+    h[k] &= fe_mask(k);                          \
+    h[k + 1] += c;                               \
+  }
+  EDV_C(0) EDV_C(4) EDV_C(1) EDV_C(5) EDV_C(2) EDV_C(6) EDV_C(3) EDV_C(7) EDV_C(4) EDV_C(8)
+  {
+    uint64_t c = h[9] >> 25;
+    h[9] &= M25;
+    h[0] += c * 19;
+  }
+  EDV_C(0)
+#undef EDV_C
+#pragma unroll
+  for (int k = 0; k < 10; ++k) out.v[k] = (uint32_t)h[k];
+}
+
+#ifdef EDV_BOUND_CHECK
+static inline bool fe_in_class(const fe& f, uint32_t even_max, uint32_t odd_max) {
+  for (int k = 0; k < 10; ++k)
+    if (f.v[k] > ((k & 1) ? odd_max : even_max)) return false;
+  return true;
+}
+#define EDV_IS_W(f) fe_in_class(f, 5u << 26, (5u << 25) + (1u << 18))
+#define EDV_IS_L(f) fe_in_class(f, 3u << 26, (3u << 25) + (1u << 18))
+#define EDV_IS_C(f) fe_in_class(f, (1u << 26) - 1, (1u << 25) + (1u << 18))
+#endif
+
+// h = f * g.  f in W, g in L; h in C.  100 multiply-adds.
+EDV_HD void fe_mul(fe& h, const fe& f, const fe& g) {
+  EDV_ASSERT(EDV_IS_W(f) && EDV_IS_L(g));
+  uint32_t g19[10], f2[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+    g19[k] = 19u * g.v[k];
+    f2[k] = (k & 1) ? 2u * f.v[k] : f.v[k];
+  }
+  uint64_t acc[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+    uint64_t a = 0;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      const int j = k - i;
+      const uint32_t fi = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
+      const uint32_t gj = j >= 0 ? g.v[j] : g19[j + 10];
+      a += (uint64_t)fi * gj;
+    }
+    acc[k] = a;
+  }
+  fe_carry64(h, acc);
+}
+
+// h = f^2.  f in L; h in C.  55 multiply-adds.
+EDV_HD void fe_sq(fe& h, const fe& f) {
+  EDV_ASSERT(EDV_IS_L(f));
+  uint32_t d[10], d2[10], d19[10], d38[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+    d[k] = f.v[k];
+    d2[k] = 2u * f.v[k];
+    d19[k] = 19u * f.v[k];
+    d38[k] = 38u * f.v[k];
+  }
+  uint64_t acc[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+    uint64_t a = 0;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+#pragma unroll
+      for (int j = i; j < 10; ++j) {
+        if ((i + j) % 10 != k) continue;
+        const bool both_odd = (i & 1) && (j & 1);
+        const bool wrap = i + j >= 10;
+        const uint32_t fi = (i != j) ? d2[i] : d[i];
+        const uint32_t fj = wrap ? (both_odd ? d38[j] : d19[j]) : (both_odd ? d2[j] : d[j]);
+        a += (uint64_t)fi * fj;
+      }
+    }
+    acc[k] = a;
+  }
+  fe_carry64(h, acc);
+}
+
+// h = f^(2^n), n >= 1.
+EDV_HDNI void fe_sqn(fe& h, const fe& f, int n) {
+  fe_sq(h, f);
+#pragma unroll 1
+  for (int i = 1; i < n; ++i) fe_sq(h, h);
+}
+
+// One 32-bit carry pass: any class up to 2^31 per limb -> C.
+EDV_HD void fe_carry(fe& h) {
+  uint32_t c;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    c = h.v[k] >> fe_width(k);
+    h.v[k] &= fe_mask(k);
+    h.v[k + 1] += c;
+  }
+  c = h.v[9] >> 25;
+  h.v[9] &= M25;
+  h.v[0] += 19u * c;
+  c = h.v[0] >> 26;
+  h.v[0] &= M26;
+  h.v[1] += c;
+}
+
+// Fully reduce into [0, p) (every limb within its width).
+EDV_HD void fe_canon(fe& h) {
+  fe_carry(h);
+  fe_carry(h);
+  fe_carry(h);
+  // value now in [0, 2^255); subtract p iff value + 19 >= 2^255.
+  uint32_t q = (h.v[0] + 19u) >> 26;
+#pragma unroll
+  for (int k = 1; k < 10; ++k) q = (h.v[k] + q) >> fe_width(k);
+  h.v[0] += 19u * q;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    uint32_t c = h.v[k] >> fe_width(k);
+    h.v[k] &= fe_mask(k);
+    h.v[k + 1] += c;
+  }
+  h.v[9] &= M25;
+}
+
+// Little-endian 8 x u32 words of the canonical encoding of h (bit 255 = 0).
+EDV_HD void fe_tobytes(uint32_t w[8], const fe& hin) {
+  fe h = hin;
+  fe_canon(h);
+  // limb offsets 0,26,51,77,102,128,153,179,204,230
+  w[0] = h.v[0] | (h.v[1] << 26);
+  w[1] = (h.v[1] >> 6) | (h.v[2] << 19);
+  w[2] = (h.v[2] >> 13) | (h.v[3] << 13);
+  w[3] = (h.v[3] >> 19) | (h.v[4] << 6);
+  w[4] = h.v[5] | (h.v[6] << 25);
+  w[5] = (h.v[6] >> 7) | (h.v[7] << 19);
+  w[6] = (h.v[7] >> 13) | (h.v[8] << 12);
+  w[7] = (h.v[8] >> 20) | (h.v[9] << 6);
+}
+
+// fe25519_frombytes: the low 255 bits of 8 LE words (bit 255 ignored), not reduced.
+EDV_HD void fe_frombytes(fe& h, const uint32_t w[8]) {
+  h.v[0] = w[0] & M26;
+  h.v[1] = ((w[0] >> 26) | (w[1] << 6)) & M25;
+  h.v[2] = ((w[1] >> 19) | (w[2] << 13)) & M26;
+  h.v[3] = ((w[2] >> 13) | (w[3] << 19)) & M25;
+  h.v[4] = (w[3] >> 6) & M26;
+  h.v[5] = w[4] & M25;
+  h.v[6] = ((w[4] >> 25) | (w[5] << 7)) & M26;
+  h.v[7] = ((w[5] >> 19) | (w[6] << 13)) & M25;
+  h.v[8] = ((w[6] >> 12) | (w[7] << 20)) & M26;
+  h.v[9] = (w[7] >> 6) & M25;
+}
+
+EDV_HD bool fe_iszero(const fe& f) {
+  fe h = f;
+  fe_canon(h);
+  uint32_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 10; ++k) acc |= h.v[k];
+  return acc == 0;
+}
+EDV_HD uint32_t fe_isnegative(const fe& f) {
+  fe h = f;
+  fe_canon(h);
+  return h.v[0] & 1;
+}
+
+// z^(2^255 - 21) = z^-1 (ref10 addition chain: 254 squarings, 11 multiplies).
+EDV_HDNI void fe_invert(fe& out, const fe& z) {
+  fe t0, t1, t2, t3;
+  fe_sq(t0, z);
+  fe_sqn(t1, t0, 2);
+  fe_mul(t1, z, t1);
+  fe_mul(t0, t0, t1);
+  fe_sq(t2, t0);
+  fe_mul(t1, t1, t2);
+  fe_sqn(t2, t1, 5);
+  fe_mul(t1, t2, t1);
+  fe_sqn(t2, t1, 10);
+  fe_mul(t2, t2, t1);
+  fe_sqn(t3, t2, 20);
+  fe_mul(t2, t3, t2);
+  fe_sqn(t2, t2, 10);
+  fe_mul(t1, t2, t1);
+  fe_sqn(t2, t1, 50);
+  fe_mul(t2, t2, t1);
+  fe_sqn(t3, t2, 100);
+  fe_mul(t2, t3, t2);
+  fe_sqn(t2, t2, 50);
+  fe_mul(t1, t2, t1);
+  fe_sqn(t1, t1, 5);
+  fe_mul(out, t1, t0);
+}
+
+// z^(2^252 - 3) (for square roots; 250 squarings, 11 multiplies).
+EDV_HDNI void fe_pow22523(fe& out, const fe& z) {
+  fe t0, t1, t2;
+  fe_sq(t0, z);
+  fe_sqn(t1, t0, 2);
+  fe_mul(t1, z, t1);
+  fe_mul(t0, t0, t1);
+  fe_sq(t0, t0);
+  fe_mul(t0, t1, t0);
+  fe_sqn(t1, t0, 5);
+  fe_mul(t0, t1, t0);
+  fe_sqn(t1, t0, 10);
+  fe_mul(t1, t1, t0);
+  fe_sqn(t2, t1, 20);
+  fe_mul(t1, t2, t1);
+  fe_sqn(t1, t1, 10);
+  fe_mul(t0, t1, t0);
+  fe_sqn(t1, t0, 50);
+  fe_mul(t1, t1, t0);
+  fe_sqn(t2, t1, 100);
+  fe_mul(t1, t2, t1);
+  fe_sqn(t1, t1, 50);
+  fe_mul(t0, t1, t0);
+  fe_sqn(t0, t0, 2);
+  fe_mul(out, t0, z);
+}
+
+}  // namespace edv

@@ -1,0 +1,245 @@
+// ge25519.h -- edwards25519 group arithmetic (a = -1) on top of fe25519.h.
+//
+// Restates the point half of libsodium 1.0.18's verify, reached from
+// stp_core/crypto/nacl_wrappers.py:108: decoding A with
+// ge25519_frombytes_negate_vartime, the double-scalar multiplication
+// [h](-A) + [S]B, and the final encoding compared byte-for-byte with R.
+// Coordinates follow the usual extended/completed split:
+//   p2 (X:Y:Z), p3 (X:Y:Z:T), p1p1 ((X:Z),(Y:T)), cached (Y+X, Y-X, Z, 2dT),
+//   niels (y+x, y-x, 2dxy) for affine precomputed points.
+// Bound classes (fe25519.h) are annotated on every intermediate.
+#pragma once
+#include "fe25519.h"
+#include "base_table.h"
+
+namespace edv {
+
+struct ge_p2 {
+  fe X, Y, Z;
+};
+struct ge_p3 {
+  fe X, Y, Z, T;
+};
+struct ge_p1p1 {
+  fe X, Y, Z, T;
+};
+struct ge_cached {
+  fe YplusX, YminusX, Z, T2d;
+};
+struct ge_niels {
+  fe ypx, ymx, xy2d;
+};
+
+// Curve constants (d, 2d, sqrt(-1)) and base tables: base_table.h, generated
+// by tools/gen_constants.py from exact integers.
+
+EDV_HD void ge_p3_0(ge_p3& h) {
+  fe_0(h.X);
+  fe_1(h.Y);
+  fe_1(h.Z);
+  fe_0(h.T);
+}
+EDV_HD void ge_cached_0(ge_cached& h) {
+  fe_1(h.YplusX);
+  fe_1(h.YminusX);
+  fe_1(h.Z);
+  fe_0(h.T2d);
+}
+EDV_HD void ge_niels_0(ge_niels& h) {
+  fe_1(h.ypx);
+  fe_1(h.ymx);
+  fe_0(h.xy2d);
+}
+
+EDV_HD void ge_p1p1_to_p2(ge_p2& r, const ge_p1p1& p) {
+  fe_mul(r.X, p.X, p.T);
+  fe_mul(r.Y, p.Y, p.Z);
+  fe_mul(r.Z, p.Z, p.T);
+}
+EDV_HD void ge_p1p1_to_p3(ge_p3& r, const ge_p1p1& p) {
+  fe_mul(r.X, p.X, p.T);
+  fe_mul(r.Y, p.Y, p.Z);
+  fe_mul(r.Z, p.Z, p.T);
+  fe_mul(r.T, p.X, p.Y);
+}
+EDV_HD void ge_p3_to_p2(ge_p2& r, const ge_p3& p) {
+  r.X = p.X;
+  r.Y = p.Y;
+  r.Z = p.Z;
+}
+// p3 (all C) -> cached (YplusX L, YminusX L, Z C, T2d C).
+EDV_HD void ge_p3_to_cached(ge_cached& r, const ge_p3& p) {
+  fe_add(r.YplusX, p.Y, p.X);
+  fe_sub(r.YminusX, p.Y, p.X);
+  r.Z = p.Z;
+  fe_mul(r.T2d, p.T, fe_const_d2());
+}
+
+// r = 2p.  p in C.  Output: X W, Y L, Z L, T C.
+EDV_HD void ge_p2_dbl(ge_p1p1& r, const ge_p2& p) {
+  fe xx, yy, zz, aa, s;
+  fe_sq(xx, p.X);
+  fe_sq(yy, p.Y);
+  fe_sq(zz, p.Z);
+  fe_add(s, p.X, p.Y);  // L
+  fe_sq(aa, s);
+  fe_add(r.Y, yy, xx);        // L
+  fe_sub(r.Z, yy, xx);        // L
+  fe_sub4(r.X, aa, r.Y);      // W   (AA - YY - XX = 2XY)
+  fe t;
+  fe_add(t, zz, zz);
+  fe_add(t, t, xx);           // 3 C
+  fe_sub(r.T, t, yy);         // W   (2ZZ + XX - YY)
+  fe_carry(r.T);              // C
+}
+EDV_HD void ge_p3_dbl(ge_p1p1& r, const ge_p3& p) {
+  ge_p2 q;
+  ge_p3_to_p2(q, p);
+  ge_p2_dbl(r, q);
+}
+
+// r = p + q.  p in C, q cached.  Output: X L, Y L, Z L, T W.
+EDV_HD void ge_add(ge_p1p1& r, const ge_p3& p, const ge_cached& q) {
+  fe s, a, b, c, d;
+  fe_add(s, p.Y, p.X);
+  fe_mul(a, s, q.YplusX);
+  fe_sub(s, p.Y, p.X);
+  fe_mul(b, s, q.YminusX);
+  fe_mul(c, p.T, q.T2d);
+  fe_mul(d, p.Z, q.Z);
+  fe_add(d, d, d);            // L
+  fe_sub(r.X, a, b);          // L
+  fe_add(r.Y, a, b);          // L
+  fe_add(r.Z, d, c);          // L (3 C)
+  fe_sub(r.T, d, c);          // 2C + 2p: W
+}
+// r = p - q.  Output: X L, Y L, Z W, T L.
+EDV_HD void ge_sub(ge_p1p1& r, const ge_p3& p, const ge_cached& q) {
+  fe s, a, b, c, d;
+  fe_add(s, p.Y, p.X);
+  fe_mul(a, s, q.YminusX);
+  fe_sub(s, p.Y, p.X);
+  fe_mul(b, s, q.YplusX);
+  fe_mul(c, p.T, q.T2d);
+  fe_mul(d, p.Z, q.Z);
+  fe_add(d, d, d);
+  fe_sub(r.X, a, b);
+  fe_add(r.Y, a, b);
+  fe_sub(r.Z, d, c);          // W
+  fe_add(r.T, d, c);          // L
+}
+// r = p + q for affine q.  Output as ge_add.
+EDV_HD void ge_madd(ge_p1p1& r, const ge_p3& p, const ge_niels& q) {
+  fe s, a, b, c, d;
+  fe_add(s, p.Y, p.X);
+  fe_mul(a, s, q.ypx);
+  fe_sub(s, p.Y, p.X);
+  fe_mul(b, s, q.ymx);
+  fe_mul(c, p.T, q.xy2d);
+  fe_add(d, p.Z, p.Z);        // L
+  fe_sub(r.X, a, b);
+  fe_add(r.Y, a, b);
+  fe_add(r.Z, d, c);
+  fe_sub(r.T, d, c);          // W
+}
+// r = p - q for affine q.  Output as ge_sub.
+EDV_HD void ge_msub(ge_p1p1& r, const ge_p3& p, const ge_niels& q) {
+  fe s, a, b, c, d;
+  fe_add(s, p.Y, p.X);
+  fe_mul(a, s, q.ymx);
+  fe_sub(s, p.Y, p.X);
+  fe_mul(b, s, q.ypx);
+  fe_mul(c, p.T, q.xy2d);
+  fe_add(d, p.Z, p.Z);
+  fe_sub(r.X, a, b);
+  fe_add(r.Y, a, b);
+  fe_sub(r.Z, d, c);          // W
+  fe_add(r.T, d, c);
+}
+
+// p1p1 -> p2/p3 need the W operand first (fe_mul's f).  ge_add/madd leave T
+// in W, ge_sub/msub leave Z in W; ge_p2_dbl leaves X in W and T carried.
+EDV_HD void ge_p1p1_to_p3_addlike(ge_p3& r, const ge_p1p1& p) {  // T is W
+  fe_mul(r.X, p.T, p.X);
+  fe_mul(r.Y, p.Y, p.Z);
+  fe_mul(r.Z, p.T, p.Z);
+  fe_mul(r.T, p.X, p.Y);
+}
+EDV_HD void ge_p1p1_to_p3_sublike(ge_p3& r, const ge_p1p1& p) {  // Z is W
+  fe_mul(r.X, p.X, p.T);
+  fe_mul(r.Y, p.Z, p.Y);
+  fe_mul(r.Z, p.Z, p.T);
+  fe_mul(r.T, p.X, p.Y);
+}
+EDV_HD void ge_p1p1_to_p2_addlike(ge_p2& r, const ge_p1p1& p) {
+  fe_mul(r.X, p.T, p.X);
+  fe_mul(r.Y, p.Y, p.Z);
+  fe_mul(r.Z, p.T, p.Z);
+}
+EDV_HD void ge_p1p1_to_p2_sublike(ge_p2& r, const ge_p1p1& p) {
+  fe_mul(r.X, p.X, p.T);
+  fe_mul(r.Y, p.Z, p.Y);
+  fe_mul(r.Z, p.Z, p.T);
+}
+// After ge_p2_dbl: X is W, T is C, Y/Z L.
+EDV_HD void ge_dbl_to_p2(ge_p2& r, const ge_p1p1& p) {
+  fe_mul(r.X, p.X, p.T);
+  fe_mul(r.Y, p.Y, p.Z);
+  fe_mul(r.Z, p.Z, p.T);
+}
+EDV_HD void ge_dbl_to_p3(ge_p3& r, const ge_p1p1& p) {
+  fe_mul(r.X, p.X, p.T);
+  fe_mul(r.Y, p.Y, p.Z);
+  fe_mul(r.Z, p.Z, p.T);
+  fe_mul(r.T, p.X, p.Y);
+}
+
+// Encoding: y with the sign of x in bit 255 (8 LE words).
+EDV_HDNI void ge_tobytes(uint32_t s[8], const ge_p2& h) {
+  fe recip, x, y;
+  fe_invert(recip, h.Z);
+  fe_mul(x, h.X, recip);
+  fe_mul(y, h.Y, recip);
+  fe_tobytes(s, y);
+  s[7] ^= fe_isnegative(x) << 31;
+}
+
+// libsodium 1.0.18 ge25519_frombytes_negate_vartime restated; negate = false
+// gives +P (base point, signer).  Returns false if x^2 has no square root.
+EDV_HDNI bool ge_frombytes(ge_p3& h, const uint32_t s[8], bool negate) {
+  fe u, v, v3, vxx, chk, one;
+  fe_1(one);
+  fe_frombytes(h.Y, s);
+  fe_1(h.Z);
+  fe_sq(u, h.Y);
+  fe_mul(v, u, fe_const_d());
+  fe_sub(u, u, one);   // y^2 - 1           (L)
+  fe_carry(u);         // C
+  fe_add(v, v, one);   // d y^2 + 1         (C + 1)
+  fe_sq(v3, v);
+  fe_mul(v3, v3, v);   // v^3
+  fe_sq(h.X, v3);
+  fe_mul(h.X, h.X, v);
+  fe_mul(h.X, h.X, u); // u v^7
+  fe_pow22523(h.X, h.X);
+  fe_mul(h.X, h.X, v3);
+  fe_mul(h.X, h.X, u); // u v^3 (u v^7)^((p-5)/8)
+  fe_sq(vxx, h.X);
+  fe_mul(vxx, vxx, v);
+  fe_sub(chk, vxx, u); // v x^2 - u
+  if (!fe_iszero(chk)) {
+    fe_add(chk, vxx, u);
+    if (!fe_iszero(chk)) return false;
+    fe_mul(h.X, h.X, fe_const_sqrtm1());
+  }
+  const uint32_t sign = s[7] >> 31;
+  const bool flip = negate ? (fe_isnegative(h.X) == sign) : (fe_isnegative(h.X) != sign);
+  if (flip) {
+    fe_neg(h.X, h.X);
+    fe_carry(h.X);
+  }
+  fe_mul(h.T, h.X, h.Y);
+  return true;
+}
+
+}  // namespace edv

@@ -1,0 +1,110 @@
+// host_check.cpp -- TEST INFRASTRUCTURE: the kernel arithmetic (verify_core.h
+// and friends) compiled for the host CPU with EDV_BOUND_CHECK limb-bound
+// assertions, so tests/ can check the exact device code paths against the
+// oracle without a GPU.  The product (libplenum_edverify.so) never links this.
+#include <string.h>
+
+#include "verify_core.h"
+
+using namespace edv;
+
+namespace {
+struct HostTableA {
+  ge_cached e[8];
+  void store(int j, const ge_cached& c) { e[j] = c; }
+  void load(int j, ge_cached& c) const { c = e[j]; }
+};
+struct HostTableB {
+  void load(int j, ge_niels& n) const {
+    const uint32_t* p = BASE_SMALL_U32 + 30 * j;
+    memcpy(n.ypx.v, p, 40);
+    memcpy(n.ymx.v, p + 10, 40);
+    memcpy(n.xy2d.v, p + 20, 40);
+  }
+};
+}  // namespace
+
+extern "C" {
+
+int edv_host_verify(const uint8_t* sig64, const uint8_t* pk32, const uint8_t* msg, uint64_t mlen) {
+  uint32_t sig[16], pk[8];
+  memcpy(sig, sig64, 64);
+  memcpy(pk, pk32, 32);
+  HostTableA ta;
+  HostTableB tb;
+  return verify_one(sig, pk, msg, mlen, ta, tb) ? 0 : -1;
+}
+
+void edv_host_sha512_prefixed(uint8_t out[64], const uint8_t prefix64[64], const uint8_t* msg, uint64_t mlen) {
+  uint32_t pre[16], dig[16];
+  memcpy(pre, prefix64, 64);
+  sha512_prefixed<16>(dig, pre, msg, mlen);
+  memcpy(out, dig, 64);
+}
+
+void edv_host_sc_reduce(uint8_t out[32], const uint8_t in[64]) {
+  uint32_t i[16], o[8];
+  memcpy(i, in, 64);
+  sc_reduce(o, i);
+  memcpy(out, o, 32);
+}
+
+int edv_host_sc_is_canonical(const uint8_t s[32]) {
+  uint32_t w[8];
+  memcpy(w, s, 32);
+  return sc_is_canonical(w);
+}
+
+// out = canonical bytes of (a * b) for field elements given as 32-byte LE
+// integers < 2^255 (exercises fe_frombytes, fe_mul, fe_sq, fe_tobytes).
+void edv_host_fe_mul(uint8_t out[32], const uint8_t a[32], const uint8_t b[32], int square) {
+  uint32_t wa[8], wb[8], wo[8];
+  memcpy(wa, a, 32);
+  memcpy(wb, b, 32);
+  fe fa, fb, fo;
+  fe_frombytes(fa, wa);
+  fe_frombytes(fb, wb);
+  if (square)
+    fe_sq(fo, fa);
+  else
+    fe_mul(fo, fa, fb);
+  fe_tobytes(wo, fo);
+  memcpy(out, wo, 32);
+}
+
+void edv_host_fe_invert(uint8_t out[32], const uint8_t a[32]) {
+  uint32_t wa[8], wo[8];
+  memcpy(wa, a, 32);
+  fe fa, fo;
+  fe_frombytes(fa, wa);
+  fe_invert(fo, fa);
+  fe_tobytes(wo, fo);
+  memcpy(out, wo, 32);
+}
+
+// Decode (negate = 0) and re-encode a point; -1 if not on the curve.
+int edv_host_point_roundtrip(uint8_t out[32], const uint8_t in[32]) {
+  uint32_t w[8], o[8];
+  memcpy(w, in, 32);
+  ge_p3 P;
+  if (!ge_frombytes(P, w, false)) return -1;
+  ge_p2 p2;
+  ge_p3_to_p2(p2, P);
+  ge_tobytes(o, p2);
+  memcpy(out, o, 32);
+  return 0;
+}
+
+int edv_host_has_small_order(const uint8_t s[32]) {
+  uint32_t w[8];
+  memcpy(w, s, 32);
+  return has_small_order(w);
+}
+
+int edv_host_is_canonical_point(const uint8_t s[32]) {
+  uint32_t w[8];
+  memcpy(w, s, 32);
+  return is_canonical_point(w);
+}
+
+}  // extern "C"

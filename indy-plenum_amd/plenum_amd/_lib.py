@@ -1,0 +1,78 @@
+"""ctypes binding of libplenum_edverify.so (C ABI: include/edverify.h).
+
+This is the only way the Python package reaches the verifier: there is no CPU
+fallback.  If the shared library is missing, or no gfx950 device is visible,
+every verify call raises EdVerifyUnavailable (the product fails loudly rather
+than silently verifying on the host)."""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get(
+    "PLENUM_EDVERIFY_LIB", os.path.join(os.path.dirname(_HERE), "libplenum_edverify.so"))
+
+# Every symbol include/edverify.h declares, with its ctypes signature.
+_c = ctypes
+_P = _c.c_void_p
+_U64 = _c.c_uint64
+_U32 = _c.c_uint32
+_I = _c.c_int
+SIGNATURES = {
+    "edv_version": (_c.c_char_p, []),
+    "edv_last_error": (_c.c_char_p, []),
+    "edv_device_count": (_I, []),
+    "edv_create": (_P, [_I]),
+    "edv_destroy": (None, [_P]),
+    "edv_synchronize": (_I, [_P]),
+    "edv_verify_batch": (_I, [_P, _P, _P, _P, _P, _U64, _P]),
+    "edv_sign_open_batch": (_I, [_P, _P, _P, _P, _U64, _P]),
+    "edv_verify_batch_device": (_I, [_P, _P, _P, _P, _P, _U64, _P, _P]),
+    "edv_last_phase_ms": (_I, [_P, _P, _P, _P]),
+    "edv_last_kernel_ms": (_c.c_double, [_P]),
+    "edv_seed_keypair_batch": (_I, [_P, _P, _U64, _P, _P]),
+    "edv_sign_batch_device": (_I, [_P, _P, _P, _P, _P, _U64, _P, _P]),
+    "edv_sign_batch": (_I, [_P, _P, _P, _P, _P, _U64, _P]),
+    "edv_tally_device": (_I, [_P, _P, _P, _P, _P, _U64, _U32, _U32, _P, _P, _P, _P]),
+    "edv_tally_finish_device": (_I, [_P, _P, _U32, _U32, _P, _P, _P]),
+    "edv_tally": (_I, [_P, _P, _P, _P, _P, _U64, _U32, _U32, _P, _P]),
+}
+
+
+class EdVerifyUnavailable(RuntimeError):
+    """The HIP verify library or a gfx950 device is not available."""
+
+
+class EdVerifyError(RuntimeError):
+    """A library call returned a negative EDV_E* code."""
+
+    def __init__(self, code, msg):
+        super().__init__("edverify error %d: %s" % (code, msg))
+        self.code = code
+
+
+_lib = None
+
+
+def load():
+    """Load (once) and return the ctypes library; raises EdVerifyUnavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise EdVerifyUnavailable(
+            "libplenum_edverify.so not built at %s (run __graft_entry__.build())" % LIB_PATH)
+    try:
+        lib = ctypes.CDLL(LIB_PATH)
+    except OSError as ex:
+        raise EdVerifyUnavailable("cannot load %s: %s" % (LIB_PATH, ex)) from ex
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(code):
+    if code != 0:
+        raise EdVerifyError(code, load().edv_last_error().decode(errors="replace"))

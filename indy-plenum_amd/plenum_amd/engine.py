@@ -1,0 +1,189 @@
+"""EdVerifyEngine: numpy / device-pointer front end of libplenum_edverify.so.
+
+One engine = one HIP context = one GPU (include/edverify.h).  The verify
+entry points replace per-request calls of
+stp_core/crypto/nacl_wrappers.py:232-242 (Verifier.verify) with one batched
+launch; verdicts are libsodium 1.0.18's (crypto_sign_verify_detached == 0).
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import EdVerifyUnavailable, check
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _dev(x):
+    """Device pointer from a torch tensor / int / None."""
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return ctypes.c_void_p(x)
+    return ctypes.c_void_p(x.data_ptr())
+
+
+def pack_messages(msgs):
+    """list of bytes -> (uint8 buffer, uint64 offsets[n+1])."""
+    lens = np.fromiter((len(m) for m in msgs), dtype=np.uint64, count=len(msgs))
+    off = np.zeros(len(msgs) + 1, dtype=np.uint64)
+    np.cumsum(lens, out=off[1:])
+    buf = np.frombuffer(b"".join(msgs), dtype=np.uint8) if len(msgs) else np.zeros(0, np.uint8)
+    return buf, off
+
+
+def unpack_bits(bits, n):
+    return np.unpackbits(np.asarray(bits, dtype=np.uint8), bitorder="little")[:n].astype(bool)
+
+
+class EdVerifyEngine:
+    """Batched Ed25519 verify / sign / vote tally on one MI355X."""
+
+    def __init__(self, device=0):
+        lib = _lib.load()
+        ndev = lib.edv_device_count()
+        if ndev <= device:
+            raise EdVerifyUnavailable("no HIP device %d (found %d)" % (device, ndev))
+        ctx = lib.edv_create(device)
+        if not ctx:
+            raise EdVerifyUnavailable(lib.edv_last_error().decode(errors="replace"))
+        self._lib = lib
+        self._ctx = ctypes.c_void_p(ctx)
+        self.device = device
+
+    # ------------------------------------------------------------- lifecycle
+    def close(self):
+        if getattr(self, "_ctx", None):
+            self._lib.edv_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def version(self):
+        return self._lib.edv_version().decode()
+
+    def synchronize(self):
+        check(self._lib.edv_synchronize(self._ctx))
+
+    # ---------------------------------------------------------------- verify
+    def verify_bits(self, sig64, pk32, msgs, msg_off):
+        """Packed accept bitmask ((n + 7) // 8 bytes, LSB-first)."""
+        sig64 = np.ascontiguousarray(sig64, dtype=np.uint8).reshape(-1, 64)
+        pk32 = np.ascontiguousarray(pk32, dtype=np.uint8).reshape(-1, 32)
+        msgs = np.ascontiguousarray(np.frombuffer(msgs, np.uint8) if isinstance(msgs, (bytes, bytearray))
+                                    else msgs, dtype=np.uint8)
+        msg_off = np.ascontiguousarray(msg_off, dtype=np.uint64)
+        n = sig64.shape[0]
+        if pk32.shape[0] != n or msg_off.shape[0] != n + 1:
+            raise ValueError("shape mismatch: sig %d, pk %d, off %d" % (n, pk32.shape[0], msg_off.shape[0]))
+        if n and int(msg_off[-1]) > msgs.shape[0]:
+            raise ValueError("msg_off exceeds message buffer")
+        bits = np.zeros((n + 7) // 8, dtype=np.uint8)
+        if n:
+            check(self._lib.edv_verify_batch(self._ctx, _ptr(sig64), _ptr(pk32), _ptr(msgs) if msgs.size else None,
+                                             _ptr(msg_off), n, _ptr(bits)))
+        return bits
+
+    def verify_batch(self, sig64, pk32, msgs, msg_off):
+        """Bool array: accepted[i] == (crypto_sign_verify_detached(...) == 0)."""
+        n = np.asarray(sig64).reshape(-1, 64).shape[0]
+        return unpack_bits(self.verify_bits(sig64, pk32, msgs, msg_off), n)
+
+    def sign_open_batch(self, sm, sm_off, pk32):
+        """crypto_sign_open verdicts over signed messages sm_i = sig || msg
+        (exactly VerifyKey.verify(signature + msg), nacl_wrappers.py:100-108)."""
+        sm = np.ascontiguousarray(np.frombuffer(sm, np.uint8) if isinstance(sm, (bytes, bytearray)) else sm,
+                                  dtype=np.uint8)
+        sm_off = np.ascontiguousarray(sm_off, dtype=np.uint64)
+        pk32 = np.ascontiguousarray(pk32, dtype=np.uint8).reshape(-1, 32)
+        n = pk32.shape[0]
+        if sm_off.shape[0] != n + 1:
+            raise ValueError("sm_off must have n + 1 entries")
+        bits = np.zeros((n + 7) // 8, dtype=np.uint8)
+        if n:
+            check(self._lib.edv_sign_open_batch(self._ctx, _ptr(sm) if sm.size else None, _ptr(sm_off), _ptr(pk32),
+                                                n, _ptr(bits)))
+        return unpack_bits(bits, n)
+
+    def verify_batch_device(self, d_sig64, d_pk32, d_msgs, d_msg_off, n, d_accept_words, stream=None):
+        """Asynchronous verify on device buffers (torch tensors or raw pointers)."""
+        check(self._lib.edv_verify_batch_device(self._ctx, _dev(d_sig64), _dev(d_pk32), _dev(d_msgs),
+                                                _dev(d_msg_off), n, _dev(d_accept_words), _dev(stream)))
+
+    def last_phase_ms(self):
+        """(hash, table, dsm) milliseconds of the last verify launch (HIP events)."""
+        h, t, d = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        check(self._lib.edv_last_phase_ms(self._ctx, ctypes.byref(h), ctypes.byref(t), ctypes.byref(d)))
+        return h.value, t.value, d.value
+
+    # ------------------------------------------------------------------ sign
+    def seed_keypair_batch(self, seeds32):
+        seeds32 = np.ascontiguousarray(seeds32, dtype=np.uint8).reshape(-1, 32)
+        n = seeds32.shape[0]
+        pk = np.zeros((n, 32), np.uint8)
+        sk = np.zeros((n, 64), np.uint8)
+        if n:
+            check(self._lib.edv_seed_keypair_batch(self._ctx, _ptr(seeds32), n, _ptr(pk), _ptr(sk)))
+        return pk, sk
+
+    def sign_batch(self, sk64, key_idx, msgs, msg_off):
+        sk64 = np.ascontiguousarray(sk64, dtype=np.uint8).reshape(-1, 64)
+        key_idx = np.ascontiguousarray(key_idx, dtype=np.uint32)
+        msgs = np.ascontiguousarray(np.frombuffer(msgs, np.uint8) if isinstance(msgs, (bytes, bytearray))
+                                    else msgs, dtype=np.uint8)
+        msg_off = np.ascontiguousarray(msg_off, dtype=np.uint64)
+        n = key_idx.shape[0]
+        if n and int(key_idx.max()) >= sk64.shape[0]:
+            raise ValueError("key_idx out of range")
+        sig = np.zeros((n, 64), np.uint8)
+        if n:
+            check(self._lib.edv_sign_batch(self._ctx, _ptr(sk64), _ptr(key_idx), _ptr(msgs) if msgs.size else None,
+                                           _ptr(msg_off), n, _ptr(sig)))
+        return sig
+
+    def sign_batch_device(self, d_sk64, d_key_idx, d_msgs, d_msg_off, n, d_sig_out, stream=None):
+        check(self._lib.edv_sign_batch_device(self._ctx, _dev(d_sk64), _dev(d_key_idx), _dev(d_msgs),
+                                              _dev(d_msg_off), n, _dev(d_sig_out), _dev(stream)))
+
+    # ----------------------------------------------------------------- tally
+    def tally(self, key, voter, phase, valid, n_keys, n_validators):
+        """Distinct-voter PREPARE/COMMIT counts and quorum flags per key.
+        Returns (counts uint32[n_keys, 2], prepare_quorum bool[n_keys],
+        commit_quorum bool[n_keys])."""
+        key = np.ascontiguousarray(key, dtype=np.uint32)
+        voter = np.ascontiguousarray(voter, dtype=np.uint8)
+        phase = np.ascontiguousarray(phase, dtype=np.uint8)
+        valid = np.ascontiguousarray(valid, dtype=np.uint8)
+        nv = key.shape[0]
+        counts = np.zeros((n_keys, 2), np.uint32)
+        quorum = np.zeros(n_keys, np.uint8)
+        if n_keys:
+            check(self._lib.edv_tally(self._ctx, _ptr(key), _ptr(voter), _ptr(phase), _ptr(valid), nv, n_keys,
+                                      n_validators, _ptr(counts), _ptr(quorum)))
+        return counts, (quorum & 1).astype(bool), (quorum & 2).astype(bool)
+
+    def tally_device(self, d_key, d_voter, d_phase, d_valid, n_votes, n_keys, n_validators, d_ballot, d_counts,
+                     d_quorum, stream=None):
+        check(self._lib.edv_tally_device(self._ctx, _dev(d_key), _dev(d_voter), _dev(d_phase), _dev(d_valid),
+                                         n_votes, n_keys, n_validators, _dev(d_ballot), _dev(d_counts),
+                                         _dev(d_quorum), _dev(stream)))
+
+    def tally_finish_device(self, d_ballot, n_keys, n_validators, d_counts, d_quorum, stream=None):
+        check(self._lib.edv_tally_finish_device(self._ctx, _dev(d_ballot), n_keys, n_validators, _dev(d_counts),
+                                                _dev(d_quorum), _dev(stream)))

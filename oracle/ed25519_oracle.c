@@ -1,0 +1,543 @@
+/*
+ * ed25519_oracle.c -- TEST INFRASTRUCTURE ONLY (the parity checker).
+ *
+ * A plain-C, deliberately simple restatement of the Ed25519 verification the
+ * Plenum request-authentication path ends in:
+ *
+ *   plenum/server/client_authn.py:99-102   NaclAuthNr.authenticate -> DidVerifier.verify
+ *   plenum/common/verifier.py:48-49         DidVerifier.verify -> NaclVerifier.verify
+ *   stp_core/crypto/nacl_wrappers.py:232-242 Verifier.verify(sig, msg): key.verify(sig + msg)
+ *   stp_core/crypto/nacl_wrappers.py:100-108 VerifyKey.verify -> libnacl.crypto_sign_open(sm, pk)
+ *
+ * The arithmetic itself lives in a third-party dependency absent from
+ * /root/reference: libsodium (pinned here to 1.0.18, the version present in
+ * this image at /opt/conda/lib/libsodium.so.23; reached through libnacl).
+ * This file restates libsodium 1.0.18's published algorithm
+ * (crypto_sign/ed25519/ref10/open.c `_crypto_sign_ed25519_verify_detached`,
+ * crypto_core/ed25519/ref10/ed25519_ref10.c `ge25519_has_small_order`,
+ * `ge25519_is_canonical`, `sc25519_is_canonical`,
+ * `ge25519_frombytes_negate_vartime`) -- NOT its code: field elements are
+ * radix-2^51 with 128-bit products, scalar multiplication is plain
+ * double-and-add, reduction mod L is bit-serial.  Speed is irrelevant here;
+ * obviousness is the point.
+ *
+ * Parity pinning: tests/test_oracle.py checks every function here against the
+ * golden vectors in tests/golden/ (generated from libsodium 1.0.18 itself by
+ * tests/golden/gen_golden.py), and differentially against libsodium on random
+ * and adversarial inputs when libsodium is loadable.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
+ * this library.  The product path (indy-plenum_amd/) never does.
+ */
+#include <stdint.h>
+#include <string.h>
+#include <stddef.h>
+
+typedef unsigned __int128 u128;
+
+/* ------------------------------------------------------------------ SHA-512 */
+/* FIPS 180-4, as used by crypto_hash_sha512 in libsodium. */
+static const uint64_t K512[80] = {
+  0x428a2f98d728ae22ULL, 0x7137449123ef65cdULL, 0xb5c0fbcfec4d3b2fULL, 0xe9b5dba58189dbbcULL,
+  0x3956c25bf348b538ULL, 0x59f111f1b605d019ULL, 0x923f82a4af194f9bULL, 0xab1c5ed5da6d8118ULL,
+  0xd807aa98a3030242ULL, 0x12835b0145706fbeULL, 0x243185be4ee4b28cULL, 0x550c7dc3d5ffb4e2ULL,
+  0x72be5d74f27b896fULL, 0x80deb1fe3b1696b1ULL, 0x9bdc06a725c71235ULL, 0xc19bf174cf692694ULL,
+  0xe49b69c19ef14ad2ULL, 0xefbe4786384f25e3ULL, 0x0fc19dc68b8cd5b5ULL, 0x240ca1cc77ac9c65ULL,
+  0x2de92c6f592b0275ULL, 0x4a7484aa6ea6e483ULL, 0x5cb0a9dcbd41fbd4ULL, 0x76f988da831153b5ULL,
+  0x983e5152ee66dfabULL, 0xa831c66d2db43210ULL, 0xb00327c898fb213fULL, 0xbf597fc7beef0ee4ULL,
+  0xc6e00bf33da88fc2ULL, 0xd5a79147930aa725ULL, 0x06ca6351e003826fULL, 0x142929670a0e6e70ULL,
+  0x27b70a8546d22ffcULL, 0x2e1b21385c26c926ULL, 0x4d2c6dfc5ac42aedULL, 0x53380d139d95b3dfULL,
+  0x650a73548baf63deULL, 0x766a0abb3c77b2a8ULL, 0x81c2c92e47edaee6ULL, 0x92722c851482353bULL,
+  0xa2bfe8a14cf10364ULL, 0xa81a664bbc423001ULL, 0xc24b8b70d0f89791ULL, 0xc76c51a30654be30ULL,
+  0xd192e819d6ef5218ULL, 0xd69906245565a910ULL, 0xf40e35855771202aULL, 0x106aa07032bbd1b8ULL,
+  0x19a4c116b8d2d0c8ULL, 0x1e376c085141ab53ULL, 0x2748774cdf8eeb99ULL, 0x34b0bcb5e19b48a8ULL,
+  0x391c0cb3c5c95a63ULL, 0x4ed8aa4ae3418acbULL, 0x5b9cca4f7763e373ULL, 0x682e6ff3d6b2b8a3ULL,
+  0x748f82ee5defb2fcULL, 0x78a5636f43172f60ULL, 0x84c87814a1f0ab72ULL, 0x8cc702081a6439ecULL,
+  0x90befffa23631e28ULL, 0xa4506cebde82bde9ULL, 0xbef9a3f7b2c67915ULL, 0xc67178f2e372532bULL,
+  0xca273eceea26619cULL, 0xd186b8c721c0c207ULL, 0xeada7dd6cde0eb1eULL, 0xf57d4f7fee6ed178ULL,
+  0x06f067aa72176fbaULL, 0x0a637dc5a2c898a6ULL, 0x113f9804bef90daeULL, 0x1b710b35131c471bULL,
+  0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL, 0x431d67c49c100d4cULL,
+  0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL};
+
+typedef struct { uint64_t h[8]; uint8_t buf[128]; size_t fill; uint64_t total; } sha512_ctx;
+
+static uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+
+static void sha512_block(uint64_t h[8], const uint8_t *p) {
+  uint64_t w[80];
+  for (int i = 0; i < 16; i++) {
+    uint64_t v = 0;
+    for (int j = 0; j < 8; j++) v = (v << 8) | p[8 * i + j];
+    w[i] = v;
+  }
+  for (int i = 16; i < 80; i++) {
+    uint64_t s0 = rotr64(w[i - 15], 1) ^ rotr64(w[i - 15], 8) ^ (w[i - 15] >> 7);
+    uint64_t s1 = rotr64(w[i - 2], 19) ^ rotr64(w[i - 2], 61) ^ (w[i - 2] >> 6);
+    w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+  }
+  uint64_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+  for (int i = 0; i < 80; i++) {
+    uint64_t S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);
+    uint64_t ch = (e & f) ^ (~e & g);
+    uint64_t t1 = hh + S1 + ch + K512[i] + w[i];
+    uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);
+    uint64_t mj = (a & b) ^ (a & c) ^ (b & c);
+    uint64_t t2 = S0 + mj;
+    hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+  }
+  h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+}
+
+static void sha512_init(sha512_ctx *c) {
+  static const uint64_t iv[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
+                                 0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
+                                 0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
+  memcpy(c->h, iv, sizeof iv);
+  c->fill = 0;
+  c->total = 0;
+}
+
+static void sha512_update(sha512_ctx *c, const uint8_t *m, size_t n) {
+  c->total += n;
+  while (n) {
+    size_t take = 128 - c->fill;
+    if (take > n) take = n;
+    memcpy(c->buf + c->fill, m, take);
+    c->fill += take; m += take; n -= take;
+    if (c->fill == 128) { sha512_block(c->h, c->buf); c->fill = 0; }
+  }
+}
+
+static void sha512_final(sha512_ctx *c, uint8_t out[64]) {
+  uint64_t bits = c->total * 8;
+  uint8_t pad = 0x80;
+  sha512_update(c, &pad, 1);
+  uint8_t z = 0;
+  while (c->fill != 112) sha512_update(c, &z, 1);
+  uint8_t len[16] = {0};
+  for (int i = 0; i < 8; i++) len[15 - i] = (uint8_t)(bits >> (8 * i));
+  sha512_update(c, len, 16);
+  for (int i = 0; i < 8; i++)
+    for (int j = 0; j < 8; j++) out[8 * i + j] = (uint8_t)(c->h[i] >> (56 - 8 * j));
+}
+
+void oracle_sha512(uint8_t out[64], const uint8_t *m, uint64_t mlen) {
+  sha512_ctx c;
+  sha512_init(&c);
+  sha512_update(&c, m, (size_t)mlen);
+  sha512_final(&c, out);
+}
+
+/* ------------------------------------------------------ scalars mod L */
+/* L = 2^252 + 27742317777372353535851937790883648493, as 4 LE 64-bit words. */
+static const uint64_t Lw[4] = {0x5812631a5cf5d3edULL, 0x14def9dea2f79cd6ULL, 0ULL, 0x1000000000000000ULL};
+
+static int ge4(const uint64_t a[4], const uint64_t b[4]) {
+  for (int i = 3; i >= 0; i--) {
+    if (a[i] > b[i]) return 1;
+    if (a[i] < b[i]) return 0;
+  }
+  return 1;
+}
+static void sub4(uint64_t a[4], const uint64_t b[4]) {
+  u128 borrow = 0;
+  for (int i = 0; i < 4; i++) {
+    u128 t = (u128)a[i] - b[i] - borrow;
+    a[i] = (uint64_t)t;
+    borrow = (t >> 127) & 1;
+  }
+}
+/* r = (little-endian nbytes integer) mod L, bit-serial: r = 2r + bit; if r >= L: r -= L. */
+static void reduce_le(uint64_t r[4], const uint8_t *x, int nbytes) {
+  r[0] = r[1] = r[2] = r[3] = 0;
+  for (int bit = nbytes * 8 - 1; bit >= 0; bit--) {
+    uint64_t top = 0;
+    for (int i = 0; i < 4; i++) {
+      uint64_t nt = r[i] >> 63;
+      r[i] = (r[i] << 1) | top;
+      top = nt;
+    }
+    r[0] |= (x[bit >> 3] >> (bit & 7)) & 1;
+    if (ge4(r, Lw)) sub4(r, Lw);
+  }
+}
+static void words_to_bytes32(uint8_t out[32], const uint64_t r[4]) {
+  for (int i = 0; i < 32; i++) out[i] = (uint8_t)(r[i >> 3] >> (8 * (i & 7)));
+}
+/* sc25519_reduce: 64-byte -> 32-byte scalar mod L. */
+void oracle_sc_reduce(uint8_t out[32], const uint8_t in[64]) {
+  uint64_t r[4];
+  reduce_le(r, in, 64);
+  words_to_bytes32(out, r);
+}
+/* sc25519_is_canonical: s < L. */
+static int sc_is_canonical(const uint8_t s[32]) {
+  uint64_t w[4] = {0, 0, 0, 0};
+  for (int i = 0; i < 32; i++) w[i >> 3] |= (uint64_t)s[i] << (8 * (i & 7));
+  return !ge4(w, Lw);
+}
+/* out = (a*b + c) mod L, all 32-byte LE scalars (a, b may be >= L). */
+static void sc_muladd(uint8_t out[32], const uint8_t a[32], const uint8_t b[32], const uint8_t c[32]) {
+  uint64_t aw[4] = {0}, bw[4] = {0}, cw[4] = {0};
+  for (int i = 0; i < 32; i++) {
+    aw[i >> 3] |= (uint64_t)a[i] << (8 * (i & 7));
+    bw[i >> 3] |= (uint64_t)b[i] << (8 * (i & 7));
+    cw[i >> 3] |= (uint64_t)c[i] << (8 * (i & 7));
+  }
+  uint64_t prod[9] = {0};
+  for (int i = 0; i < 4; i++) {
+    u128 carry = 0;
+    for (int j = 0; j < 4; j++) {
+      u128 t = (u128)aw[i] * bw[j] + prod[i + j] + carry;
+      prod[i + j] = (uint64_t)t;
+      carry = t >> 64;
+    }
+    prod[i + 4] += (uint64_t)carry;
+  }
+  u128 carry = 0;
+  for (int i = 0; i < 9; i++) {
+    u128 t = (u128)prod[i] + (i < 4 ? cw[i] : 0) + carry;
+    prod[i] = (uint64_t)t;
+    carry = t >> 64;
+  }
+  uint8_t bytes[72];
+  for (int i = 0; i < 72; i++) bytes[i] = (uint8_t)(prod[i >> 3] >> (8 * (i & 7)));
+  uint64_t r[4];
+  reduce_le(r, bytes, 72);
+  words_to_bytes32(out, r);
+}
+
+/* ------------------------------------------------- GF(2^255 - 19), radix 2^51 */
+typedef struct { uint64_t v[5]; } fe;
+#define M51 ((1ULL << 51) - 1)
+
+static void fe_carry(fe *a) {
+  for (int pass = 0; pass < 3; pass++) {
+    for (int i = 0; i < 4; i++) { a->v[i + 1] += a->v[i] >> 51; a->v[i] &= M51; }
+    uint64_t c = a->v[4] >> 51;
+    a->v[4] &= M51;
+    a->v[0] += 19 * c;
+  }
+}
+static void fe_0(fe *a) { memset(a, 0, sizeof *a); }
+static void fe_1(fe *a) { fe_0(a); a->v[0] = 1; }
+static void fe_add(fe *r, const fe *a, const fe *b) {
+  for (int i = 0; i < 5; i++) r->v[i] = a->v[i] + b->v[i];
+  fe_carry(r);
+}
+static void fe_sub(fe *r, const fe *a, const fe *b) {
+  /* a + 4p - b; inputs are carried (limbs < 2^52). */
+  static const uint64_t p4[5] = {4 * (M51 - 18), 4 * M51, 4 * M51, 4 * M51, 4 * M51};
+  for (int i = 0; i < 5; i++) r->v[i] = a->v[i] + p4[i] - b->v[i];
+  fe_carry(r);
+}
+static void fe_neg(fe *r, const fe *a) { fe z; fe_0(&z); fe_sub(r, &z, a); }
+static void fe_mul(fe *r, const fe *a, const fe *b) {
+  u128 t[5] = {0, 0, 0, 0, 0};
+  for (int i = 0; i < 5; i++)
+    for (int j = 0; j < 5; j++) {
+      u128 p = (u128)a->v[i] * b->v[j];
+      if (i + j >= 5) t[i + j - 5] += p * 19; else t[i + j] += p;
+    }
+  for (int i = 0; i < 4; i++) { t[i + 1] += t[i] >> 51; t[i] &= M51; }
+  u128 c = t[4] >> 51;
+  t[4] &= M51;
+  t[0] += c * 19;
+  t[1] += t[0] >> 51;
+  t[0] &= M51;
+  for (int i = 0; i < 5; i++) r->v[i] = (uint64_t)t[i];
+  fe_carry(r);
+}
+static void fe_sq(fe *r, const fe *a) { fe_mul(r, a, a); }
+/* Fully reduce into [0, p). */
+static void fe_canon(fe *a) {
+  fe_carry(a);
+  int ge_p = a->v[4] == M51 && a->v[3] == M51 && a->v[2] == M51 && a->v[1] == M51 && a->v[0] >= M51 - 18;
+  if (ge_p) {
+    a->v[0] -= M51 - 18;
+    a->v[1] = a->v[2] = a->v[3] = a->v[4] = 0;
+  }
+}
+static void fe_tobytes(uint8_t s[32], const fe *a) {
+  fe t = *a;
+  fe_canon(&t);
+  memset(s, 0, 32);
+  for (int bit = 0; bit < 255; bit++) {
+    int limb = bit / 51, off = bit % 51;
+    if ((t.v[limb] >> off) & 1) s[bit >> 3] |= (uint8_t)(1 << (bit & 7));
+  }
+}
+/* fe25519_frombytes: 255 low bits, top bit ignored, NOT reduced mod p. */
+static void fe_frombytes(fe *a, const uint8_t s[32]) {
+  fe_0(a);
+  for (int bit = 0; bit < 255; bit++)
+    if ((s[bit >> 3] >> (bit & 7)) & 1) a->v[bit / 51] |= 1ULL << (bit % 51);
+}
+static int fe_iszero(const fe *a) {
+  uint8_t s[32];
+  fe_tobytes(s, a);
+  uint8_t acc = 0;
+  for (int i = 0; i < 32; i++) acc |= s[i];
+  return acc == 0;
+}
+static int fe_isnegative(const fe *a) {
+  uint8_t s[32];
+  fe_tobytes(s, a);
+  return s[0] & 1;
+}
+/* r = a^e for a 32-byte little-endian exponent (square-and-multiply, MSB first). */
+static void fe_pow(fe *r, const fe *a, const uint8_t e[32]) {
+  fe acc;
+  fe_1(&acc);
+  for (int bit = 255; bit >= 0; bit--) {
+    fe_sq(&acc, &acc);
+    if ((e[bit >> 3] >> (bit & 7)) & 1) fe_mul(&acc, &acc, a);
+  }
+  *r = acc;
+}
+static void fe_invert(fe *r, const fe *a) {
+  uint8_t e[32]; /* p - 2 = 2^255 - 21 */
+  memset(e, 0xff, 32);
+  e[0] = 0xeb;
+  e[31] = 0x7f;
+  fe_pow(r, a, e);
+}
+static void fe_pow22523(fe *r, const fe *a) {
+  uint8_t e[32]; /* (p - 5) / 8 = 2^252 - 3 */
+  memset(e, 0xff, 32);
+  e[0] = 0xfd;
+  e[31] = 0x0f;
+  fe_pow(r, a, e);
+}
+
+/* ----------------------------------------------------------- the curve */
+typedef struct { fe X, Y, Z, T; } ge; /* extended twisted-Edwards coordinates, a = -1 */
+
+static fe C_d, C_2d, C_sqrtm1;
+static ge C_B;
+static int consts_ready = 0;
+
+static void ge_identity(ge *p) { fe_0(&p->X); fe_1(&p->Y); fe_1(&p->Z); fe_0(&p->T); }
+
+/* add-2008-hwcd-3 (unified, complete for a = -1, d non-square). */
+static void ge_add(ge *r, const ge *p, const ge *q) {
+  fe a, b, c, d, e, f, g, h, t;
+  fe_sub(&a, &p->Y, &p->X); fe_sub(&t, &q->Y, &q->X); fe_mul(&a, &a, &t);
+  fe_add(&b, &p->Y, &p->X); fe_add(&t, &q->Y, &q->X); fe_mul(&b, &b, &t);
+  fe_mul(&c, &p->T, &q->T); fe_mul(&c, &c, &C_2d);
+  fe_mul(&d, &p->Z, &q->Z); fe_add(&d, &d, &d);
+  fe_sub(&e, &b, &a); fe_sub(&f, &d, &c); fe_add(&g, &d, &c); fe_add(&h, &b, &a);
+  fe_mul(&r->X, &e, &f); fe_mul(&r->Y, &g, &h); fe_mul(&r->T, &e, &h); fe_mul(&r->Z, &f, &g);
+}
+static void ge_dbl(ge *r, const ge *p) { ge_add(r, p, p); }
+
+/* [k]P, k a 32-byte little-endian integer, plain MSB-first double-and-add. */
+static void ge_scalarmult(ge *r, const uint8_t k[32], const ge *p) {
+  ge acc;
+  ge_identity(&acc);
+  for (int bit = 255; bit >= 0; bit--) {
+    ge_dbl(&acc, &acc);
+    if ((k[bit >> 3] >> (bit & 7)) & 1) ge_add(&acc, &acc, p);
+  }
+  *r = acc;
+}
+
+static void ge_tobytes(uint8_t s[32], const ge *p) {
+  fe zi, x, y;
+  fe_invert(&zi, &p->Z);
+  fe_mul(&x, &p->X, &zi);
+  fe_mul(&y, &p->Y, &zi);
+  fe_tobytes(s, &y);
+  s[31] ^= (uint8_t)(fe_isnegative(&x) << 7);
+}
+
+/* libsodium 1.0.18 ge25519_frombytes_negate_vartime restated: decode s and
+ * return -P (x negated) in r; -1 when x^2 = (y^2-1)/(dy^2+1) has no root.
+ * negate=0 returns +P (used for the base point and test helpers). */
+static int ge_frombytes(ge *r, const uint8_t s[32], int negate) {
+  fe u, v, v3, vxx, chk, one;
+  fe_1(&one);
+  fe_frombytes(&r->Y, s);
+  fe_1(&r->Z);
+  fe_sq(&u, &r->Y);
+  fe_mul(&v, &u, &C_d);
+  fe_sub(&u, &u, &one);          /* u = y^2 - 1 */
+  fe_add(&v, &v, &one);          /* v = d y^2 + 1 */
+  fe_sq(&v3, &v); fe_mul(&v3, &v3, &v);            /* v^3 */
+  fe_sq(&r->X, &v3); fe_mul(&r->X, &r->X, &v); fe_mul(&r->X, &r->X, &u); /* u v^7 */
+  fe_pow22523(&r->X, &r->X);
+  fe_mul(&r->X, &r->X, &v3); fe_mul(&r->X, &r->X, &u); /* u v^3 (u v^7)^((p-5)/8) */
+  fe_sq(&vxx, &r->X); fe_mul(&vxx, &vxx, &v);
+  fe_sub(&chk, &vxx, &u);
+  if (!fe_iszero(&chk)) {
+    fe_add(&chk, &vxx, &u);
+    if (!fe_iszero(&chk)) return -1;
+    fe_mul(&r->X, &r->X, &C_sqrtm1);
+  }
+  /* negate variant: flip when isnegative(x) == sign bit (libsodium 1.0.18). */
+  if (negate) {
+    if (fe_isnegative(&r->X) == (s[31] >> 7)) fe_neg(&r->X, &r->X);
+  } else {
+    if (fe_isnegative(&r->X) != (s[31] >> 7)) fe_neg(&r->X, &r->X);
+  }
+  fe_mul(&r->T, &r->X, &r->Y);
+  return 0;
+}
+
+static void init_consts(void) {
+  if (consts_ready) return;
+  fe n, dd;
+  fe_0(&n); n.v[0] = 121665;
+  fe_0(&dd); dd.v[0] = 121666;
+  fe_invert(&dd, &dd);
+  fe_mul(&C_d, &n, &dd);
+  fe_neg(&C_d, &C_d);                   /* d = -121665/121666 */
+  fe_add(&C_2d, &C_d, &C_d);
+  uint8_t e[32];                        /* (p - 1) / 4 = 2^253 - 5 */
+  memset(e, 0xff, 32);
+  e[0] = 0xfb;
+  e[31] = 0x1f;
+  fe two;
+  fe_0(&two); two.v[0] = 2;
+  fe_pow(&C_sqrtm1, &two, e);           /* sqrt(-1) = 2^((p-1)/4) */
+  uint8_t bb[32];
+  memset(bb, 0x66, 32);
+  bb[0] = 0x58;                         /* B: y = 4/5, x even */
+  ge_frombytes(&C_B, bb, 0);
+  consts_ready = 1;
+}
+
+/* libsodium 1.0.18 ge25519_has_small_order: the 7-entry blacklist, first 31
+ * bytes exact, last byte compared with the sign bit masked. */
+static const uint8_t SMALL_ORDER[7][32] = {
+  {0},
+  {1},
+  {0x26, 0xe8, 0x95, 0x8f, 0xc2, 0xb2, 0x27, 0xb0, 0x45, 0xc3, 0xf4, 0x89, 0xf2, 0xef, 0x98, 0xf0,
+   0xd5, 0xdf, 0xac, 0x05, 0xd3, 0xc6, 0x33, 0x39, 0xb1, 0x38, 0x02, 0x88, 0x6d, 0x53, 0xfc, 0x05},
+  {0xc7, 0x17, 0x6a, 0x70, 0x3d, 0x4d, 0xd8, 0x4f, 0xba, 0x3c, 0x0b, 0x76, 0x0d, 0x10, 0x67, 0x0f,
+   0x2a, 0x20, 0x53, 0xfa, 0x2c, 0x39, 0xcc, 0xc6, 0x4e, 0xc7, 0xfd, 0x77, 0x92, 0xac, 0x03, 0x7a},
+  {0xec, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff,
+   0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0x7f},
+  {0xed, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff,
+   0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0x7f},
+  {0xee, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff,
+   0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0x7f}};
+
+int oracle_has_small_order(const uint8_t s[32]) {
+  for (int k = 0; k < 7; k++) {
+    int eq = 1;
+    for (int j = 0; j < 31; j++) eq &= s[j] == SMALL_ORDER[k][j];
+    eq &= (s[31] & 0x7f) == SMALL_ORDER[k][31];
+    if (eq) return 1;
+  }
+  return 0;
+}
+
+/* ge25519_is_canonical: the 255-bit y (sign bit masked) is < p. */
+int oracle_is_canonical_point(const uint8_t s[32]) {
+  if ((s[31] & 0x7f) != 0x7f) return 1;
+  for (int i = 30; i > 0; i--)
+    if (s[i] != 0xff) return 1;
+  return s[0] < 0xed;
+}
+
+/* crypto_sign_verify_detached (libsodium 1.0.18, non-ED25519_COMPAT):
+ * returns 0 iff accepted, -1 otherwise. */
+int oracle_verify_detached(const uint8_t sig[64], const uint8_t *m, uint64_t mlen, const uint8_t pk[32]) {
+  init_consts();
+  if (!sc_is_canonical(sig + 32) || oracle_has_small_order(sig)) return -1;
+  if (!oracle_is_canonical_point(pk) || oracle_has_small_order(pk)) return -1;
+  ge negA;
+  if (ge_frombytes(&negA, pk, 1) != 0) return -1;
+  sha512_ctx c;
+  uint8_t hram[64], h[32];
+  sha512_init(&c);
+  sha512_update(&c, sig, 32);
+  sha512_update(&c, pk, 32);
+  sha512_update(&c, m, (size_t)mlen);
+  sha512_final(&c, hram);
+  oracle_sc_reduce(h, hram);
+  ge sB, hA, R;
+  ge_scalarmult(&sB, sig + 32, &C_B);
+  ge_scalarmult(&hA, h, &negA);
+  ge_add(&R, &sB, &hA);
+  uint8_t rcheck[32];
+  ge_tobytes(rcheck, &R);
+  return memcmp(rcheck, sig, 32) == 0 ? 0 : -1;
+}
+
+/* crypto_sign_open's verdict on sm = sig || msg (nacl_wrappers.py:108):
+ * smlen < 64 -> reject; otherwise split at byte 64. */
+int oracle_sign_open(const uint8_t *sm, uint64_t smlen, const uint8_t pk[32]) {
+  if (smlen < 64) return -1;
+  return oracle_verify_detached(sm, sm + 64, smlen - 64, pk);
+}
+
+/* Batch form of the same predicate over the C-ABI layout the HIP library
+ * takes (include/edverify.h): bit i of accept_bits is 1 iff accepted. */
+void oracle_verify_batch(const uint8_t *sig64, const uint8_t *pk32, const uint8_t *msgs, const uint64_t *msg_off,
+                         uint64_t n, uint8_t *accept_bits) {
+  memset(accept_bits, 0, (size_t)((n + 7) / 8));
+  for (uint64_t i = 0; i < n; i++) {
+    int ok = oracle_verify_detached(sig64 + 64 * i, msgs + msg_off[i], msg_off[i + 1] - msg_off[i], pk32 + 32 * i) == 0;
+    if (ok) accept_bits[i >> 3] |= (uint8_t)(1u << (i & 7));
+  }
+}
+
+/* crypto_sign_seed_keypair restated. sk = seed || pk. */
+void oracle_seed_keypair(uint8_t pk[32], uint8_t sk[64], const uint8_t seed[32]) {
+  init_consts();
+  uint8_t az[64];
+  oracle_sha512(az, seed, 32);
+  az[0] &= 248; az[31] &= 63; az[31] |= 64;
+  ge A;
+  ge_scalarmult(&A, az, &C_B);
+  ge_tobytes(pk, &A);
+  memcpy(sk, seed, 32);
+  memcpy(sk + 32, pk, 32);
+}
+
+/* crypto_sign_detached restated (deterministic RFC 8032 Ed25519). */
+void oracle_sign_detached(uint8_t sig[64], const uint8_t *m, uint64_t mlen, const uint8_t sk[64]) {
+  init_consts();
+  uint8_t az[64], nonce64[64], nonce[32], hram64[64], hram[32];
+  oracle_sha512(az, sk, 32);
+  sha512_ctx c;
+  sha512_init(&c);
+  sha512_update(&c, az + 32, 32);
+  sha512_update(&c, m, (size_t)mlen);
+  sha512_final(&c, nonce64);
+  oracle_sc_reduce(nonce, nonce64);
+  ge R;
+  ge_scalarmult(&R, nonce, &C_B);
+  ge_tobytes(sig, &R);
+  sha512_init(&c);
+  sha512_update(&c, sig, 32);
+  sha512_update(&c, sk + 32, 32);
+  sha512_update(&c, m, (size_t)mlen);
+  sha512_final(&c, hram64);
+  oracle_sc_reduce(hram, hram64);
+  az[0] &= 248; az[31] &= 63; az[31] |= 64;
+  sc_muladd(sig + 32, hram, az, nonce);
+}
+
+/* Test helper: decode (negate=0) and re-encode; returns -1 if not on curve. */
+int oracle_point_roundtrip(uint8_t out[32], const uint8_t in[32]) {
+  init_consts();
+  ge P;
+  if (ge_frombytes(&P, in, 0) != 0) return -1;
+  ge_tobytes(out, &P);
+  return 0;
+}
+
+/* Test helper: out = encode([k]P + Q) for encodings p, q (debug twin of the GPU DSM). */
+int oracle_double_scalarmult(uint8_t out[32], const uint8_t k[32], const uint8_t p[32], const uint8_t s[32]) {
+  init_consts();
+  ge P, a, b, r;
+  if (ge_frombytes(&P, p, 0) != 0) return -1;
+  ge_scalarmult(&a, k, &P);
+  ge_scalarmult(&b, s, &C_B);
+  ge_add(&r, &a, &b);
+  ge_tobytes(out, &r);
+  return 0;
+}

@@ -1,0 +1,102 @@
+// Microbenchmark: VALU throughput of the integer multiply forms usable for
+// GF(2^255-19) limb arithmetic on gfx950 (decides the limb representation).
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+
+#ifndef NACC
+#define NACC 8
+#endif
+#define ITERS 4096
+
+template <int KIND>
+__global__ __launch_bounds__(1024) void kbench(uint32_t* out, uint32_t seed) {
+  uint32_t a = seed ^ threadIdx.x, b = seed * 3 + blockIdx.x;
+  uint64_t acc[NACC];
+  uint32_t acc32[NACC];
+  double accd[NACC];
+  float accf[NACC];
+#pragma unroll
+  for (int j = 0; j < NACC; ++j) { acc[j] = j + threadIdx.x; acc32[j] = j * 7 + threadIdx.x; accd[j] = j + 0.5 * threadIdx.x; accf[j] = j; }
+  for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+    for (int j = 0; j < NACC; ++j) {
+      if (KIND == 0) {  // v_mad_u64_u32
+        uint64_t c;
+        asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc[j]), "=s"(c) : "v"(a), "v"(b));
+      } else if (KIND == 1) {  // v_mul_lo_u32
+        asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(acc32[j]) : "v"(a));
+      } else if (KIND == 2) {  // v_mul_hi_u32
+        asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(acc32[j]) : "v"(a));
+      } else if (KIND == 3) {  // v_mad_u32_u24
+        asm volatile("v_mad_u32_u24 %0, %1, %2, %0" : "+v"(acc32[j]) : "v"(a), "v"(b));
+      } else if (KIND == 4) {  // v_mul_hi_u32_u24
+        asm volatile("v_mul_hi_u32_u24 %0, %0, %1" : "+v"(acc32[j]) : "v"(a));
+      } else if (KIND == 5) {  // v_add_co_u32 (32-bit add w/ carry out)
+        uint64_t c;
+        asm volatile("v_add_co_u32 %0, %1, %0, %2" : "+v"(acc32[j]), "=s"(c) : "v"(a));
+      } else if (KIND == 6) {  // v_fma_f64
+        asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(accd[j]) : "v"((double)a), "v"((double)b));
+      } else if (KIND == 7) {  // v_fma_f32
+        asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(accf[j]) : "v"((float)a), "v"((float)b));
+      } else if (KIND == 8) {  // v_lshrrev_b64
+        asm volatile("v_lshrrev_b64 %0, 3, %0" : "+v"(acc[j]));
+      } else if (KIND == 9) {  // v_add_u32 (no carry)
+        asm volatile("v_add_u32 %0, %0, %1" : "+v"(acc32[j]) : "v"(a));
+      } else if (KIND == 10) { // v_lshl_add_u64 (gfx940+)
+        asm volatile("v_lshl_add_u64 %0, %0, 1, %1" : "+v"(acc[j]) : "v"((uint64_t)a));
+      } else if (KIND == 11) { // v_alignbit_b32
+        asm volatile("v_alignbit_b32 %0, %0, %1, 7" : "+v"(acc32[j]) : "v"(a));
+      } else if (KIND == 12) { // v_bfe_u32
+        asm volatile("v_bfe_u32 %0, %0, 3, 26" : "+v"(acc32[j]));
+      } else if (KIND == 13) { // v_mul_u32_u24
+        asm volatile("v_mul_u32_u24 %0, %0, %1" : "+v"(acc32[j]) : "v"(a));
+      }
+    }
+  }
+  uint32_t r = 0;
+#pragma unroll
+  for (int j = 0; j < NACC; ++j) r += (uint32_t)acc[j] + (uint32_t)(acc[j] >> 32) + acc32[j] + (uint32_t)accd[j] + (uint32_t)accf[j];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = r;
+}
+
+template <int KIND>
+static void run(const char* name, uint32_t* d, int blocks, int waves_per_block) {
+  hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
+  int threads = 64 * waves_per_block;
+  hipLaunchKernelGGL(kbench<KIND>, dim3(blocks), dim3(threads), 0, 0, d, 1u);
+  hipDeviceSynchronize();
+  hipEventRecord(e0);
+  const int reps = 3;
+  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(kbench<KIND>, dim3(blocks), dim3(threads), 0, 0, d, 1u);
+  hipEventRecord(e1); hipEventSynchronize(e1);
+  float ms; hipEventElapsedTime(&ms, e0, e1);
+  double ops = (double)reps * blocks * threads * (double)ITERS * NACC;
+  printf("%-20s blocks=%5d thr=%4d  %8.3f Gops/s (lane-ops)  = %.3f lane-ops/clk/CU @2.4GHz\n", name, blocks, threads,
+         ops / (ms * 1e6), ops / (ms * 1e-3) / 256 / 2.4e9);
+}
+
+int main() {
+  uint32_t* d; hipMalloc(&d, 256 * 8 * 1024 * sizeof(uint32_t) * 4);
+  hipDeviceProp_t p; hipGetDeviceProperties(&p, 0);
+  printf("device %s CUs=%d clock=%d kHz\n", p.gcnArchName, p.multiProcessorCount, p.clockRate);
+  int blocks = 256 * 8;
+  for (int w : {8, 16}) {
+    run<0>("v_mad_u64_u32", d, blocks, w);
+    run<1>("v_mul_lo_u32", d, blocks, w);
+    run<2>("v_mul_hi_u32", d, blocks, w);
+    run<3>("v_mad_u32_u24", d, blocks, w);
+    run<4>("v_mul_hi_u32_u24", d, blocks, w);
+    run<13>("v_mul_u32_u24", d, blocks, w);
+    run<5>("v_add_co_u32", d, blocks, w);
+    run<9>("v_add_u32", d, blocks, w);
+    run<6>("v_fma_f64", d, blocks, w);
+    run<7>("v_fma_f32", d, blocks, w);
+    run<8>("v_lshrrev_b64", d, blocks, w);
+    run<10>("v_lshl_add_u64", d, blocks, w);
+    run<11>("v_alignbit_b32", d, blocks, w);
+    run<12>("v_bfe_u32", d, blocks, w);
+  }
+  hipFree(d);
+  return 0;
+}
