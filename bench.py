@@ -1,0 +1,237 @@
+"""Ed25519 request verifies/sec on MI355X -- the BASELINE.json headline metric.
+
+One step = one pass of the verify path over this rank's batch, inputs already
+resident in HBM: hash kernel (prechecks + SHA-512(R||A||M) mod L) -> table
+kernel (decode -A, [1..8](-A)) -> dsm kernel ([h](-A) + [S]B, encode, compare,
+wave ballot) -> accept bitmask; for N > 1 the step ends with the RCCL
+all-gather of the bitmask words (the path's one exchange step).  Weak scaling:
+each rank verifies its own shard of `--n` requests.
+
+Workload (BASELINE.json configs[1]): 1M single-signature NYM requests, ~200 B
+signed payload (serialize_msg_for_signing of a NYM with an alias field), 1,000
+signers, all valid.  `--config c2` adds the 10% corrupted / non-canonical /
+small-order mix of configs[2].  Signatures are made on the GPU by the library's
+own deterministic signer (bit-exact with libsodium, tests/test_gpu_parity.py).
+
+Usage: python bench.py [--gpus N --steps K --warmup W]   (N > 1 via torch.distributed.run)
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "indy-plenum_amd"))
+
+from plenum_amd import EdVerifyEngine, pack_messages  # noqa: E402
+from plenum_amd import roofline as RL  # noqa: E402
+from plenum_amd import synth  # noqa: E402
+
+METRIC = "Ed25519 request verifies/sec (whole node) at 1/2/4/8 MI355X vs host libsodium"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=1_000_000, help="requests per GPU")
+    ap.add_argument("--signers", type=int, default=1000)
+    ap.add_argument("--alias-len", type=int, default=43, help="pads the NYM signing payload to ~200 B")
+    ap.add_argument("--config", choices=["c1", "c2"], default="c1")
+    ap.add_argument("--cpu-sample", type=int, default=400_000, help="items timed on host libsodium (rank 0, N=1)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, affinity CPUs)")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def corrupt_c2(sig, pk, msgs, off, rng):
+    """configs[2]: 10% rejects, split equally over bit flips in R/S/M, S+L,
+    S|2^255, small-order A, non-canonical A, R = identity, R + T8."""
+    n = sig.shape[0]
+    bad = rng.choice(n, size=n // 10, replace=False)
+    kinds = bad % 9
+    L = 2**252 + 27742317777372353535851937790883648493
+    small_A = bytes.fromhex("26e8958fc2b227b045c3f489f2ef98f0d5dfac05d3c63339b13802886d53fc05")
+    noncanon_A = (2**255 - 19 + 3).to_bytes(32, "little")
+    ident = (1).to_bytes(32, "little")
+    for i, k in zip(bad, kinds):
+        if k == 0:
+            sig[i, rng.integers(0, 32)] ^= 1 << int(rng.integers(0, 8))
+        elif k == 1:
+            sig[i, 32 + rng.integers(0, 31)] ^= 1 << int(rng.integers(0, 8))
+        elif k == 2:
+            a, b = int(off[i]), int(off[i + 1])
+            msgs[a + int(rng.integers(0, b - a))] ^= 1 << int(rng.integers(0, 8))
+        elif k == 3:
+            s = int.from_bytes(sig[i, 32:].tobytes(), "little") + L
+            sig[i, 32:] = np.frombuffer(s.to_bytes(32, "little"), np.uint8)
+        elif k == 4:
+            sig[i, 63] |= 0x80
+        elif k == 5:
+            pk[i] = np.frombuffer(small_A, np.uint8)
+        elif k == 6:
+            pk[i] = np.frombuffer(noncanon_A, np.uint8)
+        elif k == 7:
+            sig[i, :32] = np.frombuffer(ident, np.uint8)
+        else:
+            sig[i, :32] = np.frombuffer(synth.add_torsion(sig[i, :32].tobytes()), np.uint8)
+    expect = np.ones(n, dtype=bool)
+    expect[bad] = False
+    return expect
+
+
+def cpu_baseline(sig, pk, msgs, off, threads):
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "_build", "libcpu_baseline.so"))
+    lib.cpu_baseline_sodium_version.restype = ctypes.c_char_p
+    lib.cpu_baseline_run.restype = ctypes.c_int
+    n = sig.shape[0]
+    ok = np.zeros(n, np.uint8)
+    secs = ctypes.c_double()
+    P = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    kind = lib.cpu_baseline_run(P(sig), P(pk), P(msgs), P(off), ctypes.c_uint64(n), threads, 1, P(ok),
+                                ctypes.byref(secs))
+    if kind < 0:
+        raise RuntimeError("cpu baseline failed")
+    ver = lib.cpu_baseline_sodium_version().decode()
+    return n / secs.value, ok.astype(bool), ("reference" if kind == 1 else "port"), ver
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    eng = EdVerifyEngine(local)
+    n = args.n
+
+    # ---- synthetic signed batch (not timed)
+    seeds = synth.signer_seeds(args.signers)
+    pks, sks = eng.seed_keypair_batch(seeds)
+    msgs_l, key_idx, _ = synth.nym_messages(n, pks, alias_len=args.alias_len, seed=1 + rank,
+                                            req_id_base=synth.REQ_ID_BASE + rank * n)
+    buf, off = pack_messages(msgs_l)
+    del msgs_l
+    mlen_mean = float(np.mean(np.diff(off)))
+    d_sk = torch.from_numpy(sks).to(dev)
+    d_kidx = torch.from_numpy(key_idx.astype(np.int32)).to(dev)
+    d_msgs = torch.from_numpy(np.concatenate([buf, np.zeros(16, np.uint8)])).to(dev)
+    d_off = torch.from_numpy(off.view(np.int64)).to(dev)
+    d_sig = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+    eng.sign_batch_device(d_sk, d_kidx, d_msgs, d_off, n, d_sig)
+    d_pk = torch.from_numpy(pks).to(dev)[d_kidx.long()].contiguous()
+    torch.cuda.synchronize()
+    expect = np.ones(n, dtype=bool)
+    if args.config == "c2":
+        sig_h, pk_h, buf_h = d_sig.cpu().numpy().copy(), d_pk.cpu().numpy().copy(), buf.copy()
+        expect = corrupt_c2(sig_h, pk_h, buf_h, off, np.random.default_rng(2))
+        d_sig = torch.from_numpy(sig_h).to(dev)
+        d_pk = torch.from_numpy(pk_h).to(dev)
+        d_msgs = torch.from_numpy(np.concatenate([buf_h, np.zeros(16, np.uint8)])).to(dev)
+    nwords = (n + 63) // 64
+    d_words = torch.zeros(nwords, dtype=torch.int64, device=dev)
+    gathered = [torch.zeros_like(d_words) for _ in range(world)] if world > 1 else None
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        eng.verify_batch_device(d_sig, d_pk, d_msgs, d_off, n, d_words, stream=stream.cuda_stream)
+        if world > 1:
+            dist.all_gather(gathered, d_words)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dsm_ms, hash_ms, table_ms = [], [], []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        h, t, d = eng.last_phase_ms()  # waits for this step's events
+        hash_ms.append(h)
+        table_ms.append(t)
+        dsm_ms.append(d)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+
+    # ---- parity of the timed output against the construction
+    words = d_words.cpu().numpy().view(np.uint64)
+    got = np.unpackbits(words.view(np.uint8), bitorder="little")[:n].astype(bool)
+    mismatches = int((got != expect).sum())
+
+    total = n * world * args.steps
+    value = total / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+    dsm_avg = float(np.mean(dsm_ms))
+    achieved = n * RL.MAD_DSM_KERNEL / (dsm_avg * 1e-3) / 1e12
+    peak = RL.PEAK_MAD_PER_S / 1e12
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tpath):
+        with open(tpath) as f:
+            tj = json.load(f)
+        if tj.get("n") == n:
+            traffic = tj.get("edv_dsm_kernel_bytes")
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        s = min(args.cpu_sample, n)
+        sig_h = d_sig[:s].cpu().numpy()
+        pk_h = d_pk[:s].cpu().numpy()
+        off_h = off[: s + 1].copy()
+        msg_h = d_msgs[: int(off_h[-1]) + 16].cpu().numpy()
+        threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+        rate, ok, kind, ver = cpu_baseline(sig_h, pk_h, msg_h, off_h, threads)
+        cpu = {"value": rate, "unit": "verifies/s", "cores": threads, "kind": kind,
+               "sample": "first %d requests of this workload, libsodium %s crypto_sign_verify_detached, %d pthreads"
+                         % (s, ver or "(absent: oracle restatement)", threads),
+               "agrees_with_gpu": bool((ok == got[:s]).all())}
+
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": value, "unit": "verifies/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u32 (radix-2^25.5 GF(2^255-19), 64-bit MAD accumulators)",
+            "data": "synthetic NYM requests signed on-GPU (deterministic Ed25519, libsodium-exact)",
+            "config": {"workload": "configs[%d]: %d single-signature requests per GPU, %.0f B mean signed payload, "
+                                   "%d signers%s" % (1 if args.config == "c1" else 2, n, mlen_mean, args.signers,
+                                                     ", 10% corrupted/non-canonical/small-order" if args.config == "c2" else ", all valid"),
+                       "requests_per_gpu": n, "signers": args.signers, "parallelism": "dp%d (request-index shards)" % world},
+            "roofline": {"bound": "valu", "kernel": "edv_dsm_kernel", "achieved": achieved, "peak": peak,
+                         "unit": "TMAD/s", "frac": achieved / peak, "traffic": traffic,
+                         "algorithmic": "%d MAD per verify ((2510 + 267) field ops x 100), n=%d per launch, "
+                                        "avg launch %.3f ms" % (RL.MAD_DSM_KERNEL, n, dsm_avg)},
+            "phase_ms": {"hash": float(np.mean(hash_ms)), "table": float(np.mean(table_ms)), "dsm": dsm_avg},
+            "whole_path_frac": (n * RL.MAD_PER_VERIFY / ((float(np.mean(hash_ms)) + float(np.mean(table_ms)) + dsm_avg) * 1e-3)) / RL.PEAK_MAD_PER_S,
+            "cpu_baseline": cpu,
+            "parity": {"mismatches_vs_construction": mismatches, "accepted": int(got.sum()), "expected": int(expect.sum())},
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    eng.close()
+    if mismatches:
+        sys.exit(3)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,107 @@
+"""Synthetic signed-request batches shaped like Plenum NYM writes.
+
+Request shape follows the reference's client signing path
+(plenum/client/wallet.py:181-217 -> plenum/common/signer_did.py:114-121):
+  {identifier: b58(pk[:16]), reqId: int, protocolVersion: 1,
+   operation: {type: '1', dest: b58(16 B), verkey: '~' + b58(16 B)[, alias: ...]}}
+signed over serialize_msg_for_signing(req, ['signature']).  Signer seeds are
+i.to_bytes(2, 'little') + 30 zero bytes.
+
+`nym_messages` builds the signing bytes with one format string per request;
+tests/test_synth.py checks it byte-for-byte against serialize_msg_for_signing.
+"""
+import numpy as np
+
+from .base58 import b58encode
+from .serialization import serialize_msg_for_signing
+
+REQ_ID_BASE = 1_500_000_000_000_000
+
+
+def signer_seeds(n_signers):
+    return np.stack([np.frombuffer(i.to_bytes(2, "little") + b"\0" * 30, np.uint8) for i in range(n_signers)])
+
+
+def _pool(rng, n, nbytes):
+    raw = rng.integers(0, 256, size=(n, nbytes), dtype=np.uint8)
+    return [b58encode(bytes(r)) for r in raw]
+
+
+def nym_request(identifier, req_id, dest, verkey, alias=None, protocol_version=1):
+    op = {"type": "1", "dest": dest, "verkey": verkey}
+    if alias is not None:
+        op["alias"] = alias
+    return {"identifier": identifier, "reqId": req_id, "operation": op, "protocolVersion": protocol_version}
+
+
+def nym_messages(n, signer_pks, alias_len=0, seed=1, req_id_base=REQ_ID_BASE, pool=4096):
+    """n NYM requests from len(signer_pks) signers (request i signed by signer
+    i % n_signers).  Returns (messages: list[bytes], key_idx: uint32[n],
+    spec) where spec lets tests rebuild request i as a dict."""
+    rng = np.random.default_rng(seed)
+    n_signers = len(signer_pks)
+    idrs = [b58encode(bytes(pk[:16])) for pk in signer_pks]
+    dests = _pool(rng, pool, 16)
+    vks = ["~" + v for v in _pool(rng, pool, 16)]
+    alias = None
+    if alias_len:
+        alias = "".join(rng.choice(list("abcdefghijklmnopqrstuvwxyz0123456789"), size=alias_len))
+    key_idx = (np.arange(n) % n_signers).astype(np.uint32)
+    op_prefix = "operation:alias:%s|" % alias if alias is not None else "operation:"
+    msgs = []
+    for i in range(n):
+        s = i % n_signers
+        msgs.append(("identifier:%s|%sdest:%s|type:1|verkey:%s|protocolVersion:1|reqId:%d" % (
+            idrs[s], op_prefix, dests[i % pool], vks[(i * 7) % pool], req_id_base + i)).encode())
+    spec = dict(idrs=idrs, dests=dests, vks=vks, alias=alias, pool=pool, req_id_base=req_id_base)
+    return msgs, key_idx, spec
+
+
+def nym_request_dict(spec, i, n_signers):
+    return nym_request(spec["idrs"][i % n_signers], spec["req_id_base"] + i, spec["dests"][i % spec["pool"]],
+                       spec["vks"][(i * 7) % spec["pool"]], spec["alias"])
+
+
+def check_nym_message(spec, i, n_signers, msg):
+    return serialize_msg_for_signing(nym_request_dict(spec, i, n_signers), topLevelKeysToIgnore=["signature"]) == msg
+
+
+# --- exact-integer helper for the configs[2] "R + T8" corruption ----------
+_P = 2**255 - 19
+_D = (-121665 * pow(121666, _P - 2, _P)) % _P
+_SQRTM1 = pow(2, (_P - 1) // 4, _P)
+# an order-8 point (x, y); its y is libsodium's blacklist entry 26e8958f...
+_T8_ENC = bytes.fromhex("26e8958fc2b227b045c3f489f2ef98f0d5dfac05d3c63339b13802886d53fc05")
+
+
+def _decode(enc):
+    v = int.from_bytes(enc, "little")
+    y = v & ((1 << 255) - 1)
+    sign = v >> 255
+    if y >= _P:
+        return None
+    x2 = (y * y - 1) * pow(_D * y * y + 1, _P - 2, _P) % _P
+    x = pow(x2, (_P + 3) // 8, _P)
+    if (x * x - x2) % _P:
+        x = x * _SQRTM1 % _P
+    if (x * x - x2) % _P:
+        return None
+    if x & 1 != sign:
+        x = (_P - x) % _P
+    return x, y
+
+
+def _add(a, b):
+    (x1, y1), (x2, y2) = a, b
+    t = _D * x1 * x2 * y1 * y2 % _P
+    return ((x1 * y2 + x2 * y1) * pow(1 + t, _P - 2, _P) % _P,
+            (y1 * y2 + x1 * x2) * pow(1 - t, _P - 2, _P) % _P)
+
+
+def add_torsion(r_enc):
+    """encode(R + T8): a signature R that only the cofactored equation accepts."""
+    R = _decode(r_enc)
+    if R is None:
+        return r_enc
+    x, y = _add(R, _decode(_T8_ENC))
+    return (y | ((x & 1) << 255)).to_bytes(32, "little")
