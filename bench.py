@@ -144,7 +144,7 @@ def main():
     stream = torch.cuda.current_stream(dev)
 
     def step():
-        eng.verify_batch_device(d_sig, d_pk, d_msgs, d_off, n, d_words, stream=stream.cuda_stream)
+        eng.verify_batch_device(d_sig, d_pk, d_msgs, d_off, n, d_words, stream=stream)
         if world > 1:
             dist.all_gather(gathered, d_words)
 

@@ -25,7 +25,8 @@
  *     buffers; the library stages them through its own device buffers and
  *     returns when the result is in the caller's buffer.
  *   - _device entry points take device pointers and an optional hipStream_t
- *     (NULL = the context's stream) and are asynchronous.
+ *     (NULL = the context's stream, a blocking stream ordered after work on
+ *     the legacy NULL stream) and are asynchronous.
  *   - Bitmasks: bit i of the mask is bit (i % 8) of byte (i / 8), i.e.
  *     little-endian 64-bit words of wave ballots.  1 = libsodium returns 0.
  *   - Threading: one context per GPU; calls on one context are serialised by

@@ -420,7 +420,9 @@ edv_ctx* edv_create(int device) {
   };
   hipError_t e;
   if ((e = hipSetDevice(device)) != hipSuccess) return fail("hipSetDevice", e);
-  if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess) return fail("hipStreamCreate", e);
+  // A blocking stream: it is ordered against the legacy NULL stream, which is
+  // where PyTorch's default-stream copies that produce our inputs run.
+  if ((e = hipStreamCreate(&ctx->stream)) != hipSuccess) return fail("hipStreamCreate", e);
   for (int k = 0; k < 4; ++k)
     if ((e = hipEventCreate(&ctx->ev[k])) != hipSuccess) return fail("hipEventCreate", e);
   if ((e = hipMalloc(&ctx->d_btab_small, sizeof(BASE_SMALL_U32))) != hipSuccess) return fail("hipMalloc", e);

@@ -58,6 +58,14 @@ def load():
     global _lib
     if _lib is not None:
         return _lib
+    # PyTorch bundles its own libamdhip64.so.7 (same SONAME as /opt/rocm's).
+    # Whichever loads first serves the whole process, so let torch's runtime
+    # load first: device pointers and stream handles then come from the one
+    # runtime both sides use.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise EdVerifyUnavailable(
             "libplenum_edverify.so not built at %s (run __graft_entry__.build())" % LIB_PATH)

@@ -1,0 +1,409 @@
+"""Client authenticators with the reference API, verified in GPU batches.
+
+Reference: plenum/server/client_authn.py:22-154 (ClientAuthNr, NaclAuthNr,
+SimpleAuthNr).  `authenticate(msg, identifier=None, signature=None)` keeps the
+reference's exact check order and exception classes:
+  :72-80  signature present            -> EmptySignature / MissingSignature
+  :81-87  identifier present           -> EmptyIdentifier / MissingIdentifier
+  :88-91  b58decode(signature)         -> InvalidSignatureFormat (from the b58 error)
+  :92     serializeForSig(msg, ['signature'])
+  :93     getVerkey(identifier)        -> UnknownIdentifier (SimpleAuthNr :142-154)
+  :95-97  verkey is None               -> CouldNotAuthenticate
+  :99     DidVerifier(verkey, identifier)  (InvalidKey -> CouldNotAuthenticate)
+  :100-102 verify(sig, ser) false      -> InvalidSignature
+  :105-106 anything else               -> CouldNotAuthenticate from ex
+The verify step is libsodium's crypto_sign_open(sig || ser, pk)
+(nacl_wrappers.py:232-242, :108), run by libplenum_edverify.so on the GPU.
+
+Added on top of the reference API (the reference calls authenticate once per
+message from Node.verifySignature, node.py:2294-2318):
+  authenticate_batch(msgs)        one GPU launch for many requests; returns,
+                                  per message, the identifier or the exception
+                                  instance authenticate() would have raised.
+  prefetch(msgs)                  verify-ahead: batch-verify what the node is
+                                  about to authenticate (client REQUESTs and
+                                  PROPAGATE payloads of one rxMsgs drain,
+                                  zstack.py:528-549); later authenticate()
+                                  calls hit the verdict cache.
+  authenticate_multi(msg, sigs)   multi-signature requests (not in the
+                                  reference snapshot: parity unpinned).
+`CoreAuthNr` is an alias of GpuAuthNr; `ReqAuthenticator` aggregates
+authenticators (names from BASELINE.json's north star).
+"""
+from abc import abstractmethod
+from collections import OrderedDict
+from copy import deepcopy
+from typing import Dict
+
+from .base58 import b58decode
+from .exceptions import (CouldNotAuthenticate, EmptyIdentifier, EmptySignature, InsufficientCorrectSignatures,
+                         InsufficientSignatures, InvalidSignature, InvalidSignatureFormat, MissingIdentifier,
+                         MissingSignature, SigningException, UnknownIdentifier)
+from .serialization import serialize_msg_for_signing
+from .verifier import DidVerifier, VerkeyCache
+
+SIG = 'signature'
+SIGS = 'signatures'
+IDENTIFIER = 'identifier'
+REQ_ID = 'reqId'
+VERKEY = 'verkey'
+ROLE = 'role'
+OPERATION = 'operation'
+TXN_TYPE = 'type'
+
+
+class ClientAuthNr:
+    """Interface for client authenticators (client_authn.py:22-63)."""
+
+    @abstractmethod
+    def authenticate(self, msg: Dict, identifier: str = None, signature: str = None) -> str:
+        """Return the identifier or raise a SigningException subclass."""
+
+    @abstractmethod
+    def addIdr(self, identifier, verkey, role=None):
+        """Register an identifier's verification key."""
+
+    @abstractmethod
+    def getVerkey(self, identifier):
+        """Verification key of an identifier."""
+
+
+class _Prepared:
+    __slots__ = ("identifier", "sig", "ser", "key")
+
+    def __init__(self, identifier, sig, ser, key):
+        self.identifier, self.sig, self.ser, self.key = identifier, sig, ser, key
+
+
+class NaclAuthNr(ClientAuthNr):
+    """The reference NaclAuthNr with the Ed25519 check moved to the GPU
+    engine.  Subclasses provide addIdr / getVerkey."""
+
+    engine = None  # set by GpuAuthMixin or by the caller (an EdVerifyEngine)
+
+    def authenticate(self, msg: Dict, identifier: str = None, signature: str = None) -> str:
+        try:
+            p = self._prepare(msg, identifier, signature)
+            if not self._verify_prepared(p):
+                raise InvalidSignature
+        except SigningException as e:
+            raise e
+        except Exception as ex:
+            raise CouldNotAuthenticate from ex
+        return p.identifier
+
+    # the pre-verification half of authenticate(), reference order
+    def _prepare(self, msg, identifier=None, signature=None, ignore=(SIG,)):
+        if not signature:
+            try:
+                signature = msg[SIG]
+                if not signature:
+                    raise EmptySignature(msg.get(IDENTIFIER), msg.get(REQ_ID))
+            except KeyError:
+                raise MissingSignature(msg.get(IDENTIFIER), msg.get(REQ_ID))
+        if not identifier:
+            try:
+                identifier = msg[IDENTIFIER]
+                if not identifier:
+                    raise EmptyIdentifier(None, msg.get(REQ_ID))
+            except KeyError:
+                raise MissingIdentifier(identifier, msg.get(REQ_ID))
+        try:
+            sig = b58decode(signature)
+        except Exception as ex:
+            raise InvalidSignatureFormat from ex
+        ser = self.serializeForSig(msg, topLevelKeysToIgnore=list(ignore))
+        verkey = self.getVerkey(identifier)
+        if verkey is None:
+            raise CouldNotAuthenticate('Can not find verkey for DID {}'.format(identifier))
+        key = self._resolve_key(verkey, identifier)
+        return _Prepared(identifier, sig, ser, key)
+
+    def _resolve_key(self, verkey, identifier):
+        return DidVerifier(verkey, identifier=identifier).key
+
+    def _verify_prepared(self, p):
+        if not p.key:  # nacl_wrappers.py:237-238: no key -> False
+            return False
+        return bool(self._engine().sign_open_batch(p.sig + p.ser, [0, len(p.sig) + len(p.ser)], [p.key])[0])
+
+    def _engine(self):
+        if self.engine is None:
+            from .engine import EdVerifyEngine
+            self.engine = EdVerifyEngine(0)
+        return self.engine
+
+    @abstractmethod
+    def addIdr(self, identifier, verkey, role=None):
+        pass
+
+    @abstractmethod
+    def getVerkey(self, identifier):
+        pass
+
+    def serializeForSig(self, msg, topLevelKeysToIgnore=None):
+        return serialize_msg_for_signing(msg, topLevelKeysToIgnore=topLevelKeysToIgnore)
+
+
+class SimpleAuthNr(NaclAuthNr):
+    """client_authn.py:122-154.  `state` lookups for identifiers not added with
+    addIdr go through `nym_lookup(state, identifier)` (the reference calls
+    DomainRequestHandler.getNymDetails(state, identifier, isCommitted=False),
+    domain_req_handler.py:146-155); with no lookup the state is empty."""
+
+    def __init__(self, state=None, nym_lookup=None):
+        self.clients = {}  # type: Dict[str, Dict]
+        self.state = state
+        self.nym_lookup = nym_lookup
+
+    def addIdr(self, identifier, verkey, role=None):
+        self.clients[identifier] = {VERKEY: verkey, ROLE: role}
+
+    def getVerkey(self, identifier):
+        nym = self.clients.get(identifier)
+        if not nym:
+            nym = self.nym_lookup(self.state, identifier) if self.nym_lookup else {}
+            if not nym:
+                raise UnknownIdentifier(identifier)
+        return nym.get(VERKEY)
+
+
+class GpuAuthMixin:
+    """The GPU batch machinery.  Mix in front of any NaclAuthNr-compatible
+    class -- including the reference's own plenum.server.client_authn.SimpleAuthNr
+    (INTEGRATION.md), which keeps node.py:2482's isinstance check true."""
+
+    def _gpu_init(self, engine=None, device=0, verdict_cache_size=1 << 20):
+        self.engine = engine
+        self._device = device
+        self._keys = VerkeyCache()
+        self._verdicts = OrderedDict()
+        self._verdict_cache_size = verdict_cache_size
+        self.stats = {"batches": 0, "batch_items": 0, "cache_hits": 0, "single_verifies": 0}
+
+    def _engine(self):
+        if self.engine is None:
+            from .engine import EdVerifyEngine
+            self.engine = EdVerifyEngine(self._device)
+        return self.engine
+
+    def _resolve_key(self, verkey, identifier):
+        try:
+            hash((verkey, identifier))
+        except TypeError:
+            return DidVerifier(verkey, identifier=identifier).key
+        return self._keys.resolve(verkey, identifier)
+
+    # -- verify-ahead cache ------------------------------------------------
+    @staticmethod
+    def _vkey(p):
+        return (p.key, p.sig, p.ser)
+
+    def _remember(self, p, ok):
+        self._verdicts[self._vkey(p)] = ok
+        if len(self._verdicts) > self._verdict_cache_size:
+            self._verdicts.popitem(last=False)
+
+    def _verify_prepared(self, p):
+        if not p.key:
+            return False
+        hit = self._verdicts.get(self._vkey(p))
+        if hit is not None:
+            self.stats["cache_hits"] += 1
+            return hit
+        self.stats["single_verifies"] += 1
+        ok = bool(self._engine().sign_open_batch(p.sig + p.ser, [0, len(p.sig) + len(p.ser)], [p.key])[0])
+        self._remember(p, ok)
+        return ok
+
+    def _verify_many(self, prepared):
+        """One GPU launch over prepared items (crypto_sign_open semantics);
+        items without a usable key are False without touching the GPU."""
+        todo = [p for p in prepared if p.key]
+        out = {}
+        if todo:
+            sms, offs, keys, pos = [], [0], [], 0
+            for p in todo:
+                sms.append(p.sig)
+                sms.append(p.ser)
+                pos += len(p.sig) + len(p.ser)
+                offs.append(pos)
+                keys.append(p.key)
+            import numpy as np
+            ok = self._engine().sign_open_batch(b"".join(sms), np.asarray(offs, np.uint64),
+                                                np.frombuffer(b"".join(keys), np.uint8).reshape(-1, 32))
+            self.stats["batches"] += 1
+            self.stats["batch_items"] += len(todo)
+            for p, v in zip(todo, ok):
+                out[id(p)] = bool(v)
+        return [out.get(id(p), False) for p in prepared]
+
+    # -- batch API ----------------------------------------------------------
+    def authenticate_batch(self, msgs, identifiers=None, signatures=None):
+        """Per message: the identifier authenticate() would return, or the
+        exception instance it would raise (same class, args and __cause__)."""
+        n = len(msgs)
+        identifiers = identifiers or [None] * n
+        signatures = signatures or [None] * n
+        results = [None] * n
+        prepared, where = [], []
+        for i, msg in enumerate(msgs):
+            try:
+                prepared.append(self._prepare(msg, identifiers[i], signatures[i]))
+                where.append(i)
+            except SigningException as e:
+                results[i] = e
+            except Exception as ex:
+                e = CouldNotAuthenticate()
+                e.__cause__ = ex
+                results[i] = e
+        for i, p, ok in zip(where, prepared, self._verify_many(prepared)):
+            results[i] = p.identifier if ok else InvalidSignature()
+        return results
+
+    def prefetch(self, msgs):
+        """Verify-ahead: batch-verify every message that gets as far as the
+        verify step, and cache the verdicts for authenticate()."""
+        prepared = []
+        for msg in msgs:
+            try:
+                prepared.append(self._prepare(msg))
+            except Exception:
+                continue  # authenticate() will raise it again
+        uniq = OrderedDict()
+        for p in prepared:
+            k = self._vkey(p)
+            if k not in self._verdicts and k not in uniq:
+                uniq[k] = p
+        items = list(uniq.values())
+        for p, ok in zip(items, self._verify_many(items)):
+            self._remember(p, ok)
+        return len(items)
+
+    def clear_verdicts(self):
+        self._verdicts.clear()
+
+    # -- multi-signature extension (parity unpinned) --------------------------
+    def _prepare_multi(self, msg, signatures, threshold):
+        """Host half of authenticate_multi; returns (threshold, steps) where a
+        step is an exception to raise or a prepared item, in dict order."""
+        num_sigs = len(signatures)
+        if threshold is not None:
+            if num_sigs < threshold:
+                raise InsufficientSignatures(num_sigs, threshold)
+        else:
+            threshold = num_sigs
+        ser = None
+        steps = []
+        for idr, signature in signatures.items():
+            try:
+                try:
+                    sig = b58decode(signature)
+                except Exception as ex:
+                    raise InvalidSignatureFormat from ex
+                if ser is None:
+                    ser = self.serializeForSig(msg, topLevelKeysToIgnore=[SIG, SIGS])
+                verkey = self.getVerkey(idr)
+                if verkey is None:
+                    raise CouldNotAuthenticate('Can not find verkey for {}'.format(idr))
+                steps.append(_Prepared(idr, sig, ser, self._resolve_key(verkey, idr)))
+            except Exception as ex:
+                steps.append(ex)
+        return threshold, steps
+
+    @staticmethod
+    def _finish_multi(threshold, steps, verdict):
+        correct = []
+        for st in steps:
+            if isinstance(st, Exception):
+                raise st
+            if verdict(st):
+                correct.append(st.identifier)
+                if len(correct) == threshold:
+                    return correct
+        raise InsufficientCorrectSignatures(len(correct), threshold)
+
+    def authenticate_multi(self, msg, signatures, threshold=None):
+        """Identifiers whose signatures over msg (minus top-level 'signature'
+        and 'signatures') verify, in dict order, stopping at `threshold`
+        (default: all).  Raises InsufficientSignatures if fewer signatures
+        than the threshold are given, InsufficientCorrectSignatures if too
+        few verify, or the first per-signature error reached in order."""
+        threshold, steps = self._prepare_multi(msg, signatures, threshold)
+        items = [s for s in steps if not isinstance(s, Exception)]
+        verdicts = dict(zip(map(id, items), self._verify_many(items)))
+        return self._finish_multi(threshold, steps, lambda p: verdicts[id(p)])
+
+    def authenticate_multi_batch(self, reqs):
+        """reqs: iterable of (msg, signatures, threshold).  One GPU launch for
+        every signature of every request; per request the result list or the
+        exception authenticate_multi would raise."""
+        staged, items = [], []
+        for msg, sigs, thr in reqs:
+            try:
+                threshold, steps = self._prepare_multi(msg, sigs, thr)
+                staged.append((threshold, steps))
+                items.extend(s for s in steps if not isinstance(s, Exception))
+            except Exception as ex:
+                staged.append(ex)
+        verdicts = dict(zip(map(id, items), self._verify_many(items)))
+        out = []
+        for st in staged:
+            if isinstance(st, Exception):
+                out.append(st)
+                continue
+            try:
+                out.append(self._finish_multi(st[0], st[1], lambda p: verdicts[id(p)]))
+            except Exception as ex:
+                out.append(ex)
+        return out
+
+
+class GpuAuthNr(GpuAuthMixin, SimpleAuthNr):
+    """Drop-in SimpleAuthNr whose Ed25519 checks run on the MI355X."""
+
+    def __init__(self, state=None, nym_lookup=None, engine=None, device=0):
+        SimpleAuthNr.__init__(self, state=state, nym_lookup=nym_lookup)
+        self._gpu_init(engine=engine, device=device)
+
+
+CoreAuthNr = GpuAuthNr
+
+
+class NoAuthenticatorFound(SigningException):
+    code = 160
+    reason = 'no authenticator found'
+
+
+class ReqAuthenticator:
+    """Aggregates client authenticators (north-star name; absent from the
+    reference snapshot).  authenticate(req) returns the set of identifiers
+    every registered authenticator vouches for; each sees its own deepcopy."""
+
+    def __init__(self):
+        self._authenticators = []
+
+    def register_authenticator(self, authnr):
+        self._authenticators.append(authnr)
+
+    @property
+    def core_authenticator(self):
+        for a in self._authenticators:
+            if isinstance(a, GpuAuthMixin):
+                return a
+        raise NoAuthenticatorFound
+
+    def authenticate(self, req_data):
+        identifiers = set()
+        for a in self._authenticators:
+            rv = a.authenticate(deepcopy(req_data))
+            if rv:
+                identifiers.update([rv] if isinstance(rv, str) else rv)
+        if not identifiers:
+            raise NoAuthenticatorFound
+        return identifiers
+
+    def prefetch(self, reqs):
+        for a in self._authenticators:
+            if hasattr(a, "prefetch"):
+                a.prefetch(reqs)

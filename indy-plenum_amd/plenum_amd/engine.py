@@ -28,6 +28,20 @@ def _dev(x):
     return ctypes.c_void_p(x.data_ptr())
 
 
+def _stream_for(stream, *tensors):
+    """Explicit stream (torch.cuda.Stream / int handle) wins; otherwise, for
+    torch tensors, torch's current stream on their device, so the launch is
+    ordered after the torch ops that produced the inputs; otherwise NULL (the
+    context's own stream)."""
+    if stream is not None:
+        return ctypes.c_void_p(stream if isinstance(stream, int) else stream.cuda_stream)
+    for t in tensors:
+        if hasattr(t, "device") and getattr(t.device, "type", None) == "cuda":
+            import torch
+            return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+    return None
+
+
 def pack_messages(msgs):
     """list of bytes -> (uint8 buffer, uint64 offsets[n+1])."""
     lens = np.fromiter((len(m) for m in msgs), dtype=np.uint64, count=len(msgs))
@@ -35,6 +49,19 @@ def pack_messages(msgs):
     np.cumsum(lens, out=off[1:])
     buf = np.frombuffer(b"".join(msgs), dtype=np.uint8) if len(msgs) else np.zeros(0, np.uint8)
     return buf, off
+
+
+def _u8(x, width=None):
+    """bytes / bytearray / list of bytes / array-like -> contiguous uint8 array
+    (reshaped to (-1, width) when width is given)."""
+    if isinstance(x, (bytes, bytearray, memoryview)):
+        a = np.frombuffer(bytes(x), np.uint8)
+    elif isinstance(x, (list, tuple)) and x and isinstance(x[0], (bytes, bytearray)):
+        a = np.frombuffer(b"".join(x), np.uint8)
+    else:
+        a = np.asarray(x, dtype=np.uint8)
+    a = np.ascontiguousarray(a)
+    return a.reshape(-1, width) if width else a.reshape(-1)
 
 
 def unpack_bits(bits, n):
@@ -84,10 +111,9 @@ class EdVerifyEngine:
     # ---------------------------------------------------------------- verify
     def verify_bits(self, sig64, pk32, msgs, msg_off):
         """Packed accept bitmask ((n + 7) // 8 bytes, LSB-first)."""
-        sig64 = np.ascontiguousarray(sig64, dtype=np.uint8).reshape(-1, 64)
-        pk32 = np.ascontiguousarray(pk32, dtype=np.uint8).reshape(-1, 32)
-        msgs = np.ascontiguousarray(np.frombuffer(msgs, np.uint8) if isinstance(msgs, (bytes, bytearray))
-                                    else msgs, dtype=np.uint8)
+        sig64 = _u8(sig64, 64)
+        pk32 = _u8(pk32, 32)
+        msgs = _u8(msgs)
         msg_off = np.ascontiguousarray(msg_off, dtype=np.uint64)
         n = sig64.shape[0]
         if pk32.shape[0] != n or msg_off.shape[0] != n + 1:
@@ -102,16 +128,15 @@ class EdVerifyEngine:
 
     def verify_batch(self, sig64, pk32, msgs, msg_off):
         """Bool array: accepted[i] == (crypto_sign_verify_detached(...) == 0)."""
-        n = np.asarray(sig64).reshape(-1, 64).shape[0]
-        return unpack_bits(self.verify_bits(sig64, pk32, msgs, msg_off), n)
+        sig64 = _u8(sig64, 64)
+        return unpack_bits(self.verify_bits(sig64, pk32, msgs, msg_off), sig64.shape[0])
 
     def sign_open_batch(self, sm, sm_off, pk32):
         """crypto_sign_open verdicts over signed messages sm_i = sig || msg
         (exactly VerifyKey.verify(signature + msg), nacl_wrappers.py:100-108)."""
-        sm = np.ascontiguousarray(np.frombuffer(sm, np.uint8) if isinstance(sm, (bytes, bytearray)) else sm,
-                                  dtype=np.uint8)
+        sm = _u8(sm)
         sm_off = np.ascontiguousarray(sm_off, dtype=np.uint64)
-        pk32 = np.ascontiguousarray(pk32, dtype=np.uint8).reshape(-1, 32)
+        pk32 = _u8(pk32, 32)
         n = pk32.shape[0]
         if sm_off.shape[0] != n + 1:
             raise ValueError("sm_off must have n + 1 entries")
@@ -123,8 +148,9 @@ class EdVerifyEngine:
 
     def verify_batch_device(self, d_sig64, d_pk32, d_msgs, d_msg_off, n, d_accept_words, stream=None):
         """Asynchronous verify on device buffers (torch tensors or raw pointers)."""
+        st = _stream_for(stream, d_sig64, d_accept_words)
         check(self._lib.edv_verify_batch_device(self._ctx, _dev(d_sig64), _dev(d_pk32), _dev(d_msgs),
-                                                _dev(d_msg_off), n, _dev(d_accept_words), _dev(stream)))
+                                                _dev(d_msg_off), n, _dev(d_accept_words), st))
 
     def last_phase_ms(self):
         """(hash, table, dsm) milliseconds of the last verify launch (HIP events)."""
@@ -134,7 +160,7 @@ class EdVerifyEngine:
 
     # ------------------------------------------------------------------ sign
     def seed_keypair_batch(self, seeds32):
-        seeds32 = np.ascontiguousarray(seeds32, dtype=np.uint8).reshape(-1, 32)
+        seeds32 = _u8(seeds32, 32)
         n = seeds32.shape[0]
         pk = np.zeros((n, 32), np.uint8)
         sk = np.zeros((n, 64), np.uint8)
@@ -143,10 +169,9 @@ class EdVerifyEngine:
         return pk, sk
 
     def sign_batch(self, sk64, key_idx, msgs, msg_off):
-        sk64 = np.ascontiguousarray(sk64, dtype=np.uint8).reshape(-1, 64)
+        sk64 = _u8(sk64, 64)
         key_idx = np.ascontiguousarray(key_idx, dtype=np.uint32)
-        msgs = np.ascontiguousarray(np.frombuffer(msgs, np.uint8) if isinstance(msgs, (bytes, bytearray))
-                                    else msgs, dtype=np.uint8)
+        msgs = _u8(msgs)
         msg_off = np.ascontiguousarray(msg_off, dtype=np.uint64)
         n = key_idx.shape[0]
         if n and int(key_idx.max()) >= sk64.shape[0]:
@@ -158,8 +183,9 @@ class EdVerifyEngine:
         return sig
 
     def sign_batch_device(self, d_sk64, d_key_idx, d_msgs, d_msg_off, n, d_sig_out, stream=None):
+        st = _stream_for(stream, d_sk64, d_sig_out)
         check(self._lib.edv_sign_batch_device(self._ctx, _dev(d_sk64), _dev(d_key_idx), _dev(d_msgs),
-                                              _dev(d_msg_off), n, _dev(d_sig_out), _dev(stream)))
+                                              _dev(d_msg_off), n, _dev(d_sig_out), st))
 
     # ----------------------------------------------------------------- tally
     def tally(self, key, voter, phase, valid, n_keys, n_validators):
@@ -182,8 +208,8 @@ class EdVerifyEngine:
                      d_quorum, stream=None):
         check(self._lib.edv_tally_device(self._ctx, _dev(d_key), _dev(d_voter), _dev(d_phase), _dev(d_valid),
                                          n_votes, n_keys, n_validators, _dev(d_ballot), _dev(d_counts),
-                                         _dev(d_quorum), _dev(stream)))
+                                         _dev(d_quorum), _stream_for(stream, d_ballot)))
 
     def tally_finish_device(self, d_ballot, n_keys, n_validators, d_counts, d_quorum, stream=None):
         check(self._lib.edv_tally_finish_device(self._ctx, _dev(d_ballot), n_keys, n_validators, _dev(d_counts),
-                                                _dev(d_quorum), _dev(stream)))
+                                                _dev(d_quorum), _stream_for(stream, d_ballot)))

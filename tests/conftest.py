@@ -1,0 +1,113 @@
+"""Shared fixtures.  `-m gpu` tests need an MI355X (they run on the GPU box);
+everything else runs on a CPU.  The oracle (oracle/_build) and the host-built
+kernel arithmetic (libedv_hostcheck.so) are test infrastructure only."""
+import ctypes
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "indy-plenum_amd")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+if PKG not in sys.path:
+    sys.path.insert(0, PKG)
+if GOLDEN not in sys.path:
+    sys.path.insert(0, GOLDEN)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu on the GPU box)")
+    config.addinivalue_line("markers", "slow: long CPU test")
+
+
+def _ensure_built(path, make_dir):
+    if not os.path.exists(path):
+        subprocess.check_call(["make", "-j8"], cwd=make_dir)
+    return path
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    lib = ctypes.CDLL(_ensure_built(os.path.join(ROOT, "oracle", "_build", "libed25519_oracle.so"),
+                                    os.path.join(ROOT, "oracle")))
+    lib.oracle_verify_detached.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p]
+    lib.oracle_sign_open.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p]
+    return lib
+
+
+@pytest.fixture(scope="session")
+def hostcheck():
+    path = os.path.join(PKG, "libedv_hostcheck.so")
+    if not os.path.exists(path):
+        subprocess.check_call(["make", "libedv_hostcheck.so"], cwd=PKG)
+    return ctypes.CDLL(path)
+
+
+def load_npz(name):
+    return np.load(os.path.join(GOLDEN, name))
+
+
+def items_of(d):
+    """(sig, pk, msg, expect) tuples of a golden npz."""
+    off = d["off"]
+    return [(d["sig"][i].tobytes(), d["pk"][i].tobytes(), d["msgs"][int(off[i]):int(off[i + 1])].tobytes(),
+             bool(d["expect"][i])) for i in range(len(d["expect"]))]
+
+
+class OracleEngine:
+    """CPU test double with EdVerifyEngine's verify interface, answering with
+    the C oracle.  Used ONLY to test host-side logic (check order, exception
+    mapping, batching, sharding) without a GPU; the product has no CPU path."""
+
+    def __init__(self, lib):
+        self.lib = lib
+        self.calls = 0
+
+    def sign_open_batch(self, sm, sm_off, pk32):
+        self.calls += 1
+        sm = bytes(sm) if not isinstance(sm, np.ndarray) else sm.tobytes()
+        pk32 = np.asarray(pk32, dtype=np.uint8).reshape(-1, 32) if not isinstance(pk32, list) else \
+            np.frombuffer(b"".join(pk32), np.uint8).reshape(-1, 32)
+        off = [int(x) for x in sm_off]
+        return np.array([self.lib.oracle_sign_open(sm[off[i]:off[i + 1]], off[i + 1] - off[i], pk32[i].tobytes()) == 0
+                         for i in range(len(off) - 1)], dtype=bool)
+
+    def verify_batch(self, sig64, pk32, msgs, msg_off):
+        self.calls += 1
+        msgs = bytes(msgs) if not isinstance(msgs, np.ndarray) else msgs.tobytes()
+        sig64 = np.asarray(sig64, np.uint8).reshape(-1, 64)
+        pk32 = np.asarray(pk32, np.uint8).reshape(-1, 32)
+        off = [int(x) for x in msg_off]
+        return np.array([self.lib.oracle_verify_detached(sig64[i].tobytes(), msgs[off[i]:off[i + 1]],
+                                                         off[i + 1] - off[i], pk32[i].tobytes()) == 0
+                         for i in range(len(off) - 1)], dtype=bool)
+
+
+@pytest.fixture
+def oracle_engine(oracle):
+    return OracleEngine(oracle)
+
+
+@pytest.fixture(scope="session")
+def gpu_engine():
+    from plenum_amd import EdVerifyEngine
+    eng = EdVerifyEngine(0)
+    yield eng
+    eng.close()
+
+
+def sodium():
+    """libsodium 1.0.18 via ctypes if present (this container and the GPU
+    box image have it); None otherwise."""
+    for cand in ("/opt/conda/lib/libsodium.so.23", "libsodium.so.23"):
+        try:
+            lib = ctypes.CDLL(cand)
+        except OSError:
+            continue
+        lib.sodium_init()
+        lib.sodium_version_string.restype = ctypes.c_char_p
+        return lib
+    return None

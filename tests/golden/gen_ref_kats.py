@@ -1,0 +1,249 @@
+"""Generate reference-pinned KATs by importing the reference's own Python
+(/root/reference, hariexcel/indy-plenum v1.2) in THIS container.
+
+Run with the conda interpreter (the reference needs Python < 3.10 for
+`from collections import Iterable`, signing_serializer.py:23):
+    /opt/conda/bin/python3.9 tests/golden/gen_ref_kats.py
+
+What is imported and run for real: common/serializers/signing_serializer.py,
+common/serializers/serialization.py, plenum/common/exceptions.py,
+plenum/common/verifier.py, plenum/server/client_authn.py,
+stp_core/crypto/nacl_wrappers.py.  Third-party packages the reference needs
+that are not installed here are replaced by minimal stand-ins defined below
+(written for this generator, not copied from anywhere):
+  libnacl          -> ctypes over libsodium 1.0.18 (/opt/conda/lib/libsodium.so.23)
+  base58           -> the 0.2.4 API (b58encode -> str, b58decode -> bytes)
+  stp_core.common.log, ioflo -> logging stubs (log output only)
+  plenum.common.jsonpickle_util -> no-op setUpJsonpickle (jsonpickle absent)
+  plenum.server.domain_req_handler -> getNymDetails returns {} (empty state),
+      because the real module imports plenum/common/util.py, a SyntaxError on
+      Python >= 3.7 (util.py:337 `asyncio.async`).
+Outputs (pure data, committed): serializer_kat.json, authn_kat.json,
+quorums_kat.json.
+"""
+import ctypes
+import json
+import os
+import sys
+import types
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF = "/root/reference"
+
+# ------------------------------------------------------------------ stand-ins
+_sodium = ctypes.CDLL("/opt/conda/lib/libsodium.so.23")
+_sodium.sodium_init()
+
+libnacl = types.ModuleType("libnacl")
+libnacl.crypto_sign_PUBLICKEYBYTES = 32
+libnacl.crypto_sign_SECRETKEYBYTES = 64
+libnacl.crypto_sign_BYTES = 64
+libnacl.crypto_box_PUBLICKEYBYTES = 32
+libnacl.crypto_box_SECRETKEYBYTES = 32
+libnacl.crypto_box_NONCEBYTES = 24
+libnacl.crypto_sign_SEEDBYTES = 32
+
+
+def _unused(*a, **k):
+    raise NotImplementedError("not needed for signature verification")
+
+
+libnacl.crypto_box_afternm = libnacl.crypto_box_beforenm = _unused
+libnacl.crypto_box_open_afternm = libnacl.crypto_scalarmult_base = _unused
+
+
+def _crypto_sign_open(sm, pk):
+    m = ctypes.create_string_buffer(len(sm) + 1)
+    mlen = ctypes.c_ulonglong()
+    if _sodium.crypto_sign_open(m, ctypes.byref(mlen), sm, ctypes.c_ulonglong(len(sm)), pk):
+        raise ValueError("Failed to validate message")
+    return m.raw[:mlen.value]
+
+
+def _crypto_sign_seed_keypair(seed):
+    pk = ctypes.create_string_buffer(32)
+    sk = ctypes.create_string_buffer(64)
+    _sodium.crypto_sign_seed_keypair(pk, sk, seed)
+    return pk.raw, sk.raw
+
+
+def _crypto_sign(msg, sk):
+    sm = ctypes.create_string_buffer(len(msg) + 64)
+    smlen = ctypes.c_ulonglong()
+    _sodium.crypto_sign(sm, ctypes.byref(smlen), msg, ctypes.c_ulonglong(len(msg)), sk)
+    return sm.raw[:smlen.value]
+
+
+libnacl.crypto_sign_open = _crypto_sign_open
+libnacl.crypto_sign_seed_keypair = _crypto_sign_seed_keypair
+libnacl.crypto_sign = _crypto_sign
+libnacl.randombytes = lambda n: os.urandom(n)
+libnacl.crypto_box_keypair = lambda: (None, None)
+sys.modules["libnacl"] = libnacl
+sys.modules["libnacl.secret"] = types.ModuleType("libnacl.secret")
+libnacl.secret = sys.modules["libnacl.secret"]
+
+base58 = types.ModuleType("base58")
+_ALPH = "123456789ABCDEFGHJKLMNPQRSTUVWXYZabcdefghijkmnopqrstuvwxyz"
+
+
+def _b58encode(v):
+    if not isinstance(v, bytes):
+        raise TypeError("a bytes-like object is required")
+    nz = len(v) - len(v.lstrip(b"\0"))
+    acc, out = int.from_bytes(v, "big"), ""
+    while acc:
+        acc, r = divmod(acc, 58)
+        out = _ALPH[r] + out
+    return _ALPH[0] * nz + out
+
+
+def _b58decode(v):
+    if not isinstance(v, str):
+        v = v.decode("ascii")
+    nz = len(v) - len(v.lstrip(_ALPH[0]))
+    acc = 0
+    for c in v[nz:]:
+        acc = acc * 58 + _ALPH.index(c)
+    return b"\0" * nz + (acc.to_bytes((acc.bit_length() + 7) // 8, "big") if acc else b"")
+
+
+base58.b58encode, base58.b58decode, base58.alphabet = _b58encode, _b58decode, _ALPH
+sys.modules["base58"] = base58
+
+import logging  # noqa: E402
+
+log_mod = types.ModuleType("stp_core.common.log")
+log_mod.getlogger = lambda name=None: logging.getLogger("ref")
+sys.modules["stp_core.common.log"] = log_mod
+drh = types.ModuleType("plenum.server.domain_req_handler")
+
+
+class DomainRequestHandler:
+    @staticmethod
+    def getNymDetails(state, nym, isCommitted=True):
+        return {}
+
+
+drh.DomainRequestHandler = DomainRequestHandler
+sys.modules["plenum.server.domain_req_handler"] = drh
+# plenum/__init__.py only registers jsonpickle handlers (jsonpickle not installed)
+jp = types.ModuleType("plenum.common.jsonpickle_util")
+jp.setUpJsonpickle = lambda: None
+sys.modules["plenum.common.jsonpickle_util"] = jp
+
+sys.path.insert(0, REF)
+import stp_core.common  # noqa: E402,F401  (package __init__ only)
+
+stp_core_common = sys.modules["stp_core.common"]
+stp_core_common.log = log_mod
+
+from common.serializers.serialization import serialize_msg_for_signing  # noqa: E402
+from plenum.server.client_authn import SimpleAuthNr  # noqa: E402
+from plenum.common.verifier import DidVerifier  # noqa: E402
+
+
+# ------------------------------------------------------------------- KATs
+def serializer_kats():
+    cases = [
+        {"a": 1}, {"b": "x", "a": "y"}, {"k": [1, 2, 3]}, {"k": None}, {"k": True}, {"k": False},
+        {"k": 1.5}, {"k": 1e16}, {"k": 0.1}, {"k": -3}, {"k": 12345678901234567890},
+        {"nested": {"z": 1, "a": {"q": [1, {"w": "e"}]}}}, {"u": "héllo 世界"},
+        {"signature": "drop-me", "identifier": "idr", "reqId": 1},
+        {"l": []}, {"d": {}}, {"s": ""}, {"mixed": [None, "a", 1, 2.5, [3, 4], {"x": "y"}]},
+        {"identifier": "L5AD5g65TDQr1PPHHRoiGf", "reqId": 1513945121191691,
+         "operation": {"type": "1", "dest": "Bf9Z1tKWpcJAvKJVhZhvVZ", "verkey": "~8zH9ZSyZTFPGJ4ZPL5Rvxx"},
+         "protocolVersion": 1, "signature": "x"},
+        {"myMsg": "42 (forty-two) is the natural number that succeeds 41 and precedes 43."},
+        {"1": "a", "2": "b", "3": [1, {"2": "k"}]},
+    ]
+    out = []
+    for c in cases:
+        for ignore in (None, ["signature"]):
+            out.append({"msg": c, "ignore": ignore,
+                        "bytes_hex": serialize_msg_for_signing(c, topLevelKeysToIgnore=ignore).hex()})
+    # non-acceptable types raise
+    for bad in ({"t": (1, 2)}, {"b": b"x"}, {"s": {1, 2}}):
+        try:
+            serialize_msg_for_signing(bad)
+            res = "ok"
+        except Exception as ex:
+            res = type(ex).__name__
+        out.append({"msg_repr": repr(bad), "raises": res})
+    return out
+
+
+def authn_kats():
+    seed = b"Falcon00000000000000000000000000"
+    pk, sk = _crypto_sign_seed_keypair(seed)
+    full_vk = _b58encode(pk)
+    did_idr = _b58encode(pk[:16])
+    abbr_vk = "~" + _b58encode(pk[16:])
+    cases = []
+
+    def sign(msg):
+        ser = serialize_msg_for_signing(msg, topLevelKeysToIgnore=["signature"])
+        return _b58encode(_crypto_sign(ser, sk)[:64])
+
+    def run(name, msg, verkey, identifier=None, signature=None, register=True):
+        a = SimpleAuthNr()
+        if register:
+            a.addIdr(msg.get("identifier") if identifier is None else identifier, verkey)
+        try:
+            res = {"result": a.authenticate(msg, identifier, signature)}
+        except Exception as ex:
+            res = {"raises": type(ex).__name__,
+                   "cause": type(ex.__cause__).__name__ if ex.__cause__ is not None else None}
+        cases.append(dict(name=name, msg=msg, verkey=verkey, identifier=identifier, signature=signature,
+                          register=register, **res))
+
+    base = {"identifier": did_idr, "reqId": 1513945121191691, "protocolVersion": 1,
+            "operation": {"type": "1", "dest": "Bf9Z1tKWpcJAvKJVhZhvVZ", "verkey": "~8zH9ZSyZTFPGJ4ZPL5Rvxx"}}
+    good = dict(base, signature=sign(base))
+    run("valid-abbreviated-verkey", good, abbr_vk)
+    run("valid-full-verkey", good, full_vk)
+    cryp = dict(base, identifier=full_vk)
+    cryp = dict(cryp, signature=sign(cryp))
+    run("valid-cryptonym-no-verkey", cryp, "", register=True)
+    run("tampered-reqId", dict(good, reqId=good["reqId"] + 1), abbr_vk)
+    run("tampered-operation", dict(good, operation=dict(good["operation"], dest="x")), abbr_vk)
+    run("extra-top-level-key", dict(good, extra="1"), abbr_vk)
+    sigb = _b58decode(good["signature"])
+    run("sig-63-bytes", dict(good, signature=_b58encode(sigb[:63])), abbr_vk)
+    run("sig-65-bytes", dict(good, signature=_b58encode(sigb + b"\x01")), abbr_vk)
+    run("sig-leading-zeros", dict(good, signature=_b58encode(b"\0" * 10 + sigb)), abbr_vk)
+    run("sig-non-base58", dict(good, signature="0OIl" + good["signature"][4:]), abbr_vk)
+    run("sig-empty", dict(good, signature=""), abbr_vk)
+    run("sig-missing", dict(base), abbr_vk)
+    run("sig-not-str", dict(good, signature=12345), abbr_vk)
+    run("idr-empty", dict(good, identifier=""), abbr_vk, identifier=None, register=False)
+    nid = dict(good)
+    del nid["identifier"]
+    run("idr-missing", nid, abbr_vk, register=False)
+    run("verkey-31-bytes", good, _b58encode(pk[:31]))
+    run("verkey-abbrev-15-bytes", good, "~" + _b58encode(pk[16:31]))
+    run("verkey-hex-encoded", good, _b58encode(pk.hex().encode()))
+    run("verkey-none", good, None)
+    run("verkey-non-base58", good, "~0OIl")
+    run("unknown-identifier", good, abbr_vk, register=False)
+    run("explicit-identifier-and-signature", dict(base), abbr_vk, identifier=did_idr, signature=good["signature"])
+    run("explicit-signature-wrong", dict(base), abbr_vk, identifier=did_idr, signature=sign(dict(base, reqId=2)))
+    run("float-field", dict(base, reqId=1.5, signature=sign(dict(base, reqId=1.5))), abbr_vk)
+    run("tuple-field", dict(good, operation=(1, 2)), abbr_vk)
+    # DidVerifier KATs from plenum/test/common/test_verifier.py
+    dv = DidVerifier("~8zH9ZSyZTFPGJ4ZPL5Rvxx", identifier="99BgFBg35BehzfSADV5nM4")
+    return {"cases": cases, "did_expand": [{"verkey": "~8zH9ZSyZTFPGJ4ZPL5Rvxx", "identifier": "99BgFBg35BehzfSADV5nM4",
+                                            "expanded": dv.verkey}],
+            "seed_hex": seed.hex(), "pk_hex": pk.hex()}
+
+
+def main():
+    with open(os.path.join(HERE, "serializer_kat.json"), "w") as f:
+        json.dump(serializer_kats(), f, indent=0, ensure_ascii=True)
+    with open(os.path.join(HERE, "authn_kat.json"), "w") as f:
+        json.dump(authn_kats(), f, indent=0, ensure_ascii=True)
+    print("ok")
+
+
+if __name__ == "__main__":
+    main()

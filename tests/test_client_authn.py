@@ -1,0 +1,185 @@
+"""Host-side logic of the drop-in authenticator: check order, exception
+classes and causes, batching, verify-ahead, multi-signature extension.
+
+Verdicts come from an oracle-backed test double (conftest.OracleEngine); the
+same table runs against the real GPU engine in test_gpu_authn.py.  The
+expectations are tests/golden/authn_kat.json, produced by running the
+reference's own NaclAuthNr/SimpleAuthNr/DidVerifier (gen_ref_kats.py)."""
+import json
+import os
+
+import pytest
+
+from conftest import GOLDEN
+from plenum_amd import exceptions as X
+from plenum_amd.client_authn import GpuAuthNr, ReqAuthenticator, SimpleAuthNr
+from plenum_amd.verifier import DidVerifier
+
+
+def kat():
+    return json.load(open(os.path.join(GOLDEN, "authn_kat.json")))
+
+
+def fix_case(c):
+    msg = dict(c["msg"])
+    if c["name"] == "tuple-field":
+        msg["operation"] = tuple(msg["operation"])  # JSON turned the tuple into a list
+    return msg
+
+
+def make(engine, c):
+    a = GpuAuthNr(engine=engine)
+    if c["register"]:
+        a.addIdr(c["msg"].get("identifier") if c["identifier"] is None else c["identifier"], c["verkey"])
+    return a
+
+
+def check_result(c, outcome):
+    if "result" in c:
+        assert outcome == c["result"], c["name"]
+    else:
+        assert isinstance(outcome, Exception), (c["name"], outcome)
+        assert type(outcome).__name__ == c["raises"], (c["name"], outcome)
+        cause = type(outcome.__cause__).__name__ if outcome.__cause__ is not None else None
+        if c["cause"] in ("AttributeError", "ValueError", "Exception", "InvalidKey", None):
+            assert cause == c["cause"], (c["name"], cause)
+
+
+def run_single(a, c):
+    try:
+        return a.authenticate(fix_case(c), c["identifier"], c["signature"])
+    except Exception as ex:
+        return ex
+
+
+def test_authenticate_matches_reference_kats(oracle_engine):
+    for c in kat()["cases"]:
+        check_result(c, run_single(make(oracle_engine, c), c))
+
+
+def test_authenticate_batch_equals_single(oracle_engine):
+    cases = [c for c in kat()["cases"] if c["register"]]
+    # one authenticator holding every identity the cases use (same verkey per idr)
+    by_idr = {}
+    for c in cases:
+        idr = c["msg"].get("identifier") if c["identifier"] is None else c["identifier"]
+        by_idr.setdefault((idr, c["verkey"]), []).append(c)
+    for (idr, vk), group in by_idr.items():
+        a = GpuAuthNr(engine=oracle_engine)
+        a.addIdr(idr, vk)
+        res = a.authenticate_batch([fix_case(c) for c in group], [c["identifier"] for c in group],
+                                   [c["signature"] for c in group])
+        for c, r in zip(group, res):
+            check_result(c, r)
+
+
+def test_batch_is_one_engine_call(oracle_engine):
+    good = next(c for c in kat()["cases"] if c["name"] == "valid-abbreviated-verkey")
+    a = make(oracle_engine, good)
+    msgs = [good["msg"]] * 5 + [dict(good["msg"], reqId=7)] * 3
+    before = oracle_engine.calls
+    res = a.authenticate_batch(msgs)
+    assert oracle_engine.calls == before + 1
+    assert res[:5] == [good["msg"]["identifier"]] * 5
+    assert all(isinstance(r, X.InvalidSignature) for r in res[5:])
+
+
+def test_prefetch_then_authenticate_hits_cache(oracle_engine):
+    good = next(c for c in kat()["cases"] if c["name"] == "valid-abbreviated-verkey")
+    a = make(oracle_engine, good)
+    bad = dict(good["msg"], reqId=9)
+    assert a.prefetch([good["msg"], bad, good["msg"], {"no": "sig"}]) == 2  # deduped, unsigned skipped
+    calls = oracle_engine.calls
+    assert a.authenticate(good["msg"]) == good["msg"]["identifier"]
+    with pytest.raises(X.InvalidSignature):
+        a.authenticate(bad)
+    assert oracle_engine.calls == calls and a.stats["cache_hits"] == 2
+    with pytest.raises(X.MissingSignature):
+        a.authenticate({"no": "sig"})
+
+
+def test_did_verifier_reference_kats():
+    for d in kat()["did_expand"]:
+        assert DidVerifier(d["verkey"], identifier=d["identifier"]).verkey == d["expanded"]
+    with pytest.raises(X.InvalidKey, match="verkey FFFF"):
+        DidVerifier('FFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFF')  # test_verifier.py:18-23
+
+
+def test_reference_dummy_authenticator(oracle_engine):
+    # plenum/test/client/test_client_authn.py:39-52: getVerkey -> None
+    class Dummy(GpuAuthNr):
+        def getVerkey(self, _):
+            return None
+    good = next(c for c in kat()["cases"] if c["name"] == "valid-abbreviated-verkey")
+    with pytest.raises(X.CouldNotAuthenticate):
+        Dummy(engine=oracle_engine).authenticate(good["msg"])
+
+
+def test_simpleauthnr_state_lookup(oracle_engine):
+    good = next(c for c in kat()["cases"] if c["name"] == "valid-abbreviated-verkey")
+    idr = good["msg"]["identifier"]
+    a = GpuAuthNr(state="S", nym_lookup=lambda st, i: {"verkey": good["verkey"]} if (st, i) == ("S", idr) else {},
+                  engine=oracle_engine)
+    assert a.authenticate(good["msg"]) == idr
+    assert isinstance(a, SimpleAuthNr)
+
+
+def test_reqid_reason_text():
+    ex = X.CouldNotAuthenticate()
+    ex.__cause__ = X.InvalidKey("verkey abc")
+    assert X.reasonForClientFromException(ex) == \
+        "client request invalid: CouldNotAuthenticate() [caused by verkey abc]"
+
+
+# --- authenticate_multi (extension; parity unpinned: only per-signature
+# verdicts are pinned, by libsodium through the oracle) ----------------------
+def _multi_fixture(oracle_engine):
+    import ctypes
+    from plenum_amd.base58 import b58encode
+    from plenum_amd.serialization import serialize_msg_for_signing
+    from conftest import sodium
+    s = sodium()
+    if s is None:
+        pytest.skip("needs libsodium to sign")
+    a = GpuAuthNr(engine=oracle_engine)
+    msg = {"identifier": "x", "reqId": 1, "operation": {"type": "1"}}
+    ser = serialize_msg_for_signing(msg, topLevelKeysToIgnore=["signature", "signatures"])
+    sigs = {}
+    for i in range(4):
+        pk, sk = ctypes.create_string_buffer(32), ctypes.create_string_buffer(64)
+        s.crypto_sign_seed_keypair(pk, sk, bytes([i + 1]) * 32)
+        idr = b58encode(pk.raw[:16])
+        a.addIdr(idr, "~" + b58encode(pk.raw[16:]))
+        sig = ctypes.create_string_buffer(64)
+        s.crypto_sign_detached(sig, None, ser, ctypes.c_ulonglong(len(ser)), sk)
+        sigs[idr] = b58encode(sig.raw)
+    return a, msg, sigs
+
+
+def test_authenticate_multi(oracle_engine):
+    a, msg, sigs = _multi_fixture(oracle_engine)
+    idrs = list(sigs)
+    assert a.authenticate_multi(msg, sigs) == idrs
+    assert a.authenticate_multi(msg, sigs, threshold=2) == idrs[:2]
+    with pytest.raises(X.InsufficientSignatures):
+        a.authenticate_multi(msg, sigs, threshold=5)
+    bad = dict(sigs)
+    bad[idrs[0]] = sigs[idrs[1]]
+    assert a.authenticate_multi(msg, bad, threshold=3) == idrs[1:]
+    with pytest.raises(X.InsufficientCorrectSignatures):
+        a.authenticate_multi(msg, bad)
+    fmt = dict(sigs)
+    fmt[idrs[0]] = "0OIl"
+    with pytest.raises(X.InvalidSignatureFormat):
+        a.authenticate_multi(msg, fmt)
+    res = a.authenticate_multi_batch([(msg, sigs, None), (msg, bad, None), (msg, bad, 3), (msg, sigs, 9)])
+    assert res[0] == idrs and res[2] == idrs[1:]
+    assert isinstance(res[1], X.InsufficientCorrectSignatures) and isinstance(res[3], X.InsufficientSignatures)
+
+
+def test_req_authenticator(oracle_engine):
+    good = next(c for c in kat()["cases"] if c["name"] == "valid-abbreviated-verkey")
+    ra = ReqAuthenticator()
+    ra.register_authenticator(make(oracle_engine, good))
+    assert ra.authenticate(good["msg"]) == {good["msg"]["identifier"]}
+    assert isinstance(ra.core_authenticator, GpuAuthNr)

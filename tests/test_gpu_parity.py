@@ -1,0 +1,134 @@
+"""Parity of the HIP path (libplenum_edverify.so on the MI355X) with libsodium
+1.0.18 (golden vectors) and with the oracle (fresh random/adversarial
+batches).  Bit-exact: every accept bit must equal libsodium's verdict."""
+import ctypes
+import hashlib
+
+import numpy as np
+import pytest
+
+from conftest import items_of, load_npz
+from plenum_amd import pack_messages
+
+pytestmark = pytest.mark.gpu
+L = 2**252 + 27742317777372353535851937790883648493
+
+
+@pytest.mark.parametrize("name", ["ed25519_valid.npz", "ed25519_edge.npz"])
+def test_golden(gpu_engine, name):
+    d = load_npz(name)
+    got = gpu_engine.verify_batch(d["sig"], d["pk"], d["msgs"], d["off"])
+    assert (got == d["expect"].astype(bool)).all(), np.nonzero(got != d["expect"].astype(bool))
+
+
+def test_signer_matches_libsodium(gpu_engine):
+    k = load_npz("sign_kat.npz")
+    pk, sk = gpu_engine.seed_keypair_batch(k["seed"])
+    assert (pk == k["pk"]).all()
+    sig = gpu_engine.sign_batch(sk, np.arange(len(pk), dtype=np.uint32), k["msgs"], k["off"])
+    assert (sig == k["sig"]).all()
+
+
+def _random_batch(eng, n, seed, mlen_max=600):
+    rng = np.random.default_rng(seed)
+    pk, sk = eng.seed_keypair_batch(rng.integers(0, 256, (97, 32), dtype=np.uint8))
+    kidx = rng.integers(0, 97, n).astype(np.uint32)
+    msgs = [bytes(rng.integers(0, 256, int(rng.integers(0, mlen_max)), dtype=np.uint8)) for _ in range(n)]
+    buf, off = pack_messages(msgs)
+    sig = eng.sign_batch(sk, kidx, buf, off)
+    pks = pk[kidx].copy()
+    # corruptions, ~40%: R / S / pk bit flips, S + L, S high bit, random pk
+    for i in range(n):
+        r = rng.random()
+        if r < 0.08:
+            sig[i, rng.integers(0, 32)] ^= 1 << int(rng.integers(0, 8))
+        elif r < 0.16:
+            sig[i, 32 + rng.integers(0, 32)] ^= 1 << int(rng.integers(0, 8))
+        elif r < 0.24:
+            pks[i, rng.integers(0, 32)] ^= 1 << int(rng.integers(0, 8))
+        elif r < 0.30:
+            s = int.from_bytes(sig[i, 32:].tobytes(), "little") + L
+            if s < 2**256:
+                sig[i, 32:] = np.frombuffer(s.to_bytes(32, "little"), np.uint8)
+        elif r < 0.34:
+            sig[i, 63] |= 0x80
+        elif r < 0.40:
+            pks[i] = rng.integers(0, 256, 32, dtype=np.uint8)
+    return sig, pks, msgs, buf, off
+
+
+def test_random_batch_vs_oracle(gpu_engine, oracle):
+    n = 3001  # not a multiple of 64: ragged last ballot word
+    sig, pks, msgs, buf, off = _random_batch(gpu_engine, n, 1)
+    got = gpu_engine.verify_batch(sig, pks, buf, off)
+    want = np.array([oracle.oracle_verify_detached(sig[i].tobytes(), msgs[i], len(msgs[i]), pks[i].tobytes()) == 0
+                     for i in range(n)])
+    assert (got == want).all(), np.nonzero(got != want)
+    assert 0.5 < want.mean() < 0.75
+
+
+def test_message_offsets_and_alignment(gpu_engine, oracle):
+    # msg_off[0] != 0, odd offsets, empty messages, zero-length batch
+    sig, pks, msgs, buf, off = _random_batch(gpu_engine, 257, 2, mlen_max=50)
+    pad = np.concatenate([np.full(3, 0xAB, np.uint8), buf])
+    got = gpu_engine.verify_batch(sig, pks, pad, off + 3)
+    ref = gpu_engine.verify_batch(sig, pks, buf, off)
+    assert (got == ref).all()
+    assert gpu_engine.verify_batch(np.zeros((0, 64), np.uint8), np.zeros((0, 32), np.uint8),
+                                   np.zeros(0, np.uint8), np.zeros(1, np.uint64)).shape == (0,)
+    e = load_npz("ed25519_edge.npz")
+    got = gpu_engine.verify_batch(e["sig"][:1], e["pk"][:1], e["msgs"], e["off"][:2])
+    assert got.tolist() == [bool(e["expect"][0])]
+
+
+def test_sign_open_any_signature_length(gpu_engine, oracle):
+    d = items_of(load_npz("ed25519_valid.npz"))[:40]
+    sms, pks = [], []
+    for j, (sig, pk, msg, _) in enumerate(d):
+        cut = [64, 63, 65, 0, 10, 64][j % 6]
+        s = (sig + b"\x01")[:cut] if cut <= 65 else sig
+        sms.append(s + msg)
+        pks.append(pk)
+    buf, off = pack_messages(sms)
+    got = gpu_engine.sign_open_batch(buf, off, np.frombuffer(b"".join(pks), np.uint8).reshape(-1, 32))
+    want = [oracle.oracle_sign_open(sm, len(sm), pk) == 0 for sm, pk in zip(sms, pks)]
+    assert got.tolist() == want
+    assert sum(want) == len([j for j in range(40) if j % 6 in (0, 5)])
+
+
+def test_large_batch_properties(gpu_engine):
+    """1M requests (BASELINE configs[1] size): every honest signature accepted,
+    every corrupted one rejected, bitmask popcount exact; plus a checksum of
+    the accept mask stable across two launches (determinism)."""
+    import torch
+    from plenum_amd import synth
+    n = 1_000_000
+    pks, sks = gpu_engine.seed_keypair_batch(synth.signer_seeds(1000))
+    msgs, kidx, _ = synth.nym_messages(n, pks, alias_len=43)
+    buf, off = pack_messages(msgs)
+    dev = torch.device("cuda", 0)
+    d_msgs = torch.from_numpy(np.concatenate([buf, np.zeros(16, np.uint8)])).to(dev)
+    d_off = torch.from_numpy(off.view(np.int64)).to(dev)
+    d_sig = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+    gpu_engine.sign_batch_device(torch.from_numpy(sks).to(dev), torch.from_numpy(kidx.astype(np.int32)).to(dev),
+                                 d_msgs, d_off, n, d_sig)
+    d_pk = torch.from_numpy(pks).to(dev)[torch.from_numpy(kidx.astype(np.int64)).to(dev)].contiguous()
+    torch.cuda.synchronize()
+    sig = d_sig.cpu().numpy()
+    rng = np.random.default_rng(5)
+    bad = rng.choice(n, n // 20, replace=False)
+    sig[bad, 40] ^= 0x10
+    d_sig = torch.from_numpy(sig).to(dev)
+    words = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
+    digests = []
+    for _ in range(2):
+        gpu_engine.verify_batch_device(d_sig, d_pk, d_msgs, d_off, n, words)
+        torch.cuda.synchronize()
+        w = words.cpu().numpy()
+        digests.append(hashlib.sha256(w.tobytes()).hexdigest())
+    bits = np.unpackbits(w.view(np.uint8), bitorder="little")[:n].astype(bool)
+    want = np.ones(n, bool)
+    want[bad] = False
+    wrong = np.nonzero(bits != want)[0]
+    assert len(wrong) == 0, (len(wrong), wrong[:8], wrong[-8:], bits[wrong[:8]])
+    assert digests[0] == digests[1]

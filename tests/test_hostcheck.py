@@ -1,0 +1,84 @@
+"""The exact kernel arithmetic (indy-plenum_amd/csrc/*.h, compiled for the CPU
+with EDV_BOUND_CHECK limb-bound assertions) against the golden vectors and the
+oracle -- catches arithmetic bugs without a GPU."""
+import ctypes
+import hashlib
+import random
+
+import pytest
+
+from conftest import items_of, load_npz
+
+p = 2**255 - 19
+L = 2**252 + 27742317777372353535851937790883648493
+
+
+@pytest.mark.parametrize("name", ["ed25519_edge.npz", "ed25519_valid.npz"])
+def test_kernel_verify_on_cpu_matches_golden(hostcheck, name):
+    items = items_of(load_npz(name))
+    if name == "ed25519_valid.npz":
+        items = items[::7]  # the host build is slow (-O1, assertions)
+    for i, (sig, pk, msg, expect) in enumerate(items):
+        assert (hostcheck.edv_host_verify(sig, pk, msg, ctypes.c_uint64(len(msg))) == 0) == expect, i
+
+
+def test_kernel_sha512_any_alignment(hostcheck):
+    rng = random.Random(5)
+    for t in range(200):
+        pre = bytes(rng.getrandbits(8) for _ in range(64))
+        m = bytes(rng.getrandbits(8) for _ in range(rng.randrange(0, 600)))
+        off = rng.randrange(0, 4)
+        buf = ctypes.create_string_buffer(b"\0" * off + m + b"\0" * 8)
+        out = ctypes.create_string_buffer(64)
+        hostcheck.edv_host_sha512_prefixed(out, pre, ctypes.byref(buf, off), ctypes.c_uint64(len(m)))
+        assert out.raw == hashlib.sha512(pre + m).digest()
+
+
+def test_kernel_sc_reduce_and_canonical(hostcheck):
+    rng = random.Random(6)
+    specials = [0, 1, L - 1, L, L + 1, 2 * L, 2**512 - 1, 2**512 - 1 - L, 2**252, 2**253 - 1, (2**256 - 1) * L % 2**512]
+    for t in range(3000):
+        x = specials[t] if t < len(specials) else rng.getrandbits(512)
+        out = ctypes.create_string_buffer(32)
+        hostcheck.edv_host_sc_reduce(out, x.to_bytes(64, "little"))
+        assert int.from_bytes(out.raw, "little") == x % L, hex(x)
+    for s in [0, L - 1, L, L + 1, 2**256 - 1, 2**255, L | 2**255]:
+        assert hostcheck.edv_host_sc_is_canonical(s.to_bytes(32, "little")) == (s < L)
+
+
+def test_kernel_field_ops(hostcheck):
+    rng = random.Random(7)
+    edge = [0, 1, 2, p - 1, p, p + 1, 2**255 - 1, 19, 2**254, (1 << 26) - 1]
+    for t in range(4000):
+        a = edge[t % len(edge)] if t < 100 else rng.getrandbits(255)
+        b = edge[(t // len(edge)) % len(edge)] if t < 100 else rng.getrandbits(255)
+        out = ctypes.create_string_buffer(32)
+        hostcheck.edv_host_fe_mul(out, a.to_bytes(32, "little"), b.to_bytes(32, "little"), 0)
+        assert int.from_bytes(out.raw, "little") == a * b % p
+        hostcheck.edv_host_fe_mul(out, a.to_bytes(32, "little"), b.to_bytes(32, "little"), 1)
+        assert int.from_bytes(out.raw, "little") == a * a % p
+        if a % p and t % 8 == 0:
+            hostcheck.edv_host_fe_invert(out, a.to_bytes(32, "little"))
+            assert int.from_bytes(out.raw, "little") == pow(a, p - 2, p)
+
+
+def test_kernel_point_roundtrip_and_blacklist(hostcheck, oracle):
+    import edwards as E
+    rng = random.Random(8)
+    for t in range(200):
+        y = rng.randrange(p) if t else 1
+        enc = (y | (rng.getrandbits(1) << 255)).to_bytes(32, "little")
+        o1, o2 = ctypes.create_string_buffer(32), ctypes.create_string_buffer(32)
+        r1 = hostcheck.edv_host_point_roundtrip(o1, enc)
+        r2 = oracle.oracle_point_roundtrip(o2, enc)
+        assert r1 == r2
+        if r1 == 0:
+            assert o1.raw == o2.raw
+    for P in E.order8_points():
+        enc = E.encode(P)
+        assert hostcheck.edv_host_has_small_order(enc)
+    for y in range(p, 2**255):
+        for s in (0, 1):
+            enc = (y | (s << 255)).to_bytes(32, "little")
+            assert hostcheck.edv_host_is_canonical_point(enc) == oracle.oracle_is_canonical_point(enc) == 0
+            assert hostcheck.edv_host_has_small_order(enc) == oracle.oracle_has_small_order(enc)

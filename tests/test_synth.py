@@ -1,0 +1,31 @@
+"""The bench's synthetic NYM payloads are exactly what a Plenum client signs:
+serialize_msg_for_signing(request, ['signature']) (signer_did.py:114-121)."""
+import numpy as np
+
+from plenum_amd import synth
+
+
+def test_nym_messages_equal_serializer_output():
+    pks = np.random.default_rng(0).integers(0, 256, (7, 32), dtype=np.uint8)
+    for alias_len in (0, 43):
+        msgs, kidx, spec = synth.nym_messages(300, pks, alias_len=alias_len, seed=3)
+        for i in range(0, 300, 7):
+            assert synth.check_nym_message(spec, i, 7, msgs[i])
+        assert (kidx == np.arange(300) % 7).all()
+    msgs, _, _ = synth.nym_messages(1000, pks, alias_len=43)
+    assert abs(np.mean([len(m) for m in msgs]) - 200) < 2
+
+
+def test_signer_seeds_match_config_c0():
+    s = synth.signer_seeds(3)
+    assert s[1].tobytes() == (1).to_bytes(2, "little") + b"\0" * 30
+
+
+def test_add_torsion_changes_R():
+    import sys, os
+    from conftest import GOLDEN
+    sys.path.insert(0, GOLDEN)
+    import edwards as E
+    R = E.encode(E.mul(12345, E.B))
+    Rt = synth.add_torsion(R)
+    assert Rt != R and E.mul(8, E.decode(Rt)) == E.mul(8, E.decode(R))
