@@ -48,6 +48,11 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=400_000, help="items timed on host libsodium (rank 0, N=1)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, affinity CPUs)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--path", choices=["keyed", "general"], default="keyed",
+                    help="keyed: signers' verkeys registered once (fixed-base tables in HBM, like "
+                         "SimpleAuthNr.addIdr); general: every request carries its own key bytes")
+    ap.add_argument("--general-steps", type=int, default=5,
+                    help="also time the general path for this many steps (0 = skip)")
     return ap.parse_args()
 
 
@@ -143,10 +148,33 @@ def main():
     gathered = [torch.zeros_like(d_words) for _ in range(world)] if world > 1 else None
     stream = torch.cuda.current_stream(dev)
 
-    def step():
+    # keyed path: register the signers' verkeys once (not per request)
+    key_build_ms = None
+    if args.config == "c2":
+        # corrupted pks (small-order / non-canonical) become keys of their own
+        pk_h = d_pk.cpu().numpy()
+        uniq, inv = np.unique(pk_h, axis=0, return_inverse=True)
+        reg_pks, d_kreq = uniq, torch.from_numpy(inv.reshape(-1).astype(np.int32)).to(dev)
+    else:
+        reg_pks, d_kreq = pks, d_kidx
+    torch.cuda.synchronize()
+    tk = time.perf_counter()
+    eng.keys_reset()
+    first = eng.keys_add(reg_pks)
+    key_build_ms = (time.perf_counter() - tk) * 1e3
+    assert first == 0
+
+    def step_general():
         eng.verify_batch_device(d_sig, d_pk, d_msgs, d_off, n, d_words, stream=stream)
         if world > 1:
             dist.all_gather(gathered, d_words)
+
+    def step_keyed():
+        eng.verify_batch_keyed_device(d_sig, d_kreq, d_msgs, d_off, n, d_words, stream=stream)
+        if world > 1:
+            dist.all_gather(gathered, d_words)
+
+    step = step_keyed if args.path == "keyed" else step_general
 
     for _ in range(args.warmup):
         step()
@@ -177,11 +205,42 @@ def main():
     got = np.unpackbits(words.view(np.uint8), bitorder="little")[:n].astype(bool)
     mismatches = int((got != expect).sum())
 
+    # secondary: the other path on the same resident batch (same verdicts required)
+    other = None
+    if args.general_steps > 0:
+        ostep = step_general if args.path == "keyed" else step_keyed
+        ostep()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        o_ms = []
+        t1 = time.perf_counter()
+        for _ in range(args.general_steps):
+            ostep()
+            o_ms.append(eng.last_phase_ms())
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        o_el = time.perf_counter() - t1
+        if world > 1:
+            e = torch.tensor([o_el], dtype=torch.float64, device=dev)
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            o_el = float(e.item())
+        ow = d_words.cpu().numpy().view(np.uint64)
+        og = np.unpackbits(ow.view(np.uint8), bitorder="little")[:n].astype(bool)
+        other = {"path": "general" if args.path == "keyed" else "keyed",
+                 "value": n * world * args.general_steps / o_el,
+                 "phase_ms": {"hash": float(np.mean([x[0] for x in o_ms])), "table": float(np.mean([x[1] for x in o_ms])),
+                              "dsm_or_comb": float(np.mean([x[2] for x in o_ms]))},
+                 "same_verdicts": bool((og == got).all())}
+
     total = n * world * args.steps
     value = total / elapsed
     ms_per_step = elapsed / args.steps * 1e3
     dsm_avg = float(np.mean(dsm_ms))
-    achieved = n * RL.MAD_DSM_KERNEL / (dsm_avg * 1e-3) / 1e12
+    kernel_mad = RL.MAD_COMB_KERNEL if args.path == "keyed" else RL.MAD_DSM_KERNEL
+    kernel_name = "edv_comb_kernel" if args.path == "keyed" else "edv_dsm_kernel"
+    achieved = n * kernel_mad / (dsm_avg * 1e-3) / 1e12
     peak = RL.PEAK_MAD_PER_S / 1e12
     traffic = None
     tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -189,7 +248,7 @@ def main():
         with open(tpath) as f:
             tj = json.load(f)
         if tj.get("n") == n:
-            traffic = tj.get("edv_dsm_kernel_bytes")
+            traffic = tj.get(kernel_name + "_bytes")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -215,12 +274,16 @@ def main():
                                    "%d signers%s" % (1 if args.config == "c1" else 2, n, mlen_mean, args.signers,
                                                      ", 10% corrupted/non-canonical/small-order" if args.config == "c2" else ", all valid"),
                        "requests_per_gpu": n, "signers": args.signers, "parallelism": "dp%d (request-index shards)" % world},
-            "roofline": {"bound": "valu", "kernel": "edv_dsm_kernel", "achieved": achieved, "peak": peak,
+            "roofline": {"bound": "valu", "kernel": kernel_name, "achieved": achieved, "peak": peak,
                          "unit": "TMAD/s", "frac": achieved / peak, "traffic": traffic,
-                         "algorithmic": "%d MAD per verify ((2510 + 267) field ops x 100), n=%d per launch, "
-                                        "avg launch %.3f ms" % (RL.MAD_DSM_KERNEL, n, dsm_avg)},
-            "phase_ms": {"hash": float(np.mean(hash_ms)), "table": float(np.mean(table_ms)), "dsm": dsm_avg},
-            "whole_path_frac": (n * RL.MAD_PER_VERIFY / ((float(np.mean(hash_ms)) + float(np.mean(table_ms)) + dsm_avg) * 1e-3)) / RL.PEAK_MAD_PER_S,
+                         "algorithmic": "%d MAD per verify (%s), n=%d per launch, avg launch %.3f ms" % (
+                             kernel_mad, RL.KERNEL_WORK[kernel_name], n, dsm_avg)},
+            "path": args.path,
+            "phase_ms": {"hash": float(np.mean(hash_ms)), "table": float(np.mean(table_ms)),
+                         ("comb" if args.path == "keyed" else "dsm"): dsm_avg},
+            "key_table_build_ms": key_build_ms, "keys": int(reg_pks.shape[0]),
+            "ref10_equivalent_frac": (n * RL.MAD_PER_VERIFY / (ms_per_step * 1e-3)) / RL.PEAK_MAD_PER_S,
+            "other_path": other,
             "cpu_baseline": cpu,
             "parity": {"mismatches_vs_construction": mismatches, "accepted": int(got.sum()), "expected": int(expect.sum())},
         }

@@ -97,6 +97,28 @@ int edv_verify_batch_device(edv_ctx *ctx, const void *d_sig64, const void *d_pk3
 int edv_last_phase_ms(edv_ctx *ctx, double *hash_ms, double *table_ms, double *dsm_ms);
 double edv_last_kernel_ms(edv_ctx *ctx);
 
+/* ------------------------------------------------------ key-table path */
+
+/* Register public keys (the verkeys SimpleAuthNr.addIdr holds,
+ * plenum/server/client_authn.py:133-140).  For each key the library decodes
+ * -A once, records libsodium's key checks (canonical y, not small order, on
+ * the curve) and builds the fixed-base table (j+1) * 16^i * (-A), i < 64,
+ * j < 8, as affine niels points: 64 KiB per key in HBM (1M keys = 64 GiB).
+ * Key ids are consecutive from *first_id.  Host / device-pointer forms. */
+int edv_keys_add(edv_ctx *ctx, const uint8_t *pk32, uint64_t nkeys, uint64_t *first_id);
+int edv_keys_add_device(edv_ctx *ctx, const void *d_pk32, uint64_t nkeys, uint64_t *first_id, void *stream);
+uint64_t edv_keys_count(edv_ctx *ctx);
+/* Forget all registered keys (device memory is kept for reuse). */
+int edv_keys_reset(edv_ctx *ctx);
+
+/* Verify against registered keys: item i uses key id key_idx[i] (uint32);
+ * an id >= edv_keys_count() is rejected (never read out of bounds).
+ * Same verdicts as edv_verify_batch with pk32[i] = that key's encoding. */
+int edv_verify_batch_keyed(edv_ctx *ctx, const uint8_t *sig64, const uint32_t *key_idx, const uint8_t *msgs,
+                           const uint64_t *msg_off, uint64_t n, uint8_t *accept_bits);
+int edv_verify_batch_keyed_device(edv_ctx *ctx, const void *d_sig64, const void *d_key_idx, const void *d_msgs,
+                                  const void *d_msg_off, uint64_t n, void *d_accept_words, void *stream);
+
 /* ------------------------------------------------- signing (synthetic load) */
 
 /* crypto_sign_seed_keypair for n seeds (32 bytes each): pk32_out n*32,

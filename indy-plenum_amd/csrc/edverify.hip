@@ -172,6 +172,228 @@ __global__ __launch_bounds__(kBlock) void edv_dsm_kernel(const uint8_t* __restri
   if ((threadIdx.x & 63) == 0 && i < n) accept_words[i >> 6] = b;
 }
 
+
+// ---- key-table path ------------------------------------------------------
+// For a registered key, (j+1) * 16^i * (-A) is precomputed once as an affine
+// niels point (y+x, y-x, 2dxy), i = 0..63, j = 0..7: 512 entries of 128 B
+// (30 limbs + 2 pad words) = 64 KiB per key, resident in HBM.  [h](-A) + [S]B
+// is then a fixed-base comb over both tables: 128 mixed additions, no
+// doublings.  Key decode + validity (canonical, not small order, on curve) is
+// done once per key, exactly as libsodium does it per call.
+constexpr int kEntryWords = 32;
+constexpr int kKeyTabWords = 64 * 8 * kEntryWords;  // 16384 words = 64 KiB
+constexpr int kRowWords = 40;                        // p3 base point per row
+
+__device__ __forceinline__ void store_fe(uint32_t* p, const fe& f) {
+#pragma unroll
+  for (int l = 0; l < 10; ++l) p[l] = f.v[l];
+}
+__device__ __forceinline__ void load_fe(fe& f, const uint32_t* p) {
+#pragma unroll
+  for (int l = 0; l < 10; ++l) f.v[l] = p[l];
+}
+
+// One lane per key: decode -A, validity flag, the 64 row bases 16^i (-A).
+__global__ __launch_bounds__(kBlock) void edv_key_rows_kernel(const uint8_t* __restrict__ pk32, uint64_t nkeys,
+                                                             uint32_t* __restrict__ rows,
+                                                             uint8_t* __restrict__ valid) {
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nkeys) return;
+  uint32_t pk[8];
+  load_words(pk, pk32 + 32 * k, 8);
+  ge_p3 P;
+  const bool dec = ge_frombytes(P, pk, true);
+  valid[k] = (dec && is_canonical_point(pk) && !has_small_order(pk)) ? 1 : 0;
+  uint32_t* r = rows + k * 64 * kRowWords;
+#pragma unroll 1
+  for (int i = 0; i < 64; ++i) {
+    store_fe(r + i * kRowWords, P.X);
+    store_fe(r + i * kRowWords + 10, P.Y);
+    store_fe(r + i * kRowWords + 20, P.Z);
+    store_fe(r + i * kRowWords + 30, P.T);
+    ge_p2 q2;
+    ge_p1p1 t;
+    ge_p3_to_p2(q2, P);
+    ge_p2_dbl(t, q2);
+    ge_dbl_to_p2(q2, t);
+    ge_p2_dbl(t, q2);
+    ge_dbl_to_p2(q2, t);
+    ge_p2_dbl(t, q2);
+    ge_dbl_to_p2(q2, t);
+    ge_p2_dbl(t, q2);
+    ge_dbl_to_p3(P, t);
+  }
+}
+
+// Canonical limbs (fe_canon) so negation 2p - x stays within class C bounds.
+__device__ __forceinline__ void fe_store_canon(uint32_t* p, const fe& f) {
+  fe c = f;
+  fe_canon(c);
+  store_fe(p, c);
+}
+
+// One lane per (key, row): the 8 multiples of the row base, one shared
+// inversion (Montgomery's trick), affine niels into the table.
+__global__ __launch_bounds__(kBlock) void edv_key_fill_kernel(const uint32_t* __restrict__ rows, uint64_t nrows,
+                                                             uint32_t* __restrict__ tab, uint32_t* __restrict__ pre) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // key * 64 + i
+  if (r >= nrows) return;
+  const uint32_t* b = rows + r * kRowWords;
+  uint32_t* e = tab + r * 8 * kEntryWords;
+  uint32_t* pr = pre + r * 8 * 10;
+  ge_p3 base, m;
+  load_fe(base.X, b);
+  load_fe(base.Y, b + 10);
+  load_fe(base.Z, b + 20);
+  load_fe(base.T, b + 30);
+  ge_cached cb;
+  ge_p3_to_cached(cb, base);
+  m = base;
+  fe acc;
+#pragma unroll 1
+  for (int j = 0; j < 8; ++j) {
+    if (j > 0) {
+      ge_p1p1 t;
+      ge_add(t, m, cb);
+      ge_p1p1_to_p3_addlike(m, t);
+    }
+    store_fe(e + j * kEntryWords, m.X);
+    store_fe(e + j * kEntryWords + 10, m.Y);
+    store_fe(e + j * kEntryWords + 20, m.Z);
+    if (j == 0)
+      acc = m.Z;
+    else
+      fe_mul(acc, acc, m.Z);
+    store_fe(pr + j * 10, acc);
+  }
+  fe inv;
+  fe_invert(inv, acc);
+#pragma unroll 1
+  for (int j = 7; j >= 0; --j) {
+    fe zinv, X, Y, Z, x, y, t;
+    load_fe(X, e + j * kEntryWords);
+    load_fe(Y, e + j * kEntryWords + 10);
+    load_fe(Z, e + j * kEntryWords + 20);
+    if (j > 0) {
+      fe p;
+      load_fe(p, pr + (j - 1) * 10);
+      fe_mul(zinv, inv, p);
+      fe_mul(inv, inv, Z);
+    } else {
+      zinv = inv;
+    }
+    fe_mul(x, X, zinv);
+    fe_mul(y, Y, zinv);
+    fe_add(t, y, x);
+    fe_store_canon(e + j * kEntryWords, t);
+    fe_sub(t, y, x);
+    fe_store_canon(e + j * kEntryWords + 10, t);
+    fe_mul(t, x, y);
+    fe_mul(t, t, fe_const_d2());
+    fe_store_canon(e + j * kEntryWords + 20, t);
+    e[j * kEntryWords + 30] = 0;
+    e[j * kEntryWords + 31] = 0;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void edv_hash_keyed_kernel(const uint8_t* __restrict__ sig64,
+                                                               const uint32_t* __restrict__ key_idx,
+                                                               uint32_t key_count,
+                                                               const uint8_t* __restrict__ key_pk,
+                                                               const uint8_t* __restrict__ msgs,
+                                                               const uint64_t* __restrict__ msg_off, uint64_t n,
+                                                               uint32_t* __restrict__ h_soa,
+                                                               uint8_t* __restrict__ flags, uint64_t stride) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t sig[16], pk[8], h[8];
+  load_words(sig, sig64 + 64 * i, 16);
+  const uint32_t key = key_idx[i];
+  const bool in_range = key < key_count;  // out-of-range ids reject, never read out of bounds
+  load_words(pk, key_pk + 32 * (uint64_t)(in_range ? key : 0), 8);
+  const uint64_t o0 = msg_off[i], o1 = msg_off[i + 1];
+  const bool ok = verify_phase_hash(h, sig, pk, msgs + o0, o1 - o0) && in_range;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) h_soa[k * stride + i] = h[k];
+  flags[i] = ok ? 1 : 0;
+}
+
+__device__ __forceinline__ void load_niels(ge_niels& nb, const uint32_t* __restrict__ p) {
+  const uint4* q = (const uint4*)p;
+  uint32_t w[32];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint4 v = q[k];
+    w[4 * k] = v.x;
+    w[4 * k + 1] = v.y;
+    w[4 * k + 2] = v.z;
+    w[4 * k + 3] = v.w;
+  }
+#pragma unroll
+  for (int l = 0; l < 10; ++l) {
+    nb.ypx.v[l] = w[l];
+    nb.ymx.v[l] = w[10 + l];
+    nb.xy2d.v[l] = w[20 + l];
+  }
+}
+
+// Q += digit * T[row] for signed digit in [-8, 7] (0 adds the identity).
+__device__ __forceinline__ void comb_step(ge_p3& Q, int e, const uint32_t* __restrict__ row) {
+  const int m = e < 0 ? -e : e;
+  ge_niels nb;
+  ge_niels_0(nb);
+  if (m != 0) load_niels(nb, row + (m - 1) * kEntryWords);
+  if (e < 0) {
+    fe tmp = nb.ypx;
+    nb.ypx = nb.ymx;
+    nb.ymx = tmp;
+    fe_neg(nb.xy2d, nb.xy2d);
+  }
+  ge_p1p1 t;
+  ge_madd(t, Q, nb);
+  ge_p1p1_to_p3_addlike(Q, t);
+}
+
+__global__ __launch_bounds__(kBlock) void edv_comb_kernel(const uint8_t* __restrict__ sig64,
+                                                         const uint32_t* __restrict__ key_idx, uint32_t key_count,
+                                                         uint64_t n, const uint32_t* __restrict__ h_soa,
+                                                         const uint8_t* __restrict__ flags,
+                                                         const uint8_t* __restrict__ key_valid,
+                                                         const uint32_t* __restrict__ key_tab,
+                                                         const uint32_t* __restrict__ btab,
+                                                         unsigned long long* __restrict__ accept_words, uint64_t stride) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool ok = false;
+  if (i < n) {
+    uint32_t sig[16], h[8], hy[8], sy[8];
+    load_words(sig, sig64 + 64 * i, 16);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) h[k] = h_soa[k * stride + i];
+    const uint32_t key0 = key_idx[i];
+    const uint32_t key = key0 < key_count ? key0 : 0;  // flags[i] is 0 for an out-of-range id
+    const uint32_t* at = key_tab + (uint64_t)key * kKeyTabWords;
+    sc_recode16(hy, h);
+    sc_recode16(sy, sig + 8);
+    ge_p3 Q;
+    ge_p3_0(Q);
+#pragma unroll 1
+    for (int r = 0; r < 64; ++r) {
+      comb_step(Q, recode_digit(hy, r), at + r * 8 * kEntryWords);
+      comb_step(Q, recode_digit(sy, r), btab + r * 8 * kEntryWords);
+    }
+    ge_p2 r2;
+    ge_p3_to_p2(r2, Q);
+    uint32_t rcheck[8];
+    ge_tobytes(rcheck, r2);
+    bool eq = true;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) eq = eq && rcheck[k] == sig[k];
+    ok = eq && flags[i] && key_valid[key];
+  }
+  const unsigned long long b = __ballot(ok);
+  if ((threadIdx.x & 63) == 0 && i < n) accept_words[i >> 6] = b;
+}
+
 // Fixed-base comb: [x]B with x < 2^253, 64 madds over BASE_COMB (global).
 __device__ void ge_scalarmult_base(ge_p3& Q, const uint32_t x[8], const uint32_t* __restrict__ comb) {
   uint32_t y[8];
@@ -327,6 +549,12 @@ struct edv_ctx {
   uint64_t scratch_lanes = 0;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // hash | table | dsm boundaries
   bool timed = false;
+  // key-table store (registered public keys)
+  uint32_t* d_btab_comb32 = nullptr;  // B comb table in the 128-B entry format
+  uint8_t* d_key_pk = nullptr;
+  uint8_t* d_key_valid = nullptr;
+  uint32_t* d_key_tab = nullptr;
+  uint64_t key_count = 0, key_cap = 0;
   // staging buffers for host-pointer calls
   struct Buf {
     void* p = nullptr;
@@ -389,6 +617,176 @@ int launch_verify(edv_ctx* ctx, const void* d_sig, const void* d_pk, const void*
 
 }  // namespace
 
+
+// ------------------------------------------------------------- key tables
+
+static int keys_reserve(edv_ctx* ctx, uint64_t need) {
+  if (need <= ctx->key_cap) return 0;
+  uint64_t cap = ctx->key_cap ? ctx->key_cap : 1024;
+  while (cap < need) cap *= 2;
+  uint8_t *pk = nullptr, *valid = nullptr;
+  uint32_t* tab = nullptr;
+  hipError_t e;
+  if ((e = hipMalloc(&pk, cap * 32)) || (e = hipMalloc(&valid, cap)) ||
+      (e = hipMalloc(&tab, cap * (uint64_t)kKeyTabWords * 4))) {
+    if (pk) (void)hipFree(pk);
+    if (valid) (void)hipFree(valid);
+    if (tab) (void)hipFree(tab);
+    return set_err(EDV_ENOMEM, "key store of %llu keys: %s", (unsigned long long)cap, hipGetErrorString(e));
+  }
+  if (ctx->key_count) {
+    HIP_TRY(hipMemcpyAsync(pk, ctx->d_key_pk, ctx->key_count * 32, hipMemcpyDeviceToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(valid, ctx->d_key_valid, ctx->key_count, hipMemcpyDeviceToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(tab, ctx->d_key_tab, ctx->key_count * (uint64_t)kKeyTabWords * 4,
+                           hipMemcpyDeviceToDevice, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+  }
+  if (ctx->d_key_pk) (void)hipFree(ctx->d_key_pk);
+  if (ctx->d_key_valid) (void)hipFree(ctx->d_key_valid);
+  if (ctx->d_key_tab) (void)hipFree(ctx->d_key_tab);
+  ctx->d_key_pk = pk;
+  ctx->d_key_valid = valid;
+  ctx->d_key_tab = tab;
+  ctx->key_cap = cap;
+  return 0;
+}
+
+// Build tables for keys [first, first + nkeys) whose 32-byte encodings are
+// already in d_key_pk.
+static int keys_build(edv_ctx* ctx, uint64_t first, uint64_t nkeys, hipStream_t st) {
+  if (!nkeys) return 0;
+  int r;
+  // rows: 64 p3 bases per key; pre: 8 prefix products per row
+  if ((r = ensure(ctx->b_aux, nkeys * 64 * kRowWords * 4 + nkeys * 64 * 80 * 4))) return r;
+  uint32_t* rows = (uint32_t*)ctx->b_aux.p;
+  uint32_t* pre = rows + nkeys * 64 * kRowWords;
+  hipLaunchKernelGGL(edv_key_rows_kernel, dim3((uint32_t)div_up(nkeys, kBlock)), dim3(kBlock), 0, st,
+                     ctx->d_key_pk + 32 * first, nkeys, rows, ctx->d_key_valid + first);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(edv_key_fill_kernel, dim3((uint32_t)div_up(nkeys * 64, kBlock)), dim3(kBlock), 0, st, rows,
+                     nkeys * 64, ctx->d_key_tab + first * (uint64_t)kKeyTabWords, pre);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+static int launch_verify_keyed(edv_ctx* ctx, const void* d_sig, const void* d_kidx, const void* d_msgs,
+                               const void* d_off, uint64_t n, void* d_words, hipStream_t st) {
+  if (n == 0) return 0;
+  if (ctx->key_count == 0) return set_err(EDV_EINVAL, "no registered keys");
+  const uint8_t* sig = (const uint8_t*)d_sig;
+  const uint32_t* kidx = (const uint32_t*)d_kidx;
+  const uint64_t* off = (const uint64_t*)d_off;
+  unsigned long long* words = (unsigned long long*)d_words;
+  const uint64_t chunk = ctx->scratch_lanes;
+  const uint32_t kc = (uint32_t)ctx->key_count;
+  HIP_TRY(hipEventRecord(ctx->ev[0], st));
+  for (uint64_t c0 = 0; c0 < n; c0 += chunk) {
+    const uint64_t cn = (n - c0) < chunk ? (n - c0) : chunk;
+    const uint32_t grid = (uint32_t)div_up(cn, kBlock);
+    const bool last = c0 + cn >= n;
+    hipLaunchKernelGGL(edv_hash_keyed_kernel, dim3(grid), dim3(kBlock), 0, st, sig + 64 * c0, kidx + c0, kc,
+                       ctx->d_key_pk, (const uint8_t*)d_msgs, off + c0, cn, ctx->d_hsoa, ctx->d_flags, chunk);
+    HIP_TRY(hipGetLastError());
+    if (last) {
+      HIP_TRY(hipEventRecord(ctx->ev[1], st));
+      HIP_TRY(hipEventRecord(ctx->ev[2], st));
+    }
+    hipLaunchKernelGGL(edv_comb_kernel, dim3(grid), dim3(kBlock), 0, st, sig + 64 * c0, kidx + c0, kc, cn,
+                       ctx->d_hsoa, ctx->d_flags, ctx->d_key_valid, ctx->d_key_tab, ctx->d_btab_comb32,
+                       words + c0 / 64, chunk);
+    HIP_TRY(hipGetLastError());
+  }
+  HIP_TRY(hipEventRecord(ctx->ev[3], st));
+  ctx->timed = true;
+  return 0;
+}
+
+extern "C" {
+
+int edv_keys_add(edv_ctx* ctx, const uint8_t* pk32, uint64_t nkeys, uint64_t* first_id) {
+  int r = set_device(ctx);
+  if (r) return r;
+  if (nkeys && !pk32) return set_err(EDV_EINVAL, "null pk32");
+  if (ctx->key_count + nkeys > 0xffffffffull) return set_err(EDV_EINVAL, "too many keys");
+  if ((r = keys_reserve(ctx, ctx->key_count + nkeys))) return r;
+  const uint64_t first = ctx->key_count;
+  if (nkeys) {
+    HIP_TRY(hipMemcpyAsync(ctx->d_key_pk + 32 * first, pk32, 32 * nkeys, hipMemcpyHostToDevice, ctx->stream));
+    if ((r = keys_build(ctx, first, nkeys, ctx->stream))) return r;
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+  }
+  ctx->key_count += nkeys;
+  if (first_id) *first_id = first;
+  return 0;
+}
+
+int edv_keys_add_device(edv_ctx* ctx, const void* d_pk32, uint64_t nkeys, uint64_t* first_id, void* stream) {
+  int r = set_device(ctx);
+  if (r) return r;
+  if (nkeys && !d_pk32) return set_err(EDV_EINVAL, "null d_pk32");
+  if (ctx->key_count + nkeys > 0xffffffffull) return set_err(EDV_EINVAL, "too many keys");
+  if ((r = keys_reserve(ctx, ctx->key_count + nkeys))) return r;
+  const uint64_t first = ctx->key_count;
+  hipStream_t st = pick_stream(ctx, stream);
+  if (nkeys) {
+    HIP_TRY(hipMemcpyAsync(ctx->d_key_pk + 32 * first, d_pk32, 32 * nkeys, hipMemcpyDeviceToDevice, st));
+    if ((r = keys_build(ctx, first, nkeys, st))) return r;
+  }
+  ctx->key_count += nkeys;
+  if (first_id) *first_id = first;
+  return 0;
+}
+
+uint64_t edv_keys_count(edv_ctx* ctx) { return ctx ? ctx->key_count : 0; }
+
+int edv_keys_reset(edv_ctx* ctx) {
+  if (!ctx) return set_err(EDV_EINVAL, "null context");
+  ctx->key_count = 0;
+  return 0;
+}
+
+int edv_verify_batch_keyed_device(edv_ctx* ctx, const void* d_sig64, const void* d_key_idx, const void* d_msgs,
+                                  const void* d_msg_off, uint64_t n, void* d_accept_words, void* stream) {
+  int r = set_device(ctx);
+  if (r) return r;
+  if (n && (!d_sig64 || !d_key_idx || !d_msgs || !d_msg_off || !d_accept_words))
+    return set_err(EDV_EINVAL, "null device pointer");
+  return launch_verify_keyed(ctx, d_sig64, d_key_idx, d_msgs, d_msg_off, n, d_accept_words, pick_stream(ctx, stream));
+}
+
+int edv_verify_batch_keyed(edv_ctx* ctx, const uint8_t* sig64, const uint32_t* key_idx, const uint8_t* msgs,
+                           const uint64_t* msg_off, uint64_t n, uint8_t* accept_bits) {
+  int r = set_device(ctx);
+  if (r) return r;
+  if (n == 0) return 0;
+  if (!sig64 || !key_idx || !msg_off || !accept_bits) return set_err(EDV_EINVAL, "null pointer");
+  for (uint64_t i = 0; i < n; ++i)
+    if (msg_off[i + 1] < msg_off[i]) return set_err(EDV_EINVAL, "msg_off[%llu] decreasing", (unsigned long long)i);
+  const uint64_t m0 = msg_off[0], mbytes = msg_off[n] - m0;
+  if (mbytes && !msgs) return set_err(EDV_EINVAL, "null msgs");
+  const uint64_t nwords = div_up(n, 64);
+  if ((r = ensure(ctx->b_sig, 64 * n)) || (r = ensure(ctx->b_pk, 4 * n)) || (r = ensure(ctx->b_msg, mbytes + 16)) ||
+      (r = ensure(ctx->b_off, 8 * (n + 1))) || (r = ensure(ctx->b_bits, 8 * nwords)))
+    return r;
+  hipStream_t st = ctx->stream;
+  std::vector<uint64_t> off(n + 1);
+  for (uint64_t i = 0; i <= n; ++i) off[i] = msg_off[i] - m0;
+  HIP_TRY(hipMemcpyAsync(ctx->b_sig.p, sig64, 64 * n, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(ctx->b_pk.p, key_idx, 4 * n, hipMemcpyHostToDevice, st));
+  if (mbytes) HIP_TRY(hipMemcpyAsync(ctx->b_msg.p, msgs + m0, mbytes, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(ctx->b_off.p, off.data(), 8 * (n + 1), hipMemcpyHostToDevice, st));
+  if ((r = launch_verify_keyed(ctx, ctx->b_sig.p, ctx->b_pk.p, ctx->b_msg.p, ctx->b_off.p, n, ctx->b_bits.p, st)))
+    return r;
+  std::vector<uint64_t> words(nwords);
+  HIP_TRY(hipMemcpyAsync(words.data(), ctx->b_bits.p, 8 * nwords, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  memcpy(accept_bits, words.data(), (n + 7) / 8);
+  if (n & 7) accept_bits[n / 8] &= (uint8_t)((1u << (n & 7)) - 1);
+  return 0;
+}
+
+}  // extern "C"
+
 extern "C" {
 
 const char* edv_version(void) { return EDV_VERSION; }
@@ -431,6 +829,14 @@ edv_ctx* edv_create(int device) {
     return fail("hipMemcpy", e);
   if ((e = hipMemcpy(ctx->d_btab_comb, BASE_COMB_U32, sizeof(BASE_COMB_U32), hipMemcpyHostToDevice)) != hipSuccess)
     return fail("hipMemcpy", e);
+  {
+    std::vector<uint32_t> b32((sizeof(BASE_COMB_U32) / 4 / 30) * kEntryWords, 0u);
+    for (size_t e = 0; e < sizeof(BASE_COMB_U32) / 4 / 30; ++e)
+      memcpy(&b32[e * kEntryWords], &BASE_COMB_U32[e * 30], 30 * 4);
+    if ((e = hipMalloc(&ctx->d_btab_comb32, b32.size() * 4)) != hipSuccess) return fail("hipMalloc", e);
+    if ((e = hipMemcpy(ctx->d_btab_comb32, b32.data(), b32.size() * 4, hipMemcpyHostToDevice)) != hipSuccess)
+      return fail("hipMemcpy", e);
+  }
   ctx->scratch_lanes = kMaxLanes;
   if ((e = hipMalloc(&ctx->d_scratch, ctx->scratch_lanes / kBlock * (uint64_t)kRegionBytes)) != hipSuccess)
     return fail("hipMalloc(scratch)", e);
@@ -451,6 +857,10 @@ void edv_destroy(edv_ctx* ctx) {
   if (ctx->d_flags) (void)hipFree(ctx->d_flags);
   if (ctx->d_btab_small) (void)hipFree(ctx->d_btab_small);
   if (ctx->d_btab_comb) (void)hipFree(ctx->d_btab_comb);
+  if (ctx->d_btab_comb32) (void)hipFree(ctx->d_btab_comb32);
+  if (ctx->d_key_pk) (void)hipFree(ctx->d_key_pk);
+  if (ctx->d_key_valid) (void)hipFree(ctx->d_key_valid);
+  if (ctx->d_key_tab) (void)hipFree(ctx->d_key_tab);
   for (int k = 0; k < 4; ++k)
     if (ctx->ev[k]) (void)hipEventDestroy(ctx->ev[k]);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);

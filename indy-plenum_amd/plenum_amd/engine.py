@@ -158,6 +158,49 @@ class EdVerifyEngine:
         check(self._lib.edv_last_phase_ms(self._ctx, ctypes.byref(h), ctypes.byref(t), ctypes.byref(d)))
         return h.value, t.value, d.value
 
+    # ------------------------------------------------------------ key tables
+    def keys_add(self, pk32):
+        """Register public keys (64 KiB fixed-base table each); returns the
+        first key id (ids are consecutive)."""
+        pk32 = _u8(pk32, 32)
+        first = ctypes.c_uint64()
+        check(self._lib.edv_keys_add(self._ctx, _ptr(pk32), pk32.shape[0], ctypes.byref(first)))
+        return first.value
+
+    def keys_add_device(self, d_pk32, nkeys, stream=None):
+        first = ctypes.c_uint64()
+        check(self._lib.edv_keys_add_device(self._ctx, _dev(d_pk32), nkeys, ctypes.byref(first),
+                                            _stream_for(stream, d_pk32)))
+        return first.value
+
+    def keys_count(self):
+        return int(self._lib.edv_keys_count(self._ctx))
+
+    def keys_reset(self):
+        check(self._lib.edv_keys_reset(self._ctx))
+
+    def verify_batch_keyed(self, sig64, key_idx, msgs, msg_off):
+        """Verdicts against registered key ids (same predicate as verify_batch)."""
+        sig64 = _u8(sig64, 64)
+        key_idx = np.ascontiguousarray(key_idx, dtype=np.uint32)
+        msgs = _u8(msgs)
+        msg_off = np.ascontiguousarray(msg_off, dtype=np.uint64)
+        n = sig64.shape[0]
+        if key_idx.shape[0] != n or msg_off.shape[0] != n + 1:
+            raise ValueError("shape mismatch")
+        if n and int(msg_off[-1]) > msgs.shape[0]:
+            raise ValueError("msg_off exceeds message buffer")
+        bits = np.zeros((n + 7) // 8, dtype=np.uint8)
+        if n:
+            check(self._lib.edv_verify_batch_keyed(self._ctx, _ptr(sig64), _ptr(key_idx),
+                                                   _ptr(msgs) if msgs.size else None, _ptr(msg_off), n, _ptr(bits)))
+        return unpack_bits(bits, n)
+
+    def verify_batch_keyed_device(self, d_sig64, d_key_idx, d_msgs, d_msg_off, n, d_accept_words, stream=None):
+        st = _stream_for(stream, d_sig64, d_accept_words)
+        check(self._lib.edv_verify_batch_keyed_device(self._ctx, _dev(d_sig64), _dev(d_key_idx), _dev(d_msgs),
+                                                      _dev(d_msg_off), n, _dev(d_accept_words), st))
+
     # ------------------------------------------------------------------ sign
     def seed_keypair_batch(self, seeds32):
         seeds32 = _u8(seeds32, 32)

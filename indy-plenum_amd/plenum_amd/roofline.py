@@ -21,6 +21,14 @@ FE_ENCODE = 267
 MAD_PER_VERIFY = 305_000
 MAD_DSM_KERNEL = (FE_DSM + FE_ENCODE) * MAD_PER_FE  # 277,700
 MAD_TABLE_KERNEL = FE_DECODE * MAD_PER_FE
+# Key-table path (keys registered once): edv_comb_kernel = fixed-base comb over
+# both tables, 128 mixed additions x 7 multiplications + the encode inversion.
+FE_COMB = 128 * 7
+MAD_COMB_KERNEL = (FE_COMB + FE_ENCODE) * MAD_PER_FE  # 116,300
+KERNEL_WORK = {
+    "edv_dsm_kernel": "(2510 DSM + 267 encode) field ops x 100, ref10 a-priori count",
+    "edv_comb_kernel": "(128 mixed adds x 7 + 267 encode) field ops x 100, fixed-base comb over both tables",
+}
 SHA_ALU_PER_BLOCK = 5_000
 
 CUS = 256

@@ -132,3 +132,32 @@ def test_large_batch_properties(gpu_engine):
     wrong = np.nonzero(bits != want)[0]
     assert len(wrong) == 0, (len(wrong), wrong[:8], wrong[-8:], bits[wrong[:8]])
     assert digests[0] == digests[1]
+
+
+# ---- key-table path -------------------------------------------------------
+def test_keyed_golden_and_edge(gpu_engine):
+    """Every golden item through the key-table path (each item's pk registered
+    as its own key): same verdicts as libsodium, including small-order,
+    non-canonical and off-curve keys, and mixed-order keys."""
+    for name in ("ed25519_edge.npz", "ed25519_valid.npz"):
+        d = load_npz(name)
+        gpu_engine.keys_reset()
+        first = gpu_engine.keys_add(d["pk"])
+        kidx = np.arange(first, first + len(d["pk"]), dtype=np.uint32)
+        got = gpu_engine.verify_batch_keyed(d["sig"], kidx, d["msgs"], d["off"])
+        assert (got == d["expect"].astype(bool)).all(), np.nonzero(got != d["expect"].astype(bool))
+
+
+def test_keyed_random_vs_oracle_and_out_of_range(gpu_engine, oracle):
+    n = 2049
+    sig, pks, msgs, buf, off = _random_batch(gpu_engine, n, 9)
+    gpu_engine.keys_reset()
+    uniq, inv = np.unique(pks, axis=0, return_inverse=True)
+    first = gpu_engine.keys_add(uniq)
+    kidx = (inv.reshape(-1) + first).astype(np.uint32)
+    got = gpu_engine.verify_batch_keyed(sig, kidx, buf, off)
+    want = gpu_engine.verify_batch(sig, pks, buf, off)
+    assert (got == want).all()
+    kidx[::5] = gpu_engine.keys_count() + 7  # unregistered ids reject
+    got = gpu_engine.verify_batch_keyed(sig, kidx, buf, off)
+    assert not got[::5].any() and (got[1::5] == want[1::5]).all()
