@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "../../include/edverify.h"
+#include "comb.h"
 #include "verify_core.h"
 
 using namespace edv;
@@ -173,27 +174,18 @@ __global__ __launch_bounds__(kBlock) void edv_dsm_kernel(const uint8_t* __restri
 }
 
 
-// ---- key-table path ------------------------------------------------------
-// For a registered key, (j+1) * 16^i * (-A) is precomputed once as an affine
-// niels point (y+x, y-x, 2dxy), i = 0..63, j = 0..7: 512 entries of 128 B
-// (30 limbs + 2 pad words) = 64 KiB per key, resident in HBM.  [h](-A) + [S]B
-// is then a fixed-base comb over both tables: 128 mixed additions, no
-// doublings.  Key decode + validity (canonical, not small order, on curve) is
-// done once per key, exactly as libsodium does it per call.
-constexpr int kEntryWords = 32;
-constexpr int kKeyTabWords = 64 * 8 * kEntryWords;  // 16384 words = 64 KiB
-constexpr int kRowWords = 40;                        // p3 base point per row
+// ---- key-table path (comb.h) ---------------------------------------------
+// Registered keys: W = 4 comb tables (64 KiB each).  Base point: W = 8 comb
+// table (512 KiB) built once per context by the same kernels.
+#ifndef EDV_COMB_MIN_WAVES
+#define EDV_COMB_MIN_WAVES 3  // 168 VGPRs, 3 waves/SIMD: 2% faster than 2 (tools/ab_keyed.py)
+#endif
+constexpr int kKeyW = 4, kBaseW = 8;
+constexpr int kKeyTabWords = Window<kKeyW>::kTableWords;   // 16384 words
+constexpr int kBaseTabWords = Window<kBaseW>::kTableWords; // 131072 words
+constexpr int kRowWords = 40;
 
-__device__ __forceinline__ void store_fe(uint32_t* p, const fe& f) {
-#pragma unroll
-  for (int l = 0; l < 10; ++l) p[l] = f.v[l];
-}
-__device__ __forceinline__ void load_fe(fe& f, const uint32_t* p) {
-#pragma unroll
-  for (int l = 0; l < 10; ++l) f.v[l] = p[l];
-}
-
-// One lane per key: decode -A, validity flag, the 64 row bases 16^i (-A).
+// One lane per key: decode -A, libsodium's key checks, the 64 row bases.
 __global__ __launch_bounds__(kBlock) void edv_key_rows_kernel(const uint8_t* __restrict__ pk32, uint64_t nkeys,
                                                              uint32_t* __restrict__ rows,
                                                              uint8_t* __restrict__ valid) {
@@ -204,99 +196,42 @@ __global__ __launch_bounds__(kBlock) void edv_key_rows_kernel(const uint8_t* __r
   ge_p3 P;
   const bool dec = ge_frombytes(P, pk, true);
   valid[k] = (dec && is_canonical_point(pk) && !has_small_order(pk)) ? 1 : 0;
-  uint32_t* r = rows + k * 64 * kRowWords;
-#pragma unroll 1
-  for (int i = 0; i < 64; ++i) {
-    store_fe(r + i * kRowWords, P.X);
-    store_fe(r + i * kRowWords + 10, P.Y);
-    store_fe(r + i * kRowWords + 20, P.Z);
-    store_fe(r + i * kRowWords + 30, P.T);
-    ge_p2 q2;
-    ge_p1p1 t;
-    ge_p3_to_p2(q2, P);
-    ge_p2_dbl(t, q2);
-    ge_dbl_to_p2(q2, t);
-    ge_p2_dbl(t, q2);
-    ge_dbl_to_p2(q2, t);
-    ge_p2_dbl(t, q2);
-    ge_dbl_to_p2(q2, t);
-    ge_p2_dbl(t, q2);
-    ge_dbl_to_p3(P, t);
-  }
+  comb_rows<kKeyW>(rows + k * Window<kKeyW>::kRows * kRowWords, P);
 }
 
-// Canonical limbs (fe_canon) so negation 2p - x stays within class C bounds.
-__device__ __forceinline__ void fe_store_canon(uint32_t* p, const fe& f) {
-  fe c = f;
-  fe_canon(c);
-  store_fe(p, c);
-}
-
-// One lane per (key, row): the 8 multiples of the row base, one shared
-// inversion (Montgomery's trick), affine niels into the table.
+// One lane per (key, row).
 __global__ __launch_bounds__(kBlock) void edv_key_fill_kernel(const uint32_t* __restrict__ rows, uint64_t nrows,
                                                              uint32_t* __restrict__ tab, uint32_t* __restrict__ pre) {
-  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // key * 64 + i
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= nrows) return;
-  const uint32_t* b = rows + r * kRowWords;
-  uint32_t* e = tab + r * 8 * kEntryWords;
-  uint32_t* pr = pre + r * 8 * 10;
-  ge_p3 base, m;
-  load_fe(base.X, b);
-  load_fe(base.Y, b + 10);
-  load_fe(base.Z, b + 20);
-  load_fe(base.T, b + 30);
-  ge_cached cb;
-  ge_p3_to_cached(cb, base);
-  m = base;
-  fe acc;
-#pragma unroll 1
-  for (int j = 0; j < 8; ++j) {
-    if (j > 0) {
-      ge_p1p1 t;
-      ge_add(t, m, cb);
-      ge_p1p1_to_p3_addlike(m, t);
-    }
-    store_fe(e + j * kEntryWords, m.X);
-    store_fe(e + j * kEntryWords + 10, m.Y);
-    store_fe(e + j * kEntryWords + 20, m.Z);
-    if (j == 0)
-      acc = m.Z;
-    else
-      fe_mul(acc, acc, m.Z);
-    store_fe(pr + j * 10, acc);
-  }
-  fe inv;
-  fe_invert(inv, acc);
-#pragma unroll 1
-  for (int j = 7; j >= 0; --j) {
-    fe zinv, X, Y, Z, x, y, t;
-    load_fe(X, e + j * kEntryWords);
-    load_fe(Y, e + j * kEntryWords + 10);
-    load_fe(Z, e + j * kEntryWords + 20);
-    if (j > 0) {
-      fe p;
-      load_fe(p, pr + (j - 1) * 10);
-      fe_mul(zinv, inv, p);
-      fe_mul(inv, inv, Z);
-    } else {
-      zinv = inv;
-    }
-    fe_mul(x, X, zinv);
-    fe_mul(y, Y, zinv);
-    fe_add(t, y, x);
-    fe_store_canon(e + j * kEntryWords, t);
-    fe_sub(t, y, x);
-    fe_store_canon(e + j * kEntryWords + 10, t);
-    fe_mul(t, x, y);
-    fe_mul(t, t, fe_const_d2());
-    fe_store_canon(e + j * kEntryWords + 20, t);
-    e[j * kEntryWords + 30] = 0;
-    e[j * kEntryWords + 31] = 0;
-  }
+  constexpr int E = Window<kKeyW>::kEntries;
+  comb_fill_row<kKeyW>(tab + r * E * kEntryWords, pre + r * E * 10, rows + r * kRowWords);
 }
 
-__global__ __launch_bounds__(kBlock) void edv_hash_keyed_kernel(const uint8_t* __restrict__ sig64,
+// Base-point table: one lane decodes B and writes its 32 row bases ...
+__global__ void edv_base_rows_kernel(uint32_t* __restrict__ rows) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  uint32_t b[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) b[k] = 0x66666666u;
+  b[0] = 0x66666658u;  // B = (x, 4/5), x even
+  ge_p3 P;
+  ge_frombytes(P, b, false);
+  comb_rows<kBaseW>(rows, P);
+}
+// ... then one lane per row fills its 128 entries.
+__global__ void edv_base_fill_kernel(const uint32_t* __restrict__ rows, uint32_t* __restrict__ tab,
+                                     uint32_t* __restrict__ pre) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= Window<kBaseW>::kRows) return;
+  constexpr int E = Window<kBaseW>::kEntries;
+  comb_fill_row<kBaseW>(tab + (uint64_t)r * E * kEntryWords, pre + (uint64_t)r * E * 10, rows + r * kRowWords);
+}
+
+#ifndef EDV_HASH_MIN_WAVES
+#define EDV_HASH_MIN_WAVES 3  // 0.71 vs 0.84 ms per 1M at 2 (tools/ab_keyed.py), despite an 88-B spill
+#endif
+__global__ __launch_bounds__(kBlock, EDV_HASH_MIN_WAVES) void edv_hash_keyed_kernel(const uint8_t* __restrict__ sig64,
                                                                const uint32_t* __restrict__ key_idx,
                                                                uint32_t key_count,
                                                                const uint8_t* __restrict__ key_pk,
@@ -354,7 +289,7 @@ __device__ __forceinline__ void comb_step(ge_p3& Q, int e, const uint32_t* __res
   ge_p1p1_to_p3_addlike(Q, t);
 }
 
-__global__ __launch_bounds__(kBlock) void edv_comb_kernel(const uint8_t* __restrict__ sig64,
+__global__ __launch_bounds__(kBlock, EDV_COMB_MIN_WAVES) void edv_comb_kernel(const uint8_t* __restrict__ sig64,
                                                          const uint32_t* __restrict__ key_idx, uint32_t key_count,
                                                          uint64_t n, const uint32_t* __restrict__ h_soa,
                                                          const uint8_t* __restrict__ flags,
@@ -372,15 +307,15 @@ __global__ __launch_bounds__(kBlock) void edv_comb_kernel(const uint8_t* __restr
     const uint32_t key0 = key_idx[i];
     const uint32_t key = key0 < key_count ? key0 : 0;  // flags[i] is 0 for an out-of-range id
     const uint32_t* at = key_tab + (uint64_t)key * kKeyTabWords;
-    sc_recode16(hy, h);
-    sc_recode16(sy, sig + 8);
+    comb_recode<kKeyW>(hy, h);
+    comb_recode<kBaseW>(sy, sig + 8);
     ge_p3 Q;
     ge_p3_0(Q);
+    constexpr int EA = Window<kKeyW>::kEntries, EB = Window<kBaseW>::kEntries;
 #pragma unroll 1
-    for (int r = 0; r < 64; ++r) {
-      comb_step(Q, recode_digit(hy, r), at + r * 8 * kEntryWords);
-      comb_step(Q, recode_digit(sy, r), btab + r * 8 * kEntryWords);
-    }
+    for (int r = 0; r < Window<kKeyW>::kRows; ++r) comb_step(Q, comb_digit<kKeyW>(hy, r), at + r * EA * kEntryWords);
+#pragma unroll 1
+    for (int r = 0; r < Window<kBaseW>::kRows; ++r) comb_step(Q, comb_digit<kBaseW>(sy, r), btab + r * EB * kEntryWords);
     ge_p2 r2;
     ge_p3_to_p2(r2, Q);
     uint32_t rcheck[8];
@@ -550,7 +485,7 @@ struct edv_ctx {
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // hash | table | dsm boundaries
   bool timed = false;
   // key-table store (registered public keys)
-  uint32_t* d_btab_comb32 = nullptr;  // B comb table in the 128-B entry format
+  uint32_t* d_btab_comb32 = nullptr;  // W = 8 base-point comb table (512 KiB)
   uint8_t* d_key_pk = nullptr;
   uint8_t* d_key_valid = nullptr;
   uint32_t* d_key_tab = nullptr;
@@ -657,14 +592,15 @@ static int keys_build(edv_ctx* ctx, uint64_t first, uint64_t nkeys, hipStream_t 
   if (!nkeys) return 0;
   int r;
   // rows: 64 p3 bases per key; pre: 8 prefix products per row
-  if ((r = ensure(ctx->b_aux, nkeys * 64 * kRowWords * 4 + nkeys * 64 * 80 * 4))) return r;
+  constexpr int R = Window<kKeyW>::kRows, E = Window<kKeyW>::kEntries;
+  if ((r = ensure(ctx->b_aux, nkeys * R * kRowWords * 4 + nkeys * R * E * 10 * 4))) return r;
   uint32_t* rows = (uint32_t*)ctx->b_aux.p;
-  uint32_t* pre = rows + nkeys * 64 * kRowWords;
+  uint32_t* pre = rows + nkeys * R * kRowWords;
   hipLaunchKernelGGL(edv_key_rows_kernel, dim3((uint32_t)div_up(nkeys, kBlock)), dim3(kBlock), 0, st,
                      ctx->d_key_pk + 32 * first, nkeys, rows, ctx->d_key_valid + first);
   HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(edv_key_fill_kernel, dim3((uint32_t)div_up(nkeys * 64, kBlock)), dim3(kBlock), 0, st, rows,
-                     nkeys * 64, ctx->d_key_tab + first * (uint64_t)kKeyTabWords, pre);
+  hipLaunchKernelGGL(edv_key_fill_kernel, dim3((uint32_t)div_up(nkeys * R, kBlock)), dim3(kBlock), 0, st, rows,
+                     nkeys * R, ctx->d_key_tab + first * (uint64_t)kKeyTabWords, pre);
   HIP_TRY(hipGetLastError());
   return 0;
 }
@@ -830,12 +766,18 @@ edv_ctx* edv_create(int device) {
   if ((e = hipMemcpy(ctx->d_btab_comb, BASE_COMB_U32, sizeof(BASE_COMB_U32), hipMemcpyHostToDevice)) != hipSuccess)
     return fail("hipMemcpy", e);
   {
-    std::vector<uint32_t> b32((sizeof(BASE_COMB_U32) / 4 / 30) * kEntryWords, 0u);
-    for (size_t e = 0; e < sizeof(BASE_COMB_U32) / 4 / 30; ++e)
-      memcpy(&b32[e * kEntryWords], &BASE_COMB_U32[e * 30], 30 * 4);
-    if ((e = hipMalloc(&ctx->d_btab_comb32, b32.size() * 4)) != hipSuccess) return fail("hipMalloc", e);
-    if ((e = hipMemcpy(ctx->d_btab_comb32, b32.data(), b32.size() * 4, hipMemcpyHostToDevice)) != hipSuccess)
-      return fail("hipMemcpy", e);
+    // W = 8 base-point comb table, built on the device by the key-table kernels
+    constexpr int rowsB = Window<kBaseW>::kRows, EB = Window<kBaseW>::kEntries;
+    uint32_t *rows = nullptr, *pre = nullptr;
+    if ((e = hipMalloc(&ctx->d_btab_comb32, (size_t)kBaseTabWords * 4)) != hipSuccess) return fail("hipMalloc", e);
+    if ((e = hipMalloc(&rows, rowsB * kRowWords * 4)) != hipSuccess) return fail("hipMalloc", e);
+    if ((e = hipMalloc(&pre, (size_t)rowsB * EB * 10 * 4)) != hipSuccess) return fail("hipMalloc", e);
+    hipLaunchKernelGGL(edv_base_rows_kernel, dim3(1), dim3(64), 0, ctx->stream, rows);
+    hipLaunchKernelGGL(edv_base_fill_kernel, dim3(1), dim3(64), 0, ctx->stream, rows, ctx->d_btab_comb32, pre);
+    e = hipStreamSynchronize(ctx->stream);
+    (void)hipFree(rows);
+    (void)hipFree(pre);
+    if (e != hipSuccess) return fail("base table build", e);
   }
   ctx->scratch_lanes = kMaxLanes;
   if ((e = hipMalloc(&ctx->d_scratch, ctx->scratch_lanes / kBlock * (uint64_t)kRegionBytes)) != hipSuccess)

@@ -229,7 +229,10 @@ EDV_HDNI bool ge_frombytes(ge_p3& h, const uint32_t s[8], bool negate) {
   fe_sub(chk, vxx, u); // v x^2 - u
   if (!fe_iszero(chk)) {
     fe_add(chk, vxx, u);
-    if (!fe_iszero(chk)) return false;
+    if (!fe_iszero(chk)) {
+      ge_p3_0(h);  // not on the curve: hand back a well-formed point (the verdict is reject)
+      return false;
+    }
     fe_mul(h.X, h.X, fe_const_sqrtm1());
   }
   const uint32_t sign = s[7] >> 31;

@@ -82,3 +82,11 @@ def test_kernel_point_roundtrip_and_blacklist(hostcheck, oracle):
             enc = (y | (s << 255)).to_bytes(32, "little")
             assert hostcheck.edv_host_is_canonical_point(enc) == oracle.oracle_is_canonical_point(enc) == 0
             assert hostcheck.edv_host_has_small_order(enc) == oracle.oracle_has_small_order(enc)
+
+
+def test_kernel_comb_path_on_cpu_matches_golden(hostcheck):
+    """The key-table path's arithmetic (comb.h: W=4 key tables, W=8 base
+    table, signed-digit recoding, mixed additions) on the CPU."""
+    items = items_of(load_npz("ed25519_edge.npz"))[::3] + items_of(load_npz("ed25519_valid.npz"))[::41]
+    for i, (sig, pk, msg, expect) in enumerate(items):
+        assert (hostcheck.edv_host_verify_comb(sig, pk, msg, ctypes.c_uint64(len(msg))) == 0) == expect, i
