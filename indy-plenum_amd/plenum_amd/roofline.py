@@ -22,12 +22,14 @@ MAD_PER_VERIFY = 305_000
 MAD_DSM_KERNEL = (FE_DSM + FE_ENCODE) * MAD_PER_FE  # 277,700
 MAD_TABLE_KERNEL = FE_DECODE * MAD_PER_FE
 # Key-table path (keys registered once): edv_comb_kernel = fixed-base comb over
-# both tables, 128 mixed additions x 7 multiplications + the encode inversion.
-FE_COMB = 128 * 7
-MAD_COMB_KERNEL = (FE_COMB + FE_ENCODE) * MAD_PER_FE  # 116,300
+# both tables -- 64 rows of the W=4 key table + 32 rows of the W=8 base table --
+# 96 mixed additions x 7 multiplications, plus the encode inversion.
+COMB_ADDS = 64 + 32
+FE_COMB = COMB_ADDS * 7
+MAD_COMB_KERNEL = (FE_COMB + FE_ENCODE) * MAD_PER_FE  # 93,900
 KERNEL_WORK = {
     "edv_dsm_kernel": "(2510 DSM + 267 encode) field ops x 100, ref10 a-priori count",
-    "edv_comb_kernel": "(128 mixed adds x 7 + 267 encode) field ops x 100, fixed-base comb over both tables",
+    "edv_comb_kernel": "(96 mixed adds x 7 + 267 encode) field ops x 100, fixed-base comb: 64 key rows (W=4) + 32 base rows (W=8)",
 }
 SHA_ALU_PER_BLOCK = 5_000
 
