@@ -1,11 +1,15 @@
 """Ed25519 request verifies/sec on MI355X -- the BASELINE.json headline metric.
 
 One step = one pass of the verify path over this rank's batch, inputs already
-resident in HBM: hash kernel (prechecks + SHA-512(R||A||M) mod L) -> table
-kernel (decode -A, [1..8](-A)) -> dsm kernel ([h](-A) + [S]B, encode, compare,
-wave ballot) -> accept bitmask; for N > 1 the step ends with the RCCL
-all-gather of the bitmask words (the path's one exchange step).  Weak scaling:
-each rank verifies its own shard of `--n` requests.
+resident in HBM.  Key-table path (default; the signers' verkeys registered
+once, like SimpleAuthNr.addIdr): hash kernel (prechecks + SHA-512(R||A||M)
+mod L) -> comb kernel ([h](-A) + [S]B from the key's and the base point's
+fixed-base tables) -> encode kernel (16 results per lane share one inversion;
+encode, compare with R, wave ballot) -> accept bitmask.  General path (any key
+bytes per request): hash -> table (decode -A, [1..8](-A)) -> dsm -> encode.
+For N > 1 the step ends with the RCCL all-gather of the bitmask words (the
+path's one exchange step).  Weak scaling: each rank verifies its own shard of
+`--n` requests.
 
 Workload (BASELINE.json configs[1]): 1M single-signature NYM requests, ~200 B
 signed payload (serialize_msg_for_signing of a NYM with an alias field), 1,000
@@ -51,6 +55,8 @@ def parse():
     ap.add_argument("--path", choices=["keyed", "general"], default="keyed",
                     help="keyed: signers' verkeys registered once (fixed-base tables in HBM, like "
                          "SimpleAuthNr.addIdr); general: every request carries its own key bytes")
+    ap.add_argument("--key-window", type=int, choices=[4, 6, 8, 10], default=10,
+                    help="comb window of the key tables (edv_keys_set_window)")
     ap.add_argument("--general-steps", type=int, default=5,
                     help="also time the general path for this many steps (0 = skip)")
     return ap.parse_args()
@@ -160,6 +166,7 @@ def main():
     torch.cuda.synchronize()
     tk = time.perf_counter()
     eng.keys_reset()
+    eng.keys_set_window(args.key_window)
     first = eng.keys_add(reg_pks)
     key_build_ms = (time.perf_counter() - tk) * 1e3
     assert first == 0
@@ -182,14 +189,11 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    dsm_ms, hash_ms, table_ms = [], [], []
+    phases = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-        h, t, d = eng.last_phase_ms()  # waits for this step's events
-        hash_ms.append(h)
-        table_ms.append(t)
-        dsm_ms.append(d)
+        phases.append(eng.last_phases_ms())  # waits for this step's events
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -217,7 +221,7 @@ def main():
         t1 = time.perf_counter()
         for _ in range(args.general_steps):
             ostep()
-            o_ms.append(eng.last_phase_ms())
+            o_ms.append(eng.last_phases_ms())
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -230,15 +234,16 @@ def main():
         og = np.unpackbits(ow.view(np.uint8), bitorder="little")[:n].astype(bool)
         other = {"path": "general" if args.path == "keyed" else "keyed",
                  "value": n * world * args.general_steps / o_el,
-                 "phase_ms": {"hash": float(np.mean([x[0] for x in o_ms])), "table": float(np.mean([x[1] for x in o_ms])),
-                              "dsm_or_comb": float(np.mean([x[2] for x in o_ms]))},
+                 "phase_ms": dict(zip(("hash", "table", "dsm_or_comb", "encode"),
+                                      (float(v) for v in np.mean(np.array(o_ms), axis=0)))),
                  "same_verdicts": bool((og == got).all())}
 
     total = n * world * args.steps
     value = total / elapsed
     ms_per_step = elapsed / args.steps * 1e3
-    dsm_avg = float(np.mean(dsm_ms))
-    kernel_mad = RL.MAD_COMB_KERNEL if args.path == "keyed" else RL.MAD_DSM_KERNEL
+    ph = np.mean(np.array(phases), axis=0)
+    dsm_avg = float(ph[2])
+    kernel_mad = RL.mad_comb_kernel(args.key_window) if args.path == "keyed" else RL.MAD_DSM_KERNEL
     kernel_name = "edv_comb_kernel" if args.path == "keyed" else "edv_dsm_kernel"
     achieved = n * kernel_mad / (dsm_avg * 1e-3) / 1e12
     peak = RL.PEAK_MAD_PER_S / 1e12
@@ -277,11 +282,13 @@ def main():
             "roofline": {"bound": "valu", "kernel": kernel_name, "achieved": achieved, "peak": peak,
                          "unit": "TMAD/s", "frac": achieved / peak, "traffic": traffic,
                          "algorithmic": "%d MAD per verify (%s), n=%d per launch, avg launch %.3f ms" % (
-                             kernel_mad, RL.KERNEL_WORK[kernel_name], n, dsm_avg)},
+                             kernel_mad, RL.kernel_work(kernel_name, args.key_window), n, dsm_avg)},
             "path": args.path,
-            "phase_ms": {"hash": float(np.mean(hash_ms)), "table": float(np.mean(table_ms)),
-                         ("comb" if args.path == "keyed" else "dsm"): dsm_avg},
-            "key_table_build_ms": key_build_ms, "keys": int(reg_pks.shape[0]),
+            "phase_ms": {"hash": float(ph[0]), "table": float(ph[1]),
+                         ("comb" if args.path == "keyed" else "dsm"): dsm_avg, "encode": float(ph[3])},
+            "key_window": args.key_window, "key_table_build_ms": key_build_ms, "keys": int(reg_pks.shape[0]),
+            "value_incl_key_build_one_step": (n * world / (ms_per_step * 1e-3 + key_build_ms * 1e-3)
+                                              if args.path == "keyed" else None),
             "ref10_equivalent_frac": (n * RL.MAD_PER_VERIFY / (ms_per_step * 1e-3)) / RL.PEAK_MAD_PER_S,
             "other_path": other,
             "cpu_baseline": cpu,

@@ -89,11 +89,15 @@ int edv_verify_batch_device(edv_ctx *ctx, const void *d_sig64, const void *d_pk3
                             const void *d_msg_off, uint64_t n, void *d_accept_words, void *stream);
 
 /* Kernel timing hooks for the roofline, measured with HIP events on the
- * stream the kernels ran on.  The verify pipeline is three kernels per chunk
+ * stream the kernels ran on.  The verify pipeline is four kernels per chunk
  * of up to 2^20 items: hash (prechecks + SHA-512 + mod L), table (decode -A,
- * [1..8](-A)), dsm ([h](-A) + [S]B, encode, compare, ballot).  For a
- * multi-chunk launch hash/table cover the last chunk only.
- * edv_last_kernel_ms returns the dsm time (the dominant kernel) or < 0. */
+ * [1..8](-A); empty on the key-table path), dsm or comb ([h](-A) + [S]B), and
+ * encode (batched inversion, encode, compare with R, ballot).  For a
+ * multi-chunk launch the per-phase times cover the last chunk only.
+ * edv_last_phases_ms fills out4[0..3] = hash, table, dsm/comb, encode;
+ * edv_last_phase_ms the first three; edv_last_kernel_ms returns the dsm/comb
+ * time (the dominant kernel) or < 0. */
+int edv_last_phases_ms(edv_ctx *ctx, double *out4);
 int edv_last_phase_ms(edv_ctx *ctx, double *hash_ms, double *table_ms, double *dsm_ms);
 double edv_last_kernel_ms(edv_ctx *ctx);
 
@@ -102,14 +106,22 @@ double edv_last_kernel_ms(edv_ctx *ctx);
 /* Register public keys (the verkeys SimpleAuthNr.addIdr holds,
  * plenum/server/client_authn.py:133-140).  For each key the library decodes
  * -A once, records libsodium's key checks (canonical y, not small order, on
- * the curve) and builds the fixed-base table (j+1) * 16^i * (-A), i < 64,
- * j < 8, as affine niels points: 64 KiB per key in HBM (1M keys = 64 GiB).
+ * the curve) and builds the fixed-base comb table (j+1) * 2^(W*i) * (-A),
+ * i < ceil(253/W), j < 2^(W-1), as affine niels points in HBM.  The key
+ * window W trades HBM for additions per verify:
+ *   W = 4:  64 KiB per key, 64 additions  (1M keys =  64 GiB)
+ *   W = 6: 172 KiB per key, 43 additions  (1M keys = 172 GiB)
+ *   W = 8: 512 KiB per key, 32 additions  (default; 500k keys = 256 GiB)
  * Key ids are consecutive from *first_id.  Host / device-pointer forms. */
 int edv_keys_add(edv_ctx *ctx, const uint8_t *pk32, uint64_t nkeys, uint64_t *first_id);
 int edv_keys_add_device(edv_ctx *ctx, const void *d_pk32, uint64_t nkeys, uint64_t *first_id, void *stream);
 uint64_t edv_keys_count(edv_ctx *ctx);
 /* Forget all registered keys (device memory is kept for reuse). */
 int edv_keys_reset(edv_ctx *ctx);
+/* Set the key window (4, 6 or 8; environment EDV_KEY_WINDOW sets the
+ * context default).  Only with no keys registered; frees the key store. */
+int edv_keys_set_window(edv_ctx *ctx, int w);
+int edv_keys_window(edv_ctx *ctx);
 
 /* Verify against registered keys: item i uses key id key_idx[i] (uint32);
  * an id >= edv_keys_count() is rejected (never read out of bounds).

@@ -8,13 +8,17 @@
 // so the double-scalar multiplication of libsodium's verify,
 // [h](-A) + [S]B, becomes ROWS_A + ROWS_B mixed additions and no doublings
 // (the a-priori ref10 count: ~253 doublings + ~86 additions).
-//   A = a registered public key (client_authn.py SimpleAuthNr.addIdr keys):
-//       W = 4, 64 rows x 8 entries x 128 B = 64 KiB per key, in HBM.
-//   B = the base point: W = 8, 32 rows x 128 entries x 128 B = 512 KiB, one
-//       copy per context (L2-resident: 4 MiB per XCD).
+//   A = a registered public key (client_authn.py SimpleAuthNr.addIdr keys),
+//       in HBM; the context's key window picks memory against additions:
+//       W = 4: 64 rows x   8 entries x 128 B =  64 KiB per key, 64 additions
+//       W = 6: 43 rows x  32 entries x 128 B = 172 KiB per key, 43 additions
+//       W = 8: 32 rows x 128 entries x 128 B = 512 KiB per key, 32 additions
+//       W = 10: 26 rows x 512 entries x 128 B = 1.6 MiB per key, 26 additions
+//   B = the base point, one table per context (kBaseW, verify_core.h):
+//       W = 12: 22 rows x 2048 entries x 128 B = 5.5 MiB (L2 4 MiB per XCD, MALL).
 // Entries are 32 u32 words (30 limbs + 2 pad) so one entry is 8 dwordx4 loads.
 #pragma once
-#include "verify_core.h"
+#include "ge25519.h"
 
 namespace edv {
 
@@ -22,35 +26,110 @@ constexpr int kEntryWords = 32;
 
 template <int W>
 struct Window {
-  static constexpr int kRows = (253 + W - 1) / W;
+  static_assert(W >= 4 && W <= 16, "comb window width 4..16");
+  // x < L < 2^253 plus the digit bias must stay below 2^(W * kRows): W * kRows >= 254
+  static constexpr int kRows = (254 + W - 1) / W;
   static constexpr int kEntries = 1 << (W - 1);
   static constexpr int kTableWords = kRows * kEntries * kEntryWords;
-  // sum_i 2^(W-1) * 2^(W*i) restricted to one 32-bit word (W divides 32)
-  static constexpr uint32_t kBiasWord = W == 4 ? 0x88888888u : W == 8 ? 0x80808080u : 0u;
-  static_assert(W == 4 || W == 8, "window widths that divide 32");
+  // word k of bias = sum_{i < kRows} 2^(W-1) * 2^(W*i)   (9 words: W*kRows may exceed 256)
+  static constexpr uint32_t bias_word(int k) {
+    uint32_t w = 0;
+    for (int i = 0; i < kRows; ++i) {
+      const int b = W - 1 + W * i;
+      if ((b >> 5) == k) w |= 1u << (b & 31);
+    }
+    return w;
+  }
 };
 
 // y = x + bias: digit_i = ((y >> W*i) & (2^W - 1)) - 2^(W-1) in [-2^(W-1), 2^(W-1) - 1]
-// and x = sum digit_i 2^(W*i); requires x + bias < 2^256 (x < 2^253 suffices).
+// and x = sum digit_i 2^(W*i) for x < L (x + bias < 2^(W*kRows) since W*kRows >= 254).  Any
+// 256-bit x still yields in-range digits (table indices stay in bounds); only
+// S >= L reaches that, and it is rejected by the precheck.
 template <int W>
-EDV_HD void comb_recode(uint32_t y[8], const uint32_t x[8]) {
+EDV_HD void comb_recode(uint32_t y[9], const uint32_t x[8]) {
   uint64_t carry = 0;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const uint64_t t = (uint64_t)x[k] + Window<W>::kBiasWord + carry;
+  for (int k = 0; k < 9; ++k) {
+    const uint64_t t = (uint64_t)(k < 8 ? x[k] : 0u) + Window<W>::bias_word(k) + carry;
     y[k] = (uint32_t)t;
     carry = t >> 32;
   }
 }
 
 template <int W>
-EDV_HD int comb_digit(const uint32_t y[8], int i) {
-  constexpr int per_word = 32 / W;
-  const int w = i / per_word;
-  uint32_t v = y[0];
+EDV_HD int comb_digit(const uint32_t y[9], int i) {
+  const int b = W * i;
+  const int w = b >> 5, s = b & 31;
+  uint32_t lo = y[0], hi = y[1];
 #pragma unroll
-  for (int k = 1; k < 8; ++k) v = (w == k) ? y[k] : v;
-  return (int)((v >> (W * (i % per_word))) & ((1u << W) - 1)) - (1 << (W - 1));
+  for (int k = 1; k < 8; ++k) {
+    lo = (w == k) ? y[k] : lo;
+    hi = (w == k) ? y[k + 1] : hi;
+  }
+  const uint32_t v = (uint32_t)((((uint64_t)hi << 32) | lo) >> s);
+  return (int)(v & ((1u << W) - 1)) - (1 << (W - 1));
+}
+
+// Signed-digit entry: e * T[row] as a niels point (e = 0 gives the identity).
+// T::load(row, j, ge_niels&) gives entry j (= (j+1) * 2^(W*row) * P).
+template <class T>
+EDV_HD void comb_fetch(ge_niels& nb, int e, const T& tab, int row) {
+  const int m = e < 0 ? -e : e;
+  if (m != 0)
+    tab.load(row, m - 1, nb);
+  else
+    ge_niels_0(nb);
+}
+EDV_HD void comb_apply(ge_p3& Q, ge_niels nb, int e) {
+  if (e < 0) {
+    const fe tmp = nb.ypx;
+    nb.ypx = nb.ymx;
+    nb.ymx = tmp;
+    fe_neg(nb.xy2d, nb.xy2d);
+  }
+  ge_p1p1 t;
+  ge_madd(t, Q, nb);
+  ge_p1p1_to_p3_addlike(Q, t);
+}
+
+// Q += [x]P for x < 2^253 by the comb over P's table: kRows mixed additions
+// (7 multiplications each).  Row r + 1's entry is fetched before row r's
+// addition runs, so the table gather overlaps the arithmetic.
+#ifndef EDV_COMB_PREFETCH
+#define EDV_COMB_PREFETCH 0  // 1: fetch row r+1 during row r (no gain measured: spills at 3 waves/SIMD)
+#endif
+template <int W, class T>
+EDV_HD void comb_mul_add(ge_p3& Q, const uint32_t x[8], const T& tab) {
+  uint32_t y[9];
+  comb_recode<W>(y, x);
+#if EDV_COMB_PREFETCH
+  int e = comb_digit<W>(y, 0);
+  ge_niels cur;
+  comb_fetch(cur, e, tab, 0);
+#pragma unroll 1
+  for (int r = 0; r < Window<W>::kRows; ++r) {
+    ge_niels next;
+    int e_next = 0;
+    if (r + 1 < Window<W>::kRows) {
+      e_next = comb_digit<W>(y, r + 1);
+      comb_fetch(next, e_next, tab, r + 1);
+    } else {
+      ge_niels_0(next);
+    }
+    comb_apply(Q, cur, e);
+    cur = next;
+    e = e_next;
+  }
+#else
+#pragma unroll 1
+  for (int r = 0; r < Window<W>::kRows; ++r) {
+    const int e = comb_digit<W>(y, r);
+    ge_niels nb;
+    comb_fetch(nb, e, tab, r);
+    comb_apply(Q, nb, e);
+  }
+#endif
 }
 
 EDV_HD void store_fe(uint32_t* p, const fe& f) {
@@ -89,47 +168,73 @@ EDV_HD void comb_rows(uint32_t* rows, ge_p3 P) {
   }
 }
 
-// The kEntries multiples of one row base, one shared inversion (Montgomery's
-// trick, prefix products in `pre`, kEntries * 10 words), affine niels out.
-template <int W>
-EDV_HD void comb_fill_row(uint32_t* entries, uint32_t* pre, const uint32_t* base_words) {
-  constexpr int E = Window<W>::kEntries;
-  ge_p3 base, m;
+// Entries j = c + nch * t (t < count) of one row -- the multiples (j+1) * base
+// -- with one shared inversion (Montgomery's trick; prefix product t at
+// pre + t * pre_stride, 10 words), affine niels out.  Lane c of a row starts
+// at (c+1) * base (double-and-add) and steps by nch * base (log2(nch)
+// doublings; nch a power of two), so the nch lanes of a row write
+// consecutive entries at every step (edv_comb_fill_kernel).
+EDV_HD void comb_fill_strided(uint32_t* entries, uint32_t* pre, uint64_t pre_stride, const uint32_t* base_words,
+                              int c, int nch, int count) {
+  ge_p3 base, m, step;
   load_fe(base.X, base_words);
   load_fe(base.Y, base_words + 10);
   load_fe(base.Z, base_words + 20);
   load_fe(base.T, base_words + 30);
-  ge_cached cb;
+  ge_cached cb, cs;
   ge_p3_to_cached(cb, base);
-  m = base;
-  fe acc;
+  step = base;
 #pragma unroll 1
-  for (int j = 0; j < E; ++j) {
-    if (j > 0) {
-      ge_p1p1 t;
+  for (int s = nch; s > 1; s >>= 1) {
+    ge_p1p1 t;
+    ge_p3_dbl(t, step);
+    ge_dbl_to_p3(step, t);
+  }
+  ge_p3_to_cached(cs, step);
+  // m = (c + 1) * base, most significant bit first
+  const uint32_t k = (uint32_t)c + 1u;
+  const int top = 31 - __builtin_clz(k);
+  m = base;
+#pragma unroll 1
+  for (int bit = top - 1; bit >= 0; --bit) {
+    ge_p1p1 t;
+    ge_p3_dbl(t, m);
+    ge_dbl_to_p3(m, t);
+    if ((k >> bit) & 1u) {
       ge_add(t, m, cb);
       ge_p1p1_to_p3_addlike(m, t);
     }
-    store_fe(entries + j * kEntryWords, m.X);
-    store_fe(entries + j * kEntryWords + 10, m.Y);
-    store_fe(entries + j * kEntryWords + 20, m.Z);
-    if (j == 0)
+  }
+  fe acc;
+#pragma unroll 1
+  for (int t = 0; t < count; ++t) {
+    if (t > 0) {
+      ge_p1p1 u;
+      ge_add(u, m, cs);
+      ge_p1p1_to_p3_addlike(m, u);
+    }
+    uint32_t* e = entries + (uint64_t)(c + nch * t) * kEntryWords;
+    store_fe(e, m.X);
+    store_fe(e + 10, m.Y);
+    store_fe(e + 20, m.Z);
+    if (t == 0)
       acc = m.Z;
     else
       fe_mul(acc, acc, m.Z);
-    store_fe(pre + j * 10, acc);
+    store_fe(pre + t * pre_stride, acc);
   }
   fe inv;
   fe_invert(inv, acc);
 #pragma unroll 1
-  for (int j = E - 1; j >= 0; --j) {
-    fe zinv, X, Y, Z, x, y, t;
-    load_fe(X, entries + j * kEntryWords);
-    load_fe(Y, entries + j * kEntryWords + 10);
-    load_fe(Z, entries + j * kEntryWords + 20);
-    if (j > 0) {
+  for (int t = count - 1; t >= 0; --t) {
+    uint32_t* e = entries + (uint64_t)(c + nch * t) * kEntryWords;
+    fe zinv, X, Y, Z, x, y, u;
+    load_fe(X, e);
+    load_fe(Y, e + 10);
+    load_fe(Z, e + 20);
+    if (t > 0) {
       fe p;
-      load_fe(p, pre + (j - 1) * 10);
+      load_fe(p, pre + (t - 1) * pre_stride);
       fe_mul(zinv, inv, p);
       fe_mul(inv, inv, Z);
     } else {
@@ -137,16 +242,22 @@ EDV_HD void comb_fill_row(uint32_t* entries, uint32_t* pre, const uint32_t* base
     }
     fe_mul(x, X, zinv);
     fe_mul(y, Y, zinv);
-    fe_add(t, y, x);
-    store_fe_canon(entries + j * kEntryWords, t);
-    fe_sub(t, y, x);
-    store_fe_canon(entries + j * kEntryWords + 10, t);
-    fe_mul(t, x, y);
-    fe_mul(t, t, fe_const_d2());
-    store_fe_canon(entries + j * kEntryWords + 20, t);
-    entries[j * kEntryWords + 30] = 0;
-    entries[j * kEntryWords + 31] = 0;
+    fe_add(u, y, x);
+    store_fe_canon(e, u);
+    fe_sub(u, y, x);
+    store_fe_canon(e + 10, u);
+    fe_mul(u, x, y);
+    fe_mul(u, u, fe_const_d2());
+    store_fe_canon(e + 20, u);
+    e[30] = 0;
+    e[31] = 0;
   }
+}
+
+// The whole row (kEntries multiples) in one chunk.
+template <int W>
+EDV_HD void comb_fill_row(uint32_t* entries, uint32_t* pre, const uint32_t* base_words) {
+  comb_fill_strided(entries, pre, 10, base_words, 0, 1, Window<W>::kEntries);
 }
 
 }  // namespace edv

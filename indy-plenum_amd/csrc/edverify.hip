@@ -3,24 +3,30 @@
 // include/edverify.h.
 //
 // Kernels (one HIP stream per context):
-//   edv_verify_kernel   one lane per request: prechecks, SHA-512(R||A||M) mod L,
-//                       decode -A, [h](-A) + [S]B with signed radix-16 windows
-//                       (A multiples in a per-lane SoA scratch table, B
-//                       multiples in LDS), encode, byte compare with R, and a
-//                       wave ballot into the accept bitmask.
-//   edv_sign_kernel /
-//   edv_keypair_kernel  deterministic Ed25519 signer (synthetic request load).
-//   edv_tally_*         distinct-voter ballots -> counts -> quorum flags.
+//   general path (any 32-byte key per request):
+//     edv_hash_kernel    prechecks + SHA-512(R||A||M) mod L, one lane per request
+//     edv_table_kernel   decode -A, cached [1..8](-A) in per-block SoA scratch
+//     edv_dsm_kernel     [h](-A) + [S]B, signed radix-16, B multiples in LDS
+//   key-table path (registered keys, comb.h):
+//     edv_hash_keyed_kernel, edv_comb_kernel<W>  fixed-base combs, no doublings
+//   both paths end in
+//     edv_encode_kernel<M>  M results per lane share one inversion
+//                           (batch_encode.h), byte compare with R, wave
+//                           ballot into the accept bitmask.
+//   edv_sign_kernel / edv_keypair_kernel   deterministic Ed25519 signer
+//   edv_tally_*          distinct-voter ballots -> counts -> quorum flags.
 #include <hip/hip_runtime.h>
 
 #include <mutex>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <string>
 #include <vector>
 
 #include "../../include/edverify.h"
+#include "batch_encode.h"
 #include "comb.h"
 #include "verify_core.h"
 
@@ -89,19 +95,6 @@ struct DevTableA {
   }
 };
 
-struct LdsNiels {
-  const uint32_t* lds;  // 8 points * 30 words
-  __device__ void load(int j, ge_niels& n) const {
-    const uint32_t* p = lds + 30 * j;
-#pragma unroll
-    for (int l = 0; l < 10; ++l) {
-      n.ypx.v[l] = p[l];
-      n.ymx.v[l] = p[10 + l];
-      n.xy2d.v[l] = p[20 + l];
-    }
-  }
-};
-
 __device__ __forceinline__ void load_words(uint32_t* dst, const uint8_t* src, int nwords) {
   // src is 16-byte aligned for the sig/pk arrays (64 / 32 byte records)
   const uint4* s = (const uint4*)src;
@@ -149,108 +142,16 @@ __global__ __launch_bounds__(kBlock) void edv_table_kernel(const uint8_t* __rest
   if (!ok) flags[i] = 0;
 }
 
-__global__ __launch_bounds__(kBlock) void edv_dsm_kernel(const uint8_t* __restrict__ sig64, uint64_t n,
-                                                        const uint32_t* __restrict__ h_soa,
-                                                        const uint8_t* __restrict__ flags,
-                                                        uint32_t* __restrict__ table, uint64_t stride,
-                                                        const uint32_t* __restrict__ btab,
-                                                        unsigned long long* __restrict__ accept_words) {
-  __shared__ uint32_t lds_b[8 * 30];
-  for (int t = threadIdx.x; t < 8 * 30; t += blockDim.x) lds_b[t] = btab[t];
-  __syncthreads();
-  const LdsNiels tb{lds_b};
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  bool ok = false;
-  if (i < n) {
-    uint32_t sig[16], h[8];
-    load_words(sig, sig64 + 64 * i, 16);
+// Result points R' = (X : Y : Z), SoA [30][stride]: word w of request i at
+// w * stride + i (coalesced stores here and loads in edv_encode_kernel).
+__device__ __forceinline__ void store_point_soa(uint32_t* __restrict__ pt, uint64_t stride, uint64_t i,
+                                                const ge_p3& Q) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) h[k] = h_soa[k * stride + i];
-    const DevTableA ta(table, blockIdx.x, threadIdx.x);
-    ok = verify_phase_dsm(h, sig + 8, sig, ta, tb) && flags[i];
+  for (int l = 0; l < 10; ++l) {
+    pt[(0 + l) * stride + i] = Q.X.v[l];
+    pt[(10 + l) * stride + i] = Q.Y.v[l];
+    pt[(20 + l) * stride + i] = Q.Z.v[l];
   }
-  const unsigned long long b = __ballot(ok);
-  if ((threadIdx.x & 63) == 0 && i < n) accept_words[i >> 6] = b;
-}
-
-
-// ---- key-table path (comb.h) ---------------------------------------------
-// Registered keys: W = 4 comb tables (64 KiB each).  Base point: W = 8 comb
-// table (512 KiB) built once per context by the same kernels.
-#ifndef EDV_COMB_MIN_WAVES
-#define EDV_COMB_MIN_WAVES 3  // 168 VGPRs, 3 waves/SIMD: 2% faster than 2 (tools/ab_keyed.py)
-#endif
-constexpr int kKeyW = 4, kBaseW = 8;
-constexpr int kKeyTabWords = Window<kKeyW>::kTableWords;   // 16384 words
-constexpr int kBaseTabWords = Window<kBaseW>::kTableWords; // 131072 words
-constexpr int kRowWords = 40;
-
-// One lane per key: decode -A, libsodium's key checks, the 64 row bases.
-__global__ __launch_bounds__(kBlock) void edv_key_rows_kernel(const uint8_t* __restrict__ pk32, uint64_t nkeys,
-                                                             uint32_t* __restrict__ rows,
-                                                             uint8_t* __restrict__ valid) {
-  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= nkeys) return;
-  uint32_t pk[8];
-  load_words(pk, pk32 + 32 * k, 8);
-  ge_p3 P;
-  const bool dec = ge_frombytes(P, pk, true);
-  valid[k] = (dec && is_canonical_point(pk) && !has_small_order(pk)) ? 1 : 0;
-  comb_rows<kKeyW>(rows + k * Window<kKeyW>::kRows * kRowWords, P);
-}
-
-// One lane per (key, row).
-__global__ __launch_bounds__(kBlock) void edv_key_fill_kernel(const uint32_t* __restrict__ rows, uint64_t nrows,
-                                                             uint32_t* __restrict__ tab, uint32_t* __restrict__ pre) {
-  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= nrows) return;
-  constexpr int E = Window<kKeyW>::kEntries;
-  comb_fill_row<kKeyW>(tab + r * E * kEntryWords, pre + r * E * 10, rows + r * kRowWords);
-}
-
-// Base-point table: one lane decodes B and writes its 32 row bases ...
-__global__ void edv_base_rows_kernel(uint32_t* __restrict__ rows) {
-  if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  uint32_t b[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) b[k] = 0x66666666u;
-  b[0] = 0x66666658u;  // B = (x, 4/5), x even
-  ge_p3 P;
-  ge_frombytes(P, b, false);
-  comb_rows<kBaseW>(rows, P);
-}
-// ... then one lane per row fills its 128 entries.
-__global__ void edv_base_fill_kernel(const uint32_t* __restrict__ rows, uint32_t* __restrict__ tab,
-                                     uint32_t* __restrict__ pre) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= Window<kBaseW>::kRows) return;
-  constexpr int E = Window<kBaseW>::kEntries;
-  comb_fill_row<kBaseW>(tab + (uint64_t)r * E * kEntryWords, pre + (uint64_t)r * E * 10, rows + r * kRowWords);
-}
-
-#ifndef EDV_HASH_MIN_WAVES
-#define EDV_HASH_MIN_WAVES 3  // 0.71 vs 0.84 ms per 1M at 2 (tools/ab_keyed.py), despite an 88-B spill
-#endif
-__global__ __launch_bounds__(kBlock, EDV_HASH_MIN_WAVES) void edv_hash_keyed_kernel(const uint8_t* __restrict__ sig64,
-                                                               const uint32_t* __restrict__ key_idx,
-                                                               uint32_t key_count,
-                                                               const uint8_t* __restrict__ key_pk,
-                                                               const uint8_t* __restrict__ msgs,
-                                                               const uint64_t* __restrict__ msg_off, uint64_t n,
-                                                               uint32_t* __restrict__ h_soa,
-                                                               uint8_t* __restrict__ flags, uint64_t stride) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint32_t sig[16], pk[8], h[8];
-  load_words(sig, sig64 + 64 * i, 16);
-  const uint32_t key = key_idx[i];
-  const bool in_range = key < key_count;  // out-of-range ids reject, never read out of bounds
-  load_words(pk, key_pk + 32 * (uint64_t)(in_range ? key : 0), 8);
-  const uint64_t o0 = msg_off[i], o1 = msg_off[i + 1];
-  const bool ok = verify_phase_hash(h, sig, pk, msgs + o0, o1 - o0) && in_range;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) h_soa[k * stride + i] = h[k];
-  flags[i] = ok ? 1 : 0;
 }
 
 __device__ __forceinline__ void load_niels(ge_niels& nb, const uint32_t* __restrict__ p) {
@@ -272,61 +173,211 @@ __device__ __forceinline__ void load_niels(ge_niels& nb, const uint32_t* __restr
   }
 }
 
-// Q += digit * T[row] for signed digit in [-8, 7] (0 adds the identity).
-__device__ __forceinline__ void comb_step(ge_p3& Q, int e, const uint32_t* __restrict__ row) {
-  const int m = e < 0 ? -e : e;
-  ge_niels nb;
-  ge_niels_0(nb);
-  if (m != 0) load_niels(nb, row + (m - 1) * kEntryWords);
-  if (e < 0) {
-    fe tmp = nb.ypx;
-    nb.ypx = nb.ymx;
-    nb.ymx = tmp;
-    fe_neg(nb.xy2d, nb.xy2d);
+// A comb table in global memory (comb.h layout: row-major, 32-word entries).
+template <int W>
+struct DevComb {
+  const uint32_t* __restrict__ tab;
+  __device__ void load(int row, int j, ge_niels& nb) const {
+    load_niels(nb, tab + ((uint32_t)row * Window<W>::kEntries + (uint32_t)j) * kEntryWords);
   }
-  ge_p1p1 t;
-  ge_madd(t, Q, nb);
-  ge_p1p1_to_p3_addlike(Q, t);
+};
+
+__global__ __launch_bounds__(kBlock) void edv_dsm_kernel(const uint8_t* __restrict__ sig64, uint64_t n,
+                                                        const uint32_t* __restrict__ h_soa,
+                                                        uint32_t* __restrict__ table, uint64_t stride,
+                                                        const uint32_t* __restrict__ btab_comb,
+                                                        uint32_t* __restrict__ pt) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t S[8], h[8];
+  load_words(S, sig64 + 64 * i + 32, 8);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) h[k] = h_soa[k * stride + i];
+  const DevTableA ta(table, blockIdx.x, threadIdx.x);
+  const DevComb<kBaseW> cb{btab_comb};
+  ge_p3 Q;
+  verify_phase_dsm_point(Q, h, S, ta, cb);
+  store_point_soa(pt, stride, i, Q);
 }
 
+// Batched encode + compare + ballot.  Lane l of wave v owns requests
+// v*64*M + 64*j + l (j < M): every j is one coalesced 64-request word.
+struct DevEncode {
+  const uint32_t* __restrict__ pt;
+  uint32_t* __restrict__ pre;
+  const uint8_t* __restrict__ sig64;
+  const uint8_t* __restrict__ flags;
+  unsigned long long* __restrict__ words;
+  uint64_t stride, n, base, wbase;  // base = this lane's request for j = 0; wbase = word for j = 0
+  uint32_t lane;
+  __device__ uint64_t req(int j) const { return base + 64ull * j; }
+  __device__ bool valid(int j) const { return req(j) < n; }
+  __device__ void z(int j, fe& f) const {
+    const uint64_t r = req(j);
+#pragma unroll
+    for (int l = 0; l < 10; ++l) f.v[l] = pt[(20 + l) * stride + r];
+  }
+  __device__ void xy(int j, fe& X, fe& Y) const {
+    const uint64_t r = req(j);
+#pragma unroll
+    for (int l = 0; l < 10; ++l) {
+      X.v[l] = pt[l * stride + r];
+      Y.v[l] = pt[(10 + l) * stride + r];
+    }
+  }
+  __device__ void put_pre(int j, const fe& f) const {
+    if (!valid(j)) return;
+    const uint64_t r = req(j);
+#pragma unroll
+    for (int l = 0; l < 10; ++l) pre[l * stride + r] = f.v[l];
+  }
+  __device__ void get_pre(int j, fe& f) const {
+    fe_1(f);
+    if (!valid(j)) return;
+    const uint64_t r = req(j);
+#pragma unroll
+    for (int l = 0; l < 10; ++l) f.v[l] = pre[l * stride + r];
+  }
+  __device__ void emit(int j, const uint32_t enc[8], bool zero_z) const {
+    bool ok = false;
+    if (valid(j)) {
+      const uint64_t r = req(j);
+      const uint4* R = (const uint4*)(sig64 + 64 * r);
+      const uint4 a = R[0], b = R[1];
+      ok = !zero_z && flags[r] && enc[0] == a.x && enc[1] == a.y && enc[2] == a.z && enc[3] == a.w &&
+           enc[4] == b.x && enc[5] == b.y && enc[6] == b.z && enc[7] == b.w;
+    }
+    const unsigned long long bits = __ballot(ok);
+    if (lane == 0 && valid(j)) words[wbase + j] = bits;
+  }
+};
+
+#ifndef EDV_ENCODE_M
+#define EDV_ENCODE_M 16
+#endif
+constexpr int kEncodeM = EDV_ENCODE_M;
+
+template <int M>
+__global__ __launch_bounds__(kBlock) void edv_encode_kernel(const uint8_t* __restrict__ sig64, uint64_t n,
+                                                           const uint32_t* __restrict__ pt,
+                                                           uint32_t* __restrict__ pre,
+                                                           const uint8_t* __restrict__ flags,
+                                                           unsigned long long* __restrict__ accept_words,
+                                                           uint64_t stride) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t wave = g >> 6;
+  const uint32_t lane = (uint32_t)(g & 63);
+  if (wave * 64ull * M >= n) return;  // whole wave past the end (wave-uniform)
+  DevEncode a{pt, pre, sig64, flags, accept_words, stride, n, wave * 64ull * M + lane, wave * M, lane};
+  encode_batch<M>(a);
+}
+
+// ---- key-table path (comb.h) ---------------------------------------------
+// Registered keys: comb tables of -A at the context's key window (4, 6, 8 or 10).
+// Base point: W = 8 comb table (512 KiB) built once per context by the same
+// kernels.
+#ifndef EDV_COMB_MIN_WAVES
+#define EDV_COMB_MIN_WAVES 3  // 168 VGPRs, 3 waves/SIMD: 2% faster than 2 (tools/ab_keyed.py)
+#endif
+constexpr int kBaseTabWords = Window<kBaseW>::kTableWords;  // 131072 words at W = 8
+constexpr int kRowWords = 40;
+
+// One lane per key: decode -A, libsodium's key checks, the row bases.
+template <int W>
+__global__ __launch_bounds__(kBlock) void edv_key_rows_kernel(const uint8_t* __restrict__ pk32, uint64_t nkeys,
+                                                             uint32_t* __restrict__ rows,
+                                                             uint8_t* __restrict__ valid) {
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nkeys) return;
+  uint32_t pk[8];
+  load_words(pk, pk32 + 32 * k, 8);
+  ge_p3 P;
+  const bool dec = ge_frombytes(P, pk, true);
+  valid[k] = (dec && is_canonical_point(pk) && !has_small_order(pk)) ? 1 : 0;
+  comb_rows<W>(rows + k * Window<W>::kRows * kRowWords, P);
+}
+
+// One lane per (row, c), c < NCH, filling entries c, c + NCH, c + 2 NCH, ...
+// of its row (CH = kEntries / NCH of them, one inversion per lane).
+template <int W>
+struct FillShape {
+  static constexpr int E = Window<W>::kEntries;
+  static constexpr int CH = E < 32 ? E : 32;
+  static constexpr int NCH = E / CH;
+};
+template <int W>
+__global__ __launch_bounds__(kBlock) void edv_comb_fill_kernel(const uint32_t* __restrict__ rows, uint64_t nrows,
+                                                              uint32_t* __restrict__ tab, uint32_t* __restrict__ pre) {
+  using F = FillShape<W>;
+  const uint64_t nl = nrows * F::NCH;
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= nl) return;
+  const uint64_t r = g / F::NCH;
+  const int c = (int)(g % F::NCH);
+  comb_fill_strided(tab + r * F::E * kEntryWords, pre + g * 10, nl * 10, rows + r * kRowWords, c, F::NCH, F::CH);
+}
+
+// Base-point table: one lane decodes B and writes its 32 row bases ...
+__global__ void edv_base_rows_kernel(uint32_t* __restrict__ rows) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  uint32_t b[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) b[k] = 0x66666666u;
+  b[0] = 0x66666658u;  // B = (x, 4/5), x even
+  ge_p3 P;
+  ge_frombytes(P, b, false);
+  comb_rows<kBaseW>(rows, P);
+}
+#ifndef EDV_HASH_MIN_WAVES
+#define EDV_HASH_MIN_WAVES 3  // 0.71 vs 0.84 ms per 1M at 2 (tools/ab_keyed.py), despite an 88-B spill
+#endif
+__global__ __launch_bounds__(kBlock, EDV_HASH_MIN_WAVES) void edv_hash_keyed_kernel(const uint8_t* __restrict__ sig64,
+                                                               const uint32_t* __restrict__ key_idx,
+                                                               uint32_t key_count,
+                                                               const uint8_t* __restrict__ key_pk,
+                                                               const uint8_t* __restrict__ key_valid,
+                                                               const uint8_t* __restrict__ msgs,
+                                                               const uint64_t* __restrict__ msg_off, uint64_t n,
+                                                               uint32_t* __restrict__ h_soa,
+                                                               uint8_t* __restrict__ flags, uint64_t stride) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t sig[16], pk[8], h[8];
+  load_words(sig, sig64 + 64 * i, 16);
+  const uint32_t key = key_idx[i];
+  const bool in_range = key < key_count;  // out-of-range ids reject, never read out of bounds
+  const uint64_t k = in_range ? key : 0;
+  load_words(pk, key_pk + 32 * k, 8);
+  const uint64_t o0 = msg_off[i], o1 = msg_off[i + 1];
+  const bool ok = verify_phase_hash(h, sig, pk, msgs + o0, o1 - o0) && in_range && key_valid[k];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) h_soa[k * stride + i] = h[k];
+  flags[i] = ok ? 1 : 0;
+}
+
+// [h](-A) + [S]B over the key's comb (W) and the base comb (W = 8): no doublings.
+template <int W>
 __global__ __launch_bounds__(kBlock, EDV_COMB_MIN_WAVES) void edv_comb_kernel(const uint8_t* __restrict__ sig64,
                                                          const uint32_t* __restrict__ key_idx, uint32_t key_count,
                                                          uint64_t n, const uint32_t* __restrict__ h_soa,
-                                                         const uint8_t* __restrict__ flags,
-                                                         const uint8_t* __restrict__ key_valid,
                                                          const uint32_t* __restrict__ key_tab,
                                                          const uint32_t* __restrict__ btab,
-                                                         unsigned long long* __restrict__ accept_words, uint64_t stride) {
+                                                         uint32_t* __restrict__ pt, uint64_t stride) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  bool ok = false;
-  if (i < n) {
-    uint32_t sig[16], h[8], hy[8], sy[8];
-    load_words(sig, sig64 + 64 * i, 16);
+  if (i >= n) return;
+  uint32_t S[8], h[8];
+  load_words(S, sig64 + 64 * i + 32, 8);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) h[k] = h_soa[k * stride + i];
-    const uint32_t key0 = key_idx[i];
-    const uint32_t key = key0 < key_count ? key0 : 0;  // flags[i] is 0 for an out-of-range id
-    const uint32_t* at = key_tab + (uint64_t)key * kKeyTabWords;
-    comb_recode<kKeyW>(hy, h);
-    comb_recode<kBaseW>(sy, sig + 8);
-    ge_p3 Q;
-    ge_p3_0(Q);
-    constexpr int EA = Window<kKeyW>::kEntries, EB = Window<kBaseW>::kEntries;
-#pragma unroll 1
-    for (int r = 0; r < Window<kKeyW>::kRows; ++r) comb_step(Q, comb_digit<kKeyW>(hy, r), at + r * EA * kEntryWords);
-#pragma unroll 1
-    for (int r = 0; r < Window<kBaseW>::kRows; ++r) comb_step(Q, comb_digit<kBaseW>(sy, r), btab + r * EB * kEntryWords);
-    ge_p2 r2;
-    ge_p3_to_p2(r2, Q);
-    uint32_t rcheck[8];
-    ge_tobytes(rcheck, r2);
-    bool eq = true;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) eq = eq && rcheck[k] == sig[k];
-    ok = eq && flags[i] && key_valid[key];
-  }
-  const unsigned long long b = __ballot(ok);
-  if ((threadIdx.x & 63) == 0 && i < n) accept_words[i >> 6] = b;
+  for (int k = 0; k < 8; ++k) h[k] = h_soa[k * stride + i];
+  const uint32_t key0 = key_idx[i];
+  const uint32_t key = key0 < key_count ? key0 : 0;  // flags[i] is 0 for an out-of-range id
+  const DevComb<W> ta{key_tab + (uint64_t)key * Window<W>::kTableWords};
+  const DevComb<kBaseW> tb{btab};
+  ge_p3 Q;
+  ge_p3_0(Q);
+  comb_mul_add<W>(Q, h, ta);
+  comb_mul_add<kBaseW>(Q, S, tb);
+  store_point_soa(pt, stride, i, Q);
 }
 
 // Fixed-base comb: [x]B with x < 2^253, 64 madds over BASE_COMB (global).
@@ -476,13 +527,15 @@ uint64_t div_up(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 struct edv_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  uint32_t* d_btab_small = nullptr;
-  uint32_t* d_btab_comb = nullptr;
+  uint32_t* d_btab_comb = nullptr;    // W = 4 base comb (signer / keypair)
   uint32_t* d_scratch = nullptr;  // per-lane A tables, kMaxLanes / kBlock regions
   uint32_t* d_hsoa = nullptr;     // h words, SoA [8][kMaxLanes]
   uint8_t* d_flags = nullptr;     // precheck / decode verdicts [kMaxLanes]
+  uint32_t* d_pt = nullptr;       // R' = (X:Y:Z), SoA [30][kMaxLanes]
+  uint32_t* d_pre = nullptr;      // batch-encode prefix products, SoA [10][kMaxLanes]
   uint64_t scratch_lanes = 0;
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // hash | table | dsm boundaries
+  static constexpr int kEv = 5;   // hash | table | dsm-or-comb | encode boundaries
+  hipEvent_t ev[kEv] = {};
   bool timed = false;
   // key-table store (registered public keys)
   uint32_t* d_btab_comb32 = nullptr;  // W = 8 base-point comb table (512 KiB)
@@ -490,6 +543,7 @@ struct edv_ctx {
   uint8_t* d_key_valid = nullptr;
   uint32_t* d_key_tab = nullptr;
   uint64_t key_count = 0, key_cap = 0;
+  int key_w = 10;                     // comb window of the key tables (4, 6, 8 or 10)
   // staging buffers for host-pointer calls
   struct Buf {
     void* p = nullptr;
@@ -520,6 +574,23 @@ int set_device(edv_ctx* ctx) {
 
 hipStream_t pick_stream(edv_ctx* ctx, void* stream) { return stream ? (hipStream_t)stream : ctx->stream; }
 
+uint32_t key_tab_words(int w) {
+  return w == 4 ? Window<4>::kTableWords
+       : w == 6 ? Window<6>::kTableWords
+       : w == 10 ? Window<10>::kTableWords
+                 : Window<8>::kTableWords;
+}
+
+int launch_encode(edv_ctx* ctx, const uint8_t* sig, uint64_t cn, unsigned long long* words, uint64_t chunk,
+                  hipStream_t st) {
+  const uint64_t waves = div_up(cn, 64ull * kEncodeM);
+  const uint32_t grid = (uint32_t)div_up(waves * 64, kBlock);
+  hipLaunchKernelGGL(edv_encode_kernel<kEncodeM>, dim3(grid), dim3(kBlock), 0, st, sig, cn, ctx->d_pt, ctx->d_pre,
+                     ctx->d_flags, words, chunk);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
 int launch_verify(edv_ctx* ctx, const void* d_sig, const void* d_pk, const void* d_msgs, const void* d_off, uint64_t n,
                   void* d_words, hipStream_t st) {
   if (n == 0) return 0;
@@ -542,10 +613,13 @@ int launch_verify(edv_ctx* ctx, const void* d_sig, const void* d_pk, const void*
     HIP_TRY(hipGetLastError());
     if (last) HIP_TRY(hipEventRecord(ctx->ev[2], st));
     hipLaunchKernelGGL(edv_dsm_kernel, dim3(grid), dim3(kBlock), 0, st, sig + 64 * c0, cn, ctx->d_hsoa,
-                       ctx->d_flags, ctx->d_scratch, chunk, ctx->d_btab_small, words + c0 / 64);
+                       ctx->d_scratch, chunk, ctx->d_btab_comb32, ctx->d_pt);
     HIP_TRY(hipGetLastError());
+    if (last) HIP_TRY(hipEventRecord(ctx->ev[3], st));
+    int r = launch_encode(ctx, sig + 64 * c0, cn, words + c0 / 64, chunk, st);
+    if (r) return r;
   }
-  HIP_TRY(hipEventRecord(ctx->ev[3], st));
+  HIP_TRY(hipEventRecord(ctx->ev[4], st));
   ctx->timed = true;
   return 0;
 }
@@ -563,7 +637,7 @@ static int keys_reserve(edv_ctx* ctx, uint64_t need) {
   uint32_t* tab = nullptr;
   hipError_t e;
   if ((e = hipMalloc(&pk, cap * 32)) || (e = hipMalloc(&valid, cap)) ||
-      (e = hipMalloc(&tab, cap * (uint64_t)kKeyTabWords * 4))) {
+      (e = hipMalloc(&tab, cap * (uint64_t)key_tab_words(ctx->key_w) * 4))) {
     if (pk) (void)hipFree(pk);
     if (valid) (void)hipFree(valid);
     if (tab) (void)hipFree(tab);
@@ -572,7 +646,7 @@ static int keys_reserve(edv_ctx* ctx, uint64_t need) {
   if (ctx->key_count) {
     HIP_TRY(hipMemcpyAsync(pk, ctx->d_key_pk, ctx->key_count * 32, hipMemcpyDeviceToDevice, ctx->stream));
     HIP_TRY(hipMemcpyAsync(valid, ctx->d_key_valid, ctx->key_count, hipMemcpyDeviceToDevice, ctx->stream));
-    HIP_TRY(hipMemcpyAsync(tab, ctx->d_key_tab, ctx->key_count * (uint64_t)kKeyTabWords * 4,
+    HIP_TRY(hipMemcpyAsync(tab, ctx->d_key_tab, ctx->key_count * (uint64_t)key_tab_words(ctx->key_w) * 4,
                            hipMemcpyDeviceToDevice, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
   }
@@ -587,22 +661,40 @@ static int keys_reserve(edv_ctx* ctx, uint64_t need) {
 }
 
 // Build tables for keys [first, first + nkeys) whose 32-byte encodings are
-// already in d_key_pk.
+// already in d_key_pk, in slices of kKeyBuildSlice keys (bounded scratch).
+constexpr uint64_t kKeyBuildScratch = 128ull << 20;  // bytes of row bases + prefix products per slice
+template <int W>
+static int keys_build_w(edv_ctx* ctx, uint64_t first, uint64_t nkeys, hipStream_t st) {
+  constexpr int R = Window<W>::kRows, E = Window<W>::kEntries;
+  constexpr uint64_t per_key = (uint64_t)R * kRowWords * 4 + (uint64_t)R * E * 10 * 4;
+  const uint64_t max_slice = kKeyBuildScratch / per_key > 0 ? kKeyBuildScratch / per_key : 1;
+  const uint64_t slice = nkeys < max_slice ? nkeys : max_slice;
+  int r;
+  // rows: R p3 bases per key; pre: E prefix products per row
+  if ((r = ensure(ctx->b_aux, slice * R * kRowWords * 4 + slice * R * E * 10 * 4))) return r;
+  uint32_t* rows = (uint32_t*)ctx->b_aux.p;
+  uint32_t* pre = rows + slice * R * kRowWords;
+  for (uint64_t k0 = 0; k0 < nkeys; k0 += slice) {
+    const uint64_t kn = nkeys - k0 < slice ? nkeys - k0 : slice;
+    const uint64_t k = first + k0;
+    hipLaunchKernelGGL(edv_key_rows_kernel<W>, dim3((uint32_t)div_up(kn, kBlock)), dim3(kBlock), 0, st,
+                       ctx->d_key_pk + 32 * k, kn, rows, ctx->d_key_valid + k);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(edv_comb_fill_kernel<W>, dim3((uint32_t)div_up(kn * R * FillShape<W>::NCH, kBlock)),
+                       dim3(kBlock), 0, st, rows, kn * R, ctx->d_key_tab + k * (uint64_t)Window<W>::kTableWords, pre);
+    HIP_TRY(hipGetLastError());
+  }
+  return 0;
+}
+
 static int keys_build(edv_ctx* ctx, uint64_t first, uint64_t nkeys, hipStream_t st) {
   if (!nkeys) return 0;
-  int r;
-  // rows: 64 p3 bases per key; pre: 8 prefix products per row
-  constexpr int R = Window<kKeyW>::kRows, E = Window<kKeyW>::kEntries;
-  if ((r = ensure(ctx->b_aux, nkeys * R * kRowWords * 4 + nkeys * R * E * 10 * 4))) return r;
-  uint32_t* rows = (uint32_t*)ctx->b_aux.p;
-  uint32_t* pre = rows + nkeys * R * kRowWords;
-  hipLaunchKernelGGL(edv_key_rows_kernel, dim3((uint32_t)div_up(nkeys, kBlock)), dim3(kBlock), 0, st,
-                     ctx->d_key_pk + 32 * first, nkeys, rows, ctx->d_key_valid + first);
-  HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(edv_key_fill_kernel, dim3((uint32_t)div_up(nkeys * R, kBlock)), dim3(kBlock), 0, st, rows,
-                     nkeys * R, ctx->d_key_tab + first * (uint64_t)kKeyTabWords, pre);
-  HIP_TRY(hipGetLastError());
-  return 0;
+  switch (ctx->key_w) {
+    case 4: return keys_build_w<4>(ctx, first, nkeys, st);
+    case 6: return keys_build_w<6>(ctx, first, nkeys, st);
+    case 10: return keys_build_w<10>(ctx, first, nkeys, st);
+    default: return keys_build_w<8>(ctx, first, nkeys, st);
+  }
 }
 
 static int launch_verify_keyed(edv_ctx* ctx, const void* d_sig, const void* d_kidx, const void* d_msgs,
@@ -621,18 +713,31 @@ static int launch_verify_keyed(edv_ctx* ctx, const void* d_sig, const void* d_ki
     const uint32_t grid = (uint32_t)div_up(cn, kBlock);
     const bool last = c0 + cn >= n;
     hipLaunchKernelGGL(edv_hash_keyed_kernel, dim3(grid), dim3(kBlock), 0, st, sig + 64 * c0, kidx + c0, kc,
-                       ctx->d_key_pk, (const uint8_t*)d_msgs, off + c0, cn, ctx->d_hsoa, ctx->d_flags, chunk);
+                       ctx->d_key_pk, ctx->d_key_valid, (const uint8_t*)d_msgs, off + c0, cn, ctx->d_hsoa,
+                       ctx->d_flags, chunk);
     HIP_TRY(hipGetLastError());
     if (last) {
       HIP_TRY(hipEventRecord(ctx->ev[1], st));
       HIP_TRY(hipEventRecord(ctx->ev[2], st));
     }
-    hipLaunchKernelGGL(edv_comb_kernel, dim3(grid), dim3(kBlock), 0, st, sig + 64 * c0, kidx + c0, kc, cn,
-                       ctx->d_hsoa, ctx->d_flags, ctx->d_key_valid, ctx->d_key_tab, ctx->d_btab_comb32,
-                       words + c0 / 64, chunk);
+#define EDV_COMB_LAUNCH(W)                                                                                   \
+  hipLaunchKernelGGL(edv_comb_kernel<W>, dim3(grid), dim3(kBlock), 0, st, sig + 64 * c0, kidx + c0, kc, cn, \
+                     ctx->d_hsoa, ctx->d_key_tab, ctx->d_btab_comb32, ctx->d_pt, chunk)
+    if (ctx->key_w == 4)
+      EDV_COMB_LAUNCH(4);
+    else if (ctx->key_w == 6)
+      EDV_COMB_LAUNCH(6);
+    else if (ctx->key_w == 10)
+      EDV_COMB_LAUNCH(10);
+    else
+      EDV_COMB_LAUNCH(8);
+#undef EDV_COMB_LAUNCH
     HIP_TRY(hipGetLastError());
+    if (last) HIP_TRY(hipEventRecord(ctx->ev[3], st));
+    int r = launch_encode(ctx, sig + 64 * c0, cn, words + c0 / 64, chunk, st);
+    if (r) return r;
   }
-  HIP_TRY(hipEventRecord(ctx->ev[3], st));
+  HIP_TRY(hipEventRecord(ctx->ev[4], st));
   ctx->timed = true;
   return 0;
 }
@@ -680,6 +785,27 @@ int edv_keys_reset(edv_ctx* ctx) {
   ctx->key_count = 0;
   return 0;
 }
+
+int edv_keys_set_window(edv_ctx* ctx, int w) {
+  int r = set_device(ctx);
+  if (r) return r;
+  if (w != 4 && w != 6 && w != 8 && w != 10) return set_err(EDV_EINVAL, "key window %d (4, 6, 8 or 10)", w);
+  if (ctx->key_count) return set_err(EDV_EINVAL, "key window change with %llu keys registered (edv_keys_reset first)",
+                                     (unsigned long long)ctx->key_count);
+  if (w == ctx->key_w) return 0;
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  if (ctx->d_key_tab) (void)hipFree(ctx->d_key_tab);
+  if (ctx->d_key_pk) (void)hipFree(ctx->d_key_pk);
+  if (ctx->d_key_valid) (void)hipFree(ctx->d_key_valid);
+  ctx->d_key_tab = nullptr;
+  ctx->d_key_pk = nullptr;
+  ctx->d_key_valid = nullptr;
+  ctx->key_cap = 0;
+  ctx->key_w = w;
+  return 0;
+}
+
+int edv_keys_window(edv_ctx* ctx) { return ctx ? ctx->key_w : -1; }
 
 int edv_verify_batch_keyed_device(edv_ctx* ctx, const void* d_sig64, const void* d_key_idx, const void* d_msgs,
                                   const void* d_msg_off, uint64_t n, void* d_accept_words, void* stream) {
@@ -757,12 +883,9 @@ edv_ctx* edv_create(int device) {
   // A blocking stream: it is ordered against the legacy NULL stream, which is
   // where PyTorch's default-stream copies that produce our inputs run.
   if ((e = hipStreamCreate(&ctx->stream)) != hipSuccess) return fail("hipStreamCreate", e);
-  for (int k = 0; k < 4; ++k)
+  for (int k = 0; k < edv_ctx::kEv; ++k)
     if ((e = hipEventCreate(&ctx->ev[k])) != hipSuccess) return fail("hipEventCreate", e);
-  if ((e = hipMalloc(&ctx->d_btab_small, sizeof(BASE_SMALL_U32))) != hipSuccess) return fail("hipMalloc", e);
   if ((e = hipMalloc(&ctx->d_btab_comb, sizeof(BASE_COMB_U32))) != hipSuccess) return fail("hipMalloc", e);
-  if ((e = hipMemcpy(ctx->d_btab_small, BASE_SMALL_U32, sizeof(BASE_SMALL_U32), hipMemcpyHostToDevice)) != hipSuccess)
-    return fail("hipMemcpy", e);
   if ((e = hipMemcpy(ctx->d_btab_comb, BASE_COMB_U32, sizeof(BASE_COMB_U32), hipMemcpyHostToDevice)) != hipSuccess)
     return fail("hipMemcpy", e);
   {
@@ -773,7 +896,8 @@ edv_ctx* edv_create(int device) {
     if ((e = hipMalloc(&rows, rowsB * kRowWords * 4)) != hipSuccess) return fail("hipMalloc", e);
     if ((e = hipMalloc(&pre, (size_t)rowsB * EB * 10 * 4)) != hipSuccess) return fail("hipMalloc", e);
     hipLaunchKernelGGL(edv_base_rows_kernel, dim3(1), dim3(64), 0, ctx->stream, rows);
-    hipLaunchKernelGGL(edv_base_fill_kernel, dim3(1), dim3(64), 0, ctx->stream, rows, ctx->d_btab_comb32, pre);
+    hipLaunchKernelGGL(edv_comb_fill_kernel<kBaseW>, dim3((uint32_t)div_up(rowsB * FillShape<kBaseW>::NCH, kBlock)),
+                       dim3(kBlock), 0, ctx->stream, rows, (uint64_t)rowsB, ctx->d_btab_comb32, pre);
     e = hipStreamSynchronize(ctx->stream);
     (void)hipFree(rows);
     (void)hipFree(pre);
@@ -785,6 +909,14 @@ edv_ctx* edv_create(int device) {
   if ((e = hipMalloc(&ctx->d_hsoa, ctx->scratch_lanes * 8 * sizeof(uint32_t))) != hipSuccess)
     return fail("hipMalloc(h)", e);
   if ((e = hipMalloc(&ctx->d_flags, ctx->scratch_lanes)) != hipSuccess) return fail("hipMalloc(flags)", e);
+  if ((e = hipMalloc(&ctx->d_pt, ctx->scratch_lanes * 30 * sizeof(uint32_t))) != hipSuccess)
+    return fail("hipMalloc(pt)", e);
+  if ((e = hipMalloc(&ctx->d_pre, ctx->scratch_lanes * 10 * sizeof(uint32_t))) != hipSuccess)
+    return fail("hipMalloc(pre)", e);
+  if (const char* w = getenv("EDV_KEY_WINDOW")) {
+    const int kw = atoi(w);
+    if (kw == 4 || kw == 6 || kw == 8 || kw == 10) ctx->key_w = kw;
+  }
   return ctx;
 }
 
@@ -797,13 +929,14 @@ void edv_destroy(edv_ctx* ctx) {
   if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
   if (ctx->d_hsoa) (void)hipFree(ctx->d_hsoa);
   if (ctx->d_flags) (void)hipFree(ctx->d_flags);
-  if (ctx->d_btab_small) (void)hipFree(ctx->d_btab_small);
+  if (ctx->d_pt) (void)hipFree(ctx->d_pt);
+  if (ctx->d_pre) (void)hipFree(ctx->d_pre);
   if (ctx->d_btab_comb) (void)hipFree(ctx->d_btab_comb);
   if (ctx->d_btab_comb32) (void)hipFree(ctx->d_btab_comb32);
   if (ctx->d_key_pk) (void)hipFree(ctx->d_key_pk);
   if (ctx->d_key_valid) (void)hipFree(ctx->d_key_valid);
   if (ctx->d_key_tab) (void)hipFree(ctx->d_key_tab);
-  for (int k = 0; k < 4; ++k)
+  for (int k = 0; k < edv_ctx::kEv; ++k)
     if (ctx->ev[k]) (void)hipEventDestroy(ctx->ev[k]);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -825,11 +958,22 @@ int edv_verify_batch_device(edv_ctx* ctx, const void* d_sig64, const void* d_pk3
   return launch_verify(ctx, d_sig64, d_pk32, d_msgs, d_msg_off, n, d_accept_words, pick_stream(ctx, stream));
 }
 
-int edv_last_phase_ms(edv_ctx* ctx, double* hash_ms, double* table_ms, double* dsm_ms) {
+int edv_last_phases_ms(edv_ctx* ctx, double* out4) {
   if (!ctx || !ctx->timed) return set_err(EDV_EINVAL, "no timed verify launch yet");
-  HIP_TRY(hipEventSynchronize(ctx->ev[3]));
-  float t[3] = {0.f, 0.f, 0.f};
-  for (int k = 0; k < 3; ++k) HIP_TRY(hipEventElapsedTime(&t[k], ctx->ev[k], ctx->ev[k + 1]));
+  if (!out4) return set_err(EDV_EINVAL, "null output");
+  HIP_TRY(hipEventSynchronize(ctx->ev[edv_ctx::kEv - 1]));
+  for (int k = 0; k < edv_ctx::kEv - 1; ++k) {
+    float t = 0.f;
+    HIP_TRY(hipEventElapsedTime(&t, ctx->ev[k], ctx->ev[k + 1]));
+    out4[k] = t;
+  }
+  return 0;
+}
+
+int edv_last_phase_ms(edv_ctx* ctx, double* hash_ms, double* table_ms, double* dsm_ms) {
+  double t[4];
+  int r = edv_last_phases_ms(ctx, t);
+  if (r) return r;
   if (hash_ms) *hash_ms = t[0];
   if (table_ms) *table_ms = t[1];
   if (dsm_ms) *dsm_ms = t[2];

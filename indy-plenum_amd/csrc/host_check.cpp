@@ -6,6 +6,7 @@
 
 #include <vector>
 
+#include "batch_encode.h"
 #include "comb.h"
 #include "verify_core.h"
 
@@ -17,14 +18,44 @@ struct HostTableA {
   void store(int j, const ge_cached& c) { e[j] = c; }
   void load(int j, ge_cached& c) const { c = e[j]; }
 };
-struct HostTableB {
-  void load(int j, ge_niels& n) const {
-    const uint32_t* p = BASE_SMALL_U32 + 30 * j;
+// A comb table in host memory (comb.h layout).
+template <int W>
+struct HostComb {
+  const uint32_t* tab;
+  void load(int row, int j, ge_niels& n) const {
+    const uint32_t* p = tab + ((size_t)row * Window<W>::kEntries + j) * kEntryWords;
     memcpy(n.ypx.v, p, 40);
     memcpy(n.ymx.v, p + 10, 40);
     memcpy(n.xy2d.v, p + 20, 40);
   }
 };
+
+std::vector<uint32_t> g_btab;  // W = 8 comb of B, built by the device code on first use
+
+template <int W>
+void build_table(std::vector<uint32_t>& tab, const ge_p3& P) {
+  constexpr int rows = Window<W>::kRows, E = Window<W>::kEntries;
+  std::vector<uint32_t> rw(rows * 40), pre(32 * 10);
+  tab.assign((size_t)rows * E * kEntryWords, 0);
+  comb_rows<W>(rw.data(), P);
+  // strided lanes of up to 32 entries, as edv_comb_fill_kernel fills them
+  const int CH = E < 32 ? E : 32, NCH = E / CH;
+  for (int r = 0; r < rows; ++r)
+    for (int c = 0; c < NCH; ++c)
+      comb_fill_strided(&tab[(size_t)r * E * kEntryWords], pre.data(), 10, &rw[r * 40], c, NCH, CH);
+}
+
+const uint32_t* base_comb() {
+  if (g_btab.empty()) {
+    uint32_t b[8];
+    for (int k = 0; k < 8; ++k) b[k] = 0x66666666u;
+    b[0] = 0x66666658u;
+    ge_p3 B;
+    ge_frombytes(B, b, false);
+    build_table<kBaseW>(g_btab, B);
+  }
+  return g_btab.data();
+}
 }  // namespace
 
 extern "C" {
@@ -34,8 +65,8 @@ int edv_host_verify(const uint8_t* sig64, const uint8_t* pk32, const uint8_t* ms
   memcpy(sig, sig64, 64);
   memcpy(pk, pk32, 32);
   HostTableA ta;
-  HostTableB tb;
-  return verify_one(sig, pk, msg, mlen, ta, tb) ? 0 : -1;
+  const HostComb<kBaseW> cb{base_comb()};
+  return verify_one(sig, pk, msg, mlen, ta, cb) ? 0 : -1;
 }
 
 void edv_host_sha512_prefixed(uint8_t out[64], const uint8_t prefix64[64], const uint8_t* msg, uint64_t mlen) {
@@ -110,71 +141,142 @@ int edv_host_is_canonical_point(const uint8_t s[32]) {
   return is_canonical_point(w);
 }
 
-// The key-table (comb) path on the CPU: build the W = 4 table of -A and the
-// W = 8 table of B with the device code, then [h](-A) + [S]B by the comb.
-static std::vector<uint32_t> g_btab;
+}  // extern "C"
 
-static void build_table(std::vector<uint32_t>& tab, const ge_p3& P, int W) {
-  const int rows = W == 4 ? Window<4>::kRows : Window<8>::kRows;
-  const int E = W == 4 ? Window<4>::kEntries : Window<8>::kEntries;
-  std::vector<uint32_t> rw(rows * 40), pre(E * 10);
-  tab.assign((size_t)rows * E * kEntryWords, 0);
-  if (W == 4) comb_rows<4>(rw.data(), P); else comb_rows<8>(rw.data(), P);
-  for (int r = 0; r < rows; ++r) {
-    if (W == 4) comb_fill_row<4>(&tab[(size_t)r * E * kEntryWords], pre.data(), &rw[r * 40]);
-    else comb_fill_row<8>(&tab[(size_t)r * E * kEntryWords], pre.data(), &rw[r * 40]);
-  }
-}
-
-static void comb_add(ge_p3& Q, int e, const uint32_t* row) {
-  const int m = e < 0 ? -e : e;
-  ge_niels nb;
-  ge_niels_0(nb);
-  if (m) {
-    const uint32_t* p = row + (m - 1) * kEntryWords;
-    load_fe(nb.ypx, p);
-    load_fe(nb.ymx, p + 10);
-    load_fe(nb.xy2d, p + 20);
-  }
-  if (e < 0) {
-    fe t = nb.ypx;
-    nb.ypx = nb.ymx;
-    nb.ymx = t;
-    fe_neg(nb.xy2d, nb.xy2d);
-  }
-  ge_p1p1 t;
-  ge_madd(t, Q, nb);
-  ge_p1p1_to_p3_addlike(Q, t);
-}
-
-int edv_host_verify_comb(const uint8_t* sig64, const uint8_t* pk32, const uint8_t* msg, uint64_t mlen) {
-  uint32_t sig[16], pk[8], h[8], hy[8], sy[8];
-  memcpy(sig, sig64, 64);
-  memcpy(pk, pk32, 32);
-  if (g_btab.empty()) {
-    uint32_t b[8];
-    for (int k = 0; k < 8; ++k) b[k] = 0x66666666u;
-    b[0] = 0x66666658u;
-    ge_p3 B;
-    ge_frombytes(B, b, false);
-    build_table(g_btab, B, 8);
-  }
+// The key-table (comb) path on the CPU: build the W-window table of -A and
+// the W = 8 table of B with the device code, then [h](-A) + [S]B by the comb
+// (comb_mul_add, the kernel's code).  Result point and the combined prechecks.
+template <int W>
+static bool comb_point(ge_p3& Q, const uint32_t sig[16], const uint32_t pk[8], const uint8_t* msg, uint64_t mlen) {
+  uint32_t h[8];
   bool ok = verify_phase_hash(h, sig, pk, msg, mlen);
   ge_p3 A;
   ok = ge_frombytes(A, pk, true) && is_canonical_point(pk) && !has_small_order(pk) && ok;
   std::vector<uint32_t> atab;
-  build_table(atab, A, 4);
-  comb_recode<4>(hy, h);
-  comb_recode<8>(sy, sig + 8);
-  ge_p3 Q;
+  build_table<W>(atab, A);
   ge_p3_0(Q);
-  for (int r = 0; r < Window<4>::kRows; ++r) comb_add(Q, comb_digit<4>(hy, r), &atab[(size_t)r * 8 * kEntryWords]);
-  for (int r = 0; r < Window<8>::kRows; ++r) comb_add(Q, comb_digit<8>(sy, r), &g_btab[(size_t)r * 128 * kEntryWords]);
-  ge_p2 r2;
-  ge_p3_to_p2(r2, Q);
-  uint32_t rc[8];
-  ge_tobytes(rc, r2);
-  return (ok && memcmp(rc, sig, 32) == 0) ? 0 : -1;
+  comb_mul_add<W>(Q, h, HostComb<W>{atab.data()});
+  comb_mul_add<kBaseW>(Q, sig + 8, HostComb<kBaseW>{base_comb()});
+  return ok;
+}
+
+static bool comb_point_w(int w, ge_p3& Q, const uint32_t sig[16], const uint32_t pk[8], const uint8_t* msg,
+                         uint64_t mlen) {
+  switch (w) {
+    case 4: return comb_point<4>(Q, sig, pk, msg, mlen);
+    case 5: return comb_point<5>(Q, sig, pk, msg, mlen);
+    case 6: return comb_point<6>(Q, sig, pk, msg, mlen);
+    case 7: return comb_point<7>(Q, sig, pk, msg, mlen);
+    case 9: return comb_point<9>(Q, sig, pk, msg, mlen);
+    case 10: return comb_point<10>(Q, sig, pk, msg, mlen);
+    case 11: return comb_point<11>(Q, sig, pk, msg, mlen);
+    case 12: return comb_point<12>(Q, sig, pk, msg, mlen);
+    default: return comb_point<8>(Q, sig, pk, msg, mlen);
+  }
+}
+
+extern "C" {
+
+int edv_host_verify_comb_w(const uint8_t* sig64, const uint8_t* pk32, const uint8_t* msg, uint64_t mlen, int w) {
+  uint32_t sig[16], pk[8];
+  memcpy(sig, sig64, 64);
+  memcpy(pk, pk32, 32);
+  ge_p3 Q;
+  const bool ok = comb_point_w(w, Q, sig, pk, msg, mlen);
+  return (ok && encode_equals(Q, sig)) ? 0 : -1;
+}
+
+int edv_host_verify_comb(const uint8_t* sig64, const uint8_t* pk32, const uint8_t* msg, uint64_t mlen) {
+  return edv_host_verify_comb_w(sig64, pk32, msg, mlen, 4);
+}
+
+}  // extern "C"
+
+template <int W>
+static int digits_w(const uint32_t x[8], int* out) {
+  uint32_t y[9];
+  comb_recode<W>(y, x);
+  for (int r = 0; r < Window<W>::kRows; ++r) out[r] = comb_digit<W>(y, r);
+  return Window<W>::kRows;
+}
+
+extern "C" {
+
+// comb.h signed radix-2^W digits of a 32-byte scalar; returns the row count.
+int edv_host_comb_digits(const uint8_t x32[32], int w, int* out) {
+  uint32_t x[8];
+  memcpy(x, x32, 32);
+  switch (w) {
+    case 4: return digits_w<4>(x, out);
+    case 5: return digits_w<5>(x, out);
+    case 6: return digits_w<6>(x, out);
+    case 7: return digits_w<7>(x, out);
+    case 8: return digits_w<8>(x, out);
+    case 9: return digits_w<9>(x, out);
+    case 10: return digits_w<10>(x, out);
+    case 11: return digits_w<11>(x, out);
+    case 12: return digits_w<12>(x, out);
+    case 13: return digits_w<13>(x, out);
+    case 14: return digits_w<14>(x, out);
+    default: return -1;
+  }
+}
+
+}  // extern "C"
+
+// The batched encode (batch_encode.h) over groups of M = 16 consecutive items,
+// as edv_encode_kernel runs it per lane.  zero_z[i] != 0 forces item i's Z to
+// 0 (exercises the poisoned-group guard).  Bits: 1 = accept.
+namespace {
+struct HostEncode {
+  const std::vector<ge_p3>* Q;
+  std::vector<fe>* pre;
+  const uint32_t* R;       // 16 words per item (sig)
+  const uint8_t* ok;
+  uint8_t* bits;
+  uint64_t base, n;
+  bool valid(int j) const { return base + j < n; }
+  void z(int j, fe& f) const { f = (*Q)[base + j].Z; }
+  void xy(int j, fe& X, fe& Y) const {
+    X = (*Q)[base + j].X;
+    Y = (*Q)[base + j].Y;
+  }
+  void put_pre(int j, const fe& f) const {
+    if (valid(j)) (*pre)[base + j] = f;
+  }
+  void get_pre(int j, fe& f) const {
+    if (valid(j)) f = (*pre)[base + j]; else fe_1(f);
+  }
+  void emit(int j, const uint32_t enc[8], bool zero_z) const {
+    if (!valid(j)) return;
+    const uint64_t i = base + j;
+    const bool acc = !zero_z && ok[i] && memcmp(enc, R + 16 * i, 32) == 0;
+    if (acc) bits[i / 8] |= (uint8_t)(1u << (i % 8));
+  }
+};
+}  // namespace
+
+extern "C" {
+
+int edv_host_verify_batch_comb(const uint8_t* sig64, const uint8_t* pk32, const uint8_t* msgs, const uint64_t* off,
+                               uint64_t n, int w, const uint8_t* zero_z, uint8_t* bits) {
+  std::vector<ge_p3> Q(n);
+  std::vector<fe> pre(n);
+  std::vector<uint32_t> sig(16 * n);
+  std::vector<uint8_t> ok(n);
+  memcpy(sig.data(), sig64, 64 * n);
+  for (uint64_t i = 0; i < n; ++i) {
+    uint32_t pk[8];
+    memcpy(pk, pk32 + 32 * i, 32);
+    ok[i] = comb_point_w(w, Q[i], &sig[16 * i], pk, msgs + off[i], off[i + 1] - off[i]);
+    if (zero_z && zero_z[i]) fe_0(Q[i].Z);
+  }
+  memset(bits, 0, (n + 7) / 8);
+  for (uint64_t g = 0; g < n; g += 16) {
+    HostEncode a{&Q, &pre, sig.data(), ok.data(), bits, g, n};
+    encode_batch<16>(a);
+  }
+  return 0;
 }
 
 }  // extern "C"

@@ -35,9 +35,7 @@ static const uint64_t SHA512_K[80] = {
     0x431d67c49c100d4cULL, 0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL};
 
 EDV_HD uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
-EDV_HD uint32_t bswap32(uint32_t x) {
-  return (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
-}
+EDV_HD uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
 EDV_HD void sha512_compress(uint64_t st[8], uint64_t w[16]) {
   uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
@@ -76,54 +74,75 @@ EDV_HD void sha512_compress(uint64_t st[8], uint64_t w[16]) {
   st[7] += h;
 }
 
-// 4 message bytes starting at message byte p (little-endian u32), zero past
-// mlen, with the 0x80 pad byte at position mlen.
-EDV_HD uint32_t msg_word(const uint8_t* msg, uint64_t mlen, uint64_t p) {
-  uint32_t v = 0;
-  if (p < mlen) {
-    const uintptr_t addr = (uintptr_t)(msg + p);
-    const uint32_t* aw = (const uint32_t*)(addr & ~(uintptr_t)3);
-    const uint32_t sh = (uint32_t)(addr & 3);
-    const uint32_t lo = aw[0];
-    uint32_t hi = 0;
-    if (sh != 0 && p + 4 - sh < mlen) hi = aw[1];
-    v = sh ? (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * sh)) : lo;
+// (hi:lo) >> (8 * sh) low word: message word from two aligned words.
+EDV_HD uint32_t funnel8(uint32_t hi, uint32_t lo, uint32_t sh) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_alignbit(hi, lo, 8 * sh);
+#else
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * sh));
+#endif
+}
+
+// One 128-byte block of the stream prefix || msg || 0x80 || 0... as 16
+// big-endian words.  Message word u (bytes 4u..4u+3) = funnel8(A[u+1], A[u], sh)
+// over the aligned words A[k] = aw[k], k < na, of the message's aligned base;
+// no byte past the aligned word holding the last message byte is read.
+// Blocks that reach the end of the message get the tail masked and the 0x80
+// pad byte placed (branch taken per lane only for those blocks).
+template <int NP, bool FIRST>
+EDV_HD void sha512_block_words(uint64_t w[16], uint64_t b, const uint32_t* prefix, const uint32_t* aw, uint64_t na,
+                               uint32_t sh, uint64_t mlen) {
+  const int64_t u0 = 32 * (int64_t)b - NP;  // message word index of stream word 0
+  uint32_t A[33];
+#pragma unroll
+  for (int t = 0; t < 33; ++t) {
+    const int64_t k = u0 + t;
+    if (FIRST && t < NP) {
+      A[t] = 0;
+    } else {
+      A[t] = (k >= 0 && (uint64_t)k < na) ? aw[k] : 0u;
+    }
   }
-  if (p + 4 > mlen) {
-    const uint64_t nvalid = p < mlen ? mlen - p : 0;  // 0..3
-    v &= (uint32_t)((1ull << (8 * nvalid)) - 1);
-    if (p <= mlen) v |= 0x80u << (8 * (uint32_t)(mlen - p));
+  uint32_t le[32];
+#pragma unroll
+  for (int t = 0; t < 32; ++t) le[t] = (FIRST && t < NP) ? prefix[t < NP ? t : 0] : funnel8(A[t + 1], A[t], sh);
+  if (4 * (u0 + 32) > (int64_t)mlen) {
+#pragma unroll
+    for (int t = (FIRST ? NP : 0); t < 32; ++t) {
+      const int64_t rem = (int64_t)mlen - 4 * (u0 + t);  // message bytes left at this word
+      const uint32_t r = rem <= 0 ? 0u : rem >= 4 ? 4u : (uint32_t)rem;
+      const uint32_t keep = r >= 4 ? 0xffffffffu : ((1u << (8 * r)) - 1u);
+      const uint32_t pad = (rem >= 0 && rem < 4) ? (0x80u << (8 * (uint32_t)rem)) : 0u;
+      le[t] = (le[t] & keep) | pad;
+    }
   }
-  return v;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) w[j] = ((uint64_t)bswap32(le[2 * j]) << 32) | bswap32(le[2 * j + 1]);
 }
 
 // SHA-512(prefix || msg).  prefix: NP little-endian u32 words (NP = 8 or 16).
 // digest: 16 little-endian u32 words = the 64 digest bytes in order.
 template <int NP>
 EDV_HD void sha512_prefixed(uint32_t digest[16], const uint32_t prefix[NP], const uint8_t* msg, uint64_t mlen) {
+  static_assert(NP <= 16, "the prefix must fit block 0");
   uint64_t st[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL, 0xa54ff53a5f1d36f1ULL,
                     0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL, 0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
   const uint64_t total = 4 * NP + mlen;            // stream bytes before padding
   const uint64_t nblocks = (total + 16) / 128 + 1;  // incl. 0x80 and 128-bit length
   const uint64_t bitlen = total * 8;
-  // Block 0 holds the whole prefix (NP <= 16 words < 32), so the prefix is
-  // only ever indexed with compile-time indices (no scratch spills).
+  const uint32_t sh = (uint32_t)((uintptr_t)msg & 3);
+  const uint32_t* aw = (const uint32_t*)(msg - sh);  // pointer arithmetic keeps the address space
+  const uint64_t na = (sh + mlen + 3) / 4;
+  uint64_t w[16];
+  sha512_block_words<NP, true>(w, 0, prefix, aw, na, sh, mlen);
+  if (nblocks == 1) {
+    w[14] = 0;
+    w[15] = bitlen;
+  }
+  sha512_compress(st, w);
 #pragma unroll 1
-  for (uint64_t b = 0; b < nblocks; ++b) {
-    uint64_t w[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      uint32_t le[2];
-#pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        const int t0 = 2 * j + half;  // u32 index within the block
-        if (t0 < NP)
-          le[half] = (b == 0) ? prefix[t0] : msg_word(msg, mlen, 4 * (32 * b + t0 - NP));
-        else
-          le[half] = msg_word(msg, mlen, 4 * (32 * b + t0 - NP));
-      }
-      w[j] = ((uint64_t)bswap32(le[0]) << 32) | bswap32(le[1]);
-    }
+  for (uint64_t b = 1; b < nblocks; ++b) {
+    sha512_block_words<NP, false>(w, b, prefix, aw, na, sh, mlen);
     if (b == nblocks - 1) {
       w[14] = 0;
       w[15] = bitlen;

@@ -15,6 +15,7 @@
 // The same code is compiled for gfx950 (the product kernels) and for the host
 // (csrc/host_selftest.cpp) so the arithmetic can be checked on a CPU.
 #pragma once
+#include "comb.h"
 #include "ge25519.h"
 #include "sc25519.h"
 #include "sha512.h"
@@ -105,17 +106,18 @@ EDV_HD bool verify_phase_table(const uint32_t pk[8], TA& ta) {
   return ok;
 }
 
-// Phase 3: encode([h](-A) + [S]B) == R, signed radix-16 windows, 4 doublings
-// per digit.  TA::load(j, ge_cached&) gives (j+1)(-A); TB::load(j, ge_niels&)
-// gives (j+1)B.
-template <class TA, class TB>
-EDV_HD bool verify_phase_dsm(const uint32_t h[8], const uint32_t S[8], const uint32_t R[8], const TA& ta,
-                             const TB& tb) {
-  uint32_t hy[8], sy[8];
+// Phase 3: R' = [h](-A) + [S]B.  [h](-A): signed radix-16 windows, 4
+// doublings per digit, TA::load(j, ge_cached&) gives (j+1)(-A).  [S]B: the
+// W = 8 fixed-base comb of B (CB::load(row, j, ge_niels&), comb.h), 32 mixed
+// additions and no doublings of its own.
+#ifndef EDV_BASE_W
+#define EDV_BASE_W 16
+#endif
+constexpr int kBaseW = EDV_BASE_W;  // base-point comb window: 16 rows x 32768 entries (64 MiB)
+template <class TA, class CB>
+EDV_HD void verify_phase_dsm_point(ge_p3& Q, const uint32_t h[8], const uint32_t S[8], const TA& ta, const CB& cb) {
+  uint32_t hy[8];
   sc_recode16(hy, h);
-  sc_recode16(sy, S);
-
-  ge_p3 Q;
   ge_p3_0(Q);
   ge_p1p1 t;
 #pragma unroll 1
@@ -132,39 +134,25 @@ EDV_HD bool verify_phase_dsm(const uint32_t h[8], const uint32_t S[8], const uin
       ge_p2_dbl(t, q2);
       ge_dbl_to_p3(Q, t);
     }
-    // + digit_i(h) * (-A)
-    {
-      const int e = recode_digit(hy, i);
-      const int m = e < 0 ? -e : e;
-      ge_cached c;
-      ge_cached_0(c);
-      if (m != 0) ta.load(m - 1, c);
-      if (e < 0) {
-        fe tmp = c.YplusX;
-        c.YplusX = c.YminusX;
-        c.YminusX = tmp;
-        fe_neg(c.T2d, c.T2d);
-      }
-      ge_add(t, Q, c);
-      ge_p1p1_to_p3_addlike(Q, t);
+    const int e = recode_digit(hy, i);
+    const int m = e < 0 ? -e : e;
+    ge_cached c;
+    ge_cached_0(c);
+    if (m != 0) ta.load(m - 1, c);
+    if (e < 0) {
+      fe tmp = c.YplusX;
+      c.YplusX = c.YminusX;
+      c.YminusX = tmp;
+      fe_neg(c.T2d, c.T2d);
     }
-    // + digit_i(S) * B
-    {
-      const int e = recode_digit(sy, i);
-      const int m = e < 0 ? -e : e;
-      ge_niels nb;
-      ge_niels_0(nb);
-      if (m != 0) tb.load(m - 1, nb);
-      if (e < 0) {
-        fe tmp = nb.ypx;
-        nb.ypx = nb.ymx;
-        nb.ymx = tmp;
-        fe_neg(nb.xy2d, nb.xy2d);
-      }
-      ge_madd(t, Q, nb);
-      ge_p1p1_to_p3_addlike(Q, t);
-    }
+    ge_add(t, Q, c);
+    ge_p1p1_to_p3_addlike(Q, t);
   }
+  comb_mul_add<kBaseW>(Q, S, cb);
+}
+
+// encode(R') == R byte for byte (per-request inversion; the kernels batch it).
+EDV_HD bool encode_equals(const ge_p3& Q, const uint32_t R[8]) {
   ge_p2 r2;
   ge_p3_to_p2(r2, Q);
   uint32_t rcheck[8];
@@ -173,6 +161,14 @@ EDV_HD bool verify_phase_dsm(const uint32_t h[8], const uint32_t S[8], const uin
 #pragma unroll
   for (int k = 0; k < 8; ++k) eq = eq && rcheck[k] == R[k];
   return eq;
+}
+
+template <class TA, class CB>
+EDV_HD bool verify_phase_dsm(const uint32_t h[8], const uint32_t S[8], const uint32_t R[8], const TA& ta,
+                             const CB& cb) {
+  ge_p3 Q;
+  verify_phase_dsm_point(Q, h, S, ta, cb);
+  return encode_equals(Q, R);
 }
 
 // All three phases for one request (host self-test and the fused kernel).

@@ -27,12 +27,15 @@ SIGNATURES = {
     "edv_verify_batch": (_I, [_P, _P, _P, _P, _P, _U64, _P]),
     "edv_sign_open_batch": (_I, [_P, _P, _P, _P, _U64, _P]),
     "edv_verify_batch_device": (_I, [_P, _P, _P, _P, _P, _U64, _P, _P]),
+    "edv_last_phases_ms": (_I, [_P, _P]),
     "edv_last_phase_ms": (_I, [_P, _P, _P, _P]),
     "edv_last_kernel_ms": (_c.c_double, [_P]),
     "edv_keys_add": (_I, [_P, _P, _U64, _P]),
     "edv_keys_add_device": (_I, [_P, _P, _U64, _P, _P]),
     "edv_keys_count": (_U64, [_P]),
     "edv_keys_reset": (_I, [_P]),
+    "edv_keys_set_window": (_I, [_P, _I]),
+    "edv_keys_window": (_I, [_P]),
     "edv_verify_batch_keyed": (_I, [_P, _P, _P, _P, _P, _U64, _P]),
     "edv_verify_batch_keyed_device": (_I, [_P, _P, _P, _P, _P, _U64, _P, _P]),
     "edv_seed_keypair_batch": (_I, [_P, _P, _U64, _P, _P]),

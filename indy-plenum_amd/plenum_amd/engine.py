@@ -158,10 +158,26 @@ class EdVerifyEngine:
         check(self._lib.edv_last_phase_ms(self._ctx, ctypes.byref(h), ctypes.byref(t), ctypes.byref(d)))
         return h.value, t.value, d.value
 
+    def last_phases_ms(self):
+        """(hash, table, dsm-or-comb, encode) milliseconds of the last verify
+        launch, from HIP events on the launch stream."""
+        out = (ctypes.c_double * 4)()
+        check(self._lib.edv_last_phases_ms(self._ctx, out))
+        return tuple(out)
+
     # ------------------------------------------------------------ key tables
+    def keys_set_window(self, w):
+        """Comb window of the key tables: 4 (64 KiB/key, 64 additions per
+        verify), 6 (172 KiB, 43) or 8 (512 KiB, 32).  Only with no keys."""
+        check(self._lib.edv_keys_set_window(self._ctx, int(w)))
+
+    @property
+    def keys_window(self):
+        return int(self._lib.edv_keys_window(self._ctx))
+
     def keys_add(self, pk32):
-        """Register public keys (64 KiB fixed-base table each); returns the
-        first key id (ids are consecutive)."""
+        """Register public keys (a fixed-base comb table each, edverify.h);
+        returns the first key id (ids are consecutive)."""
         pk32 = _u8(pk32, 32)
         first = ctypes.c_uint64()
         check(self._lib.edv_keys_add(self._ctx, _ptr(pk32), pk32.shape[0], ctypes.byref(first)))

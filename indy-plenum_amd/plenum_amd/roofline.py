@@ -7,8 +7,9 @@ a priori from libsodium's ref10 algorithm, not from this implementation:
     = 2,510 (double-scalar multiplication) + 270 (decode A) + 270 (encode's inversion)
   one field op = 100 32x32->64 multiply-adds  ->  305,000 MAD per verify
   SHA-512 = 5,000 32-bit ALU ops per 128-byte block, ceil((mlen + 81) / 128) blocks.
-The dominant kernel (edv_dsm_kernel) carries the double-scalar multiplication
-and the encode: (2,510 + 267) * 100 = 277,700 MAD per verify.
+The general path's dominant kernel (edv_dsm_kernel) carries the double-scalar
+multiplication: 2,510 * 100 = 251,000 MAD per verify; the encode's inversion
+is shared by 16 requests in edv_encode_kernel (batch_encode.h).
 
 Peak: v_mad_u64_u32 issues at half rate on gfx950 (64 lane-ops/clk/CU;
 tools/microbench/ubench_int.hip measured 58.7 at 16 waves/CU), so
@@ -19,18 +20,46 @@ FE_DSM = 2510
 FE_DECODE = 270
 FE_ENCODE = 267
 MAD_PER_VERIFY = 305_000
-MAD_DSM_KERNEL = (FE_DSM + FE_ENCODE) * MAD_PER_FE  # 277,700
+# General path: edv_dsm_kernel carries the double-scalar multiplication (the
+# a-priori ref10 count); edv_table_kernel the decode of A.
+MAD_DSM_KERNEL = FE_DSM * MAD_PER_FE  # 251,000
 MAD_TABLE_KERNEL = FE_DECODE * MAD_PER_FE
-# Key-table path (keys registered once): edv_comb_kernel = fixed-base comb over
-# both tables -- 64 rows of the W=4 key table + 32 rows of the W=8 base table --
-# 96 mixed additions x 7 multiplications, plus the encode inversion.
-COMB_ADDS = 64 + 32
-FE_COMB = COMB_ADDS * 7
-MAD_COMB_KERNEL = (FE_COMB + FE_ENCODE) * MAD_PER_FE  # 93,900
-KERNEL_WORK = {
-    "edv_dsm_kernel": "(2510 DSM + 267 encode) field ops x 100, ref10 a-priori count",
-    "edv_comb_kernel": "(96 mixed adds x 7 + 267 encode) field ops x 100, fixed-base comb: 64 key rows (W=4) + 32 base rows (W=8)",
-}
+# Key-table path (keys registered once): edv_comb_kernel<W> = fixed-base combs
+# over both tables -- ceil(254 / W) rows of the key table + ceil(254 / 16) = 16
+# rows of the W = 16 base table (verify_core.h kBaseW) -- one mixed addition
+# (7 multiplications) per row.
+BASE_W = 16
+
+
+def key_rows(w):
+    return (254 + w - 1) // w
+
+
+BASE_ROWS = key_rows(BASE_W)
+
+
+def mad_comb_kernel(w):
+    return (key_rows(w) + BASE_ROWS) * 7 * MAD_PER_FE  # W=10: 29,400; W=8: 33,600
+
+
+# edv_encode_kernel<M>: per request 3 multiplications of Montgomery's trick +
+# 2 (x, y) + the shared inversion (FE_ENCODE) / M.
+def mad_encode_kernel(m):
+    return (5 + FE_ENCODE / m) * MAD_PER_FE
+
+
+MAD_COMB_KERNEL = mad_comb_kernel(10)
+
+
+def kernel_work(name, w=8):
+    if name == "edv_comb_kernel":
+        return ("(%d key rows (W=%d) + %d base rows (W=%d)) mixed additions x 7 field ops x 100 MAD"
+                % (key_rows(w), w, BASE_ROWS, BASE_W))
+    if name == "edv_dsm_kernel":
+        return "2510 field ops (ref10 a-priori double-scalar multiplication) x 100 MAD"
+    return ""
+
+
 SHA_ALU_PER_BLOCK = 5_000
 
 CUS = 256

@@ -90,3 +90,61 @@ def test_kernel_comb_path_on_cpu_matches_golden(hostcheck):
     items = items_of(load_npz("ed25519_edge.npz"))[::3] + items_of(load_npz("ed25519_valid.npz"))[::41]
     for i, (sig, pk, msg, expect) in enumerate(items):
         assert (hostcheck.edv_host_verify_comb(sig, pk, msg, ctypes.c_uint64(len(msg))) == 0) == expect, i
+
+
+@pytest.mark.parametrize("w", [4, 5, 6, 7, 8, 9, 10, 11, 12])
+def test_kernel_comb_windows(hostcheck, w):
+    """comb.h's generic signed radix-2^W recoding (9-word bias; W = 5, 6, 7
+    digits straddle 32-bit words) at every window the key store can use."""
+    items = items_of(load_npz("ed25519_edge.npz"))[::23] + items_of(load_npz("ed25519_valid.npz"))[::97]
+    for i, (sig, pk, msg, expect) in enumerate(items):
+        got = hostcheck.edv_host_verify_comb_w(sig, pk, msg, ctypes.c_uint64(len(msg)), w) == 0
+        assert got == expect, (w, i)
+
+
+def test_kernel_batch_encode(hostcheck):
+    """batch_encode.h (Montgomery's trick over 16 results, the edv_encode_kernel
+    code) gives per-item verdicts: mixed accept/reject groups, a ragged last
+    group, and a poisoned Z = 0 that must reject only its own item."""
+    import numpy as np
+    items = items_of(load_npz("ed25519_valid.npz"))[:23] + items_of(load_npz("ed25519_edge.npz"))[::9]
+    n = len(items)
+    sig = b"".join(s for s, _, _, _ in items)
+    pk = b"".join(k for _, k, _, _ in items)
+    msgs = b"".join(m for _, _, m, _ in items) + b"\0" * 8
+    off = np.zeros(n + 1, np.uint64)
+    off[1:] = np.cumsum([len(m) for _, _, m, _ in items])
+    expect = np.array([e for _, _, _, e in items], bool)
+    for zero_at in (None, 5, n - 1):
+        zz = np.zeros(n, np.uint8)
+        if zero_at is not None:
+            zz[zero_at] = 1
+        bits = ctypes.create_string_buffer((n + 7) // 8)
+        hostcheck.edv_host_verify_batch_comb(sig, pk, msgs, off.ctypes.data_as(ctypes.c_void_p), ctypes.c_uint64(n), 8,
+                                             zz.ctypes.data_as(ctypes.c_void_p), bits)
+        got = np.unpackbits(np.frombuffer(bits.raw, np.uint8), bitorder="little")[:n].astype(bool)
+        want = expect.copy()
+        if zero_at is not None:
+            want[zero_at] = False
+        assert (got == want).all(), (zero_at, np.nonzero(got != want))
+
+
+def test_comb_recoding_exact_up_to_L():
+    """Signed radix-2^W digits (comb.h) reconstruct every scalar below L,
+    including the top of the range where x + bias needs W*rows >= 254 bits
+    (W = 11 with 23 rows would overflow there), and stay in table range."""
+    import ctypes as C
+    from conftest import PKG
+    import os
+    lib = C.CDLL(os.path.join(PKG, "libedv_hostcheck.so"))
+    rng = random.Random(11)
+    xs = [0, 1, L - 1, L - 2, 2**252, 2**252 - 1, L - 2**200] + [rng.randrange(L) for _ in range(300)]
+    xs += [L - 1 - rng.randrange(2**128) for _ in range(100)]
+    for w in range(4, 15):
+        out = (C.c_int * 80)()
+        for x in xs:
+            rows = lib.edv_host_comb_digits(x.to_bytes(32, "little"), w, out)
+            assert rows == -(-254 // w)
+            d = list(out[:rows])
+            assert all(-(1 << (w - 1)) <= v < (1 << (w - 1)) for v in d), (w, x)
+            assert sum(v << (w * i) for i, v in enumerate(d)) == x, (w, hex(x))

@@ -1,5 +1,6 @@
 """A/B timing of library variants on the keyed configs[1] workload.
-usage: python tools/ab_keyed.py lib1.so lib2.so ...  (each run in a child process)"""
+usage: python tools/ab_keyed.py lib1.so[:W] lib2.so[:W] ...  (each run in a child process;
+W = key window, default 8; also times the general path once per library)"""
 import json, os, subprocess, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CHILD = r'''
@@ -9,7 +10,8 @@ sys.path.insert(0, os.path.join(%r, "indy-plenum_amd"))
 from plenum_amd import EdVerifyEngine, pack_messages, synth
 n = 1_000_000
 dev = torch.device("cuda", 0); torch.cuda.set_device(0)
-eng = EdVerifyEngine(0)
+torch.zeros(1, device=dev); torch.cuda.synchronize()
+t0 = time.perf_counter(); eng = EdVerifyEngine(0); create_ms = (time.perf_counter() - t0) * 1e3
 pks, sks = eng.seed_keypair_batch(synth.signer_seeds(1000))
 msgs, kidx, _ = synth.nym_messages(n, pks, alias_len=43)
 buf, off = pack_messages(msgs)
@@ -18,17 +20,34 @@ d_off = torch.from_numpy(off.view(np.int64)).to(dev)
 d_k = torch.from_numpy(kidx.astype(np.int32)).to(dev)
 d_sig = torch.empty((n, 64), dtype=torch.uint8, device=dev)
 eng.sign_batch_device(torch.from_numpy(sks).to(dev), d_k, d_msgs, d_off, n, d_sig)
-eng.keys_add(pks)
+eng.keys_set_window(int(os.environ.get("AB_KEY_WINDOW", "8")))
+t0 = time.perf_counter(); eng.keys_add(pks); kb = (time.perf_counter() - t0) * 1e3
 words = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
+def med(res):
+    a = np.median(np.array(res[2:]), axis=0)
+    return dict(zip(("hash", "table", "core", "encode"), [round(float(x), 4) for x in a]))
 res = []
-for it in range(12):
+for it in range(10):
     eng.verify_batch_keyed_device(d_sig, d_k, d_msgs, d_off, n, words)
-    res.append(eng.last_phase_ms())
+    res.append(eng.last_phases_ms())
 bits = np.unpackbits(words.cpu().numpy().view(np.uint8), bitorder="little")[:n]
-print(json.dumps({"comb_ms": sorted(r[2] for r in res[2:])[len(res[2:])//2], "hash_ms": sorted(r[0] for r in res[2:])[len(res[2:])//2], "all_ok": int(bits.sum()) == n}))
+t0 = time.perf_counter(); eng.keys_reset(); eng.keys_add(pks); kb2 = (time.perf_counter() - t0) * 1e3
+out = {"keyed": med(res), "keyed_ok": int(bits.sum()) == n, "key_build_ms": [round(kb, 2), round(kb2, 2)],
+       "create_ms": round(create_ms, 1)}
+if os.environ.get("AB_GENERAL", "1") == "1":
+    d_pk = torch.from_numpy(pks).to(dev)[d_k.long()].contiguous()
+    words.zero_()
+    res = []
+    for it in range(5):
+        eng.verify_batch_device(d_sig, d_pk, d_msgs, d_off, n, words)
+        res.append(eng.last_phases_ms())
+    bits = np.unpackbits(words.cpu().numpy().view(np.uint8), bitorder="little")[:n]
+    out.update({"general": med(res), "general_ok": int(bits.sum()) == n})
+print(json.dumps(out))
 ''' % ROOT
-for lib in sys.argv[1:]:
-    env = dict(os.environ, PLENUM_EDVERIFY_LIB=os.path.abspath(lib))
+for spec in sys.argv[1:]:
+    lib, _, w = spec.partition(":")
+    env = dict(os.environ, PLENUM_EDVERIFY_LIB=os.path.abspath(lib), AB_KEY_WINDOW=w or "8")
     out = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
     line = [l for l in out.stdout.splitlines() if l.startswith("{")]
-    print(os.path.basename(lib), line[-1] if line else out.stderr[-2000:], flush=True)
+    print(os.path.basename(lib), "W=%s" % (w or "8"), line[-1] if line else out.stderr[-2000:], flush=True)

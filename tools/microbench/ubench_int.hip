@@ -51,6 +51,16 @@ __global__ __launch_bounds__(1024) void kbench(uint32_t* out, uint32_t seed) {
         asm volatile("v_bfe_u32 %0, %0, 3, 26" : "+v"(acc32[j]));
       } else if (KIND == 13) { // v_mul_u32_u24
         asm volatile("v_mul_u32_u24 %0, %0, %1" : "+v"(acc32[j]) : "v"(a));
+      } else if (KIND == 14) { // v_lshl_add_u32
+        asm volatile("v_lshl_add_u32 %0, %0, 4, %1" : "+v"(acc32[j]) : "v"(a));
+      } else if (KIND == 15) { // v_and_b32
+        asm volatile("v_and_b32 %0, %0, %1" : "+v"(acc32[j]) : "v"(a));
+      } else if (KIND == 16) { // v_mov_b32
+        asm volatile("v_mov_b32 %0, %1" : "=v"(acc32[j]) : "v"(acc32[(j + 1) % NACC]));
+      } else if (KIND == 17) { // v_add_co_u32 + v_addc_co_u32 (64-bit add)
+        asm volatile("v_add_co_u32 %0, vcc, %0, %1\n v_addc_co_u32 %2, vcc, %2, 0, vcc" : "+v"(acc32[j]), "+v"(b) : "v"(a) : "vcc");
+      } else if (KIND == 18) { // v_mad_u32_u16
+        asm volatile("v_mad_u32_u16 %0, %1, %2, %0" : "+v"(acc32[j]) : "v"(a), "v"(b));
       }
     }
   }
@@ -96,6 +106,10 @@ int main() {
     run<10>("v_lshl_add_u64", d, blocks, w);
     run<11>("v_alignbit_b32", d, blocks, w);
     run<12>("v_bfe_u32", d, blocks, w);
+    run<14>("v_lshl_add_u32", d, blocks, w);
+    run<15>("v_and_b32", d, blocks, w);
+    run<16>("v_mov_b32", d, blocks, w);
+    run<17>("v_add_co+v_addc", d, blocks, w);
   }
   hipFree(d);
   return 0;
