@@ -57,6 +57,31 @@ EDV_HD void comb_recode(uint32_t y[9], const uint32_t x[8]) {
   }
 }
 
+// (hi:lo) >> s, low word (v_alignbit_b32 on the device).
+EDV_HD uint32_t funnel32(uint32_t hi, uint32_t lo, uint32_t s) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_alignbit(hi, lo, s);
+#else
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> s);
+#endif
+}
+
+// The digits of comb_recode's y, lowest first, by shifting y right W bits per
+// digit: static register indexing only (a per-row select over y, or a
+// private array indexed by the row, ends up in scratch memory).
+template <int W>
+struct CombDigits {
+  uint32_t y[9];
+  EDV_HDM explicit CombDigits(const uint32_t x[8]) { comb_recode<W>(y, x); }
+  EDV_HDM int next() {
+    const int d = (int)(y[0] & ((1u << W) - 1)) - (1 << (W - 1));
+#pragma unroll
+    for (int k = 0; k < 8; ++k) y[k] = funnel32(y[k + 1], y[k], W);
+    y[8] >>= W;
+    return d;
+  }
+};
+
 template <int W>
 EDV_HD int comb_digit(const uint32_t y[9], int i) {
   const int b = W * i;
@@ -71,27 +96,44 @@ EDV_HD int comb_digit(const uint32_t y[9], int i) {
   return (int)(v & ((1u << W) - 1)) - (1 << (W - 1));
 }
 
-// Signed-digit entry: e * T[row] as a niels point (e = 0 gives the identity).
-// T::load(row, j, ge_niels&) gives entry j (= (j+1) * 2^(W*row) * P).
+// Signed-digit entry of row `row` for digit e: T::load(row, j, ge_niels&)
+// gives entry j (= (j+1) * 2^(W*row) * P), or the identity for j = -1 (an
+// address select in the accessors, so no data is shuffled); the sign is
+// applied by ge_madd_signed on Q's side.  A conditional swap of whole fe
+// structs is lowered through scratch memory, so none is done here.
 template <class T>
 EDV_HD void comb_fetch(ge_niels& nb, int e, const T& tab, int row) {
   const int m = e < 0 ? -e : e;
-  if (m != 0)
-    tab.load(row, m - 1, nb);
-  else
-    ge_niels_0(nb);
+  tab.load(row, m - 1, nb);
 }
-EDV_HD void comb_apply(ge_p3& Q, ge_niels nb, int e) {
-  if (e < 0) {
-    const fe tmp = nb.ypx;
-    nb.ypx = nb.ymx;
-    nb.ymx = tmp;
-    fe_neg(nb.xy2d, nb.xy2d);
+#ifndef EDV_SIGNED_MADD
+#define EDV_SIGNED_MADD 0  // 1: fold the sign into ge_madd_signed (p side) instead of selecting the entry
+#endif
+EDV_HD void comb_apply(ge_p3& Q, ge_niels& nb, int e) {
+#if EDV_SIGNED_MADD
+  ge_madd_signed(Q, Q, nb, e < 0);
+#else
+  // -entry = (y-x, y+x, -2dxy): per-limb selects in place (no struct swap)
+  const bool neg = e < 0;
+#pragma unroll
+  for (int l = 0; l < 10; ++l) {
+    const uint32_t p = nb.ypx.v[l], m = nb.ymx.v[l], t = nb.xy2d.v[l];
+    nb.ypx.v[l] = neg ? m : p;
+    nb.ymx.v[l] = neg ? p : m;
+    nb.xy2d.v[l] = neg ? two_p(l) - t : t;
   }
-  ge_p1p1 t;
-  ge_madd(t, Q, nb);
-  ge_p1p1_to_p3_addlike(Q, t);
+  ge_p1p1 u;
+  ge_madd(u, Q, nb);
+  ge_p1p1_to_p3_addlike(Q, u);
+#endif
 }
+
+// The identity as a niels entry (y+x, y-x, 2dxy) = (1, 1, 0), padded to kEntryWords.
+#if defined(__HIPCC__)
+__device__ __constant__ const uint32_t kNielsIdentity[kEntryWords] = {1, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                                                                      1, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+static const uint32_t kNielsIdentityHost[kEntryWords] = {1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 
 // Q += [x]P for x < 2^253 by the comb over P's table: kRows mixed additions
 // (7 multiplications each).  Row r + 1's entry is fetched before row r's
@@ -101,10 +143,9 @@ EDV_HD void comb_apply(ge_p3& Q, ge_niels nb, int e) {
 #endif
 template <int W, class T>
 EDV_HD void comb_mul_add(ge_p3& Q, const uint32_t x[8], const T& tab) {
-  uint32_t y[9];
-  comb_recode<W>(y, x);
+  CombDigits<W> dg(x);
 #if EDV_COMB_PREFETCH
-  int e = comb_digit<W>(y, 0);
+  int e = dg.next();
   ge_niels cur;
   comb_fetch(cur, e, tab, 0);
 #pragma unroll 1
@@ -112,7 +153,7 @@ EDV_HD void comb_mul_add(ge_p3& Q, const uint32_t x[8], const T& tab) {
     ge_niels next;
     int e_next = 0;
     if (r + 1 < Window<W>::kRows) {
-      e_next = comb_digit<W>(y, r + 1);
+      e_next = dg.next();
       comb_fetch(next, e_next, tab, r + 1);
     } else {
       ge_niels_0(next);
@@ -124,10 +165,10 @@ EDV_HD void comb_mul_add(ge_p3& Q, const uint32_t x[8], const T& tab) {
 #else
 #pragma unroll 1
   for (int r = 0; r < Window<W>::kRows; ++r) {
-    const int e = comb_digit<W>(y, r);
+    const int e = dg.next();
     ge_niels nb;
     comb_fetch(nb, e, tab, r);
-    comb_apply(Q, nb, e);
+    comb_apply(Q, nb, e);  // nb is consumed
   }
 #endif
 }

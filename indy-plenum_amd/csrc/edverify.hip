@@ -38,7 +38,7 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr uint64_t kMaxLanes = 1ull << 20;  // scratch lanes (grid-stride beyond)
-constexpr int kTableWords = 8 * 4 * 10;     // [1..8](-A) cached, u32 limbs
+constexpr int kTableWords = 9 * 4 * 10;     // [1..8](-A) cached + the identity (slot 8), u32 limbs
 
 thread_local std::string g_err;
 
@@ -83,8 +83,8 @@ struct DevTableA {
       __builtin_amdgcn_raw_buffer_store_b32(c.T2d.v[l], rsrc, off, (30 + l) * kBlock * 4, 0);
     }
   }
-  __device__ void load(int j, ge_cached& c) const {
-    const int off = lane_off + j * (40 * kBlock * 4);
+  __device__ void load(int j, ge_cached& c) const {  // j = -1: the identity (slot 8)
+    const int off = lane_off + (j >= 0 ? j : 8) * (40 * kBlock * 4);
 #pragma unroll
     for (int l = 0; l < 10; ++l) {
       c.YplusX.v[l] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, off, (0 + l) * kBlock * 4, 0);
@@ -112,7 +112,7 @@ __device__ __forceinline__ void load_words(uint32_t* dst, const uint8_t* src, in
 // ---- split pipeline: hash -> table -> dsm (each kernel gets its own
 // register budget; intermediates are SoA in the context scratch).
 
-__global__ __launch_bounds__(kBlock) void edv_hash_kernel(const uint8_t* __restrict__ sig64,
+__global__ __launch_bounds__(kBlock, 4) void edv_hash_kernel(const uint8_t* __restrict__ sig64,
                                                          const uint8_t* __restrict__ pk32,
                                                          const uint8_t* __restrict__ msgs,
                                                          const uint64_t* __restrict__ msg_off, uint64_t n,
@@ -177,15 +177,21 @@ __device__ __forceinline__ void load_niels(ge_niels& nb, const uint32_t* __restr
 template <int W>
 struct DevComb {
   const uint32_t* __restrict__ tab;
+  const uint32_t* __restrict__ ident;  // kEntryWords-word identity entry (global memory)
   __device__ void load(int row, int j, ge_niels& nb) const {
-    load_niels(nb, tab + ((uint32_t)row * Window<W>::kEntries + (uint32_t)j) * kEntryWords);
+    const uint32_t* p = j >= 0 ? tab + ((uint32_t)row * Window<W>::kEntries + (uint32_t)j) * kEntryWords : ident;
+    load_niels(nb, p);
   }
 };
 
-__global__ __launch_bounds__(kBlock) void edv_dsm_kernel(const uint8_t* __restrict__ sig64, uint64_t n,
+#ifndef EDV_DSM_MIN_WAVES
+#define EDV_DSM_MIN_WAVES 2
+#endif
+__global__ __launch_bounds__(kBlock, EDV_DSM_MIN_WAVES) void edv_dsm_kernel(const uint8_t* __restrict__ sig64, uint64_t n,
                                                         const uint32_t* __restrict__ h_soa,
                                                         uint32_t* __restrict__ table, uint64_t stride,
                                                         const uint32_t* __restrict__ btab_comb,
+                                                        const uint32_t* __restrict__ ident,
                                                         uint32_t* __restrict__ pt) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -194,7 +200,7 @@ __global__ __launch_bounds__(kBlock) void edv_dsm_kernel(const uint8_t* __restri
 #pragma unroll
   for (int k = 0; k < 8; ++k) h[k] = h_soa[k * stride + i];
   const DevTableA ta(table, blockIdx.x, threadIdx.x);
-  const DevComb<kBaseW> cb{btab_comb};
+  const DevComb<kBaseW> cb{btab_comb, ident};
   ge_p3 Q;
   verify_phase_dsm_point(Q, h, S, ta, cb);
   store_point_soa(pt, stride, i, Q);
@@ -277,7 +283,7 @@ __global__ __launch_bounds__(kBlock) void edv_encode_kernel(const uint8_t* __res
 // Base point: W = 8 comb table (512 KiB) built once per context by the same
 // kernels.
 #ifndef EDV_COMB_MIN_WAVES
-#define EDV_COMB_MIN_WAVES 3  // 168 VGPRs, 3 waves/SIMD: 2% faster than 2 (tools/ab_keyed.py)
+#define EDV_COMB_MIN_WAVES 4  // 128 VGPRs: 1M lanes = 3.8 rounds of 262k (3 waves: 5.1 rounds -> 15% tail); -11% vs 3 (tools/ab_keyed.py)
 #endif
 constexpr int kBaseTabWords = Window<kBaseW>::kTableWords;  // 131072 words at W = 8
 constexpr int kRowWords = 40;
@@ -329,7 +335,7 @@ __global__ void edv_base_rows_kernel(uint32_t* __restrict__ rows) {
   comb_rows<kBaseW>(rows, P);
 }
 #ifndef EDV_HASH_MIN_WAVES
-#define EDV_HASH_MIN_WAVES 3  // 0.71 vs 0.84 ms per 1M at 2 (tools/ab_keyed.py), despite an 88-B spill
+#define EDV_HASH_MIN_WAVES 4  // 115 VGPRs since the branch-free schedule (sha512.h)
 #endif
 __global__ __launch_bounds__(kBlock, EDV_HASH_MIN_WAVES) void edv_hash_keyed_kernel(const uint8_t* __restrict__ sig64,
                                                                const uint32_t* __restrict__ key_idx,
@@ -362,6 +368,7 @@ __global__ __launch_bounds__(kBlock, EDV_COMB_MIN_WAVES) void edv_comb_kernel(co
                                                          uint64_t n, const uint32_t* __restrict__ h_soa,
                                                          const uint32_t* __restrict__ key_tab,
                                                          const uint32_t* __restrict__ btab,
+                                                         const uint32_t* __restrict__ ident,
                                                          uint32_t* __restrict__ pt, uint64_t stride) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -371,8 +378,8 @@ __global__ __launch_bounds__(kBlock, EDV_COMB_MIN_WAVES) void edv_comb_kernel(co
   for (int k = 0; k < 8; ++k) h[k] = h_soa[k * stride + i];
   const uint32_t key0 = key_idx[i];
   const uint32_t key = key0 < key_count ? key0 : 0;  // flags[i] is 0 for an out-of-range id
-  const DevComb<W> ta{key_tab + (uint64_t)key * Window<W>::kTableWords};
-  const DevComb<kBaseW> tb{btab};
+  const DevComb<W> ta{key_tab + (uint64_t)key * Window<W>::kTableWords, ident};
+  const DevComb<kBaseW> tb{btab, ident};
   ge_p3 Q;
   ge_p3_0(Q);
   comb_mul_add<W>(Q, h, ta);
@@ -538,7 +545,8 @@ struct edv_ctx {
   hipEvent_t ev[kEv] = {};
   bool timed = false;
   // key-table store (registered public keys)
-  uint32_t* d_btab_comb32 = nullptr;  // W = 8 base-point comb table (512 KiB)
+  uint32_t* d_btab_comb32 = nullptr;  // base-point comb table (kBaseW; 64 MiB at W = 16)
+  uint32_t* d_ident = nullptr;        // identity niels entry (comb accessors' j = -1)
   uint8_t* d_key_pk = nullptr;
   uint8_t* d_key_valid = nullptr;
   uint32_t* d_key_tab = nullptr;
@@ -613,7 +621,7 @@ int launch_verify(edv_ctx* ctx, const void* d_sig, const void* d_pk, const void*
     HIP_TRY(hipGetLastError());
     if (last) HIP_TRY(hipEventRecord(ctx->ev[2], st));
     hipLaunchKernelGGL(edv_dsm_kernel, dim3(grid), dim3(kBlock), 0, st, sig + 64 * c0, cn, ctx->d_hsoa,
-                       ctx->d_scratch, chunk, ctx->d_btab_comb32, ctx->d_pt);
+                       ctx->d_scratch, chunk, ctx->d_btab_comb32, ctx->d_ident, ctx->d_pt);
     HIP_TRY(hipGetLastError());
     if (last) HIP_TRY(hipEventRecord(ctx->ev[3], st));
     int r = launch_encode(ctx, sig + 64 * c0, cn, words + c0 / 64, chunk, st);
@@ -722,7 +730,7 @@ static int launch_verify_keyed(edv_ctx* ctx, const void* d_sig, const void* d_ki
     }
 #define EDV_COMB_LAUNCH(W)                                                                                   \
   hipLaunchKernelGGL(edv_comb_kernel<W>, dim3(grid), dim3(kBlock), 0, st, sig + 64 * c0, kidx + c0, kc, cn, \
-                     ctx->d_hsoa, ctx->d_key_tab, ctx->d_btab_comb32, ctx->d_pt, chunk)
+                     ctx->d_hsoa, ctx->d_key_tab, ctx->d_btab_comb32, ctx->d_ident, ctx->d_pt, chunk)
     if (ctx->key_w == 4)
       EDV_COMB_LAUNCH(4);
     else if (ctx->key_w == 6)
@@ -886,6 +894,10 @@ edv_ctx* edv_create(int device) {
   for (int k = 0; k < edv_ctx::kEv; ++k)
     if ((e = hipEventCreate(&ctx->ev[k])) != hipSuccess) return fail("hipEventCreate", e);
   if ((e = hipMalloc(&ctx->d_btab_comb, sizeof(BASE_COMB_U32))) != hipSuccess) return fail("hipMalloc", e);
+  if ((e = hipMalloc(&ctx->d_ident, sizeof(kNielsIdentityHost))) != hipSuccess) return fail("hipMalloc", e);
+  if ((e = hipMemcpy(ctx->d_ident, kNielsIdentityHost, sizeof(kNielsIdentityHost), hipMemcpyHostToDevice)) !=
+      hipSuccess)
+    return fail("hipMemcpy", e);
   if ((e = hipMemcpy(ctx->d_btab_comb, BASE_COMB_U32, sizeof(BASE_COMB_U32), hipMemcpyHostToDevice)) != hipSuccess)
     return fail("hipMemcpy", e);
   {
@@ -930,6 +942,7 @@ void edv_destroy(edv_ctx* ctx) {
   if (ctx->d_hsoa) (void)hipFree(ctx->d_hsoa);
   if (ctx->d_flags) (void)hipFree(ctx->d_flags);
   if (ctx->d_pt) (void)hipFree(ctx->d_pt);
+  if (ctx->d_ident) (void)hipFree(ctx->d_ident);
   if (ctx->d_pre) (void)hipFree(ctx->d_pre);
   if (ctx->d_btab_comb) (void)hipFree(ctx->d_btab_comb);
   if (ctx->d_btab_comb32) (void)hipFree(ctx->d_btab_comb32);

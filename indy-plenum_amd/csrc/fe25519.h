@@ -23,9 +23,11 @@
 #include <hip/hip_runtime.h>
 #define EDV_HD __host__ __device__ __forceinline__
 #define EDV_HDNI __host__ __device__ __forceinline__
+#define EDV_HDM __host__ __device__ __forceinline__
 #else
 #define EDV_HD static inline
 #define EDV_HDNI static
+#define EDV_HDM inline
 #endif
 
 #ifdef EDV_BOUND_CHECK

@@ -157,6 +157,69 @@ EDV_HD void ge_msub(ge_p1p1& r, const ge_p3& p, const ge_niels& q) {
   fe_add(r.T, d, c);
 }
 
+// r = p + q or p - q (neg) for affine q, straight to p3: ge_madd/ge_msub +
+// ge_p1p1_to_p3_*, with the sign folded into selects on p's side so the
+// table entry is used exactly as loaded.  -q = (y-x, y+x, -2dxy), so for neg
+// the Y+X / Y-X multiplicands swap (a, b come out swapped: X3 = b - a) and
+// 2Z +/- T*2dxy swap roles (Z3 = 2Z - c, T3 = 2Z + c).  Classes: a, b, c C;
+// X3, Y3, plus L; minus W.
+EDV_HD void ge_madd_signed(ge_p3& r, const ge_p3& p, const ge_niels& q, bool neg) {
+  fe sp, sm, a, b, c, d, plus, minus, t;
+  fe_add(sp, p.Y, p.X);       // L
+  fe_sub(sm, p.Y, p.X);       // L
+  t = sp;
+  fe_cmov(sp, sm, neg);
+  fe_cmov(sm, t, neg);
+  fe_mul(a, sp, q.ypx);
+  fe_mul(b, sm, q.ymx);
+  fe_mul(c, p.T, q.xy2d);
+  fe_add(d, p.Z, p.Z);        // L
+  fe X3, Y3;
+  fe_sub(X3, a, b);           // L
+  fe_sub(t, b, a);            // L
+  fe_cmov(X3, t, neg);
+  fe_add(Y3, a, b);           // L
+  fe_add(plus, d, c);         // L
+  fe_sub(minus, d, c);        // W
+  fe zs = plus, ts = minus;   // r.Z-side / r.T-side of the p1p1 point
+  fe_cmov(zs, minus, neg);    // W
+  fe_cmov(ts, plus, neg);     // W
+  fe_mul(r.X, ts, X3);
+  fe_mul(r.Y, zs, Y3);
+  fe_mul(r.Z, minus, plus);
+  fe_mul(r.T, X3, Y3);
+}
+
+// r = p + q or p - q (neg) for cached q, straight to p3 (ge_add/ge_sub +
+// ge_p1p1_to_p3_*), the sign folded in as in ge_madd_signed.
+EDV_HD void ge_add_signed(ge_p3& r, const ge_p3& p, const ge_cached& q, bool neg) {
+  fe sp, sm, a, b, c, d, plus, minus, t;
+  fe_add(sp, p.Y, p.X);
+  fe_sub(sm, p.Y, p.X);
+  t = sp;
+  fe_cmov(sp, sm, neg);
+  fe_cmov(sm, t, neg);
+  fe_mul(a, sp, q.YplusX);
+  fe_mul(b, sm, q.YminusX);
+  fe_mul(c, p.T, q.T2d);
+  fe_mul(d, p.Z, q.Z);
+  fe_add(d, d, d);            // L
+  fe X3, Y3;
+  fe_sub(X3, a, b);
+  fe_sub(t, b, a);
+  fe_cmov(X3, t, neg);
+  fe_add(Y3, a, b);
+  fe_add(plus, d, c);         // L
+  fe_sub(minus, d, c);        // W
+  fe zs = plus, ts = minus;
+  fe_cmov(zs, minus, neg);
+  fe_cmov(ts, plus, neg);
+  fe_mul(r.X, ts, X3);
+  fe_mul(r.Y, zs, Y3);
+  fe_mul(r.Z, minus, plus);
+  fe_mul(r.T, X3, Y3);
+}
+
 // p1p1 -> p2/p3 need the W operand first (fe_mul's f).  ge_add/madd leave T
 // in W, ge_sub/msub leave Z in W; ge_p2_dbl leaves X in W and T carried.
 EDV_HD void ge_p1p1_to_p3_addlike(ge_p3& r, const ge_p1p1& p) {  // T is W

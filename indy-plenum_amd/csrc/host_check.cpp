@@ -14,16 +14,16 @@ using namespace edv;
 
 namespace {
 struct HostTableA {
-  ge_cached e[8];
+  ge_cached e[9];  // slot 8: the identity
   void store(int j, const ge_cached& c) { e[j] = c; }
-  void load(int j, ge_cached& c) const { c = e[j]; }
+  void load(int j, ge_cached& c) const { c = e[j >= 0 ? j : 8]; }
 };
 // A comb table in host memory (comb.h layout).
 template <int W>
 struct HostComb {
   const uint32_t* tab;
   void load(int row, int j, ge_niels& n) const {
-    const uint32_t* p = tab + ((size_t)row * Window<W>::kEntries + j) * kEntryWords;
+    const uint32_t* p = j >= 0 ? tab + ((size_t)row * Window<W>::kEntries + j) * kEntryWords : kNielsIdentityHost;
     memcpy(n.ypx.v, p, 40);
     memcpy(n.ymx.v, p + 10, 40);
     memcpy(n.xy2d.v, p + 20, 40);

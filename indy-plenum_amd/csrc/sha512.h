@@ -37,31 +37,40 @@ static const uint64_t SHA512_K[80] = {
 EDV_HD uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
 EDV_HD uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
+#define EDV_SHA_ROUND(KI, WI)                                                        \
+  {                                                                                \
+    const uint64_t S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);             \
+    const uint64_t ch = (e & f) ^ (~e & g);                                        \
+    const uint64_t t1 = h + S1 + ch + (KI) + (WI);                                 \
+    const uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);             \
+    const uint64_t mj = (a & b) ^ (a & c) ^ (b & c);                               \
+    h = g;                                                                         \
+    g = f;                                                                         \
+    f = e;                                                                         \
+    e = d + t1;                                                                    \
+    d = c;                                                                         \
+    c = b;                                                                         \
+    b = a;                                                                         \
+    a = t1 + S0 + mj;                                                              \
+  }
+
+// Rounds 0..15 on the block words, then 64 rounds with the message schedule
+// in place (w[i] <- sigma1(w[i-2]) + w[i-7] + sigma0(w[i-15]) + w[i-16]).
+// No per-round branch: a conditional schedule made the compiler copy the
+// whole w[16] array every round.
 EDV_HD void sha512_compress(uint64_t st[8], uint64_t w[16]) {
   uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) EDV_SHA_ROUND(SHA512_K[i], w[i])
 #pragma unroll 1
-  for (int r = 0; r < 80; r += 16) {
+  for (int r = 16; r < 80; r += 16) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      if (r > 0) {
-        const uint64_t w15 = w[(i + 1) & 15], w2 = w[(i + 14) & 15];
-        const uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ (w15 >> 7);
-        const uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ (w2 >> 6);
-        w[i] += s0 + w[(i + 9) & 15] + s1;
-      }
-      const uint64_t S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);
-      const uint64_t ch = (e & f) ^ (~e & g);
-      const uint64_t t1 = h + S1 + ch + SHA512_K[r + i] + w[i];
-      const uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);
-      const uint64_t mj = (a & b) ^ (a & c) ^ (b & c);
-      h = g;
-      g = f;
-      f = e;
-      e = d + t1;
-      d = c;
-      c = b;
-      b = a;
-      a = t1 + S0 + mj;
+      const uint64_t w15 = w[(i + 1) & 15], w2 = w[(i + 14) & 15];
+      const uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ (w15 >> 7);
+      const uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ (w2 >> 6);
+      w[i] += s0 + w[(i + 9) & 15] + s1;
+      EDV_SHA_ROUND(SHA512_K[r + i], w[i])
     }
   }
   st[0] += a;
@@ -73,6 +82,7 @@ EDV_HD void sha512_compress(uint64_t st[8], uint64_t w[16]) {
   st[6] += g;
   st[7] += h;
 }
+#undef EDV_SHA_ROUND
 
 // (hi:lo) >> (8 * sh) low word: message word from two aligned words.
 EDV_HD uint32_t funnel8(uint32_t hi, uint32_t lo, uint32_t sh) {

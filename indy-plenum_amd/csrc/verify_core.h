@@ -85,7 +85,8 @@ EDV_HD bool verify_phase_hash(uint32_t h[8], const uint32_t sig[16], const uint3
 }
 
 // Phase 2: decode -A and store the cached multiples [1..8](-A) through TA:
-//   TA::store(j, const ge_cached&) for j in 0..7 (= (j+1)(-A)).
+//   TA::store(j, const ge_cached&) for j in 0..7 (= (j+1)(-A)); slot 8 holds
+//   the identity (TA::load(-1) in phase 3).
 template <class TA>
 EDV_HD bool verify_phase_table(const uint32_t pk[8], TA& ta) {
   ge_p3 A;
@@ -103,6 +104,8 @@ EDV_HD bool verify_phase_table(const uint32_t pk[8], TA& ta) {
     ge_p3_to_cached(c, acc);
     ta.store(j, c);
   }
+  ge_cached_0(c);
+  ta.store(8, c);
   return ok;
 }
 
@@ -116,6 +119,8 @@ EDV_HD bool verify_phase_table(const uint32_t pk[8], TA& ta) {
 constexpr int kBaseW = EDV_BASE_W;  // base-point comb window: 16 rows x 32768 entries (64 MiB)
 template <class TA, class CB>
 EDV_HD void verify_phase_dsm_point(ge_p3& Q, const uint32_t h[8], const uint32_t S[8], const TA& ta, const CB& cb) {
+  // radix-16 digits of h, top first: shift the recoded words left 4 bits per
+  // digit (static register indexing; see CombDigits)
   uint32_t hy[8];
   sc_recode16(hy, h);
   ge_p3_0(Q);
@@ -134,19 +139,14 @@ EDV_HD void verify_phase_dsm_point(ge_p3& Q, const uint32_t h[8], const uint32_t
       ge_p2_dbl(t, q2);
       ge_dbl_to_p3(Q, t);
     }
-    const int e = recode_digit(hy, i);
+    const int e = (int)(hy[7] >> 28) - 8;  // = recode_digit(hy, i) of the unshifted words
+#pragma unroll
+    for (int k = 7; k > 0; --k) hy[k] = funnel32(hy[k], hy[k - 1], 28);
+    hy[0] <<= 4;
     const int m = e < 0 ? -e : e;
     ge_cached c;
-    ge_cached_0(c);
-    if (m != 0) ta.load(m - 1, c);
-    if (e < 0) {
-      fe tmp = c.YplusX;
-      c.YplusX = c.YminusX;
-      c.YminusX = tmp;
-      fe_neg(c.T2d, c.T2d);
-    }
-    ge_add(t, Q, c);
-    ge_p1p1_to_p3_addlike(Q, t);
+    ta.load(m - 1, c);  // m = 0: the identity (an address select in the accessor)
+    ge_add_signed(Q, Q, c, e < 0);
   }
   comb_mul_add<kBaseW>(Q, S, cb);
 }
