@@ -89,15 +89,23 @@ int edv_verify_batch_device(edv_ctx *ctx, const void *d_sig64, const void *d_pk3
                             const void *d_msg_off, uint64_t n, void *d_accept_words, void *stream);
 
 /* Kernel timing hooks for the roofline, measured with HIP events on the
- * stream the kernels ran on.  The verify pipeline is four kernels per chunk
- * of up to 2^20 items: hash (prechecks + SHA-512 + mod L), table (decode -A,
- * [1..8](-A); empty on the key-table path), dsm or comb ([h](-A) + [S]B), and
- * encode (batched inversion, encode, compare with R, ballot).  For a
- * multi-chunk launch the per-phase times cover the last chunk only.
- * edv_last_phases_ms fills out4[0..3] = hash, table, dsm/comb, encode;
- * edv_last_phase_ms the first three; edv_last_kernel_ms returns the dsm/comb
- * time (the dominant kernel) or < 0. */
+ * streams the kernels ran on.  The verify pipeline is four kernels: hash
+ * (prechecks + SHA-512 + mod L), table (decode -A, [1..8](-A); empty on the
+ * key-table path), dsm or comb ([h](-A) + [S]B), and encode (batched
+ * inversion, encode, compare with R, ballot).  Each chunk of up to 2^20 items
+ * is cut into up to 4 sub-batches whose kernels alternate between two
+ * streams (one sub-batch's encode and tail overlap the next one's work);
+ * edv_last_launch_count() is the number of sub-batches (kernel launches per
+ * phase) of the last chunk.  edv_last_phases_ms fills out4[0..3] = hash,
+ * table, dsm/comb, encode, each the SUM of that phase's launch durations in
+ * the last chunk (average launch = sum / count); edv_last_phase_ms the first
+ * three; edv_last_kernel_ms returns the dsm/comb sum (the dominant kernel)
+ * or < 0. */
 int edv_last_phases_ms(edv_ctx *ctx, double *out4);
+int edv_last_launch_count(edv_ctx *ctx);
+/* Sub-batches per chunk (1..4, default 4); 1 = no overlap (each kernel runs
+ * alone on the GPU, e.g. to time one kernel in isolation). */
+int edv_set_pipeline(edv_ctx *ctx, int sub_batches);
 int edv_last_phase_ms(edv_ctx *ctx, double *hash_ms, double *table_ms, double *dsm_ms);
 double edv_last_kernel_ms(edv_ctx *ctx);
 

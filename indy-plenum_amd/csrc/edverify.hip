@@ -541,8 +541,19 @@ struct edv_ctx {
   uint32_t* d_pt = nullptr;       // R' = (X:Y:Z), SoA [30][kMaxLanes]
   uint32_t* d_pre = nullptr;      // batch-encode prefix products, SoA [10][kMaxLanes]
   uint64_t scratch_lanes = 0;
-  static constexpr int kEv = 5;   // hash | table | dsm-or-comb | encode boundaries
-  hipEvent_t ev[kEv] = {};
+  // Pipelined launches: each chunk of up to kMaxLanes requests is cut into
+  // kSub sub-batches whose kernels alternate between `stream` (or the
+  // caller's) and `stream2`, so one sub-batch's encode (a latency-bound
+  // kernel of ~1 wave per SIMD) and the kernels' tail rounds overlap the next
+  // sub-batch's work.  ev_sub[s][0..4] bracket hash | table | dsm-or-comb |
+  // encode of sub-batch s.
+  static constexpr int kSub = 4;
+  static constexpr int kEv = 5;
+  hipStream_t stream2 = nullptr;
+  hipEvent_t ev_sub[kSub][kEv] = {};
+  hipEvent_t ev_join[2] = {};
+  int last_nsub = 0;
+  int max_sub = kSub;  // edv_set_pipeline
   bool timed = false;
   // key-table store (registered public keys)
   uint32_t* d_btab_comb32 = nullptr;  // base-point comb table (kBaseW; 64 MiB at W = 16)
@@ -589,47 +600,126 @@ uint32_t key_tab_words(int w) {
                  : Window<8>::kTableWords;
 }
 
-int launch_encode(edv_ctx* ctx, const uint8_t* sig, uint64_t cn, unsigned long long* words, uint64_t chunk,
-                  hipStream_t st) {
+int launch_encode(edv_ctx* ctx, const uint8_t* sig, uint64_t cn, unsigned long long* words, uint64_t off,
+                  uint64_t chunk, hipStream_t st) {
   const uint64_t waves = div_up(cn, 64ull * kEncodeM);
   const uint32_t grid = (uint32_t)div_up(waves * 64, kBlock);
-  hipLaunchKernelGGL(edv_encode_kernel<kEncodeM>, dim3(grid), dim3(kBlock), 0, st, sig, cn, ctx->d_pt, ctx->d_pre,
-                     ctx->d_flags, words, chunk);
+  hipLaunchKernelGGL(edv_encode_kernel<kEncodeM>, dim3(grid), dim3(kBlock), 0, st, sig, cn, ctx->d_pt + off,
+                     ctx->d_pre + off, ctx->d_flags + off, words, chunk);
   HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+// The kernels of one sub-batch [off, off + cn) of a chunk (scratch index
+// off.. with the chunk's stride), on stream q, bracketed by ev[0..4].
+struct SubBatch {
+  const uint8_t* sig;  // first request of the sub-batch
+  const uint8_t* pk;   // general path: its keys
+  const uint32_t* kidx;  // keyed path: its key ids
+  const uint64_t* off;   // its msg_off
+  unsigned long long* words;
+  uint64_t cn, soff;
+};
+
+int launch_sub(edv_ctx* ctx, bool keyed, const SubBatch& b, const uint8_t* msgs, uint64_t chunk, hipStream_t q,
+               hipEvent_t* ev) {
+  const uint32_t grid = (uint32_t)div_up(b.cn, kBlock);
+  uint32_t* hs = ctx->d_hsoa + b.soff;
+  uint8_t* fl = ctx->d_flags + b.soff;
+  uint32_t* pt = ctx->d_pt + b.soff;
+  HIP_TRY(hipEventRecord(ev[0], q));
+  if (keyed) {
+    const uint32_t kc = (uint32_t)ctx->key_count;
+    hipLaunchKernelGGL(edv_hash_keyed_kernel, dim3(grid), dim3(kBlock), 0, q, b.sig, b.kidx, kc, ctx->d_key_pk,
+                       ctx->d_key_valid, msgs, b.off, b.cn, hs, fl, chunk);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(ev[1], q));
+    HIP_TRY(hipEventRecord(ev[2], q));
+#define EDV_COMB_LAUNCH(W)                                                                                   \
+  hipLaunchKernelGGL(edv_comb_kernel<W>, dim3(grid), dim3(kBlock), 0, q, b.sig, b.kidx, kc, b.cn, hs,        \
+                     ctx->d_key_tab, ctx->d_btab_comb32, ctx->d_ident, pt, chunk)
+    if (ctx->key_w == 4)
+      EDV_COMB_LAUNCH(4);
+    else if (ctx->key_w == 6)
+      EDV_COMB_LAUNCH(6);
+    else if (ctx->key_w == 10)
+      EDV_COMB_LAUNCH(10);
+    else
+      EDV_COMB_LAUNCH(8);
+#undef EDV_COMB_LAUNCH
+    HIP_TRY(hipGetLastError());
+  } else {
+    // the per-lane A tables are per 256-lane block of the chunk: sub-batch
+    // offsets are multiples of the block size, so each sub-batch has its own
+    uint32_t* tab = (uint32_t*)((char*)ctx->d_scratch + (b.soff / kBlock) * (uint64_t)kRegionBytes);
+    hipLaunchKernelGGL(edv_hash_kernel, dim3(grid), dim3(kBlock), 0, q, b.sig, b.pk, msgs, b.off, b.cn, hs, fl, chunk);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(ev[1], q));
+    hipLaunchKernelGGL(edv_table_kernel, dim3(grid), dim3(kBlock), 0, q, b.pk, b.cn, tab, fl, chunk);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(ev[2], q));
+    hipLaunchKernelGGL(edv_dsm_kernel, dim3(grid), dim3(kBlock), 0, q, b.sig, b.cn, hs, tab, chunk, ctx->d_btab_comb32,
+                       ctx->d_ident, pt);
+    HIP_TRY(hipGetLastError());
+  }
+  HIP_TRY(hipEventRecord(ev[3], q));
+  int r = launch_encode(ctx, b.sig, b.cn, b.words, b.soff, chunk, q);
+  if (r) return r;
+  HIP_TRY(hipEventRecord(ev[4], q));
+  return 0;
+}
+
+// Sub-batch boundaries: multiples of 64 * kEncodeM (whole encode groups and
+// bitmask words) and of kBlock (whole A-table regions).
+constexpr uint64_t kSubAlign = 64ull * kEncodeM > (uint64_t)kBlock ? 64ull * kEncodeM : (uint64_t)kBlock;
+
+int launch_pipeline(edv_ctx* ctx, bool keyed, const void* d_sig, const void* d_keys, const void* d_msgs,
+                    const void* d_off, uint64_t n, void* d_words, hipStream_t st) {
+  if (n == 0) return 0;
+  const uint8_t* sig = (const uint8_t*)d_sig;
+  const uint64_t* off = (const uint64_t*)d_off;
+  unsigned long long* words = (unsigned long long*)d_words;
+  const uint64_t chunk = ctx->scratch_lanes;  // multiple of kSubAlign
+  // stream2 starts after everything already queued on st (the inputs)
+  HIP_TRY(hipEventRecord(ctx->ev_join[0], st));
+  HIP_TRY(hipStreamWaitEvent(ctx->stream2, ctx->ev_join[0], 0));
+  for (uint64_t c0 = 0; c0 < n; c0 += chunk) {
+    const uint64_t cn = (n - c0) < chunk ? (n - c0) : chunk;
+    // sub-batches of the chunk; the next chunk reuses the scratch, so it
+    // starts only after both streams are done with this one
+    const uint64_t per = div_up(div_up(cn, (uint64_t)ctx->max_sub), kSubAlign) * kSubAlign;
+    int ns = 0;
+    for (uint64_t s0 = 0; s0 < cn; s0 += per, ++ns) {
+      SubBatch b;
+      b.cn = (cn - s0) < per ? (cn - s0) : per;
+      b.soff = s0;
+      b.sig = sig + 64 * (c0 + s0);
+      b.pk = keyed ? nullptr : (const uint8_t*)d_keys + 32 * (c0 + s0);
+      b.kidx = keyed ? (const uint32_t*)d_keys + (c0 + s0) : nullptr;
+      b.off = off + c0 + s0;
+      b.words = words + (c0 + s0) / 64;
+      hipStream_t q = (ns & 1) ? ctx->stream2 : st;
+      int r = launch_sub(ctx, keyed, b, (const uint8_t*)d_msgs, chunk, q, ctx->ev_sub[ns]);
+      if (r) return r;
+    }
+    ctx->last_nsub = ns;
+    if (c0 + cn < n) {  // join before the scratch is reused
+      HIP_TRY(hipEventRecord(ctx->ev_join[1], ctx->stream2));
+      HIP_TRY(hipStreamWaitEvent(st, ctx->ev_join[1], 0));
+      HIP_TRY(hipEventRecord(ctx->ev_join[0], st));
+      HIP_TRY(hipStreamWaitEvent(ctx->stream2, ctx->ev_join[0], 0));
+    }
+  }
+  // the caller's stream completes when both have
+  HIP_TRY(hipEventRecord(ctx->ev_join[1], ctx->stream2));
+  HIP_TRY(hipStreamWaitEvent(st, ctx->ev_join[1], 0));
+  ctx->timed = true;
   return 0;
 }
 
 int launch_verify(edv_ctx* ctx, const void* d_sig, const void* d_pk, const void* d_msgs, const void* d_off, uint64_t n,
                   void* d_words, hipStream_t st) {
-  if (n == 0) return 0;
-  const uint8_t* sig = (const uint8_t*)d_sig;
-  const uint8_t* pk = (const uint8_t*)d_pk;
-  const uint64_t* off = (const uint64_t*)d_off;
-  unsigned long long* words = (unsigned long long*)d_words;
-  const uint64_t chunk = ctx->scratch_lanes;  // multiple of 64
-  HIP_TRY(hipEventRecord(ctx->ev[0], st));
-  for (uint64_t c0 = 0; c0 < n; c0 += chunk) {
-    const uint64_t cn = (n - c0) < chunk ? (n - c0) : chunk;
-    const uint32_t grid = (uint32_t)div_up(cn, kBlock);
-    const bool last = c0 + cn >= n;
-    hipLaunchKernelGGL(edv_hash_kernel, dim3(grid), dim3(kBlock), 0, st, sig + 64 * c0, pk + 32 * c0,
-                       (const uint8_t*)d_msgs, off + c0, cn, ctx->d_hsoa, ctx->d_flags, chunk);
-    HIP_TRY(hipGetLastError());
-    if (last) HIP_TRY(hipEventRecord(ctx->ev[1], st));
-    hipLaunchKernelGGL(edv_table_kernel, dim3(grid), dim3(kBlock), 0, st, pk + 32 * c0, cn, ctx->d_scratch,
-                       ctx->d_flags, chunk);
-    HIP_TRY(hipGetLastError());
-    if (last) HIP_TRY(hipEventRecord(ctx->ev[2], st));
-    hipLaunchKernelGGL(edv_dsm_kernel, dim3(grid), dim3(kBlock), 0, st, sig + 64 * c0, cn, ctx->d_hsoa,
-                       ctx->d_scratch, chunk, ctx->d_btab_comb32, ctx->d_ident, ctx->d_pt);
-    HIP_TRY(hipGetLastError());
-    if (last) HIP_TRY(hipEventRecord(ctx->ev[3], st));
-    int r = launch_encode(ctx, sig + 64 * c0, cn, words + c0 / 64, chunk, st);
-    if (r) return r;
-  }
-  HIP_TRY(hipEventRecord(ctx->ev[4], st));
-  ctx->timed = true;
-  return 0;
+  return launch_pipeline(ctx, false, d_sig, d_pk, d_msgs, d_off, n, d_words, st);
 }
 
 }  // namespace
@@ -709,45 +799,7 @@ static int launch_verify_keyed(edv_ctx* ctx, const void* d_sig, const void* d_ki
                                const void* d_off, uint64_t n, void* d_words, hipStream_t st) {
   if (n == 0) return 0;
   if (ctx->key_count == 0) return set_err(EDV_EINVAL, "no registered keys");
-  const uint8_t* sig = (const uint8_t*)d_sig;
-  const uint32_t* kidx = (const uint32_t*)d_kidx;
-  const uint64_t* off = (const uint64_t*)d_off;
-  unsigned long long* words = (unsigned long long*)d_words;
-  const uint64_t chunk = ctx->scratch_lanes;
-  const uint32_t kc = (uint32_t)ctx->key_count;
-  HIP_TRY(hipEventRecord(ctx->ev[0], st));
-  for (uint64_t c0 = 0; c0 < n; c0 += chunk) {
-    const uint64_t cn = (n - c0) < chunk ? (n - c0) : chunk;
-    const uint32_t grid = (uint32_t)div_up(cn, kBlock);
-    const bool last = c0 + cn >= n;
-    hipLaunchKernelGGL(edv_hash_keyed_kernel, dim3(grid), dim3(kBlock), 0, st, sig + 64 * c0, kidx + c0, kc,
-                       ctx->d_key_pk, ctx->d_key_valid, (const uint8_t*)d_msgs, off + c0, cn, ctx->d_hsoa,
-                       ctx->d_flags, chunk);
-    HIP_TRY(hipGetLastError());
-    if (last) {
-      HIP_TRY(hipEventRecord(ctx->ev[1], st));
-      HIP_TRY(hipEventRecord(ctx->ev[2], st));
-    }
-#define EDV_COMB_LAUNCH(W)                                                                                   \
-  hipLaunchKernelGGL(edv_comb_kernel<W>, dim3(grid), dim3(kBlock), 0, st, sig + 64 * c0, kidx + c0, kc, cn, \
-                     ctx->d_hsoa, ctx->d_key_tab, ctx->d_btab_comb32, ctx->d_ident, ctx->d_pt, chunk)
-    if (ctx->key_w == 4)
-      EDV_COMB_LAUNCH(4);
-    else if (ctx->key_w == 6)
-      EDV_COMB_LAUNCH(6);
-    else if (ctx->key_w == 10)
-      EDV_COMB_LAUNCH(10);
-    else
-      EDV_COMB_LAUNCH(8);
-#undef EDV_COMB_LAUNCH
-    HIP_TRY(hipGetLastError());
-    if (last) HIP_TRY(hipEventRecord(ctx->ev[3], st));
-    int r = launch_encode(ctx, sig + 64 * c0, cn, words + c0 / 64, chunk, st);
-    if (r) return r;
-  }
-  HIP_TRY(hipEventRecord(ctx->ev[4], st));
-  ctx->timed = true;
-  return 0;
+  return launch_pipeline(ctx, true, d_sig, d_kidx, d_msgs, d_off, n, d_words, st);
 }
 
 extern "C" {
@@ -891,8 +943,14 @@ edv_ctx* edv_create(int device) {
   // A blocking stream: it is ordered against the legacy NULL stream, which is
   // where PyTorch's default-stream copies that produce our inputs run.
   if ((e = hipStreamCreate(&ctx->stream)) != hipSuccess) return fail("hipStreamCreate", e);
-  for (int k = 0; k < edv_ctx::kEv; ++k)
-    if ((e = hipEventCreate(&ctx->ev[k])) != hipSuccess) return fail("hipEventCreate", e);
+  if ((e = hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking)) != hipSuccess)
+    return fail("hipStreamCreate", e);
+  for (int sb = 0; sb < edv_ctx::kSub; ++sb)
+    for (int k = 0; k < edv_ctx::kEv; ++k)
+      if ((e = hipEventCreate(&ctx->ev_sub[sb][k])) != hipSuccess) return fail("hipEventCreate", e);
+  for (int k = 0; k < 2; ++k)
+    if ((e = hipEventCreateWithFlags(&ctx->ev_join[k], hipEventDisableTiming)) != hipSuccess)
+      return fail("hipEventCreate", e);
   if ((e = hipMalloc(&ctx->d_btab_comb, sizeof(BASE_COMB_U32))) != hipSuccess) return fail("hipMalloc", e);
   if ((e = hipMalloc(&ctx->d_ident, sizeof(kNielsIdentityHost))) != hipSuccess) return fail("hipMalloc", e);
   if ((e = hipMemcpy(ctx->d_ident, kNielsIdentityHost, sizeof(kNielsIdentityHost), hipMemcpyHostToDevice)) !=
@@ -949,8 +1007,13 @@ void edv_destroy(edv_ctx* ctx) {
   if (ctx->d_key_pk) (void)hipFree(ctx->d_key_pk);
   if (ctx->d_key_valid) (void)hipFree(ctx->d_key_valid);
   if (ctx->d_key_tab) (void)hipFree(ctx->d_key_tab);
-  for (int k = 0; k < edv_ctx::kEv; ++k)
-    if (ctx->ev[k]) (void)hipEventDestroy(ctx->ev[k]);
+  if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
+  for (int sb = 0; sb < edv_ctx::kSub; ++sb)
+    for (int k = 0; k < edv_ctx::kEv; ++k)
+      if (ctx->ev_sub[sb][k]) (void)hipEventDestroy(ctx->ev_sub[sb][k]);
+  for (int k = 0; k < 2; ++k)
+    if (ctx->ev_join[k]) (void)hipEventDestroy(ctx->ev_join[k]);
+  if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -974,12 +1037,25 @@ int edv_verify_batch_device(edv_ctx* ctx, const void* d_sig64, const void* d_pk3
 int edv_last_phases_ms(edv_ctx* ctx, double* out4) {
   if (!ctx || !ctx->timed) return set_err(EDV_EINVAL, "no timed verify launch yet");
   if (!out4) return set_err(EDV_EINVAL, "null output");
-  HIP_TRY(hipEventSynchronize(ctx->ev[edv_ctx::kEv - 1]));
-  for (int k = 0; k < edv_ctx::kEv - 1; ++k) {
-    float t = 0.f;
-    HIP_TRY(hipEventElapsedTime(&t, ctx->ev[k], ctx->ev[k + 1]));
-    out4[k] = t;
+  for (int k = 0; k < edv_ctx::kEv - 1; ++k) out4[k] = 0.0;
+  for (int sb = 0; sb < ctx->last_nsub; ++sb) {
+    HIP_TRY(hipEventSynchronize(ctx->ev_sub[sb][edv_ctx::kEv - 1]));
+    for (int k = 0; k < edv_ctx::kEv - 1; ++k) {
+      float t = 0.f;
+      HIP_TRY(hipEventElapsedTime(&t, ctx->ev_sub[sb][k], ctx->ev_sub[sb][k + 1]));
+      out4[k] += t;
+    }
   }
+  return 0;
+}
+
+int edv_last_launch_count(edv_ctx* ctx) { return ctx ? ctx->last_nsub : 0; }
+
+int edv_set_pipeline(edv_ctx* ctx, int sub_batches) {
+  if (!ctx) return set_err(EDV_EINVAL, "null context");
+  if (sub_batches < 1 || sub_batches > edv_ctx::kSub)
+    return set_err(EDV_EINVAL, "sub_batches %d (1..%d)", sub_batches, edv_ctx::kSub);
+  ctx->max_sub = sub_batches;
   return 0;
 }
 

@@ -28,6 +28,8 @@ SIGNATURES = {
     "edv_sign_open_batch": (_I, [_P, _P, _P, _P, _U64, _P]),
     "edv_verify_batch_device": (_I, [_P, _P, _P, _P, _P, _U64, _P, _P]),
     "edv_last_phases_ms": (_I, [_P, _P]),
+    "edv_last_launch_count": (_I, [_P]),
+    "edv_set_pipeline": (_I, [_P, _I]),
     "edv_last_phase_ms": (_I, [_P, _P, _P, _P]),
     "edv_last_kernel_ms": (_c.c_double, [_P]),
     "edv_keys_add": (_I, [_P, _P, _U64, _P]),
@@ -82,7 +84,10 @@ def load():
         lib = ctypes.CDLL(LIB_PATH)
     except OSError as ex:
         raise EdVerifyUnavailable("cannot load %s: %s" % (LIB_PATH, ex)) from ex
+    lenient = os.environ.get("PLENUM_EDVERIFY_LENIENT") == "1"  # A/B tools loading older builds
     for name, (res, args) in SIGNATURES.items():
+        if lenient and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

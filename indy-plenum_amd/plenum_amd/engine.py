@@ -160,10 +160,19 @@ class EdVerifyEngine:
 
     def last_phases_ms(self):
         """(hash, table, dsm-or-comb, encode) milliseconds of the last verify
-        launch, from HIP events on the launch stream."""
+        launch, from HIP events on the launch streams: per phase the sum over
+        the last chunk's sub-batch launches (see last_launch_count)."""
         out = (ctypes.c_double * 4)()
         check(self._lib.edv_last_phases_ms(self._ctx, out))
         return tuple(out)
+
+    def last_launch_count(self):
+        """Kernel launches per phase (sub-batches) in the last verify chunk."""
+        return int(self._lib.edv_last_launch_count(self._ctx))
+
+    def set_pipeline(self, sub_batches):
+        """Sub-batches per chunk (1..4; 1 = kernels run one at a time)."""
+        check(self._lib.edv_set_pipeline(self._ctx, int(sub_batches)))
 
     # ------------------------------------------------------------ key tables
     def keys_set_window(self, w):

@@ -161,3 +161,29 @@ def test_keyed_random_vs_oracle_and_out_of_range(gpu_engine, oracle):
     kidx[::5] = gpu_engine.keys_count() + 7  # unregistered ids reject
     got = gpu_engine.verify_batch_keyed(sig, kidx, buf, off)
     assert not got[::5].any() and (got[1::5] == want[1::5]).all()
+
+
+@pytest.mark.parametrize("n", [1023, 1024, 1025, 4096, 4097, 6143])
+def test_sub_batch_boundaries(gpu_engine, oracle, n):
+    """The pipelined launcher cuts a chunk into up to 4 sub-batches aligned to
+    1024 requests on two streams: sizes around those boundaries give the same
+    bits as one un-pipelined launch, and both match the oracle (sampled)."""
+    sig, pks, msgs, buf, off = _random_batch(gpu_engine, n, 100 + n, mlen_max=120)
+    gpu_engine.set_pipeline(4)
+    got4 = gpu_engine.verify_batch(sig, pks, buf, off)
+    per = -(-(-(-n // 4)) // 1024) * 1024  # ceil(ceil(n / 4) / 1024) * 1024
+    assert gpu_engine.last_launch_count() == -(-n // per)
+    gpu_engine.set_pipeline(1)
+    got1 = gpu_engine.verify_batch(sig, pks, buf, off)
+    assert gpu_engine.last_launch_count() == 1
+    gpu_engine.set_pipeline(4)
+    assert (got4 == got1).all(), np.nonzero(got4 != got1)
+    for i in list(range(0, n, 97)) + [n - 1]:
+        want = oracle.oracle_verify_detached(sig[i].tobytes(), msgs[i], len(msgs[i]), pks[i].tobytes()) == 0
+        assert got4[i] == want, i
+    # keyed path: the same requests against registered keys
+    gpu_engine.keys_reset()
+    uniq, inv = np.unique(pks, axis=0, return_inverse=True)
+    gpu_engine.keys_add(uniq)
+    gotk = gpu_engine.verify_batch_keyed(sig, inv.reshape(-1).astype(np.uint32), buf, off)
+    assert (gotk == got1).all(), np.nonzero(gotk != got1)
