@@ -57,6 +57,8 @@ def parse():
                          "SimpleAuthNr.addIdr); general: every request carries its own key bytes")
     ap.add_argument("--key-window", type=int, choices=[4, 6, 8, 10], default=10,
                     help="comb window of the key tables (edv_keys_set_window)")
+    ap.add_argument("--pipeline", type=int, default=4, choices=[1, 2, 3, 4],
+                    help="sub-batches per chunk (edv_set_pipeline; 1 = one launch per kernel, no overlap)")
     ap.add_argument("--general-steps", type=int, default=5,
                     help="also time the general path for this many steps (0 = skip)")
     return ap.parse_args()
@@ -124,6 +126,7 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
     eng = EdVerifyEngine(local)
+    eng.set_pipeline(args.pipeline)
     n = args.n
 
     # ---- synthetic signed batch (not timed)
@@ -249,20 +252,25 @@ def main():
     kernel_name = "edv_comb_kernel" if args.path == "keyed" else "edv_dsm_kernel"
     achieved = (n / launches) * kernel_mad / (dsm_avg * 1e-3) / 1e12
     peak = RL.PEAK_MAD_PER_S / 1e12
+    # HBM bytes per launch from the committed PMC pass (tools/pmc_passes.sh ->
+    # tools/pmc_summary.py): 2 x FETCH_SIZE + WRITE_SIZE per request (gfx950
+    # FETCH_SIZE correction), times the requests of one launch
     traffic = None
     tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tpath):
         with open(tpath) as f:
             tj = json.load(f)
-        if tj.get("n") == n:
-            traffic = tj.get(kernel_name + "_bytes")
+        key = "%s<%d>" % (kernel_name, args.key_window) if args.path == "keyed" else kernel_name
+        row = tj.get("kernels", {}).get(key)
+        if row and "traffic_bytes_per_request" in row:
+            traffic = row["traffic_bytes_per_request"] * (n / launches)
 
     # the dominant kernel alone on the GPU (one sub-batch, no overlap), one
     # untimed step: its own roofline fraction beside the overlapped one above
     eng.set_pipeline(1)
     step()
     solo = eng.last_phases_ms()
-    eng.set_pipeline(4)
+    eng.set_pipeline(args.pipeline)
     solo_ms = float(solo[2])
     standalone = {"avg_launch_ms": solo_ms, "n_per_launch": n,
                   "achieved": n * kernel_mad / (solo_ms * 1e-3) / 1e12,

@@ -139,12 +139,16 @@ static const uint32_t kNielsIdentityHost[kEntryWords] = {1, 0, 0, 0, 0, 0, 0, 0,
 // (7 multiplications each).  Row r + 1's entry is fetched before row r's
 // addition runs, so the table gather overlaps the arithmetic.
 #ifndef EDV_COMB_PREFETCH
-#define EDV_COMB_PREFETCH 0  // 1: fetch row r+1 during row r (no gain measured: spills at 3 waves/SIMD)
+#define EDV_COMB_PREFETCH 0  // 0: none (best: the comb is VALU-bound); 1: row r+1 into registers (spills); 2: touch its line (-5%)
 #endif
+// T::touch(row, j) (optional prefetch): a 4-byte load of entry j's 128-B line
+// whose value is folded into `sink` one row later, so the line is in L2/MALL
+// when the row's own loads arrive and no wait is placed early.
 template <int W, class T>
-EDV_HD void comb_mul_add(ge_p3& Q, const uint32_t x[8], const T& tab) {
+EDV_HD uint32_t comb_mul_add(ge_p3& Q, const uint32_t x[8], const T& tab) {
   CombDigits<W> dg(x);
-#if EDV_COMB_PREFETCH
+  uint32_t sink = 0;
+#if EDV_COMB_PREFETCH == 1
   int e = dg.next();
   ge_niels cur;
   comb_fetch(cur, e, tab, 0);
@@ -162,6 +166,24 @@ EDV_HD void comb_mul_add(ge_p3& Q, const uint32_t x[8], const T& tab) {
     cur = next;
     e = e_next;
   }
+#elif EDV_COMB_PREFETCH == 2
+  int e = dg.next();
+  uint32_t pf = 0;
+#pragma unroll 1
+  for (int r = 0; r < Window<W>::kRows; ++r) {
+    sink ^= pf;
+    int e_next = 0;
+    if (r + 1 < Window<W>::kRows) {
+      e_next = dg.next();
+      const int m = e_next < 0 ? -e_next : e_next;
+      pf = tab.touch(r + 1, m - 1);
+    }
+    ge_niels nb;
+    comb_fetch(nb, e, tab, r);
+    comb_apply(Q, nb, e);
+    e = e_next;
+  }
+  sink ^= pf;
 #else
 #pragma unroll 1
   for (int r = 0; r < Window<W>::kRows; ++r) {
@@ -171,6 +193,7 @@ EDV_HD void comb_mul_add(ge_p3& Q, const uint32_t x[8], const T& tab) {
     comb_apply(Q, nb, e);  // nb is consumed
   }
 #endif
+  return sink;
 }
 
 EDV_HD void store_fe(uint32_t* p, const fe& f) {

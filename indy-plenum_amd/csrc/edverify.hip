@@ -182,6 +182,10 @@ struct DevComb {
     const uint32_t* p = j >= 0 ? tab + ((uint32_t)row * Window<W>::kEntries + (uint32_t)j) * kEntryWords : ident;
     load_niels(nb, p);
   }
+  __device__ uint32_t touch(int row, int j) const {  // comb_mul_add's line prefetch
+    const uint32_t* p = j >= 0 ? tab + ((uint32_t)row * Window<W>::kEntries + (uint32_t)j) * kEntryWords : ident;
+    return *(const volatile uint32_t*)p;
+  }
 };
 
 #ifndef EDV_DSM_MIN_WAVES
@@ -202,8 +206,9 @@ __global__ __launch_bounds__(kBlock, EDV_DSM_MIN_WAVES) void edv_dsm_kernel(cons
   const DevTableA ta(table, blockIdx.x, threadIdx.x);
   const DevComb<kBaseW> cb{btab_comb, ident};
   ge_p3 Q;
-  verify_phase_dsm_point(Q, h, S, ta, cb);
+  const uint32_t sink = verify_phase_dsm_point(Q, h, S, ta, cb);
   store_point_soa(pt, stride, i, Q);
+  if (sink == 0x9e3779b9u && stride == 0) pt[i] = sink;  // keeps the prefetches live
 }
 
 // Batched encode + compare + ballot.  Lane l of wave v owns requests
@@ -382,9 +387,10 @@ __global__ __launch_bounds__(kBlock, EDV_COMB_MIN_WAVES) void edv_comb_kernel(co
   const DevComb<kBaseW> tb{btab, ident};
   ge_p3 Q;
   ge_p3_0(Q);
-  comb_mul_add<W>(Q, h, ta);
-  comb_mul_add<kBaseW>(Q, S, tb);
+  uint32_t sink = comb_mul_add<W>(Q, h, ta);
+  sink ^= comb_mul_add<kBaseW>(Q, S, tb);
   store_point_soa(pt, stride, i, Q);
+  if (sink == 0x9e3779b9u && key0 == 0xffffffffu && key_count == 0) pt[i] = sink;  // keeps the prefetches live
 }
 
 // Fixed-base comb: [x]B with x < 2^253, 64 madds over BASE_COMB (global).

@@ -118,7 +118,8 @@ EDV_HD bool verify_phase_table(const uint32_t pk[8], TA& ta) {
 #endif
 constexpr int kBaseW = EDV_BASE_W;  // base-point comb window: 16 rows x 32768 entries (64 MiB)
 template <class TA, class CB>
-EDV_HD void verify_phase_dsm_point(ge_p3& Q, const uint32_t h[8], const uint32_t S[8], const TA& ta, const CB& cb) {
+EDV_HD uint32_t verify_phase_dsm_point(ge_p3& Q, const uint32_t h[8], const uint32_t S[8], const TA& ta,
+                                       const CB& cb) {
   // radix-16 digits of h, top first: shift the recoded words left 4 bits per
   // digit (static register indexing; see CombDigits)
   uint32_t hy[8];
@@ -148,7 +149,7 @@ EDV_HD void verify_phase_dsm_point(ge_p3& Q, const uint32_t h[8], const uint32_t
     ta.load(m - 1, c);  // m = 0: the identity (an address select in the accessor)
     ge_add_signed(Q, Q, c, e < 0);
   }
-  comb_mul_add<kBaseW>(Q, S, cb);
+  return comb_mul_add<kBaseW>(Q, S, cb);  // the base comb's prefetch sink (comb.h)
 }
 
 // encode(R') == R byte for byte (per-request inversion; the kernels batch it).

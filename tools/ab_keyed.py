@@ -21,6 +21,8 @@ d_k = torch.from_numpy(kidx.astype(np.int32)).to(dev)
 d_sig = torch.empty((n, 64), dtype=torch.uint8, device=dev)
 eng.sign_batch_device(torch.from_numpy(sks).to(dev), d_k, d_msgs, d_off, n, d_sig)
 eng.keys_set_window(int(os.environ.get("AB_KEY_WINDOW", "8")))
+if hasattr(eng._lib, "edv_set_pipeline"):
+    eng.set_pipeline(int(os.environ.get("AB_PIPELINE", "1")))
 t0 = time.perf_counter(); eng.keys_add(pks); kb = (time.perf_counter() - t0) * 1e3
 words = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
 def med(res):
