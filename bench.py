@@ -48,7 +48,9 @@ def parse():
     ap.add_argument("--n", type=int, default=1_000_000, help="requests per GPU")
     ap.add_argument("--signers", type=int, default=1000)
     ap.add_argument("--alias-len", type=int, default=43, help="pads the NYM signing payload to ~200 B")
-    ap.add_argument("--config", choices=["c1", "c2"], default="c1")
+    ap.add_argument("--config", choices=["c1", "c2", "c3"], default="c1",
+                    help="c1: configs[1] all-valid NYMs; c2: configs[2] 10%% corrupted; c3: configs[3] "
+                         "multi-signature requests, 64 B - 4 KiB payloads")
     ap.add_argument("--cpu-sample", type=int, default=400_000, help="items timed on host libsodium (rank 0, N=1)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, affinity CPUs)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -59,6 +61,8 @@ def parse():
                     help="comb window of the key tables (edv_keys_set_window)")
     ap.add_argument("--pipeline", type=int, default=4, choices=[1, 2, 3, 4],
                     help="sub-batches per chunk (edv_set_pipeline; 1 = one launch per kernel, no overlap)")
+    ap.add_argument("--length-buckets", action="store_true",
+                    help="hash lanes in SHA-512 block-count order (edv_set_length_buckets on)")
     ap.add_argument("--general-steps", type=int, default=5,
                     help="also time the general path for this many steps (0 = skip)")
     return ap.parse_args()
@@ -127,30 +131,56 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
     eng = EdVerifyEngine(local)
     eng.set_pipeline(args.pipeline)
+    eng.set_length_buckets(args.length_buckets)
     n = args.n
 
     # ---- synthetic signed batch (not timed)
     seeds = synth.signer_seeds(args.signers)
     pks, sks = eng.seed_keypair_batch(seeds)
-    msgs_l, key_idx, _ = synth.nym_messages(n, pks, alias_len=args.alias_len, seed=1 + rank,
-                                            req_id_base=synth.REQ_ID_BASE + rank * n)
-    buf, off = pack_messages(msgs_l)
-    del msgs_l
-    mlen_mean = float(np.mean(np.diff(off)))
     d_sk = torch.from_numpy(sks).to(dev)
+    expect = np.ones(n, dtype=bool)
+    if args.config in ("c1", "c2"):
+        msgs_l, key_idx, _ = synth.nym_messages(n, pks, alias_len=args.alias_len, seed=1 + rank,
+                                                req_id_base=synth.REQ_ID_BASE + rank * n)
+        buf, off = pack_messages(msgs_l)
+        del msgs_l
+        item_start, item_end = off[:-1].copy(), off[1:].copy()
+        req_desc = ""
+    else:
+        # configs[3]: multi-signature requests, 1-5 signatures each (distinct
+        # signers), payloads log-uniform 64 B - 4 KiB; the k signatures of a
+        # request share its one message copy (message spans)
+        rng = np.random.default_rng(3 + rank)
+        ks = rng.integers(1, 6, size=n)
+        nreq = int(np.searchsorted(np.cumsum(ks), n)) + 1
+        ks = ks[:nreq]
+        ks[-1] -= int(ks.sum()) - n
+        lens = np.exp(rng.uniform(np.log(64), np.log(4096), nreq)).astype(np.int64)
+        roff = np.zeros(nreq + 1, np.uint64)
+        roff[1:] = np.cumsum(lens)
+        buf = rng.integers(33, 127, size=int(roff[-1]), dtype=np.uint8)  # printable serialized bytes
+        item_req = np.repeat(np.arange(nreq), ks)
+        slot = np.arange(n) - np.repeat(np.cumsum(ks) - ks, ks)
+        key_idx = ((item_req * 7 + slot * 131) % args.signers).astype(np.uint32)  # distinct within a request
+        item_start, item_end = roff[:-1][item_req], roff[1:][item_req]
+        req_desc = ", %d requests x 1-5 signatures (mean %.2f), payload %d-%d B log-uniform" % (
+            nreq, n / nreq, int(lens.min()), int(lens.max()))
+    mlen_mean = float(np.mean(item_end - item_start))
     d_kidx = torch.from_numpy(key_idx.astype(np.int32)).to(dev)
     d_msgs = torch.from_numpy(np.concatenate([buf, np.zeros(16, np.uint8)])).to(dev)
-    d_off = torch.from_numpy(off.view(np.int64)).to(dev)
+    d_ms = torch.from_numpy(item_start.astype(np.int64)).to(dev)
+    d_me = torch.from_numpy(item_end.astype(np.int64)).to(dev)
     d_sig = torch.empty((n, 64), dtype=torch.uint8, device=dev)
-    eng.sign_batch_device(d_sk, d_kidx, d_msgs, d_off, n, d_sig)
+    eng.sign_spans_device(d_sk, d_kidx, d_msgs, d_ms, d_me, n, d_sig)
     d_pk = torch.from_numpy(pks).to(dev)[d_kidx.long()].contiguous()
     torch.cuda.synchronize()
-    expect = np.ones(n, dtype=bool)
     if args.config == "c2":
+        off = np.concatenate([item_start, item_end[-1:]])
         sig_h, pk_h, buf_h = d_sig.cpu().numpy().copy(), d_pk.cpu().numpy().copy(), buf.copy()
         expect = corrupt_c2(sig_h, pk_h, buf_h, off, np.random.default_rng(2))
         d_sig = torch.from_numpy(sig_h).to(dev)
         d_pk = torch.from_numpy(pk_h).to(dev)
+        buf = buf_h
         d_msgs = torch.from_numpy(np.concatenate([buf_h, np.zeros(16, np.uint8)])).to(dev)
     nwords = (n + 63) // 64
     d_words = torch.zeros(nwords, dtype=torch.int64, device=dev)
@@ -175,12 +205,12 @@ def main():
     assert first == 0
 
     def step_general():
-        eng.verify_batch_device(d_sig, d_pk, d_msgs, d_off, n, d_words, stream=stream)
+        eng.verify_spans_device(d_sig, d_pk, False, d_msgs, d_ms, d_me, n, d_words, stream=stream)
         if world > 1:
             dist.all_gather(gathered, d_words)
 
     def step_keyed():
-        eng.verify_batch_keyed_device(d_sig, d_kreq, d_msgs, d_off, n, d_words, stream=stream)
+        eng.verify_spans_device(d_sig, d_kreq, True, d_msgs, d_ms, d_me, n, d_words, stream=stream)
         if world > 1:
             dist.all_gather(gathered, d_words)
 
@@ -279,11 +309,14 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        s = min(args.cpu_sample, n)
+        s = min(args.cpu_sample if args.config != "c3" else args.cpu_sample // 4, n)
         sig_h = d_sig[:s].cpu().numpy()
         pk_h = d_pk[:s].cpu().numpy()
-        off_h = off[: s + 1].copy()
-        msg_h = d_msgs[: int(off_h[-1]) + 16].cpu().numpy()
+        # contiguous copy of the sample's messages (the harness takes offsets)
+        starts, ends = item_start[:s].astype(np.int64), item_end[:s].astype(np.int64)
+        off_h = np.zeros(s + 1, np.uint64)
+        off_h[1:] = np.cumsum(ends - starts)
+        msg_h = np.concatenate([buf[a:b] for a, b in zip(starts, ends)] + [np.zeros(16, np.uint8)])
         threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
         rate, ok, kind, ver = cpu_baseline(sig_h, pk_h, msg_h, off_h, threads)
         cpu = {"value": rate, "unit": "verifies/s", "cores": threads, "kind": kind,
@@ -297,9 +330,10 @@ def main():
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u32 (radix-2^25.5 GF(2^255-19), 64-bit MAD accumulators)",
             "data": "synthetic NYM requests signed on-GPU (deterministic Ed25519, libsodium-exact)",
-            "config": {"workload": "configs[%d]: %d single-signature requests per GPU, %.0f B mean signed payload, "
-                                   "%d signers%s" % (1 if args.config == "c1" else 2, n, mlen_mean, args.signers,
-                                                     ", 10% corrupted/non-canonical/small-order" if args.config == "c2" else ", all valid"),
+            "config": {"workload": "configs[%d]: %d %s per GPU, %.0f B mean signed payload, %d signers%s%s" % (
+                int(args.config[1]), n, "signature verifications" if args.config == "c3" else "single-signature requests",
+                mlen_mean, args.signers,
+                ", 10% corrupted/non-canonical/small-order" if args.config == "c2" else ", all valid", req_desc),
                        "requests_per_gpu": n, "signers": args.signers, "parallelism": "dp%d (request-index shards)" % world},
             "roofline": {"bound": "valu", "kernel": kernel_name, "achieved": achieved, "peak": peak,
                          "unit": "TMAD/s", "frac": achieved / peak, "traffic": traffic,

@@ -106,6 +106,13 @@ int edv_last_launch_count(edv_ctx *ctx);
 /* Sub-batches per chunk (1..4, default 4); 1 = no overlap (each kernel runs
  * alone on the GPU, e.g. to time one kernel in isolation). */
 int edv_set_pipeline(edv_ctx *ctx, int sub_batches);
+/* Hash lanes in SHA-512 block-count order (default off): a wave then hashes
+ * messages of one length, but its lanes read scattered requests.  Measured
+ * (profiles/r01d_*): configs[1] -6% (the reorder breaks the coalesced reads
+ * of adjacent requests), configs[3] +-0% (per-lane message reads, not wave
+ * divergence, bound the hash there).  A batch of one block count skips the
+ * reordering. */
+int edv_set_length_buckets(edv_ctx *ctx, int on);
 int edv_last_phase_ms(edv_ctx *ctx, double *hash_ms, double *table_ms, double *dsm_ms);
 double edv_last_kernel_ms(edv_ctx *ctx);
 
@@ -139,6 +146,15 @@ int edv_verify_batch_keyed(edv_ctx *ctx, const uint8_t *sig64, const uint32_t *k
 int edv_verify_batch_keyed_device(edv_ctx *ctx, const void *d_sig64, const void *d_key_idx, const void *d_msgs,
                                   const void *d_msg_off, uint64_t n, void *d_accept_words, void *stream);
 
+/* Either path with message spans instead of contiguous offsets: item i's
+ * message is d_msgs[d_msg_start[i] .. d_msg_end[i]) (uint64 each), so the k
+ * signatures of a multi-signature request (authenticate_multi, configs[3])
+ * share one copy of the serialized message.  keyed = 0: d_keys is n * 32 key
+ * bytes; keyed = 1: n uint32 registered key ids. */
+int edv_verify_spans_device(edv_ctx *ctx, const void *d_sig64, const void *d_keys, int keyed, const void *d_msgs,
+                            const void *d_msg_start, const void *d_msg_end, uint64_t n, void *d_accept_words,
+                            void *stream);
+
 /* ------------------------------------------------- signing (synthetic load) */
 
 /* crypto_sign_seed_keypair for n seeds (32 bytes each): pk32_out n*32,
@@ -149,6 +165,11 @@ int edv_seed_keypair_batch(edv_ctx *ctx, const uint8_t *seeds32, uint64_t n, uin
  * item i is signed with key d_sk64[key_idx[i]] over its message. */
 int edv_sign_batch_device(edv_ctx *ctx, const void *d_sk64, const void *d_key_idx, const void *d_msgs,
                           const void *d_msg_off, uint64_t n, void *d_sig64_out, void *stream);
+
+/* Signer with message spans (d_msg_start / d_msg_end, as edv_verify_spans_device). */
+int edv_sign_spans_device(edv_ctx *ctx, const void *d_sk64, const void *d_key_idx, const void *d_msgs,
+                          const void *d_msg_start, const void *d_msg_end, uint64_t n, void *d_sig64_out,
+                          void *stream);
 
 /* Host-pointer convenience form of edv_sign_batch_device. */
 int edv_sign_batch(edv_ctx *ctx, const uint8_t *sk64, const uint32_t *key_idx, const uint8_t *msgs,

@@ -112,18 +112,98 @@ __device__ __forceinline__ void load_words(uint32_t* dst, const uint8_t* src, in
 // ---- split pipeline: hash -> table -> dsm (each kernel gets its own
 // register budget; intermediates are SoA in the context scratch).
 
+// Length buckets (edv_len_*_kernel): requests sorted by SHA-512 block count,
+// longest first, so the lanes of a wave hash messages of equal length.
+// perm[t] = the request lane t hashes; bucket_ctl[kLenBuckets] != 0 when the
+// batch spans more than one block count (else perm is not written and lane t
+// hashes request t).
+constexpr int kLenBuckets = 64;  // block counts 0..62; 63 = longer
+constexpr int kBucketCtlWords = 2 * kLenBuckets + 1;
+__device__ __forceinline__ uint64_t hash_lane_request(uint64_t t, const uint32_t* __restrict__ perm,
+                                                      const uint32_t* __restrict__ bucket_ctl) {
+  return (perm && bucket_ctl[kLenBuckets]) ? perm[t] : t;
+}
+
+// Message i = msgs[ms[i] .. me[i]): me = msg_off + 1 for contiguous offsets,
+// separate arrays for spans (several signatures over one message).
+__device__ __forceinline__ uint32_t len_bucket(const uint64_t* __restrict__ ms, const uint64_t* __restrict__ me,
+                                               uint64_t i) {
+  const uint64_t blocks = (me[i] - ms[i] + 64 + 17 + 127) / 128;  // SHA-512 blocks of R||A||M
+  return blocks < (uint64_t)(kLenBuckets - 1) ? (uint32_t)blocks : (uint32_t)(kLenBuckets - 1);
+}
+
+// Wave-aggregated atomic add of 1 per lane to ctr[key]: one atomic per
+// distinct key in the wave; returns this lane's slot.
+__device__ __forceinline__ uint32_t wave_bucket_slot(uint32_t* ctr, uint32_t key, bool active) {
+  uint64_t todo = __ballot(active);
+  uint32_t slot = 0;
+  const uint32_t lane = threadIdx.x & 63;
+  while (todo) {
+    const int leader = __ffsll((unsigned long long)todo) - 1;
+    const uint32_t lkey = __shfl(key, leader);
+    const uint64_t same = __ballot(active && key == lkey) & todo;
+    uint32_t base = 0;
+    if (lane == (uint32_t)leader) base = atomicAdd(&ctr[lkey], (uint32_t)__popcll(same));
+    base = __shfl(base, leader);
+    if ((same >> lane) & 1ull) slot = base + (uint32_t)__popcll(same & ((1ull << lane) - 1ull));
+    todo &= ~same;
+  }
+  return slot;
+}
+
+// bucket_ctl layout: [0, 64) counts, [64] bucketed flag, [65, 129) cursors.
+__global__ __launch_bounds__(kBlock) void edv_len_hist_kernel(const uint64_t* __restrict__ ms,
+                                                             const uint64_t* __restrict__ me, uint64_t n,
+                                                             uint32_t* __restrict__ bucket_ctl) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = i < n;
+  const uint32_t b = active ? len_bucket(ms, me, i) : 0;
+  (void)wave_bucket_slot(bucket_ctl, b, active);
+}
+
+// One wave: cursors = exclusive prefix over buckets, longest first.
+__global__ void edv_len_scan_kernel(uint32_t* __restrict__ bucket_ctl) {
+  const uint32_t lane = threadIdx.x;  // 64 lanes = kLenBuckets
+  const uint32_t bucket = kLenBuckets - 1 - lane;
+  const uint32_t c = bucket_ctl[bucket];
+  uint32_t incl = c;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t v = __shfl_up(incl, d);
+    if (lane >= (uint32_t)d) incl += v;
+  }
+  bucket_ctl[kLenBuckets + 1 + bucket] = incl - c;
+  const uint64_t nonempty = __ballot(c != 0);
+  if (lane == 0) bucket_ctl[kLenBuckets] = __popcll(nonempty) > 1 ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(kBlock) void edv_len_scatter_kernel(const uint64_t* __restrict__ ms,
+                                                                const uint64_t* __restrict__ me, uint64_t n,
+                                                                uint32_t* __restrict__ bucket_ctl,
+                                                                uint32_t* __restrict__ perm) {
+  if (!bucket_ctl[kLenBuckets]) return;  // one block count: lane t hashes request t
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = i < n;
+  const uint32_t b = active ? len_bucket(ms, me, i) : 0;
+  const uint32_t slot = wave_bucket_slot(bucket_ctl + kLenBuckets + 1, b, active);
+  if (active) perm[slot] = (uint32_t)i;
+}
+
 __global__ __launch_bounds__(kBlock, 4) void edv_hash_kernel(const uint8_t* __restrict__ sig64,
                                                          const uint8_t* __restrict__ pk32,
                                                          const uint8_t* __restrict__ msgs,
-                                                         const uint64_t* __restrict__ msg_off, uint64_t n,
+                                                         const uint64_t* __restrict__ ms,
+                                                         const uint64_t* __restrict__ me, uint64_t n,
                                                          uint32_t* __restrict__ h_soa, uint8_t* __restrict__ flags,
-                                                         uint64_t stride) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+                                                         uint64_t stride, const uint32_t* __restrict__ perm,
+                                                         const uint32_t* __restrict__ bucket_ctl) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const uint64_t i = hash_lane_request(t, perm, bucket_ctl);
   uint32_t sig[16], pk[8], h[8];
   load_words(sig, sig64 + 64 * i, 16);
   load_words(pk, pk32 + 32 * i, 8);
-  const uint64_t o0 = msg_off[i], o1 = msg_off[i + 1];
+  const uint64_t o0 = ms[i], o1 = me[i];
   const bool ok = verify_phase_hash(h, sig, pk, msgs + o0, o1 - o0);
 #pragma unroll
   for (int k = 0; k < 8; ++k) h_soa[k * stride + i] = h[k];
@@ -348,18 +428,22 @@ __global__ __launch_bounds__(kBlock, EDV_HASH_MIN_WAVES) void edv_hash_keyed_ker
                                                                const uint8_t* __restrict__ key_pk,
                                                                const uint8_t* __restrict__ key_valid,
                                                                const uint8_t* __restrict__ msgs,
-                                                               const uint64_t* __restrict__ msg_off, uint64_t n,
+                                                               const uint64_t* __restrict__ ms,
+                                                               const uint64_t* __restrict__ me, uint64_t n,
                                                                uint32_t* __restrict__ h_soa,
-                                                               uint8_t* __restrict__ flags, uint64_t stride) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+                                                               uint8_t* __restrict__ flags, uint64_t stride,
+                                                               const uint32_t* __restrict__ perm,
+                                                               const uint32_t* __restrict__ bucket_ctl) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const uint64_t i = hash_lane_request(t, perm, bucket_ctl);
   uint32_t sig[16], pk[8], h[8];
   load_words(sig, sig64 + 64 * i, 16);
   const uint32_t key = key_idx[i];
   const bool in_range = key < key_count;  // out-of-range ids reject, never read out of bounds
   const uint64_t k = in_range ? key : 0;
   load_words(pk, key_pk + 32 * k, 8);
-  const uint64_t o0 = msg_off[i], o1 = msg_off[i + 1];
+  const uint64_t o0 = ms[i], o1 = me[i];
   const bool ok = verify_phase_hash(h, sig, pk, msgs + o0, o1 - o0) && in_range && key_valid[k];
 #pragma unroll
   for (int k = 0; k < 8; ++k) h_soa[k * stride + i] = h[k];
@@ -464,7 +548,8 @@ __global__ __launch_bounds__(kBlock) void edv_keypair_kernel(const uint8_t* __re
 __global__ __launch_bounds__(kBlock) void edv_sign_kernel(const uint8_t* __restrict__ sk64,
                                                          const uint32_t* __restrict__ key_idx,
                                                          const uint8_t* __restrict__ msgs,
-                                                         const uint64_t* __restrict__ msg_off, uint64_t n,
+                                                         const uint64_t* __restrict__ ms,
+                                                         const uint64_t* __restrict__ me, uint64_t n,
                                                          const uint32_t* __restrict__ comb,
                                                          uint8_t* __restrict__ sig_out) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -476,8 +561,8 @@ __global__ __launch_bounds__(kBlock) void edv_sign_kernel(const uint8_t* __restr
     seed[k] = sk[k];
     pk[k] = sk[8 + k];
   }
-  const uint8_t* m = msgs + msg_off[i];
-  const uint64_t mlen = msg_off[i + 1] - msg_off[i];
+  const uint8_t* m = msgs + ms[i];
+  const uint64_t mlen = me[i] - ms[i];
   sha512_prefixed<8>(az, seed, nullptr, 0);
   clamp_reduce(a_red, a_cl, az);
   uint32_t nonce_full[16], nonce[8];
@@ -546,6 +631,9 @@ struct edv_ctx {
   uint8_t* d_flags = nullptr;     // precheck / decode verdicts [kMaxLanes]
   uint32_t* d_pt = nullptr;       // R' = (X:Y:Z), SoA [30][kMaxLanes]
   uint32_t* d_pre = nullptr;      // batch-encode prefix products, SoA [10][kMaxLanes]
+  uint32_t* d_perm = nullptr;     // length-bucket order of the hash lanes [kMaxLanes]
+  uint32_t* d_bucket = nullptr;   // per sub-batch: counts | flag | cursors (kBucketCtlWords each)
+  bool bucketing = false;         // edv_set_length_buckets (off: the reorder breaks coalesced loads)
   uint64_t scratch_lanes = 0;
   // Pipelined launches: each chunk of up to kMaxLanes requests is cut into
   // kSub sub-batches whose kernels alternate between `stream` (or the
@@ -622,22 +710,36 @@ struct SubBatch {
   const uint8_t* sig;  // first request of the sub-batch
   const uint8_t* pk;   // general path: its keys
   const uint32_t* kidx;  // keyed path: its key ids
-  const uint64_t* off;   // its msg_off
+  const uint64_t* ms;    // its message starts
+  const uint64_t* me;    // its message ends
   unsigned long long* words;
   uint64_t cn, soff;
 };
 
 int launch_sub(edv_ctx* ctx, bool keyed, const SubBatch& b, const uint8_t* msgs, uint64_t chunk, hipStream_t q,
-               hipEvent_t* ev) {
+               hipEvent_t* ev, int sub) {
   const uint32_t grid = (uint32_t)div_up(b.cn, kBlock);
   uint32_t* hs = ctx->d_hsoa + b.soff;
   uint8_t* fl = ctx->d_flags + b.soff;
   uint32_t* pt = ctx->d_pt + b.soff;
+  uint32_t* perm = nullptr;
+  uint32_t* bctl = ctx->d_bucket + (uint64_t)sub * kBucketCtlWords;
   HIP_TRY(hipEventRecord(ev[0], q));
+  if (ctx->bucketing && b.cn > 64) {
+    // hash lanes in SHA-512 block-count order (longest first)
+    perm = ctx->d_perm + b.soff;
+    HIP_TRY(hipMemsetAsync(bctl, 0, kBucketCtlWords * 4, q));
+    hipLaunchKernelGGL(edv_len_hist_kernel, dim3(grid), dim3(kBlock), 0, q, b.ms, b.me, b.cn, bctl);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(edv_len_scan_kernel, dim3(1), dim3(64), 0, q, bctl);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(edv_len_scatter_kernel, dim3(grid), dim3(kBlock), 0, q, b.ms, b.me, b.cn, bctl, perm);
+    HIP_TRY(hipGetLastError());
+  }
   if (keyed) {
     const uint32_t kc = (uint32_t)ctx->key_count;
     hipLaunchKernelGGL(edv_hash_keyed_kernel, dim3(grid), dim3(kBlock), 0, q, b.sig, b.kidx, kc, ctx->d_key_pk,
-                       ctx->d_key_valid, msgs, b.off, b.cn, hs, fl, chunk);
+                       ctx->d_key_valid, msgs, b.ms, b.me, b.cn, hs, fl, chunk, perm, bctl);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ev[1], q));
     HIP_TRY(hipEventRecord(ev[2], q));
@@ -658,7 +760,8 @@ int launch_sub(edv_ctx* ctx, bool keyed, const SubBatch& b, const uint8_t* msgs,
     // the per-lane A tables are per 256-lane block of the chunk: sub-batch
     // offsets are multiples of the block size, so each sub-batch has its own
     uint32_t* tab = (uint32_t*)((char*)ctx->d_scratch + (b.soff / kBlock) * (uint64_t)kRegionBytes);
-    hipLaunchKernelGGL(edv_hash_kernel, dim3(grid), dim3(kBlock), 0, q, b.sig, b.pk, msgs, b.off, b.cn, hs, fl, chunk);
+    hipLaunchKernelGGL(edv_hash_kernel, dim3(grid), dim3(kBlock), 0, q, b.sig, b.pk, msgs, b.ms, b.me, b.cn, hs, fl,
+                       chunk, perm, bctl);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ev[1], q));
     hipLaunchKernelGGL(edv_table_kernel, dim3(grid), dim3(kBlock), 0, q, b.pk, b.cn, tab, fl, chunk);
@@ -680,10 +783,9 @@ int launch_sub(edv_ctx* ctx, bool keyed, const SubBatch& b, const uint8_t* msgs,
 constexpr uint64_t kSubAlign = 64ull * kEncodeM > (uint64_t)kBlock ? 64ull * kEncodeM : (uint64_t)kBlock;
 
 int launch_pipeline(edv_ctx* ctx, bool keyed, const void* d_sig, const void* d_keys, const void* d_msgs,
-                    const void* d_off, uint64_t n, void* d_words, hipStream_t st) {
+                    const uint64_t* ms, const uint64_t* me, uint64_t n, void* d_words, hipStream_t st) {
   if (n == 0) return 0;
   const uint8_t* sig = (const uint8_t*)d_sig;
-  const uint64_t* off = (const uint64_t*)d_off;
   unsigned long long* words = (unsigned long long*)d_words;
   const uint64_t chunk = ctx->scratch_lanes;  // multiple of kSubAlign
   // stream2 starts after everything already queued on st (the inputs)
@@ -702,10 +804,11 @@ int launch_pipeline(edv_ctx* ctx, bool keyed, const void* d_sig, const void* d_k
       b.sig = sig + 64 * (c0 + s0);
       b.pk = keyed ? nullptr : (const uint8_t*)d_keys + 32 * (c0 + s0);
       b.kidx = keyed ? (const uint32_t*)d_keys + (c0 + s0) : nullptr;
-      b.off = off + c0 + s0;
+      b.ms = ms + c0 + s0;
+      b.me = me + c0 + s0;
       b.words = words + (c0 + s0) / 64;
       hipStream_t q = (ns & 1) ? ctx->stream2 : st;
-      int r = launch_sub(ctx, keyed, b, (const uint8_t*)d_msgs, chunk, q, ctx->ev_sub[ns]);
+      int r = launch_sub(ctx, keyed, b, (const uint8_t*)d_msgs, chunk, q, ctx->ev_sub[ns], ns);
       if (r) return r;
     }
     ctx->last_nsub = ns;
@@ -725,7 +828,8 @@ int launch_pipeline(edv_ctx* ctx, bool keyed, const void* d_sig, const void* d_k
 
 int launch_verify(edv_ctx* ctx, const void* d_sig, const void* d_pk, const void* d_msgs, const void* d_off, uint64_t n,
                   void* d_words, hipStream_t st) {
-  return launch_pipeline(ctx, false, d_sig, d_pk, d_msgs, d_off, n, d_words, st);
+  const uint64_t* off = (const uint64_t*)d_off;
+  return launch_pipeline(ctx, false, d_sig, d_pk, d_msgs, off, off + 1, n, d_words, st);
 }
 
 }  // namespace
@@ -805,7 +909,8 @@ static int launch_verify_keyed(edv_ctx* ctx, const void* d_sig, const void* d_ki
                                const void* d_off, uint64_t n, void* d_words, hipStream_t st) {
   if (n == 0) return 0;
   if (ctx->key_count == 0) return set_err(EDV_EINVAL, "no registered keys");
-  return launch_pipeline(ctx, true, d_sig, d_kidx, d_msgs, d_off, n, d_words, st);
+  const uint64_t* off = (const uint64_t*)d_off;
+  return launch_pipeline(ctx, true, d_sig, d_kidx, d_msgs, off, off + 1, n, d_words, st);
 }
 
 extern "C" {
@@ -880,6 +985,18 @@ int edv_verify_batch_keyed_device(edv_ctx* ctx, const void* d_sig64, const void*
   if (n && (!d_sig64 || !d_key_idx || !d_msgs || !d_msg_off || !d_accept_words))
     return set_err(EDV_EINVAL, "null device pointer");
   return launch_verify_keyed(ctx, d_sig64, d_key_idx, d_msgs, d_msg_off, n, d_accept_words, pick_stream(ctx, stream));
+}
+
+int edv_verify_spans_device(edv_ctx* ctx, const void* d_sig64, const void* d_keys, int keyed, const void* d_msgs,
+                            const void* d_msg_start, const void* d_msg_end, uint64_t n, void* d_accept_words,
+                            void* stream) {
+  int r = set_device(ctx);
+  if (r) return r;
+  if (n && (!d_sig64 || !d_keys || !d_msgs || !d_msg_start || !d_msg_end || !d_accept_words))
+    return set_err(EDV_EINVAL, "null device pointer");
+  if (n && keyed && ctx->key_count == 0) return set_err(EDV_EINVAL, "no registered keys");
+  return launch_pipeline(ctx, keyed != 0, d_sig64, d_keys, d_msgs, (const uint64_t*)d_msg_start,
+                         (const uint64_t*)d_msg_end, n, d_accept_words, pick_stream(ctx, stream));
 }
 
 int edv_verify_batch_keyed(edv_ctx* ctx, const uint8_t* sig64, const uint32_t* key_idx, const uint8_t* msgs,
@@ -989,6 +1106,10 @@ edv_ctx* edv_create(int device) {
     return fail("hipMalloc(pt)", e);
   if ((e = hipMalloc(&ctx->d_pre, ctx->scratch_lanes * 10 * sizeof(uint32_t))) != hipSuccess)
     return fail("hipMalloc(pre)", e);
+  if ((e = hipMalloc(&ctx->d_perm, ctx->scratch_lanes * sizeof(uint32_t))) != hipSuccess)
+    return fail("hipMalloc(perm)", e);
+  if ((e = hipMalloc(&ctx->d_bucket, edv_ctx::kSub * kBucketCtlWords * sizeof(uint32_t))) != hipSuccess)
+    return fail("hipMalloc(bucket)", e);
   if (const char* w = getenv("EDV_KEY_WINDOW")) {
     const int kw = atoi(w);
     if (kw == 4 || kw == 6 || kw == 8 || kw == 10) ctx->key_w = kw;
@@ -1006,6 +1127,8 @@ void edv_destroy(edv_ctx* ctx) {
   if (ctx->d_hsoa) (void)hipFree(ctx->d_hsoa);
   if (ctx->d_flags) (void)hipFree(ctx->d_flags);
   if (ctx->d_pt) (void)hipFree(ctx->d_pt);
+  if (ctx->d_perm) (void)hipFree(ctx->d_perm);
+  if (ctx->d_bucket) (void)hipFree(ctx->d_bucket);
   if (ctx->d_ident) (void)hipFree(ctx->d_ident);
   if (ctx->d_pre) (void)hipFree(ctx->d_pre);
   if (ctx->d_btab_comb) (void)hipFree(ctx->d_btab_comb);
@@ -1056,6 +1179,12 @@ int edv_last_phases_ms(edv_ctx* ctx, double* out4) {
 }
 
 int edv_last_launch_count(edv_ctx* ctx) { return ctx ? ctx->last_nsub : 0; }
+
+int edv_set_length_buckets(edv_ctx* ctx, int on) {
+  if (!ctx) return set_err(EDV_EINVAL, "null context");
+  ctx->bucketing = on != 0;
+  return 0;
+}
 
 int edv_set_pipeline(edv_ctx* ctx, int sub_batches) {
   if (!ctx) return set_err(EDV_EINVAL, "null context");
@@ -1165,9 +1294,26 @@ int edv_sign_batch_device(edv_ctx* ctx, const void* d_sk64, const void* d_key_id
   if (n == 0) return 0;
   if (!d_sk64 || !d_key_idx || !d_msgs || !d_msg_off || !d_sig64_out) return set_err(EDV_EINVAL, "null device pointer");
   hipStream_t st = pick_stream(ctx, stream);
+  const uint64_t* off = (const uint64_t*)d_msg_off;
   hipLaunchKernelGGL(edv_sign_kernel, dim3((uint32_t)div_up(n, kBlock)), dim3(kBlock), 0, st, (const uint8_t*)d_sk64,
-                     (const uint32_t*)d_key_idx, (const uint8_t*)d_msgs, (const uint64_t*)d_msg_off, n,
-                     ctx->d_btab_comb, (uint8_t*)d_sig64_out);
+                     (const uint32_t*)d_key_idx, (const uint8_t*)d_msgs, off, off + 1, n, ctx->d_btab_comb,
+                     (uint8_t*)d_sig64_out);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int edv_sign_spans_device(edv_ctx* ctx, const void* d_sk64, const void* d_key_idx, const void* d_msgs,
+                          const void* d_msg_start, const void* d_msg_end, uint64_t n, void* d_sig64_out,
+                          void* stream) {
+  int r = set_device(ctx);
+  if (r) return r;
+  if (n == 0) return 0;
+  if (!d_sk64 || !d_key_idx || !d_msgs || !d_msg_start || !d_msg_end || !d_sig64_out)
+    return set_err(EDV_EINVAL, "null device pointer");
+  hipStream_t st = pick_stream(ctx, stream);
+  hipLaunchKernelGGL(edv_sign_kernel, dim3((uint32_t)div_up(n, kBlock)), dim3(kBlock), 0, st, (const uint8_t*)d_sk64,
+                     (const uint32_t*)d_key_idx, (const uint8_t*)d_msgs, (const uint64_t*)d_msg_start,
+                     (const uint64_t*)d_msg_end, n, ctx->d_btab_comb, (uint8_t*)d_sig64_out);
   HIP_TRY(hipGetLastError());
   return 0;
 }

@@ -94,31 +94,49 @@ EDV_HD uint32_t funnel8(uint32_t hi, uint32_t lo, uint32_t sh) {
 }
 
 // One 128-byte block of the stream prefix || msg || 0x80 || 0... as 16
-// big-endian words.  Message word u (bytes 4u..4u+3) = funnel8(A[u+1], A[u], sh)
-// over the aligned words A[k] = aw[k], k < na, of the message's aligned base;
-// no byte past the aligned word holding the last message byte is read.
-// Blocks that reach the end of the message get the tail masked and the 0x80
-// pad byte placed (branch taken per lane only for those blocks).
+// big-endian words.  The message is read as 16-byte chunks of its 16-byte
+// aligned base (c16[q], q < nq: only chunks holding message bytes, so no read
+// can leave the pages the message lies in): at most 9 dwordx4 loads per block
+// instead of 33 dword loads.  Message word t of the block is the byte funnel
+// (sh = msg & 3) of window words V[j], V[j+1], where V is the loaded window
+// shifted by s4 = 0..3 words (per-lane selects).  Blocks that reach the end of
+// the message get the tail masked and the 0x80 pad byte placed.
+struct Chunk16 {
+  uint32_t x, y, z, w;
+};
 template <int NP, bool FIRST>
-EDV_HD void sha512_block_words(uint64_t w[16], uint64_t b, const uint32_t* prefix, const uint32_t* aw, uint64_t na,
-                               uint32_t sh, uint64_t mlen) {
-  const int64_t u0 = 32 * (int64_t)b - NP;  // message word index of stream word 0
-  uint32_t A[33];
+EDV_HD void sha512_block_words(uint64_t w[16], uint64_t b, const uint32_t* prefix, const Chunk16* c16, uint64_t nq,
+                               uint32_t d16, uint64_t mlen) {
+  constexpr int T0 = FIRST ? NP : 0;          // first message word of the block
+  constexpr int NW = 32 - T0;                 // message words in the block
+  constexpr int NCH = (NW * 4 + 15 + 15) / 16;  // chunks covering them at any misalignment
+  const int64_t u0 = 32 * (int64_t)b - NP;    // message word index of stream word 0
+  const uint64_t pos = d16 + 4 * (uint64_t)(u0 + T0);  // base16 byte of the block's first message byte
+  const uint64_t q0 = pos >> 4;
+  const uint32_t s4 = (uint32_t)(pos >> 2) & 3u, sh = d16 & 3u;
+  uint32_t W[4 * NCH];
 #pragma unroll
-  for (int t = 0; t < 33; ++t) {
-    const int64_t k = u0 + t;
-    if (FIRST && t < NP) {
-      A[t] = 0;
-    } else {
-      A[t] = (k >= 0 && (uint64_t)k < na) ? aw[k] : 0u;
-    }
+  for (int c = 0; c < NCH; ++c) {
+    Chunk16 v = {0u, 0u, 0u, 0u};
+    if (q0 + c < nq) v = c16[q0 + c];
+    W[4 * c] = v.x;
+    W[4 * c + 1] = v.y;
+    W[4 * c + 2] = v.z;
+    W[4 * c + 3] = v.w;
+  }
+  uint32_t V[NW + 1];
+#pragma unroll
+  for (int j = 0; j <= NW; ++j) {
+    const uint32_t a0 = W[j], a1 = j + 1 < 4 * NCH ? W[j + 1] : 0u, a2 = j + 2 < 4 * NCH ? W[j + 2] : 0u,
+                   a3 = j + 3 < 4 * NCH ? W[j + 3] : 0u;
+    V[j] = s4 == 0 ? a0 : s4 == 1 ? a1 : s4 == 2 ? a2 : a3;
   }
   uint32_t le[32];
 #pragma unroll
-  for (int t = 0; t < 32; ++t) le[t] = (FIRST && t < NP) ? prefix[t < NP ? t : 0] : funnel8(A[t + 1], A[t], sh);
+  for (int t = 0; t < 32; ++t) le[t] = t < T0 ? prefix[t < NP ? t : 0] : funnel8(V[t - T0 + 1], V[t - T0], sh);
   if (4 * (u0 + 32) > (int64_t)mlen) {
 #pragma unroll
-    for (int t = (FIRST ? NP : 0); t < 32; ++t) {
+    for (int t = T0; t < 32; ++t) {
       const int64_t rem = (int64_t)mlen - 4 * (u0 + t);  // message bytes left at this word
       const uint32_t r = rem <= 0 ? 0u : rem >= 4 ? 4u : (uint32_t)rem;
       const uint32_t keep = r >= 4 ? 0xffffffffu : ((1u << (8 * r)) - 1u);
@@ -140,11 +158,11 @@ EDV_HD void sha512_prefixed(uint32_t digest[16], const uint32_t prefix[NP], cons
   const uint64_t total = 4 * NP + mlen;            // stream bytes before padding
   const uint64_t nblocks = (total + 16) / 128 + 1;  // incl. 0x80 and 128-bit length
   const uint64_t bitlen = total * 8;
-  const uint32_t sh = (uint32_t)((uintptr_t)msg & 3);
-  const uint32_t* aw = (const uint32_t*)(msg - sh);  // pointer arithmetic keeps the address space
-  const uint64_t na = (sh + mlen + 3) / 4;
+  const uint32_t d16 = (uint32_t)((uintptr_t)msg & 15);
+  const Chunk16* c16 = (const Chunk16*)(msg - d16);  // pointer arithmetic keeps the address space
+  const uint64_t nq = (d16 + mlen + 15) / 16;
   uint64_t w[16];
-  sha512_block_words<NP, true>(w, 0, prefix, aw, na, sh, mlen);
+  sha512_block_words<NP, true>(w, 0, prefix, c16, nq, d16, mlen);
   if (nblocks == 1) {
     w[14] = 0;
     w[15] = bitlen;
@@ -152,7 +170,7 @@ EDV_HD void sha512_prefixed(uint32_t digest[16], const uint32_t prefix[NP], cons
   sha512_compress(st, w);
 #pragma unroll 1
   for (uint64_t b = 1; b < nblocks; ++b) {
-    sha512_block_words<NP, false>(w, b, prefix, aw, na, sh, mlen);
+    sha512_block_words<NP, false>(w, b, prefix, c16, nq, d16, mlen);
     if (b == nblocks - 1) {
       w[14] = 0;
       w[15] = bitlen;

@@ -30,6 +30,7 @@ SIGNATURES = {
     "edv_last_phases_ms": (_I, [_P, _P]),
     "edv_last_launch_count": (_I, [_P]),
     "edv_set_pipeline": (_I, [_P, _I]),
+    "edv_set_length_buckets": (_I, [_P, _I]),
     "edv_last_phase_ms": (_I, [_P, _P, _P, _P]),
     "edv_last_kernel_ms": (_c.c_double, [_P]),
     "edv_keys_add": (_I, [_P, _P, _U64, _P]),
@@ -40,8 +41,10 @@ SIGNATURES = {
     "edv_keys_window": (_I, [_P]),
     "edv_verify_batch_keyed": (_I, [_P, _P, _P, _P, _P, _U64, _P]),
     "edv_verify_batch_keyed_device": (_I, [_P, _P, _P, _P, _P, _U64, _P, _P]),
+    "edv_verify_spans_device": (_I, [_P, _P, _P, _I, _P, _P, _P, _U64, _P, _P]),
     "edv_seed_keypair_batch": (_I, [_P, _P, _U64, _P, _P]),
     "edv_sign_batch_device": (_I, [_P, _P, _P, _P, _P, _U64, _P, _P]),
+    "edv_sign_spans_device": (_I, [_P, _P, _P, _P, _P, _P, _U64, _P, _P]),
     "edv_sign_batch": (_I, [_P, _P, _P, _P, _P, _U64, _P]),
     "edv_tally_device": (_I, [_P, _P, _P, _P, _P, _U64, _U32, _U32, _P, _P, _P, _P]),
     "edv_tally_finish_device": (_I, [_P, _P, _U32, _U32, _P, _P, _P]),

@@ -174,6 +174,10 @@ class EdVerifyEngine:
         """Sub-batches per chunk (1..4; 1 = kernels run one at a time)."""
         check(self._lib.edv_set_pipeline(self._ctx, int(sub_batches)))
 
+    def set_length_buckets(self, on):
+        """Hash lanes sorted by SHA-512 block count (default off; edverify.h)."""
+        check(self._lib.edv_set_length_buckets(self._ctx, 1 if on else 0))
+
     # ------------------------------------------------------------ key tables
     def keys_set_window(self, w):
         """Comb window of the key tables: 4 (64 KiB/key, 64 additions per
@@ -226,6 +230,16 @@ class EdVerifyEngine:
         check(self._lib.edv_verify_batch_keyed_device(self._ctx, _dev(d_sig64), _dev(d_key_idx), _dev(d_msgs),
                                                       _dev(d_msg_off), n, _dev(d_accept_words), st))
 
+    def verify_spans_device(self, d_sig64, d_keys, keyed, d_msgs, d_msg_start, d_msg_end, n, d_accept_words,
+                            stream=None):
+        """Verify with message spans (item i = msgs[start[i]:end[i]]): the
+        signatures of a multi-signature request share one message copy.
+        keyed: d_keys are uint32 key ids, else n x 32 key bytes."""
+        st = _stream_for(stream, d_sig64, d_accept_words)
+        check(self._lib.edv_verify_spans_device(self._ctx, _dev(d_sig64), _dev(d_keys), 1 if keyed else 0,
+                                                _dev(d_msgs), _dev(d_msg_start), _dev(d_msg_end), n,
+                                                _dev(d_accept_words), st))
+
     # ------------------------------------------------------------------ sign
     def seed_keypair_batch(self, seeds32):
         seeds32 = _u8(seeds32, 32)
@@ -254,6 +268,12 @@ class EdVerifyEngine:
         st = _stream_for(stream, d_sk64, d_sig_out)
         check(self._lib.edv_sign_batch_device(self._ctx, _dev(d_sk64), _dev(d_key_idx), _dev(d_msgs),
                                               _dev(d_msg_off), n, _dev(d_sig_out), st))
+
+    def sign_spans_device(self, d_sk64, d_key_idx, d_msgs, d_msg_start, d_msg_end, n, d_sig_out, stream=None):
+        """Deterministic signatures over message spans (item i = msgs[start[i]:end[i]])."""
+        st = _stream_for(stream, d_sig_out)
+        check(self._lib.edv_sign_spans_device(self._ctx, _dev(d_sk64), _dev(d_key_idx), _dev(d_msgs),
+                                              _dev(d_msg_start), _dev(d_msg_end), n, _dev(d_sig_out), st))
 
     # ----------------------------------------------------------------- tally
     def tally(self, key, voter, phase, valid, n_keys, n_validators):

@@ -187,3 +187,75 @@ def test_sub_batch_boundaries(gpu_engine, oracle, n):
     gpu_engine.keys_add(uniq)
     gotk = gpu_engine.verify_batch_keyed(sig, inv.reshape(-1).astype(np.uint32), buf, off)
     assert (gotk == got1).all(), np.nonzero(gotk != got1)
+
+
+def test_length_buckets_mixed_lengths(gpu_engine, oracle):
+    """configs[3]-style lengths (log-uniform 0 B .. 4 KiB): the hash lanes run in
+    SHA-512 block-count order; verdicts equal the unsorted run and the oracle."""
+    rng = np.random.default_rng(33)
+    n = 2500
+    pk, sk = gpu_engine.seed_keypair_batch(rng.integers(0, 256, (31, 32), dtype=np.uint8))
+    kidx = rng.integers(0, 31, n).astype(np.uint32)
+    lens = np.exp(rng.uniform(0, np.log(4096), n)).astype(int)
+    lens[::17] = 0
+    msgs = [bytes(rng.integers(0, 256, int(m), dtype=np.uint8)) for m in lens]
+    buf, off = pack_messages(msgs)
+    sig = gpu_engine.sign_batch(sk, kidx, buf, off)
+    sig[::5, 33] ^= 4
+    pks = pk[kidx]
+    gpu_engine.set_length_buckets(True)
+    got = gpu_engine.verify_batch(sig, pks, buf, off)
+    gpu_engine.set_length_buckets(False)
+    plain = gpu_engine.verify_batch(sig, pks, buf, off)
+    gpu_engine.set_length_buckets(True)
+    assert (got == plain).all(), np.nonzero(got != plain)
+    want = np.ones(n, bool)
+    want[::5] = False
+    assert (got == want).all(), np.nonzero(got != want)
+    for i in range(0, n, 83):
+        assert got[i] == (oracle.oracle_verify_detached(sig[i].tobytes(), msgs[i], len(msgs[i]),
+                                                       pks[i].tobytes()) == 0), i
+
+
+def test_spans_share_messages(gpu_engine):
+    """edv_verify_spans_device: k signatures over one message copy (multi-sig
+    requests) give the same bits as the contiguous layout with duplicated
+    messages, on both paths."""
+    import torch
+    rng = np.random.default_rng(34)
+    pk, sk = gpu_engine.seed_keypair_batch(rng.integers(0, 256, (9, 32), dtype=np.uint8))
+    reqs = [bytes(rng.integers(0, 256, int(rng.integers(64, 900)), dtype=np.uint8)) for _ in range(300)]
+    rbuf, roff = pack_messages(reqs)
+    item_req, item_key = [], []
+    for r in range(len(reqs)):
+        k = int(rng.integers(1, 6))
+        item_req += [r] * k
+        item_key += list(rng.choice(9, k, replace=False))
+    item_req = np.array(item_req)
+    item_key = np.array(item_key, np.uint32)
+    n = len(item_req)
+    dup = [reqs[r] for r in item_req]
+    dbuf, doff = pack_messages(dup)
+    sig = gpu_engine.sign_batch(sk, item_key, dbuf, doff)
+    sig[::7, 5] ^= 1
+    want = gpu_engine.verify_batch(sig, pk[item_key], dbuf, doff)
+    assert want.sum() == n - len(range(0, n, 7))
+    dev = torch.device("cuda", 0)
+    d_sig = torch.from_numpy(sig).to(dev)
+    d_msgs = torch.from_numpy(np.concatenate([rbuf, np.zeros(16, np.uint8)])).to(dev)
+    d_ms = torch.from_numpy(roff[:-1][item_req].astype(np.int64)).to(dev)
+    d_me = torch.from_numpy(roff[1:][item_req].astype(np.int64)).to(dev)
+    words = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
+    d_pk = torch.from_numpy(pk[item_key]).to(dev)
+    gpu_engine.verify_spans_device(d_sig, d_pk, False, d_msgs, d_ms, d_me, n, words)
+    torch.cuda.synchronize()
+    got = np.unpackbits(words.cpu().numpy().view(np.uint8), bitorder="little")[:n].astype(bool)
+    assert (got == want).all()
+    gpu_engine.keys_reset()
+    gpu_engine.keys_add(pk)
+    words.zero_()
+    d_k = torch.from_numpy(item_key.astype(np.int32)).to(dev)
+    gpu_engine.verify_spans_device(d_sig, d_k, True, d_msgs, d_ms, d_me, n, words)
+    torch.cuda.synchronize()
+    got = np.unpackbits(words.cpu().numpy().view(np.uint8), bitorder="little")[:n].astype(bool)
+    assert (got == want).all()

@@ -27,8 +27,8 @@ def test_kernel_sha512_any_alignment(hostcheck):
     for t in range(200):
         pre = bytes(rng.getrandbits(8) for _ in range(64))
         m = bytes(rng.getrandbits(8) for _ in range(rng.randrange(0, 600)))
-        off = rng.randrange(0, 4)
-        buf = ctypes.create_string_buffer(b"\0" * off + m + b"\0" * 8)
+        off = rng.randrange(0, 16)
+        buf = ctypes.create_string_buffer(b"\0" * off + m + b"\0" * 16)
         out = ctypes.create_string_buffer(64)
         hostcheck.edv_host_sha512_prefixed(out, pre, ctypes.byref(buf, off), ctypes.c_uint64(len(m)))
         assert out.raw == hashlib.sha512(pre + m).digest()
