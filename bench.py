@@ -45,12 +45,13 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=1_000_000, help="requests per GPU")
+    ap.add_argument("--n", "--requests", dest="n", type=int, default=1_000_000, help="requests per GPU")
     ap.add_argument("--signers", type=int, default=1000)
     ap.add_argument("--alias-len", type=int, default=43, help="pads the NYM signing payload to ~200 B")
-    ap.add_argument("--config", choices=["c1", "c2", "c3"], default="c1",
+    ap.add_argument("--config", choices=["c1", "c2", "c3", "c4"], default="c1",
                     help="c1: configs[1] all-valid NYMs; c2: configs[2] 10%% corrupted; c3: configs[3] "
-                         "multi-signature requests, 64 B - 4 KiB payloads")
+                         "multi-signature requests, 64 B - 4 KiB payloads; c4: configs[4] 2M NYMs per GPU "
+                         "(16M on 8) + 25-validator PREPARE/COMMIT tally in the step")
     ap.add_argument("--cpu-sample", type=int, default=400_000, help="items timed on host libsodium (rank 0, N=1)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, affinity CPUs)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -63,6 +64,9 @@ def parse():
                     help="sub-batches per chunk (edv_set_pipeline; 1 = one launch per kernel, no overlap)")
     ap.add_argument("--length-buckets", action="store_true",
                     help="hash lanes in SHA-512 block-count order (edv_set_length_buckets on)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (the product); gloo only to rehearse N > 1 on one GPU")
+    ap.add_argument("--same-device", action="store_true", help="every rank on cuda:0 (with --dist-backend gloo)")
     ap.add_argument("--general-steps", type=int, default=5,
                     help="also time the general path for this many steps (0 = skip)")
     return ap.parse_args()
@@ -125,21 +129,26 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.same_device:  # rehearsal of the N > 1 logic on a one-GPU box (gloo)
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
     eng = EdVerifyEngine(local)
     eng.set_pipeline(args.pipeline)
     eng.set_length_buckets(args.length_buckets)
-    n = args.n
+    n = args.n if not (args.config == "c4" and args.n == 1_000_000) else 2_000_000
 
     # ---- synthetic signed batch (not timed)
     seeds = synth.signer_seeds(args.signers)
     pks, sks = eng.seed_keypair_batch(seeds)
     d_sk = torch.from_numpy(sks).to(dev)
     expect = np.ones(n, dtype=bool)
-    if args.config in ("c1", "c2"):
+    if args.config in ("c1", "c2", "c4"):
         msgs_l, key_idx, _ = synth.nym_messages(n, pks, alias_len=args.alias_len, seed=1 + rank,
                                                 req_id_base=synth.REQ_ID_BASE + rank * n)
         buf, off = pack_messages(msgs_l)
@@ -216,6 +225,58 @@ def main():
 
     step = step_keyed if args.path == "keyed" else step_general
 
+    tally_check = None
+    if args.config == "c4":
+        # configs[4]: votes of 3PC batches (Max3PCBatchSize = 100 requests,
+        # plenum/config.py:185): K = all ranks' requests / 100 keys x 25
+        # validators x {PREPARE, COMMIT}.  Vote j of this rank is backed by
+        # request j's signature (its accept bit) and ~5% are missing/invalid.
+        # Step += unpack bits -> ballot scatter -> RCCL all-reduce(MAX) of the
+        # ballots (set union) -> counts + Quorums(25) flags (quorums.py:15-32).
+        V = 25
+        n_keys = n * world // 100
+        nv = n // 2
+        g = np.arange(nv, dtype=np.int64) + rank * nv
+        v_key = (g // (2 * V)).astype(np.uint32)
+        v_phase = ((g % (2 * V)) // V).astype(np.uint8)
+        v_voter = (g % V).astype(np.uint8)
+        keep = np.random.default_rng(40 + rank).random(nv) >= 0.05
+        d_vkey, d_vphase, d_vvoter = (torch.from_numpy(a).to(dev) for a in
+                                      (v_key.astype(np.int32), v_phase, v_voter))
+        d_keep = torch.from_numpy(keep.astype(np.uint8)).to(dev)
+        d_ballot = torch.zeros(n_keys * 2 * V, dtype=torch.uint8, device=dev)
+        d_counts = torch.zeros(n_keys * 2, dtype=torch.int32, device=dev)
+        d_quorum = torch.zeros(n_keys, dtype=torch.uint8, device=dev)
+        shifts = torch.arange(8, dtype=torch.uint8, device=dev)
+        verify_step = step
+
+        def step_c4():
+            verify_step()
+            bits = ((d_words.view(torch.uint8)[: (nv + 7) // 8].unsqueeze(1) >> shifts) & 1).reshape(-1)[:nv]
+            d_valid = bits * d_keep
+            eng.tally_device(d_vkey, d_vvoter, d_vphase, d_valid, nv, n_keys, V, d_ballot, d_counts, d_quorum,
+                             stream=stream)
+            if world > 1:
+                dist.all_reduce(d_ballot, op=dist.ReduceOp.MAX)
+            eng.tally_finish_device(d_ballot, n_keys, V, d_counts, d_quorum, stream=stream)
+
+        step = step_c4
+
+        def tally_check():
+            # expected: every rank's kept votes (all signatures valid here)
+            cnt = np.zeros(n_keys * 2, np.int64)
+            for r in range(world):
+                gr = np.arange(nv, dtype=np.int64) + r * nv
+                kr = np.random.default_rng(40 + r).random(nv) >= 0.05
+                np.add.at(cnt, (gr // (2 * V)) * 2 + (gr % (2 * V)) // V, kr.astype(np.int64))
+            f = (V - 1) // 3
+            q = ((cnt[0::2] >= V - f - 1).astype(np.uint8) | ((cnt[1::2] >= V - f).astype(np.uint8) << 1))
+            got_c = d_counts.cpu().numpy().astype(np.int64)
+            got_q = d_quorum.cpu().numpy()
+            return {"keys": n_keys, "votes_per_gpu": nv, "validators": V,
+                    "counts_match": bool((got_c == cnt).all()), "quorum_match": bool((got_q == q).all()),
+                    "prepare_quorums": int((got_q & 1).sum()), "commit_quorums": int((got_q >> 1 & 1).sum())}
+
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -236,6 +297,8 @@ def main():
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
+
+    tally_result = tally_check() if tally_check else None
 
     # ---- parity of the timed output against the construction
     words = d_words.cpu().numpy().view(np.uint64)
@@ -333,7 +396,9 @@ def main():
             "config": {"workload": "configs[%d]: %d %s per GPU, %.0f B mean signed payload, %d signers%s%s" % (
                 int(args.config[1]), n, "signature verifications" if args.config == "c3" else "single-signature requests",
                 mlen_mean, args.signers,
-                ", 10% corrupted/non-canonical/small-order" if args.config == "c2" else ", all valid", req_desc),
+                ", 10% corrupted/non-canonical/small-order" if args.config == "c2" else ", all valid",
+                req_desc + (" + PREPARE/COMMIT tally of %d keys x 25 validators in the step (RCCL all-reduce MAX "
+                            "of the ballots)" % (n * world // 100) if args.config == "c4" else "")),
                        "requests_per_gpu": n, "signers": args.signers, "parallelism": "dp%d (request-index shards)" % world},
             "roofline": {"bound": "valu", "kernel": kernel_name, "achieved": achieved, "peak": peak,
                          "unit": "TMAD/s", "frac": achieved / peak, "traffic": traffic,
@@ -353,6 +418,7 @@ def main():
             "other_path": other,
             "cpu_baseline": cpu,
             "parity": {"mismatches_vs_construction": mismatches, "accepted": int(got.sum()), "expected": int(expect.sum())},
+            "tally": tally_result,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
