@@ -173,13 +173,28 @@ class GpuAuthMixin:
     class -- including the reference's own plenum.server.client_authn.SimpleAuthNr
     (INTEGRATION.md), which keeps node.py:2482's isinstance check true."""
 
-    def _gpu_init(self, engine=None, device=0, verdict_cache_size=1 << 20):
+    def _gpu_init(self, engine=None, device=0, verdict_cache_size=1 << 20, key_window=8, max_keys=16384,
+                  hot_key_uses=2):
+        """key_window / max_keys: the engine's key store (comb tables in HBM,
+        edv_keys_set_window: W=8 is 512 KiB per key, so 16,384 keys = 8 GiB).
+        Verkeys given to addIdr, and keys seen in `hot_key_uses` requests, are
+        registered; their requests take the key-table path, the rest the
+        general path (same verdicts).  The authenticator owns the engine's key
+        store (it resets it on first use)."""
         self.engine = engine
         self._device = device
         self._keys = VerkeyCache()
         self._verdicts = OrderedDict()
         self._verdict_cache_size = verdict_cache_size
-        self.stats = {"batches": 0, "batch_items": 0, "cache_hits": 0, "single_verifies": 0}
+        self._key_window = key_window
+        self._max_keys = max_keys
+        self._hot_key_uses = hot_key_uses
+        self._key_ids = {}            # 32-byte key -> engine key id
+        self._key_uses = {}
+        self._keys_pending = OrderedDict()
+        self._key_store_ready = False
+        self.stats = {"batches": 0, "batch_items": 0, "cache_hits": 0, "single_verifies": 0, "keyed_items": 0,
+                      "keys_registered": 0}
 
     def _engine(self):
         if self.engine is None:
@@ -193,6 +208,84 @@ class GpuAuthMixin:
         except TypeError:
             return DidVerifier(verkey, identifier=identifier).key
         return self._keys.resolve(verkey, identifier)
+
+    # -- key-table registration (edv_keys_add) --------------------------------
+    def addIdr(self, identifier, verkey, role=None):
+        super().addIdr(identifier, verkey, role)
+        try:
+            key = self._resolve_key(verkey, identifier)
+        except Exception:
+            return  # authenticate() raises the reference's error for this key later
+        if key and len(key) == 32 and key not in self._key_ids:
+            self._keys_pending[key] = None
+
+    def _register_keys(self, keys):
+        eng = self._engine()
+        if not hasattr(eng, "keys_add"):
+            return
+        if not self._key_store_ready:
+            eng.keys_reset()
+            if hasattr(eng, "keys_set_window"):
+                eng.keys_set_window(self._key_window)
+            self._key_store_ready = True
+        room = self._max_keys - len(self._key_ids)
+        fresh = [k for k in OrderedDict.fromkeys(keys) if k not in self._key_ids][:max(room, 0)]
+        if not fresh:
+            return
+        import numpy as np
+        first = eng.keys_add(np.frombuffer(b"".join(fresh), np.uint8).reshape(-1, 32))
+        for i, k in enumerate(fresh):
+            self._key_ids[k] = first + i
+        self.stats["keys_registered"] += len(fresh)
+
+    def _split_keyed(self, todo):
+        """Register pending and hot keys, then split items into (keyed, general)."""
+        hot = []
+        for p in todo:
+            if p.key in self._key_ids:
+                continue
+            u = self._key_uses.get(p.key, 0) + 1
+            self._key_uses[p.key] = u
+            if u >= self._hot_key_uses:
+                hot.append(p.key)
+        if self._keys_pending or hot:
+            keys = list(self._keys_pending) + hot
+            self._keys_pending.clear()
+            self._register_keys(keys)
+            for k in keys:
+                self._key_uses.pop(k, None)
+        keyed = [p for p in todo if p.key in self._key_ids]
+        general = [p for p in todo if p.key not in self._key_ids]
+        return keyed, general
+
+    def _verify_keyed(self, items):
+        """crypto_sign_open(sig || ser) against registered keys: the split at
+        byte 64 done on the host (nacl_wrappers.py:108), len < 64 rejects."""
+        import numpy as np
+        n = len(items)
+        sig = np.zeros((n, 64), np.uint8)
+        ids = np.zeros(n, np.uint32)
+        msgs, offs, pos, short = [], [0], 0, np.zeros(n, bool)
+        for i, p in enumerate(items):
+            if len(p.sig) == 64:
+                s64, m = p.sig, p.ser
+            else:
+                sm = p.sig + p.ser
+                if len(sm) < 64:
+                    short[i] = True
+                    s64, m = b"\0" * 64, b""
+                else:
+                    s64, m = sm[:64], sm[64:]
+            sig[i] = np.frombuffer(s64, np.uint8)
+            ids[i] = self._key_ids[p.key]
+            msgs.append(m)
+            pos += len(m)
+            offs.append(pos)
+        ok = self._engine().verify_batch_keyed(sig, ids, np.frombuffer(b"".join(msgs), np.uint8),
+                                               np.asarray(offs, np.uint64))
+        ok = np.asarray(ok, bool) & ~short
+        self.stats["keyed_items"] += n
+        return ok
 
     # -- verify-ahead cache ------------------------------------------------
     @staticmethod
@@ -212,15 +305,22 @@ class GpuAuthMixin:
             self.stats["cache_hits"] += 1
             return hit
         self.stats["single_verifies"] += 1
-        ok = bool(self._engine().sign_open_batch(p.sig + p.ser, [0, len(p.sig) + len(p.ser)], [p.key])[0])
+        ok = self._verify_many([p])[0]
         self._remember(p, ok)
         return ok
 
     def _verify_many(self, prepared):
-        """One GPU launch over prepared items (crypto_sign_open semantics);
-        items without a usable key are False without touching the GPU."""
+        """GPU launches over prepared items (crypto_sign_open semantics): items
+        whose key is registered take the key-table path, the rest one general
+        launch; items without a usable key are False without touching the GPU."""
         todo = [p for p in prepared if p.key]
         out = {}
+        keyed, todo = self._split_keyed(todo)
+        if keyed:
+            for p, v in zip(keyed, self._verify_keyed(keyed)):
+                out[id(p)] = bool(v)
+            self.stats["batches"] += 1
+            self.stats["batch_items"] += len(keyed)
         if todo:
             sms, offs, keys, pos = [], [0], [], 0
             for p in todo:

@@ -65,6 +65,28 @@ class OracleEngine:
     def __init__(self, lib):
         self.lib = lib
         self.calls = 0
+        self.keys = []
+        self.window = 10
+
+    def keys_reset(self):
+        self.keys = []
+
+    def keys_set_window(self, w):
+        assert not self.keys
+        self.window = w
+
+    def keys_add(self, pk32):
+        first = len(self.keys)
+        self.keys.extend(bytes(r) for r in np.asarray(pk32, np.uint8).reshape(-1, 32))
+        return first
+
+    def verify_batch_keyed(self, sig64, key_idx, msgs, msg_off):
+        self.calls += 1
+        pk = np.frombuffer(b"".join(self.keys[int(k)] if int(k) < len(self.keys) else b"\0" * 32
+                                    for k in key_idx), np.uint8).reshape(-1, 32)
+        ok = self.verify_batch(sig64, pk, msgs, msg_off)
+        self.calls -= 1
+        return ok & np.array([int(k) < len(self.keys) for k in key_idx], bool)
 
     def sign_open_batch(self, sm, sm_off, pk32):
         self.calls += 1

@@ -183,3 +183,36 @@ def test_req_authenticator(oracle_engine):
     ra.register_authenticator(make(oracle_engine, good))
     assert ra.authenticate(good["msg"]) == {good["msg"]["identifier"]}
     assert isinstance(ra.core_authenticator, GpuAuthNr)
+
+
+def _outcomes(engine, max_keys):
+    out, keyed = [], 0
+    for c in kat()["cases"]:
+        a = GpuAuthNr(engine=engine)
+        a._max_keys = max_keys
+        if c["register"]:
+            a.addIdr(c["msg"].get("identifier") if c["identifier"] is None else c["identifier"], c["verkey"])
+        r = run_single(a, c)
+        out.append(r if not isinstance(r, Exception) else (type(r).__name__,
+                                                            type(r.__cause__).__name__ if r.__cause__ else None))
+        keyed += a.stats["keyed_items"]
+    return out, keyed
+
+
+def test_keyed_and_general_paths_agree(oracle_engine):
+    """addIdr registers verkeys in the engine's key store (key-table path);
+    with no room (max_keys = 0) the same requests take the general path. The
+    reference KAT outcomes (incl. 63/65-byte signatures split at byte 64 on
+    the host for the keyed path) are identical either way."""
+    with_keys, n_keyed = _outcomes(oracle_engine, 16)
+    without, n_general = _outcomes(oracle_engine, 0)
+    assert with_keys == without
+    assert n_keyed > 0 and n_general == 0
+
+
+def test_hot_keys_get_registered(oracle_engine):
+    good = next(c for c in kat()["cases"] if c["name"] == "valid-abbreviated-verkey")
+    a = GpuAuthNr(engine=oracle_engine, nym_lookup=lambda st, idr: {"verkey": good["verkey"]})
+    msgs = [dict(good["msg"]) for _ in range(4)]
+    assert a.authenticate_batch(msgs) == [good["msg"]["identifier"]] * 4
+    assert a.stats["keys_registered"] == 1 and a.stats["keyed_items"] == 4
