@@ -1,0 +1,323 @@
+// hostpack.cpp -- plenum_amd._hostpack: the host half of the authenticator's
+// batch path in native code (CPython extension, host CPU only).
+//
+// The reference does this per request in Python (plenum/server/client_authn.py:
+// 89 b58decode(signature), :92 serializeForSig -> common/serializers/
+// signing_serializer.py:35-91, nacl_wrappers.py:108 sig || msg).  SURVEY §8(f)
+// row 2: with the verify on the GPU this host work is the bottleneck of the
+// drop-in.  Every function here either returns the exact bytes the reference
+// code produces or returns None ("take the Python path"), so the reference's
+// exceptions (class, args, __cause__) are always raised by the Python
+// restatement, never reimplemented here:
+//   serialize_for_signing(obj, ignore) -> bytes | None
+//       fast path for exact str / int / bool / float / None / list / dict with
+//       str keys; float and int text come from PyObject_Str (Python's own repr),
+//       key order from PyUnicode_Compare (list.sort on str).  Anything else
+//       (subclasses, tuples, non-str keys, unencodable text) -> None.
+//   b58decode(v) -> bytes | None        (base58 0.2.4 semantics; None on any
+//                                        character outside the alphabet)
+//   pack_split64(sigs, sers) -> (sig64, msgs, off, short)
+//       crypto_sign_open's split of sm = sig || ser at byte 64, packed:
+//       sig64 n*64 bytes, msgs + off (n+1 uint64 LE), short[i] = len(sm) < 64
+//   pack_sm(sigs, sers, keys) -> (sm, off, pk32)   (edv_sign_open_batch layout)
+#define PY_SSIZE_T_CLEAN
+#include <Python.h>
+
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+namespace {
+
+// ------------------------------------------------------------------ serialize
+
+bool ser_obj(PyObject* o, int level, PyObject* ignore, std::string& out);
+
+bool append_str(PyObject* s, std::string& out) {
+  Py_ssize_t n = 0;
+  const char* p = PyUnicode_AsUTF8AndSize(s, &n);
+  if (!p) {
+    PyErr_Clear();  // e.g. lone surrogates: the reference's encode raises -> Python path
+    return false;
+  }
+  out.append(p, (size_t)n);
+  return true;
+}
+
+bool append_text_of(PyObject* o, std::string& out) {  // str(o)
+  PyObject* s = PyObject_Str(o);
+  if (!s) {
+    PyErr_Clear();
+    return false;
+  }
+  const bool ok = append_str(s, out);
+  Py_DECREF(s);
+  return ok;
+}
+
+bool ignored(PyObject* k, PyObject* ignore) {
+  if (!ignore) return false;
+  const Py_ssize_t n = PySequence_Fast_GET_SIZE(ignore);
+  PyObject** items = PySequence_Fast_ITEMS(ignore);
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    if (PyUnicode_CheckExact(items[i]) && PyUnicode_Compare(k, items[i]) == 0) return true;
+  }
+  return false;
+}
+
+bool ser_dict(PyObject* d, int level, PyObject* ignore, std::string& out) {
+  std::vector<PyObject*> keys;
+  Py_ssize_t pos = 0;
+  PyObject *k, *v;
+  while (PyDict_Next(d, &pos, &k, &v)) {
+    if (!PyUnicode_CheckExact(k)) return false;  // non-str keys: the reference may raise -> Python path
+    if (level == 0 && ignored(k, ignore)) continue;
+    keys.push_back(k);
+  }
+  bool cmp_err = false;
+  std::sort(keys.begin(), keys.end(), [&](PyObject* a, PyObject* b) {
+    const int c = PyUnicode_Compare(a, b);
+    if (c == -1 && PyErr_Occurred()) cmp_err = true;
+    return c < 0;
+  });
+  if (cmp_err) {
+    PyErr_Clear();
+    return false;
+  }
+  for (size_t i = 0; i < keys.size(); ++i) {
+    if (i) out.push_back('|');
+    if (!append_str(keys[i], out)) return false;
+    out.push_back(':');
+    PyObject* val = PyDict_GetItem(d, keys[i]);  // borrowed
+    if (!val || !ser_obj(val, level + 1, nullptr, out)) return false;
+  }
+  return true;
+}
+
+constexpr int kMaxDepth = 500;  // deeper: the Python path (which may hit RecursionError like the reference)
+
+bool ser_obj(PyObject* o, int level, PyObject* ignore, std::string& out) {
+  if (level > kMaxDepth) return false;
+  if (PyUnicode_CheckExact(o)) return append_str(o, out);
+  if (PyDict_CheckExact(o)) return ser_dict(o, level, ignore, out);
+  if (PyList_CheckExact(o)) {
+    const Py_ssize_t n = PyList_GET_SIZE(o);
+    for (Py_ssize_t i = 0; i < n; ++i) {
+      if (i) out.push_back(',');
+      if (!ser_obj(PyList_GET_ITEM(o, i), level + 1, nullptr, out)) return false;
+    }
+    return true;
+  }
+  if (o == Py_None) return true;
+  if (PyBool_Check(o)) {
+    out.append(o == Py_True ? "True" : "False");
+    return true;
+  }
+  if (PyLong_CheckExact(o) || PyFloat_CheckExact(o)) return append_text_of(o, out);
+  return false;  // tuples, sets, subclasses, other types: the Python path decides
+}
+
+PyObject* py_serialize_for_signing(PyObject*, PyObject* args) {
+  PyObject *obj, *ignore = Py_None;
+  if (!PyArg_ParseTuple(args, "O|O", &obj, &ignore)) return nullptr;
+  PyObject* ign = nullptr;
+  if (ignore != Py_None) {
+    ign = PySequence_Fast(ignore, "ignore must be a sequence");
+    if (!ign) return nullptr;
+  }
+  std::string out;
+  out.reserve(256);
+  const bool ok = ser_obj(obj, 0, ign, out);
+  Py_XDECREF(ign);
+  if (!ok) Py_RETURN_NONE;
+  return PyBytes_FromStringAndSize(out.data(), (Py_ssize_t)out.size());
+}
+
+// ------------------------------------------------------------------- base58
+
+const char kAlphabet[] = "123456789ABCDEFGHJKLMNPQRSTUVWXYZabcdefghijkmnopqrstuvwxyz";
+
+struct B58Index {
+  int8_t v[256];
+  B58Index() {
+    memset(v, -1, sizeof v);
+    for (int i = 0; i < 58; ++i) v[(unsigned char)kAlphabet[i]] = (int8_t)i;
+  }
+};
+const B58Index kIndex;
+
+// false on a character outside the alphabet.  Base conversion on 32-bit
+// limbs, five base-58 digits (58^5 < 2^32) per multiply-add pass.
+bool b58decode_raw(const unsigned char* s, size_t n, std::vector<uint8_t>& out) {
+  size_t nz = 0;
+  while (nz < n && s[nz] == '1') ++nz;
+  std::vector<uint32_t> limb;  // little-endian base 2^32 magnitude
+  limb.reserve(n / 5 + 2);
+  size_t i = nz;
+  while (i < n) {
+    uint32_t mul = 1, chunk = 0;
+    for (int k = 0; k < 5 && i < n; ++k, ++i) {
+      const int d = kIndex.v[s[i]];
+      if (d < 0) return false;
+      chunk = chunk * 58u + (uint32_t)d;
+      mul *= 58u;
+    }
+    uint64_t carry = chunk;
+    for (size_t j = 0; j < limb.size(); ++j) {
+      const uint64_t t = (uint64_t)limb[j] * mul + carry;
+      limb[j] = (uint32_t)t;
+      carry = t >> 32;
+    }
+    if (carry) limb.push_back((uint32_t)carry);
+  }
+  out.assign(nz, 0);
+  bool lead = true;
+  for (size_t j = limb.size(); j-- > 0;) {
+    for (int sh = 24; sh >= 0; sh -= 8) {
+      const uint8_t byte = (uint8_t)(limb[j] >> sh);
+      if (lead && byte == 0) continue;
+      lead = false;
+      out.push_back(byte);
+    }
+  }
+  return true;
+}
+
+PyObject* py_b58decode(PyObject*, PyObject* v) {
+  const unsigned char* s = nullptr;
+  Py_ssize_t n = 0;
+  if (PyUnicode_CheckExact(v)) {
+    if (!PyUnicode_IS_ASCII(v)) Py_RETURN_NONE;  // the reference raises ValueError
+    s = (const unsigned char*)PyUnicode_AsUTF8AndSize(v, &n);
+    if (!s) return nullptr;
+  } else if (PyBytes_CheckExact(v)) {
+    s = (const unsigned char*)PyBytes_AS_STRING(v);
+    n = PyBytes_GET_SIZE(v);
+    for (Py_ssize_t i = 0; i < n; ++i)
+      if (s[i] >= 0x80) Py_RETURN_NONE;  // .decode('ascii') raises in the reference
+  } else {
+    Py_RETURN_NONE;
+  }
+  std::vector<uint8_t> out;
+  if (!b58decode_raw(s, (size_t)n, out)) Py_RETURN_NONE;
+  return PyBytes_FromStringAndSize((const char*)out.data(), (Py_ssize_t)out.size());
+}
+
+// ------------------------------------------------------------------ packing
+
+bool bytes_of(PyObject* o, const char** p, Py_ssize_t* n) {
+  if (!PyBytes_Check(o)) {
+    PyErr_SetString(PyExc_TypeError, "bytes expected");
+    return false;
+  }
+  *p = PyBytes_AS_STRING(o);
+  *n = PyBytes_GET_SIZE(o);
+  return true;
+}
+
+PyObject* py_pack_split64(PyObject*, PyObject* args) {
+  PyObject *sigs, *sers;
+  if (!PyArg_ParseTuple(args, "OO", &sigs, &sers)) return nullptr;
+  PyObject* fs = PySequence_Fast(sigs, "sigs must be a sequence");
+  if (!fs) return nullptr;
+  PyObject* fm = PySequence_Fast(sers, "sers must be a sequence");
+  if (!fm) {
+    Py_DECREF(fs);
+    return nullptr;
+  }
+  const Py_ssize_t n = PySequence_Fast_GET_SIZE(fs);
+  PyObject* ret = nullptr;
+  if (PySequence_Fast_GET_SIZE(fm) != n) {
+    PyErr_SetString(PyExc_ValueError, "length mismatch");
+  } else {
+    std::string sig64((size_t)n * 64, '\0'), msgs, shortv((size_t)n, '\0');
+    std::vector<uint64_t> off((size_t)n + 1, 0);
+    bool ok = true;
+    for (Py_ssize_t i = 0; i < n && ok; ++i) {
+      const char *s, *m;
+      Py_ssize_t ns, nm;
+      ok = bytes_of(PySequence_Fast_GET_ITEM(fs, i), &s, &ns) && bytes_of(PySequence_Fast_GET_ITEM(fm, i), &m, &nm);
+      if (!ok) break;
+      if (ns + nm < 64) {
+        shortv[(size_t)i] = 1;  // crypto_sign_open: smlen < 64 rejects
+      } else if (ns >= 64) {
+        memcpy(&sig64[(size_t)i * 64], s, 64);
+        msgs.append(s + 64, (size_t)(ns - 64));  // sm[64:] = sig[64:] || ser
+        msgs.append(m, (size_t)nm);
+      } else {
+        memcpy(&sig64[(size_t)i * 64], s, (size_t)ns);
+        memcpy(&sig64[(size_t)i * 64 + ns], m, (size_t)(64 - ns));
+        msgs.append(m + (64 - ns), (size_t)(nm - (64 - ns)));
+      }
+      off[(size_t)i + 1] = msgs.size();
+    }
+    if (ok)
+      ret = Py_BuildValue("(y#y#y#y#)", sig64.data(), (Py_ssize_t)sig64.size(), msgs.data(), (Py_ssize_t)msgs.size(),
+                          (const char*)off.data(), (Py_ssize_t)(off.size() * 8), shortv.data(),
+                          (Py_ssize_t)shortv.size());
+  }
+  Py_DECREF(fs);
+  Py_DECREF(fm);
+  return ret;
+}
+
+PyObject* py_pack_sm(PyObject*, PyObject* args) {
+  PyObject *sigs, *sers, *keys;
+  if (!PyArg_ParseTuple(args, "OOO", &sigs, &sers, &keys)) return nullptr;
+  PyObject* fs = PySequence_Fast(sigs, "sigs must be a sequence");
+  PyObject* fm = fs ? PySequence_Fast(sers, "sers must be a sequence") : nullptr;
+  PyObject* fk = fm ? PySequence_Fast(keys, "keys must be a sequence") : nullptr;
+  PyObject* ret = nullptr;
+  if (fk) {
+    const Py_ssize_t n = PySequence_Fast_GET_SIZE(fs);
+    if (PySequence_Fast_GET_SIZE(fm) != n || PySequence_Fast_GET_SIZE(fk) != n) {
+      PyErr_SetString(PyExc_ValueError, "length mismatch");
+    } else {
+      std::string sm, pk((size_t)n * 32, '\0');
+      std::vector<uint64_t> off((size_t)n + 1, 0);
+      bool ok = true;
+      for (Py_ssize_t i = 0; i < n && ok; ++i) {
+        const char *s, *m, *k;
+        Py_ssize_t ns, nm, nk;
+        ok = bytes_of(PySequence_Fast_GET_ITEM(fs, i), &s, &ns) && bytes_of(PySequence_Fast_GET_ITEM(fm, i), &m, &nm) &&
+             bytes_of(PySequence_Fast_GET_ITEM(fk, i), &k, &nk);
+        if (!ok) break;
+        if (nk != 32) {
+          PyErr_SetString(PyExc_ValueError, "keys must be 32 bytes");
+          ok = false;
+          break;
+        }
+        sm.append(s, (size_t)ns);
+        sm.append(m, (size_t)nm);
+        off[(size_t)i + 1] = sm.size();
+        memcpy(&pk[(size_t)i * 32], k, 32);
+      }
+      if (ok)
+        ret = Py_BuildValue("(y#y#y#)", sm.data(), (Py_ssize_t)sm.size(), (const char*)off.data(),
+                            (Py_ssize_t)(off.size() * 8), pk.data(), (Py_ssize_t)pk.size());
+    }
+  }
+  Py_XDECREF(fs);
+  Py_XDECREF(fm);
+  Py_XDECREF(fk);
+  return ret;
+}
+
+PyMethodDef kMethods[] = {
+    {"serialize_for_signing", py_serialize_for_signing, METH_VARARGS,
+     "serialize_for_signing(obj, ignore=None) -> bytes, or None for the Python path"},
+    {"b58decode", py_b58decode, METH_O, "b58decode(str | bytes) -> bytes, or None for the Python path"},
+    {"pack_split64", py_pack_split64, METH_VARARGS,
+     "pack_split64(sigs, sers) -> (sig64, msgs, off_u64le, short): crypto_sign_open's split at byte 64"},
+    {"pack_sm", py_pack_sm, METH_VARARGS, "pack_sm(sigs, sers, keys) -> (sm, off_u64le, pk32)"},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyModuleDef kModule = {PyModuleDef_HEAD_INIT, "_hostpack",
+                       "Native host packing for the GPU authenticator (see csrc/hostpack.cpp)", -1, kMethods};
+
+}  // namespace
+
+PyMODINIT_FUNC PyInit__hostpack(void) { return PyModule_Create(&kModule); }

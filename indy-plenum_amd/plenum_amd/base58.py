@@ -22,7 +22,21 @@ def b58encode(v):
     return alphabet[0] * nz + "".join(reversed(out))
 
 
+try:  # native fast path (csrc/hostpack.cpp): exact bytes, or None -> the code below
+    from . import _hostpack
+except ImportError:  # pragma: no cover
+    _hostpack = None
+
+
 def b58decode(v):
+    if _hostpack is not None:
+        r = _hostpack.b58decode(v)
+        if r is not None:
+            return r
+    return b58decode_py(v)
+
+
+def b58decode_py(v):
     if not isinstance(v, str):
         v = v.decode("ascii")
     nz = len(v) - len(v.lstrip(alphabet[0]))

@@ -42,6 +42,36 @@ from .exceptions import (CouldNotAuthenticate, EmptyIdentifier, EmptySignature, 
 from .serialization import serialize_msg_for_signing
 from .verifier import DidVerifier, VerkeyCache
 
+try:  # native packing (csrc/hostpack.cpp)
+    from ._hostpack import pack_sm as _pack_sm, pack_split64 as _pack_split64
+except ImportError:  # pragma: no cover - same layout in Python
+    import struct as _struct
+
+    def _pack_sm(sigs, sers, keys):
+        offs, pos = [0], 0
+        for s_, m in zip(sigs, sers):
+            pos += len(s_) + len(m)
+            offs.append(pos)
+        sm = b"".join(s_ + m for s_, m in zip(sigs, sers))
+        return sm, _struct.pack("<%dQ" % len(offs), *offs), b"".join(keys)
+
+    def _pack_split64(sigs, sers):
+        sig64, msgs, offs, short, pos = [], [], [0], [], 0
+        for s_, m in zip(sigs, sers):
+            sm = s_ + m
+            if len(sm) < 64:
+                sig64.append(b"\0" * 64)
+                short.append(1)
+                sm = b""
+            else:
+                sig64.append(sm[:64])
+                short.append(0)
+                sm = sm[64:]
+            msgs.append(sm)
+            pos += len(sm)
+            offs.append(pos)
+        return b"".join(sig64), b"".join(msgs), _struct.pack("<%dQ" % len(offs), *offs), bytes(short)
+
 SIG = 'signature'
 SIGS = 'signatures'
 IDENTIFIER = 'identifier'
@@ -262,29 +292,12 @@ class GpuAuthMixin:
         """crypto_sign_open(sig || ser) against registered keys: the split at
         byte 64 done on the host (nacl_wrappers.py:108), len < 64 rejects."""
         import numpy as np
-        n = len(items)
-        sig = np.zeros((n, 64), np.uint8)
-        ids = np.zeros(n, np.uint32)
-        msgs, offs, pos, short = [], [0], 0, np.zeros(n, bool)
-        for i, p in enumerate(items):
-            if len(p.sig) == 64:
-                s64, m = p.sig, p.ser
-            else:
-                sm = p.sig + p.ser
-                if len(sm) < 64:
-                    short[i] = True
-                    s64, m = b"\0" * 64, b""
-                else:
-                    s64, m = sm[:64], sm[64:]
-            sig[i] = np.frombuffer(s64, np.uint8)
-            ids[i] = self._key_ids[p.key]
-            msgs.append(m)
-            pos += len(m)
-            offs.append(pos)
-        ok = self._engine().verify_batch_keyed(sig, ids, np.frombuffer(b"".join(msgs), np.uint8),
-                                               np.asarray(offs, np.uint64))
-        ok = np.asarray(ok, bool) & ~short
-        self.stats["keyed_items"] += n
+        sig64, msgs, off, short = _pack_split64([p.sig for p in items], [p.ser for p in items])
+        ids = np.fromiter((self._key_ids[p.key] for p in items), np.uint32, len(items))
+        ok = self._engine().verify_batch_keyed(np.frombuffer(sig64, np.uint8).reshape(-1, 64), ids,
+                                               np.frombuffer(msgs, np.uint8), np.frombuffer(off, np.uint64))
+        ok = np.asarray(ok, bool) & (np.frombuffer(short, np.uint8) == 0)
+        self.stats["keyed_items"] += len(items)
         return ok
 
     # -- verify-ahead cache ------------------------------------------------
@@ -322,16 +335,10 @@ class GpuAuthMixin:
             self.stats["batches"] += 1
             self.stats["batch_items"] += len(keyed)
         if todo:
-            sms, offs, keys, pos = [], [0], [], 0
-            for p in todo:
-                sms.append(p.sig)
-                sms.append(p.ser)
-                pos += len(p.sig) + len(p.ser)
-                offs.append(pos)
-                keys.append(p.key)
             import numpy as np
-            ok = self._engine().sign_open_batch(b"".join(sms), np.asarray(offs, np.uint64),
-                                                np.frombuffer(b"".join(keys), np.uint8).reshape(-1, 32))
+            sm, off, pk = _pack_sm([p.sig for p in todo], [p.ser for p in todo], [p.key for p in todo])
+            ok = self._engine().sign_open_batch(np.frombuffer(sm, np.uint8), np.frombuffer(off, np.uint64),
+                                                np.frombuffer(pk, np.uint8).reshape(-1, 32))
             self.stats["batches"] += 1
             self.stats["batch_items"] += len(todo)
             for p, v in zip(todo, ok):

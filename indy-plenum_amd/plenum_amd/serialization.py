@@ -50,5 +50,15 @@ class SigningSerializer:
 signing_serializer = SigningSerializer()
 
 
+try:  # native fast path (csrc/hostpack.cpp): exact bytes or None -> this module's code
+    from . import _hostpack
+except ImportError:  # pragma: no cover - built by __graft_entry__.build() / make
+    _hostpack = None
+
+
 def serialize_msg_for_signing(msg, topLevelKeysToIgnore=None):
+    if _hostpack is not None:
+        r = _hostpack.serialize_for_signing(msg, topLevelKeysToIgnore)
+        if r is not None:
+            return r
     return signing_serializer.serialize(msg, topLevelKeysToIgnore=topLevelKeysToIgnore)

@@ -1,0 +1,129 @@
+"""The native host packer (indy-plenum_amd/csrc/hostpack.cpp, plenum_amd._hostpack)
+against the Python restatements that the reference pins (serializer_kat.json from
+the reference's own signing_serializer.py; base58 0.2.4 semantics): every fast-path
+result is byte-identical, and every case the reference would treat differently
+(tuples, non-str keys, subclasses, unencodable text, characters outside the
+alphabet) returns None so the Python path -- and its exact exception -- runs."""
+import json
+import math
+import os
+import random
+import struct
+
+import pytest
+
+from conftest import GOLDEN
+from plenum_amd import _hostpack as H
+from plenum_amd import client_authn
+from plenum_amd.base58 import b58decode_py, b58encode
+from plenum_amd.serialization import signing_serializer
+
+
+def py_ser(obj, ignore=None):
+    return signing_serializer.serialize(obj, topLevelKeysToIgnore=ignore)
+
+
+def test_native_is_loaded():
+    assert client_authn._pack_sm is H.pack_sm and client_authn._pack_split64 is H.pack_split64
+
+
+def test_serializer_reference_kats_native():
+    n = 0
+    for case in json.load(open(os.path.join(GOLDEN, "serializer_kat.json"))):
+        if "bytes_hex" not in case:
+            continue
+        got = H.serialize_for_signing(case["msg"], case["ignore"])
+        if got is not None:  # fast path: must be the reference's bytes
+            assert got.hex() == case["bytes_hex"], case["msg"]
+            n += 1
+    assert n >= 35
+
+
+def _rand_scalar(r):
+    k = r.randrange(8)
+    if k == 0:
+        return r.choice(["", "abc", "ключ", "值|:,", "é́", "x" * r.randrange(50)])
+    if k == 1:
+        return r.randrange(-10**30, 10**30)
+    if k == 2:
+        return r.choice([0.0, -0.0, 1e16, 1e-5, 1.5e15, 123456789012345678.0, 0.1, 1 / 3, 2.5e-300, math.inf, -math.inf])
+    if k == 3:
+        return struct.unpack("<d", struct.pack("<Q", r.getrandbits(64)))[0]
+    if k == 4:
+        return r.choice([True, False])
+    if k == 5:
+        return None
+    if k == 6:
+        return r.randrange(-5, 5)
+    return r.random() * 10 ** r.randrange(-20, 20)
+
+
+def _rand_obj(r, depth=0):
+    k = r.randrange(10)
+    if depth > 4 or k < 5:
+        return _rand_scalar(r)
+    if k < 7:
+        return [_rand_obj(r, depth + 1) for _ in range(r.randrange(5))]
+    keys = ["".join(r.choice("abcXYZ_é1") for _ in range(r.randrange(1, 5))) for _ in range(r.randrange(6))]
+    return {k_: _rand_obj(r, depth + 1) for k_ in keys}
+
+
+def test_serializer_fuzz_native_equals_python():
+    r = random.Random(12)
+    fast = 0
+    for _ in range(3000):
+        obj = _rand_obj(r)
+        ignore = r.choice([None, ["signature"], ["a", "b"], []])
+        got = H.serialize_for_signing(obj, ignore)
+        want = py_ser(obj, ignore) if isinstance(obj, dict) else py_ser(obj)
+        assert got is not None, obj
+        assert got == want, obj
+        fast += 1
+    assert fast == 3000
+
+
+@pytest.mark.parametrize("obj", [
+    {"t": (1, 2)}, {"b": b"x"}, {"s": {1, 2}}, {1: "a"}, {"a": {2: "b"}}, {"x": "\ud800"},
+    {"e": __import__("enum").IntEnum("E", "A").A}, (1, 2), {"l": [1, (2,)]},
+])
+def test_serializer_unusual_types_take_python_path(obj):
+    assert H.serialize_for_signing(obj, None) is None
+
+
+def test_b58decode_native():
+    r = random.Random(3)
+    for _ in range(5000):
+        v = b"\0" * r.randrange(3) + bytes(r.getrandbits(8) for _ in range(r.randrange(0, 90)))
+        s = b58encode(v)
+        assert H.b58decode(s) == b58decode_py(s) == v
+        assert H.b58decode(s.encode()) == v
+    for bad in ["0OIl", "abc0", "é", "1 1", b"\xff", 17, None, bytearray(b"11")]:
+        assert H.b58decode(bad) is None
+
+
+def test_pack_split64_is_crypto_sign_open_split():
+    r = random.Random(4)
+    for _ in range(200):
+        n = r.randrange(0, 12)
+        sigs = [bytes(r.getrandbits(8) for _ in range(r.choice([0, 10, 63, 64, 65, 100]))) for _ in range(n)]
+        sers = [bytes(r.getrandbits(8) for _ in range(r.randrange(0, 70))) for _ in range(n)]
+        sig64, msgs, off, short = H.pack_split64(sigs, sers)
+        offs = struct.unpack("<%dQ" % (n + 1), off)
+        for i in range(n):
+            sm = sigs[i] + sers[i]
+            if len(sm) < 64:
+                assert short[i] == 1 and offs[i + 1] == offs[i]
+            else:
+                assert short[i] == 0
+                assert sig64[64 * i:64 * i + 64] == sm[:64]
+                assert msgs[offs[i]:offs[i + 1]] == sm[64:]
+
+
+def test_pack_sm_layout():
+    sigs, sers, keys = [b"s" * 64, b"t" * 3], [b"m", b""], [b"k" * 32, b"q" * 32]
+    sm, off, pk = H.pack_sm(sigs, sers, keys)
+    assert sm == b"s" * 64 + b"m" + b"t" * 3
+    assert struct.unpack("<3Q", off) == (0, 65, 68)
+    assert pk == b"k" * 32 + b"q" * 32
+    with pytest.raises(ValueError):
+        H.pack_sm([b"a"], [b"b"], [b"short"])
