@@ -116,6 +116,15 @@ static inline bool fe_in_class(const fe& f, uint32_t even_max, uint32_t odd_max)
 #endif
 
 // h = f * g.  f in W, g in L; h in C.  100 multiply-adds.
+// EDV_FE_MUL_ORDER 1 emits the products operand-major (for each f_i, one
+// product into each of the 10 accumulators), so consecutive v_mad_u64_u32 go
+// to different accumulators; 0 emits them accumulator-major.
+// EDV_FE_MUL_ORDER 2 computes the accumulators in order with the previous
+// limb's carry as the chain's initial addend (no separate 64-bit carry adds;
+// one accumulator live; a serial chain per multiply).
+#ifndef EDV_FE_MUL_ORDER
+#define EDV_FE_MUL_ORDER 2  // 2: -3% comb time vs 0 and 1 (tools/ab_keyed.py)
+#endif
 EDV_HD void fe_mul(fe& h, const fe& f, const fe& g) {
   EDV_ASSERT(EDV_IS_W(f) && EDV_IS_L(g));
   uint32_t g19[10], f2[10];
@@ -124,7 +133,46 @@ EDV_HD void fe_mul(fe& h, const fe& f, const fe& g) {
     g19[k] = 19u * g.v[k];
     f2[k] = (k & 1) ? 2u * f.v[k] : f.v[k];
   }
+#if EDV_FE_MUL_ORDER == 2
+  uint64_t c = 0;
+  uint32_t o[10];  // h may alias f or g
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+    uint64_t a = c;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      const int j = k - i;
+      const uint32_t fi = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
+      const uint32_t gj = j >= 0 ? g.v[j] : g19[j + 10];
+      a += (uint64_t)fi * gj;
+    }
+    o[k] = (uint32_t)a & fe_mask(k);
+    c = a >> fe_width(k);
+  }
+  {
+    const uint64_t t = (uint64_t)o[0] + c * 19u;  // carry out of limb 9 wraps as 19 * 2^0
+    o[0] = (uint32_t)t & M26;
+    o[1] += (uint32_t)(t >> 26);
+  }
+#pragma unroll
+  for (int k = 0; k < 10; ++k) h.v[k] = o[k];
+  return;
+#endif
   uint64_t acc[10];
+#if EDV_FE_MUL_ORDER == 1
+#pragma unroll
+  for (int k = 0; k < 10; ++k) acc[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+      const int j = k - i;
+      const uint32_t fi = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
+      const uint32_t gj = j >= 0 ? g.v[j] : g19[j + 10];
+      acc[k] += (uint64_t)fi * gj;
+    }
+  }
+#else
 #pragma unroll
   for (int k = 0; k < 10; ++k) {
     uint64_t a = 0;
@@ -137,10 +185,12 @@ EDV_HD void fe_mul(fe& h, const fe& f, const fe& g) {
     }
     acc[k] = a;
   }
+#endif
   fe_carry64(h, acc);
 }
 
-// h = f^2.  f in L; h in C.  55 multiply-adds.
+// h = f^2.  f in L; h in C.  55 multiply-adds.  With EDV_FE_MUL_ORDER 2 the
+// carry of limb k-1 is the initial addend of limb k's chain (as fe_mul).
 EDV_HD void fe_sq(fe& h, const fe& f) {
   EDV_ASSERT(EDV_IS_L(f));
   uint32_t d[10], d2[10], d19[10], d38[10];
@@ -152,9 +202,11 @@ EDV_HD void fe_sq(fe& h, const fe& f) {
     d38[k] = 38u * f.v[k];
   }
   uint64_t acc[10];
+  uint64_t c = 0;
+  uint32_t o[10];
 #pragma unroll
   for (int k = 0; k < 10; ++k) {
-    uint64_t a = 0;
+    uint64_t a = EDV_FE_MUL_ORDER == 2 ? c : 0;
 #pragma unroll
     for (int i = 0; i < 10; ++i) {
 #pragma unroll
@@ -168,8 +220,20 @@ EDV_HD void fe_sq(fe& h, const fe& f) {
       }
     }
     acc[k] = a;
+    if (EDV_FE_MUL_ORDER == 2) {
+      o[k] = (uint32_t)a & fe_mask(k);
+      c = a >> fe_width(k);
+    }
   }
-  fe_carry64(h, acc);
+  if (EDV_FE_MUL_ORDER == 2) {
+    const uint64_t t = (uint64_t)o[0] + c * 19u;
+    o[0] = (uint32_t)t & M26;
+    o[1] += (uint32_t)(t >> 26);
+#pragma unroll
+    for (int k = 0; k < 10; ++k) h.v[k] = o[k];
+  } else {
+    fe_carry64(h, acc);
+  }
 }
 
 // h = f^(2^n), n >= 1.
