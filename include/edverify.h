@@ -175,6 +175,18 @@ int edv_sign_spans_device(edv_ctx *ctx, const void *d_sk64, const void *d_key_id
 int edv_sign_batch(edv_ctx *ctx, const uint8_t *sk64, const uint32_t *key_idx, const uint8_t *msgs,
                    const uint64_t *msg_off, uint64_t n, uint8_t *sig64_out);
 
+/* ---------------------------------------------------- request digests */
+
+/* Request.digest = sha256(serialize_msg_for_signing(signingState))
+ * (plenum/common/request.py:51-52), computed for every request at
+ * construction: SHA-256 of each message, 32 bytes per item.  For a request
+ * with no top-level keys besides identifier / reqId / operation /
+ * protocolVersion / signature its signing bytes ARE the signingState bytes,
+ * so the verify batch's message buffer serves both. */
+int edv_sha256_spans_device(edv_ctx *ctx, const void *d_msgs, const void *d_msg_start, const void *d_msg_end,
+                            uint64_t n, void *d_out32, void *stream);
+int edv_sha256_batch(edv_ctx *ctx, const uint8_t *msgs, const uint64_t *msg_off, uint64_t n, uint8_t *out32);
+
 /* ------------------------------------------------------ quorum vote tally */
 
 /* Votes are (key, voter, phase) triples with an accept flag; the tally keeps

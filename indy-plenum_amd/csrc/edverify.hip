@@ -28,6 +28,7 @@
 #include "../../include/edverify.h"
 #include "batch_encode.h"
 #include "comb.h"
+#include "sha256.h"
 #include "verify_core.h"
 
 using namespace edv;
@@ -589,6 +590,20 @@ __global__ __launch_bounds__(kBlock) void edv_sign_kernel(const uint8_t* __restr
     so[k] = rb[k];
     so[8 + k] = s[k];
   }
+}
+
+// Request digests (request.py:51-52): SHA-256 of each message span.
+__global__ __launch_bounds__(kBlock) void edv_sha256_kernel(const uint8_t* __restrict__ msgs,
+                                                           const uint64_t* __restrict__ ms,
+                                                           const uint64_t* __restrict__ me, uint64_t n,
+                                                           uint8_t* __restrict__ out32) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t d[8];
+  sha256_msg(d, msgs + ms[i], me[i] - ms[i]);
+  uint4* o = (uint4*)(out32 + 32 * i);
+  o[0] = make_uint4(d[0], d[1], d[2], d[3]);
+  o[1] = make_uint4(d[4], d[5], d[6], d[7]);
 }
 
 __global__ void edv_tally_scatter_kernel(const uint32_t* __restrict__ key, const uint8_t* __restrict__ voter,
@@ -1315,6 +1330,43 @@ int edv_sign_spans_device(edv_ctx* ctx, const void* d_sk64, const void* d_key_id
                      (const uint32_t*)d_key_idx, (const uint8_t*)d_msgs, (const uint64_t*)d_msg_start,
                      (const uint64_t*)d_msg_end, n, ctx->d_btab_comb, (uint8_t*)d_sig64_out);
   HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int edv_sha256_spans_device(edv_ctx* ctx, const void* d_msgs, const void* d_msg_start, const void* d_msg_end,
+                            uint64_t n, void* d_out32, void* stream) {
+  int r = set_device(ctx);
+  if (r) return r;
+  if (n == 0) return 0;
+  if (!d_msgs || !d_msg_start || !d_msg_end || !d_out32) return set_err(EDV_EINVAL, "null device pointer");
+  hipStream_t st = pick_stream(ctx, stream);
+  hipLaunchKernelGGL(edv_sha256_kernel, dim3((uint32_t)div_up(n, kBlock)), dim3(kBlock), 0, st,
+                     (const uint8_t*)d_msgs, (const uint64_t*)d_msg_start, (const uint64_t*)d_msg_end, n,
+                     (uint8_t*)d_out32);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int edv_sha256_batch(edv_ctx* ctx, const uint8_t* msgs, const uint64_t* msg_off, uint64_t n, uint8_t* out32) {
+  int r = set_device(ctx);
+  if (r) return r;
+  if (n == 0) return 0;
+  if (!msg_off || !out32) return set_err(EDV_EINVAL, "null pointer");
+  for (uint64_t i = 0; i < n; ++i)
+    if (msg_off[i + 1] < msg_off[i]) return set_err(EDV_EINVAL, "msg_off[%llu] decreasing", (unsigned long long)i);
+  const uint64_t m0 = msg_off[0], mbytes = msg_off[n] - m0;
+  if (mbytes && !msgs) return set_err(EDV_EINVAL, "null msgs");
+  if ((r = ensure(ctx->b_msg, mbytes + 16)) || (r = ensure(ctx->b_off, 8 * (n + 1))) || (r = ensure(ctx->b_sig, 32 * n)))
+    return r;
+  hipStream_t st = ctx->stream;
+  std::vector<uint64_t> off(n + 1);
+  for (uint64_t i = 0; i <= n; ++i) off[i] = msg_off[i] - m0;
+  if (mbytes) HIP_TRY(hipMemcpyAsync(ctx->b_msg.p, msgs + m0, mbytes, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(ctx->b_off.p, off.data(), 8 * (n + 1), hipMemcpyHostToDevice, st));
+  const uint64_t* d_off = (const uint64_t*)ctx->b_off.p;
+  if ((r = edv_sha256_spans_device(ctx, ctx->b_msg.p, d_off, d_off + 1, n, ctx->b_sig.p, st))) return r;
+  HIP_TRY(hipMemcpyAsync(out32, ctx->b_sig.p, 32 * n, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
   return 0;
 }
 

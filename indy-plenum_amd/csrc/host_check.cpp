@@ -8,6 +8,7 @@
 
 #include "batch_encode.h"
 #include "comb.h"
+#include "sha256.h"
 #include "verify_core.h"
 
 using namespace edv;
@@ -75,6 +76,12 @@ void edv_host_sha512_prefixed(uint8_t out[64], const uint8_t prefix64[64], const
   memcpy(pre, prefix64, 64);
   sha512_prefixed<16>(dig, pre, msg, mlen);
   memcpy(out, dig, 64);
+}
+
+void edv_host_sha256(uint8_t out[32], const uint8_t* msg, uint64_t mlen) {
+  uint32_t d[8];
+  sha256_msg(d, msg, mlen);
+  memcpy(out, d, 32);
 }
 
 void edv_host_sc_reduce(uint8_t out[32], const uint8_t in[64]) {

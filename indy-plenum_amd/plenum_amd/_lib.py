@@ -46,6 +46,8 @@ SIGNATURES = {
     "edv_sign_batch_device": (_I, [_P, _P, _P, _P, _P, _U64, _P, _P]),
     "edv_sign_spans_device": (_I, [_P, _P, _P, _P, _P, _P, _U64, _P, _P]),
     "edv_sign_batch": (_I, [_P, _P, _P, _P, _P, _U64, _P]),
+    "edv_sha256_spans_device": (_I, [_P, _P, _P, _P, _U64, _P, _P]),
+    "edv_sha256_batch": (_I, [_P, _P, _P, _U64, _P]),
     "edv_tally_device": (_I, [_P, _P, _P, _P, _P, _U64, _U32, _U32, _P, _P, _P, _P]),
     "edv_tally_finish_device": (_I, [_P, _P, _U32, _U32, _P, _P, _P]),
     "edv_tally": (_I, [_P, _P, _P, _P, _P, _U64, _U32, _U32, _P, _P]),

@@ -275,6 +275,25 @@ class EdVerifyEngine:
         check(self._lib.edv_sign_spans_device(self._ctx, _dev(d_sk64), _dev(d_key_idx), _dev(d_msgs),
                                               _dev(d_msg_start), _dev(d_msg_end), n, _dev(d_sig_out), st))
 
+    # -------------------------------------------------------------- digests
+    def sha256_batch(self, msgs, msg_off):
+        """SHA-256 of each message (host buffers): n x 32 uint8."""
+        msgs = _u8(msgs)
+        msg_off = np.ascontiguousarray(msg_off, dtype=np.uint64)
+        n = msg_off.shape[0] - 1
+        out = np.zeros((max(n, 0), 32), np.uint8)
+        if n > 0:
+            if int(msg_off[-1]) > msgs.shape[0]:
+                raise ValueError("msg_off exceeds message buffer")
+            check(self._lib.edv_sha256_batch(self._ctx, _ptr(msgs) if msgs.size else None, _ptr(msg_off), n,
+                                              _ptr(out)))
+        return out
+
+    def sha256_spans_device(self, d_msgs, d_msg_start, d_msg_end, n, d_out32, stream=None):
+        st = _stream_for(stream, d_out32)
+        check(self._lib.edv_sha256_spans_device(self._ctx, _dev(d_msgs), _dev(d_msg_start), _dev(d_msg_end), n,
+                                                _dev(d_out32), st))
+
     # ----------------------------------------------------------------- tally
     def tally(self, key, voter, phase, valid, n_keys, n_validators):
         """Distinct-voter PREPARE/COMMIT counts and quorum flags per key.

@@ -148,3 +148,16 @@ def test_comb_recoding_exact_up_to_L():
             d = list(out[:rows])
             assert all(-(1 << (w - 1)) <= v < (1 << (w - 1)) for v in d), (w, x)
             assert sum(v << (w * i) for i, v in enumerate(d)) == x, (w, hex(x))
+
+
+def test_kernel_sha256_any_alignment(hostcheck):
+    """csrc/sha256.h (request digests) vs hashlib, all block boundaries and 16 alignments."""
+    rng = random.Random(21)
+    lens = list(range(0, 200)) + [247, 248, 255, 256, 311, 312, 319, 320, 1000, 4095, 4096]
+    for t, n in enumerate(lens):
+        m = bytes(rng.getrandbits(8) for _ in range(n))
+        off = t % 16
+        buf = ctypes.create_string_buffer(b"\0" * off + m + b"\0" * 16)
+        out = ctypes.create_string_buffer(32)
+        hostcheck.edv_host_sha256(out, ctypes.byref(buf, off), ctypes.c_uint64(n))
+        assert out.raw == hashlib.sha256(m).digest(), n
