@@ -113,6 +113,10 @@ __device__ __forceinline__ void load_words(uint32_t* dst, const uint8_t* src, in
 // ---- split pipeline: hash -> table -> dsm (each kernel gets its own
 // register budget; intermediates are SoA in the context scratch).
 
+#ifndef EDV_HASH_MIN_WAVES
+#define EDV_HASH_MIN_WAVES 4  // 115 VGPRs since the branch-free schedule (sha512.h)
+#endif
+
 // Length buckets (edv_len_*_kernel): requests sorted by SHA-512 block count,
 // longest first, so the lanes of a wave hash messages of equal length.
 // perm[t] = the request lane t hashes; bucket_ctl[kLenBuckets] != 0 when the
@@ -190,7 +194,7 @@ __global__ __launch_bounds__(kBlock) void edv_len_scatter_kernel(const uint64_t*
   if (active) perm[slot] = (uint32_t)i;
 }
 
-__global__ __launch_bounds__(kBlock, 4) void edv_hash_kernel(const uint8_t* __restrict__ sig64,
+__global__ __launch_bounds__(kBlock, EDV_HASH_MIN_WAVES) void edv_hash_kernel(const uint8_t* __restrict__ sig64,
                                                          const uint8_t* __restrict__ pk32,
                                                          const uint8_t* __restrict__ msgs,
                                                          const uint64_t* __restrict__ ms,
@@ -420,9 +424,6 @@ __global__ void edv_base_rows_kernel(uint32_t* __restrict__ rows) {
   ge_frombytes(P, b, false);
   comb_rows<kBaseW>(rows, P);
 }
-#ifndef EDV_HASH_MIN_WAVES
-#define EDV_HASH_MIN_WAVES 4  // 115 VGPRs since the branch-free schedule (sha512.h)
-#endif
 __global__ __launch_bounds__(kBlock, EDV_HASH_MIN_WAVES) void edv_hash_keyed_kernel(const uint8_t* __restrict__ sig64,
                                                                const uint32_t* __restrict__ key_idx,
                                                                uint32_t key_count,

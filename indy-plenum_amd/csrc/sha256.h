@@ -84,10 +84,11 @@ EDV_HD void sha256_block_words(uint32_t w[16], uint64_t b, const Chunk16* c16, u
   const uint64_t q0 = pos >> 4;
   const uint32_t s4 = (uint32_t)(pos >> 2) & 3u, sh = d16 & 3u;
   uint32_t W[4 * NCH];
+  const int avail = chunks_left(nq, q0);
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     Chunk16 v = {0u, 0u, 0u, 0u};
-    if (q0 + c < nq) v = c16[q0 + c];
+    if (c < avail) v = c16[q0 + c];
     W[4 * c] = v.x;
     W[4 * c + 1] = v.y;
     W[4 * c + 2] = v.z;
@@ -104,14 +105,9 @@ EDV_HD void sha256_block_words(uint32_t w[16], uint64_t b, const Chunk16* c16, u
   for (int t = 0; t < 16; ++t) le[t] = funnel8(V[t + 1], V[t], sh);
   const int64_t u0 = 16 * (int64_t)b;
   if (4 * (u0 + 16) > (int64_t)mlen) {
+    const int32_t rb = bytes_left(mlen, u0);
 #pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      const int64_t rem = (int64_t)mlen - 4 * (u0 + t);
-      const uint32_t r = rem <= 0 ? 0u : rem >= 4 ? 4u : (uint32_t)rem;
-      const uint32_t keep = r >= 4 ? 0xffffffffu : ((1u << (8 * r)) - 1u);
-      const uint32_t pad = (rem >= 0 && rem < 4) ? (0x80u << (8 * (uint32_t)rem)) : 0u;
-      le[t] = (le[t] & keep) | pad;
-    }
+    for (int t = 0; t < 16; ++t) le[t] = tail_word(le[t], rb - 4 * t);
   }
 #pragma unroll
   for (int t = 0; t < 16; ++t) w[t] = bswap32(le[t]);

@@ -104,6 +104,27 @@ EDV_HD uint32_t funnel8(uint32_t hi, uint32_t lo, uint32_t sh) {
 struct Chunk16 {
   uint32_t x, y, z, w;
 };
+
+// Chunks of this block that hold message bytes: nq - q0 clamped to [0, 16]
+// (one 64-bit compare per block; the per-chunk guards are then 32-bit).
+EDV_HD int chunks_left(uint64_t nq, uint64_t q0) {
+  return nq <= q0 ? 0 : (nq - q0 >= 16 ? 16 : (int)(nq - q0));
+}
+
+// Message bytes left at a block's first word, clamped to [-1024, 1024] so the
+// per-word tail arithmetic is 32-bit.
+EDV_HD int32_t bytes_left(uint64_t mlen, int64_t word0) {
+  const int64_t r = (int64_t)mlen - 4 * word0;
+  return r < -1024 ? -1024 : r > 1024 ? 1024 : (int32_t)r;
+}
+
+// Word with `rem` message bytes left at it: keep min(rem, 4) bytes, put the
+// 0x80 pad byte at byte rem when 0 <= rem < 4.
+EDV_HD uint32_t tail_word(uint32_t v, int32_t rem) {
+  const uint32_t keep = rem >= 4 ? 0xffffffffu : rem <= 0 ? 0u : (0xffffffffu >> (32 - 8 * rem));
+  const uint32_t pad = (uint32_t)rem < 4u ? (0x80u << (8 * rem)) : 0u;
+  return (v & keep) | pad;
+}
 template <int NP, bool FIRST>
 EDV_HD void sha512_block_words(uint64_t w[16], uint64_t b, const uint32_t* prefix, const Chunk16* c16, uint64_t nq,
                                uint32_t d16, uint64_t mlen) {
@@ -115,10 +136,11 @@ EDV_HD void sha512_block_words(uint64_t w[16], uint64_t b, const uint32_t* prefi
   const uint64_t q0 = pos >> 4;
   const uint32_t s4 = (uint32_t)(pos >> 2) & 3u, sh = d16 & 3u;
   uint32_t W[4 * NCH];
+  const int avail = chunks_left(nq, q0);
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     Chunk16 v = {0u, 0u, 0u, 0u};
-    if (q0 + c < nq) v = c16[q0 + c];
+    if (c < avail) v = c16[q0 + c];
     W[4 * c] = v.x;
     W[4 * c + 1] = v.y;
     W[4 * c + 2] = v.z;
@@ -135,14 +157,9 @@ EDV_HD void sha512_block_words(uint64_t w[16], uint64_t b, const uint32_t* prefi
 #pragma unroll
   for (int t = 0; t < 32; ++t) le[t] = t < T0 ? prefix[t < NP ? t : 0] : funnel8(V[t - T0 + 1], V[t - T0], sh);
   if (4 * (u0 + 32) > (int64_t)mlen) {
+    const int32_t rb = bytes_left(mlen, u0);  // bytes left at stream word 0 of the block
 #pragma unroll
-    for (int t = T0; t < 32; ++t) {
-      const int64_t rem = (int64_t)mlen - 4 * (u0 + t);  // message bytes left at this word
-      const uint32_t r = rem <= 0 ? 0u : rem >= 4 ? 4u : (uint32_t)rem;
-      const uint32_t keep = r >= 4 ? 0xffffffffu : ((1u << (8 * r)) - 1u);
-      const uint32_t pad = (rem >= 0 && rem < 4) ? (0x80u << (8 * (uint32_t)rem)) : 0u;
-      le[t] = (le[t] & keep) | pad;
-    }
+    for (int t = T0; t < 32; ++t) le[t] = tail_word(le[t], rb - 4 * t);
   }
 #pragma unroll
   for (int j = 0; j < 16; ++j) w[j] = ((uint64_t)bswap32(le[2 * j]) << 32) | bswap32(le[2 * j + 1]);
