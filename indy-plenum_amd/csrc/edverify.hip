@@ -215,7 +215,10 @@ __global__ __launch_bounds__(kBlock, EDV_HASH_MIN_WAVES) void edv_hash_kernel(co
   flags[i] = ok ? 1 : 0;
 }
 
-__global__ __launch_bounds__(kBlock) void edv_table_kernel(const uint8_t* __restrict__ pk32, uint64_t n,
+#ifndef EDV_TABLE_MIN_WAVES
+#define EDV_TABLE_MIN_WAVES 2  // 168 VGPRs (+spill) beats 256+256 AGPRs at 1 wave: table -8%
+#endif
+__global__ __launch_bounds__(kBlock, EDV_TABLE_MIN_WAVES) void edv_table_kernel(const uint8_t* __restrict__ pk32, uint64_t n,
                                                           uint32_t* __restrict__ table, uint8_t* __restrict__ flags,
                                                           uint64_t stride) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
