@@ -34,6 +34,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "indy-plenum_amd"))
 
 from plenum_amd import EdVerifyEngine, pack_messages  # noqa: E402
+from plenum_amd.engine import lengths_mixed  # noqa: E402
 from plenum_amd import roofline as RL  # noqa: E402
 from plenum_amd import synth  # noqa: E402
 
@@ -62,8 +63,9 @@ def parse():
                     help="comb window of the key tables (edv_keys_set_window)")
     ap.add_argument("--pipeline", type=int, default=4, choices=[1, 2, 3, 4],
                     help="sub-batches per chunk (edv_set_pipeline; 1 = one launch per kernel, no overlap)")
-    ap.add_argument("--length-buckets", action="store_true",
-                    help="hash lanes in SHA-512 block-count order (edv_set_length_buckets on)")
+    ap.add_argument("--length-buckets", choices=["auto", "on", "off"], default="auto",
+                    help="hash lanes in SHA-512 block-count order (edv_set_length_buckets); auto = the "
+                         "library's rule for host offsets, applied to this batch's lengths")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (the product); gloo only to rehearse N > 1 on one GPU")
     ap.add_argument("--same-device", action="store_true", help="every rank on cuda:0 (with --dist-backend gloo)")
@@ -140,7 +142,6 @@ def main():
             dist.init_process_group(args.dist_backend)
     eng = EdVerifyEngine(local)
     eng.set_pipeline(args.pipeline)
-    eng.set_length_buckets(args.length_buckets)
     n = args.n if not (args.config == "c4" and args.n == 1_000_000) else 2_000_000
 
     # ---- synthetic signed batch (not timed)
@@ -175,6 +176,8 @@ def main():
         req_desc = ", %d requests x 1-5 signatures (mean %.2f), payload %d-%d B log-uniform" % (
             nreq, n / nreq, int(lens.min()), int(lens.max()))
     mlen_mean = float(np.mean(item_end - item_start))
+    buckets = args.length_buckets == "on" or (args.length_buckets == "auto" and lengths_mixed(item_start, item_end))
+    eng.set_length_buckets(1 if buckets else 0)
     d_kidx = torch.from_numpy(key_idx.astype(np.int32)).to(dev)
     d_msgs = torch.from_numpy(np.concatenate([buf, np.zeros(16, np.uint8)])).to(dev)
     d_ms = torch.from_numpy(item_start.astype(np.int64)).to(dev)
@@ -411,6 +414,7 @@ def main():
             "phase_ms": {"hash": float(ph[0]), "table": float(ph[1]),
                          ("comb" if args.path == "keyed" else "dsm"): dsm_sum, "encode": float(ph[3]),
                          "note": "per-phase sums over %d overlapped sub-batch launches" % launches},
+            "length_buckets": bool(buckets),
             "key_window": args.key_window, "key_table_build_ms": key_build_ms, "keys": int(reg_pks.shape[0]),
             "value_incl_key_build_one_step": (n * world / (ms_per_step * 1e-3 + key_build_ms * 1e-3)
                                               if args.path == "keyed" else None),

@@ -106,13 +106,18 @@ int edv_last_launch_count(edv_ctx *ctx);
 /* Sub-batches per chunk (1..4, default 4); 1 = no overlap (each kernel runs
  * alone on the GPU, e.g. to time one kernel in isolation). */
 int edv_set_pipeline(edv_ctx *ctx, int sub_batches);
-/* Hash lanes in SHA-512 block-count order (default off): a wave then hashes
- * messages of one length, but its lanes read scattered requests.  Measured
- * (profiles/r01d_*): configs[1] -6% (the reorder breaks the coalesced reads
- * of adjacent requests), configs[3] +-0% (per-lane message reads, not wave
- * divergence, bound the hash there).  A batch of one block count skips the
- * reordering. */
-int edv_set_length_buckets(edv_ctx *ctx, int on);
+/* Hash lanes in SHA-512 block-count order: without it every lane of a wave
+ * runs as many SHA-512 blocks as the longest message of its wave.  The order
+ * is a stable descending radix sort of the block counts (rocPRIM, one 6-bit
+ * pass, ~50 us per 1M requests), so a batch of one block count keeps the
+ * identity order.  mode 0 off, 1 on, 2 auto (default): calls with host
+ * offsets (edv_verify_batch, edv_verify_batch_keyed, edv_sign_open_batch)
+ * sort when unsorted waves would run > 1.25x the batch's blocks; device-
+ * pointer calls cannot see the lengths without a sync and treat auto as off.
+ * Measured (profiles/r01g_*): configs[3] (64 B - 4 KiB log-uniform) hash
+ * 4.72 -> 1.50 ms per 1M signatures, whole step 154M -> 297M/s; configs[1]
+ * (all 2 blocks) -8% if forced on (the sort's launches), hence auto. */
+int edv_set_length_buckets(edv_ctx *ctx, int mode);
 int edv_last_phase_ms(edv_ctx *ctx, double *hash_ms, double *table_ms, double *dsm_ms);
 double edv_last_kernel_ms(edv_ctx *ctx);
 

@@ -25,6 +25,9 @@
 #include <string>
 #include <vector>
 
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+
 #include "../../include/edverify.h"
 #include "batch_encode.h"
 #include "comb.h"
@@ -117,81 +120,29 @@ __device__ __forceinline__ void load_words(uint32_t* dst, const uint8_t* src, in
 #define EDV_HASH_MIN_WAVES 4  // 115 VGPRs since the branch-free schedule (sha512.h)
 #endif
 
-// Length buckets (edv_len_*_kernel): requests sorted by SHA-512 block count,
-// longest first, so the lanes of a wave hash messages of equal length.
-// perm[t] = the request lane t hashes; bucket_ctl[kLenBuckets] != 0 when the
-// batch spans more than one block count (else perm is not written and lane t
-// hashes request t).
-constexpr int kLenBuckets = 64;  // block counts 0..62; 63 = longer
-constexpr int kBucketCtlWords = 2 * kLenBuckets + 1;
-__device__ __forceinline__ uint64_t hash_lane_request(uint64_t t, const uint32_t* __restrict__ perm,
-                                                      const uint32_t* __restrict__ bucket_ctl) {
-  return (perm && bucket_ctl[kLenBuckets]) ? perm[t] : t;
+// Length buckets: the lanes of a wave should hash messages of equal SHA-512
+// block count, or every lane runs as many blocks as the longest message of
+// its wave (configs[3], 64 B - 4 KiB log-uniform: 3.2x the VALU work).
+// edv_len_key_kernel writes each request's block count (capped at 63) and a
+// stable descending radix sort over those 6 bits (rocPRIM onesweep, one
+// pass) yields perm: lane t hashes request perm[t], longest first.  Equal
+// block counts keep request order (stability), so a batch of one length gets
+// the identity permutation and keeps its coalesced loads.
+constexpr int kLenKeyBits = 6;  // block counts 0..62; 63 = longer
+__device__ __forceinline__ uint64_t hash_lane_request(uint64_t t, const uint32_t* __restrict__ perm) {
+  return perm ? perm[t] : t;
 }
 
 // Message i = msgs[ms[i] .. me[i]): me = msg_off + 1 for contiguous offsets,
 // separate arrays for spans (several signatures over one message).
-__device__ __forceinline__ uint32_t len_bucket(const uint64_t* __restrict__ ms, const uint64_t* __restrict__ me,
-                                               uint64_t i) {
+__global__ __launch_bounds__(kBlock) void edv_len_key_kernel(const uint64_t* __restrict__ ms,
+                                                            const uint64_t* __restrict__ me, uint64_t n,
+                                                            uint8_t* __restrict__ key) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
   const uint64_t blocks = (me[i] - ms[i] + 64 + 17 + 127) / 128;  // SHA-512 blocks of R||A||M
-  return blocks < (uint64_t)(kLenBuckets - 1) ? (uint32_t)blocks : (uint32_t)(kLenBuckets - 1);
-}
-
-// Wave-aggregated atomic add of 1 per lane to ctr[key]: one atomic per
-// distinct key in the wave; returns this lane's slot.
-__device__ __forceinline__ uint32_t wave_bucket_slot(uint32_t* ctr, uint32_t key, bool active) {
-  uint64_t todo = __ballot(active);
-  uint32_t slot = 0;
-  const uint32_t lane = threadIdx.x & 63;
-  while (todo) {
-    const int leader = __ffsll((unsigned long long)todo) - 1;
-    const uint32_t lkey = __shfl(key, leader);
-    const uint64_t same = __ballot(active && key == lkey) & todo;
-    uint32_t base = 0;
-    if (lane == (uint32_t)leader) base = atomicAdd(&ctr[lkey], (uint32_t)__popcll(same));
-    base = __shfl(base, leader);
-    if ((same >> lane) & 1ull) slot = base + (uint32_t)__popcll(same & ((1ull << lane) - 1ull));
-    todo &= ~same;
-  }
-  return slot;
-}
-
-// bucket_ctl layout: [0, 64) counts, [64] bucketed flag, [65, 129) cursors.
-__global__ __launch_bounds__(kBlock) void edv_len_hist_kernel(const uint64_t* __restrict__ ms,
-                                                             const uint64_t* __restrict__ me, uint64_t n,
-                                                             uint32_t* __restrict__ bucket_ctl) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool active = i < n;
-  const uint32_t b = active ? len_bucket(ms, me, i) : 0;
-  (void)wave_bucket_slot(bucket_ctl, b, active);
-}
-
-// One wave: cursors = exclusive prefix over buckets, longest first.
-__global__ void edv_len_scan_kernel(uint32_t* __restrict__ bucket_ctl) {
-  const uint32_t lane = threadIdx.x;  // 64 lanes = kLenBuckets
-  const uint32_t bucket = kLenBuckets - 1 - lane;
-  const uint32_t c = bucket_ctl[bucket];
-  uint32_t incl = c;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t v = __shfl_up(incl, d);
-    if (lane >= (uint32_t)d) incl += v;
-  }
-  bucket_ctl[kLenBuckets + 1 + bucket] = incl - c;
-  const uint64_t nonempty = __ballot(c != 0);
-  if (lane == 0) bucket_ctl[kLenBuckets] = __popcll(nonempty) > 1 ? 1u : 0u;
-}
-
-__global__ __launch_bounds__(kBlock) void edv_len_scatter_kernel(const uint64_t* __restrict__ ms,
-                                                                const uint64_t* __restrict__ me, uint64_t n,
-                                                                uint32_t* __restrict__ bucket_ctl,
-                                                                uint32_t* __restrict__ perm) {
-  if (!bucket_ctl[kLenBuckets]) return;  // one block count: lane t hashes request t
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool active = i < n;
-  const uint32_t b = active ? len_bucket(ms, me, i) : 0;
-  const uint32_t slot = wave_bucket_slot(bucket_ctl + kLenBuckets + 1, b, active);
-  if (active) perm[slot] = (uint32_t)i;
+  constexpr uint64_t cap = (1u << kLenKeyBits) - 1;
+  key[i] = (uint8_t)(blocks < cap ? blocks : cap);
 }
 
 __global__ __launch_bounds__(kBlock, EDV_HASH_MIN_WAVES) void edv_hash_kernel(const uint8_t* __restrict__ sig64,
@@ -200,11 +151,10 @@ __global__ __launch_bounds__(kBlock, EDV_HASH_MIN_WAVES) void edv_hash_kernel(co
                                                          const uint64_t* __restrict__ ms,
                                                          const uint64_t* __restrict__ me, uint64_t n,
                                                          uint32_t* __restrict__ h_soa, uint8_t* __restrict__ flags,
-                                                         uint64_t stride, const uint32_t* __restrict__ perm,
-                                                         const uint32_t* __restrict__ bucket_ctl) {
+                                                         uint64_t stride, const uint32_t* __restrict__ perm) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
-  const uint64_t i = hash_lane_request(t, perm, bucket_ctl);
+  const uint64_t i = hash_lane_request(t, perm);
   uint32_t sig[16], pk[8], h[8];
   load_words(sig, sig64 + 64 * i, 16);
   load_words(pk, pk32 + 32 * i, 8);
@@ -437,11 +387,10 @@ __global__ __launch_bounds__(kBlock, EDV_HASH_MIN_WAVES) void edv_hash_keyed_ker
                                                                const uint64_t* __restrict__ me, uint64_t n,
                                                                uint32_t* __restrict__ h_soa,
                                                                uint8_t* __restrict__ flags, uint64_t stride,
-                                                               const uint32_t* __restrict__ perm,
-                                                               const uint32_t* __restrict__ bucket_ctl) {
+                                                               const uint32_t* __restrict__ perm) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
-  const uint64_t i = hash_lane_request(t, perm, bucket_ctl);
+  const uint64_t i = hash_lane_request(t, perm);
   uint32_t sig[16], pk[8], h[8];
   load_words(sig, sig64 + 64 * i, 16);
   const uint32_t key = key_idx[i];
@@ -637,6 +586,26 @@ __global__ void edv_tally_count_kernel(const uint8_t* __restrict__ ballot, uint3
 
 uint64_t div_up(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 
+// Auto length buckets (edv_set_length_buckets mode 2) for calls whose offsets
+// are on the host: sort the hash lanes when unsorted waves would run more than
+// 1.25x the batch's SHA-512 blocks (each wave runs its longest message's
+// block count on all 64 lanes).  Uniform batches (configs[1]: 147-149 B, all
+// 2 blocks) skip the sort's launches.
+bool lengths_mixed(const uint64_t* off, uint64_t n) {
+  uint64_t sum = 0, padded = 0;
+  for (uint64_t g = 0; g < n; g += 64) {
+    const uint64_t e = g + 64 < n ? g + 64 : n;
+    uint64_t mx = 0;
+    for (uint64_t i = g; i < e; ++i) {
+      const uint64_t b = (off[i + 1] - off[i] + 64 + 17 + 127) / 128;
+      sum += b;
+      mx = b > mx ? b : mx;
+    }
+    padded += mx * (e - g);
+  }
+  return 4 * padded > 5 * sum;
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ context
@@ -651,8 +620,11 @@ struct edv_ctx {
   uint32_t* d_pt = nullptr;       // R' = (X:Y:Z), SoA [30][kMaxLanes]
   uint32_t* d_pre = nullptr;      // batch-encode prefix products, SoA [10][kMaxLanes]
   uint32_t* d_perm = nullptr;     // length-bucket order of the hash lanes [kMaxLanes]
-  uint32_t* d_bucket = nullptr;   // per sub-batch: counts | flag | cursors (kBucketCtlWords each)
-  bool bucketing = false;         // edv_set_length_buckets (off: the reorder breaks coalesced loads)
+  uint8_t* d_lenkey = nullptr;    // block-count keys, in | sorted [2][kMaxLanes]
+  void* d_sort_tmp = nullptr;     // radix-sort temporary storage, one slot per sub-batch
+  size_t sort_tmp_bytes = 0;      // per slot (sized for kMaxLanes)
+  int bucket_mode = 2;            // edv_set_length_buckets: 0 off, 1 on, 2 auto
+  bool bucket_now = false;        // this launch sorts its hash lanes
   uint64_t scratch_lanes = 0;
   // Pipelined launches: each chunk of up to kMaxLanes requests is cut into
   // kSub sub-batches whose kernels alternate between `stream` (or the
@@ -742,23 +714,22 @@ int launch_sub(edv_ctx* ctx, bool keyed, const SubBatch& b, const uint8_t* msgs,
   uint8_t* fl = ctx->d_flags + b.soff;
   uint32_t* pt = ctx->d_pt + b.soff;
   uint32_t* perm = nullptr;
-  uint32_t* bctl = ctx->d_bucket + (uint64_t)sub * kBucketCtlWords;
   HIP_TRY(hipEventRecord(ev[0], q));
-  if (ctx->bucketing && b.cn > 64) {
-    // hash lanes in SHA-512 block-count order (longest first)
+  if (ctx->bucket_now && b.cn > 64) {
+    // hash lanes in SHA-512 block-count order, longest first (stable)
     perm = ctx->d_perm + b.soff;
-    HIP_TRY(hipMemsetAsync(bctl, 0, kBucketCtlWords * 4, q));
-    hipLaunchKernelGGL(edv_len_hist_kernel, dim3(grid), dim3(kBlock), 0, q, b.ms, b.me, b.cn, bctl);
+    uint8_t* key = ctx->d_lenkey + b.soff;
+    hipLaunchKernelGGL(edv_len_key_kernel, dim3(grid), dim3(kBlock), 0, q, b.ms, b.me, b.cn, key);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(edv_len_scan_kernel, dim3(1), dim3(64), 0, q, bctl);
-    HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(edv_len_scatter_kernel, dim3(grid), dim3(kBlock), 0, q, b.ms, b.me, b.cn, bctl, perm);
-    HIP_TRY(hipGetLastError());
+    size_t tmp = ctx->sort_tmp_bytes;
+    HIP_TRY(rocprim::radix_sort_pairs_desc((char*)ctx->d_sort_tmp + (size_t)sub * tmp, tmp, key, key + kMaxLanes,
+                                           rocprim::counting_iterator<uint32_t>(0), perm, (uint32_t)b.cn, 0,
+                                           kLenKeyBits, q));
   }
   if (keyed) {
     const uint32_t kc = (uint32_t)ctx->key_count;
     hipLaunchKernelGGL(edv_hash_keyed_kernel, dim3(grid), dim3(kBlock), 0, q, b.sig, b.kidx, kc, ctx->d_key_pk,
-                       ctx->d_key_valid, msgs, b.ms, b.me, b.cn, hs, fl, chunk, perm, bctl);
+                       ctx->d_key_valid, msgs, b.ms, b.me, b.cn, hs, fl, chunk, perm);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ev[1], q));
     HIP_TRY(hipEventRecord(ev[2], q));
@@ -780,7 +751,7 @@ int launch_sub(edv_ctx* ctx, bool keyed, const SubBatch& b, const uint8_t* msgs,
     // offsets are multiples of the block size, so each sub-batch has its own
     uint32_t* tab = (uint32_t*)((char*)ctx->d_scratch + (b.soff / kBlock) * (uint64_t)kRegionBytes);
     hipLaunchKernelGGL(edv_hash_kernel, dim3(grid), dim3(kBlock), 0, q, b.sig, b.pk, msgs, b.ms, b.me, b.cn, hs, fl,
-                       chunk, perm, bctl);
+                       chunk, perm);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ev[1], q));
     hipLaunchKernelGGL(edv_table_kernel, dim3(grid), dim3(kBlock), 0, q, b.pk, b.cn, tab, fl, chunk);
@@ -814,7 +785,10 @@ int launch_pipeline(edv_ctx* ctx, bool keyed, const void* d_sig, const void* d_k
     const uint64_t cn = (n - c0) < chunk ? (n - c0) : chunk;
     // sub-batches of the chunk; the next chunk reuses the scratch, so it
     // starts only after both streams are done with this one
-    const uint64_t per = div_up(div_up(cn, (uint64_t)ctx->max_sub), kSubAlign) * kSubAlign;
+    // (sorted hash lanes: at most 2 -- measured on configs[3], 3 or 4
+    // sub-batches are 10% slower than 1 or 2)
+    const uint64_t nsub = ctx->bucket_now && ctx->max_sub > 2 ? 2 : (uint64_t)ctx->max_sub;
+    const uint64_t per = div_up(div_up(cn, nsub), kSubAlign) * kSubAlign;
     int ns = 0;
     for (uint64_t s0 = 0; s0 < cn; s0 += per, ++ns) {
       SubBatch b;
@@ -1003,6 +977,7 @@ int edv_verify_batch_keyed_device(edv_ctx* ctx, const void* d_sig64, const void*
   if (r) return r;
   if (n && (!d_sig64 || !d_key_idx || !d_msgs || !d_msg_off || !d_accept_words))
     return set_err(EDV_EINVAL, "null device pointer");
+  ctx->bucket_now = ctx->bucket_mode == 1;
   return launch_verify_keyed(ctx, d_sig64, d_key_idx, d_msgs, d_msg_off, n, d_accept_words, pick_stream(ctx, stream));
 }
 
@@ -1014,6 +989,7 @@ int edv_verify_spans_device(edv_ctx* ctx, const void* d_sig64, const void* d_key
   if (n && (!d_sig64 || !d_keys || !d_msgs || !d_msg_start || !d_msg_end || !d_accept_words))
     return set_err(EDV_EINVAL, "null device pointer");
   if (n && keyed && ctx->key_count == 0) return set_err(EDV_EINVAL, "no registered keys");
+  ctx->bucket_now = ctx->bucket_mode == 1;
   return launch_pipeline(ctx, keyed != 0, d_sig64, d_keys, d_msgs, (const uint64_t*)d_msg_start,
                          (const uint64_t*)d_msg_end, n, d_accept_words, pick_stream(ctx, stream));
 }
@@ -1035,6 +1011,7 @@ int edv_verify_batch_keyed(edv_ctx* ctx, const uint8_t* sig64, const uint32_t* k
   hipStream_t st = ctx->stream;
   std::vector<uint64_t> off(n + 1);
   for (uint64_t i = 0; i <= n; ++i) off[i] = msg_off[i] - m0;
+  ctx->bucket_now = ctx->bucket_mode == 1 || (ctx->bucket_mode == 2 && lengths_mixed(off.data(), n));
   HIP_TRY(hipMemcpyAsync(ctx->b_sig.p, sig64, 64 * n, hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemcpyAsync(ctx->b_pk.p, key_idx, 4 * n, hipMemcpyHostToDevice, st));
   if (mbytes) HIP_TRY(hipMemcpyAsync(ctx->b_msg.p, msgs + m0, mbytes, hipMemcpyHostToDevice, st));
@@ -1127,8 +1104,14 @@ edv_ctx* edv_create(int device) {
     return fail("hipMalloc(pre)", e);
   if ((e = hipMalloc(&ctx->d_perm, ctx->scratch_lanes * sizeof(uint32_t))) != hipSuccess)
     return fail("hipMalloc(perm)", e);
-  if ((e = hipMalloc(&ctx->d_bucket, edv_ctx::kSub * kBucketCtlWords * sizeof(uint32_t))) != hipSuccess)
-    return fail("hipMalloc(bucket)", e);
+  if ((e = hipMalloc(&ctx->d_lenkey, 2 * ctx->scratch_lanes)) != hipSuccess) return fail("hipMalloc(lenkey)", e);
+  if ((e = rocprim::radix_sort_pairs_desc(nullptr, ctx->sort_tmp_bytes, ctx->d_lenkey, ctx->d_lenkey + kMaxLanes,
+                                          rocprim::counting_iterator<uint32_t>(0), ctx->d_perm,
+                                          (uint32_t)ctx->scratch_lanes, 0, kLenKeyBits, ctx->stream)) != hipSuccess)
+    return fail("radix sort size", e);
+  ctx->sort_tmp_bytes = (ctx->sort_tmp_bytes + 255) & ~(size_t)255;
+  if ((e = hipMalloc(&ctx->d_sort_tmp, edv_ctx::kSub * ctx->sort_tmp_bytes)) != hipSuccess)
+    return fail("hipMalloc(sort)", e);
   if (const char* w = getenv("EDV_KEY_WINDOW")) {
     const int kw = atoi(w);
     if (kw == 4 || kw == 6 || kw == 8 || kw == 10) ctx->key_w = kw;
@@ -1147,7 +1130,8 @@ void edv_destroy(edv_ctx* ctx) {
   if (ctx->d_flags) (void)hipFree(ctx->d_flags);
   if (ctx->d_pt) (void)hipFree(ctx->d_pt);
   if (ctx->d_perm) (void)hipFree(ctx->d_perm);
-  if (ctx->d_bucket) (void)hipFree(ctx->d_bucket);
+  if (ctx->d_lenkey) (void)hipFree(ctx->d_lenkey);
+  if (ctx->d_sort_tmp) (void)hipFree(ctx->d_sort_tmp);
   if (ctx->d_ident) (void)hipFree(ctx->d_ident);
   if (ctx->d_pre) (void)hipFree(ctx->d_pre);
   if (ctx->d_btab_comb) (void)hipFree(ctx->d_btab_comb);
@@ -1179,6 +1163,7 @@ int edv_verify_batch_device(edv_ctx* ctx, const void* d_sig64, const void* d_pk3
   if (r) return r;
   if (n && (!d_sig64 || !d_pk32 || !d_msgs || !d_msg_off || !d_accept_words))
     return set_err(EDV_EINVAL, "null device pointer");
+  ctx->bucket_now = ctx->bucket_mode == 1;
   return launch_verify(ctx, d_sig64, d_pk32, d_msgs, d_msg_off, n, d_accept_words, pick_stream(ctx, stream));
 }
 
@@ -1199,9 +1184,10 @@ int edv_last_phases_ms(edv_ctx* ctx, double* out4) {
 
 int edv_last_launch_count(edv_ctx* ctx) { return ctx ? ctx->last_nsub : 0; }
 
-int edv_set_length_buckets(edv_ctx* ctx, int on) {
+int edv_set_length_buckets(edv_ctx* ctx, int mode) {
   if (!ctx) return set_err(EDV_EINVAL, "null context");
-  ctx->bucketing = on != 0;
+  if (mode < 0 || mode > 2) return set_err(EDV_EINVAL, "length-bucket mode %d (0 off, 1 on, 2 auto)", mode);
+  ctx->bucket_mode = mode;
   return 0;
 }
 
@@ -1249,6 +1235,7 @@ int edv_verify_batch(edv_ctx* ctx, const uint8_t* sig64, const uint8_t* pk32, co
   // offsets rebased to 0 for the staged copy
   std::vector<uint64_t> off(n + 1);
   for (uint64_t i = 0; i <= n; ++i) off[i] = msg_off[i] - m0;
+  ctx->bucket_now = ctx->bucket_mode == 1 || (ctx->bucket_mode == 2 && lengths_mixed(off.data(), n));
   HIP_TRY(hipMemcpyAsync(ctx->b_sig.p, sig64, 64 * n, hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemcpyAsync(ctx->b_pk.p, pk32, 32 * n, hipMemcpyHostToDevice, st));
   if (mbytes) HIP_TRY(hipMemcpyAsync(ctx->b_msg.p, msgs + m0, mbytes, hipMemcpyHostToDevice, st));

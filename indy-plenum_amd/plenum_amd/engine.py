@@ -64,6 +64,21 @@ def _u8(x, width=None):
     return a.reshape(-1, width) if width else a.reshape(-1)
 
 
+def lengths_mixed(msg_start, msg_end):
+    """The auto length-bucket rule of edverify.c (lengths_mixed) for callers of
+    the device-pointer entry points that hold the lengths on the host: True
+    when unsorted 64-lane waves would run > 1.25x the batch's SHA-512 blocks."""
+    blocks = (np.asarray(msg_end, np.int64) - np.asarray(msg_start, np.int64) + 64 + 17 + 127) // 128
+    n = blocks.size
+    if n == 0:
+        return False
+    pad = (-n) % 64
+    w = np.concatenate([blocks, np.zeros(pad, np.int64)]).reshape(-1, 64)
+    cnt = np.full(w.shape[0], 64, np.int64)
+    cnt[-1] = 64 - pad
+    return 4 * int((w.max(axis=1) * cnt).sum()) > 5 * int(blocks.sum())
+
+
 def unpack_bits(bits, n):
     return np.unpackbits(np.asarray(bits, dtype=np.uint8), bitorder="little")[:n].astype(bool)
 
@@ -174,9 +189,11 @@ class EdVerifyEngine:
         """Sub-batches per chunk (1..4; 1 = kernels run one at a time)."""
         check(self._lib.edv_set_pipeline(self._ctx, int(sub_batches)))
 
-    def set_length_buckets(self, on):
-        """Hash lanes sorted by SHA-512 block count (default off; edverify.h)."""
-        check(self._lib.edv_set_length_buckets(self._ctx, 1 if on else 0))
+    def set_length_buckets(self, mode):
+        """Hash lanes sorted by SHA-512 block count: False/0 off, True/1 on,
+        "auto"/2 (the default; host-offset calls decide per batch, edverify.h)."""
+        m = {"auto": 2, "on": 1, "off": 0}.get(mode, mode)
+        check(self._lib.edv_set_length_buckets(self._ctx, int(m)))
 
     # ------------------------------------------------------------ key tables
     def keys_set_window(self, w):

@@ -9,6 +9,7 @@ import pytest
 
 from conftest import items_of, load_npz
 from plenum_amd import pack_messages
+from plenum_amd.engine import lengths_mixed
 
 pytestmark = pytest.mark.gpu
 L = 2**252 + 27742317777372353535851937790883648493
@@ -170,14 +171,21 @@ def test_sub_batch_boundaries(gpu_engine, oracle, n):
     bits as one un-pipelined launch, and both match the oracle (sampled)."""
     sig, pks, msgs, buf, off = _random_batch(gpu_engine, n, 100 + n, mlen_max=120)
     gpu_engine.set_pipeline(4)
+    gpu_engine.set_length_buckets(False)
     got4 = gpu_engine.verify_batch(sig, pks, buf, off)
     per = -(-(-(-n // 4)) // 1024) * 1024  # ceil(ceil(n / 4) / 1024) * 1024
     assert gpu_engine.last_launch_count() == -(-n // per)
+    gpu_engine.set_length_buckets(True)  # sorted hash lanes: at most 2 sub-batches
+    got2 = gpu_engine.verify_batch(sig, pks, buf, off)
+    per = -(-(-(-n // 2)) // 1024) * 1024
+    assert gpu_engine.last_launch_count() == -(-n // per)
+    gpu_engine.set_length_buckets("auto")
     gpu_engine.set_pipeline(1)
     got1 = gpu_engine.verify_batch(sig, pks, buf, off)
     assert gpu_engine.last_launch_count() == 1
     gpu_engine.set_pipeline(4)
     assert (got4 == got1).all(), np.nonzero(got4 != got1)
+    assert (got2 == got1).all(), np.nonzero(got2 != got1)
     for i in list(range(0, n, 97)) + [n - 1]:
         want = oracle.oracle_verify_detached(sig[i].tobytes(), msgs[i], len(msgs[i]), pks[i].tobytes()) == 0
         assert got4[i] == want, i
@@ -203,12 +211,21 @@ def test_length_buckets_mixed_lengths(gpu_engine, oracle):
     sig = gpu_engine.sign_batch(sk, kidx, buf, off)
     sig[::5, 33] ^= 4
     pks = pk[kidx]
+    assert lengths_mixed(off[:-1], off[1:])
     gpu_engine.set_length_buckets(True)
     got = gpu_engine.verify_batch(sig, pks, buf, off)
     gpu_engine.set_length_buckets(False)
     plain = gpu_engine.verify_batch(sig, pks, buf, off)
-    gpu_engine.set_length_buckets(True)
+    gpu_engine.set_length_buckets("auto")
+    auto = gpu_engine.verify_batch(sig, pks, buf, off)
     assert (got == plain).all(), np.nonzero(got != plain)
+    assert (auto == plain).all(), np.nonzero(auto != plain)
+    gpu_engine.keys_reset()
+    gpu_engine.keys_add(pk)
+    gpu_engine.set_length_buckets(True)
+    keyed = gpu_engine.verify_batch_keyed(sig, kidx, buf, off)
+    gpu_engine.set_length_buckets("auto")
+    assert (keyed == plain).all(), np.nonzero(keyed != plain)
     want = np.ones(n, bool)
     want[::5] = False
     assert (got == want).all(), np.nonzero(got != want)
@@ -259,3 +276,11 @@ def test_spans_share_messages(gpu_engine):
     torch.cuda.synchronize()
     got = np.unpackbits(words.cpu().numpy().view(np.uint8), bitorder="little")[:n].astype(bool)
     assert (got == want).all()
+    for keyed, keys in ((True, d_k), (False, d_pk)):  # sorted hash lanes over spans
+        gpu_engine.set_length_buckets(True)
+        words.zero_()
+        gpu_engine.verify_spans_device(d_sig, keys, keyed, d_msgs, d_ms, d_me, n, words)
+        torch.cuda.synchronize()
+        gpu_engine.set_length_buckets("auto")
+        got = np.unpackbits(words.cpu().numpy().view(np.uint8), bitorder="little")[:n].astype(bool)
+        assert (got == want).all(), keyed

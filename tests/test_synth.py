@@ -29,3 +29,26 @@ def test_add_torsion_changes_R():
     R = E.encode(E.mul(12345, E.B))
     Rt = synth.add_torsion(R)
     assert Rt != R and E.mul(8, E.decode(Rt)) == E.mul(8, E.decode(R))
+
+
+def test_lengths_mixed_rule():
+    """The auto length-bucket rule (edverify.hip lengths_mixed, mirrored by
+    engine.lengths_mixed): configs[1] NYM payloads (one SHA-512 block count)
+    stay unsorted; configs[3]'s log-uniform 64 B - 4 KiB payloads sort."""
+    import numpy as np
+    from plenum_amd.engine import lengths_mixed
+    msgs, _, _ = synth.nym_messages(4096, [bytes(range(32))] * 4)
+    lens = np.array([len(m) for m in msgs])
+    off = np.concatenate([[0], np.cumsum(lens)])
+    assert not lengths_mixed(off[:-1], off[1:])
+    rng = np.random.default_rng(3)
+    lens = np.exp(rng.uniform(np.log(64), np.log(4096), 4096)).astype(np.int64)
+    off = np.concatenate([[0], np.cumsum(lens)])
+    assert lengths_mixed(off[:-1], off[1:])
+    assert not lengths_mixed([], [])
+    # exactly the 1.25x threshold: one 3-block message per wave of 2-block ones
+    blk2, blk3 = 100, 300  # (len + 81 + 127) // 128 = 2 / 3 blocks
+    lens = np.full(64, blk2)
+    lens[0] = blk3
+    off = np.concatenate([[0], np.cumsum(lens)])
+    assert lengths_mixed(off[:-1], off[1:])  # 64*3 = 192 > 1.25 * 129
