@@ -214,15 +214,17 @@ __device__ __forceinline__ void load_niels(ge_niels& nb, const uint32_t* __restr
 // A comb table in global memory (comb.h layout: row-major, 32-word entries).
 template <int W>
 struct DevComb {
-  const uint32_t* __restrict__ tab;
+  const uint32_t* __restrict__ tab;    // entry 0 of row 0
   const uint32_t* __restrict__ ident;  // kEntryWords-word identity entry (global memory)
-  __device__ void load(int row, int j, ge_niels& nb) const {
-    const uint32_t* p = j >= 0 ? tab + ((uint32_t)row * Window<W>::kEntries + (uint32_t)j) * kEntryWords : ident;
-    load_niels(nb, p);
+  // words from row r to row r + 1: one table's row for the base table; for
+  // the key store (row-major over keys) key_cap tables' rows
+  uint64_t row_words = (uint64_t)Window<W>::kEntries * kEntryWords;
+  __device__ const uint32_t* entry(int row, int j) const {
+    return j >= 0 ? tab + (uint64_t)(uint32_t)row * row_words + (uint32_t)j * kEntryWords : ident;
   }
+  __device__ void load(int row, int j, ge_niels& nb) const { load_niels(nb, entry(row, j)); }
   __device__ uint32_t touch(int row, int j) const {  // comb_mul_add's line prefetch
-    const uint32_t* p = j >= 0 ? tab + ((uint32_t)row * Window<W>::kEntries + (uint32_t)j) * kEntryWords : ident;
-    return *(const volatile uint32_t*)p;
+    return *(const volatile uint32_t*)entry(row, j);
   }
 };
 
@@ -322,7 +324,7 @@ __global__ __launch_bounds__(kBlock) void edv_encode_kernel(const uint8_t* __res
 }
 
 // ---- key-table path (comb.h) ---------------------------------------------
-// Registered keys: comb tables of -A at the context's key window (4, 6, 8 or 10).
+// Registered keys: comb tables of -A at the context's key window (EDV_KEY_WINDOWS).
 // Base point: W = 8 comb table (512 KiB) built once per context by the same
 // kernels.
 #ifndef EDV_COMB_MIN_WAVES
@@ -354,16 +356,22 @@ struct FillShape {
   static constexpr int CH = E < 32 ? E : 32;
   static constexpr int NCH = E / CH;
 };
+// Row r of the launch is row r % kRows of table key0 + r / kRows; the store is
+// row-major over tables: row `row` of table k at (row * cap + k) * kEntries
+// entries (the base table: key0 = 0, cap = 1).
 template <int W>
 __global__ __launch_bounds__(kBlock) void edv_comb_fill_kernel(const uint32_t* __restrict__ rows, uint64_t nrows,
-                                                              uint32_t* __restrict__ tab, uint32_t* __restrict__ pre) {
+                                                              uint32_t* __restrict__ tab, uint32_t* __restrict__ pre,
+                                                              uint64_t key0, uint64_t cap) {
   using F = FillShape<W>;
   const uint64_t nl = nrows * F::NCH;
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= nl) return;
   const uint64_t r = g / F::NCH;
   const int c = (int)(g % F::NCH);
-  comb_fill_strided(tab + r * F::E * kEntryWords, pre + g * 10, nl * 10, rows + r * kRowWords, c, F::NCH, F::CH);
+  const uint64_t row = r % Window<W>::kRows, k = key0 + r / Window<W>::kRows;
+  comb_fill_strided(tab + (row * cap + k) * F::E * kEntryWords, pre + g * 10, nl * 10, rows + r * kRowWords, c,
+                    F::NCH, F::CH);
 }
 
 // Base-point table: one lane decodes B and writes its 32 row bases ...
@@ -409,7 +417,7 @@ template <int W>
 __global__ __launch_bounds__(kBlock, EDV_COMB_MIN_WAVES) void edv_comb_kernel(const uint8_t* __restrict__ sig64,
                                                          const uint32_t* __restrict__ key_idx, uint32_t key_count,
                                                          uint64_t n, const uint32_t* __restrict__ h_soa,
-                                                         const uint32_t* __restrict__ key_tab,
+                                                         const uint32_t* __restrict__ key_tab, uint64_t key_cap,
                                                          const uint32_t* __restrict__ btab,
                                                          const uint32_t* __restrict__ ident,
                                                          uint32_t* __restrict__ pt, uint64_t stride) {
@@ -421,7 +429,8 @@ __global__ __launch_bounds__(kBlock, EDV_COMB_MIN_WAVES) void edv_comb_kernel(co
   for (int k = 0; k < 8; ++k) h[k] = h_soa[k * stride + i];
   const uint32_t key0 = key_idx[i];
   const uint32_t key = key0 < key_count ? key0 : 0;  // flags[i] is 0 for an out-of-range id
-  const DevComb<W> ta{key_tab + (uint64_t)key * Window<W>::kTableWords, ident};
+  constexpr uint64_t kRowWordsW = (uint64_t)Window<W>::kEntries * kEntryWords;
+  const DevComb<W> ta{key_tab + (uint64_t)key * kRowWordsW, ident, key_cap * kRowWordsW};  // row-major store
   const DevComb<kBaseW> tb{btab, ident};
   ge_p3 Q;
   ge_p3_0(Q);
@@ -647,7 +656,7 @@ struct edv_ctx {
   uint8_t* d_key_valid = nullptr;
   uint32_t* d_key_tab = nullptr;
   uint64_t key_count = 0, key_cap = 0;
-  int key_w = 10;                     // comb window of the key tables (4, 6, 8 or 10)
+  int key_w = 10;                     // comb window of the key tables (EDV_KEY_WINDOWS)
   // staging buffers for host-pointer calls
   struct Buf {
     void* p = nullptr;
@@ -678,11 +687,27 @@ int set_device(edv_ctx* ctx) {
 
 hipStream_t pick_stream(edv_ctx* ctx, void* stream) { return stream ? (hipStream_t)stream : ctx->stream; }
 
+// Key windows a context accepts (edv_keys_set_window); every one instantiates
+// its own comb / fill kernels.
+#define EDV_KEY_WINDOWS(X) X(4) X(6) X(8) X(10) X(12) X(13) X(14) X(16)
+bool key_window_ok(int w) {
+#define EDV_KW_OK(W) || w == W
+  return false EDV_KEY_WINDOWS(EDV_KW_OK);
+#undef EDV_KW_OK
+}
+uint32_t key_rows(int w) {
+#define EDV_KW_ROWS(W) \
+  if (w == W) return Window<W>::kRows;
+  EDV_KEY_WINDOWS(EDV_KW_ROWS)
+#undef EDV_KW_ROWS
+  return Window<8>::kRows;
+}
 uint32_t key_tab_words(int w) {
-  return w == 4 ? Window<4>::kTableWords
-       : w == 6 ? Window<6>::kTableWords
-       : w == 10 ? Window<10>::kTableWords
-                 : Window<8>::kTableWords;
+#define EDV_KW_WORDS(W) \
+  if (w == W) return Window<W>::kTableWords;
+  EDV_KEY_WINDOWS(EDV_KW_WORDS)
+#undef EDV_KW_WORDS
+  return Window<8>::kTableWords;
 }
 
 int launch_encode(edv_ctx* ctx, const uint8_t* sig, uint64_t cn, unsigned long long* words, uint64_t off,
@@ -735,15 +760,17 @@ int launch_sub(edv_ctx* ctx, bool keyed, const SubBatch& b, const uint8_t* msgs,
     HIP_TRY(hipEventRecord(ev[2], q));
 #define EDV_COMB_LAUNCH(W)                                                                                   \
   hipLaunchKernelGGL(edv_comb_kernel<W>, dim3(grid), dim3(kBlock), 0, q, b.sig, b.kidx, kc, b.cn, hs,        \
-                     ctx->d_key_tab, ctx->d_btab_comb32, ctx->d_ident, pt, chunk)
-    if (ctx->key_w == 4)
-      EDV_COMB_LAUNCH(4);
-    else if (ctx->key_w == 6)
-      EDV_COMB_LAUNCH(6);
-    else if (ctx->key_w == 10)
-      EDV_COMB_LAUNCH(10);
-    else
-      EDV_COMB_LAUNCH(8);
+                     ctx->d_key_tab, ctx->key_cap, ctx->d_btab_comb32, ctx->d_ident, pt, chunk)
+#define EDV_COMB_CASE(W) \
+  case W:                \
+    EDV_COMB_LAUNCH(W);  \
+    break;
+    switch (ctx->key_w) {
+      EDV_KEY_WINDOWS(EDV_COMB_CASE)
+      default:
+        return set_err(EDV_EINVAL, "key window %d", ctx->key_w);
+    }
+#undef EDV_COMB_CASE
 #undef EDV_COMB_LAUNCH
     HIP_TRY(hipGetLastError());
   } else {
@@ -832,7 +859,7 @@ int launch_verify(edv_ctx* ctx, const void* d_sig, const void* d_pk, const void*
 
 static int keys_reserve(edv_ctx* ctx, uint64_t need) {
   if (need <= ctx->key_cap) return 0;
-  uint64_t cap = ctx->key_cap ? ctx->key_cap : 1024;
+  uint64_t cap = ctx->key_cap ? ctx->key_cap : 64;  // W = 16: 64 MiB per key
   while (cap < need) cap *= 2;
   uint8_t *pk = nullptr, *valid = nullptr;
   uint32_t* tab = nullptr;
@@ -847,8 +874,11 @@ static int keys_reserve(edv_ctx* ctx, uint64_t need) {
   if (ctx->key_count) {
     HIP_TRY(hipMemcpyAsync(pk, ctx->d_key_pk, ctx->key_count * 32, hipMemcpyDeviceToDevice, ctx->stream));
     HIP_TRY(hipMemcpyAsync(valid, ctx->d_key_valid, ctx->key_count, hipMemcpyDeviceToDevice, ctx->stream));
-    HIP_TRY(hipMemcpyAsync(tab, ctx->d_key_tab, ctx->key_count * (uint64_t)key_tab_words(ctx->key_w) * 4,
-                           hipMemcpyDeviceToDevice, ctx->stream));
+    // row-major over keys: row r of every table is one slab of key_cap tables
+    const uint64_t rows = key_rows(ctx->key_w), row_bytes = key_tab_words(ctx->key_w) / rows * 4;
+    for (uint64_t r = 0; r < rows; ++r)
+      HIP_TRY(hipMemcpyAsync((char*)tab + r * cap * row_bytes, (const char*)ctx->d_key_tab + r * ctx->key_cap * row_bytes,
+                             ctx->key_count * row_bytes, hipMemcpyDeviceToDevice, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
   }
   if (ctx->d_key_pk) (void)hipFree(ctx->d_key_pk);
@@ -882,7 +912,7 @@ static int keys_build_w(edv_ctx* ctx, uint64_t first, uint64_t nkeys, hipStream_
                        ctx->d_key_pk + 32 * k, kn, rows, ctx->d_key_valid + k);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(edv_comb_fill_kernel<W>, dim3((uint32_t)div_up(kn * R * FillShape<W>::NCH, kBlock)),
-                       dim3(kBlock), 0, st, rows, kn * R, ctx->d_key_tab + k * (uint64_t)Window<W>::kTableWords, pre);
+                       dim3(kBlock), 0, st, rows, kn * R, ctx->d_key_tab, pre, k, ctx->key_cap);
     HIP_TRY(hipGetLastError());
   }
   return 0;
@@ -890,12 +920,15 @@ static int keys_build_w(edv_ctx* ctx, uint64_t first, uint64_t nkeys, hipStream_
 
 static int keys_build(edv_ctx* ctx, uint64_t first, uint64_t nkeys, hipStream_t st) {
   if (!nkeys) return 0;
+#define EDV_BUILD_CASE(W) \
+  case W:                 \
+    return keys_build_w<W>(ctx, first, nkeys, st);
   switch (ctx->key_w) {
-    case 4: return keys_build_w<4>(ctx, first, nkeys, st);
-    case 6: return keys_build_w<6>(ctx, first, nkeys, st);
-    case 10: return keys_build_w<10>(ctx, first, nkeys, st);
-    default: return keys_build_w<8>(ctx, first, nkeys, st);
+    EDV_KEY_WINDOWS(EDV_BUILD_CASE)
+    default:
+      return set_err(EDV_EINVAL, "key window %d", ctx->key_w);
   }
+#undef EDV_BUILD_CASE
 }
 
 static int launch_verify_keyed(edv_ctx* ctx, const void* d_sig, const void* d_kidx, const void* d_msgs,
@@ -953,7 +986,7 @@ int edv_keys_reset(edv_ctx* ctx) {
 int edv_keys_set_window(edv_ctx* ctx, int w) {
   int r = set_device(ctx);
   if (r) return r;
-  if (w != 4 && w != 6 && w != 8 && w != 10) return set_err(EDV_EINVAL, "key window %d (4, 6, 8 or 10)", w);
+  if (!key_window_ok(w)) return set_err(EDV_EINVAL, "key window %d (4, 6, 8, 10, 12, 13, 14 or 16)", w);
   if (ctx->key_count) return set_err(EDV_EINVAL, "key window change with %llu keys registered (edv_keys_reset first)",
                                      (unsigned long long)ctx->key_count);
   if (w == ctx->key_w) return 0;
@@ -1086,7 +1119,7 @@ edv_ctx* edv_create(int device) {
     if ((e = hipMalloc(&pre, (size_t)rowsB * EB * 10 * 4)) != hipSuccess) return fail("hipMalloc", e);
     hipLaunchKernelGGL(edv_base_rows_kernel, dim3(1), dim3(64), 0, ctx->stream, rows);
     hipLaunchKernelGGL(edv_comb_fill_kernel<kBaseW>, dim3((uint32_t)div_up(rowsB * FillShape<kBaseW>::NCH, kBlock)),
-                       dim3(kBlock), 0, ctx->stream, rows, (uint64_t)rowsB, ctx->d_btab_comb32, pre);
+                       dim3(kBlock), 0, ctx->stream, rows, (uint64_t)rowsB, ctx->d_btab_comb32, pre, 0ull, 1ull);
     e = hipStreamSynchronize(ctx->stream);
     (void)hipFree(rows);
     (void)hipFree(pre);
@@ -1114,7 +1147,7 @@ edv_ctx* edv_create(int device) {
     return fail("hipMalloc(sort)", e);
   if (const char* w = getenv("EDV_KEY_WINDOW")) {
     const int kw = atoi(w);
-    if (kw == 4 || kw == 6 || kw == 8 || kw == 10) ctx->key_w = kw;
+    if (key_window_ok(kw)) ctx->key_w = kw;
   }
   return ctx;
 }

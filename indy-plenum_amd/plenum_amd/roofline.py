@@ -39,7 +39,7 @@ BASE_ROWS = key_rows(BASE_W)
 
 
 def mad_comb_kernel(w):
-    return (key_rows(w) + BASE_ROWS) * 7 * MAD_PER_FE  # W=10: 29,400; W=8: 33,600
+    return (key_rows(w) + BASE_ROWS) * 7 * MAD_PER_FE  # W=13: 25,200; W=10: 29,400; W=8: 33,600
 
 
 # edv_encode_kernel<M>: per request 3 multiplications of Montgomery's trick +

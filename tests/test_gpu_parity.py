@@ -164,6 +164,51 @@ def test_keyed_random_vs_oracle_and_out_of_range(gpu_engine, oracle):
     assert not got[::5].any() and (got[1::5] == want[1::5]).all()
 
 
+@pytest.mark.parametrize("w", [4, 6, 8, 12, 13, 14, 16])
+def test_keyed_every_window(gpu_engine, w):
+    """The key store at every window edv_keys_set_window accepts (the default
+    10 is covered above): golden edge + valid items, each key its own table."""
+    e, v = load_npz("ed25519_edge.npz"), load_npz("ed25519_valid.npz")
+    try:
+        gpu_engine.keys_reset()
+        gpu_engine.keys_set_window(w)
+        assert gpu_engine.keys_window == w
+        for d, step in ((e, 2), (v, 9)):
+            gpu_engine.keys_reset()
+            sel = np.arange(0, len(d["pk"]), step)
+            first = gpu_engine.keys_add(d["pk"][sel])
+            kidx = np.full(len(d["pk"]), 0xFFFFFFFF, np.uint32)
+            kidx[sel] = np.arange(first, first + len(sel), dtype=np.uint32)
+            got = gpu_engine.verify_batch_keyed(d["sig"], kidx, d["msgs"], d["off"])
+            want = d["expect"].astype(bool).copy()
+            want[np.setdiff1d(np.arange(len(want)), sel)] = False  # unregistered ids reject
+            assert (got == want).all(), (w, np.nonzero(got != want))
+    finally:
+        gpu_engine.keys_reset()
+        gpu_engine.keys_set_window(10)
+
+
+@pytest.mark.parametrize("w", [10, 13])
+def test_keyed_store_growth(gpu_engine, w):
+    """Keys registered in slices across key-store growth (64 -> 128 -> 256
+    tables): the row-major store is re-laid out on every growth, and earlier
+    keys keep their verdicts."""
+    d = load_npz("ed25519_edge.npz")
+    try:
+        gpu_engine.keys_reset()
+        gpu_engine.keys_set_window(w)
+        ids = []
+        for a in range(0, len(d["pk"]), 40):
+            first = gpu_engine.keys_add(d["pk"][a:a + 40])
+            ids.extend(range(first, first + len(d["pk"][a:a + 40])))
+        kidx = np.asarray(ids, np.uint32)
+        got = gpu_engine.verify_batch_keyed(d["sig"], kidx, d["msgs"], d["off"])
+        assert (got == d["expect"].astype(bool)).all(), np.nonzero(got != d["expect"].astype(bool))
+    finally:
+        gpu_engine.keys_reset()
+        gpu_engine.keys_set_window(10)
+
+
 @pytest.mark.parametrize("n", [1023, 1024, 1025, 4096, 4097, 6143])
 def test_sub_batch_boundaries(gpu_engine, oracle, n):
     """The pipelined launcher cuts a chunk into up to 4 sub-batches aligned to
