@@ -342,11 +342,12 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     ph = np.mean(np.array(phases), axis=0)  # per step: per-phase sums over the sub-batch launches
     launches = eng.last_launch_count()
+    n_chunk = eng.last_chunk_items()  # the phase times cover the last 2^20-request chunk
     dsm_sum = float(ph[2])
     dsm_avg = dsm_sum / launches
     kernel_mad = RL.mad_comb_kernel(args.key_window) if args.path == "keyed" else RL.MAD_DSM_KERNEL
     kernel_name = "edv_comb_kernel" if args.path == "keyed" else "edv_dsm_kernel"
-    achieved = (n / launches) * kernel_mad / (dsm_avg * 1e-3) / 1e12
+    achieved = (n_chunk / launches) * kernel_mad / (dsm_avg * 1e-3) / 1e12
     peak = RL.PEAK_MAD_PER_S / 1e12
     # HBM bytes per launch from the committed PMC pass (tools/pmc_passes.sh ->
     # tools/pmc_summary.py): 2 x FETCH_SIZE + WRITE_SIZE per request (gfx950
@@ -359,7 +360,7 @@ def main():
         key = "%s<%d>" % (kernel_name, args.key_window) if args.path == "keyed" else kernel_name
         row = tj.get("kernels", {}).get(key)
         if row and "traffic_bytes_per_request" in row:
-            traffic = row["traffic_bytes_per_request"] * (n / launches)
+            traffic = row["traffic_bytes_per_request"] * (n_chunk / launches)
 
     # the dominant kernel alone on the GPU (one sub-batch, no overlap), one
     # untimed step: its own roofline fraction beside the overlapped one above
@@ -368,9 +369,10 @@ def main():
     solo = eng.last_phases_ms()
     eng.set_pipeline(args.pipeline)
     solo_ms = float(solo[2])
-    standalone = {"avg_launch_ms": solo_ms, "n_per_launch": n,
-                  "achieved": n * kernel_mad / (solo_ms * 1e-3) / 1e12,
-                  "frac": n * kernel_mad / (solo_ms * 1e-3) / RL.PEAK_MAD_PER_S,
+    solo_n = eng.last_chunk_items()
+    standalone = {"avg_launch_ms": solo_ms, "n_per_launch": solo_n,
+                  "achieved": solo_n * kernel_mad / (solo_ms * 1e-3) / 1e12,
+                  "frac": solo_n * kernel_mad / (solo_ms * 1e-3) / RL.PEAK_MAD_PER_S,
                   "note": "same kernel, one launch over the whole batch with nothing else running (untimed step)"}
 
     cpu = None
@@ -405,15 +407,16 @@ def main():
                        "requests_per_gpu": n, "signers": args.signers, "parallelism": "dp%d (request-index shards)" % world},
             "roofline": {"bound": "valu", "kernel": kernel_name, "achieved": achieved, "peak": peak,
                          "unit": "TMAD/s", "frac": achieved / peak, "traffic": traffic,
-                         "algorithmic": "%d MAD per verify (%s), %d launches per step of n=%d requests each, "
-                                        "avg launch %.3f ms (HIP events on the launch streams)" % (
-                             kernel_mad, RL.kernel_work(kernel_name, args.key_window), launches, n // launches,
-                             dsm_avg),
+                         "algorithmic": "%d MAD per verify (%s), %d launches per chunk of %d requests (n=%d each; "
+                                        "%d requests per step), avg launch %.3f ms (HIP events on the launch streams)" % (
+                             kernel_mad, RL.kernel_work(kernel_name, args.key_window), launches, n_chunk,
+                             n_chunk // launches, n, dsm_avg),
                          "standalone": standalone},
             "path": args.path,
             "phase_ms": {"hash": float(ph[0]), "table": float(ph[1]),
                          ("comb" if args.path == "keyed" else "dsm"): dsm_sum, "encode": float(ph[3]),
-                         "note": "per-phase sums over %d overlapped sub-batch launches" % launches},
+                         "note": "per-phase sums over the %d overlapped sub-batch launches of the last "
+                                 "%d-request chunk" % (launches, n_chunk)},
             "length_buckets": bool(buckets),
             "key_window": args.key_window, "key_table_build_ms": key_build_ms, "keys": int(reg_pks.shape[0]),
             "value_incl_key_build_one_step": (n * world / (ms_per_step * 1e-3 + key_build_ms * 1e-3)

@@ -103,6 +103,9 @@ int edv_verify_batch_device(edv_ctx *ctx, const void *d_sig64, const void *d_pk3
  * or < 0. */
 int edv_last_phases_ms(edv_ctx *ctx, double *out4);
 int edv_last_launch_count(edv_ctx *ctx);
+/* Requests in the last chunk of the last verify call (a call over more than
+ * 2^20 requests runs in chunks; the phase times cover the last one). */
+uint64_t edv_last_chunk_items(edv_ctx *ctx);
 /* Sub-batches per chunk (1..4, default 4); 1 = no overlap (each kernel runs
  * alone on the GPU, e.g. to time one kernel in isolation). */
 int edv_set_pipeline(edv_ctx *ctx, int sub_batches);

@@ -26,7 +26,7 @@ constexpr int kEntryWords = 32;
 
 template <int W>
 struct Window {
-  static_assert(W >= 4 && W <= 16, "comb window width 4..16");
+  static_assert(W >= 4 && W <= 20, "comb window width 4..20");
   // x < L < 2^253 plus the digit bias must stay below 2^(W * kRows): W * kRows >= 254
   static constexpr int kRows = (254 + W - 1) / W;
   static constexpr int kEntries = 1 << (W - 1);

@@ -330,7 +330,7 @@ __global__ __launch_bounds__(kBlock) void edv_encode_kernel(const uint8_t* __res
 #ifndef EDV_COMB_MIN_WAVES
 #define EDV_COMB_MIN_WAVES 4  // 128 VGPRs: 1M lanes = 3.8 rounds of 262k (3 waves: 5.1 rounds -> 15% tail); -11% vs 3 (tools/ab_keyed.py)
 #endif
-constexpr int kBaseTabWords = Window<kBaseW>::kTableWords;  // 131072 words at W = 8
+constexpr int kBaseTabWords = Window<kBaseW>::kTableWords;  // 218M words at W = 20
 constexpr int kRowWords = 40;
 
 // One lane per key: decode -A, libsodium's key checks, the row bases.
@@ -647,10 +647,11 @@ struct edv_ctx {
   hipEvent_t ev_sub[kSub][kEv] = {};
   hipEvent_t ev_join[2] = {};
   int last_nsub = 0;
+  uint64_t last_chunk_n = 0;  // requests in the last chunk (what edv_last_phases_ms covers)
   int max_sub = kSub;  // edv_set_pipeline
   bool timed = false;
   // key-table store (registered public keys)
-  uint32_t* d_btab_comb32 = nullptr;  // base-point comb table (kBaseW; 64 MiB at W = 16)
+  uint32_t* d_btab_comb32 = nullptr;  // base-point comb table (kBaseW; 832 MiB at W = 20)
   uint32_t* d_ident = nullptr;        // identity niels entry (comb accessors' j = -1)
   uint8_t* d_key_pk = nullptr;
   uint8_t* d_key_valid = nullptr;
@@ -832,6 +833,7 @@ int launch_pipeline(edv_ctx* ctx, bool keyed, const void* d_sig, const void* d_k
       if (r) return r;
     }
     ctx->last_nsub = ns;
+    ctx->last_chunk_n = cn;
     if (c0 + cn < n) {  // join before the scratch is reused
       HIP_TRY(hipEventRecord(ctx->ev_join[1], ctx->stream2));
       HIP_TRY(hipStreamWaitEvent(st, ctx->ev_join[1], 0));
@@ -893,7 +895,8 @@ static int keys_reserve(edv_ctx* ctx, uint64_t need) {
 
 // Build tables for keys [first, first + nkeys) whose 32-byte encodings are
 // already in d_key_pk, in slices of kKeyBuildSlice keys (bounded scratch).
-constexpr uint64_t kKeyBuildScratch = 128ull << 20;  // bytes of row bases + prefix products per slice
+constexpr uint64_t kKeyBuildScratch = 1ull << 30;  // bytes of row bases + prefix products per slice (the row
+                                                   // kernel is one lane per key: fewer, larger slices)
 template <int W>
 static int keys_build_w(edv_ctx* ctx, uint64_t first, uint64_t nkeys, hipStream_t st) {
   constexpr int R = Window<W>::kRows, E = Window<W>::kEntries;
@@ -1216,6 +1219,7 @@ int edv_last_phases_ms(edv_ctx* ctx, double* out4) {
 }
 
 int edv_last_launch_count(edv_ctx* ctx) { return ctx ? ctx->last_nsub : 0; }
+uint64_t edv_last_chunk_items(edv_ctx* ctx) { return ctx ? ctx->last_chunk_n : 0; }
 
 int edv_set_length_buckets(edv_ctx* ctx, int mode) {
   if (!ctx) return set_err(EDV_EINVAL, "null context");

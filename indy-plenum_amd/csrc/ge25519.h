@@ -222,11 +222,13 @@ EDV_HD void ge_add_signed(ge_p3& r, const ge_p3& p, const ge_cached& q, bool neg
 
 // p1p1 -> p2/p3 need the W operand first (fe_mul's f).  ge_add/madd leave T
 // in W, ge_sub/msub leave Z in W; ge_p2_dbl leaves X in W and T carried.
+// T3 = Y * X (not X * Y): the four products then need 2 * Y / 2 * T odd limbs
+// and 19 * X / 19 * Z premultiplies only (fe_mul's f2 / g19), not three each.
 EDV_HD void ge_p1p1_to_p3_addlike(ge_p3& r, const ge_p1p1& p) {  // T is W
   fe_mul(r.X, p.T, p.X);
   fe_mul(r.Y, p.Y, p.Z);
   fe_mul(r.Z, p.T, p.Z);
-  fe_mul(r.T, p.X, p.Y);
+  fe_mul(r.T, p.Y, p.X);
 }
 EDV_HD void ge_p1p1_to_p3_sublike(ge_p3& r, const ge_p1p1& p) {  // Z is W
   fe_mul(r.X, p.X, p.T);

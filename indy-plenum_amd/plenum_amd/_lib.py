@@ -29,6 +29,7 @@ SIGNATURES = {
     "edv_verify_batch_device": (_I, [_P, _P, _P, _P, _P, _U64, _P, _P]),
     "edv_last_phases_ms": (_I, [_P, _P]),
     "edv_last_launch_count": (_I, [_P]),
+    "edv_last_chunk_items": (_U64, [_P]),
     "edv_set_pipeline": (_I, [_P, _I]),
     "edv_set_length_buckets": (_I, [_P, _I]),
     "edv_last_phase_ms": (_I, [_P, _P, _P, _P]),

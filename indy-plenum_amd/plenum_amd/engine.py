@@ -185,6 +185,10 @@ class EdVerifyEngine:
         """Kernel launches per phase (sub-batches) in the last verify chunk."""
         return int(self._lib.edv_last_launch_count(self._ctx))
 
+    def last_chunk_items(self):
+        """Requests in the last verify chunk (what last_phases_ms covers)."""
+        return int(self._lib.edv_last_chunk_items(self._ctx))
+
     def set_pipeline(self, sub_batches):
         """Sub-batches per chunk (1..4; 1 = kernels run one at a time)."""
         check(self._lib.edv_set_pipeline(self._ctx, int(sub_batches)))

@@ -25,10 +25,10 @@ MAD_PER_VERIFY = 305_000
 MAD_DSM_KERNEL = FE_DSM * MAD_PER_FE  # 251,000
 MAD_TABLE_KERNEL = FE_DECODE * MAD_PER_FE
 # Key-table path (keys registered once): edv_comb_kernel<W> = fixed-base combs
-# over both tables -- ceil(254 / W) rows of the key table + ceil(254 / 16) = 16
-# rows of the W = 16 base table (verify_core.h kBaseW) -- one mixed addition
+# over both tables -- ceil(254 / W) rows of the key table + ceil(254 / 20) = 13
+# rows of the W = 20 base table (verify_core.h kBaseW) -- one mixed addition
 # (7 multiplications) per row.
-BASE_W = 16
+BASE_W = 20
 
 
 def key_rows(w):
@@ -39,7 +39,7 @@ BASE_ROWS = key_rows(BASE_W)
 
 
 def mad_comb_kernel(w):
-    return (key_rows(w) + BASE_ROWS) * 7 * MAD_PER_FE  # W=13: 25,200; W=10: 29,400; W=8: 33,600
+    return (key_rows(w) + BASE_ROWS) * 7 * MAD_PER_FE  # W=13: 23,100; W=10: 27,300; W=8: 31,500
 
 
 # edv_encode_kernel<M>: per request 3 multiplications of Montgomery's trick +
