@@ -134,14 +134,19 @@ double edv_last_kernel_ms(edv_ctx *ctx);
  * window W trades HBM for additions per verify:
  *   W = 4:  64 KiB per key, 64 additions  (1M keys =  64 GiB)
  *   W = 6: 172 KiB per key, 43 additions  (1M keys = 172 GiB)
- *   W = 8: 512 KiB per key, 32 additions  (default; 500k keys = 256 GiB)
+ *   W = 8: 512 KiB per key, 32 additions  (500k keys = 256 GiB)
+ *   W = 10: 1.6 MiB per key, 26 additions (context default)
+ *   W = 12 / 13 / 14 / 16: 5.5 / 10 / 19 / 64 MiB per key, 22 / 20 / 19 / 16
+ *   additions (bench.py uses 13: 1,000 keys = 10 GiB)
+ * Tables are stored row-major over keys (row r of every key in one slab), so
+ * lanes verifying different keys gather from one slab at a time.
  * Key ids are consecutive from *first_id.  Host / device-pointer forms. */
 int edv_keys_add(edv_ctx *ctx, const uint8_t *pk32, uint64_t nkeys, uint64_t *first_id);
 int edv_keys_add_device(edv_ctx *ctx, const void *d_pk32, uint64_t nkeys, uint64_t *first_id, void *stream);
 uint64_t edv_keys_count(edv_ctx *ctx);
 /* Forget all registered keys (device memory is kept for reuse). */
 int edv_keys_reset(edv_ctx *ctx);
-/* Set the key window (4, 6 or 8; environment EDV_KEY_WINDOW sets the
+/* Set the key window (4, 6, 8, 10, 12, 13, 14 or 16; environment EDV_KEY_WINDOW sets the
  * context default).  Only with no keys registered; frees the key store. */
 int edv_keys_set_window(edv_ctx *ctx, int w);
 int edv_keys_window(edv_ctx *ctx);

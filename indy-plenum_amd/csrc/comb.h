@@ -14,8 +14,9 @@
 //       W = 6: 43 rows x  32 entries x 128 B = 172 KiB per key, 43 additions
 //       W = 8: 32 rows x 128 entries x 128 B = 512 KiB per key, 32 additions
 //       W = 10: 26 rows x 512 entries x 128 B = 1.6 MiB per key, 26 additions
+//       W = 13: 20 rows x 4096 entries x 128 B = 10 MiB per key, 20 additions
 //   B = the base point, one table per context (kBaseW, verify_core.h):
-//       W = 12: 22 rows x 2048 entries x 128 B = 5.5 MiB (L2 4 MiB per XCD, MALL).
+//       W = 20: 13 rows x 524288 entries x 128 B = 832 MiB.
 // Entries are 32 u32 words (30 limbs + 2 pad) so one entry is 8 dwordx4 loads.
 #pragma once
 #include "ge25519.h"

@@ -202,7 +202,9 @@ class EdVerifyEngine:
     # ------------------------------------------------------------ key tables
     def keys_set_window(self, w):
         """Comb window of the key tables: 4 (64 KiB/key, 64 additions per
-        verify), 6 (172 KiB, 43) or 8 (512 KiB, 32).  Only with no keys."""
+        verify), 6 (172 KiB, 43), 8 (512 KiB, 32), 10 (1.6 MiB, 26; the
+        default), 12, 13 (10 MiB, 20), 14 or 16 (64 MiB, 16).  Only with no
+        keys registered."""
         check(self._lib.edv_keys_set_window(self._ctx, int(w)))
 
     @property
