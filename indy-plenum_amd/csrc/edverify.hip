@@ -412,7 +412,10 @@ __global__ __launch_bounds__(kBlock, EDV_HASH_MIN_WAVES) void edv_hash_keyed_ker
   flags[i] = ok ? 1 : 0;
 }
 
-// [h](-A) + [S]B over the key's comb (W) and the base comb (W = 8): no doublings.
+#ifndef EDV_COMB_SET
+#define EDV_COMB_SET 1  // 1: the key comb's row 0 by comb_set (1 multiplication, not a 7-multiplication addition)
+#endif
+// [h](-A) + [S]B over the key's comb (W) and the base comb (kBaseW): no doublings.
 template <int W>
 __global__ __launch_bounds__(kBlock, EDV_COMB_MIN_WAVES) void edv_comb_kernel(const uint8_t* __restrict__ sig64,
                                                          const uint32_t* __restrict__ key_idx, uint32_t key_count,
@@ -433,9 +436,14 @@ __global__ __launch_bounds__(kBlock, EDV_COMB_MIN_WAVES) void edv_comb_kernel(co
   const DevComb<W> ta{key_tab + (uint64_t)key * kRowWordsW, ident, key_cap * kRowWordsW};  // row-major store
   const DevComb<kBaseW> tb{btab, ident};
   ge_p3 Q;
+#if EDV_COMB_SET
+  comb_mul_set<W>(Q, h, ta);  // Q = [h](-A): row 0 set, not added to the identity
+  uint32_t sink = comb_mul_add<kBaseW>(Q, S, tb);
+#else
   ge_p3_0(Q);
   uint32_t sink = comb_mul_add<W>(Q, h, ta);
   sink ^= comb_mul_add<kBaseW>(Q, S, tb);
+#endif
   store_point_soa(pt, stride, i, Q);
   if (sink == 0x9e3779b9u && key0 == 0xffffffffu && key_count == 0) pt[i] = sink;  // keeps the prefetches live
 }

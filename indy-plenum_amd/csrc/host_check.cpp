@@ -162,8 +162,7 @@ static bool comb_point(ge_p3& Q, const uint32_t sig[16], const uint32_t pk[8], c
   ok = ge_frombytes(A, pk, true) && is_canonical_point(pk) && !has_small_order(pk) && ok;
   std::vector<uint32_t> atab;
   build_table<W>(atab, A);
-  ge_p3_0(Q);
-  comb_mul_add<W>(Q, h, HostComb<W>{atab.data()});
+  comb_mul_set<W>(Q, h, HostComb<W>{atab.data()});
   comb_mul_add<kBaseW>(Q, sig + 8, HostComb<kBaseW>{base_comb()});
   return ok;
 }
