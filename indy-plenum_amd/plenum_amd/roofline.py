@@ -27,7 +27,8 @@ MAD_TABLE_KERNEL = FE_DECODE * MAD_PER_FE
 # Key-table path (keys registered once): edv_comb_kernel<W> = fixed-base combs
 # over both tables -- ceil(254 / W) rows of the key table + ceil(254 / 20) = 13
 # rows of the W = 20 base table (verify_core.h kBaseW) -- one mixed addition
-# (7 multiplications) per row.
+# (7 multiplications) per row, except the key comb's row 0, which is set with
+# one multiplication (comb.h comb_set).
 BASE_W = 20
 
 
@@ -39,7 +40,7 @@ BASE_ROWS = key_rows(BASE_W)
 
 
 def mad_comb_kernel(w):
-    return (key_rows(w) + BASE_ROWS) * 7 * MAD_PER_FE  # W=13: 23,100; W=10: 27,300; W=8: 31,500
+    return ((key_rows(w) - 1 + BASE_ROWS) * 7 + 1) * MAD_PER_FE  # W=13: 22,500; W=10: 26,700; W=8: 30,900
 
 
 # edv_encode_kernel<M>: per request 3 multiplications of Montgomery's trick +
@@ -53,8 +54,8 @@ MAD_COMB_KERNEL = mad_comb_kernel(10)
 
 def kernel_work(name, w=8):
     if name == "edv_comb_kernel":
-        return ("(%d key rows (W=%d) + %d base rows (W=%d)) mixed additions x 7 field ops x 100 MAD"
-                % (key_rows(w), w, BASE_ROWS, BASE_W))
+        return ("((%d - 1 key rows (W=%d; row 0 set with 1 field op) + %d base rows (W=%d)) mixed additions "
+                "x 7 field ops + 1) x 100 MAD" % (key_rows(w), w, BASE_ROWS, BASE_W))
     if name == "edv_dsm_kernel":
         return "2510 field ops (ref10 a-priori double-scalar multiplication) x 100 MAD"
     return ""
