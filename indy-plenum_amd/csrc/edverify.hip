@@ -330,7 +330,7 @@ __global__ __launch_bounds__(kBlock) void edv_encode_kernel(const uint8_t* __res
 #ifndef EDV_COMB_MIN_WAVES
 #define EDV_COMB_MIN_WAVES 4  // 128 VGPRs: 1M lanes = 3.8 rounds of 262k (3 waves: 5.1 rounds -> 15% tail); -11% vs 3 (tools/ab_keyed.py)
 #endif
-constexpr int kBaseTabWords = Window<kBaseW>::kTableWords;  // 218M words at W = 20
+constexpr int kBaseTabWords = Window<kBaseW>::kTableWords;  // 805M words at W = 22
 constexpr int kRowWords = 40;
 
 // One lane per key: decode -A, libsodium's key checks, the row bases.
@@ -659,7 +659,7 @@ struct edv_ctx {
   int max_sub = kSub;  // edv_set_pipeline
   bool timed = false;
   // key-table store (registered public keys)
-  uint32_t* d_btab_comb32 = nullptr;  // base-point comb table (kBaseW; 832 MiB at W = 20)
+  uint32_t* d_btab_comb32 = nullptr;  // base-point comb table (kBaseW; 3 GiB at W = 22)
   uint32_t* d_ident = nullptr;        // identity niels entry (comb accessors' j = -1)
   uint8_t* d_key_pk = nullptr;
   uint8_t* d_key_valid = nullptr;

@@ -25,11 +25,11 @@ MAD_PER_VERIFY = 305_000
 MAD_DSM_KERNEL = FE_DSM * MAD_PER_FE  # 251,000
 MAD_TABLE_KERNEL = FE_DECODE * MAD_PER_FE
 # Key-table path (keys registered once): edv_comb_kernel<W> = fixed-base combs
-# over both tables -- ceil(254 / W) rows of the key table + ceil(254 / 20) = 13
-# rows of the W = 20 base table (verify_core.h kBaseW) -- one mixed addition
+# over both tables -- ceil(254 / W) rows of the key table + ceil(254 / 22) = 12
+# rows of the W = 22 base table (verify_core.h kBaseW) -- one mixed addition
 # (7 multiplications) per row, except the key comb's row 0, which is set with
 # one multiplication (comb.h comb_set).
-BASE_W = 20
+BASE_W = 22
 
 
 def key_rows(w):
@@ -40,7 +40,7 @@ BASE_ROWS = key_rows(BASE_W)
 
 
 def mad_comb_kernel(w):
-    return ((key_rows(w) - 1 + BASE_ROWS) * 7 + 1) * MAD_PER_FE  # W=13: 22,500; W=10: 26,700; W=8: 30,900
+    return ((key_rows(w) - 1 + BASE_ROWS) * 7 + 1) * MAD_PER_FE  # W=13: 21,800; W=10: 26,000; W=8: 30,200
 
 
 # edv_encode_kernel<M>: per request 3 multiplications of Montgomery's trick +
