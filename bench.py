@@ -59,7 +59,7 @@ def parse():
     ap.add_argument("--path", choices=["keyed", "general"], default="keyed",
                     help="keyed: signers' verkeys registered once (fixed-base tables in HBM, like "
                          "SimpleAuthNr.addIdr); general: every request carries its own key bytes")
-    ap.add_argument("--key-window", type=int, choices=[4, 6, 8, 10, 12, 13, 14, 16], default=13,
+    ap.add_argument("--key-window", type=int, choices=[4, 6, 8, 10, 12, 13, 14, 16], default=14,
                     help="comb window of the key tables (edv_keys_set_window)")
     ap.add_argument("--pipeline", type=int, default=4, choices=[1, 2, 3, 4],
                     help="sub-batches per chunk (edv_set_pipeline; 1 = one launch per kernel, no overlap)")
