@@ -74,42 +74,6 @@ def parse():
     return ap.parse_args()
 
 
-def corrupt_c2(sig, pk, msgs, off, rng):
-    """configs[2]: 10% rejects, split equally over bit flips in R/S/M, S+L,
-    S|2^255, small-order A, non-canonical A, R = identity, R + T8."""
-    n = sig.shape[0]
-    bad = rng.choice(n, size=n // 10, replace=False)
-    kinds = bad % 9
-    L = 2**252 + 27742317777372353535851937790883648493
-    small_A = bytes.fromhex("26e8958fc2b227b045c3f489f2ef98f0d5dfac05d3c63339b13802886d53fc05")
-    noncanon_A = (2**255 - 19 + 3).to_bytes(32, "little")
-    ident = (1).to_bytes(32, "little")
-    for i, k in zip(bad, kinds):
-        if k == 0:
-            sig[i, rng.integers(0, 32)] ^= 1 << int(rng.integers(0, 8))
-        elif k == 1:
-            sig[i, 32 + rng.integers(0, 31)] ^= 1 << int(rng.integers(0, 8))
-        elif k == 2:
-            a, b = int(off[i]), int(off[i + 1])
-            msgs[a + int(rng.integers(0, b - a))] ^= 1 << int(rng.integers(0, 8))
-        elif k == 3:
-            s = int.from_bytes(sig[i, 32:].tobytes(), "little") + L
-            sig[i, 32:] = np.frombuffer(s.to_bytes(32, "little"), np.uint8)
-        elif k == 4:
-            sig[i, 63] |= 0x80
-        elif k == 5:
-            pk[i] = np.frombuffer(small_A, np.uint8)
-        elif k == 6:
-            pk[i] = np.frombuffer(noncanon_A, np.uint8)
-        elif k == 7:
-            sig[i, :32] = np.frombuffer(ident, np.uint8)
-        else:
-            sig[i, :32] = np.frombuffer(synth.add_torsion(sig[i, :32].tobytes()), np.uint8)
-    expect = np.ones(n, dtype=bool)
-    expect[bad] = False
-    return expect
-
-
 def cpu_baseline(sig, pk, msgs, off, threads):
     lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "_build", "libcpu_baseline.so"))
     lib.cpu_baseline_sodium_version.restype = ctypes.c_char_p
@@ -189,7 +153,7 @@ def main():
     if args.config == "c2":
         off = np.concatenate([item_start, item_end[-1:]])
         sig_h, pk_h, buf_h = d_sig.cpu().numpy().copy(), d_pk.cpu().numpy().copy(), buf.copy()
-        expect = corrupt_c2(sig_h, pk_h, buf_h, off, np.random.default_rng(2))
+        expect = synth.corrupt_configs2(sig_h, pk_h, buf_h, off, np.random.default_rng(2))
         d_sig = torch.from_numpy(sig_h).to(dev)
         d_pk = torch.from_numpy(pk_h).to(dev)
         buf = buf_h
@@ -247,6 +211,10 @@ def main():
         d_vkey, d_vphase, d_vvoter = (torch.from_numpy(a).to(dev) for a in
                                       (v_key.astype(np.int32), v_phase, v_voter))
         d_keep = torch.from_numpy(keep.astype(np.uint8)).to(dev)
+        # the primary of each key's view (view = key // 1000, primary = view % V):
+        # its PREPARE never counts (replica.py:1289-1291)
+        primary = ((np.arange(n_keys) // 1000) % V).astype(np.uint8)
+        d_primary = torch.from_numpy(primary).to(dev)
         d_ballot = torch.zeros(n_keys * 2 * V, dtype=torch.uint8, device=dev)
         d_counts = torch.zeros(n_keys * 2, dtype=torch.int32, device=dev)
         d_quorum = torch.zeros(n_keys, dtype=torch.uint8, device=dev)
@@ -258,7 +226,7 @@ def main():
             bits = ((d_words.view(torch.uint8)[: (nv + 7) // 8].unsqueeze(1) >> shifts) & 1).reshape(-1)[:nv]
             d_valid = bits * d_keep
             eng.tally_device(d_vkey, d_vvoter, d_vphase, d_valid, nv, n_keys, V, d_ballot, d_counts, d_quorum,
-                             stream=stream)
+                             stream=stream, d_primary=d_primary)
             if world > 1:
                 dist.all_reduce(d_ballot, op=dist.ReduceOp.MAX)
             eng.tally_finish_device(d_ballot, n_keys, V, d_counts, d_quorum, stream=stream)
@@ -271,7 +239,9 @@ def main():
             for r in range(world):
                 gr = np.arange(nv, dtype=np.int64) + r * nv
                 kr = np.random.default_rng(40 + r).random(nv) >= 0.05
-                np.add.at(cnt, (gr // (2 * V)) * 2 + (gr % (2 * V)) // V, kr.astype(np.int64))
+                kk, ph, vv = gr // (2 * V), (gr % (2 * V)) // V, gr % V
+                kr &= ~((ph == 0) & (vv == primary[kk]))
+                np.add.at(cnt, kk * 2 + ph, kr.astype(np.int64))
             f = (V - 1) // 3
             q = ((cnt[0::2] >= V - f - 1).astype(np.uint8) | ((cnt[1::2] >= V - f).astype(np.uint8) << 1))
             got_c = d_counts.cpu().numpy().astype(np.int64)

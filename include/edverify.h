@@ -137,12 +137,16 @@ double edv_last_kernel_ms(edv_ctx *ctx);
  *   W = 8: 512 KiB per key, 32 additions  (500k keys = 256 GiB)
  *   W = 10: 1.6 MiB per key, 26 additions (context default)
  *   W = 12 / 13 / 14 / 16: 5.5 / 10 / 19 / 64 MiB per key, 22 / 20 / 19 / 16
- *   additions (bench.py uses 13: 1,000 keys = 10 GiB)
+ *   additions (bench.py headline: 14, 1,000 keys = 19 GiB)
  * Tables are stored row-major over keys (row r of every key in one slab), so
  * lanes verifying different keys gather from one slab at a time.
  * Key ids are consecutive from *first_id.  Host / device-pointer forms. */
 int edv_keys_add(edv_ctx *ctx, const uint8_t *pk32, uint64_t nkeys, uint64_t *first_id);
 int edv_keys_add_device(edv_ctx *ctx, const void *d_pk32, uint64_t nkeys, uint64_t *first_id, void *stream);
+/* Re-register slots [first_id, first_id + nkeys) with new keys (all < the
+ * registered count): the caller's LRU eviction.  Waits for in-flight work on
+ * the device first, so no verify reads a half-rebuilt table. */
+int edv_keys_set(edv_ctx *ctx, uint64_t first_id, const uint8_t *pk32, uint64_t nkeys);
 uint64_t edv_keys_count(edv_ctx *ctx);
 /* Forget all registered keys (device memory is kept for reuse). */
 int edv_keys_reset(edv_ctx *ctx);
@@ -207,13 +211,18 @@ int edv_sha256_batch(edv_ctx *ctx, const uint8_t *msgs, const uint64_t *msg_off,
  * vote counts once) and compares against Quorums(n_validators)
  * (quorums.py:15-32: f = (n-1)//3 for n >= 4 else 0; prepare = n-f-1,
  * commit = n-f).
+ * A PREPARE from the primary of its key's view never counts: the replica
+ * rejects it as SuspiciousNode(PR_FRM_PRIMARY) before Prepares.addVote
+ * (plenum/server/replica.py:1289-1291).
  *   d_key, d_voter, d_phase, d_valid : n_votes entries (uint32, uint8, uint8, uint8)
+ *   d_primary: n_keys bytes, the primary's voter index per key (0xff = none),
+ *              or NULL (no primary rejection)
  *   d_ballot : n_keys * n_validators * 2 bytes of scratch/output, zeroed here;
  *              ballot[(k * 2 + phase) * n_validators + v] = 1 if a valid vote
  *   d_counts : n_keys * 2 uint32 (distinct voters per key and phase)
  *   d_quorum : n_keys bytes: bit0 = prepare quorum, bit1 = commit quorum. */
 int edv_tally_device(edv_ctx *ctx, const void *d_key, const void *d_voter, const void *d_phase, const void *d_valid,
-                     uint64_t n_votes, uint32_t n_keys, uint32_t n_validators, void *d_ballot, void *d_counts,
+                     const void *d_primary, uint64_t n_votes, uint32_t n_keys, uint32_t n_validators, void *d_ballot, void *d_counts,
                      void *d_quorum, void *stream);
 
 /* Second half of the tally alone: counts + quorum flags from a ballot array
@@ -223,7 +232,7 @@ int edv_tally_finish_device(edv_ctx *ctx, const void *d_ballot, uint32_t n_keys,
 
 /* Host-pointer convenience form of edv_tally_device. */
 int edv_tally(edv_ctx *ctx, const uint32_t *key, const uint8_t *voter, const uint8_t *phase, const uint8_t *valid,
-              uint64_t n_votes, uint32_t n_keys, uint32_t n_validators, uint32_t *counts_out, uint8_t *quorum_out);
+              const uint8_t *primary, uint64_t n_votes, uint32_t n_keys, uint32_t n_validators, uint32_t *counts_out, uint8_t *quorum_out);
 
 #ifdef __cplusplus
 }

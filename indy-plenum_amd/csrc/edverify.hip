@@ -576,14 +576,19 @@ __global__ __launch_bounds__(kBlock) void edv_sha256_kernel(const uint8_t* __res
   o[1] = make_uint4(d[4], d[5], d[6], d[7]);
 }
 
+// Replica.validatePrepare (plenum/server/replica.py:1289-1291): a PREPARE from
+// the primary of its key's view is rejected (SuspiciousNode) before it reaches
+// Prepares.addVote, so it never counts.  primary[k] = that voter (0xff: none).
 __global__ void edv_tally_scatter_kernel(const uint32_t* __restrict__ key, const uint8_t* __restrict__ voter,
                                          const uint8_t* __restrict__ phase, const uint8_t* __restrict__ valid,
-                                         uint64_t n_votes, uint32_t n_keys, uint32_t n_validators,
-                                         uint8_t* __restrict__ ballot) {
+                                         const uint8_t* __restrict__ primary, uint64_t n_votes, uint32_t n_keys,
+                                         uint32_t n_validators, uint8_t* __restrict__ ballot) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_votes) return;
   const uint32_t k = key[i], v = voter[i], ph = phase[i];
-  if (valid[i] && k < n_keys && v < n_validators && ph < 2) ballot[((uint64_t)k * 2 + ph) * n_validators + v] = 1;
+  if (!valid[i] || k >= n_keys || v >= n_validators || ph >= 2) return;
+  if (ph == 0 && primary && primary[k] == v) return;
+  ballot[((uint64_t)k * 2 + ph) * n_validators + v] = 1;
 }
 
 __global__ void edv_tally_count_kernel(const uint8_t* __restrict__ ballot, uint32_t n_keys, uint32_t n_validators,
@@ -882,6 +887,9 @@ static int keys_reserve(edv_ctx* ctx, uint64_t need) {
     return set_err(EDV_ENOMEM, "key store of %llu keys: %s", (unsigned long long)cap, hipGetErrorString(e));
   }
   if (ctx->key_count) {
+    // table builds of edv_keys_add_device may still run on a caller's stream:
+    // the copies below must see them complete
+    HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpyAsync(pk, ctx->d_key_pk, ctx->key_count * 32, hipMemcpyDeviceToDevice, ctx->stream));
     HIP_TRY(hipMemcpyAsync(valid, ctx->d_key_valid, ctx->key_count, hipMemcpyDeviceToDevice, ctx->stream));
     // row-major over keys: row r of every table is one slab of key_cap tables
@@ -983,6 +991,23 @@ int edv_keys_add_device(edv_ctx* ctx, const void* d_pk32, uint64_t nkeys, uint64
   }
   ctx->key_count += nkeys;
   if (first_id) *first_id = first;
+  return 0;
+}
+
+int edv_keys_set(edv_ctx* ctx, uint64_t first_id, const uint8_t* pk32, uint64_t nkeys) {
+  int r = set_device(ctx);
+  if (r) return r;
+  if (nkeys && !pk32) return set_err(EDV_EINVAL, "null pk32");
+  if (first_id > ctx->key_count || nkeys > ctx->key_count - first_id)
+    return set_err(EDV_EINVAL, "keys [%llu, %llu) outside the %llu registered", (unsigned long long)first_id,
+                   (unsigned long long)(first_id + nkeys), (unsigned long long)ctx->key_count);
+  if (nkeys) {
+    // in-flight verifies may still read the old tables of these slots
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyAsync(ctx->d_key_pk + 32 * first_id, pk32, 32 * nkeys, hipMemcpyHostToDevice, ctx->stream));
+    if ((r = keys_build(ctx, first_id, nkeys, ctx->stream))) return r;
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+  }
   return 0;
 }
 
@@ -1455,7 +1480,7 @@ int edv_tally_finish_device(edv_ctx* ctx, const void* d_ballot, uint32_t n_keys,
 }
 
 int edv_tally_device(edv_ctx* ctx, const void* d_key, const void* d_voter, const void* d_phase, const void* d_valid,
-                     uint64_t n_votes, uint32_t n_keys, uint32_t n_validators, void* d_ballot, void* d_counts,
+                     const void* d_primary, uint64_t n_votes, uint32_t n_keys, uint32_t n_validators, void* d_ballot, void* d_counts,
                      void* d_quorum, void* stream) {
   int r = set_device(ctx);
   if (r) return r;
@@ -1467,22 +1492,23 @@ int edv_tally_device(edv_ctx* ctx, const void* d_key, const void* d_voter, const
     if (!d_key || !d_voter || !d_phase || !d_valid) return set_err(EDV_EINVAL, "null vote pointer");
     hipLaunchKernelGGL(edv_tally_scatter_kernel, dim3((uint32_t)div_up(n_votes, kBlock)), dim3(kBlock), 0, st,
                        (const uint32_t*)d_key, (const uint8_t*)d_voter, (const uint8_t*)d_phase,
-                       (const uint8_t*)d_valid, n_votes, n_keys, n_validators, (uint8_t*)d_ballot);
+                       (const uint8_t*)d_valid, (const uint8_t*)d_primary, n_votes, n_keys, n_validators,
+                       (uint8_t*)d_ballot);
     HIP_TRY(hipGetLastError());
   }
   return edv_tally_finish_device(ctx, d_ballot, n_keys, n_validators, d_counts, d_quorum, st);
 }
 
 int edv_tally(edv_ctx* ctx, const uint32_t* key, const uint8_t* voter, const uint8_t* phase, const uint8_t* valid,
-              uint64_t n_votes, uint32_t n_keys, uint32_t n_validators, uint32_t* counts_out, uint8_t* quorum_out) {
+              const uint8_t* primary, uint64_t n_votes, uint32_t n_keys, uint32_t n_validators, uint32_t* counts_out, uint8_t* quorum_out) {
   int r = set_device(ctx);
   if (r) return r;
   if (n_keys == 0) return 0;
   if (!counts_out || !quorum_out) return set_err(EDV_EINVAL, "null output");
   void *d_key = nullptr, *d_voter = nullptr, *d_phase = nullptr, *d_valid = nullptr, *d_ballot = nullptr,
-       *d_counts = nullptr, *d_quorum = nullptr;
+       *d_counts = nullptr, *d_quorum = nullptr, *d_primary = nullptr;
   auto cleanup = [&]() {
-    for (void* p : {d_key, d_voter, d_phase, d_valid, d_ballot, d_counts, d_quorum})
+    for (void* p : {d_key, d_voter, d_phase, d_valid, d_ballot, d_counts, d_quorum, d_primary})
       if (p) (void)hipFree(p);
   };
   hipStream_t st = ctx->stream;
@@ -1490,9 +1516,14 @@ int edv_tally(edv_ctx* ctx, const uint32_t* key, const uint8_t* voter, const uin
   hipError_t e = hipSuccess;
   if ((e = hipMalloc(&d_key, 4 * nv)) || (e = hipMalloc(&d_voter, nv)) || (e = hipMalloc(&d_phase, nv)) ||
       (e = hipMalloc(&d_valid, nv)) || (e = hipMalloc(&d_ballot, (size_t)n_keys * 2 * n_validators + 16)) ||
-      (e = hipMalloc(&d_counts, 8ull * n_keys)) || (e = hipMalloc(&d_quorum, n_keys))) {
+      (e = hipMalloc(&d_counts, 8ull * n_keys)) || (e = hipMalloc(&d_quorum, n_keys)) ||
+      (primary && (e = hipMalloc(&d_primary, n_keys)))) {
     cleanup();
     return set_err(EDV_ENOMEM, "hipMalloc: %s", hipGetErrorString(e));
+  }
+  if (primary && (e = hipMemcpyAsync(d_primary, primary, n_keys, hipMemcpyHostToDevice, st))) {
+    cleanup();
+    return set_err(EDV_EHIP, "hipMemcpyAsync: %s", hipGetErrorString(e));
   }
   if (n_votes) {
     if ((e = hipMemcpyAsync(d_key, key, 4 * n_votes, hipMemcpyHostToDevice, st)) ||
@@ -1503,7 +1534,7 @@ int edv_tally(edv_ctx* ctx, const uint32_t* key, const uint8_t* voter, const uin
       return set_err(EDV_EHIP, "hipMemcpyAsync: %s", hipGetErrorString(e));
     }
   }
-  r = edv_tally_device(ctx, d_key, d_voter, d_phase, d_valid, n_votes, n_keys, n_validators, d_ballot, d_counts,
+  r = edv_tally_device(ctx, d_key, d_voter, d_phase, d_valid, d_primary, n_votes, n_keys, n_validators, d_ballot, d_counts,
                        d_quorum, st);
   if (!r) {
     if ((e = hipMemcpyAsync(counts_out, d_counts, 8ull * n_keys, hipMemcpyDeviceToHost, st)) ||

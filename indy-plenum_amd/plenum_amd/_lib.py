@@ -36,6 +36,7 @@ SIGNATURES = {
     "edv_last_kernel_ms": (_c.c_double, [_P]),
     "edv_keys_add": (_I, [_P, _P, _U64, _P]),
     "edv_keys_add_device": (_I, [_P, _P, _U64, _P, _P]),
+    "edv_keys_set": (_I, [_P, _U64, _P, _U64]),
     "edv_keys_count": (_U64, [_P]),
     "edv_keys_reset": (_I, [_P]),
     "edv_keys_set_window": (_I, [_P, _I]),
@@ -49,9 +50,9 @@ SIGNATURES = {
     "edv_sign_batch": (_I, [_P, _P, _P, _P, _P, _U64, _P]),
     "edv_sha256_spans_device": (_I, [_P, _P, _P, _P, _U64, _P, _P]),
     "edv_sha256_batch": (_I, [_P, _P, _P, _U64, _P]),
-    "edv_tally_device": (_I, [_P, _P, _P, _P, _P, _U64, _U32, _U32, _P, _P, _P, _P]),
+    "edv_tally_device": (_I, [_P, _P, _P, _P, _P, _P, _U64, _U32, _U32, _P, _P, _P, _P]),
     "edv_tally_finish_device": (_I, [_P, _P, _U32, _U32, _P, _P, _P]),
-    "edv_tally": (_I, [_P, _P, _P, _P, _P, _U64, _U32, _U32, _P, _P]),
+    "edv_tally": (_I, [_P, _P, _P, _P, _P, _P, _U64, _U32, _U32, _P, _P]),
 }
 
 

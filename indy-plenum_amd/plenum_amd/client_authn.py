@@ -15,6 +15,20 @@ reference's exact check order and exception classes:
 The verify step is libsodium's crypto_sign_open(sig || ser, pk)
 (nacl_wrappers.py:232-242, :108), run by libplenum_edverify.so on the GPU.
 
+GpuAuthMixin carries ALL of it -- authenticate, the batch machinery, the
+verdict cache, the key-table routing -- and relies on its host class only for
+getVerkey / addIdr (and the `clients` / `state` they use).  Mixed in front of
+the reference's own plenum.server.client_authn.SimpleAuthNr:
+
+    class GpuSimpleAuthNr(GpuAuthMixin, SimpleAuthNr): ...
+
+every authenticate() goes through the engine (no libsodium call), the
+exceptions are the reference's classes (exceptions.py re-exports them inside a
+node), and node.py:2482's isinstance(..., SimpleAuthNr) stays true.
+tests/golden/check_dropin_ref.py proves exactly this against the real
+reference class.  GpuAuthNr is the same mixin over this repo's restatement of
+SimpleAuthNr (standalone use).
+
 Added on top of the reference API (the reference calls authenticate once per
 message from Node.verifySignature, node.py:2294-2318):
   authenticate_batch(msgs)        one GPU launch for many requests; returns,
@@ -39,6 +53,7 @@ from .base58 import b58decode
 from .exceptions import (CouldNotAuthenticate, EmptyIdentifier, EmptySignature, InsufficientCorrectSignatures,
                          InsufficientSignatures, InvalidSignature, InvalidSignatureFormat, MissingIdentifier,
                          MissingSignature, SigningException, UnknownIdentifier)
+from .keystore import KeyStore, auto_window
 from .serialization import serialize_msg_for_signing
 from .verifier import DidVerifier, VerkeyCache
 
@@ -78,24 +93,8 @@ IDENTIFIER = 'identifier'
 REQ_ID = 'reqId'
 VERKEY = 'verkey'
 ROLE = 'role'
-OPERATION = 'operation'
-TXN_TYPE = 'type'
 
-
-class ClientAuthNr:
-    """Interface for client authenticators (client_authn.py:22-63)."""
-
-    @abstractmethod
-    def authenticate(self, msg: Dict, identifier: str = None, signature: str = None) -> str:
-        """Return the identifier or raise a SigningException subclass."""
-
-    @abstractmethod
-    def addIdr(self, identifier, verkey, role=None):
-        """Register an identifier's verification key."""
-
-    @abstractmethod
-    def getVerkey(self, identifier):
-        """Verification key of an identifier."""
+KEY_STORE_BYTES = 32 << 30  # HBM for key tables: the window is the widest that fits max_keys
 
 
 class _Prepared:
@@ -105,12 +104,73 @@ class _Prepared:
         self.identifier, self.sig, self.ser, self.key = identifier, sig, ser, key
 
 
-class NaclAuthNr(ClientAuthNr):
-    """The reference NaclAuthNr with the Ed25519 check moved to the GPU
-    engine.  Subclasses provide addIdr / getVerkey."""
+class _GpuState:
+    """Per-authenticator GPU state (created on first use)."""
 
-    engine = None  # set by GpuAuthMixin or by the caller (an EdVerifyEngine)
+    def __init__(self, engine=None, device=0, devices=None, verdict_cache_size=1 << 20, key_window="auto",
+                 max_keys=16384, hot_key_uses=2, key_store_bytes=KEY_STORE_BYTES):
+        self.engine = engine
+        self.device = device
+        self.devices = devices
+        self.keys = VerkeyCache()
+        self.verdicts = OrderedDict()
+        self.verdict_cache_size = verdict_cache_size
+        self.key_window = auto_window(max_keys, key_store_bytes) if key_window == "auto" else key_window
+        self.max_keys = max_keys
+        self.hot_key_uses = hot_key_uses
+        self.key_uses = OrderedDict()   # key -> successful general-path verifies (bounded LRU)
+        self.key_uses_max = 1 << 16
+        self.pending = OrderedDict()    # addIdr keys waiting for a free slot
+        self.hot = OrderedDict()        # keys that earned a slot (hot_key_uses verified requests)
+        self.stats = {"batches": 0, "batch_items": 0, "cache_hits": 0, "single_verifies": 0, "keyed_items": 0,
+                      "keys_registered": 0}
 
+
+class GpuAuthMixin:
+    """The GPU authenticator.  Mix in front of any class with the reference
+    ClientAuthNr's getVerkey / addIdr -- the reference SimpleAuthNr included
+    (INTEGRATION.md); call _gpu_init() from the constructor to configure, or
+    leave it for the defaults."""
+
+    def _gpu_init(self, engine=None, device=0, **options):
+        """engine: an EdVerifyEngine / MultiEngine (default: one on `device`;
+        devices=[...] or "all": a MultiEngine sharding every batch over them).
+        options (_GpuState): verdict_cache_size; key_window ('auto' = widest
+        comb whose max_keys tables fit key_store_bytes, e.g. 16,384 keys in
+        32 GiB -> W=10, 1,000 keys -> W=14); max_keys; hot_key_uses."""
+        self._edv = _GpuState(engine=engine, device=device, **options)
+
+    @property
+    def _g(self):
+        g = self.__dict__.get("_edv")
+        if g is None:
+            g = self._edv = _GpuState()
+        return g
+
+    @property
+    def engine(self):
+        return self._g.engine
+
+    @engine.setter
+    def engine(self, eng):
+        self._g.engine = eng
+
+    @property
+    def stats(self):
+        return self._g.stats
+
+    def _engine(self):
+        g = self._g
+        if g.engine is None:
+            if g.devices is not None:
+                from .multi import MultiEngine
+                g.engine = MultiEngine(g.devices)
+            else:
+                from .engine import EdVerifyEngine
+                g.engine = EdVerifyEngine(g.device)
+        return g.engine
+
+    # -- the reference authenticate(), verify on the GPU ----------------------
     def authenticate(self, msg: Dict, identifier: str = None, signature: str = None) -> str:
         try:
             p = self._prepare(msg, identifier, signature)
@@ -122,8 +182,8 @@ class NaclAuthNr(ClientAuthNr):
             raise CouldNotAuthenticate from ex
         return p.identifier
 
-    # the pre-verification half of authenticate(), reference order
     def _prepare(self, msg, identifier=None, signature=None, ignore=(SIG,)):
+        """Everything authenticate() does before the verify, reference order."""
         if not signature:
             try:
                 signature = msg[SIG]
@@ -149,155 +209,91 @@ class NaclAuthNr(ClientAuthNr):
         key = self._resolve_key(verkey, identifier)
         return _Prepared(identifier, sig, ser, key)
 
-    def _resolve_key(self, verkey, identifier):
-        return DidVerifier(verkey, identifier=identifier).key
-
-    def _verify_prepared(self, p):
-        if not p.key:  # nacl_wrappers.py:237-238: no key -> False
-            return False
-        return bool(self._engine().sign_open_batch(p.sig + p.ser, [0, len(p.sig) + len(p.ser)], [p.key])[0])
-
-    def _engine(self):
-        if self.engine is None:
-            from .engine import EdVerifyEngine
-            self.engine = EdVerifyEngine(0)
-        return self.engine
-
-    @abstractmethod
-    def addIdr(self, identifier, verkey, role=None):
-        pass
-
-    @abstractmethod
-    def getVerkey(self, identifier):
-        pass
-
     def serializeForSig(self, msg, topLevelKeysToIgnore=None):
+        """The reference serializer's exact bytes (native, KAT-pinned)."""
         return serialize_msg_for_signing(msg, topLevelKeysToIgnore=topLevelKeysToIgnore)
-
-
-class SimpleAuthNr(NaclAuthNr):
-    """client_authn.py:122-154.  `state` lookups for identifiers not added with
-    addIdr go through `nym_lookup(state, identifier)` (the reference calls
-    DomainRequestHandler.getNymDetails(state, identifier, isCommitted=False),
-    domain_req_handler.py:146-155); with no lookup the state is empty."""
-
-    def __init__(self, state=None, nym_lookup=None):
-        self.clients = {}  # type: Dict[str, Dict]
-        self.state = state
-        self.nym_lookup = nym_lookup
-
-    def addIdr(self, identifier, verkey, role=None):
-        self.clients[identifier] = {VERKEY: verkey, ROLE: role}
-
-    def getVerkey(self, identifier):
-        nym = self.clients.get(identifier)
-        if not nym:
-            nym = self.nym_lookup(self.state, identifier) if self.nym_lookup else {}
-            if not nym:
-                raise UnknownIdentifier(identifier)
-        return nym.get(VERKEY)
-
-
-class GpuAuthMixin:
-    """The GPU batch machinery.  Mix in front of any NaclAuthNr-compatible
-    class -- including the reference's own plenum.server.client_authn.SimpleAuthNr
-    (INTEGRATION.md), which keeps node.py:2482's isinstance check true."""
-
-    def _gpu_init(self, engine=None, device=0, verdict_cache_size=1 << 20, key_window=8, max_keys=16384,
-                  hot_key_uses=2):
-        """key_window / max_keys: the engine's key store (comb tables in HBM,
-        edv_keys_set_window: W=8 is 512 KiB per key, so 16,384 keys = 8 GiB).
-        Verkeys given to addIdr, and keys seen in `hot_key_uses` requests, are
-        registered; their requests take the key-table path, the rest the
-        general path (same verdicts).  The authenticator owns the engine's key
-        store (it resets it on first use)."""
-        self.engine = engine
-        self._device = device
-        self._keys = VerkeyCache()
-        self._verdicts = OrderedDict()
-        self._verdict_cache_size = verdict_cache_size
-        self._key_window = key_window
-        self._max_keys = max_keys
-        self._hot_key_uses = hot_key_uses
-        self._key_ids = {}            # 32-byte key -> engine key id
-        self._key_uses = {}
-        self._keys_pending = OrderedDict()
-        self._key_store_ready = False
-        self.stats = {"batches": 0, "batch_items": 0, "cache_hits": 0, "single_verifies": 0, "keyed_items": 0,
-                      "keys_registered": 0}
-
-    def _engine(self):
-        if self.engine is None:
-            from .engine import EdVerifyEngine
-            self.engine = EdVerifyEngine(self._device)
-        return self.engine
 
     def _resolve_key(self, verkey, identifier):
         try:
             hash((verkey, identifier))
         except TypeError:
             return DidVerifier(verkey, identifier=identifier).key
-        return self._keys.resolve(verkey, identifier)
+        return self._g.keys.resolve(verkey, identifier)
 
-    # -- key-table registration (edv_keys_add) --------------------------------
+    # -- key-table registration -------------------------------------------------
     def addIdr(self, identifier, verkey, role=None):
         super().addIdr(identifier, verkey, role)
+        self._queue_key(identifier, verkey)
+
+    def _queue_key(self, identifier, verkey):
+        """addIdr'd keys take a free key-table slot at the next batch."""
         try:
             key = self._resolve_key(verkey, identifier)
         except Exception:
             return  # authenticate() raises the reference's error for this key later
-        if key and len(key) == 32 and key not in self._key_ids:
-            self._keys_pending[key] = None
+        if key and len(key) == 32:
+            g = self._g
+            g.pending[key] = None
+            while len(g.pending) > g.max_keys:
+                g.pending.popitem(last=False)
 
-    def _register_keys(self, keys):
-        eng = self._engine()
-        if not hasattr(eng, "keys_add"):
-            return
-        if not self._key_store_ready:
-            eng.keys_reset()
-            if hasattr(eng, "keys_set_window"):
-                eng.keys_set_window(self._key_window)
-            self._key_store_ready = True
-        room = self._max_keys - len(self._key_ids)
-        fresh = [k for k in OrderedDict.fromkeys(keys) if k not in self._key_ids][:max(room, 0)]
-        if not fresh:
-            return
-        import numpy as np
-        first = eng.keys_add(np.frombuffer(b"".join(fresh), np.uint8).reshape(-1, 32))
-        for i, k in enumerate(fresh):
-            self._key_ids[k] = first + i
-        self.stats["keys_registered"] += len(fresh)
+    def _key_store(self):
+        g = self._g
+        if g.max_keys <= 0:
+            return None
+        return KeyStore.attach(self._engine(), g.key_window, g.max_keys)
 
-    def _split_keyed(self, todo):
-        """Register pending and hot keys, then split items into (keyed, general)."""
-        hot = []
-        for p in todo:
-            if p.key in self._key_ids:
+    def _route(self, todo):
+        """Register waiting keys, then split items into (keyed + ids, general)."""
+        g = self._g
+        ks = self._key_store()
+        if ks is None:
+            return [], [], todo
+        batch_keys = [p.key for p in todo]
+        if g.hot:  # earned a slot: may evict least-recently-used keys not in this batch
+            got = ks.register(list(g.hot), pinned=batch_keys, evict=True)
+            g.stats["keys_registered"] += len(got)
+            g.hot.clear()
+        if g.pending:  # addIdr keys: free slots only
+            room = ks.free_slots()
+            if room > 0:
+                take = [k for k in g.pending if k not in ks][:room]
+                got = ks.register(take, evict=False)
+                g.stats["keys_registered"] += len(got)
+            g.pending.clear()  # registered, or no room: later keys get in by use (hot)
+        ids = ks.lookup(batch_keys)
+        keyed = [(p, i) for p, i in zip(todo, ids) if i is not None]
+        general = [p for p, i in zip(todo, ids) if i is None]
+        return [p for p, _ in keyed], [i for _, i in keyed], general
+
+    def _count_verified(self, items, oks):
+        """A general-path key earns a slot after hot_key_uses requests that
+        VERIFIED (bad signatures cannot push keys into the store)."""
+        g = self._g
+        if g.max_keys <= 0:
+            return
+        uses = g.key_uses
+        for p, ok in zip(items, oks):
+            if not ok:
                 continue
-            u = self._key_uses.get(p.key, 0) + 1
-            self._key_uses[p.key] = u
-            if u >= self._hot_key_uses:
-                hot.append(p.key)
-        if self._keys_pending or hot:
-            keys = list(self._keys_pending) + hot
-            self._keys_pending.clear()
-            self._register_keys(keys)
-            for k in keys:
-                self._key_uses.pop(k, None)
-        keyed = [p for p in todo if p.key in self._key_ids]
-        general = [p for p in todo if p.key not in self._key_ids]
-        return keyed, general
+            u = uses.pop(p.key, 0) + 1
+            if u >= g.hot_key_uses:
+                g.hot[p.key] = None
+            else:
+                uses[p.key] = u
+        while len(uses) > g.key_uses_max:
+            uses.popitem(last=False)
 
-    def _verify_keyed(self, items):
+    def _verify_keyed(self, items, ids):
         """crypto_sign_open(sig || ser) against registered keys: the split at
         byte 64 done on the host (nacl_wrappers.py:108), len < 64 rejects."""
         import numpy as np
         sig64, msgs, off, short = _pack_split64([p.sig for p in items], [p.ser for p in items])
-        ids = np.fromiter((self._key_ids[p.key] for p in items), np.uint32, len(items))
-        ok = self._engine().verify_batch_keyed(np.frombuffer(sig64, np.uint8).reshape(-1, 64), ids,
-                                               np.frombuffer(msgs, np.uint8), np.frombuffer(off, np.uint64))
+        ok = self._engine().verify_batch_keyed(np.frombuffer(sig64, np.uint8).reshape(-1, 64),
+                                               np.asarray(ids, np.uint32), np.frombuffer(msgs, np.uint8),
+                                               np.frombuffer(off, np.uint64))
         ok = np.asarray(ok, bool) & (np.frombuffer(short, np.uint8) == 0)
-        self.stats["keyed_items"] += len(items)
+        self._g.stats["keyed_items"] += len(items)
         return ok
 
     # -- verify-ahead cache ------------------------------------------------
@@ -306,18 +302,20 @@ class GpuAuthMixin:
         return (p.key, p.sig, p.ser)
 
     def _remember(self, p, ok):
-        self._verdicts[self._vkey(p)] = ok
-        if len(self._verdicts) > self._verdict_cache_size:
-            self._verdicts.popitem(last=False)
+        g = self._g
+        g.verdicts[self._vkey(p)] = ok
+        if len(g.verdicts) > g.verdict_cache_size:
+            g.verdicts.popitem(last=False)
 
     def _verify_prepared(self, p):
-        if not p.key:
+        if not p.key:  # nacl_wrappers.py:237-238: no key -> False
             return False
-        hit = self._verdicts.get(self._vkey(p))
+        g = self._g
+        hit = g.verdicts.get(self._vkey(p))
         if hit is not None:
-            self.stats["cache_hits"] += 1
+            g.stats["cache_hits"] += 1
             return hit
-        self.stats["single_verifies"] += 1
+        g.stats["single_verifies"] += 1
         ok = self._verify_many([p])[0]
         self._remember(p, ok)
         return ok
@@ -326,23 +324,25 @@ class GpuAuthMixin:
         """GPU launches over prepared items (crypto_sign_open semantics): items
         whose key is registered take the key-table path, the rest one general
         launch; items without a usable key are False without touching the GPU."""
+        g = self._g
         todo = [p for p in prepared if p.key]
         out = {}
-        keyed, todo = self._split_keyed(todo)
+        keyed, ids, general = self._route(todo)
         if keyed:
-            for p, v in zip(keyed, self._verify_keyed(keyed)):
+            for p, v in zip(keyed, self._verify_keyed(keyed, ids)):
                 out[id(p)] = bool(v)
-            self.stats["batches"] += 1
-            self.stats["batch_items"] += len(keyed)
-        if todo:
+            g.stats["batches"] += 1
+            g.stats["batch_items"] += len(keyed)
+        if general:
             import numpy as np
-            sm, off, pk = _pack_sm([p.sig for p in todo], [p.ser for p in todo], [p.key for p in todo])
+            sm, off, pk = _pack_sm([p.sig for p in general], [p.ser for p in general], [p.key for p in general])
             ok = self._engine().sign_open_batch(np.frombuffer(sm, np.uint8), np.frombuffer(off, np.uint64),
                                                 np.frombuffer(pk, np.uint8).reshape(-1, 32))
-            self.stats["batches"] += 1
-            self.stats["batch_items"] += len(todo)
-            for p, v in zip(todo, ok):
+            g.stats["batches"] += 1
+            g.stats["batch_items"] += len(general)
+            for p, v in zip(general, ok):
                 out[id(p)] = bool(v)
+            self._count_verified(general, ok)
         return [out.get(id(p), False) for p in prepared]
 
     # -- batch API ----------------------------------------------------------
@@ -370,17 +370,19 @@ class GpuAuthMixin:
 
     def prefetch(self, msgs):
         """Verify-ahead: batch-verify every message that gets as far as the
-        verify step, and cache the verdicts for authenticate()."""
+        verify step, and cache the verdicts for authenticate().  Returns the
+        number of distinct signatures verified."""
         prepared = []
         for msg in msgs:
             try:
                 prepared.append(self._prepare(msg))
             except Exception:
                 continue  # authenticate() will raise it again
+        verdicts = self._g.verdicts
         uniq = OrderedDict()
         for p in prepared:
             k = self._vkey(p)
-            if k not in self._verdicts and k not in uniq:
+            if k not in verdicts and k not in uniq:
                 uniq[k] = p
         items = list(uniq.values())
         for p, ok in zip(items, self._verify_many(items)):
@@ -388,7 +390,7 @@ class GpuAuthMixin:
         return len(items)
 
     def clear_verdicts(self):
-        self._verdicts.clear()
+        self._g.verdicts.clear()
 
     # -- multi-signature extension (parity unpinned) --------------------------
     def _prepare_multi(self, msg, signatures, threshold):
@@ -466,12 +468,65 @@ class GpuAuthMixin:
         return out
 
 
-class GpuAuthNr(GpuAuthMixin, SimpleAuthNr):
+class ClientAuthNr:
+    """Interface for client authenticators (client_authn.py:22-63)."""
+
+    @abstractmethod
+    def authenticate(self, msg: Dict, identifier: str = None, signature: str = None) -> str:
+        """Return the identifier or raise a SigningException subclass."""
+
+    @abstractmethod
+    def addIdr(self, identifier, verkey, role=None):
+        """Register an identifier's verification key."""
+
+    @abstractmethod
+    def getVerkey(self, identifier):
+        """Verification key of an identifier."""
+
+
+class NaclAuthNr(GpuAuthMixin, ClientAuthNr):
+    """client_authn.py:66-119 with the Ed25519 check on the GPU engine.
+    Subclasses provide addIdr / getVerkey."""
+
+    @abstractmethod
+    def addIdr(self, identifier, verkey, role=None):
+        pass
+
+    @abstractmethod
+    def getVerkey(self, identifier):
+        pass
+
+
+class SimpleAuthNr(NaclAuthNr):
+    """client_authn.py:122-154.  `state` lookups for identifiers not added with
+    addIdr go through `nym_lookup(state, identifier)` (the reference calls
+    DomainRequestHandler.getNymDetails(state, identifier, isCommitted=False),
+    domain_req_handler.py:146-155); with no lookup the state is empty."""
+
+    def __init__(self, state=None, nym_lookup=None):
+        self.clients = {}  # type: Dict[str, Dict]
+        self.state = state
+        self.nym_lookup = nym_lookup
+
+    def addIdr(self, identifier, verkey, role=None):
+        self.clients[identifier] = {VERKEY: verkey, ROLE: role}
+        self._queue_key(identifier, verkey)
+
+    def getVerkey(self, identifier):
+        nym = self.clients.get(identifier)
+        if not nym:
+            nym = self.nym_lookup(self.state, identifier) if self.nym_lookup else {}
+            if not nym:
+                raise UnknownIdentifier(identifier)
+        return nym.get(VERKEY)
+
+
+class GpuAuthNr(SimpleAuthNr):
     """Drop-in SimpleAuthNr whose Ed25519 checks run on the MI355X."""
 
-    def __init__(self, state=None, nym_lookup=None, engine=None, device=0):
+    def __init__(self, state=None, nym_lookup=None, engine=None, device=0, **options):
         SimpleAuthNr.__init__(self, state=state, nym_lookup=nym_lookup)
-        self._gpu_init(engine=engine, device=device)
+        self._gpu_init(engine=engine, device=device, **options)
 
 
 CoreAuthNr = GpuAuthNr

@@ -11,14 +11,7 @@ Both are a few MB at 16M requests; they are timed separately in bench.py.
 import torch
 import torch.distributed as dist
 
-
-def shard_bounds(n, world, rank):
-    """[lo, hi) request range of `rank`; lo is a multiple of 64."""
-    words = (n + 63) // 64
-    per = (words + world - 1) // world
-    lo = min(n, rank * per * 64)
-    hi = min(n, (rank + 1) * per * 64)
-    return lo, hi
+from .multi import shard_bounds  # noqa: F401  (64-aligned request-index shards)
 
 
 def words_per_rank(n, world):

@@ -225,11 +225,19 @@ class EdVerifyEngine:
                                             _stream_for(stream, d_pk32)))
         return first.value
 
+    def keys_set(self, first_id, pk32):
+        """Rebuild registered slots first_id.. with new keys (LRU eviction)."""
+        pk32 = _u8(pk32, 32)
+        check(self._lib.edv_keys_set(self._ctx, int(first_id), _ptr(pk32), pk32.shape[0]))
+
     def keys_count(self):
         return int(self._lib.edv_keys_count(self._ctx))
 
+    keys_generation = 0  # bumped by keys_reset: a KeyStore (keystore.py) drops its ids
+
     def keys_reset(self):
         check(self._lib.edv_keys_reset(self._ctx))
+        self.keys_generation += 1
 
     def verify_batch_keyed(self, sig64, key_idx, msgs, msg_off):
         """Verdicts against registered key ids (same predicate as verify_batch)."""
@@ -318,8 +326,10 @@ class EdVerifyEngine:
                                                 _dev(d_out32), st))
 
     # ----------------------------------------------------------------- tally
-    def tally(self, key, voter, phase, valid, n_keys, n_validators):
+    def tally(self, key, voter, phase, valid, n_keys, n_validators, primary=None):
         """Distinct-voter PREPARE/COMMIT counts and quorum flags per key.
+        primary: per-key voter index of the view's primary (0xff = none) --
+        its PREPARE never counts (replica.py:1289-1291); None = no primary.
         Returns (counts uint32[n_keys, 2], prepare_quorum bool[n_keys],
         commit_quorum bool[n_keys])."""
         key = np.ascontiguousarray(key, dtype=np.uint32)
@@ -327,18 +337,24 @@ class EdVerifyEngine:
         phase = np.ascontiguousarray(phase, dtype=np.uint8)
         valid = np.ascontiguousarray(valid, dtype=np.uint8)
         nv = key.shape[0]
+        if not (voter.shape[0] == phase.shape[0] == valid.shape[0] == nv):
+            raise ValueError("vote arrays differ in length")
+        if primary is not None:
+            primary = np.ascontiguousarray(primary, dtype=np.uint8)
+            if primary.shape[0] != n_keys:
+                raise ValueError("primary must have n_keys entries")
         counts = np.zeros((n_keys, 2), np.uint32)
         quorum = np.zeros(n_keys, np.uint8)
         if n_keys:
-            check(self._lib.edv_tally(self._ctx, _ptr(key), _ptr(voter), _ptr(phase), _ptr(valid), nv, n_keys,
-                                      n_validators, _ptr(counts), _ptr(quorum)))
+            check(self._lib.edv_tally(self._ctx, _ptr(key), _ptr(voter), _ptr(phase), _ptr(valid), _ptr(primary),
+                                      nv, n_keys, n_validators, _ptr(counts), _ptr(quorum)))
         return counts, (quorum & 1).astype(bool), (quorum & 2).astype(bool)
 
     def tally_device(self, d_key, d_voter, d_phase, d_valid, n_votes, n_keys, n_validators, d_ballot, d_counts,
-                     d_quorum, stream=None):
+                     d_quorum, stream=None, d_primary=None):
         check(self._lib.edv_tally_device(self._ctx, _dev(d_key), _dev(d_voter), _dev(d_phase), _dev(d_valid),
-                                         n_votes, n_keys, n_validators, _dev(d_ballot), _dev(d_counts),
-                                         _dev(d_quorum), _stream_for(stream, d_ballot)))
+                                         _dev(d_primary), n_votes, n_keys, n_validators, _dev(d_ballot),
+                                         _dev(d_counts), _dev(d_quorum), _stream_for(stream, d_ballot)))
 
     def tally_finish_device(self, d_ballot, n_keys, n_validators, d_counts, d_quorum, stream=None):
         check(self._lib.edv_tally_finish_device(self._ctx, _dev(d_ballot), n_keys, n_validators, _dev(d_counts),

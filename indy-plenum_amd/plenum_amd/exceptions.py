@@ -1,93 +1,76 @@
-"""The authentication exceptions of the reference, same names, codes, reasons
-and constructor behaviour (plenum/common/exceptions.py:4-9, 28-112, 115-117),
-so callers that map them (node.py:1383-1397 REQNACK via
-reasonForClientFromException node.py:2568-2571; node.py:1315 SuspiciousNode)
-see identical objects.  InsufficientSignatures / InsufficientCorrectSignatures
-belong to the authenticate_multi extension, which the reference snapshot does
-not have (parity unpinned)."""
+"""The authentication exceptions of the reference (plenum/common/exceptions.py:
+4-9, 28-117).
 
+Inside a Plenum node (the reference package importable) these names ARE the
+reference's classes, re-exported: what the drop-in raises is caught by the
+node's own handlers -- `except BaseExc` in validateNodeMsg turning a forged
+PROPAGATE into SuspiciousNode (node.py:1313-1316) and the REQNACK mapping of
+validateClientMsg (node.py:1383-1397, reasonForClientFromException
+node.py:2568-2571).  Without the reference package (standalone use, this
+repo's tests) the same names, codes, reasons and constructor behaviour are
+defined here.  InsufficientSignatures / InsufficientCorrectSignatures belong
+to the authenticate_multi extension, which the reference snapshot does not
+have (parity unpinned); they derive from SigningException either
+way."""
 
-class ReqInfo:
-    def __init__(self, identifier=None, reqId=None):
-        self.identifier = identifier
-        self.reqId = reqId
+_NAMES = ("ReqInfo", "BaseExc", "SigningException", "CouldNotAuthenticate", "MissingSignature", "EmptySignature",
+          "InvalidSignatureFormat", "InvalidSignature", "MissingIdentifier", "EmptyIdentifier",
+          "UnknownIdentifier", "InvalidIdentifier", "InvalidKey", "SuspiciousNode")
 
+try:
+    import plenum.common.exceptions as _ref
+    globals().update({name: getattr(_ref, name) for name in _NAMES})
+    REFERENCE = True
+except Exception:
+    REFERENCE = False
 
-class BaseExc(Exception):
-    def __str__(self):
-        return "{}{}".format(self.__class__.__name__, self.args)
+if not REFERENCE:
+    class ReqInfo:
+        def __init__(self, identifier=None, reqId=None):
+            self.identifier = identifier
+            self.reqId = reqId
 
+    class BaseExc(Exception):
+        def __str__(self):
+            return "{}{}".format(self.__class__.__name__, self.args)
 
-class SigningException(BaseExc):
-    pass
+    class SigningException(BaseExc):
+        pass
 
+    def _signing(name, code, reason, req_info):
+        """A SigningException subclass; with req_info its constructor takes
+        (identifier=None, reqId=None) like ReqInfo and records no args."""
+        bases = (SigningException, ReqInfo) if req_info else (SigningException,)
+        ns = {"code": code, "reason": reason, "__module__": __name__}
+        if req_info:
+            ns["__init__"] = lambda self, *a, **k: ReqInfo.__init__(self, *a, **k)
+        return type(name, bases, ns)
 
-class CouldNotAuthenticate(SigningException, ReqInfo):
-    code = 110
-    reason = 'could not authenticate'
+    CouldNotAuthenticate = _signing("CouldNotAuthenticate", 110, 'could not authenticate', True)
+    MissingSignature = _signing("MissingSignature", 120, 'missing signature', False)
+    EmptySignature = _signing("EmptySignature", 121, 'empty signature', True)
+    InvalidSignatureFormat = _signing("InvalidSignatureFormat", 123, 'invalid signature format', True)
+    InvalidSignature = _signing("InvalidSignature", 125, 'invalid signature', True)
+    MissingIdentifier = _signing("MissingIdentifier", 130, 'missing identifier', False)
+    EmptyIdentifier = _signing("EmptyIdentifier", 131, 'empty identifier', False)
+    UnknownIdentifier = _signing("UnknownIdentifier", 133, 'unknown identifier', True)
+    InvalidIdentifier = _signing("InvalidIdentifier", 135, 'invalid identifier', True)
 
-    def __init__(self, *args, **kwargs):
-        ReqInfo.__init__(self, *args, **kwargs)
+    class InvalidKey(Exception):
+        code = 142
+        reason = 'invalid key'
 
+    class SuspiciousNode(BaseExc):
+        """node.py:1315 wraps an authentication failure of a node message:
+        SuspiciousNode(frm, ex, msg) (exceptions.py:120-131; `suspicion` is the
+        caught exception there, so code/reason come from it when present)."""
 
-class MissingSignature(SigningException):
-    code = 120
-    reason = 'missing signature'
-
-
-class EmptySignature(SigningException, ReqInfo):
-    code = 121
-    reason = 'empty signature'
-
-    def __init__(self, *args, **kwargs):
-        ReqInfo.__init__(self, *args, **kwargs)
-
-
-class InvalidSignatureFormat(SigningException, ReqInfo):
-    code = 123
-    reason = 'invalid signature format'
-
-    def __init__(self, *args, **kwargs):
-        ReqInfo.__init__(self, *args, **kwargs)
-
-
-class InvalidSignature(SigningException, ReqInfo):
-    code = 125
-    reason = 'invalid signature'
-
-    def __init__(self, *args, **kwargs):
-        ReqInfo.__init__(self, *args, **kwargs)
-
-
-class MissingIdentifier(SigningException):
-    code = 130
-    reason = 'missing identifier'
-
-
-class EmptyIdentifier(SigningException):
-    code = 131
-    reason = 'empty identifier'
-
-
-class UnknownIdentifier(SigningException, ReqInfo):
-    code = 133
-    reason = 'unknown identifier'
-
-    def __init__(self, *args, **kwargs):
-        ReqInfo.__init__(self, *args, **kwargs)
-
-
-class InvalidIdentifier(SigningException, ReqInfo):
-    code = 135
-    reason = 'invalid identifier'
-
-    def __init__(self, *args, **kwargs):
-        ReqInfo.__init__(self, *args, **kwargs)
-
-
-class InvalidKey(Exception):
-    code = 142
-    reason = 'invalid key'
+        def __init__(self, node, suspicion, offendingMsg):
+            node = node.decode() if isinstance(node, bytes) else node
+            self.code = getattr(suspicion, "code", None) if suspicion else None
+            self.reason = getattr(suspicion, "reason", None) if suspicion else None
+            self.node = node.split(":", 1)[0]
+            self.offendingMsg = offendingMsg
 
 
 # --- authenticate_multi extension (not in the reference snapshot) ----------
@@ -109,14 +92,11 @@ class InsufficientCorrectSignatures(SigningException):
 
 def friendlyEx(ex):
     """plenum/common/util.py:354-365: exception text with its __cause__ chain."""
-    cur, friendly, end = ex, "", ""
-    while cur:
-        if len(friendly):
-            friendly += " [caused by "
-            end += "]"
-        friendly += "{}".format(cur)
-        cur = cur.__cause__
-    return friendly + end
+    parts = []
+    while ex:
+        parts.append("{}".format(ex))
+        ex = ex.__cause__
+    return " [caused by ".join(parts) + "]" * (len(parts) - 1)
 
 
 def reasonForClientFromException(ex):

@@ -1,0 +1,143 @@
+"""The registered-key store of one engine, shared by every authenticator that
+uses the engine.
+
+The key-table path (edv_keys_add / edv_verify_batch_keyed) verifies a request
+against a key id; the id -> key binding lives in the engine's HBM.  One
+KeyStore object per engine owns that binding, so two authenticators sharing an
+engine (e.g. under ReqAuthenticator) can never see each other's ids point at
+different keys.  The engine's keys_generation (bumped by every keys_reset)
+is checked on each use: a reset by anyone else empties the map instead of
+leaving stale ids.
+
+Capacity is bounded (max_keys tables at the chosen comb window); once full,
+least-recently-used keys are evicted in place (edv_keys_set rebuilds a slot),
+never a key the current batch is using.  Which keys get in is the caller's
+policy (client_authn.GpuAuthMixin): keys given to addIdr while there is free
+room, and keys that verified successfully hot_key_uses times.  A key whose
+registration fails (allocation, HIP error) is remembered as unregistrable and
+its requests keep taking the general path, which gives the same verdicts.
+"""
+from collections import OrderedDict
+
+import numpy as np
+
+# comb windows the library builds (edverify.h edv_keys_set_window)
+WINDOWS = (4, 6, 8, 10, 12, 13, 14, 16)
+
+
+def key_rows(w):
+    return (254 + w - 1) // w
+
+
+def key_table_bytes(w):
+    """HBM per registered key at window w: rows x 2^(w-1) entries x 128 B."""
+    return key_rows(w) * (1 << (w - 1)) * 128
+
+
+def auto_window(max_keys, budget_bytes):
+    """Widest window whose max_keys tables fit in budget_bytes (>= 4)."""
+    best = WINDOWS[0]
+    for w in WINDOWS:
+        if key_table_bytes(w) * max_keys <= budget_bytes:
+            best = w
+    return best
+
+
+class KeyStore:
+    def __init__(self, engine, window, capacity):
+        self.engine = engine
+        self.window = window
+        self.capacity = capacity
+        self._ids = OrderedDict()     # key bytes -> id, LRU order (oldest first)
+        self._slot_key = []           # id -> key bytes
+        self._failed = OrderedDict()  # keys that could not be registered
+        self._generation = None
+
+    @classmethod
+    def attach(cls, engine, window, capacity):
+        """The engine's store (created by the first caller, whose window and
+        capacity it keeps); None if the engine has no key-table path."""
+        if not hasattr(engine, "keys_add"):
+            return None
+        ks = getattr(engine, "_edv_key_store", None)
+        if ks is None:
+            ks = cls(engine, window, capacity)
+            engine._edv_key_store = ks
+        return ks
+
+    def _sync(self):
+        gen = getattr(self.engine, "keys_generation", 0)
+        if self._generation == gen:
+            return
+        # first use, or someone reset the engine's store: start from empty
+        self.engine.keys_reset()
+        if hasattr(self.engine, "keys_set_window"):
+            self.engine.keys_set_window(self.window)
+        self._ids.clear()
+        self._slot_key = []
+        self._generation = getattr(self.engine, "keys_generation", 0)
+
+    def __len__(self):
+        return len(self._ids)
+
+    def __contains__(self, key):
+        return key in self._ids and self._generation == getattr(self.engine, "keys_generation", 0)
+
+    def free_slots(self):
+        self._sync()
+        return self.capacity - len(self._ids)
+
+    def lookup(self, keys):
+        """Ids of keys (None for unregistered), marking them recently used."""
+        self._sync()
+        out = []
+        for k in keys:
+            i = self._ids.get(k)
+            if i is not None:
+                self._ids.move_to_end(k)
+            out.append(i)
+        return out
+
+    def register(self, keys, pinned=(), evict=True):
+        """Register keys not yet in the store: into free slots, then (evict)
+        over least-recently-used keys outside `pinned`.  Returns the keys
+        registered."""
+        self._sync()
+        fresh = [k for k in OrderedDict.fromkeys(keys) if k not in self._ids and k not in self._failed]
+        if not fresh:
+            return []
+        room = max(self.capacity - len(self._ids), 0)
+        new, over = fresh[:room], fresh[room:]
+        done = []
+        if new:
+            try:
+                first = self.engine.keys_add(np.frombuffer(b"".join(new), np.uint8).reshape(-1, 32))
+            except Exception:
+                self._fail(new)
+                new = []
+            for j, k in enumerate(new):
+                self._ids[k] = first + j
+                self._slot_key.append(k)
+            done += new
+        if over and evict and hasattr(self.engine, "keys_set"):
+            pinned = set(pinned)
+            victims = [k for k in self._ids if k not in pinned][:len(over)]
+            for k_new, k_old in zip(over, victims):
+                slot = self._ids.pop(k_old)
+                try:
+                    self.engine.keys_set(slot, np.frombuffer(k_new, np.uint8).reshape(1, 32))
+                except Exception:
+                    # the slot's old table may be half rewritten: retire the slot
+                    self._slot_key[slot] = None
+                    self._fail([k_new])
+                    continue
+                self._slot_key[slot] = k_new
+                self._ids[k_new] = slot
+                done.append(k_new)
+        return done
+
+    def _fail(self, keys):
+        for k in keys:
+            self._failed[k] = None
+        while len(self._failed) > 65536:
+            self._failed.popitem(last=False)

@@ -1,0 +1,126 @@
+"""MultiEngine: every GPU of the box behind one engine object, inside one
+process.
+
+A Plenum node is one asyncio process (stp_core/loop/looper.py:141-151), so the
+drop-in authenticator cannot use the one-process-per-GPU torch.distributed
+layout bench.py uses.  MultiEngine holds one EdVerifyEngine (one HIP context
+and stream) per device and splits each batch by contiguous request index,
+shard bounds multiples of 64 (dist.shard_bounds -- the same partition the
+RCCL path uses).  The shards run concurrently: one host
+thread per device, and the ctypes calls release the GIL while the device
+works.  Verdicts are concatenated in request order, so the result is the
+single-engine result exactly.
+
+The key store is replicated: keys_add / keys_set register the same keys on
+every device (the same ids everywhere), so a keyed shard can run on any GPU.
+"""
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+from .engine import _u8
+
+
+def shard_bounds(n, world, rank):
+    """[lo, hi) request range of `rank`; lo is a multiple of 64 (dist.py)."""
+    words = (n + 63) // 64
+    per = (words + world - 1) // world
+    return min(n, rank * per * 64), min(n, (rank + 1) * per * 64)
+
+
+class MultiEngine:
+    def __init__(self, devices=None, engines=None, min_shard=4096):
+        """devices: device indices ("all" / None = every visible device);
+        engines: ready engines (e.g. test doubles) instead.  Batches smaller
+        than min_shard per device use fewer devices."""
+        if engines is None:
+            from . import _lib
+            from .engine import EdVerifyEngine
+            if devices in (None, "all"):
+                devices = range(_lib.load().edv_device_count())
+            engines = [EdVerifyEngine(d) for d in devices]
+        if not engines:
+            raise ValueError("no engines")
+        self.engines = list(engines)
+        self.min_shard = min_shard
+        self._pool = ThreadPoolExecutor(max_workers=len(self.engines)) if len(self.engines) > 1 else None
+        self.keys_generation = 0
+
+    def __len__(self):
+        return len(self.engines)
+
+    def close(self):
+        if self._pool:
+            self._pool.shutdown()
+        for e in self.engines:
+            if hasattr(e, "close"):
+                e.close()
+
+    # ------------------------------------------------------------ sharding
+    def _shards(self, n):
+        world = max(1, min(len(self.engines), -(-n // self.min_shard)))
+        return [shard_bounds(n, world, r) for r in range(world)]
+
+    def _run(self, n, call):
+        """call(engine, lo, hi) -> bool array for [lo, hi); results concatenated."""
+        shards = [(e, lo, hi) for e, (lo, hi) in zip(self.engines, self._shards(n)) if hi > lo]
+        if len(shards) <= 1 or self._pool is None:
+            parts = [call(e, lo, hi) for e, lo, hi in shards]
+        else:
+            futs = [self._pool.submit(call, e, lo, hi) for e, lo, hi in shards]
+            parts = [f.result() for f in futs]
+        if not parts:
+            return np.zeros(0, bool)
+        return np.concatenate([np.asarray(p, bool) for p in parts])
+
+    # -------------------------------------------------------------- verify
+    def verify_batch(self, sig64, pk32, msgs, msg_off):
+        sig64, pk32, msgs = _u8(sig64, 64), _u8(pk32, 32), _u8(msgs)
+        off = np.ascontiguousarray(msg_off, dtype=np.uint64)
+        return self._run(sig64.shape[0], lambda e, lo, hi: e.verify_batch(sig64[lo:hi], pk32[lo:hi], msgs,
+                                                                          off[lo:hi + 1]))
+
+    def sign_open_batch(self, sm, sm_off, pk32):
+        sm, pk32 = _u8(sm), _u8(pk32, 32)
+        off = np.ascontiguousarray(sm_off, dtype=np.uint64)
+        return self._run(pk32.shape[0], lambda e, lo, hi: e.sign_open_batch(sm, off[lo:hi + 1], pk32[lo:hi]))
+
+    def verify_batch_keyed(self, sig64, key_idx, msgs, msg_off):
+        sig64, msgs = _u8(sig64, 64), _u8(msgs)
+        kidx = np.ascontiguousarray(key_idx, dtype=np.uint32)
+        off = np.ascontiguousarray(msg_off, dtype=np.uint64)
+        return self._run(sig64.shape[0], lambda e, lo, hi: e.verify_batch_keyed(sig64[lo:hi], kidx[lo:hi], msgs,
+                                                                                off[lo:hi + 1]))
+
+    # ---------------------------------------------------- replicated key store
+    def keys_reset(self):
+        for e in self.engines:
+            e.keys_reset()
+        self.keys_generation += 1
+
+    def keys_set_window(self, w):
+        for e in self.engines:
+            e.keys_set_window(w)
+
+    def keys_add(self, pk32):
+        firsts = {e.keys_add(pk32) for e in self.engines}
+        if len(firsts) != 1:
+            raise RuntimeError("key stores of the devices diverged (first ids %s)" % sorted(firsts))
+        return firsts.pop()
+
+    def keys_set(self, first_id, pk32):
+        for e in self.engines:
+            e.keys_set(first_id, pk32)
+
+    def keys_count(self):
+        return self.engines[0].keys_count()
+
+    # ----------------------------------------------------- one-device helpers
+    def tally(self, *a, **k):
+        return self.engines[0].tally(*a, **k)
+
+    def seed_keypair_batch(self, seeds32):
+        return self.engines[0].seed_keypair_batch(seeds32)
+
+    def sign_batch(self, sk64, key_idx, msgs, msg_off):
+        return self.engines[0].sign_batch(sk64, key_idx, msgs, msg_off)

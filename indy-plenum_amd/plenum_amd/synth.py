@@ -105,3 +105,40 @@ def add_torsion(r_enc):
         return r_enc
     x, y = _add(R, _decode(_T8_ENC))
     return (y | ((x & 1) << 255)).to_bytes(32, "little")
+
+
+def corrupt_configs2(sig, pk, msgs, off, rng):
+    """configs[2] in place on host arrays: 10% rejects, split equally over bit
+    flips in R/S/M, S+L, S|2^255, small-order A, non-canonical A, R =
+    identity, R + T8.  Returns the expected verdicts."""
+    n = sig.shape[0]
+    bad = rng.choice(n, size=n // 10, replace=False)
+    kinds = bad % 9
+    L = 2**252 + 27742317777372353535851937790883648493
+    small_A = bytes.fromhex("26e8958fc2b227b045c3f489f2ef98f0d5dfac05d3c63339b13802886d53fc05")
+    noncanon_A = (2**255 - 19 + 3).to_bytes(32, "little")
+    ident = (1).to_bytes(32, "little")
+    for i, k in zip(bad, kinds):
+        if k == 0:
+            sig[i, rng.integers(0, 32)] ^= 1 << int(rng.integers(0, 8))
+        elif k == 1:
+            sig[i, 32 + rng.integers(0, 31)] ^= 1 << int(rng.integers(0, 8))
+        elif k == 2:
+            a, b = int(off[i]), int(off[i + 1])
+            msgs[a + int(rng.integers(0, b - a))] ^= 1 << int(rng.integers(0, 8))
+        elif k == 3:
+            s = int.from_bytes(sig[i, 32:].tobytes(), "little") + L
+            sig[i, 32:] = np.frombuffer(s.to_bytes(32, "little"), np.uint8)
+        elif k == 4:
+            sig[i, 63] |= 0x80
+        elif k == 5:
+            pk[i] = np.frombuffer(small_A, np.uint8)
+        elif k == 6:
+            pk[i] = np.frombuffer(noncanon_A, np.uint8)
+        elif k == 7:
+            sig[i, :32] = np.frombuffer(ident, np.uint8)
+        else:
+            sig[i, :32] = np.frombuffer(add_torsion(sig[i, :32].tobytes()), np.uint8)
+    expect = np.ones(n, dtype=bool)
+    expect[bad] = False
+    return expect

@@ -57,55 +57,7 @@ def items_of(d):
              bool(d["expect"][i])) for i in range(len(d["expect"]))]
 
 
-class OracleEngine:
-    """CPU test double with EdVerifyEngine's verify interface, answering with
-    the C oracle.  Used ONLY to test host-side logic (check order, exception
-    mapping, batching, sharding) without a GPU; the product has no CPU path."""
-
-    def __init__(self, lib):
-        self.lib = lib
-        self.calls = 0
-        self.keys = []
-        self.window = 10
-
-    def keys_reset(self):
-        self.keys = []
-
-    def keys_set_window(self, w):
-        assert not self.keys
-        self.window = w
-
-    def keys_add(self, pk32):
-        first = len(self.keys)
-        self.keys.extend(bytes(r) for r in np.asarray(pk32, np.uint8).reshape(-1, 32))
-        return first
-
-    def verify_batch_keyed(self, sig64, key_idx, msgs, msg_off):
-        self.calls += 1
-        pk = np.frombuffer(b"".join(self.keys[int(k)] if int(k) < len(self.keys) else b"\0" * 32
-                                    for k in key_idx), np.uint8).reshape(-1, 32)
-        ok = self.verify_batch(sig64, pk, msgs, msg_off)
-        self.calls -= 1
-        return ok & np.array([int(k) < len(self.keys) for k in key_idx], bool)
-
-    def sign_open_batch(self, sm, sm_off, pk32):
-        self.calls += 1
-        sm = bytes(sm) if not isinstance(sm, np.ndarray) else sm.tobytes()
-        pk32 = np.asarray(pk32, dtype=np.uint8).reshape(-1, 32) if not isinstance(pk32, list) else \
-            np.frombuffer(b"".join(pk32), np.uint8).reshape(-1, 32)
-        off = [int(x) for x in sm_off]
-        return np.array([self.lib.oracle_sign_open(sm[off[i]:off[i + 1]], off[i + 1] - off[i], pk32[i].tobytes()) == 0
-                         for i in range(len(off) - 1)], dtype=bool)
-
-    def verify_batch(self, sig64, pk32, msgs, msg_off):
-        self.calls += 1
-        msgs = bytes(msgs) if not isinstance(msgs, np.ndarray) else msgs.tobytes()
-        sig64 = np.asarray(sig64, np.uint8).reshape(-1, 64)
-        pk32 = np.asarray(pk32, np.uint8).reshape(-1, 32)
-        off = [int(x) for x in msg_off]
-        return np.array([self.lib.oracle_verify_detached(sig64[i].tobytes(), msgs[off[i]:off[i + 1]],
-                                                         off[i + 1] - off[i], pk32[i].tobytes()) == 0
-                         for i in range(len(off) - 1)], dtype=bool)
+from engine_double import OracleEngine  # noqa: E402
 
 
 @pytest.fixture

@@ -9,134 +9,23 @@ What is imported and run for real: common/serializers/signing_serializer.py,
 common/serializers/serialization.py, plenum/common/exceptions.py,
 plenum/common/verifier.py, plenum/server/client_authn.py,
 stp_core/crypto/nacl_wrappers.py.  Third-party packages the reference needs
-that are not installed here are replaced by minimal stand-ins defined below
-(written for this generator, not copied from anywhere):
-  libnacl          -> ctypes over libsodium 1.0.18 (/opt/conda/lib/libsodium.so.23)
-  base58           -> the 0.2.4 API (b58encode -> str, b58decode -> bytes)
-  stp_core.common.log, ioflo -> logging stubs (log output only)
-  plenum.common.jsonpickle_util -> no-op setUpJsonpickle (jsonpickle absent)
-  plenum.server.domain_req_handler -> getNymDetails returns {} (empty state),
-      because the real module imports plenum/common/util.py, a SyntaxError on
-      Python >= 3.7 (util.py:337 `asyncio.async`).
-Outputs (pure data, committed): serializer_kat.json, authn_kat.json,
-quorums_kat.json.
+that are not installed here are replaced by the stand-ins of ref_standins.py
+(libnacl over libsodium 1.0.18, the base58 0.2.4 API, logging stubs, and a
+domain_req_handler whose getNymDetails answers from an empty state).
+Outputs (pure data, committed): serializer_kat.json, authn_kat.json.  The
+quorum / vote-set fixture is gen_ref_quorums.py.
 """
-import ctypes
 import json
 import os
 import sys
-import types
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-REF = "/root/reference"
+sys.path.insert(0, HERE)
+import ref_standins as R  # noqa: E402
 
-# ------------------------------------------------------------------ stand-ins
-_sodium = ctypes.CDLL("/opt/conda/lib/libsodium.so.23")
-_sodium.sodium_init()
-
-libnacl = types.ModuleType("libnacl")
-libnacl.crypto_sign_PUBLICKEYBYTES = 32
-libnacl.crypto_sign_SECRETKEYBYTES = 64
-libnacl.crypto_sign_BYTES = 64
-libnacl.crypto_box_PUBLICKEYBYTES = 32
-libnacl.crypto_box_SECRETKEYBYTES = 32
-libnacl.crypto_box_NONCEBYTES = 24
-libnacl.crypto_sign_SEEDBYTES = 32
-
-
-def _unused(*a, **k):
-    raise NotImplementedError("not needed for signature verification")
-
-
-libnacl.crypto_box_afternm = libnacl.crypto_box_beforenm = _unused
-libnacl.crypto_box_open_afternm = libnacl.crypto_scalarmult_base = _unused
-
-
-def _crypto_sign_open(sm, pk):
-    m = ctypes.create_string_buffer(len(sm) + 1)
-    mlen = ctypes.c_ulonglong()
-    if _sodium.crypto_sign_open(m, ctypes.byref(mlen), sm, ctypes.c_ulonglong(len(sm)), pk):
-        raise ValueError("Failed to validate message")
-    return m.raw[:mlen.value]
-
-
-def _crypto_sign_seed_keypair(seed):
-    pk = ctypes.create_string_buffer(32)
-    sk = ctypes.create_string_buffer(64)
-    _sodium.crypto_sign_seed_keypair(pk, sk, seed)
-    return pk.raw, sk.raw
-
-
-def _crypto_sign(msg, sk):
-    sm = ctypes.create_string_buffer(len(msg) + 64)
-    smlen = ctypes.c_ulonglong()
-    _sodium.crypto_sign(sm, ctypes.byref(smlen), msg, ctypes.c_ulonglong(len(msg)), sk)
-    return sm.raw[:smlen.value]
-
-
-libnacl.crypto_sign_open = _crypto_sign_open
-libnacl.crypto_sign_seed_keypair = _crypto_sign_seed_keypair
-libnacl.crypto_sign = _crypto_sign
-libnacl.randombytes = lambda n: os.urandom(n)
-libnacl.crypto_box_keypair = lambda: (None, None)
-sys.modules["libnacl"] = libnacl
-sys.modules["libnacl.secret"] = types.ModuleType("libnacl.secret")
-libnacl.secret = sys.modules["libnacl.secret"]
-
-base58 = types.ModuleType("base58")
-_ALPH = "123456789ABCDEFGHJKLMNPQRSTUVWXYZabcdefghijkmnopqrstuvwxyz"
-
-
-def _b58encode(v):
-    if not isinstance(v, bytes):
-        raise TypeError("a bytes-like object is required")
-    nz = len(v) - len(v.lstrip(b"\0"))
-    acc, out = int.from_bytes(v, "big"), ""
-    while acc:
-        acc, r = divmod(acc, 58)
-        out = _ALPH[r] + out
-    return _ALPH[0] * nz + out
-
-
-def _b58decode(v):
-    if not isinstance(v, str):
-        v = v.decode("ascii")
-    nz = len(v) - len(v.lstrip(_ALPH[0]))
-    acc = 0
-    for c in v[nz:]:
-        acc = acc * 58 + _ALPH.index(c)
-    return b"\0" * nz + (acc.to_bytes((acc.bit_length() + 7) // 8, "big") if acc else b"")
-
-
-base58.b58encode, base58.b58decode, base58.alphabet = _b58encode, _b58decode, _ALPH
-sys.modules["base58"] = base58
-
-import logging  # noqa: E402
-
-log_mod = types.ModuleType("stp_core.common.log")
-log_mod.getlogger = lambda name=None: logging.getLogger("ref")
-sys.modules["stp_core.common.log"] = log_mod
-drh = types.ModuleType("plenum.server.domain_req_handler")
-
-
-class DomainRequestHandler:
-    @staticmethod
-    def getNymDetails(state, nym, isCommitted=True):
-        return {}
-
-
-drh.DomainRequestHandler = DomainRequestHandler
-sys.modules["plenum.server.domain_req_handler"] = drh
-# plenum/__init__.py only registers jsonpickle handlers (jsonpickle not installed)
-jp = types.ModuleType("plenum.common.jsonpickle_util")
-jp.setUpJsonpickle = lambda: None
-sys.modules["plenum.common.jsonpickle_util"] = jp
-
-sys.path.insert(0, REF)
-import stp_core.common  # noqa: E402,F401  (package __init__ only)
-
-stp_core_common = sys.modules["stp_core.common"]
-stp_core_common.log = log_mod
+R.install()
+_b58encode, _b58decode = R.b58encode, R.b58decode
+_crypto_sign_seed_keypair, _crypto_sign = R.crypto_sign_seed_keypair, R.crypto_sign
 
 from common.serializers.serialization import serialize_msg_for_signing  # noqa: E402
 from plenum.server.client_authn import SimpleAuthNr  # noqa: E402

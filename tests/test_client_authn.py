@@ -11,6 +11,7 @@ import os
 import pytest
 
 from conftest import GOLDEN
+from engine_double import OracleEngine
 from plenum_amd import exceptions as X
 from plenum_amd.client_authn import GpuAuthNr, ReqAuthenticator, SimpleAuthNr
 from plenum_amd.verifier import DidVerifier
@@ -188,8 +189,7 @@ def test_req_authenticator(oracle_engine):
 def _outcomes(engine, max_keys):
     out, keyed = [], 0
     for c in kat()["cases"]:
-        a = GpuAuthNr(engine=engine)
-        a._max_keys = max_keys
+        a = GpuAuthNr(engine=engine, max_keys=max_keys)
         if c["register"]:
             a.addIdr(c["msg"].get("identifier") if c["identifier"] is None else c["identifier"], c["verkey"])
         r = run_single(a, c)
@@ -199,20 +199,95 @@ def _outcomes(engine, max_keys):
     return out, keyed
 
 
-def test_keyed_and_general_paths_agree(oracle_engine):
+def test_keyed_and_general_paths_agree(oracle):
     """addIdr registers verkeys in the engine's key store (key-table path);
-    with no room (max_keys = 0) the same requests take the general path. The
+    with no store (max_keys = 0) the same requests take the general path. The
     reference KAT outcomes (incl. 63/65-byte signatures split at byte 64 on
     the host for the keyed path) are identical either way."""
-    with_keys, n_keyed = _outcomes(oracle_engine, 16)
-    without, n_general = _outcomes(oracle_engine, 0)
+    with_keys, n_keyed = _outcomes(OracleEngine(oracle), 16)
+    without, n_general = _outcomes(OracleEngine(oracle), 0)
     assert with_keys == without
     assert n_keyed > 0 and n_general == 0
 
 
-def test_hot_keys_get_registered(oracle_engine):
-    good = next(c for c in kat()["cases"] if c["name"] == "valid-abbreviated-verkey")
-    a = GpuAuthNr(engine=oracle_engine, nym_lookup=lambda st, idr: {"verkey": good["verkey"]})
-    msgs = [dict(good["msg"]) for _ in range(4)]
-    assert a.authenticate_batch(msgs) == [good["msg"]["identifier"]] * 4
+def _signed(n_signers, n_msgs, seed=1):
+    """n_msgs NYM-like requests from n_signers libsodium keys: (idrs, verkeys, msgs)."""
+    import ctypes
+    from plenum_amd.base58 import b58encode
+    from plenum_amd.serialization import serialize_msg_for_signing
+    from conftest import sodium
+    s = sodium()
+    if s is None:
+        pytest.skip("needs libsodium to sign")
+    keys = []
+    for i in range(n_signers):
+        pk, sk = ctypes.create_string_buffer(32), ctypes.create_string_buffer(64)
+        s.crypto_sign_seed_keypair(pk, sk, bytes([seed, i + 1]) + b"\0" * 30)
+        keys.append((b58encode(pk.raw[:16]), "~" + b58encode(pk.raw[16:]), sk))
+    msgs = []
+    for j in range(n_msgs):
+        idr, _, sk = keys[j % n_signers]
+        m = {"identifier": idr, "reqId": 1000 + j, "operation": {"type": "1", "dest": "d%d" % j}}
+        ser = serialize_msg_for_signing(m, topLevelKeysToIgnore=["signature"])
+        sig = ctypes.create_string_buffer(64)
+        s.crypto_sign_detached(sig, None, ser, ctypes.c_ulonglong(len(ser)), sk)
+        msgs.append(dict(m, signature=b58encode(sig.raw)))
+    return [k[0] for k in keys], [k[1] for k in keys], msgs
+
+
+def test_hot_keys_get_registered_after_verifying(oracle_engine):
+    idrs, vks, msgs = _signed(1, 8)
+    a = GpuAuthNr(engine=oracle_engine, nym_lookup=lambda st, idr: {"verkey": vks[0]})
+    assert a.authenticate_batch(msgs[:4]) == [idrs[0]] * 4      # general path, 4 verified uses
+    assert len(a._g.hot) == 1 and a.stats["keyed_items"] == 0   # earned a slot
+    assert a.authenticate_batch(msgs[4:]) == [idrs[0]] * 4      # registered, now keyed
     assert a.stats["keys_registered"] == 1 and a.stats["keyed_items"] == 4
+
+
+def test_bad_signatures_do_not_promote_keys(oracle_engine):
+    idrs, vks, msgs = _signed(1, 6)
+    a = GpuAuthNr(engine=oracle_engine, nym_lookup=lambda st, idr: {"verkey": vks[0]})
+    forged = [dict(m, reqId=m["reqId"] + 1) for m in msgs]
+    for _ in range(3):
+        assert all(isinstance(r, X.InvalidSignature) for r in a.authenticate_batch(forged))
+    assert a.stats["keys_registered"] == 0 and len(a._g.hot) == 0
+
+
+def test_two_authenticators_share_one_engine(oracle_engine):
+    """ids of one authenticator must never point at another's keys."""
+    idrs, vks, msgs = _signed(2, 4)
+    a, b = GpuAuthNr(engine=oracle_engine), GpuAuthNr(engine=oracle_engine)
+    a.addIdr(idrs[0], vks[0])
+    b.addIdr(idrs[1], vks[1])
+    assert a.authenticate_batch([msgs[0], msgs[2]]) == [idrs[0]] * 2
+    assert b.authenticate_batch([msgs[1], msgs[3]]) == [idrs[1]] * 2
+    assert a.authenticate_batch([msgs[0], msgs[2]]) == [idrs[0]] * 2   # a's id still bound to a's key
+    assert a.stats["keyed_items"] == 4 and b.stats["keyed_items"] == 2
+    # b's identity cannot authenticate through a (a has no NYM for it)
+    r = a.authenticate_batch([msgs[1]])[0]
+    assert isinstance(r, X.UnknownIdentifier)
+    # a reset of the engine's store by anyone: ids are dropped, verdicts stay right
+    oracle_engine.keys_reset()
+    assert b.authenticate_batch([msgs[1]]) == [idrs[1]]
+
+
+def test_key_store_lru_eviction(oracle_engine):
+    idrs, vks, msgs = _signed(3, 30)
+    table = dict(zip(idrs, vks))
+    a = GpuAuthNr(engine=oracle_engine, nym_lookup=lambda st, idr: {"verkey": table[idr]}, max_keys=2,
+                  hot_key_uses=1)
+    for k in range(0, 30, 3):  # one signer per batch, cycling over 3 signers with room for 2
+        s = (k // 3) % 3
+        assert a.authenticate_batch([msgs[k + s]] * 2) == [idrs[s]] * 2
+    assert len(oracle_engine.keys) == 2 and a.stats["keys_registered"] >= 3
+    assert a.stats["keyed_items"] > 0
+
+
+def test_registration_failure_falls_back_to_general(oracle_engine):
+    idrs, vks, msgs = _signed(1, 6)
+    oracle_engine.fail_keys_add = True
+    a = GpuAuthNr(engine=oracle_engine)
+    a.addIdr(idrs[0], vks[0])
+    assert a.authenticate_batch(msgs[:3]) == [idrs[0]] * 3
+    assert a.authenticate_batch(msgs[3:]) == [idrs[0]] * 3
+    assert a.stats["keyed_items"] == 0 and a.stats["keys_registered"] == 0

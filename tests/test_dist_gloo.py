@@ -33,7 +33,7 @@ def _worker(rank, world, port, q):
     sys.path.insert(0, os.path.join(ROOT, "indy-plenum_amd"))
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from plenum_amd.dist import gather_bitmask, shard_bounds, union_ballots
-    from plenum_amd.tally import ballots_from_votes
+    from tally_oracle import ballots_from_votes
     import tally_oracle
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)

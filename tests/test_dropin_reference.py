@@ -1,0 +1,35 @@
+"""The drop-in against the REAL reference classes: tests/golden/check_dropin_ref.py
+mixes GpuAuthMixin in front of /root/reference's own SimpleAuthNr (Python 3.9,
+ref_standins.py) over the oracle-backed engine double and asserts the KAT
+outcomes, engine-only verification (0 libsodium calls), the reference's
+BaseExc / SuspiciousNode for a forged PROPAGATE (node.py:1313-1316), and 0
+engine calls for authenticate() after prefetch().  Runs in the container that
+holds the reference (CPU); the committed dropin_ref_check.json is the record."""
+import json
+import os
+import subprocess
+
+import pytest
+
+from conftest import GOLDEN, ROOT
+
+PY39 = "/opt/conda/bin/python3.9"
+
+
+@pytest.mark.skipif(not (os.path.exists(PY39) and os.path.isdir("/root/reference/plenum")),
+                    reason="needs the reference tree and Python 3.9 (container only)")
+def test_mixin_over_reference_simpleauthnr():
+    out = subprocess.run([PY39, os.path.join(GOLDEN, "check_dropin_ref.py")], cwd=ROOT, capture_output=True,
+                         text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    got = json.loads(out.stdout.strip().splitlines()[-1])
+    assert got["ok"] and got["libsodium_crypto_sign_open_calls"] == 0 and got["engine_calls"] > 0
+    assert got["raised"] == got["raised_reference_baseexc"] > 0
+    assert got["authenticate_after_prefetch_engine_calls"] == 0
+
+
+def test_committed_record():
+    rec = json.load(open(os.path.join(GOLDEN, "dropin_ref_check.json")))
+    assert rec["ok"] and rec["matched"] == rec["cases"] == 50
+    assert rec["libsodium_crypto_sign_open_calls"] == 0
+    assert rec["forged_propagate"].startswith("SuspiciousNode")

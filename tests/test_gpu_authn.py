@@ -1,6 +1,7 @@
 """The drop-in authenticator on the real GPU engine: the reference KAT table
 (tests/golden/authn_kat.json from the reference's own NaclAuthNr) and batch
 == single, with no CPU verification anywhere on the path."""
+import numpy as np
 import pytest
 
 import test_client_authn as T
@@ -50,3 +51,102 @@ def test_keyed_and_general_paths_agree_on_gpu(gpu_engine):
             assert r == c["result"], c["name"]
         else:
             assert r[0] == c["raises"], c["name"]
+
+
+class _Counting:
+    """Pass-through engine proxy counting verify launches."""
+
+    def __init__(self, eng):
+        self.eng = eng
+        self.launches = 0
+
+    def __getattr__(self, name):
+        attr = getattr(self.eng, name)
+        if name in ("verify_batch", "verify_batch_keyed", "sign_open_batch"):
+            def counted(*a, **k):
+                self.launches += 1
+                return attr(*a, **k)
+            return counted
+        return attr
+
+
+def _drain(gpu_engine, n_req=100, n_nodes=25, n_signers=10):
+    """A synthetic rxMsgs drain (stp_zmq/zstack.py:528-549): n_req client
+    REQUESTs (every 10th forged after signing) plus, for each, the n_nodes - 1
+    PROPAGATE copies other nodes send (node.py:1313-1316, 2304-2306)."""
+    import json
+    from plenum_amd import pack_messages, synth
+    from plenum_amd.base58 import b58encode
+    from plenum_amd.serialization import serialize_msg_for_signing
+    pks, sks = gpu_engine.seed_keypair_batch(synth.signer_seeds(n_signers))
+    idrs = [b58encode(bytes(pk[:16])) for pk in pks]
+    vks = ["~" + b58encode(bytes(pk[16:])) for pk in pks]
+    reqs = [synth.nym_request(idrs[i % n_signers], 1_600_000_000_000_000 + i, "dest%d" % i, "~vk%d" % i)
+            for i in range(n_req)]
+    sers = [serialize_msg_for_signing(r, topLevelKeysToIgnore=["signature"]) for r in reqs]
+    buf, off = pack_messages(sers)
+    sig = gpu_engine.sign_batch(sks, (np.arange(n_req) % n_signers).astype(np.uint32), buf, off)
+    for i, r in enumerate(reqs):
+        r["signature"] = b58encode(sig[i].tobytes())
+        if i % 10 == 3:
+            r["operation"]["dest"] += "x"  # forged after signing
+    rx = []
+    for i, r in enumerate(reqs):
+        rx.append((json.dumps(r), b"client%d" % i))
+        for node in range(1, n_nodes):
+            rx.append((json.dumps({"op": "PROPAGATE", "request": r, "senderClient": "client%d" % i}),
+                       b"Node%d" % node))
+    return reqs, rx, idrs, vks, pks, sers, sig
+
+
+def test_verify_ahead_drain_on_gpu(gpu_engine, oracle):
+    """One rxMsgs drain of 100 REQUESTs + 24 PROPAGATE copies each: exactly one
+    engine launch (the n copies dedupe to one verify each), then authenticate()
+    on Request.as_dict-shaped dicts (plenum/common/request.py:27-39) hits the
+    cache for all of them (0 single-verify launches); verdicts == the oracle."""
+    from plenum_amd.batching import prefetch_drain
+    reqs, rx, idrs, vks, pks, sers, sig = _drain(gpu_engine)
+    eng = _Counting(gpu_engine)
+    a = GpuAuthNr(engine=eng)
+    for idr, vk in zip(idrs, vks):
+        a.addIdr(idr, vk)
+    assert prefetch_drain(a, rx) == 100
+    assert eng.launches == 1 and a.stats["keyed_items"] == 100
+    for i, r in enumerate(reqs):
+        as_dict = {"identifier": r["identifier"], "reqId": r["reqId"], "operation": r["operation"],
+                   "signature": r["signature"], "protocolVersion": r["protocolVersion"]}
+        ser = sers[i] if i % 10 != 3 else None
+        want = ser is not None and oracle.oracle_verify_detached(sig[i].tobytes(), ser, len(ser),
+                                                                 pks[i % 10].tobytes()) == 0
+        if want:
+            assert a.authenticate(as_dict) == r["identifier"]
+        else:
+            with pytest.raises(Exception) as ei:
+                a.authenticate(as_dict)
+            assert type(ei.value).__name__ == "InvalidSignature"
+    assert eng.launches == 1 and a.stats["single_verifies"] == 0 and a.stats["cache_hits"] == 100
+
+
+def test_multi_engine_one_device(gpu_engine):
+    """The single-process multi-GPU path with the devices of this box (one
+    here): MultiEngine through the authenticator == the plain engine."""
+    from plenum_amd.multi import MultiEngine
+    reqs, rx, idrs, vks, pks, sers, sig = _drain(gpu_engine, n_nodes=1)
+    me = MultiEngine(engines=[gpu_engine])
+    a, b = GpuAuthNr(engine=me, max_keys=0), GpuAuthNr(engine=gpu_engine, max_keys=0)
+    for idr, vk in zip(idrs, vks):
+        a.addIdr(idr, vk)
+        b.addIdr(idr, vk)
+    ra = [r if isinstance(r, str) else type(r).__name__ for r in a.authenticate_batch(reqs)]
+    rb = [r if isinstance(r, str) else type(r).__name__ for r in b.authenticate_batch(reqs)]
+    assert ra == rb and ra.count("InvalidSignature") == 10
+    auto = MultiEngine("all")
+    try:
+        assert len(auto) >= 1
+        c = GpuAuthNr(engine=auto)
+        for idr, vk in zip(idrs, vks):
+            c.addIdr(idr, vk)
+        rc = [r if isinstance(r, str) else type(r).__name__ for r in c.authenticate_batch(reqs)]
+        assert rc == rb and c.stats["keyed_items"] == len(reqs)
+    finally:
+        auto.close()

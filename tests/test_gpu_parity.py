@@ -97,10 +97,10 @@ def test_sign_open_any_signature_length(gpu_engine, oracle):
     assert sum(want) == len([j for j in range(40) if j % 6 in (0, 5)])
 
 
-def test_large_batch_properties(gpu_engine):
-    """1M requests (BASELINE configs[1] size): every honest signature accepted,
-    every corrupted one rejected, bitmask popcount exact; plus a checksum of
-    the accept mask stable across two launches (determinism)."""
+@pytest.fixture(scope="module")
+def nym_1m(gpu_engine):
+    """BASELINE configs[1] on the device: 1M NYM requests (~200 B signed
+    payload, synth.nym_messages), 1,000 signers, signed on the GPU."""
     import torch
     from plenum_amd import synth
     n = 1_000_000
@@ -113,26 +113,88 @@ def test_large_batch_properties(gpu_engine):
     d_sig = torch.empty((n, 64), dtype=torch.uint8, device=dev)
     gpu_engine.sign_batch_device(torch.from_numpy(sks).to(dev), torch.from_numpy(kidx.astype(np.int32)).to(dev),
                                  d_msgs, d_off, n, d_sig)
-    d_pk = torch.from_numpy(pks).to(dev)[torch.from_numpy(kidx.astype(np.int64)).to(dev)].contiguous()
     torch.cuda.synchronize()
-    sig = d_sig.cpu().numpy()
+    return dict(n=n, pks=pks, kidx=kidx, buf=buf, off=off, sig=d_sig.cpu().numpy(), msgs=msgs)
+
+
+def _bits(words, n):
+    return np.unpackbits(words.cpu().numpy().view(np.uint8), bitorder="little")[:n].astype(bool)
+
+
+def _oracle_sample(oracle, sig, pk, buf, off, idx):
+    return np.array([oracle.oracle_verify_detached(sig[i].tobytes(), buf[int(off[i]):int(off[i + 1])].tobytes(),
+                                                   int(off[i + 1] - off[i]), pk[i].tobytes()) == 0 for i in idx])
+
+
+def test_large_batch_properties(gpu_engine, nym_1m):
+    """1M requests (BASELINE configs[1] size), general path: every honest
+    signature accepted, every corrupted one rejected, bitmask popcount exact;
+    plus a checksum of the accept mask stable across two launches."""
+    import torch
+    n, dev = nym_1m["n"], torch.device("cuda", 0)
+    sig = nym_1m["sig"].copy()
     rng = np.random.default_rng(5)
     bad = rng.choice(n, n // 20, replace=False)
     sig[bad, 40] ^= 0x10
     d_sig = torch.from_numpy(sig).to(dev)
+    d_pk = torch.from_numpy(nym_1m["pks"][nym_1m["kidx"]]).to(dev)
+    d_msgs = torch.from_numpy(np.concatenate([nym_1m["buf"], np.zeros(16, np.uint8)])).to(dev)
+    d_off = torch.from_numpy(nym_1m["off"].view(np.int64)).to(dev)
     words = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
     digests = []
     for _ in range(2):
         gpu_engine.verify_batch_device(d_sig, d_pk, d_msgs, d_off, n, words)
         torch.cuda.synchronize()
-        w = words.cpu().numpy()
-        digests.append(hashlib.sha256(w.tobytes()).hexdigest())
-    bits = np.unpackbits(w.view(np.uint8), bitorder="little")[:n].astype(bool)
+        digests.append(hashlib.sha256(words.cpu().numpy().tobytes()).hexdigest())
+    bits = _bits(words, n)
     want = np.ones(n, bool)
     want[bad] = False
     wrong = np.nonzero(bits != want)[0]
     assert len(wrong) == 0, (len(wrong), wrong[:8], wrong[-8:], bits[wrong[:8]])
     assert digests[0] == digests[1]
+
+
+@pytest.mark.parametrize("config", ["c1", "c2"])
+def test_keyed_headline_1m(gpu_engine, oracle, nym_1m, config):
+    """The headline configuration as bench.py times it: key-table path at key
+    window 14, 1M requests, message spans, 4 sub-batches.  c1: all valid ->
+    every bit set.  c2: the configs[2] 10% corruption mix (synth.corrupt_configs2:
+    R/S/M bit flips, S+L, S|2^255, small-order and non-canonical A, R = identity,
+    R+T8; corrupted keys registered as keys of their own) -> the construction's
+    verdicts exactly, and a 6,000-item oracle sample (every corruption kind)."""
+    import torch
+    from plenum_amd import synth
+    n, dev = nym_1m["n"], torch.device("cuda", 0)
+    sig, buf, off = nym_1m["sig"].copy(), nym_1m["buf"].copy(), nym_1m["off"]
+    pk = nym_1m["pks"][nym_1m["kidx"]].copy()
+    expect = np.ones(n, bool)
+    if config == "c2":
+        expect = synth.corrupt_configs2(sig, pk, buf, off, np.random.default_rng(2))
+    uniq, inv = np.unique(pk, axis=0, return_inverse=True)
+    try:
+        gpu_engine.keys_reset()
+        gpu_engine.keys_set_window(14)
+        assert gpu_engine.keys_add(uniq) == 0
+        d_sig = torch.from_numpy(sig).to(dev)
+        d_k = torch.from_numpy(inv.reshape(-1).astype(np.int32)).to(dev)
+        d_msgs = torch.from_numpy(np.concatenate([buf, np.zeros(16, np.uint8)])).to(dev)
+        d_ms = torch.from_numpy(off[:-1].astype(np.int64)).to(dev)
+        d_me = torch.from_numpy(off[1:].astype(np.int64)).to(dev)
+        words = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
+        gpu_engine.set_pipeline(4)
+        gpu_engine.verify_spans_device(d_sig, d_k, True, d_msgs, d_ms, d_me, n, words)
+        torch.cuda.synchronize()
+        got = _bits(words, n)
+    finally:
+        gpu_engine.keys_reset()
+        gpu_engine.keys_set_window(10)
+    wrong = np.nonzero(got != expect)[0]
+    assert len(wrong) == 0, (config, len(wrong), wrong[:8])
+    rng = np.random.default_rng(77)
+    bad = np.nonzero(~expect)[0]
+    idx = np.concatenate([rng.choice(n, 3000, replace=False),
+                          bad[:3000] if len(bad) else np.zeros(0, np.int64), [0, n - 1]]).astype(np.int64)
+    assert (_oracle_sample(oracle, sig, pk, buf, off, idx) == got[idx]).all()
 
 
 # ---- key-table path -------------------------------------------------------

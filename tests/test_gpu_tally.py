@@ -46,3 +46,51 @@ def test_tally_c4_shape(gpu_engine):
     counts, prep, com = gpu_engine.tally(k, v, ph, ok, n_keys, nv)
     c2, p2, m2 = tally_oracle.tally(k, v, ph, ok, n_keys, nv)
     assert (counts == c2).all() and (prep == p2).all() and (com == m2).all()
+
+
+def _kat():
+    import json
+    from conftest import GOLDEN
+    return json.load(open(os.path.join(GOLDEN, "tally_kat.json")))
+
+
+def test_tally_matches_reference_vote_sets(gpu_engine):
+    """tally_kat.json: vote streams run through the reference's own
+    Prepares/Commits (models.py) and Quorums (quorums.py), with the primary's
+    PREPARE rejected (replica.py:1289-1291)."""
+    for case in _kat():
+        v = np.array(case["votes"], np.int64).reshape(-1, 4)
+        counts, prep, com = gpu_engine.tally(v[:, 0], v[:, 1], v[:, 2], v[:, 3], len(case["keys"]), case["n"],
+                                             primary=case["primary"])
+        e = case["expect"]
+        assert counts.tolist() == e["counts"], case["name"]
+        assert prep.tolist() == e["prepared"] and com.tolist() == e["committed"], case["name"]
+
+
+def test_three_phase_tally_on_gpu(gpu_engine):
+    from plenum_amd.tally import ThreePhaseTally
+    case = next(c for c in _kat() if c["name"] == "random-n25")
+    names = ["N%d" % i for i in range(case["n"])]
+    t = ThreePhaseTally(gpu_engine, names)
+    for view, seq in case["keys"]:
+        t._keys.setdefault((view, seq), len(t._keys))
+    for kk, voter, phase, valid in case["votes"]:
+        t.add(*case["keys"][kk], names[voter], phase, bool(valid))
+    res = t.run()
+    e = case["expect"]
+    assert [res[tuple(k)][2] for k in case["keys"]] == e["prepared"]
+    assert [res[tuple(k)][3] for k in case["keys"]] == e["committed"]
+
+
+def test_tally_primary_c4_shape(gpu_engine):
+    """configs[4] shape with a primary per key (view = key // 1000)."""
+    rng = np.random.default_rng(5)
+    n_keys, nv = 160_000, 25
+    k = np.repeat(np.arange(n_keys, dtype=np.uint32), nv * 2)
+    v = np.tile(np.repeat(np.arange(nv, dtype=np.uint8), 2), n_keys)
+    ph = np.tile(np.array([0, 1], np.uint8), n_keys * nv)
+    ok = (rng.random(k.size) >= 0.05).astype(np.uint8)
+    primary = ((np.arange(n_keys) // 1000) % nv).astype(np.uint8)
+    counts, prep, com = gpu_engine.tally(k, v, ph, ok, n_keys, nv, primary=primary)
+    c2, p2, m2 = tally_oracle.tally(k, v, ph, ok, n_keys, nv, primary=primary)
+    assert (counts == c2).all() and (prep == p2).all() and (com == m2).all()

@@ -1,42 +1,89 @@
 """Quorum thresholds (plenum/server/quorums.py:15-32 with getMaxFailures,
 plenum/common/util.py:217-228) and the distinct-voter tally semantics
-(plenum/server/models.py:21-37).  The reference's quorums.py cannot be
-imported here (util.py:337 is a SyntaxError on Python >= 3.7), so the values
-are pinned by the formula table below, which matches the thresholds the
-reference's tests assume (n=4: f=1, prepare 2, commit 3; n=25: f=8)."""
-import sys
+(plenum/server/models.py:21-106, primary PREPARE rejected per
+replica.py:1289-1291).  Pinned by tests/golden/quorums_kat.json and
+tally_kat.json, which gen_ref_quorums.py produced by running the reference's
+own quorums.py / models.py (Prepares, Commits) under Python 3.9."""
+import json
 import os
+import sys
 
 import numpy as np
 
-from conftest import ROOT
+from conftest import GOLDEN, ROOT
 from plenum_amd.quorums import Quorums, getMaxFailures
-from plenum_amd.tally import ballots_from_votes
+from plenum_amd.tally import ThreePhaseTally
 
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 import tally_oracle  # noqa: E402
 
 
-def test_quorum_table():
-    table = {1: (0, 0, 1), 3: (0, 2, 3), 4: (1, 2, 3), 7: (2, 4, 5), 10: (3, 6, 7), 25: (8, 16, 17), 31: (10, 20, 21)}
-    for n, (f, prep, com) in table.items():
-        q = Quorums(n)
-        assert (q.f, q.prepare.value, q.commit.value) == (f, prep, com)
-        assert q.propagate.value == f + 1 and q.checkpoint.value == 2 * f
-        assert tally_oracle.thresholds(n) == (prep, com)
-    for n in range(1, 64):
-        assert getMaxFailures(n) == tally_oracle.max_failures(n)
-        assert Quorums(n).commit.is_reached(n - getMaxFailures(n))
-        assert not Quorums(n).commit.is_reached(n - getMaxFailures(n) - 1)
+def quorums_kat():
+    return json.load(open(os.path.join(GOLDEN, "quorums_kat.json")))
 
 
-def test_tally_oracle_set_semantics():
-    votes = [(0, 1, 0, 1), (0, 1, 0, 1), (0, 2, 0, 1), (0, 3, 0, 0), (1, 1, 1, 1)]
-    counts, qp, qc = tally_oracle.tally_sets(votes, 4)
-    assert counts == {(0, 0): 2, (1, 1): 1} and (qp, qc) == (2, 3)
-    k, v, p, ok = map(np.array, zip(*votes))
-    c, prep, com = tally_oracle.tally(k, v, p, ok, 2, 4)
-    assert c.tolist() == [[2, 0], [0, 1]] and prep.tolist() == [True, False] and com.tolist() == [False, False]
+def tally_kat():
+    return json.load(open(os.path.join(GOLDEN, "tally_kat.json")))
+
+
+def test_quorum_table_matches_reference():
+    rows = quorums_kat()
+    assert [r["n"] for r in rows] == list(range(1, 64))
+    for r in rows:
+        q = Quorums(r["n"])
+        assert q.f == r["f"] == getMaxFailures(r["n"]) == tally_oracle.max_failures(r["n"])
+        for name, v in r.items():
+            if name not in ("n", "f"):
+                assert getattr(q, name).value == v, (r["n"], name)
+        assert tally_oracle.thresholds(r["n"]) == (r["prepare"], r["commit"])
+        assert q.commit.is_reached(r["commit"]) and not q.commit.is_reached(r["commit"] - 1)
+
+
+def _arrays(case):
+    v = np.array(case["votes"], np.int64).reshape(-1, 4)
+    return v[:, 0], v[:, 1], v[:, 2], v[:, 3]
+
+
+def test_tally_oracle_matches_reference_vote_sets():
+    for case in tally_kat():
+        k, v, ph, ok = _arrays(case)
+        counts, prep, com = tally_oracle.tally(k, v, ph, ok, len(case["keys"]), case["n"], primary=case["primary"])
+        e = case["expect"]
+        assert counts.tolist() == e["counts"], case["name"]
+        assert prep.tolist() == e["prepared"] and com.tolist() == e["committed"], case["name"]
+        assert (e["prepare_quorum"], e["commit_quorum"]) == tally_oracle.thresholds(case["n"])
+
+
+def test_primary_prepare_never_counts():
+    case = next(c for c in tally_kat() if c["name"] == "primary-prepare-would-reach-quorum")
+    k, v, ph, ok = _arrays(case)
+    without, prep_wo, _ = tally_oracle.tally(k, v, ph, ok, len(case["keys"]), case["n"])
+    assert prep_wo[0] and not case["expect"]["prepared"][0]  # counting the primary would be one vote early
+
+
+class _OracleTallyEngine:
+    def tally(self, key, voter, phase, valid, n_keys, n_validators, primary=None):
+        return tally_oracle.tally(key, voter, phase, valid, n_keys, n_validators, primary=primary)
+
+
+def test_three_phase_tally_host_mapping():
+    """ThreePhaseTally's name/key mapping and primary rule (rank (view + inst) % n,
+    primary_selector.py:353-354) against the reference's vote sets."""
+    for case in tally_kat():
+        n = case["n"]
+        names = ["Node%d" % (i + 1) for i in range(n)]
+        # the fixture's primary of key k is view % n, i.e. instance 0
+        assert all(p == view % n for p, (view, _) in zip(case["primary"], case["keys"]))
+        t = ThreePhaseTally(_OracleTallyEngine(), names)
+        for view, seq in case["keys"]:  # fixture key order
+            t._keys.setdefault((view, seq), len(t._keys))
+        for kk, voter, phase, valid in case["votes"]:
+            view, seq = case["keys"][kk]
+            t.add(view, seq, names[voter], phase, bool(valid))
+        res = t.run()
+        e = case["expect"]
+        for i, (view, seq) in enumerate(case["keys"]):
+            assert res[(view, seq)] == (e["counts"][i][0], e["counts"][i][1], e["prepared"][i], e["committed"][i])
 
 
 def test_ballot_union_equals_set_union():
@@ -47,7 +94,7 @@ def test_ballot_union_equals_set_union():
     p = rng.integers(0, 2, 4000)
     ok = rng.random(4000) < 0.95
     half = 2000
-    b = np.maximum(ballots_from_votes(k[:half], v[:half], p[:half], ok[:half], n_keys, nv),
-                   ballots_from_votes(k[half:], v[half:], p[half:], ok[half:], n_keys, nv))
+    b = np.maximum(tally_oracle.ballots_from_votes(k[:half], v[:half], p[:half], ok[:half], n_keys, nv),
+                   tally_oracle.ballots_from_votes(k[half:], v[half:], p[half:], ok[half:], n_keys, nv))
     counts, _, _ = tally_oracle.tally(k, v, p, ok, n_keys, nv)
     assert (b.sum(axis=2) == counts).all()

@@ -1,0 +1,12 @@
+#!/bin/bash
+# GPU test pass: pytest -m gpu (one process), then smoke.  Output under gpurun_out/.
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+rc=$?
+tail -5 gpurun_out/pytest_gpu.log
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+rc=$?
+tail -2 gpurun_out/smoke.log
+exit $rc
