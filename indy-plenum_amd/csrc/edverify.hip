@@ -675,7 +675,17 @@ struct edv_ctx {
   struct Buf {
     void* p = nullptr;
     size_t cap = 0;
+    bool pinned = false;  // hipHostMalloc'd host memory
   } b_sig, b_pk, b_msg, b_off, b_bits, b_aux;
+  // Host-pointer verifies (host_verify): chunks of kHostChunk requests go
+  // through two slots of pinned host + device buffers; the CPU copy of chunk
+  // c + 1 into pinned memory and its H2D copy (on stream_copy) overlap the
+  // kernels of chunk c (on stream).
+  static constexpr int kSlots = 2;
+  hipStream_t stream_copy = nullptr;
+  hipEvent_t ev_h2d[kSlots] = {}, ev_done[kSlots] = {};
+  Buf h_sig[kSlots], h_key[kSlots], h_msg[kSlots], h_off[kSlots], h_bits[kSlots];
+  Buf d_sig[kSlots], d_key[kSlots], d_msg[kSlots], d_off[kSlots], d_bits[kSlots];
 };
 
 namespace {
@@ -691,6 +701,30 @@ int ensure(edv_ctx::Buf& b, size_t bytes) {
   if (e != hipSuccess) return set_err(EDV_ENOMEM, "hipMalloc(%zu): %s", want, hipGetErrorString(e));
   b.cap = want;
   return 0;
+}
+
+int ensure_pinned(edv_ctx::Buf& b, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  if (b.cap >= bytes) return 0;
+  if (b.p) (void)hipHostFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+  size_t want = bytes + bytes / 4 + 64;
+  hipError_t e = hipHostMalloc(&b.p, want, hipHostMallocDefault);
+  if (e != hipSuccess) return set_err(EDV_ENOMEM, "hipHostMalloc(%zu): %s", want, hipGetErrorString(e));
+  b.cap = want;
+  b.pinned = true;
+  return 0;
+}
+
+void free_buf(edv_ctx::Buf& b) {
+  if (!b.p) return;
+  if (b.pinned)
+    (void)hipHostFree(b.p);
+  else
+    (void)hipFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
 }
 
 int set_device(edv_ctx* ctx) {
@@ -958,6 +992,69 @@ static int launch_verify_keyed(edv_ctx* ctx, const void* d_sig, const void* d_ki
   return launch_pipeline(ctx, true, d_sig, d_kidx, d_msgs, off, off + 1, n, d_words, st);
 }
 
+// Host-pointer verify: chunks of kHostChunk requests staged through pinned
+// memory in two slots.  Chunk c: CPU copy into pinned slot c % 2 (after the
+// slot's previous chunk finished), H2D on stream_copy, kernels + bitmask D2H
+// on the context stream after the H2D event.  So the CPU copy and H2D of chunk
+// c + 1 run while chunk c's kernels do.  key_bytes: 32 (pk32) or 4 (key ids).
+constexpr uint64_t kHostChunk = 1ull << 18;
+static int host_verify(edv_ctx* ctx, bool keyed, const uint8_t* sig64, const uint8_t* keys, const uint8_t* msgs,
+                       const uint64_t* msg_off, uint64_t n, uint8_t* accept_bits) {
+  const uint64_t key_bytes = keyed ? 4 : 32;
+  for (uint64_t i = 0; i < n; ++i)
+    if (msg_off[i + 1] < msg_off[i]) return set_err(EDV_EINVAL, "msg_off[%llu] decreasing", (unsigned long long)i);
+  if (msg_off[n] > msg_off[0] && !msgs) return set_err(EDV_EINVAL, "null msgs");
+  if (keyed && ctx->key_count == 0) return set_err(EDV_EINVAL, "no registered keys");
+  const uint64_t nchunks = div_up(n, kHostChunk);
+  uint64_t pend[edv_ctx::kSlots] = {};  // chunk index + 1 whose bits sit in the slot (0 = none)
+  auto drain = [&](int sl) -> int {     // wait for the slot's chunk, copy its bits out
+    if (!pend[sl]) return 0;
+    HIP_TRY(hipEventSynchronize(ctx->ev_done[sl]));
+    const uint64_t c = pend[sl] - 1, c0 = c * kHostChunk, cn = (n - c0) < kHostChunk ? (n - c0) : kHostChunk;
+    memcpy(accept_bits + c0 / 8, ctx->h_bits[sl].p, (cn + 7) / 8);
+    pend[sl] = 0;
+    return 0;
+  };
+  int r;
+  for (uint64_t c = 0; c < nchunks; ++c) {
+    const int sl = (int)(c % edv_ctx::kSlots);
+    if ((r = drain(sl))) return r;
+    const uint64_t c0 = c * kHostChunk, cn = (n - c0) < kHostChunk ? (n - c0) : kHostChunk;
+    const uint64_t m0 = msg_off[c0], mbytes = msg_off[c0 + cn] - m0, nwords = div_up(cn, 64);
+    if ((r = ensure_pinned(ctx->h_sig[sl], 64 * cn)) || (r = ensure_pinned(ctx->h_key[sl], key_bytes * cn)) ||
+        (r = ensure_pinned(ctx->h_msg[sl], mbytes + 16)) || (r = ensure_pinned(ctx->h_off[sl], 8 * (cn + 1))) ||
+        (r = ensure_pinned(ctx->h_bits[sl], 8 * nwords)) || (r = ensure(ctx->d_sig[sl], 64 * cn)) ||
+        (r = ensure(ctx->d_key[sl], key_bytes * cn)) || (r = ensure(ctx->d_msg[sl], mbytes + 16)) ||
+        (r = ensure(ctx->d_off[sl], 8 * (cn + 1))) || (r = ensure(ctx->d_bits[sl], 8 * nwords)))
+      return r;
+    uint64_t* off = (uint64_t*)ctx->h_off[sl].p;
+    for (uint64_t i = 0; i <= cn; ++i) off[i] = msg_off[c0 + i] - m0;
+    memcpy(ctx->h_sig[sl].p, sig64 + 64 * c0, 64 * cn);
+    memcpy(ctx->h_key[sl].p, keys + key_bytes * c0, key_bytes * cn);
+    if (mbytes) memcpy(ctx->h_msg[sl].p, msgs + m0, mbytes);
+    ctx->bucket_now = ctx->bucket_mode == 1 || (ctx->bucket_mode == 2 && lengths_mixed(off, cn));
+    hipStream_t cs = ctx->stream_copy;
+    HIP_TRY(hipMemcpyAsync(ctx->d_sig[sl].p, ctx->h_sig[sl].p, 64 * cn, hipMemcpyHostToDevice, cs));
+    HIP_TRY(hipMemcpyAsync(ctx->d_key[sl].p, ctx->h_key[sl].p, key_bytes * cn, hipMemcpyHostToDevice, cs));
+    if (mbytes) HIP_TRY(hipMemcpyAsync(ctx->d_msg[sl].p, ctx->h_msg[sl].p, mbytes, hipMemcpyHostToDevice, cs));
+    HIP_TRY(hipMemcpyAsync(ctx->d_off[sl].p, off, 8 * (cn + 1), hipMemcpyHostToDevice, cs));
+    HIP_TRY(hipEventRecord(ctx->ev_h2d[sl], cs));
+    hipStream_t st = ctx->stream;
+    HIP_TRY(hipStreamWaitEvent(st, ctx->ev_h2d[sl], 0));
+    const uint64_t* d_off = (const uint64_t*)ctx->d_off[sl].p;
+    if ((r = launch_pipeline(ctx, keyed, ctx->d_sig[sl].p, ctx->d_key[sl].p, ctx->d_msg[sl].p, d_off, d_off + 1, cn,
+                             ctx->d_bits[sl].p, st)))
+      return r;
+    HIP_TRY(hipMemcpyAsync(ctx->h_bits[sl].p, ctx->d_bits[sl].p, 8 * nwords, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipEventRecord(ctx->ev_done[sl], st));
+    pend[sl] = c + 1;
+  }
+  for (int sl = 0; sl < edv_ctx::kSlots; ++sl)
+    if ((r = drain(sl))) return r;
+  if (n & 7) accept_bits[n / 8] &= (uint8_t)((1u << (n & 7)) - 1);
+  return 0;
+}
+
 extern "C" {
 
 int edv_keys_add(edv_ctx* ctx, const uint8_t* pk32, uint64_t nkeys, uint64_t* first_id) {
@@ -1069,30 +1166,7 @@ int edv_verify_batch_keyed(edv_ctx* ctx, const uint8_t* sig64, const uint32_t* k
   if (r) return r;
   if (n == 0) return 0;
   if (!sig64 || !key_idx || !msg_off || !accept_bits) return set_err(EDV_EINVAL, "null pointer");
-  for (uint64_t i = 0; i < n; ++i)
-    if (msg_off[i + 1] < msg_off[i]) return set_err(EDV_EINVAL, "msg_off[%llu] decreasing", (unsigned long long)i);
-  const uint64_t m0 = msg_off[0], mbytes = msg_off[n] - m0;
-  if (mbytes && !msgs) return set_err(EDV_EINVAL, "null msgs");
-  const uint64_t nwords = div_up(n, 64);
-  if ((r = ensure(ctx->b_sig, 64 * n)) || (r = ensure(ctx->b_pk, 4 * n)) || (r = ensure(ctx->b_msg, mbytes + 16)) ||
-      (r = ensure(ctx->b_off, 8 * (n + 1))) || (r = ensure(ctx->b_bits, 8 * nwords)))
-    return r;
-  hipStream_t st = ctx->stream;
-  std::vector<uint64_t> off(n + 1);
-  for (uint64_t i = 0; i <= n; ++i) off[i] = msg_off[i] - m0;
-  ctx->bucket_now = ctx->bucket_mode == 1 || (ctx->bucket_mode == 2 && lengths_mixed(off.data(), n));
-  HIP_TRY(hipMemcpyAsync(ctx->b_sig.p, sig64, 64 * n, hipMemcpyHostToDevice, st));
-  HIP_TRY(hipMemcpyAsync(ctx->b_pk.p, key_idx, 4 * n, hipMemcpyHostToDevice, st));
-  if (mbytes) HIP_TRY(hipMemcpyAsync(ctx->b_msg.p, msgs + m0, mbytes, hipMemcpyHostToDevice, st));
-  HIP_TRY(hipMemcpyAsync(ctx->b_off.p, off.data(), 8 * (n + 1), hipMemcpyHostToDevice, st));
-  if ((r = launch_verify_keyed(ctx, ctx->b_sig.p, ctx->b_pk.p, ctx->b_msg.p, ctx->b_off.p, n, ctx->b_bits.p, st)))
-    return r;
-  std::vector<uint64_t> words(nwords);
-  HIP_TRY(hipMemcpyAsync(words.data(), ctx->b_bits.p, 8 * nwords, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
-  memcpy(accept_bits, words.data(), (n + 7) / 8);
-  if (n & 7) accept_bits[n / 8] &= (uint8_t)((1u << (n & 7)) - 1);
-  return 0;
+  return host_verify(ctx, true, sig64, (const uint8_t*)key_idx, msgs, msg_off, n, accept_bits);
 }
 
 }  // extern "C"
@@ -1133,6 +1207,12 @@ edv_ctx* edv_create(int device) {
   if ((e = hipStreamCreate(&ctx->stream)) != hipSuccess) return fail("hipStreamCreate", e);
   if ((e = hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking)) != hipSuccess)
     return fail("hipStreamCreate", e);
+  if ((e = hipStreamCreateWithFlags(&ctx->stream_copy, hipStreamNonBlocking)) != hipSuccess)
+    return fail("hipStreamCreate", e);
+  for (int k = 0; k < edv_ctx::kSlots; ++k)
+    if ((e = hipEventCreateWithFlags(&ctx->ev_h2d[k], hipEventDisableTiming)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&ctx->ev_done[k], hipEventDisableTiming)) != hipSuccess)
+      return fail("hipEventCreate", e);
   for (int sb = 0; sb < edv_ctx::kSub; ++sb)
     for (int k = 0; k < edv_ctx::kEv; ++k)
       if ((e = hipEventCreate(&ctx->ev_sub[sb][k])) != hipSuccess) return fail("hipEventCreate", e);
@@ -1192,8 +1272,15 @@ void edv_destroy(edv_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  for (edv_ctx::Buf* b : {&ctx->b_sig, &ctx->b_pk, &ctx->b_msg, &ctx->b_off, &ctx->b_bits, &ctx->b_aux})
-    if (b->p) (void)hipFree(b->p);
+  if (ctx->stream_copy) (void)hipStreamSynchronize(ctx->stream_copy);
+  for (edv_ctx::Buf* b : {&ctx->b_sig, &ctx->b_pk, &ctx->b_msg, &ctx->b_off, &ctx->b_bits, &ctx->b_aux}) free_buf(*b);
+  for (int k = 0; k < edv_ctx::kSlots; ++k) {
+    for (edv_ctx::Buf* b : {&ctx->h_sig[k], &ctx->h_key[k], &ctx->h_msg[k], &ctx->h_off[k], &ctx->h_bits[k],
+                            &ctx->d_sig[k], &ctx->d_key[k], &ctx->d_msg[k], &ctx->d_off[k], &ctx->d_bits[k]})
+      free_buf(*b);
+    if (ctx->ev_h2d[k]) (void)hipEventDestroy(ctx->ev_h2d[k]);
+    if (ctx->ev_done[k]) (void)hipEventDestroy(ctx->ev_done[k]);
+  }
   if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
   if (ctx->d_hsoa) (void)hipFree(ctx->d_hsoa);
   if (ctx->d_flags) (void)hipFree(ctx->d_flags);
@@ -1215,6 +1302,7 @@ void edv_destroy(edv_ctx* ctx) {
   for (int k = 0; k < 2; ++k)
     if (ctx->ev_join[k]) (void)hipEventDestroy(ctx->ev_join[k]);
   if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
+  if (ctx->stream_copy) (void)hipStreamDestroy(ctx->stream_copy);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -1291,32 +1379,7 @@ int edv_verify_batch(edv_ctx* ctx, const uint8_t* sig64, const uint8_t* pk32, co
   if (r) return r;
   if (n == 0) return 0;
   if (!sig64 || !pk32 || !msg_off || !accept_bits) return set_err(EDV_EINVAL, "null pointer");
-  const uint64_t m0 = msg_off[0], m1 = msg_off[n];
-  if (m1 < m0) return set_err(EDV_EINVAL, "msg_off not monotone");
-  for (uint64_t i = 0; i < n; ++i)
-    if (msg_off[i + 1] < msg_off[i]) return set_err(EDV_EINVAL, "msg_off[%llu] decreasing", (unsigned long long)i);
-  const uint64_t mbytes = m1 - m0;
-  if (mbytes && !msgs) return set_err(EDV_EINVAL, "null msgs");
-  const uint64_t nwords = div_up(n, 64);
-  if ((r = ensure(ctx->b_sig, 64 * n)) || (r = ensure(ctx->b_pk, 32 * n)) || (r = ensure(ctx->b_msg, mbytes + 16)) ||
-      (r = ensure(ctx->b_off, 8 * (n + 1))) || (r = ensure(ctx->b_bits, 8 * nwords)))
-    return r;
-  hipStream_t st = ctx->stream;
-  // offsets rebased to 0 for the staged copy
-  std::vector<uint64_t> off(n + 1);
-  for (uint64_t i = 0; i <= n; ++i) off[i] = msg_off[i] - m0;
-  ctx->bucket_now = ctx->bucket_mode == 1 || (ctx->bucket_mode == 2 && lengths_mixed(off.data(), n));
-  HIP_TRY(hipMemcpyAsync(ctx->b_sig.p, sig64, 64 * n, hipMemcpyHostToDevice, st));
-  HIP_TRY(hipMemcpyAsync(ctx->b_pk.p, pk32, 32 * n, hipMemcpyHostToDevice, st));
-  if (mbytes) HIP_TRY(hipMemcpyAsync(ctx->b_msg.p, msgs + m0, mbytes, hipMemcpyHostToDevice, st));
-  HIP_TRY(hipMemcpyAsync(ctx->b_off.p, off.data(), 8 * (n + 1), hipMemcpyHostToDevice, st));
-  if ((r = launch_verify(ctx, ctx->b_sig.p, ctx->b_pk.p, ctx->b_msg.p, ctx->b_off.p, n, ctx->b_bits.p, st))) return r;
-  std::vector<uint64_t> words(nwords);
-  HIP_TRY(hipMemcpyAsync(words.data(), ctx->b_bits.p, 8 * nwords, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
-  memcpy(accept_bits, words.data(), (n + 7) / 8);
-  if (n & 7) accept_bits[n / 8] &= (uint8_t)((1u << (n & 7)) - 1);
-  return 0;
+  return host_verify(ctx, false, sig64, pk32, msgs, msg_off, n, accept_bits);
 }
 
 int edv_sign_open_batch(edv_ctx* ctx, const uint8_t* sm, const uint64_t* sm_off, const uint8_t* pk32, uint64_t n,

@@ -186,6 +186,58 @@ bool b58decode_raw(const unsigned char* s, size_t n, std::vector<uint8_t>& out) 
   return true;
 }
 
+// base58 0.2.4 b58encode: leading zero bytes -> '1's, the rest as a
+// big-endian base-58 number (repeated division of the byte string).
+std::string b58encode_raw(const uint8_t* v, size_t n) {
+  static const char kAlpha[] = "123456789ABCDEFGHJKLMNPQRSTUVWXYZabcdefghijkmnopqrstuvwxyz";
+  size_t nz = 0;
+  while (nz < n && v[nz] == 0) ++nz;
+  std::vector<uint8_t> num(v + nz, v + n);
+  std::string digits;
+  size_t start = 0;
+  while (start < num.size()) {
+    uint32_t rem = 0;
+    for (size_t i = start; i < num.size(); ++i) {
+      const uint32_t cur = rem * 256 + num[i];
+      num[i] = (uint8_t)(cur / 58);
+      rem = cur % 58;
+    }
+    digits.push_back(kAlpha[rem]);
+    while (start < num.size() && num[start] == 0) ++start;
+  }
+  return std::string(nz, '1') + std::string(digits.rbegin(), digits.rend());
+}
+
+// b58encode_rows(buf, width) -> [b58encode(buf[i*width:(i+1)*width]) ...]
+PyObject* py_b58encode_rows(PyObject*, PyObject* args) {
+  Py_buffer b;
+  Py_ssize_t width;
+  if (!PyArg_ParseTuple(args, "y*n", &b, &width)) return nullptr;
+  if (width <= 0 || b.len % width) {
+    PyBuffer_Release(&b);
+    PyErr_SetString(PyExc_ValueError, "buffer length is not a multiple of width");
+    return nullptr;
+  }
+  const Py_ssize_t rows = b.len / width;
+  PyObject* out = PyList_New(rows);
+  if (!out) {
+    PyBuffer_Release(&b);
+    return nullptr;
+  }
+  for (Py_ssize_t i = 0; i < rows; ++i) {
+    const std::string e = b58encode_raw((const uint8_t*)b.buf + i * width, (size_t)width);
+    PyObject* str = PyUnicode_FromStringAndSize(e.data(), (Py_ssize_t)e.size());
+    if (!str) {
+      Py_DECREF(out);
+      PyBuffer_Release(&b);
+      return nullptr;
+    }
+    PyList_SET_ITEM(out, i, str);
+  }
+  PyBuffer_Release(&b);
+  return out;
+}
+
 PyObject* py_b58decode(PyObject*, PyObject* v) {
   const unsigned char* s = nullptr;
   Py_ssize_t n = 0;
@@ -310,6 +362,8 @@ PyMethodDef kMethods[] = {
     {"serialize_for_signing", py_serialize_for_signing, METH_VARARGS,
      "serialize_for_signing(obj, ignore=None) -> bytes, or None for the Python path"},
     {"b58decode", py_b58decode, METH_O, "b58decode(str | bytes) -> bytes, or None for the Python path"},
+    {"b58encode_rows", py_b58encode_rows, METH_VARARGS,
+     "b58encode_rows(buf, width) -> list of b58encode(row) for each width-byte row (synthetic loads)"},
     {"pack_split64", py_pack_split64, METH_VARARGS,
      "pack_split64(sigs, sers) -> (sig64, msgs, off_u64le, short): crypto_sign_open's split at byte 64"},
     {"pack_sm", py_pack_sm, METH_VARARGS, "pack_sm(sigs, sers, keys) -> (sm, off_u64le, pk32)"},
