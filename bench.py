@@ -61,7 +61,7 @@ def parse():
                          "SimpleAuthNr.addIdr); general: every request carries its own key bytes")
     ap.add_argument("--key-window", type=int, choices=[4, 6, 8, 10, 12, 13, 14, 16], default=14,
                     help="comb window of the key tables (edv_keys_set_window)")
-    ap.add_argument("--pipeline", type=int, default=4, choices=[1, 2, 3, 4],
+    ap.add_argument("--pipeline", type=int, default=1, choices=[1, 2, 3, 4],
                     help="sub-batches per chunk (edv_set_pipeline; 1 = one launch per kernel, no overlap)")
     ap.add_argument("--length-buckets", choices=["auto", "on", "off"], default="auto",
                     help="hash lanes in SHA-512 block-count order (edv_set_length_buckets); auto = the "

@@ -106,7 +106,7 @@ int edv_last_launch_count(edv_ctx *ctx);
 /* Requests in the last chunk of the last verify call (a call over more than
  * 2^20 requests runs in chunks; the phase times cover the last one). */
 uint64_t edv_last_chunk_items(edv_ctx *ctx);
-/* Sub-batches per chunk (1..4, default 4); 1 = no overlap (each kernel runs
+/* Sub-batches per chunk (1..4, default 1); 1 = no overlap (each kernel runs
  * alone on the GPU, e.g. to time one kernel in isolation). */
 int edv_set_pipeline(edv_ctx *ctx, int sub_batches);
 /* Hash lanes in SHA-512 block-count order: without it every lane of a wave

@@ -415,6 +415,82 @@ __global__ __launch_bounds__(kBlock, EDV_HASH_MIN_WAVES) void edv_hash_keyed_ker
 #ifndef EDV_COMB_SET
 #define EDV_COMB_SET 1  // 1: the key comb's row 0 by comb_set (1 multiplication, not a 7-multiplication addition)
 #endif
+#ifndef EDV_COMB_LDS
+#define EDV_COMB_LDS 0  // 1: entries gathered one row ahead by LDS-DMA (comb_dual_lds): -3% c1, -10% c2 (r02b A/B)
+#endif
+
+// LDS-DMA gather of one 128-B table entry per lane: 8 global_load_lds_dwordx4,
+// piece k of every lane at lds + k * 1 KiB + lane * 16 B (the DMA's lane-linear
+// destination).  No VGPR holds the entry while it is in flight, so the next
+// row's gather runs under the current row's mixed addition without the
+// register cost of a register prefetch (which spilled at 4 waves / SIMD).
+constexpr int kLdsWaveWords = 8 * 64 * 4;  // 8 KiB per wave
+__device__ __forceinline__ void dma_entry(const uint32_t* src, uint32_t* lds) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + 4 * k),
+                                     (__attribute__((address_space(3))) void*)(lds + k * 256), 16, 0, 0);
+}
+__device__ __forceinline__ void lds_entry(ge_niels& nb, const uint32_t* lds, uint32_t lane) {
+  uint32_t w[32];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint4 v = *(const uint4*)(lds + k * 256 + lane * 4);
+    w[4 * k] = v.x;
+    w[4 * k + 1] = v.y;
+    w[4 * k + 2] = v.z;
+    w[4 * k + 3] = v.w;
+  }
+#pragma unroll
+  for (int l = 0; l < 10; ++l) {
+    nb.ypx.v[l] = w[l];
+    nb.ymx.v[l] = w[10 + l];
+    nb.xy2d.v[l] = w[20 + l];
+  }
+}
+
+// [h](-A) + [S]B over the key comb (W) and the base comb (kBaseW) as one
+// stream of kRows(W) + kRows(kBaseW) entries: entry s + 1 is DMA'd into the
+// wave's LDS slot right after entry s has been read out of it, so each gather
+// has a whole mixed addition (x 4 waves per SIMD) to land.
+template <int W>
+__device__ void comb_dual_lds(ge_p3& Q, const uint32_t h[8], const uint32_t S[8], const DevComb<W>& ta,
+                              const DevComb<kBaseW>& tb, uint32_t* lds, uint32_t lane) {
+  constexpr int RK = Window<W>::kRows, RB = Window<kBaseW>::kRows;
+  CombDigits<W> dh(h);
+  int e = dh.next();
+  dma_entry(ta.entry(0, (e < 0 ? -e : e) - 1), lds);
+  ge_niels nb;
+  lds_entry(nb, lds, lane);
+  int e_next = dh.next();
+  dma_entry(ta.entry(1, (e_next < 0 ? -e_next : e_next) - 1), lds);
+  comb_set_entry(Q, nb, e);
+#pragma unroll 1
+  for (int r = 1; r < RK; ++r) {
+    e = e_next;
+    lds_entry(nb, lds, lane);
+    if (r + 1 < RK) {
+      e_next = dh.next();
+      dma_entry(ta.entry(r + 1, (e_next < 0 ? -e_next : e_next) - 1), lds);
+    } else {  // the base comb's row 0: digit 0 of S + bias needs only the low word
+      e_next = (int)((S[0] + Window<kBaseW>::bias_word(0)) & ((1u << kBaseW) - 1)) - (1 << (kBaseW - 1));
+      dma_entry(tb.entry(0, (e_next < 0 ? -e_next : e_next) - 1), lds);
+    }
+    comb_apply(Q, nb, e);
+  }
+  CombDigits<kBaseW> ds(S);
+  e_next = ds.next();
+#pragma unroll 1
+  for (int r = 0; r < RB; ++r) {
+    e = e_next;
+    lds_entry(nb, lds, lane);
+    if (r + 1 < RB) {
+      e_next = ds.next();
+      dma_entry(tb.entry(r + 1, (e_next < 0 ? -e_next : e_next) - 1), lds);
+    }
+    comb_apply(Q, nb, e);
+  }
+}
 // [h](-A) + [S]B over the key's comb (W) and the base comb (kBaseW): no doublings.
 template <int W>
 __global__ __launch_bounds__(kBlock, EDV_COMB_MIN_WAVES) void edv_comb_kernel(const uint8_t* __restrict__ sig64,
@@ -436,7 +512,11 @@ __global__ __launch_bounds__(kBlock, EDV_COMB_MIN_WAVES) void edv_comb_kernel(co
   const DevComb<W> ta{key_tab + (uint64_t)key * kRowWordsW, ident, key_cap * kRowWordsW};  // row-major store
   const DevComb<kBaseW> tb{btab, ident};
   ge_p3 Q;
-#if EDV_COMB_SET
+#if EDV_COMB_LDS
+  __shared__ uint32_t lds_slots[kBlock / 64][kLdsWaveWords];
+  comb_dual_lds<W>(Q, h, S, ta, tb, lds_slots[threadIdx.x >> 6], threadIdx.x & 63);
+  uint32_t sink = 0;
+#elif EDV_COMB_SET
   comb_mul_set<W>(Q, h, ta);  // Q = [h](-A): row 0 set, not added to the identity
   uint32_t sink = comb_mul_add<kBaseW>(Q, S, tb);
 #else
@@ -661,7 +741,7 @@ struct edv_ctx {
   hipEvent_t ev_join[2] = {};
   int last_nsub = 0;
   uint64_t last_chunk_n = 0;  // requests in the last chunk (what edv_last_phases_ms covers)
-  int max_sub = kSub;  // edv_set_pipeline
+  int max_sub = 1;  // edv_set_pipeline (1, 2 and 4 sub-batches measure within 1% at 1M: profiles/r02b)
   bool timed = false;
   // key-table store (registered public keys)
   uint32_t* d_btab_comb32 = nullptr;  // base-point comb table (kBaseW; 3 GiB at W = 22)
@@ -737,7 +817,9 @@ hipStream_t pick_stream(edv_ctx* ctx, void* stream) { return stream ? (hipStream
 
 // Key windows a context accepts (edv_keys_set_window); every one instantiates
 // its own comb / fill kernels.
+#ifndef EDV_KEY_WINDOWS
 #define EDV_KEY_WINDOWS(X) X(4) X(6) X(8) X(10) X(12) X(13) X(14) X(16)
+#endif
 bool key_window_ok(int w) {
 #define EDV_KW_OK(W) || w == W
   return false EDV_KEY_WINDOWS(EDV_KW_OK);

@@ -115,6 +115,42 @@ static inline bool fe_in_class(const fe& f, uint32_t even_max, uint32_t odd_max)
 #define EDV_IS_C(f) fe_in_class(f, (1u << 26) - 1, (1u << 25) + (1u << 18))
 #endif
 
+// acc += a * b as one v_mad_u64_u32 in program order (EDV_MAD_CHAIN): inline
+// asm keeps the compiler from re-associating a carry-started chain into a
+// zero-started chain plus a 64-bit add of the carry.
+#ifndef EDV_MAD_CHAIN
+#define EDV_MAD_CHAIN 1  // +3.5% on the keyed step (tools/ab_libs.py, profiles/r02b)
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && EDV_MAD_CHAIN
+__device__ __forceinline__ void mad_acc(uint64_t& acc, uint32_t a, uint32_t b) {
+  uint64_t carry_out;  // VOP3b sdst (unused)
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(carry_out) : "v"(a), "v"(b));
+}
+// acc += sum_i a[i] * b[i], ten MADs in one asm block (one serial chain)
+__device__ __forceinline__ void mad_acc10(uint64_t& acc, const uint32_t a[10], const uint32_t b[10]) {
+  uint64_t co;
+  asm("v_mad_u64_u32 %0, %1, %2, %12, %0\n\t"
+      "v_mad_u64_u32 %0, %1, %3, %13, %0\n\t"
+      "v_mad_u64_u32 %0, %1, %4, %14, %0\n\t"
+      "v_mad_u64_u32 %0, %1, %5, %15, %0\n\t"
+      "v_mad_u64_u32 %0, %1, %6, %16, %0\n\t"
+      "v_mad_u64_u32 %0, %1, %7, %17, %0\n\t"
+      "v_mad_u64_u32 %0, %1, %8, %18, %0\n\t"
+      "v_mad_u64_u32 %0, %1, %9, %19, %0\n\t"
+      "v_mad_u64_u32 %0, %1, %10, %20, %0\n\t"
+      "v_mad_u64_u32 %0, %1, %11, %21, %0"
+      : "+v"(acc), "=s"(co)
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]), "v"(a[8]),
+        "v"(a[9]), "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]), "v"(b[5]), "v"(b[6]), "v"(b[7]),
+        "v"(b[8]), "v"(b[9]));
+}
+#else
+EDV_HD void mad_acc(uint64_t& acc, uint32_t a, uint32_t b) { acc += (uint64_t)a * b; }
+EDV_HD void mad_acc10(uint64_t& acc, const uint32_t a[10], const uint32_t b[10]) {
+  for (int i = 0; i < 10; ++i) acc += (uint64_t)a[i] * b[i];
+}
+#endif
+
 // h = f * g.  f in W, g in L; h in C.  100 multiply-adds.
 // EDV_FE_MUL_ORDER 1 emits the products operand-major (for each f_i, one
 // product into each of the 10 accumulators), so consecutive v_mad_u64_u32 go
@@ -138,6 +174,20 @@ EDV_HD void fe_mul(fe& h, const fe& f, const fe& g) {
   uint32_t o[10];  // h may alias f or g
 #pragma unroll
   for (int k = 0; k < 10; ++k) {
+#if EDV_MAD_CHAIN
+    // the chain starts from the carry of limb k - 1 (one v_mad_u64_u32 per
+    // product, no separate 64-bit add of the carry, which the compiler's
+    // reassociation otherwise emits)
+    uint64_t a = c;
+    uint32_t fa[10], gb[10];
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      const int j = k - i;
+      fa[i] = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
+      gb[i] = j >= 0 ? g.v[j] : g19[j + 10];
+    }
+    mad_acc10(a, fa, gb);
+#else
     uint64_t a = c;
 #pragma unroll
     for (int i = 0; i < 10; ++i) {
@@ -146,6 +196,7 @@ EDV_HD void fe_mul(fe& h, const fe& f, const fe& g) {
       const uint32_t gj = j >= 0 ? g.v[j] : g19[j + 10];
       a += (uint64_t)fi * gj;
     }
+#endif
     o[k] = (uint32_t)a & fe_mask(k);
     c = a >> fe_width(k);
   }

@@ -34,7 +34,27 @@ static const uint64_t SHA512_K[80] = {
     0x113f9804bef90daeULL, 0x1b710b35131c471bULL, 0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL,
     0x431d67c49c100d4cULL, 0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL};
 
-EDV_HD uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+// 64-bit rotate / shift on the 32-bit halves: two v_alignbit_b32 per rotate
+// (the compiler's i64 rotate is two 64-bit shifts + two ors).  n is a
+// compile-time constant at every call, so the branches fold.
+EDV_HD uint64_t rotr64(uint64_t x, int n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  if (n < 32)
+    return ((uint64_t)__builtin_amdgcn_alignbit(lo, hi, n) << 32) | __builtin_amdgcn_alignbit(hi, lo, n);
+  return ((uint64_t)__builtin_amdgcn_alignbit(hi, lo, n - 32) << 32) | __builtin_amdgcn_alignbit(lo, hi, n - 32);
+#else
+  return (x >> n) | (x << (64 - n));
+#endif
+}
+EDV_HD uint64_t shr64(uint64_t x, int n) {  // 0 < n < 32
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  return ((uint64_t)(hi >> n) << 32) | __builtin_amdgcn_alignbit(hi, lo, n);
+#else
+  return x >> n;
+#endif
+}
 EDV_HD uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
 #define EDV_SHA_ROUND(KI, WI)                                                        \
@@ -43,7 +63,7 @@ EDV_HD uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
     const uint64_t ch = (e & f) ^ (~e & g);                                        \
     const uint64_t t1 = h + S1 + ch + (KI) + (WI);                                 \
     const uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);             \
-    const uint64_t mj = (a & b) ^ (a & c) ^ (b & c);                               \
+    const uint64_t mj = (a & b) | (c & (a | b));                                   \
     h = g;                                                                         \
     g = f;                                                                         \
     f = e;                                                                         \
@@ -67,8 +87,8 @@ EDV_HD void sha512_compress(uint64_t st[8], uint64_t w[16]) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const uint64_t w15 = w[(i + 1) & 15], w2 = w[(i + 14) & 15];
-      const uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ (w15 >> 7);
-      const uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ (w2 >> 6);
+      const uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ shr64(w15, 7);
+      const uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ shr64(w2, 6);
       w[i] += s0 + w[(i + 9) & 15] + s1;
       EDV_SHA_ROUND(SHA512_K[r + i], w[i])
     }
