@@ -64,37 +64,48 @@ int set_err(int code, const char* fmt, ...) {
 
 // ------------------------------------------------------------------ accessors
 
-// Per-lane cached multiples [1..8](-A), SoA per 256-lane block: word w of lane t
-// lives at region + (w * 256 + t) * 4, so every access is a coalesced
-// buffer_load/store with one VGPR (voffset) of addressing and the limb index in
-// the scalar offset.
+// Per-lane cached multiples [1..8](-A) (+ the identity in slot 8), AoS per
+// lane: lane t of a 256-lane block owns kTableWords contiguous words in the
+// block's region, entry j at word 40 j (YplusX | YminusX | Z | T2d).  A lane
+// reads its own 160-B entry with 10 dwordx4 loads, i.e. 1-2 cache lines per
+// entry.  (The former SoA layout -- word w of every lane in one 1 KiB row --
+// made each per-lane random entry index touch 40 different lines: 88 KB of
+// FETCH per request against ~12 KB of entries, profiles/r01m.)
 constexpr uint32_t kRegionBytes = kTableWords * kBlock * 4;
 struct DevTableA {
-  __amdgpu_buffer_rsrc_t rsrc;  // this block's region (wave-uniform)
-  uint32_t lane_off;            // threadIdx.x * 4
-  __device__ DevTableA(uint32_t* scratch, uint32_t block, uint32_t lane) {
-    rsrc = __builtin_amdgcn_make_buffer_rsrc((char*)scratch + (uint64_t)block * kRegionBytes, 0, kRegionBytes,
-                                             0x00020000);
-    lane_off = lane * 4;
-  }
+  uint32_t* __restrict__ base;  // this lane's 9 entries
+  __device__ DevTableA(uint32_t* scratch, uint32_t block, uint32_t lane)
+      : base((uint32_t*)((char*)scratch + (uint64_t)block * kRegionBytes) + lane * kTableWords) {}
   __device__ void store(int j, const ge_cached& c) const {
-    const int off = lane_off + j * (40 * kBlock * 4);
+    uint4* p = (uint4*)(base + j * 40);
+    uint32_t w[40];
 #pragma unroll
     for (int l = 0; l < 10; ++l) {
-      __builtin_amdgcn_raw_buffer_store_b32(c.YplusX.v[l], rsrc, off, (0 + l) * kBlock * 4, 0);
-      __builtin_amdgcn_raw_buffer_store_b32(c.YminusX.v[l], rsrc, off, (10 + l) * kBlock * 4, 0);
-      __builtin_amdgcn_raw_buffer_store_b32(c.Z.v[l], rsrc, off, (20 + l) * kBlock * 4, 0);
-      __builtin_amdgcn_raw_buffer_store_b32(c.T2d.v[l], rsrc, off, (30 + l) * kBlock * 4, 0);
+      w[l] = c.YplusX.v[l];
+      w[10 + l] = c.YminusX.v[l];
+      w[20 + l] = c.Z.v[l];
+      w[30 + l] = c.T2d.v[l];
     }
+#pragma unroll
+    for (int k = 0; k < 10; ++k) p[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
   }
   __device__ void load(int j, ge_cached& c) const {  // j = -1: the identity (slot 8)
-    const int off = lane_off + (j >= 0 ? j : 8) * (40 * kBlock * 4);
+    const uint4* p = (const uint4*)(base + (j >= 0 ? j : 8) * 40);
+    uint32_t w[40];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+      const uint4 v = p[k];
+      w[4 * k] = v.x;
+      w[4 * k + 1] = v.y;
+      w[4 * k + 2] = v.z;
+      w[4 * k + 3] = v.w;
+    }
 #pragma unroll
     for (int l = 0; l < 10; ++l) {
-      c.YplusX.v[l] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, off, (0 + l) * kBlock * 4, 0);
-      c.YminusX.v[l] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, off, (10 + l) * kBlock * 4, 0);
-      c.Z.v[l] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, off, (20 + l) * kBlock * 4, 0);
-      c.T2d.v[l] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, off, (30 + l) * kBlock * 4, 0);
+      c.YplusX.v[l] = w[l];
+      c.YminusX.v[l] = w[10 + l];
+      c.Z.v[l] = w[20 + l];
+      c.T2d.v[l] = w[30 + l];
     }
   }
 };

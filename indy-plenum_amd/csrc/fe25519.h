@@ -144,10 +144,40 @@ __device__ __forceinline__ void mad_acc10(uint64_t& acc, const uint32_t a[10], c
         "v"(a[9]), "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]), "v"(b[5]), "v"(b[6]), "v"(b[7]),
         "v"(b[8]), "v"(b[9]));
 }
+// the squaring chains: 6 (even limbs) or 5 (odd limbs) products
+__device__ __forceinline__ void mad_acc6(uint64_t& acc, const uint32_t a[6], const uint32_t b[6]) {
+  uint64_t co;
+  asm("v_mad_u64_u32 %0, %1, %2, %8, %0\n\t"
+      "v_mad_u64_u32 %0, %1, %3, %9, %0\n\t"
+      "v_mad_u64_u32 %0, %1, %4, %10, %0\n\t"
+      "v_mad_u64_u32 %0, %1, %5, %11, %0\n\t"
+      "v_mad_u64_u32 %0, %1, %6, %12, %0\n\t"
+      "v_mad_u64_u32 %0, %1, %7, %13, %0"
+      : "+v"(acc), "=s"(co)
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(b[0]), "v"(b[1]), "v"(b[2]),
+        "v"(b[3]), "v"(b[4]), "v"(b[5]));
+}
+__device__ __forceinline__ void mad_acc5(uint64_t& acc, const uint32_t a[5], const uint32_t b[5]) {
+  uint64_t co;
+  asm("v_mad_u64_u32 %0, %1, %2, %7, %0\n\t"
+      "v_mad_u64_u32 %0, %1, %3, %8, %0\n\t"
+      "v_mad_u64_u32 %0, %1, %4, %9, %0\n\t"
+      "v_mad_u64_u32 %0, %1, %5, %10, %0\n\t"
+      "v_mad_u64_u32 %0, %1, %6, %11, %0"
+      : "+v"(acc), "=s"(co)
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]),
+        "v"(b[4]));
+}
 #else
 EDV_HD void mad_acc(uint64_t& acc, uint32_t a, uint32_t b) { acc += (uint64_t)a * b; }
 EDV_HD void mad_acc10(uint64_t& acc, const uint32_t a[10], const uint32_t b[10]) {
   for (int i = 0; i < 10; ++i) acc += (uint64_t)a[i] * b[i];
+}
+EDV_HD void mad_acc6(uint64_t& acc, const uint32_t a[6], const uint32_t b[6]) {
+  for (int i = 0; i < 6; ++i) acc += (uint64_t)a[i] * b[i];
+}
+EDV_HD void mad_acc5(uint64_t& acc, const uint32_t a[5], const uint32_t b[5]) {
+  for (int i = 0; i < 5; ++i) acc += (uint64_t)a[i] * b[i];
 }
 #endif
 
@@ -258,6 +288,8 @@ EDV_HD void fe_sq(fe& h, const fe& f) {
 #pragma unroll
   for (int k = 0; k < 10; ++k) {
     uint64_t a = EDV_FE_MUL_ORDER == 2 ? c : 0;
+    uint32_t pa[6], pb[6];
+    int np = 0;
 #pragma unroll
     for (int i = 0; i < 10; ++i) {
 #pragma unroll
@@ -267,8 +299,20 @@ EDV_HD void fe_sq(fe& h, const fe& f) {
         const bool wrap = i + j >= 10;
         const uint32_t fi = (i != j) ? d2[i] : d[i];
         const uint32_t fj = wrap ? (both_odd ? d38[j] : d19[j]) : (both_odd ? d2[j] : d[j]);
-        a += (uint64_t)fi * fj;
+        if (EDV_FE_MUL_ORDER == 2 && EDV_MAD_CHAIN) {
+          pa[np] = fi;  // carry-started chain, one asm block per limb
+          pb[np] = fj;
+          ++np;
+        } else {
+          a += (uint64_t)fi * fj;
+        }
       }
+    }
+    if (EDV_FE_MUL_ORDER == 2 && EDV_MAD_CHAIN) {
+      if (k & 1)
+        mad_acc5(a, pa, pb);
+      else
+        mad_acc6(a, pa, pb);
     }
     acc[k] = a;
     if (EDV_FE_MUL_ORDER == 2) {

@@ -43,11 +43,16 @@ if cfg == "c2":
 eng.keys_set_window(W)
 eng.keys_add(reg)
 words = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
-step = lambda: eng.verify_batch_keyed_device(d_sig, d_k, d_msgs, d_off, n, words)
+if os.environ.get("AB_PATH") == "general":
+    d_pk = torch.from_numpy(pks[kidx] if cfg != "c2" else pk).to(dev)
+    step = lambda: eng.verify_batch_device(d_sig, d_pk, d_msgs, d_off, n, words)
+    reps = 5
+else:
+    step = lambda: eng.verify_batch_keyed_device(d_sig, d_k, d_msgs, d_off, n, words)
+    reps = 30
 eng.set_pipeline(4)
 for _ in range(3): step()
 torch.cuda.synchronize()
-reps = 30
 t0 = time.perf_counter()
 for _ in range(reps): step()
 torch.cuda.synchronize()
@@ -78,12 +83,13 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--window", type=int, default=14)
     ap.add_argument("--config", default="c1")
+    ap.add_argument("--path", default="keyed", choices=["keyed", "general"])
     ap.add_argument("libs", nargs="+")
     a = ap.parse_args()
     for r in range(a.rounds):
         for lib in a.libs:
             env = dict(os.environ, PLENUM_EDVERIFY_LIB=os.path.abspath(lib), PLENUM_EDVERIFY_LENIENT="1",
-                       AB_W=str(a.window), AB_CONFIG=a.config)
+                       AB_W=str(a.window), AB_CONFIG=a.config, AB_PATH=a.path)
             out = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
             line = [x for x in out.stdout.splitlines() if x.startswith("{")]
             print("round %d %s W=%d %s: %s" % (r, os.path.basename(lib), a.window, a.config,
