@@ -24,6 +24,7 @@
 #include <Python.h>
 
 #include <stdint.h>
+#include <stdio.h>
 #include <string.h>
 
 #include <algorithm>
@@ -37,6 +38,10 @@ namespace {
 bool ser_obj(PyObject* o, int level, PyObject* ignore, std::string& out);
 
 bool append_str(PyObject* s, std::string& out) {
+  if (PyUnicode_IS_ASCII(s)) {
+    out.append((const char*)PyUnicode_1BYTE_DATA(s), (size_t)PyUnicode_GET_LENGTH(s));
+    return true;
+  }
   Py_ssize_t n = 0;
   const char* p = PyUnicode_AsUTF8AndSize(s, &n);
   if (!p) {
@@ -68,26 +73,56 @@ bool ignored(PyObject* k, PyObject* ignore) {
   return false;
 }
 
+// str < str as list.sort orders them (code points); one-byte strings (the
+// common case) compare with memcmp, others through PyUnicode_Compare.
+bool str_less(PyObject* a, PyObject* b, bool& err) {
+  if (PyUnicode_KIND(a) == PyUnicode_1BYTE_KIND && PyUnicode_KIND(b) == PyUnicode_1BYTE_KIND) {
+    const Py_ssize_t na = PyUnicode_GET_LENGTH(a), nb = PyUnicode_GET_LENGTH(b);
+    const int c = memcmp(PyUnicode_1BYTE_DATA(a), PyUnicode_1BYTE_DATA(b), (size_t)(na < nb ? na : nb));
+    return c < 0 || (c == 0 && na < nb);
+  }
+  const int c = PyUnicode_Compare(a, b);
+  if (c == -1 && PyErr_Occurred()) err = true;
+  return c < 0;
+}
+
 bool ser_dict(PyObject* d, int level, PyObject* ignore, std::string& out) {
-  std::vector<PyObject*> keys;
-  Py_ssize_t pos = 0;
+  // keys on the stack for ordinary dicts (insertion sort), a vector beyond
+  constexpr Py_ssize_t kSmall = 24;
+  PyObject* small[kSmall];
+  std::vector<PyObject*> big;
+  const Py_ssize_t nd = PyDict_GET_SIZE(d);
+  PyObject** keys = small;
+  if (nd > kSmall) {
+    big.resize((size_t)nd);
+    keys = big.data();
+  }
+  Py_ssize_t nk = 0, pos = 0;
   PyObject *k, *v;
   while (PyDict_Next(d, &pos, &k, &v)) {
     if (!PyUnicode_CheckExact(k)) return false;  // non-str keys: the reference may raise -> Python path
     if (level == 0 && ignored(k, ignore)) continue;
-    keys.push_back(k);
+    keys[nk++] = k;
   }
   bool cmp_err = false;
-  std::sort(keys.begin(), keys.end(), [&](PyObject* a, PyObject* b) {
-    const int c = PyUnicode_Compare(a, b);
-    if (c == -1 && PyErr_Occurred()) cmp_err = true;
-    return c < 0;
-  });
+  if (nk <= kSmall) {
+    for (Py_ssize_t i = 1; i < nk; ++i) {
+      PyObject* x = keys[i];
+      Py_ssize_t j = i;
+      while (j > 0 && str_less(x, keys[j - 1], cmp_err)) {
+        keys[j] = keys[j - 1];
+        --j;
+      }
+      keys[j] = x;
+    }
+  } else {
+    std::sort(keys, keys + nk, [&](PyObject* a, PyObject* b) { return str_less(a, b, cmp_err); });
+  }
   if (cmp_err) {
     PyErr_Clear();
     return false;
   }
-  for (size_t i = 0; i < keys.size(); ++i) {
+  for (Py_ssize_t i = 0; i < nk; ++i) {
     if (i) out.push_back('|');
     if (!append_str(keys[i], out)) return false;
     out.push_back(':');
@@ -116,7 +151,19 @@ bool ser_obj(PyObject* o, int level, PyObject* ignore, std::string& out) {
     out.append(o == Py_True ? "True" : "False");
     return true;
   }
-  if (PyLong_CheckExact(o) || PyFloat_CheckExact(o)) return append_text_of(o, out);
+  if (PyLong_CheckExact(o)) {  // str(int): decimal, without a temporary str for 64-bit values
+    int overflow = 0;
+    const long long x = PyLong_AsLongLongAndOverflow(o, &overflow);
+    if (overflow || (x == -1 && PyErr_Occurred())) {
+      PyErr_Clear();
+      return append_text_of(o, out);
+    }
+    char b[24];
+    const int len = snprintf(b, sizeof b, "%lld", x);
+    out.append(b, (size_t)len);
+    return true;
+  }
+  if (PyFloat_CheckExact(o)) return append_text_of(o, out);
   return false;  // tuples, sets, subclasses, other types: the Python path decides
 }
 
@@ -149,34 +196,41 @@ struct B58Index {
 };
 const B58Index kIndex;
 
-// false on a character outside the alphabet.  Base conversion on 32-bit
-// limbs, five base-58 digits (58^5 < 2^32) per multiply-add pass.
+// false on a character outside the alphabet.  Base conversion on 64-bit
+// limbs, ten base-58 digits (58^10 < 2^59) per multiply-add pass with 128-bit
+// products (an 88-character signature: 9 passes over at most 4 limbs).
 bool b58decode_raw(const unsigned char* s, size_t n, std::vector<uint8_t>& out) {
   size_t nz = 0;
   while (nz < n && s[nz] == '1') ++nz;
-  std::vector<uint32_t> limb;  // little-endian base 2^32 magnitude
-  limb.reserve(n / 5 + 2);
-  size_t i = nz;
+  uint64_t stack_limbs[16];
+  std::vector<uint64_t> heap;
+  uint64_t* limb = stack_limbs;
+  const size_t cap = (n - nz) / 10 + 2;
+  if (cap > 16) {
+    heap.resize(cap);
+    limb = heap.data();
+  }
+  size_t nl = 0, i = nz;
   while (i < n) {
-    uint32_t mul = 1, chunk = 0;
-    for (int k = 0; k < 5 && i < n; ++k, ++i) {
+    uint64_t mul = 1, chunk = 0;
+    for (int k = 0; k < 10 && i < n; ++k, ++i) {
       const int d = kIndex.v[s[i]];
       if (d < 0) return false;
-      chunk = chunk * 58u + (uint32_t)d;
+      chunk = chunk * 58u + (uint64_t)d;
       mul *= 58u;
     }
-    uint64_t carry = chunk;
-    for (size_t j = 0; j < limb.size(); ++j) {
-      const uint64_t t = (uint64_t)limb[j] * mul + carry;
-      limb[j] = (uint32_t)t;
-      carry = t >> 32;
+    unsigned __int128 carry = chunk;
+    for (size_t j = 0; j < nl; ++j) {
+      const unsigned __int128 t = (unsigned __int128)limb[j] * mul + carry;
+      limb[j] = (uint64_t)t;
+      carry = t >> 64;
     }
-    if (carry) limb.push_back((uint32_t)carry);
+    if (carry) limb[nl++] = (uint64_t)carry;
   }
   out.assign(nz, 0);
   bool lead = true;
-  for (size_t j = limb.size(); j-- > 0;) {
-    for (int sh = 24; sh >= 0; sh -= 8) {
+  for (size_t j = nl; j-- > 0;) {
+    for (int sh = 56; sh >= 0; sh -= 8) {
       const uint8_t byte = (uint8_t)(limb[j] >> sh);
       if (lead && byte == 0) continue;
       lead = false;
@@ -358,7 +412,134 @@ PyObject* py_pack_sm(PyObject*, PyObject* args) {
   return ret;
 }
 
+// scan_batch(msgs, ignore) -> (fast, idrs, sig64, msgbuf, off, short)
+// The host half of NaclAuthNr.authenticate for a batch of request dicts
+// (client_authn.py:72-92) where every step succeeds without a decision the
+// Python code must make: msg[signature] is a non-empty str, msg[identifier] a
+// non-empty str, b58decode(signature) succeeds and serialize_for_signing takes
+// its native path.  For those items (fast[i] = 1) the signed stream
+// sm = b58decode(sig) || ser is split at byte 64 like crypto_sign_open
+// (nacl_wrappers.py:108): sig64 (n * 64), messages (msgbuf + off[n + 1],
+// uint64 LE), short[i] = len(sm) < 64.  idrs[i] is the identifier (fast items)
+// or None.  Every other item (fast[i] = 0, zero-length slots) takes the
+// Python _prepare, which raises the reference's exception.
+PyObject* py_scan_batch(PyObject*, PyObject* args) {
+  PyObject *msgs, *ignore = Py_None;
+  if (!PyArg_ParseTuple(args, "O|O", &msgs, &ignore)) return nullptr;
+  PyObject* fm = PySequence_Fast(msgs, "msgs must be a sequence");
+  if (!fm) return nullptr;
+  PyObject* ign = nullptr;
+  if (ignore != Py_None) {
+    ign = PySequence_Fast(ignore, "ignore must be a sequence");
+    if (!ign) {
+      Py_DECREF(fm);
+      return nullptr;
+    }
+  }
+  static PyObject* k_sig = PyUnicode_InternFromString("signature");
+  static PyObject* k_idr = PyUnicode_InternFromString("identifier");
+  const Py_ssize_t n = PySequence_Fast_GET_SIZE(fm);
+  std::string fast((size_t)n, '\0'), shortv((size_t)n, '\0'), sig64((size_t)n * 64, '\0'), buf;
+  std::vector<uint64_t> off((size_t)n + 1, 0);
+  PyObject* idrs = PyList_New(n);
+  if (!idrs) {
+    Py_DECREF(fm);
+    Py_XDECREF(ign);
+    return nullptr;
+  }
+  std::vector<uint8_t> sig;
+  std::string ser;
+  buf.reserve((size_t)n * 160);
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    PyObject* m = PySequence_Fast_GET_ITEM(fm, i);
+    PyObject* idr = Py_None;
+    bool ok = PyDict_CheckExact(m);
+    PyObject *sv = nullptr, *iv = nullptr;
+    if (ok) {
+      sv = PyDict_GetItemWithError(m, k_sig);
+      iv = sv ? PyDict_GetItemWithError(m, k_idr) : nullptr;
+      if (PyErr_Occurred()) PyErr_Clear();
+      ok = sv && iv && PyUnicode_CheckExact(sv) && PyUnicode_GET_LENGTH(sv) > 0 && PyUnicode_CheckExact(iv) &&
+           PyUnicode_GET_LENGTH(iv) > 0 && PyUnicode_IS_ASCII(sv);
+    }
+    if (ok) {
+      Py_ssize_t ns = 0;
+      const unsigned char* sp = (const unsigned char*)PyUnicode_AsUTF8AndSize(sv, &ns);
+      ok = sp && b58decode_raw(sp, (size_t)ns, sig);
+      if (!sp) PyErr_Clear();
+    }
+    if (ok) {
+      ser.clear();
+      ok = ser_obj(m, 0, ign, ser);
+    }
+    if (ok) {
+      fast[(size_t)i] = 1;
+      idr = iv;
+      const size_t ls = sig.size(), lm = ser.size();
+      char* dst = &sig64[(size_t)i * 64];
+      if (ls + lm < 64) {
+        shortv[(size_t)i] = 1;  // crypto_sign_open: smlen < 64 rejects
+      } else if (ls >= 64) {
+        memcpy(dst, sig.data(), 64);
+        buf.append((const char*)sig.data() + 64, ls - 64);
+        buf.append(ser);
+      } else {
+        memcpy(dst, sig.data(), ls);
+        memcpy(dst + ls, ser.data(), 64 - ls);
+        buf.append(ser, 64 - ls, std::string::npos);
+      }
+    }
+    off[(size_t)i + 1] = buf.size();
+    Py_INCREF(idr);
+    PyList_SET_ITEM(idrs, i, idr);
+  }
+  Py_DECREF(fm);
+  Py_XDECREF(ign);
+  PyObject* ret = Py_BuildValue("(y#Oy#y#y#y#)", fast.data(), (Py_ssize_t)n, idrs, sig64.data(),
+                                (Py_ssize_t)sig64.size(), buf.data(), (Py_ssize_t)buf.size(), (const char*)off.data(),
+                                (Py_ssize_t)(off.size() * 8), shortv.data(), (Py_ssize_t)n);
+  Py_DECREF(idrs);
+  return ret;
+}
+
+// gather_items(sig64, msgbuf, off, idx) -> (sig64', msgbuf', off'): the items
+// idx (uint32 LE) of a split batch, repacked contiguously.
+PyObject* py_gather_items(PyObject*, PyObject* args) {
+  Py_buffer bs, bm, bo, bi;
+  if (!PyArg_ParseTuple(args, "y*y*y*y*", &bs, &bm, &bo, &bi)) return nullptr;
+  const uint64_t* off = (const uint64_t*)bo.buf;
+  const uint32_t* idx = (const uint32_t*)bi.buf;
+  const Py_ssize_t n = bo.len / 8 - 1, k = bi.len / 4;
+  std::string sig((size_t)k * 64, '\0'), msg;
+  std::vector<uint64_t> o((size_t)k + 1, 0);
+  bool ok = n >= 0 && bs.len >= n * 64;
+  for (Py_ssize_t j = 0; j < k && ok; ++j) {
+    const uint32_t i = idx[j];
+    if ((Py_ssize_t)i >= n || off[i + 1] < off[i] || off[i + 1] > (uint64_t)bm.len) {
+      ok = false;
+      break;
+    }
+    memcpy(&sig[(size_t)j * 64], (const char*)bs.buf + (size_t)i * 64, 64);
+    msg.append((const char*)bm.buf + off[i], off[i + 1] - off[i]);
+    o[(size_t)j + 1] = msg.size();
+  }
+  PyBuffer_Release(&bs);
+  PyBuffer_Release(&bm);
+  PyBuffer_Release(&bo);
+  PyBuffer_Release(&bi);
+  if (!ok) {
+    PyErr_SetString(PyExc_ValueError, "gather_items: index or offsets out of range");
+    return nullptr;
+  }
+  return Py_BuildValue("(y#y#y#)", sig.data(), (Py_ssize_t)sig.size(), msg.data(), (Py_ssize_t)msg.size(),
+                       (const char*)o.data(), (Py_ssize_t)(o.size() * 8));
+}
+
 PyMethodDef kMethods[] = {
+    {"scan_batch", py_scan_batch, METH_VARARGS,
+     "scan_batch(msgs, ignore) -> (fast, idrs, sig64, msgbuf, off, short): authenticate()'s host steps for a batch"},
+    {"gather_items", py_gather_items, METH_VARARGS,
+     "gather_items(sig64, msgbuf, off, idx_u32) -> (sig64, msgbuf, off) of the selected items"},
     {"serialize_for_signing", py_serialize_for_signing, METH_VARARGS,
      "serialize_for_signing(obj, ignore=None) -> bytes, or None for the Python path"},
     {"b58decode", py_b58decode, METH_O, "b58decode(str | bytes) -> bytes, or None for the Python path"},

@@ -44,6 +44,7 @@ message from Node.verifySignature, node.py:2294-2318):
 `CoreAuthNr` is an alias of GpuAuthNr; `ReqAuthenticator` aggregates
 authenticators (names from BASELINE.json's north star).
 """
+import copy
 from abc import abstractmethod
 from collections import OrderedDict
 from copy import deepcopy
@@ -56,6 +57,11 @@ from .exceptions import (CouldNotAuthenticate, EmptyIdentifier, EmptySignature, 
 from .keystore import KeyStore, auto_window
 from .serialization import serialize_msg_for_signing
 from .verifier import DidVerifier, VerkeyCache
+
+try:  # native batch scan (csrc/hostpack.cpp): authenticate()'s host steps for a whole batch
+    from ._hostpack import gather_items as _gather_items, scan_batch as _scan_batch
+except ImportError:  # pragma: no cover - the per-message path below
+    _scan_batch = _gather_items = None
 
 try:  # native packing (csrc/hostpack.cpp)
     from ._hostpack import pack_sm as _pack_sm, pack_split64 as _pack_split64
@@ -95,6 +101,16 @@ VERKEY = 'verkey'
 ROLE = 'role'
 
 KEY_STORE_BYTES = 32 << 30  # HBM for key tables: the window is the widest that fits max_keys
+
+
+_MISSING = object()
+
+
+class _KeyOnly:
+    __slots__ = ("key",)
+
+    def __init__(self, key):
+        self.key = key
 
 
 class _Prepared:
@@ -349,6 +365,125 @@ class GpuAuthMixin:
     def authenticate_batch(self, msgs, identifiers=None, signatures=None):
         """Per message: the identifier authenticate() would return, or the
         exception instance it would raise (same class, args and __cause__)."""
+        if _scan_batch is not None and not identifiers and not signatures:
+            return self._authenticate_batch_scanned(msgs)
+        return self._authenticate_batch_each(msgs, identifiers, signatures)
+
+    def _key_for(self, identifier):
+        """getVerkey + DidVerifier for one identifier (authenticate()'s
+        :93-99): the key bytes (None = no key: the verify fails), or the
+        exception authenticate() would raise."""
+        try:
+            verkey = self.getVerkey(identifier)
+            if verkey is None:
+                raise CouldNotAuthenticate('Can not find verkey for DID {}'.format(identifier))
+            return self._resolve_key(verkey, identifier)
+        except SigningException as e:
+            return e
+        except Exception as ex:
+            e = CouldNotAuthenticate()
+            e.__cause__ = ex
+            return e
+
+    @staticmethod
+    def _fresh(e):
+        """A per-message copy of an exception (same class, args, __cause__)."""
+        c = copy.copy(e)
+        c.__cause__ = e.__cause__
+        return c
+
+    def _authenticate_batch_scanned(self, msgs):
+        """authenticate_batch with the host steps in native code: one
+        _hostpack.scan_batch over the dicts (signature / identifier checks,
+        b58decode, serialization, crypto_sign_open's split at byte 64), the
+        verkey resolved once per identifier of the batch, one GPU launch per
+        path.  Messages the scan leaves to Python (odd types, missing fields,
+        bad base58 ...) go through _prepare, which raises the reference's
+        exception."""
+        import numpy as np
+        n = len(msgs)
+        fast, idrs, sig64, mbuf, off, short = _scan_batch(msgs, [SIG])
+        results = [None] * n
+        key_of = {}
+        keys = [None] * n
+        fast_idx = []
+        for i, idr in enumerate(idrs):
+            if idr is None:
+                continue
+            k = key_of.get(idr, _MISSING)
+            if k is _MISSING:
+                k = key_of[idr] = self._key_for(idr)
+            if k is None or k.__class__ is bytes:
+                keys[i] = k
+                fast_idx.append(i)
+            else:
+                results[i] = self._fresh(k)
+        if fast_idx:
+            ok = self._verify_split(fast_idx, keys, sig64, mbuf, off, short)
+            for i, v in zip(fast_idx, ok):
+                results[i] = idrs[i] if v else InvalidSignature()
+        slow = [i for i in range(n) if not fast[i]]
+        if slow:
+            for i, r in zip(slow, self._authenticate_batch_each([msgs[i] for i in slow])):
+                results[i] = r
+        return results
+
+    def _verify_split(self, idx, keys, sig64, mbuf, off, short):
+        """Verdicts of the scanned items idx (split sig64 / messages of the
+        whole batch): registered keys on the key-table path, the rest one
+        general launch, no key -> False."""
+        import numpy as np
+        g = self._g
+        m = len(idx)
+        idx_a = np.asarray(idx, np.uint32)
+        short_a = np.frombuffer(short, np.uint8)[idx_a] != 0
+        ok = np.zeros(m, bool)
+        item_keys = [keys[i] for i in idx]
+        uniq = list(dict.fromkeys(k for k in item_keys if k))
+        ks = self._key_store()
+        kid_of = {}
+        if ks is not None and uniq:
+            if g.hot:
+                got = ks.register(list(g.hot), pinned=uniq, evict=True)
+                g.stats["keys_registered"] += len(got)
+                g.hot.clear()
+            if g.pending:
+                room = ks.free_slots()
+                if room > 0:
+                    got = ks.register([k for k in g.pending if k not in ks][:room], evict=False)
+                    g.stats["keys_registered"] += len(got)
+                g.pending.clear()
+            kid_of = {k: i for k, i in zip(uniq, ks.lookup(uniq)) if i is not None}
+        kid = np.fromiter((kid_of.get(k, -1) if k else -2 for k in item_keys), np.int64, m)
+        keyed = np.nonzero(kid >= 0)[0]
+        general = np.nonzero(kid == -1)[0]
+        eng = self._engine()
+        full = len(idx) == len(keys)
+        for sel, is_keyed in ((keyed, True), (general, False)):
+            if not len(sel):
+                continue
+            if full and len(sel) == m:
+                s_sig, s_msg, s_off = sig64, mbuf, off
+            else:
+                s_sig, s_msg, s_off = _gather_items(sig64, mbuf, off, idx_a[sel].tobytes())
+            s_sig = np.frombuffer(s_sig, np.uint8).reshape(-1, 64)
+            s_msg, s_off = np.frombuffer(s_msg, np.uint8), np.frombuffer(s_off, np.uint64)
+            if is_keyed:
+                v = eng.verify_batch_keyed(s_sig, kid[sel].astype(np.uint32), s_msg, s_off)
+                g.stats["keyed_items"] += len(sel)
+            else:
+                pk = np.frombuffer(b"".join(item_keys[j] for j in sel), np.uint8).reshape(-1, 32)
+                v = eng.verify_batch(s_sig, pk, s_msg, s_off)
+            ok[sel] = np.asarray(v, bool)
+            g.stats["batches"] += 1
+            g.stats["batch_items"] += len(sel)
+        ok &= ~short_a
+        if len(general):
+            gen_ok = ok[general]
+            self._count_verified([_KeyOnly(item_keys[j]) for j in general[gen_ok]], [True] * int(gen_ok.sum()))
+        return ok
+
+    def _authenticate_batch_each(self, msgs, identifiers=None, signatures=None):
         n = len(msgs)
         identifiers = identifiers or [None] * n
         signatures = signatures or [None] * n

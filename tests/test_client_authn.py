@@ -291,3 +291,85 @@ def test_registration_failure_falls_back_to_general(oracle_engine):
     assert a.authenticate_batch(msgs[:3]) == [idrs[0]] * 3
     assert a.authenticate_batch(msgs[3:]) == [idrs[0]] * 3
     assert a.stats["keyed_items"] == 0 and a.stats["keys_registered"] == 0
+
+
+def _outcome(r):
+    if isinstance(r, Exception):
+        return (type(r).__name__, r.args, type(r.__cause__).__name__ if r.__cause__ else None)
+    return r
+
+
+def test_scanned_batch_equals_single_on_kats(oracle):
+    """authenticate_batch's native-scan path (hostpack.scan_batch) gives, per
+    message, exactly what authenticate() gives -- including every reference
+    KAT error case, in one mixed batch over one authenticator."""
+    from plenum_amd import client_authn as CA
+    assert CA._scan_batch is not None
+    cases = [c for c in kat()["cases"] if c["identifier"] is None and c["signature"] is None]
+    for max_keys in (16, 0):
+        eng = OracleEngine(oracle)
+        a = GpuAuthNr(engine=eng, max_keys=max_keys)
+        b = GpuAuthNr(engine=OracleEngine(oracle), max_keys=max_keys)
+        for c in cases:
+            if c["register"] and c["name"] not in ("verkey-31-bytes", "verkey-hex-encoded", "verkey-none",
+                                                   "verkey-non-base58", "verkey-abbrev-15-bytes"):
+                idr = c["msg"].get("identifier")
+                a.addIdr(idr, c["verkey"])
+                b.addIdr(idr, c["verkey"])
+        msgs = [fix_case(c) for c in cases] * 3
+        got = [_outcome(r) for r in a.authenticate_batch(msgs)]
+        want = []
+        for m in msgs:
+            try:
+                want.append(_outcome(b.authenticate(m)))
+            except Exception as ex:
+                want.append(_outcome(ex))
+        assert got == want
+
+
+def test_scanned_batch_fuzz(oracle):
+    """Random request dicts (valid, tampered, odd field types, missing / empty
+    fields, non-base58, short signatures): scanned batch == per-message."""
+    import random
+    idrs, vks, msgs = _signed(3, 60, seed=9)
+    rnd = random.Random(5)
+    pool = []
+    for m in msgs:
+        m = dict(m)
+        r = rnd.random()
+        if r < 0.1:
+            m["reqId"] += 1
+        elif r < 0.15:
+            m["signature"] = ""
+        elif r < 0.2:
+            del m["signature"]
+        elif r < 0.25:
+            m["identifier"] = ""
+        elif r < 0.3:
+            m["signature"] = m["signature"][:20]
+        elif r < 0.35:
+            m["signature"] = "0" + m["signature"]
+        elif r < 0.4:
+            m["operation"] = {"type": "1", "x": (1, 2)}
+        elif r < 0.45:
+            m["extra"] = [1, 2.5, None, True, {"k": "v"}]
+        elif r < 0.5:
+            m["identifier"] = "unknownIdr"
+        elif r < 0.55:
+            m["signature"] = 12345
+        pool.append(m)
+    for max_keys in (16, 0):
+        a = GpuAuthNr(engine=OracleEngine(oracle), max_keys=max_keys)
+        b = GpuAuthNr(engine=OracleEngine(oracle), max_keys=max_keys)
+        for idr, vk in zip(idrs, vks):
+            a.addIdr(idr, vk)
+            b.addIdr(idr, vk)
+        got = [_outcome(r) for r in a.authenticate_batch(pool)]
+        want = []
+        for m in pool:
+            try:
+                want.append(_outcome(b.authenticate(m)))
+            except Exception as ex:
+                want.append(_outcome(ex))
+        assert got == want
+        assert sum(isinstance(x, str) for x in got) > 10
