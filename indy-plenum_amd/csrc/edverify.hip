@@ -6,7 +6,8 @@
 //   general path (any 32-byte key per request):
 //     edv_hash_kernel    prechecks + SHA-512(R||A||M) mod L, one lane per request
 //     edv_table_kernel   decode -A, cached [1..8](-A) in per-block SoA scratch
-//     edv_dsm_kernel     [h](-A) + [S]B, signed radix-16, B multiples in LDS
+//     edv_dsm_kernel     [h](-A) + [S]B: signed radix-16 windows over the
+//                        lane's cached multiples, [S]B from the base comb (HBM)
 //   key-table path (registered keys, comb.h):
 //     edv_hash_keyed_kernel, edv_comb_kernel<W>  fixed-base combs, no doublings
 //   both paths end in
