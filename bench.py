@@ -193,6 +193,56 @@ def reference_path_baseline(eng, n, host):
     return out
 
 
+def general_dsm_roofline(eng, d_pk, n, o_ms):
+    """The general path's ladder kernel against the MAD peak, priced at the
+    implementation's own count for the split it ran (roofline.mad_dsm_kernel:
+    K tables per distinct key, decided per sub-batch from its distinct-key
+    count, reproduced here from the same keys)."""
+    pk = d_pk.cpu().numpy()
+    launches = eng.last_launch_count()
+    per = -(-min(n, 1 << 20) // launches)
+    splits = []
+    for s0 in range(0, min(n, 1 << 20), per):
+        sub = pk[s0:s0 + per]
+        splits.append(RL.split_of(len(np.unique(sub.view(np.dtype((np.void, 32))))), len(sub)))
+    k = splits[0]
+    dsm_ms = float(np.mean(np.array(o_ms), axis=0)[2]) / launches
+    mad = RL.mad_dsm_kernel(k)
+    achieved = per * mad / (dsm_ms * 1e-3) / 1e12
+    return {"split_tables": k, "dsm_kernel_mad_per_request": mad,
+            "dsm_roofline": {"bound": "valu-mad", "achieved": achieved, "peak": RL.PEAK_MAD_PER_S / 1e12,
+                             "unit": "T MAD/s", "frac": achieved / (RL.PEAK_MAD_PER_S / 1e12),
+                             "work": "fe_dsm_split(%d) = %d field ops x 100 MAD" % (k, RL.fe_dsm_split(k))}}
+
+
+def time_general_distinct(eng, args, n, d_msgs, d_ms, d_me, stream, steps=3):
+    """General path with every request signed by a key of its own (n keys;
+    the dedupe finds no sharing, K = 1): the worst case of the general path,
+    on the same messages."""
+    dev = d_msgs.device
+    pks, sks = eng.seed_keypair_batch(synth.signer_seeds(n))
+    d_k = torch.arange(n, dtype=torch.int32, device=dev)
+    d_sig = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+    eng.sign_spans_device(torch.from_numpy(sks).to(dev), d_k, d_msgs, d_ms, d_me, n, d_sig)
+    d_pk = torch.from_numpy(pks).to(dev)
+    words = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
+    eng.verify_spans_device(d_sig, d_pk, False, d_msgs, d_ms, d_me, n, words, stream=stream)
+    torch.cuda.synchronize()
+    ms = []
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng.verify_spans_device(d_sig, d_pk, False, d_msgs, d_ms, d_me, n, words, stream=stream)
+        ms.append(eng.last_phases_ms())
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    bits = np.unpackbits(words.cpu().numpy().view(np.uint8), bitorder="little")[:n]
+    out = {"value": n * steps / el, "keys": n, "all_accepted": bool(bits.all()),
+           "phase_ms": dict(zip(("hash", "table", "dsm", "encode"),
+                                (float(v) for v in np.mean(np.array(ms), axis=0))))}
+    out.update(general_dsm_roofline(eng, d_pk, n, ms))
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -409,6 +459,10 @@ def main():
                  "phase_ms": dict(zip(("hash", "table", "dsm_or_comb", "encode"),
                                       (float(v) for v in np.mean(np.array(o_ms), axis=0)))),
                  "same_verdicts": bool((og == got).all())}
+        if args.path == "keyed":
+            other.update(general_dsm_roofline(eng, d_pk, n, o_ms))
+            if args.config == "c1" and rank == 0:
+                other["distinct_keys"] = time_general_distinct(eng, args, n, d_msgs, d_ms, d_me, stream)
 
     total = n * world * args.steps
     value = total / elapsed
@@ -418,7 +472,10 @@ def main():
     n_chunk = eng.last_chunk_items()  # the phase times cover the last 2^20-request chunk
     dsm_sum = float(ph[2])
     dsm_avg = dsm_sum / launches
-    kernel_mad = RL.mad_comb_kernel(args.key_window) if args.path == "keyed" else RL.MAD_DSM_KERNEL
+    if args.path == "keyed":
+        kernel_mad = RL.mad_comb_kernel(args.key_window)
+    else:
+        kernel_mad = general_dsm_roofline(eng, d_pk, n, phases)["dsm_kernel_mad_per_request"]
     kernel_name = "edv_comb_kernel" if args.path == "keyed" else "edv_dsm_kernel"
     achieved = (n_chunk / launches) * kernel_mad / (dsm_avg * 1e-3) / 1e12
     peak = RL.PEAK_MAD_PER_S / 1e12

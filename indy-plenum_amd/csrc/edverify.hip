@@ -5,7 +5,9 @@
 // Kernels (one HIP stream per context):
 //   general path (any 32-byte key per request):
 //     edv_hash_kernel    prechecks + SHA-512(R||A||M) mod L, one lane per request
-//     edv_table_kernel   decode -A, cached [1..8](-A) in per-block SoA scratch
+//     edv_dedup_*        distinct keys of the sub-batch (hash table in HBM)
+//     edv_table_kernel   per distinct key: decode -A, cached [1..8](-A) (AoS);
+//                        4 tables [1..8]2^(64t)(-A) for keys with >= 4 requests
 //     edv_dsm_kernel     [h](-A) + [S]B: signed radix-16 windows over the
 //                        lane's cached multiples, [S]B from the base comb (HBM)
 //   key-table path (registered keys, comb.h):
@@ -77,6 +79,7 @@ struct DevTableA {
   uint32_t* __restrict__ base;  // this lane's 9 entries
   __device__ DevTableA(uint32_t* scratch, uint32_t block, uint32_t lane)
       : base((uint32_t*)((char*)scratch + (uint64_t)block * kRegionBytes) + lane * kTableWords) {}
+  __device__ DevTableA(uint32_t* scratch, uint64_t slot) : base(scratch + slot * kTableWords) {}
   __device__ void store(int j, const ge_cached& c) const {
     uint4* p = (uint4*)(base + j * 40);
     uint32_t w[40];
@@ -108,6 +111,20 @@ struct DevTableA {
       c.Z.v[l] = w[20 + l];
       c.T2d.v[l] = w[30 + l];
     }
+  }
+};
+
+// K tables of one distinct key, consecutive slots (u * K + t) of the scratch
+struct DevTableSplit {
+  uint32_t* __restrict__ base;
+  __device__ DevTableSplit(uint32_t* scratch, uint64_t first_slot) : base(scratch + first_slot * kTableWords) {}
+  __device__ void store(int t, int j, const ge_cached& c) const {
+    DevTableA a(base, (uint64_t)t);
+    a.store(j, c);
+  }
+  __device__ void load(int t, int j, ge_cached& c) const {
+    const DevTableA a(base, (uint64_t)t);
+    a.load(j, c);
   }
 };
 
@@ -180,16 +197,106 @@ __global__ __launch_bounds__(kBlock, EDV_HASH_MIN_WAVES) void edv_hash_kernel(co
 #ifndef EDV_TABLE_MIN_WAVES
 #define EDV_TABLE_MIN_WAVES 2  // 168 VGPRs (+spill) beats 256+256 AGPRs at 1 wave: table -8%
 #endif
-__global__ __launch_bounds__(kBlock, EDV_TABLE_MIN_WAVES) void edv_table_kernel(const uint8_t* __restrict__ pk32, uint64_t n,
-                                                          uint32_t* __restrict__ table, uint8_t* __restrict__ flags,
-                                                          uint64_t stride) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+// ---- general path, distinct keys of a sub-batch: the table kernel decodes
+// each distinct 32-byte key once (a batch of 1M requests from 1,000 signers
+// builds 1,000 tables, not 1M).  Open-addressing hash table over the
+// sub-batch: slot = request index of the key's representative (0xffffffff =
+// empty); the full 32 bytes are compared, so distinct keys never share a
+// table whatever their hash.  Which request becomes the representative
+// depends on the order of the atomics; the table -- a function of the key
+// bytes only -- does not.
+constexpr uint32_t kEmptySlot = 0xffffffffu;
+__device__ __forceinline__ uint32_t key_hash(const uint32_t pk[8]) {
+  uint32_t h = pk[0] * 0x9e3779b1u;
+  h ^= pk[1] * 0x85ebca77u;
+  h ^= (pk[2] ^ pk[5]) * 0xc2b2ae3du;
+  h ^= (pk[3] ^ pk[7]) * 0x27d4eb2fu;
+  return h ^ (h >> 15);
+}
+__device__ __forceinline__ bool same_key(const uint8_t* __restrict__ pk32, uint64_t a, const uint32_t pk[8]) {
+  uint32_t w[8];
+  load_words(w, pk32 + 32 * a, 8);
+  bool eq = true;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) eq = eq && w[k] == pk[k];
+  return eq;
+}
+// slot of request i's key (inserting i as the representative if new)
+__device__ uint32_t dedup_slot(const uint8_t* __restrict__ pk32, uint64_t i, uint32_t* __restrict__ slots,
+                               uint32_t nslots, bool insert) {
   uint32_t pk[8];
   load_words(pk, pk32 + 32 * i, 8);
-  DevTableA ta(table, blockIdx.x, threadIdx.x);
-  const bool ok = verify_phase_table(pk, ta);
-  if (!ok) flags[i] = 0;
+  uint32_t h = key_hash(pk) % nslots;
+  for (uint32_t probe = 0; probe < nslots; ++probe) {
+    uint32_t s = __atomic_load_n(&slots[h], __ATOMIC_RELAXED);
+    if (s == kEmptySlot) {
+      if (!insert) return kEmptySlot;  // unreachable after the insert pass
+      s = atomicCAS(&slots[h], kEmptySlot, (uint32_t)i);
+      if (s == kEmptySlot) return h;
+    }
+    if (s == (uint32_t)i || same_key(pk32, s, pk)) return h;
+    h = h + 1 == nslots ? 0 : h + 1;
+  }
+  return kEmptySlot;  // table full: impossible with nslots = 2n
+}
+// every request records its key's slot
+__global__ __launch_bounds__(kBlock) void edv_dedup_insert_kernel(const uint8_t* __restrict__ pk32, uint64_t n,
+                                                                 uint32_t* __restrict__ slots, uint32_t nslots,
+                                                                 uint32_t* __restrict__ req_slot) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  req_slot[i] = dedup_slot(pk32, i, slots, nslots, true);
+}
+// representative -> compact key index u (reps[u] = its request)
+__global__ __launch_bounds__(kBlock) void edv_dedup_assign_kernel(uint64_t n, const uint32_t* __restrict__ slots,
+                                                                 const uint32_t* __restrict__ req_slot,
+                                                                 uint32_t* __restrict__ slot_u,
+                                                                 uint32_t* __restrict__ reps,
+                                                                 uint32_t* __restrict__ count) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t h = req_slot[i];
+  if (slots[h] == (uint32_t)i) {
+    const uint32_t u = atomicAdd(count, 1u);
+    slot_u[h] = u;
+    reps[u] = (uint32_t)i;
+  }
+}
+
+// Tables per distinct key: K = 8 with at least 16 requests per distinct key
+// in the sub-batch, K = 4 with at least 4, else 1.  The K tables of all keys
+// then fit the sub-batch's scratch (K * count <= n), and the 256 (K-1)/K
+// extra doublings per key cost at most 256 (K-1)/K^2 per request against
+// 256 (K-1)/K saved in every ladder.  Decided on the device from the
+// distinct-key count, identically by the table and ladder kernels.
+__device__ __forceinline__ int split_of(uint32_t count, uint64_t n) {
+  return 16ull * count <= n ? 8 : 4ull * count <= n ? 4 : 1;
+}
+
+// Tables of distinct key u (u < *count): decode -A of request reps[u]'s key,
+// the K tables into slots u*K.., key_ok[u] = the key decodes.
+__global__ __launch_bounds__(kBlock, EDV_TABLE_MIN_WAVES) void edv_table_kernel(const uint8_t* __restrict__ pk32,
+                                                          uint64_t n, const uint32_t* __restrict__ reps,
+                                                          const uint32_t* __restrict__ count,
+                                                          uint32_t* __restrict__ table, uint8_t* __restrict__ key_ok) {
+  const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t cnt = *count;
+  if (u >= cnt) return;
+  uint32_t pk[8];
+  load_words(pk, pk32 + 32 * (uint64_t)reps[u], 8);
+  bool ok;
+  const int k = split_of(cnt, n);
+  if (k == 8) {
+    const DevTableSplit tas(table, 8 * u);
+    ok = verify_phase_table_split<8>(pk, tas);
+  } else if (k == 4) {
+    const DevTableSplit tas(table, 4 * u);
+    ok = verify_phase_table_split<4>(pk, tas);
+  } else {
+    DevTableA ta(table, u);
+    ok = verify_phase_table(pk, ta);
+  }
+  key_ok[u] = ok ? 1 : 0;
 }
 
 // Result points R' = (X : Y : Z), SoA [30][stride]: word w of request i at
@@ -248,17 +355,34 @@ __global__ __launch_bounds__(kBlock, EDV_DSM_MIN_WAVES) void edv_dsm_kernel(cons
                                                         uint32_t* __restrict__ table, uint64_t stride,
                                                         const uint32_t* __restrict__ btab_comb,
                                                         const uint32_t* __restrict__ ident,
-                                                        uint32_t* __restrict__ pt) {
+                                                        uint32_t* __restrict__ pt,
+                                                        const uint32_t* __restrict__ req_slot,
+                                                        const uint32_t* __restrict__ slot_u,
+                                                        const uint32_t* __restrict__ count,
+                                                        const uint8_t* __restrict__ key_ok,
+                                                        uint8_t* __restrict__ flags) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t S[8], h[8];
   load_words(S, sig64 + 64 * i + 32, 8);
 #pragma unroll
   for (int k = 0; k < 8; ++k) h[k] = h_soa[k * stride + i];
-  const DevTableA ta(table, blockIdx.x, threadIdx.x);
+  const uint32_t u = slot_u[req_slot[i]];
+  if (!key_ok[u]) flags[i] = 0;  // the key does not decode: reject (the table is still written, so the ladder runs)
   const DevComb<kBaseW> cb{btab_comb, ident};
   ge_p3 Q;
-  const uint32_t sink = verify_phase_dsm_point(Q, h, S, ta, cb);
+  uint32_t sink;
+  const int split = split_of(*count, n);
+  if (split == 8) {
+    const DevTableSplit tas(table, 8ull * u);
+    sink = verify_phase_dsm_split_point<8>(Q, h, S, tas, cb);
+  } else if (split == 4) {
+    const DevTableSplit tas(table, 4ull * u);
+    sink = verify_phase_dsm_split_point<4>(Q, h, S, tas, cb);
+  } else {
+    const DevTableA ta(table, (uint64_t)u);
+    sink = verify_phase_dsm_point(Q, h, S, ta, cb);
+  }
   store_point_soa(pt, stride, i, Q);
   if (sink == 0x9e3779b9u && stride == 0) pt[i] = sink;  // keeps the prefetches live
 }
@@ -735,6 +859,13 @@ struct edv_ctx {
   uint32_t* d_pre = nullptr;      // batch-encode prefix products, SoA [10][kMaxLanes]
   uint32_t* d_perm = nullptr;     // length-bucket order of the hash lanes [kMaxLanes]
   uint8_t* d_lenkey = nullptr;    // block-count keys, in | sorted [2][kMaxLanes]
+  // general-path key dedupe (per sub-batch at its lane offset): hash slots
+  // [2][kMaxLanes] (2 per lane), slot -> key index [2][kMaxLanes], request ->
+  // slot, key index -> representative request [kMaxLanes] each; key_ok
+  // [kMaxLanes]; distinct-key counts [kSub]
+  uint32_t* d_dedup = nullptr;
+  uint8_t* d_key_ok = nullptr;
+  uint32_t* d_ucount = nullptr;
   void* d_sort_tmp = nullptr;     // radix-sort temporary storage, one slot per sub-batch
   size_t sort_tmp_bytes = 0;      // per slot (sized for kMaxLanes)
   int bucket_mode = 2;            // edv_set_length_buckets: 0 off, 1 on, 2 auto
@@ -749,6 +880,10 @@ struct edv_ctx {
   static constexpr int kSub = 4;
   static constexpr int kEv = 5;
   hipStream_t stream2 = nullptr;
+  // general path: a sub-batch's key dedupe + tables run on stream_key while
+  // its hash kernel runs (both read only the keys); the ladder waits for both
+  hipStream_t stream_key = nullptr;
+  hipEvent_t ev_kfork[kSub] = {}, ev_kjoin[kSub] = {};
   hipEvent_t ev_sub[kSub][kEv] = {};
   hipEvent_t ev_join[2] = {};
   int last_nsub = 0;
@@ -919,15 +1054,36 @@ int launch_sub(edv_ctx* ctx, bool keyed, const SubBatch& b, const uint8_t* msgs,
     // the per-lane A tables are per 256-lane block of the chunk: sub-batch
     // offsets are multiples of the block size, so each sub-batch has its own
     uint32_t* tab = (uint32_t*)((char*)ctx->d_scratch + (b.soff / kBlock) * (uint64_t)kRegionBytes);
+    const uint64_t L = kMaxLanes;
+    uint32_t* slots = ctx->d_dedup + 2 * b.soff;
+    uint32_t* slot_u = ctx->d_dedup + 2 * L + 2 * b.soff;
+    uint32_t* req_slot = ctx->d_dedup + 4 * L + b.soff;
+    uint32_t* reps = ctx->d_dedup + 5 * L + b.soff;
+    uint8_t* key_ok = ctx->d_key_ok + b.soff;
+    uint32_t* count = ctx->d_ucount + sub;
+    const uint32_t nslots = (uint32_t)(2 * b.cn);
+    hipStream_t qk = ctx->stream_key;
+    HIP_TRY(hipEventRecord(ctx->ev_kfork[sub], q));
+    HIP_TRY(hipStreamWaitEvent(qk, ctx->ev_kfork[sub], 0));
+    HIP_TRY(hipMemsetAsync(slots, 0xff, nslots * sizeof(uint32_t), qk));
+    HIP_TRY(hipMemsetAsync(count, 0, sizeof(uint32_t), qk));
+    hipLaunchKernelGGL(edv_dedup_insert_kernel, dim3(grid), dim3(kBlock), 0, qk, b.pk, b.cn, slots, nslots, req_slot);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(edv_dedup_assign_kernel, dim3(grid), dim3(kBlock), 0, qk, b.cn, slots, req_slot, slot_u, reps,
+                       count);
+    HIP_TRY(hipGetLastError());
+    // one lane per distinct key; the grid covers the worst case (all distinct)
+    hipLaunchKernelGGL(edv_table_kernel, dim3(grid), dim3(kBlock), 0, qk, b.pk, b.cn, reps, count, tab, key_ok);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(ctx->ev_kjoin[sub], qk));
     hipLaunchKernelGGL(edv_hash_kernel, dim3(grid), dim3(kBlock), 0, q, b.sig, b.pk, msgs, b.ms, b.me, b.cn, hs, fl,
                        chunk, perm);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ev[1], q));
-    hipLaunchKernelGGL(edv_table_kernel, dim3(grid), dim3(kBlock), 0, q, b.pk, b.cn, tab, fl, chunk);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(ev[2], q));
+    HIP_TRY(hipStreamWaitEvent(q, ctx->ev_kjoin[sub], 0));
+    HIP_TRY(hipEventRecord(ev[2], q));  // hash | key tables not hidden behind it | ladder
     hipLaunchKernelGGL(edv_dsm_kernel, dim3(grid), dim3(kBlock), 0, q, b.sig, b.cn, hs, tab, chunk, ctx->d_btab_comb32,
-                       ctx->d_ident, pt);
+                       ctx->d_ident, pt, req_slot, slot_u, count, key_ok, fl);
     HIP_TRY(hipGetLastError());
   }
   HIP_TRY(hipEventRecord(ev[3], q));
@@ -1303,6 +1459,12 @@ edv_ctx* edv_create(int device) {
     return fail("hipStreamCreate", e);
   if ((e = hipStreamCreateWithFlags(&ctx->stream_copy, hipStreamNonBlocking)) != hipSuccess)
     return fail("hipStreamCreate", e);
+  if ((e = hipStreamCreateWithFlags(&ctx->stream_key, hipStreamNonBlocking)) != hipSuccess)
+    return fail("hipStreamCreate", e);
+  for (int sb = 0; sb < edv_ctx::kSub; ++sb)
+    if ((e = hipEventCreateWithFlags(&ctx->ev_kfork[sb], hipEventDisableTiming)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&ctx->ev_kjoin[sb], hipEventDisableTiming)) != hipSuccess)
+      return fail("hipEventCreate", e);
   for (int k = 0; k < edv_ctx::kSlots; ++k)
     if ((e = hipEventCreateWithFlags(&ctx->ev_h2d[k], hipEventDisableTiming)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&ctx->ev_done[k], hipEventDisableTiming)) != hipSuccess)
@@ -1348,6 +1510,11 @@ edv_ctx* edv_create(int device) {
   if ((e = hipMalloc(&ctx->d_perm, ctx->scratch_lanes * sizeof(uint32_t))) != hipSuccess)
     return fail("hipMalloc(perm)", e);
   if ((e = hipMalloc(&ctx->d_lenkey, 2 * ctx->scratch_lanes)) != hipSuccess) return fail("hipMalloc(lenkey)", e);
+  if ((e = hipMalloc(&ctx->d_dedup, 6 * ctx->scratch_lanes * sizeof(uint32_t))) != hipSuccess)
+    return fail("hipMalloc(dedup)", e);
+  if ((e = hipMalloc(&ctx->d_key_ok, ctx->scratch_lanes)) != hipSuccess) return fail("hipMalloc(key_ok)", e);
+  if ((e = hipMalloc(&ctx->d_ucount, edv_ctx::kSub * sizeof(uint32_t))) != hipSuccess)
+    return fail("hipMalloc(ucount)", e);
   if ((e = rocprim::radix_sort_pairs_desc(nullptr, ctx->sort_tmp_bytes, ctx->d_lenkey, ctx->d_lenkey + kMaxLanes,
                                           rocprim::counting_iterator<uint32_t>(0), ctx->d_perm,
                                           (uint32_t)ctx->scratch_lanes, 0, kLenKeyBits, ctx->stream)) != hipSuccess)
@@ -1367,6 +1534,8 @@ void edv_destroy(edv_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->stream_copy) (void)hipStreamSynchronize(ctx->stream_copy);
+  if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
+  if (ctx->stream_key) (void)hipStreamSynchronize(ctx->stream_key);
   for (edv_ctx::Buf* b : {&ctx->b_sig, &ctx->b_pk, &ctx->b_msg, &ctx->b_off, &ctx->b_bits, &ctx->b_aux}) free_buf(*b);
   for (int k = 0; k < edv_ctx::kSlots; ++k) {
     for (edv_ctx::Buf* b : {&ctx->h_sig[k], &ctx->h_key[k], &ctx->h_msg[k], &ctx->h_off[k], &ctx->h_bits[k],
@@ -1381,6 +1550,9 @@ void edv_destroy(edv_ctx* ctx) {
   if (ctx->d_pt) (void)hipFree(ctx->d_pt);
   if (ctx->d_perm) (void)hipFree(ctx->d_perm);
   if (ctx->d_lenkey) (void)hipFree(ctx->d_lenkey);
+  if (ctx->d_dedup) (void)hipFree(ctx->d_dedup);
+  if (ctx->d_key_ok) (void)hipFree(ctx->d_key_ok);
+  if (ctx->d_ucount) (void)hipFree(ctx->d_ucount);
   if (ctx->d_sort_tmp) (void)hipFree(ctx->d_sort_tmp);
   if (ctx->d_ident) (void)hipFree(ctx->d_ident);
   if (ctx->d_pre) (void)hipFree(ctx->d_pre);
@@ -1389,13 +1561,16 @@ void edv_destroy(edv_ctx* ctx) {
   if (ctx->d_key_pk) (void)hipFree(ctx->d_key_pk);
   if (ctx->d_key_valid) (void)hipFree(ctx->d_key_valid);
   if (ctx->d_key_tab) (void)hipFree(ctx->d_key_tab);
-  if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
-  for (int sb = 0; sb < edv_ctx::kSub; ++sb)
+  for (int sb = 0; sb < edv_ctx::kSub; ++sb) {
     for (int k = 0; k < edv_ctx::kEv; ++k)
       if (ctx->ev_sub[sb][k]) (void)hipEventDestroy(ctx->ev_sub[sb][k]);
+    if (ctx->ev_kfork[sb]) (void)hipEventDestroy(ctx->ev_kfork[sb]);
+    if (ctx->ev_kjoin[sb]) (void)hipEventDestroy(ctx->ev_kjoin[sb]);
+  }
   for (int k = 0; k < 2; ++k)
     if (ctx->ev_join[k]) (void)hipEventDestroy(ctx->ev_join[k]);
   if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
+  if (ctx->stream_key) (void)hipStreamDestroy(ctx->stream_key);
   if (ctx->stream_copy) (void)hipStreamDestroy(ctx->stream_copy);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;

@@ -19,6 +19,12 @@ struct HostTableA {
   void store(int j, const ge_cached& c) { e[j] = c; }
   void load(int j, ge_cached& c) const { c = e[j >= 0 ? j : 8]; }
 };
+template <int K>
+struct HostTableSplit {
+  HostTableA t[K];
+  void store(int s, int j, const ge_cached& c) const { const_cast<HostTableA&>(t[s]).store(j, c); }
+  void load(int s, int j, ge_cached& c) const { t[s].load(j, c); }
+};
 // A comb table in host memory (comb.h layout).
 template <int W>
 struct HostComb {
@@ -69,6 +75,35 @@ int edv_host_verify(const uint8_t* sig64, const uint8_t* pk32, const uint8_t* ms
   HostTableA ta;
   const HostComb<kBaseW> cb{base_comb()};
   return verify_one(sig, pk, msg, mlen, ta, cb) ? 0 : -1;
+}
+
+// The general path's split-table ladder (K tables of 2^(256t/K)(-A)), as
+// edv_table_kernel / edv_dsm_kernel run it for keys shared by >= 4 requests.
+int edv_host_verify_split(const uint8_t* sig64, const uint8_t* pk32, const uint8_t* msg, uint64_t mlen, int k) {
+  uint32_t sig[16], pk[8], h[8];
+  memcpy(sig, sig64, 64);
+  memcpy(pk, pk32, 32);
+  const HostComb<kBaseW> cb{base_comb()};
+  bool ok = verify_phase_hash(h, sig, pk, msg, mlen);
+  ge_p3 Q;
+  if (k == 8) {
+    HostTableSplit<8> tas;
+    ok = verify_phase_table_split<8>(pk, tas) && ok;
+    verify_phase_dsm_split_point<8>(Q, h, sig + 8, tas, cb);
+  } else if (k == 4) {
+    HostTableSplit<4> tas;
+    ok = verify_phase_table_split<4>(pk, tas) && ok;
+    verify_phase_dsm_split_point<4>(Q, h, sig + 8, tas, cb);
+  } else if (k == 2) {
+    HostTableSplit<2> tas;
+    ok = verify_phase_table_split<2>(pk, tas) && ok;
+    verify_phase_dsm_split_point<2>(Q, h, sig + 8, tas, cb);
+  } else {
+    HostTableSplit<1> tas;
+    ok = verify_phase_table_split<1>(pk, tas) && ok;
+    verify_phase_dsm_split_point<1>(Q, h, sig + 8, tas, cb);
+  }
+  return encode_equals(Q, sig) && ok ? 0 : -1;
 }
 
 void edv_host_sha512_prefixed(uint8_t out[64], const uint8_t prefix64[64], const uint8_t* msg, uint64_t mlen) {

@@ -152,6 +152,89 @@ EDV_HD uint32_t verify_phase_dsm_point(ge_p3& Q, const uint32_t h[8], const uint
   return comb_mul_add<kBaseW>(Q, S, cb);  // the base comb's prefetch sink (comb.h)
 }
 
+// Split tables for keys shared by many requests (the general path's distinct
+// keys, edverify.hip): h = sum_t h_t 2^(256 t / K), t < K, and table t holds
+// [1..8] 2^(256 t / K)(-A), so the ladder runs 256 / K - 4 doublings instead
+// of 252 and the same 64 additions; the K - 1 extra tables cost 256 (K-1)/K
+// doublings once per key.  TAS::store(t, j, c) / TAS::load(t, j, c) address
+// table t (j = -1: the identity).  Same point as verify_phase_dsm_point
+// (another order of the same group operations).
+template <int K, class TAS>
+EDV_HD bool verify_phase_table_split(const uint32_t pk[8], const TAS& tas) {
+  ge_p3 P;
+  const bool ok = ge_frombytes(P, pk, true);
+#pragma unroll 1
+  for (int t = 0; t < K; ++t) {
+    if (t > 0) {  // P = 2^(256/K) P
+      ge_p2 q2;
+      ge_p1p1 d;
+      ge_p3_to_p2(q2, P);
+#pragma unroll 1
+      for (int k = 0; k < 256 / K - 1; ++k) {
+        ge_p2_dbl(d, q2);
+        ge_dbl_to_p2(q2, d);
+      }
+      ge_p2_dbl(d, q2);
+      ge_dbl_to_p3(P, d);
+    }
+    ge_cached c;
+    ge_p3 acc = P;
+    ge_p1p1 u;
+    ge_p3_to_cached(c, acc);
+    tas.store(t, 0, c);
+    const ge_cached a1 = c;
+#pragma unroll 1
+    for (int j = 1; j < 8; ++j) {
+      ge_add(u, acc, a1);
+      ge_p1p1_to_p3_addlike(acc, u);
+      ge_p3_to_cached(c, acc);
+      tas.store(t, j, c);
+    }
+    ge_cached_0(c);
+    tas.store(t, 8, c);
+  }
+  return ok;
+}
+
+template <int K, class TAS, class CB>
+EDV_HD uint32_t verify_phase_dsm_split_point(ge_p3& Q, const uint32_t h[8], const uint32_t S[8], const TAS& tas,
+                                             const CB& cb) {
+  constexpr int kWords = 8 / K;       // recoded words per table
+  constexpr int kDigits = 8 * kWords;  // radix-16 digits per table
+  uint32_t hy[8];
+  sc_recode16(hy, h);
+  ge_p3_0(Q);
+  ge_p1p1 t;
+#pragma unroll 1
+  for (int i = kDigits - 1; i >= 0; --i) {
+    if (i != kDigits - 1) {
+      ge_p2 q2;
+      ge_p3_to_p2(q2, Q);
+      ge_p2_dbl(t, q2);
+      ge_dbl_to_p2(q2, t);
+      ge_p2_dbl(t, q2);
+      ge_dbl_to_p2(q2, t);
+      ge_p2_dbl(t, q2);
+      ge_dbl_to_p2(q2, t);
+      ge_p2_dbl(t, q2);
+      ge_dbl_to_p3(Q, t);
+    }
+#pragma unroll
+    for (int s = K - 1; s >= 0; --s) {
+      uint32_t* w = hy + s * kWords;
+      const int e = (int)(w[kWords - 1] >> 28) - 8;  // digit s * kDigits + i
+#pragma unroll
+      for (int k = kWords - 1; k > 0; --k) w[k] = funnel32(w[k], w[k - 1], 28);
+      w[0] <<= 4;
+      const int m = e < 0 ? -e : e;
+      ge_cached c;
+      tas.load(s, m - 1, c);
+      ge_add_signed(Q, Q, c, e < 0);
+    }
+  }
+  return comb_mul_add<kBaseW>(Q, S, cb);
+}
+
 // encode(R') == R byte for byte (per-request inversion; the kernels batch it).
 EDV_HD bool encode_equals(const ge_p3& Q, const uint32_t R[8]) {
   ge_p2 r2;

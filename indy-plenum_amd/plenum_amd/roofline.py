@@ -24,12 +24,31 @@ MAD_PER_VERIFY = 305_000
 # a-priori ref10 count); edv_table_kernel the decode of A.
 MAD_DSM_KERNEL = FE_DSM * MAD_PER_FE  # 251,000
 MAD_TABLE_KERNEL = FE_DECODE * MAD_PER_FE
+
+
+# The implementation's edv_dsm_kernel with K split tables per distinct key
+# (verify_core.h verify_phase_dsm_split_point): 64/K - 1 steps of 4 doublings
+# (3 x (4 sq + 3 mul) + (4 sq + 4 mul) = 29 field ops), 64 cached additions
+# (4 + 4 field ops), 12 base-comb mixed additions (7).  K = 1: 2,423 field ops
+# (ref10's 2,510 less its sliding-window bookkeeping); K = 4: 1,031; K = 8: 799.
+def fe_dsm_split(k):
+    return (64 // k - 1) * 29 + 64 * 8 + BASE_ROWS_DSM * 7
+
+
+def mad_dsm_kernel(k):
+    return fe_dsm_split(k) * MAD_PER_FE
+
+
+def split_of(distinct, n):
+    """edverify.hip split_of: tables per distinct key of a sub-batch."""
+    return 8 if 16 * distinct <= n else 4 if 4 * distinct <= n else 1
 # Key-table path (keys registered once): edv_comb_kernel<W> = fixed-base combs
 # over both tables -- ceil(254 / W) rows of the key table + ceil(254 / 22) = 12
 # rows of the W = 22 base table (verify_core.h kBaseW) -- one mixed addition
 # (7 multiplications) per row, except the key comb's row 0, which is set with
 # one multiplication (comb.h comb_set).
 BASE_W = 22
+BASE_ROWS_DSM = (254 + BASE_W - 1) // BASE_W
 
 
 def key_rows(w):
@@ -57,7 +76,8 @@ def kernel_work(name, w=8):
         return ("((%d - 1 key rows (W=%d; row 0 set with 1 field op) + %d base rows (W=%d)) mixed additions "
                 "x 7 field ops + 1) x 100 MAD" % (key_rows(w), w, BASE_ROWS, BASE_W))
     if name == "edv_dsm_kernel":
-        return "2510 field ops (ref10 a-priori double-scalar multiplication) x 100 MAD"
+        return ("((64/K - 1) x 29 + 64 x 8 + 12 x 7) field ops x 100 MAD (K split tables per distinct key, "
+                "roofline.fe_dsm_split)")
     return ""
 
 

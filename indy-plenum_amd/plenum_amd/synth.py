@@ -19,7 +19,11 @@ REQ_ID_BASE = 1_500_000_000_000_000
 
 
 def signer_seeds(n_signers):
-    return np.stack([np.frombuffer(i.to_bytes(2, "little") + b"\0" * 30, np.uint8) for i in range(n_signers)])
+    """Seed i = i little-endian in the first bytes, zeros after (i < 2^16: the
+    C0 seeds; larger counts -- distinct-key batches -- use 4 bytes)."""
+    seeds = np.zeros((n_signers, 32), np.uint8)
+    seeds[:, :4] = np.arange(n_signers, dtype="<u4").view(np.uint8).reshape(-1, 4)
+    return seeds
 
 
 def _pool(rng, n, nbytes):

@@ -68,6 +68,52 @@ def test_random_batch_vs_oracle(gpu_engine, oracle):
     assert 0.5 < want.mean() < 0.75
 
 
+def test_general_key_dedupe(gpu_engine, oracle):
+    """General path, distinct-key dedupe (edv_dedup_*): requests share keys;
+    keys that differ only in words the slot hash ignores (bytes 16..19 and
+    24..27) collide in the hash table and must still get their own tables;
+    a non-decodable key repeated across requests rejects all of them."""
+    rng = np.random.default_rng(11)
+    pk, sk = gpu_engine.seed_keypair_batch(rng.integers(0, 256, (5, 32), dtype=np.uint8))
+    n = 2500
+    kidx = rng.integers(0, 5, n).astype(np.uint32)
+    msgs = [bytes(rng.integers(0, 256, int(rng.integers(0, 300)), dtype=np.uint8)) for _ in range(n)]
+    buf, off = pack_messages(msgs)
+    sig = gpu_engine.sign_batch(sk, kidx, buf, off)
+    pks = pk[kidx].copy()
+    variant = rng.integers(0, 4, n)
+    pks[variant == 1, 16] ^= 0x01  # same slot hash as the true key
+    pks[variant == 2, 25] ^= 0x40  # ditto
+    pks[variant == 3] = pk[kidx[variant == 3]]
+    pks[variant == 3, 31] = 0x7F  # y >= p for many keys: usually fails to decode
+    pks[variant == 3, :31] = 0xFF
+    got = gpu_engine.verify_batch(sig, pks, buf, off)
+    want = np.array([oracle.oracle_verify_detached(sig[i].tobytes(), msgs[i], len(msgs[i]), pks[i].tobytes()) == 0
+                     for i in range(n)])
+    assert (got == want).all(), np.nonzero(got != want)
+    assert want[variant == 0].all() and not want[variant != 0].any()
+
+
+def test_general_distinct_keys(gpu_engine, oracle):
+    """Every request its own key (the dedupe's worst case), 4 sub-batches."""
+    rng = np.random.default_rng(12)
+    n = 5000
+    pk, sk = gpu_engine.seed_keypair_batch(rng.integers(0, 256, (n, 32), dtype=np.uint8))
+    msgs = [bytes(rng.integers(0, 256, int(rng.integers(0, 200)), dtype=np.uint8)) for _ in range(n)]
+    buf, off = pack_messages(msgs)
+    sig = gpu_engine.sign_batch(sk, np.arange(n, dtype=np.uint32), buf, off)
+    bad = rng.choice(n, 250, replace=False)
+    sig[bad, 5] ^= 0x20
+    try:
+        gpu_engine.set_pipeline(4)
+        got = gpu_engine.verify_batch(sig, pk, buf, off)
+    finally:
+        gpu_engine.set_pipeline(1)
+    want = np.ones(n, bool)
+    want[bad] = False
+    assert (got == want).all(), np.nonzero(got != want)
+
+
 def test_message_offsets_and_alignment(gpu_engine, oracle):
     # msg_off[0] != 0, odd offsets, empty messages, zero-length batch
     sig, pks, msgs, buf, off = _random_batch(gpu_engine, 257, 2, mlen_max=50)

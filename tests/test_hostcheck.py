@@ -92,6 +92,17 @@ def test_kernel_comb_path_on_cpu_matches_golden(hostcheck):
         assert (hostcheck.edv_host_verify_comb(sig, pk, msg, ctypes.c_uint64(len(msg))) == 0) == expect, i
 
 
+@pytest.mark.parametrize("k", [1, 2, 4, 8])
+def test_kernel_split_ladder(hostcheck, k):
+    """The general path's split-table ladder (verify_core.h
+    verify_phase_table_split / verify_phase_dsm_split_point: K tables of
+    2^(256t/K)(-A), 256/K - 4 doublings) on the CPU, edge + valid vectors."""
+    items = items_of(load_npz("ed25519_edge.npz"))[::7] + items_of(load_npz("ed25519_valid.npz"))[::61]
+    for i, (sig, pk, msg, expect) in enumerate(items):
+        got = hostcheck.edv_host_verify_split(sig, pk, msg, ctypes.c_uint64(len(msg)), k) == 0
+        assert got == expect, (k, i)
+
+
 @pytest.mark.parametrize("w", [4, 5, 6, 7, 8, 9, 10, 11, 12])
 def test_kernel_comb_windows(hostcheck, w):
     """comb.h's generic signed radix-2^W recoding (9-word bias; W = 5, 6, 7

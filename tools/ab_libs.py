@@ -2,7 +2,8 @@
 workload (1M NYM requests, 1,000 signers), alternating variants in child
 processes on one box so every variant sees the same device and clock regime.
 
-usage: python tools/ab_libs.py [--rounds R] [--window W] [--config c1|c2] lib_a.so lib_b.so ...
+usage: python tools/ab_libs.py [--rounds R] [--window W] [--config c1|c2|distinct] [--path keyed|general] lib_a.so ...
+(distinct: every request signed by its own key)
 Per run: wall ms per 1M-request keyed step with 4 sub-batches (the bench
 step), the comb phase alone with 1 sub-batch, correctness vs construction.
 """
@@ -22,7 +23,7 @@ n = 1_000_000
 W = int(os.environ["AB_W"]); cfg = os.environ["AB_CONFIG"]
 dev = torch.device("cuda", 0); torch.cuda.set_device(0)
 eng = EdVerifyEngine(0)
-pks, sks = eng.seed_keypair_batch(synth.signer_seeds(1000))
+pks, sks = eng.seed_keypair_batch(synth.signer_seeds(n if cfg == "distinct" else 1000))
 msgs, kidx, _ = synth.nym_messages(n, pks, alias_len=43)
 buf, off = pack_messages(msgs)
 d_msgs = torch.from_numpy(np.concatenate([buf, np.zeros(16, np.uint8)])).to(dev)
@@ -40,8 +41,9 @@ if cfg == "c2":
     d_sig = torch.from_numpy(sig).to(dev)
     d_msgs = torch.from_numpy(np.concatenate([b2, np.zeros(16, np.uint8)])).to(dev)
     d_k = torch.from_numpy(inv.reshape(-1).astype(np.int32)).to(dev)
-eng.keys_set_window(W)
-eng.keys_add(reg)
+if os.environ.get("AB_PATH") != "general":
+    eng.keys_set_window(W)
+    eng.keys_add(reg)
 words = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
 if os.environ.get("AB_PATH") == "general":
     d_pk = torch.from_numpy(pks[kidx] if cfg != "c2" else pk).to(dev)
