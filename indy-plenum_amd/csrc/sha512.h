@@ -57,13 +57,37 @@ EDV_HD uint64_t shr64(uint64_t x, int n) {  // 0 < n < 32
 }
 EDV_HD uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
+// Three-input bitwise functions as one gfx950 v_bitop3_b32 per 32-bit half
+// (truth table over x = 0xf0, y = 0xcc, z = 0xaa).  The compiler lowers
+// x ^ y ^ z to two v_xor_b32 per half and Maj to xor + bfi; with bitop3 a
+// round's Sigma0/Sigma1/sigma0/sigma1/Maj take 10 instructions instead of 20.
+template <int TT>
+EDV_HD uint64_t bitop3_64(uint64_t x, uint64_t y, uint64_t z) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)x, (uint32_t)y, (uint32_t)z, TT);
+  const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(x >> 32), (uint32_t)(y >> 32), (uint32_t)(z >> 32), TT);
+  // The empty asm makes the pair opaque: otherwise the optimizer splits the
+  // 64-bit adds that consume it into a 32-bit add of the high halves plus a
+  // 64-bit add of the zero-extended low half (+1 v_mov and +1 add per use).
+  uint64_t r = ((uint64_t)hi << 32) | lo;
+  asm("" : "+v"(r));
+  return r;
+#else
+  static_assert(TT == 0x96 || TT == 0xca || TT == 0xe8, "host form of this table");
+  if (TT == 0x96) return x ^ y ^ z;
+  if (TT == 0xca) return (x & y) ^ (~x & z);
+  return (x & y) | (z & (x | y));
+#endif
+}
+EDV_HD uint64_t xor3_64(uint64_t x, uint64_t y, uint64_t z) { return bitop3_64<0x96>(x, y, z); }
+
 #define EDV_SHA_ROUND(KI, WI)                                                        \
   {                                                                                \
-    const uint64_t S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);             \
-    const uint64_t ch = (e & f) ^ (~e & g);                                        \
+    const uint64_t S1 = xor3_64(rotr64(e, 14), rotr64(e, 18), rotr64(e, 41));      \
+    const uint64_t ch = bitop3_64<0xca>(e, f, g);                                  \
     const uint64_t t1 = h + S1 + ch + (KI) + (WI);                                 \
-    const uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);             \
-    const uint64_t mj = (a & b) | (c & (a | b));                                   \
+    const uint64_t S0 = xor3_64(rotr64(a, 28), rotr64(a, 34), rotr64(a, 39));      \
+    const uint64_t mj = bitop3_64<0xe8>(a, b, c);                                  \
     h = g;                                                                         \
     g = f;                                                                         \
     f = e;                                                                         \
@@ -87,8 +111,8 @@ EDV_HD void sha512_compress(uint64_t st[8], uint64_t w[16]) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const uint64_t w15 = w[(i + 1) & 15], w2 = w[(i + 14) & 15];
-      const uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ shr64(w15, 7);
-      const uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ shr64(w2, 6);
+      const uint64_t s0 = xor3_64(rotr64(w15, 1), rotr64(w15, 8), shr64(w15, 7));
+      const uint64_t s1 = xor3_64(rotr64(w2, 19), rotr64(w2, 61), shr64(w2, 6));
       w[i] += s0 + w[(i + 9) & 15] + s1;
       EDV_SHA_ROUND(SHA512_K[r + i], w[i])
     }

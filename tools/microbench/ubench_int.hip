@@ -61,6 +61,12 @@ __global__ __launch_bounds__(1024) void kbench(uint32_t* out, uint32_t seed) {
         asm volatile("v_add_co_u32 %0, vcc, %0, %1\n v_addc_co_u32 %2, vcc, %2, 0, vcc" : "+v"(acc32[j]), "+v"(b) : "v"(a) : "vcc");
       } else if (KIND == 18) { // v_mad_u32_u16
         asm volatile("v_mad_u32_u16 %0, %1, %2, %0" : "+v"(acc32[j]) : "v"(a), "v"(b));
+      } else if (KIND == 19) { // v_bitop3_b32 (gfx950)
+        asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(acc32[j]) : "v"(a), "v"(b));
+      } else if (KIND == 20) { // v_cndmask_b32 on a VCC mask
+        asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(acc32[j]) : "v"(a));
+      } else if (KIND == 21) { // v_lshrrev_b32
+        asm volatile("v_lshrrev_b32 %0, 7, %0" : "+v"(acc32[j]));
       }
     }
   }
@@ -110,6 +116,9 @@ int main() {
     run<15>("v_and_b32", d, blocks, w);
     run<16>("v_mov_b32", d, blocks, w);
     run<17>("v_add_co+v_addc", d, blocks, w);
+    run<19>("v_bitop3_b32", d, blocks, w);
+    run<20>("v_cndmask_b32", d, blocks, w);
+    run<21>("v_lshrrev_b32", d, blocks, w);
   }
   hipFree(d);
   return 0;
