@@ -18,6 +18,8 @@ __global__ __launch_bounds__(1024) void kbench(uint32_t* out, uint32_t seed) {
   float accf[NACC];
 #pragma unroll
   for (int j = 0; j < NACC; ++j) { acc[j] = j + threadIdx.x; acc32[j] = j * 7 + threadIdx.x; accd[j] = j + 0.5 * threadIdx.x; accf[j] = j; }
+  const uint64_t smask = __ballot(threadIdx.x & 1);
+  if (KIND == 32) asm volatile("v_cmp_gt_u32 vcc, %0, %1" : : "v"(a), "v"(b) : "vcc");
   for (int it = 0; it < ITERS; ++it) {
 #pragma unroll
     for (int j = 0; j < NACC; ++j) {
@@ -67,6 +69,37 @@ __global__ __launch_bounds__(1024) void kbench(uint32_t* out, uint32_t seed) {
         asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(acc32[j]) : "v"(a));
       } else if (KIND == 21) { // v_lshrrev_b32
         asm volatile("v_lshrrev_b32 %0, 7, %0" : "+v"(acc32[j]));
+      } else if (KIND == 22) { // v_cndmask_b32_e64 on an SGPR-pair mask
+        asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(acc32[j]) : "v"(a), "s"(smask));
+      } else if (KIND == 23) { // v_cmp (vcc) + v_cndmask_b32_e32, as the compiler emits them
+        asm volatile("v_cmp_gt_u32 vcc, %1, %2\n\tv_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(acc32[j]) : "v"(a), "v"(b) : "vcc");
+      } else if (KIND == 24) { // v_cmp alone
+        asm volatile("v_cmp_gt_u32 vcc, %0, %1" : : "v"(acc32[j]), "v"(b) : "vcc");
+      } else if (KIND == 25) { // v_bfi_b32
+        asm volatile("v_bfi_b32 %0, %1, %0, %2" : "+v"(acc32[j]) : "v"(a), "v"(b));
+      } else if (KIND == 26) { // v_perm_b32
+        asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(acc32[j]) : "v"(a), "v"(b));
+      } else if (KIND == 27) { // v_sub_u32
+        asm volatile("v_sub_u32 %0, %0, %1" : "+v"(acc32[j]) : "v"(a));
+      } else if (KIND == 28) { // v_add3_u32
+        asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(acc32[j]) : "v"(a), "v"(b));
+      } else if (KIND == 29) { // v_lshlrev_b32
+        asm volatile("v_lshlrev_b32 %0, 3, %0" : "+v"(acc32[j]));
+      } else if (KIND == 30) { // v_ashrrev_i32
+        asm volatile("v_ashrrev_i32 %0, 3, %0" : "+v"(acc32[j]));
+      } else if (KIND == 31) { // v_bitop3_b32 as a select on a lane mask
+        asm volatile("v_bitop3_b32 %0, %1, %0, %2 bitop3:0xca" : "+v"(acc32[j]) : "v"(a), "v"(b));
+      } else if (KIND == 32) { // v_cndmask_b32_e32 with vcc set once per kernel by v_cmp
+        asm volatile("v_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(acc32[j]) : "v"(a) : "vcc");
+      } else if (KIND == 33) { // v_lshlrev_b64
+        asm volatile("v_lshlrev_b64 %0, 3, %0" : "+v"(acc[j]));
+      } else if (KIND == 34) { // v_mad_u64_u32 independent of acc chain: 2 accumulators interleaved
+        uint64_t c;
+        asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc[j]), "=s"(c) : "v"(acc32[j]), "v"(b));
+      } else if (KIND == 35) { // v_mul_lo_u32 by constant 19 (as the compiler emits 19*g)
+        asm volatile("v_mul_lo_u32 %0, %0, 19" : "+v"(acc32[j]));
+      } else if (KIND == 36) { // v_sub_co_u32 + v_subb (64-bit sub)
+        asm volatile("v_sub_co_u32 %0, vcc, %0, %1\n v_subb_co_u32 %2, vcc, %2, 0, vcc" : "+v"(acc32[j]), "+v"(b) : "v"(a) : "vcc");
       }
     }
   }
@@ -97,7 +130,7 @@ int main() {
   hipDeviceProp_t p; hipGetDeviceProperties(&p, 0);
   printf("device %s CUs=%d clock=%d kHz\n", p.gcnArchName, p.multiProcessorCount, p.clockRate);
   int blocks = 256 * 8;
-  for (int w : {8, 16}) {
+  for (int w : {16}) {
     run<0>("v_mad_u64_u32", d, blocks, w);
     run<1>("v_mul_lo_u32", d, blocks, w);
     run<2>("v_mul_hi_u32", d, blocks, w);
@@ -119,6 +152,21 @@ int main() {
     run<19>("v_bitop3_b32", d, blocks, w);
     run<20>("v_cndmask_b32", d, blocks, w);
     run<21>("v_lshrrev_b32", d, blocks, w);
+    run<22>("v_cndmask_e64 smask", d, blocks, w);
+    run<23>("v_cmp+v_cndmask_e32", d, blocks, w);
+    run<24>("v_cmp (vcc)", d, blocks, w);
+    run<25>("v_bfi_b32", d, blocks, w);
+    run<26>("v_perm_b32", d, blocks, w);
+    run<27>("v_sub_u32", d, blocks, w);
+    run<28>("v_add3_u32", d, blocks, w);
+    run<29>("v_lshlrev_b32", d, blocks, w);
+    run<30>("v_ashrrev_i32", d, blocks, w);
+    run<31>("v_bitop3 select", d, blocks, w);
+    run<32>("v_cndmask_e32 vcc set", d, blocks, w);
+    run<33>("v_lshlrev_b64", d, blocks, w);
+    run<34>("v_mad_u64_u32 var a", d, blocks, w);
+    run<35>("v_mul_lo_u32 x19", d, blocks, w);
+    run<36>("v_sub_co+v_subb", d, blocks, w);
   }
   hipFree(d);
   return 0;
