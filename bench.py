@@ -63,9 +63,10 @@ def parse():
                     help="comb window of the key tables (edv_keys_set_window)")
     ap.add_argument("--pipeline", type=int, default=1, choices=[1, 2, 3, 4],
                     help="sub-batches per chunk (edv_set_pipeline; 1 = one launch per kernel, no overlap)")
-    ap.add_argument("--length-buckets", choices=["auto", "on", "off"], default="auto",
+    ap.add_argument("--length-buckets", choices=["auto", "on", "off", "packed"], default="auto",
                     help="hash lanes in SHA-512 block-count order (edv_set_length_buckets); auto = the "
-                         "library's rule for host offsets, applied to this batch's lengths")
+                         "library's rule for host offsets, applied to this batch's lengths; packed = sorted "
+                         "and packed into the length-bucketed SoA unit layout (mode 3)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (the product); gloo only to rehearse N > 1 on one GPU")
     ap.add_argument("--same-device", action="store_true", help="every rank on cuda:0 (with --dist-backend gloo)")
@@ -293,8 +294,9 @@ def main():
         req_desc = ", %d requests x 1-5 signatures (mean %.2f), payload %d-%d B log-uniform" % (
             nreq, n / nreq, int(lens.min()), int(lens.max()))
     mlen_mean = float(np.mean(item_end - item_start))
-    buckets = args.length_buckets == "on" or (args.length_buckets == "auto" and lengths_mixed(item_start, item_end))
-    eng.set_length_buckets(1 if buckets else 0)
+    buckets = args.length_buckets in ("on", "packed") or (args.length_buckets == "auto" and
+                                                           lengths_mixed(item_start, item_end))
+    eng.set_length_buckets(3 if args.length_buckets == "packed" else 1 if buckets else 0)
     d_kidx = torch.from_numpy(key_idx.astype(np.int32)).to(dev)
     d_msgs = torch.from_numpy(np.concatenate([buf, np.zeros(16, np.uint8)])).to(dev)
     d_ms = torch.from_numpy(item_start.astype(np.int64)).to(dev)
@@ -604,7 +606,7 @@ def main():
                          ("comb" if args.path == "keyed" else "dsm"): dsm_sum, "encode": float(ph[3]),
                          "note": "per-phase sums over the %d overlapped sub-batch launches of the last "
                                  "%d-request chunk" % (launches, n_chunk)},
-            "length_buckets": bool(buckets),
+            "length_buckets": "packed" if args.length_buckets == "packed" else bool(buckets),
             "key_window": args.key_window, "key_table_build_ms": key_build_ms, "keys": int(reg_pks.shape[0]),
             "value_incl_key_build_one_step": (n * world / (ms_per_step * 1e-3 + key_build_ms * 1e-3)
                                               if args.path == "keyed" else None),

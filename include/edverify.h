@@ -119,8 +119,19 @@ int edv_set_pipeline(edv_ctx *ctx, int sub_batches);
  * pointer calls cannot see the lengths without a sync and treat auto as off.
  * Measured (profiles/r01g_*): configs[3] (64 B - 4 KiB log-uniform) hash
  * 4.72 -> 1.50 ms per 1M signatures, whole step 154M -> 297M/s; configs[1]
- * (all 2 blocks) -8% if forced on (the sort's launches), hence auto. */
+ * (all 2 blocks) -8% if forced on (the sort's launches), hence auto.
+ * mode 3 = sorted + packed (north_star (1)): each 64-lane group of sorted
+ * hash lanes gets a region of the context's unit arena where
+ * edv_pack_units_kernel writes its messages as padded big-endian SHA-512
+ * stream words, lane-interleaved, so the hash kernels' message loads are
+ * coalesced 1 KiB wave accesses with no byte shuffling (one sub-batch per
+ * chunk).  Groups that do not fit the arena are read in place.  The accept
+ * bits do not depend on the mode. */
 int edv_set_length_buckets(edv_ctx *ctx, int mode);
+/* Size of the unit arena of mode 3 in bytes (default 1.25 GiB = 1,280 B per
+ * lane of a 2^20-request chunk; allocated on first use; 0 = none).  Takes
+ * effect at the next mode-3 launch. */
+int edv_set_unit_arena(edv_ctx *ctx, uint64_t bytes);
 int edv_last_phase_ms(edv_ctx *ctx, double *hash_ms, double *table_ms, double *dsm_ms);
 double edv_last_kernel_ms(edv_ctx *ctx);
 

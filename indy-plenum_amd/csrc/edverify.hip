@@ -29,6 +29,7 @@
 #include <vector>
 
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
 
 #include "../../include/edverify.h"
@@ -174,13 +175,68 @@ __global__ __launch_bounds__(kBlock) void edv_len_key_kernel(const uint64_t* __r
   key[i] = (uint8_t)(blocks < cap ? blocks : cap);
 }
 
+// ---- Packed (SoA) message layout, edv_set_length_buckets mode 3 (north_star
+// (1)): after the block-count sort, each 64-lane group of sorted hash lanes
+// owns a region of the context's unit arena, units(longest message of the
+// group) x 64 lanes x 16 B, unit p of lane l at region + p * 64 + l
+// (sha512.h pack_lane_units: padded big-endian stream words after R || A).
+// edv_group_units_kernel sizes the groups, an exclusive scan places them,
+// edv_pack_units_kernel fills them (coalesced 1 KiB stores per wave) and the
+// hash kernels read them with coalesced 1 KiB loads and no byte shuffling.
+// A group whose region would pass the arena's end is read in place (AoS).
+struct UnitArena {
+  Chunk16* __restrict__ base;            // null: no packing
+  const uint64_t* __restrict__ gunits;   // units per lane of group g
+  const uint64_t* __restrict__ goff;     // exclusive prefix sum of gunits
+  uint64_t cap;                          // arena size in units
+  // lane t's unit 0, or null if its group is not packed
+  __device__ __forceinline__ Chunk16* lane(uint64_t t) const {
+    if (!base) return nullptr;
+    const uint64_t g = t >> 6;
+    const uint64_t o = goff[g];
+    return (o + gunits[g]) * 64 <= cap ? base + o * 64 + (t & 63) : nullptr;
+  }
+};
+
+__global__ __launch_bounds__(kBlock) void edv_group_units_kernel(const uint64_t* __restrict__ ms,
+                                                                const uint64_t* __restrict__ me, uint64_t n,
+                                                                const uint32_t* __restrict__ perm,
+                                                                uint64_t* __restrict__ gunits) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t u = 0;
+  if (t < n) {
+    const uint64_t i = perm[t];
+    u = sha512_units64(me[i] - ms[i]);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {  // every lane of the wave takes part (no early return above)
+    const uint64_t v = __shfl_xor(u, o, 64);
+    u = v > u ? v : u;
+  }
+  if ((threadIdx.x & 63) == 0 && t < n) gunits[t >> 6] = u;
+}
+
+__global__ __launch_bounds__(kBlock) void edv_pack_units_kernel(const uint8_t* __restrict__ msgs,
+                                                               const uint64_t* __restrict__ ms,
+                                                               const uint64_t* __restrict__ me, uint64_t n,
+                                                               const uint32_t* __restrict__ perm, UnitArena ua) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  Chunk16* u = ua.lane(t);
+  if (!u) return;
+  const uint64_t i = perm[t];
+  pack_lane_units(u, 64, msgs + ms[i], me[i] - ms[i]);
+}
+
+template <bool kUnits>
 __global__ __launch_bounds__(kBlock, EDV_HASH_MIN_WAVES) void edv_hash_kernel(const uint8_t* __restrict__ sig64,
                                                          const uint8_t* __restrict__ pk32,
                                                          const uint8_t* __restrict__ msgs,
                                                          const uint64_t* __restrict__ ms,
                                                          const uint64_t* __restrict__ me, uint64_t n,
                                                          uint32_t* __restrict__ h_soa, uint8_t* __restrict__ flags,
-                                                         uint64_t stride, const uint32_t* __restrict__ perm) {
+                                                         uint64_t stride, const uint32_t* __restrict__ perm,
+                                                         UnitArena ua) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
   const uint64_t i = hash_lane_request(t, perm);
@@ -188,7 +244,9 @@ __global__ __launch_bounds__(kBlock, EDV_HASH_MIN_WAVES) void edv_hash_kernel(co
   load_words(sig, sig64 + 64 * i, 16);
   load_words(pk, pk32 + 32 * i, 8);
   const uint64_t o0 = ms[i], o1 = me[i];
-  const bool ok = verify_phase_hash(h, sig, pk, msgs + o0, o1 - o0);
+  const Chunk16* units = kUnits ? ua.lane(t) : nullptr;
+  const bool ok = units ? verify_phase_hash_units(h, sig, pk, units, 64, o1 - o0)
+                        : verify_phase_hash(h, sig, pk, msgs + o0, o1 - o0);
 #pragma unroll
   for (int k = 0; k < 8; ++k) h_soa[k * stride + i] = h[k];
   flags[i] = ok ? 1 : 0;
@@ -521,6 +579,7 @@ __global__ void edv_base_rows_kernel(uint32_t* __restrict__ rows) {
   ge_frombytes(P, b, false);
   comb_rows<kBaseW>(rows, P);
 }
+template <bool kUnits>
 __global__ __launch_bounds__(kBlock, EDV_HASH_MIN_WAVES) void edv_hash_keyed_kernel(const uint8_t* __restrict__ sig64,
                                                                const uint32_t* __restrict__ key_idx,
                                                                uint32_t key_count,
@@ -531,7 +590,7 @@ __global__ __launch_bounds__(kBlock, EDV_HASH_MIN_WAVES) void edv_hash_keyed_ker
                                                                const uint64_t* __restrict__ me, uint64_t n,
                                                                uint32_t* __restrict__ h_soa,
                                                                uint8_t* __restrict__ flags, uint64_t stride,
-                                                               const uint32_t* __restrict__ perm) {
+                                                               const uint32_t* __restrict__ perm, UnitArena ua) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
   const uint64_t i = hash_lane_request(t, perm);
@@ -542,7 +601,10 @@ __global__ __launch_bounds__(kBlock, EDV_HASH_MIN_WAVES) void edv_hash_keyed_ker
   const uint64_t k = in_range ? key : 0;
   load_words(pk, key_pk + 32 * k, 8);
   const uint64_t o0 = ms[i], o1 = me[i];
-  const bool ok = verify_phase_hash(h, sig, pk, msgs + o0, o1 - o0) && in_range && key_valid[k];
+  const Chunk16* units = kUnits ? ua.lane(t) : nullptr;
+  const bool hashed = units ? verify_phase_hash_units(h, sig, pk, units, 64, o1 - o0)
+                            : verify_phase_hash(h, sig, pk, msgs + o0, o1 - o0);
+  const bool ok = hashed && in_range && key_valid[k];
 #pragma unroll
   for (int k = 0; k < 8; ++k) h_soa[k * stride + i] = h[k];
   flags[i] = ok ? 1 : 0;
@@ -868,8 +930,18 @@ struct edv_ctx {
   uint32_t* d_ucount = nullptr;
   void* d_sort_tmp = nullptr;     // radix-sort temporary storage, one slot per sub-batch
   size_t sort_tmp_bytes = 0;      // per slot (sized for kMaxLanes)
-  int bucket_mode = 2;            // edv_set_length_buckets: 0 off, 1 on, 2 auto
+  int bucket_mode = 2;            // edv_set_length_buckets: 0 off, 1 on, 2 auto, 3 on + packed units
   bool bucket_now = false;        // this launch sorts its hash lanes
+  bool pack_now = false;          // ... and packs the messages into the unit arena (mode 3)
+  // packed message layout (mode 3): per-group units and offsets
+  // [kMaxLanes / 64 + 1] each, the scan's temporary storage, the arena
+  uint64_t* d_gunits = nullptr;
+  uint64_t* d_goff = nullptr;
+  void* d_scan_tmp = nullptr;
+  size_t scan_tmp_bytes = 0;
+  Chunk16* d_arena = nullptr;
+  uint64_t arena_units = 0;                  // allocated
+  uint64_t arena_want = kMaxLanes * 80ull;   // edv_set_unit_arena (1.25 GiB: 1,280 B per lane)
   uint64_t scratch_lanes = 0;
   // Pipelined launches: each chunk of up to kMaxLanes requests is cut into
   // kSub sub-batches whose kernels alternate between `stream` (or the
@@ -997,6 +1069,42 @@ int launch_encode(edv_ctx* ctx, const uint8_t* sig, uint64_t cn, unsigned long l
   return 0;
 }
 
+// Length-bucket flags of the next launch: mode 1 / 3 always sort (3 also
+// packs), mode 2 sorts when the caller saw mixed lengths (host offsets).
+void set_bucketing(edv_ctx* ctx, bool mixed) {
+  ctx->bucket_now = ctx->bucket_mode == 1 || ctx->bucket_mode == 3 || (ctx->bucket_mode == 2 && mixed);
+  ctx->pack_now = ctx->bucket_mode == 3;
+}
+
+int ensure_arena(edv_ctx* ctx) {
+  const uint64_t groups = kMaxLanes / 64;
+  if (!ctx->d_gunits) {
+    HIP_TRY(hipMalloc(&ctx->d_gunits, (groups + 1) * sizeof(uint64_t)));
+    HIP_TRY(hipMalloc(&ctx->d_goff, (groups + 1) * sizeof(uint64_t)));
+    size_t bytes = 0;
+    HIP_TRY(rocprim::exclusive_scan(nullptr, bytes, ctx->d_gunits, ctx->d_goff, (uint64_t)0, (size_t)groups,
+                                    rocprim::plus<uint64_t>(), ctx->stream));
+    ctx->scan_tmp_bytes = bytes;
+    HIP_TRY(hipMalloc(&ctx->d_scan_tmp, bytes ? bytes : 16));
+  }
+  if (ctx->arena_units != ctx->arena_want) {
+    if (ctx->d_arena) {
+      HIP_TRY(hipDeviceSynchronize());  // earlier launches may still read the old arena
+      HIP_TRY(hipFree(ctx->d_arena));
+    }
+    ctx->d_arena = nullptr;
+    ctx->arena_units = 0;
+    if (ctx->arena_want) {
+      hipError_t e = hipMalloc(&ctx->d_arena, ctx->arena_want * sizeof(Chunk16));
+      if (e != hipSuccess)
+        return set_err(EDV_ENOMEM, "unit arena (%llu units): %s", (unsigned long long)ctx->arena_want,
+                       hipGetErrorString(e));
+    }
+    ctx->arena_units = ctx->arena_want;
+  }
+  return 0;
+}
+
 // The kernels of one sub-batch [off, off + cn) of a chunk (scratch index
 // off.. with the chunk's stride), on stream q, bracketed by ev[0..4].
 struct SubBatch {
@@ -1009,6 +1117,26 @@ struct SubBatch {
   uint64_t cn, soff;
 };
 
+// Packed message layout of a sorted sub-batch (the UnitArena comment):
+// group sizes, their exclusive scan, the pack; *ua describes the result.
+int launch_pack(edv_ctx* ctx, const SubBatch& b, const uint8_t* msgs, const uint32_t* perm, hipStream_t q,
+                UnitArena* ua) {
+  int r = ensure_arena(ctx);
+  if (r) return r;
+  if (!ctx->d_arena) return 0;  // arena size 0: every group reads in place
+  const uint32_t grid = (uint32_t)div_up(b.cn, kBlock);
+  const uint64_t groups = div_up(b.cn, 64);
+  hipLaunchKernelGGL(edv_group_units_kernel, dim3(grid), dim3(kBlock), 0, q, b.ms, b.me, b.cn, perm, ctx->d_gunits);
+  HIP_TRY(hipGetLastError());
+  size_t tmp = ctx->scan_tmp_bytes;
+  HIP_TRY(rocprim::exclusive_scan(ctx->d_scan_tmp, tmp, ctx->d_gunits, ctx->d_goff, (uint64_t)0, (size_t)groups,
+                                  rocprim::plus<uint64_t>(), q));
+  *ua = {ctx->d_arena, ctx->d_gunits, ctx->d_goff, ctx->arena_units};
+  hipLaunchKernelGGL(edv_pack_units_kernel, dim3(grid), dim3(kBlock), 0, q, msgs, b.ms, b.me, b.cn, perm, *ua);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
 int launch_sub(edv_ctx* ctx, bool keyed, const SubBatch& b, const uint8_t* msgs, uint64_t chunk, hipStream_t q,
                hipEvent_t* ev, int sub) {
   const uint32_t grid = (uint32_t)div_up(b.cn, kBlock);
@@ -1016,8 +1144,9 @@ int launch_sub(edv_ctx* ctx, bool keyed, const SubBatch& b, const uint8_t* msgs,
   uint8_t* fl = ctx->d_flags + b.soff;
   uint32_t* pt = ctx->d_pt + b.soff;
   uint32_t* perm = nullptr;
+  UnitArena ua = {nullptr, nullptr, nullptr, 0};
   HIP_TRY(hipEventRecord(ev[0], q));
-  if (ctx->bucket_now && b.cn > 64) {
+  if (ctx->bucket_now && (b.cn > 64 || ctx->pack_now)) {
     // hash lanes in SHA-512 block-count order, longest first (stable)
     perm = ctx->d_perm + b.soff;
     uint8_t* key = ctx->d_lenkey + b.soff;
@@ -1028,10 +1157,18 @@ int launch_sub(edv_ctx* ctx, bool keyed, const SubBatch& b, const uint8_t* msgs,
                                            rocprim::counting_iterator<uint32_t>(0), perm, (uint32_t)b.cn, 0,
                                            kLenKeyBits, q));
   }
+  if (ctx->pack_now && perm) {
+    int r = launch_pack(ctx, b, msgs, perm, q, &ua);
+    if (r) return r;
+  }
   if (keyed) {
     const uint32_t kc = (uint32_t)ctx->key_count;
-    hipLaunchKernelGGL(edv_hash_keyed_kernel, dim3(grid), dim3(kBlock), 0, q, b.sig, b.kidx, kc, ctx->d_key_pk,
-                       ctx->d_key_valid, msgs, b.ms, b.me, b.cn, hs, fl, chunk, perm);
+    if (ua.base)
+      hipLaunchKernelGGL(edv_hash_keyed_kernel<true>, dim3(grid), dim3(kBlock), 0, q, b.sig, b.kidx, kc,
+                         ctx->d_key_pk, ctx->d_key_valid, msgs, b.ms, b.me, b.cn, hs, fl, chunk, perm, ua);
+    else
+      hipLaunchKernelGGL(edv_hash_keyed_kernel<false>, dim3(grid), dim3(kBlock), 0, q, b.sig, b.kidx, kc,
+                         ctx->d_key_pk, ctx->d_key_valid, msgs, b.ms, b.me, b.cn, hs, fl, chunk, perm, ua);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ev[1], q));
     HIP_TRY(hipEventRecord(ev[2], q));
@@ -1076,8 +1213,12 @@ int launch_sub(edv_ctx* ctx, bool keyed, const SubBatch& b, const uint8_t* msgs,
     hipLaunchKernelGGL(edv_table_kernel, dim3(grid), dim3(kBlock), 0, qk, b.pk, b.cn, reps, count, tab, key_ok);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev_kjoin[sub], qk));
-    hipLaunchKernelGGL(edv_hash_kernel, dim3(grid), dim3(kBlock), 0, q, b.sig, b.pk, msgs, b.ms, b.me, b.cn, hs, fl,
-                       chunk, perm);
+    if (ua.base)
+      hipLaunchKernelGGL(edv_hash_kernel<true>, dim3(grid), dim3(kBlock), 0, q, b.sig, b.pk, msgs, b.ms, b.me, b.cn,
+                         hs, fl, chunk, perm, ua);
+    else
+      hipLaunchKernelGGL(edv_hash_kernel<false>, dim3(grid), dim3(kBlock), 0, q, b.sig, b.pk, msgs, b.ms, b.me, b.cn,
+                         hs, fl, chunk, perm, ua);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ev[1], q));
     HIP_TRY(hipStreamWaitEvent(q, ctx->ev_kjoin[sub], 0));
@@ -1112,7 +1253,8 @@ int launch_pipeline(edv_ctx* ctx, bool keyed, const void* d_sig, const void* d_k
     // starts only after both streams are done with this one
     // (sorted hash lanes: at most 2 -- measured on configs[3], 3 or 4
     // sub-batches are 10% slower than 1 or 2)
-    const uint64_t nsub = ctx->bucket_now && ctx->max_sub > 2 ? 2 : (uint64_t)ctx->max_sub;
+    // (packed units: 1 -- the sub-batch owns the whole unit arena)
+    const uint64_t nsub = ctx->pack_now ? 1 : ctx->bucket_now && ctx->max_sub > 2 ? 2 : (uint64_t)ctx->max_sub;
     const uint64_t per = div_up(div_up(cn, nsub), kSubAlign) * kSubAlign;
     int ns = 0;
     for (uint64_t s0 = 0; s0 < cn; s0 += per, ++ns) {
@@ -1282,7 +1424,7 @@ static int host_verify(edv_ctx* ctx, bool keyed, const uint8_t* sig64, const uin
     memcpy(ctx->h_sig[sl].p, sig64 + 64 * c0, 64 * cn);
     memcpy(ctx->h_key[sl].p, keys + key_bytes * c0, key_bytes * cn);
     if (mbytes) memcpy(ctx->h_msg[sl].p, msgs + m0, mbytes);
-    ctx->bucket_now = ctx->bucket_mode == 1 || (ctx->bucket_mode == 2 && lengths_mixed(off, cn));
+    set_bucketing(ctx, ctx->bucket_mode == 2 && lengths_mixed(off, cn));
     hipStream_t cs = ctx->stream_copy;
     HIP_TRY(hipMemcpyAsync(ctx->d_sig[sl].p, ctx->h_sig[sl].p, 64 * cn, hipMemcpyHostToDevice, cs));
     HIP_TRY(hipMemcpyAsync(ctx->d_key[sl].p, ctx->h_key[sl].p, key_bytes * cn, hipMemcpyHostToDevice, cs));
@@ -1393,7 +1535,7 @@ int edv_verify_batch_keyed_device(edv_ctx* ctx, const void* d_sig64, const void*
   if (r) return r;
   if (n && (!d_sig64 || !d_key_idx || !d_msgs || !d_msg_off || !d_accept_words))
     return set_err(EDV_EINVAL, "null device pointer");
-  ctx->bucket_now = ctx->bucket_mode == 1;
+  set_bucketing(ctx, false);
   return launch_verify_keyed(ctx, d_sig64, d_key_idx, d_msgs, d_msg_off, n, d_accept_words, pick_stream(ctx, stream));
 }
 
@@ -1405,7 +1547,7 @@ int edv_verify_spans_device(edv_ctx* ctx, const void* d_sig64, const void* d_key
   if (n && (!d_sig64 || !d_keys || !d_msgs || !d_msg_start || !d_msg_end || !d_accept_words))
     return set_err(EDV_EINVAL, "null device pointer");
   if (n && keyed && ctx->key_count == 0) return set_err(EDV_EINVAL, "no registered keys");
-  ctx->bucket_now = ctx->bucket_mode == 1;
+  set_bucketing(ctx, false);
   return launch_pipeline(ctx, keyed != 0, d_sig64, d_keys, d_msgs, (const uint64_t*)d_msg_start,
                          (const uint64_t*)d_msg_end, n, d_accept_words, pick_stream(ctx, stream));
 }
@@ -1549,6 +1691,10 @@ void edv_destroy(edv_ctx* ctx) {
   if (ctx->d_flags) (void)hipFree(ctx->d_flags);
   if (ctx->d_pt) (void)hipFree(ctx->d_pt);
   if (ctx->d_perm) (void)hipFree(ctx->d_perm);
+  if (ctx->d_gunits) (void)hipFree(ctx->d_gunits);
+  if (ctx->d_goff) (void)hipFree(ctx->d_goff);
+  if (ctx->d_scan_tmp) (void)hipFree(ctx->d_scan_tmp);
+  if (ctx->d_arena) (void)hipFree(ctx->d_arena);
   if (ctx->d_lenkey) (void)hipFree(ctx->d_lenkey);
   if (ctx->d_dedup) (void)hipFree(ctx->d_dedup);
   if (ctx->d_key_ok) (void)hipFree(ctx->d_key_ok);
@@ -1589,7 +1735,7 @@ int edv_verify_batch_device(edv_ctx* ctx, const void* d_sig64, const void* d_pk3
   if (r) return r;
   if (n && (!d_sig64 || !d_pk32 || !d_msgs || !d_msg_off || !d_accept_words))
     return set_err(EDV_EINVAL, "null device pointer");
-  ctx->bucket_now = ctx->bucket_mode == 1;
+  set_bucketing(ctx, false);
   return launch_verify(ctx, d_sig64, d_pk32, d_msgs, d_msg_off, n, d_accept_words, pick_stream(ctx, stream));
 }
 
@@ -1613,8 +1759,15 @@ uint64_t edv_last_chunk_items(edv_ctx* ctx) { return ctx ? ctx->last_chunk_n : 0
 
 int edv_set_length_buckets(edv_ctx* ctx, int mode) {
   if (!ctx) return set_err(EDV_EINVAL, "null context");
-  if (mode < 0 || mode > 2) return set_err(EDV_EINVAL, "length-bucket mode %d (0 off, 1 on, 2 auto)", mode);
+  if (mode < 0 || mode > 3)
+    return set_err(EDV_EINVAL, "length-bucket mode %d (0 off, 1 on, 2 auto, 3 on + packed units)", mode);
   ctx->bucket_mode = mode;
+  return 0;
+}
+
+int edv_set_unit_arena(edv_ctx* ctx, uint64_t bytes) {
+  if (!ctx) return set_err(EDV_EINVAL, "null context");
+  ctx->arena_want = bytes / sizeof(Chunk16);
   return 0;
 }
 

@@ -113,6 +113,22 @@ void edv_host_sha512_prefixed(uint8_t out[64], const uint8_t prefix64[64], const
   memcpy(out, dig, 64);
 }
 
+// The packed unit layout: M packed into units at `stride` (a lane of a
+// lane-interleaved group), then hashed from them; also hands the units back.
+void edv_host_sha512_units(uint8_t out[64], const uint8_t prefix64[64], const uint8_t* msg, uint64_t mlen,
+                           uint64_t stride, uint8_t* units_out) {
+  uint32_t pre[16], dig[16];
+  memcpy(pre, prefix64, 64);
+  const uint64_t nu = sha512_units64(mlen);
+  std::vector<Chunk16> u(nu * stride, Chunk16{0xdeadbeefu, 0xdeadbeefu, 0xdeadbeefu, 0xdeadbeefu});
+  pack_lane_units(u.data(), stride, msg, mlen);
+  sha512_prefixed_units(dig, pre, u.data(), stride, mlen);
+  memcpy(out, dig, 64);
+  if (units_out)
+    for (uint64_t p = 0; p < nu; ++p) memcpy(units_out + 16 * p, &u[p * stride], 16);
+}
+uint64_t edv_host_sha512_units_count(uint64_t mlen) { return sha512_units64(mlen); }
+
 void edv_host_sha256(uint8_t out[32], const uint8_t* msg, uint64_t mlen) {
   uint32_t d[8];
   sha256_msg(d, msg, mlen);

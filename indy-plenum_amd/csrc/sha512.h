@@ -245,4 +245,86 @@ EDV_HD void sha512_prefixed(uint32_t digest[16], const uint32_t prefix[NP], cons
   }
 }
 
+// ---- Length-bucketed SoA message layout (north_star (1)).
+//
+// For a 64-byte prefix (R || A) the SHA-512 stream is R || A || M || 0x80 ||
+// 0... || bitlen, and M starts exactly at stream word 8: the message part of
+// the stream is (SHA-512 blocks) * 128 - 64 bytes = 8 * nblocks - 4 "units"
+// of 16 bytes (two big-endian stream words).  pack_lane_units writes a lane's
+// units, already byte-swapped, padded and carrying the bit length, at
+// out[p * stride]; with stride 64 and lane-interleaved groups (edverify.hip
+// edv_pack_units_kernel) the hash kernel's unit loads are one coalesced 1 KiB
+// access per wave and need no funnel, select or tail masking.
+EDV_HD uint64_t sha512_nblocks64(uint64_t mlen) { return (64 + mlen + 16) / 128 + 1; }
+EDV_HD uint64_t sha512_units64(uint64_t mlen) { return 8 * sha512_nblocks64(mlen) - 4; }
+
+EDV_HD void pack_lane_units(Chunk16* out, uint64_t stride, const uint8_t* msg, uint64_t mlen) {
+  const uint64_t nunits = sha512_units64(mlen);
+  const uint32_t d16 = (uint32_t)((uintptr_t)msg & 15);
+  const Chunk16* c16 = (const Chunk16*)(msg - d16);
+  const uint64_t nq = (d16 + mlen + 15) / 16;  // chunks holding message bytes
+  const uint32_t s4 = d16 >> 2, sh = d16 & 3u;
+  const uint64_t bitlen = (64 + mlen) * 8;
+  Chunk16 cur = {0u, 0u, 0u, 0u};
+  if (nq > 0) cur = c16[0];
+#pragma unroll 1
+  for (uint64_t p = 0; p < nunits; ++p) {
+    Chunk16 nxt = {0u, 0u, 0u, 0u};
+    if (p + 1 < nq) nxt = c16[p + 1];
+    // message bytes [16p, 16p + 16) = bytes d16.. of the 32-byte window cur || nxt
+    const uint32_t W[8] = {cur.x, cur.y, cur.z, cur.w, nxt.x, nxt.y, nxt.z, nxt.w};
+    uint32_t V[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) V[j] = s4 == 0 ? W[j] : s4 == 1 ? W[j + 1] : s4 == 2 ? W[j + 2] : W[j + 3];
+    uint32_t le[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) le[k] = funnel8(V[k + 1], V[k], sh);
+    if (16 * (p + 1) > mlen) {
+      const int32_t rb = bytes_left(mlen, (int64_t)(4 * p));  // message bytes left at the unit's first byte
+#pragma unroll
+      for (int k = 0; k < 4; ++k) le[k] = tail_word(le[k], rb - 4 * k);
+    }
+    uint64_t w0 = ((uint64_t)bswap32(le[0]) << 32) | bswap32(le[1]);
+    uint64_t w1 = ((uint64_t)bswap32(le[2]) << 32) | bswap32(le[3]);
+    if (p + 1 == nunits) w1 = bitlen;  // the high length word (w0) is zero padding
+    out[p * stride] = {(uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32)};
+    cur = nxt;
+  }
+}
+
+// SHA-512(prefix || M) from the unit layout above: prefix = 16 little-endian
+// u32 words (R || A), units[p * stride] = unit p of M's stream.
+EDV_HD void sha512_prefixed_units(uint32_t digest[16], const uint32_t prefix[16], const Chunk16* units, uint64_t stride,
+                                  uint64_t mlen) {
+  uint64_t st[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL, 0xa54ff53a5f1d36f1ULL,
+                    0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL, 0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
+  const uint64_t nblocks = sha512_nblocks64(mlen);
+  uint64_t w[16];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) w[j] = ((uint64_t)bswap32(prefix[2 * j]) << 32) | bswap32(prefix[2 * j + 1]);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const Chunk16 u = units[q * stride];
+    w[8 + 2 * q] = ((uint64_t)u.y << 32) | u.x;
+    w[9 + 2 * q] = ((uint64_t)u.w << 32) | u.z;
+  }
+  sha512_compress(st, w);
+#pragma unroll 1
+  for (uint64_t b = 1; b < nblocks; ++b) {
+    const Chunk16* ub = units + (8 * b - 4) * stride;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const Chunk16 u = ub[q * stride];
+      w[2 * q] = ((uint64_t)u.y << 32) | u.x;
+      w[2 * q + 1] = ((uint64_t)u.w << 32) | u.z;
+    }
+    sha512_compress(st, w);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    digest[2 * j] = bswap32((uint32_t)(st[j] >> 32));
+    digest[2 * j + 1] = bswap32((uint32_t)st[j]);
+  }
+}
+
 }  // namespace edv

@@ -83,6 +83,22 @@ EDV_HD bool verify_phase_hash(uint32_t h[8], const uint32_t sig[16], const uint3
   sc_reduce(h, digest);
   return ok;
 }
+// The same with M in the packed unit layout (sha512.h pack_lane_units).
+EDV_HD bool verify_phase_hash_units(uint32_t h[8], const uint32_t sig[16], const uint32_t pk[8], const Chunk16* units,
+                                    uint64_t stride, uint64_t mlen) {
+  const uint32_t* R = sig;
+  const uint32_t* S = sig + 8;
+  const bool ok = sc_is_canonical(S) && !has_small_order(R) && is_canonical_point(pk) && !has_small_order(pk);
+  uint32_t prefix[16], digest[16];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    prefix[k] = R[k];
+    prefix[8 + k] = pk[k];
+  }
+  sha512_prefixed_units(digest, prefix, units, stride, mlen);
+  sc_reduce(h, digest);
+  return ok;
+}
 
 // Phase 2: decode -A and store the cached multiples [1..8](-A) through TA:
 //   TA::store(j, const ge_cached&) for j in 0..7 (= (j+1)(-A)); slot 8 holds

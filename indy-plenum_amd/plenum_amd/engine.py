@@ -195,9 +195,15 @@ class EdVerifyEngine:
 
     def set_length_buckets(self, mode):
         """Hash lanes sorted by SHA-512 block count: False/0 off, True/1 on,
-        "auto"/2 (the default; host-offset calls decide per batch, edverify.h)."""
-        m = {"auto": 2, "on": 1, "off": 0}.get(mode, mode)
+        "auto"/2 (the default; host-offset calls decide per batch, edverify.h),
+        "packed"/3 sorted and packed into the length-bucketed SoA unit layout."""
+        m = {"auto": 2, "on": 1, "off": 0, "packed": 3}.get(mode, mode)
         check(self._lib.edv_set_length_buckets(self._ctx, int(m)))
+
+    def set_unit_arena(self, nbytes):
+        """Unit-arena size of the packed mode in bytes (groups beyond it are
+        hashed in place)."""
+        check(self._lib.edv_set_unit_arena(self._ctx, int(nbytes)))
 
     # ------------------------------------------------------------ key tables
     def keys_set_window(self, w):

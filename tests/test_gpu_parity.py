@@ -387,6 +387,52 @@ def test_length_buckets_mixed_lengths(gpu_engine, oracle):
                                                        pks[i].tobytes()) == 0), i
 
 
+@pytest.mark.parametrize("arena", [None, 300 * 1024])
+def test_packed_units_mixed_lengths(gpu_engine, oracle, arena):
+    """Length-bucketed SoA packing (mode "packed", north_star (1)): messages of
+    every SHA-512 block count 0 B .. 4 KiB (plus exact block boundaries) at
+    every byte alignment, packed into lane-interleaved units and hashed from
+    them; the bits equal the in-place (AoS) run and the oracle, on both paths.
+    A 300 KiB arena holds only the first groups: the rest are read in place."""
+    rng = np.random.default_rng(35)
+    n = 3000
+    pk, sk = gpu_engine.seed_keypair_batch(rng.integers(0, 256, (23, 32), dtype=np.uint8))
+    kidx = rng.integers(0, 23, n).astype(np.uint32)
+    lens = np.exp(rng.uniform(0, np.log(4096), n)).astype(int)
+    lens[::13] = 0
+    edges = [128 * b + d for b in range(33) for d in (-81, -80, -79, -65, -64, -63) if 0 <= 128 * b + d <= 4096]
+    lens[2::11][:len(edges)] = edges
+    msgs = [bytes(rng.integers(0, 256, int(m), dtype=np.uint8)) for m in lens]
+    buf, off = pack_messages(msgs)
+    sig = gpu_engine.sign_batch(sk, kidx, buf, off)
+    sig[::6, 12] ^= 2
+    sig[3::11, 50] ^= 8
+    pks = pk[kidx]
+    gpu_engine.set_length_buckets(False)
+    plain = gpu_engine.verify_batch(sig, pks, buf, off)
+    try:
+        if arena is not None:
+            gpu_engine.set_unit_arena(arena)
+        gpu_engine.set_length_buckets("packed")
+        got = gpu_engine.verify_batch(sig, pks, buf, off)
+        assert (got == plain).all(), np.nonzero(got != plain)
+        gpu_engine.keys_reset()
+        gpu_engine.keys_add(pk)
+        keyed = gpu_engine.verify_batch_keyed(sig, kidx, buf, off)
+        assert (keyed == plain).all(), np.nonzero(keyed != plain)
+    finally:
+        gpu_engine.set_length_buckets("auto")
+        gpu_engine.set_unit_arena(1280 << 20)
+        gpu_engine.keys_reset()
+    want = np.ones(n, bool)
+    want[::6] = False
+    want[3::11] = False
+    assert (plain == want).all(), np.nonzero(plain != want)
+    for i in range(0, n, 71):
+        assert got[i] == (oracle.oracle_verify_detached(sig[i].tobytes(), msgs[i], len(msgs[i]),
+                                                       pks[i].tobytes()) == 0), i
+
+
 def test_spans_share_messages(gpu_engine):
     """edv_verify_spans_device: k signatures over one message copy (multi-sig
     requests) give the same bits as the contiguous layout with duplicated
@@ -429,11 +475,12 @@ def test_spans_share_messages(gpu_engine):
     torch.cuda.synchronize()
     got = np.unpackbits(words.cpu().numpy().view(np.uint8), bitorder="little")[:n].astype(bool)
     assert (got == want).all()
-    for keyed, keys in ((True, d_k), (False, d_pk)):  # sorted hash lanes over spans
-        gpu_engine.set_length_buckets(True)
+    for keyed, keys, mode in ((True, d_k, True), (False, d_pk, True), (True, d_k, "packed"),
+                              (False, d_pk, "packed")):  # sorted / packed hash lanes over spans
+        gpu_engine.set_length_buckets(mode)
         words.zero_()
         gpu_engine.verify_spans_device(d_sig, keys, keyed, d_msgs, d_ms, d_me, n, words)
         torch.cuda.synchronize()
         gpu_engine.set_length_buckets("auto")
         got = np.unpackbits(words.cpu().numpy().view(np.uint8), bitorder="little")[:n].astype(bool)
-        assert (got == want).all(), keyed
+        assert (got == want).all(), (keyed, mode)

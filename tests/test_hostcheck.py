@@ -34,6 +34,37 @@ def test_kernel_sha512_any_alignment(hostcheck):
         assert out.raw == hashlib.sha512(pre + m).digest()
 
 
+def test_kernel_sha512_packed_units(hostcheck):
+    """Length-bucketed SoA layout (sha512.h pack_lane_units /
+    sha512_prefixed_units): every SHA-512 block boundary of R||A||M around
+    0..4 KiB, any alignment, lane stride 1 and 64; the units are the padded
+    big-endian stream words after the 64-byte prefix, bit length last."""
+    hostcheck.edv_host_sha512_units_count.restype = ctypes.c_uint64
+    rng = random.Random(8)
+    lens = sorted({k for b in range(34) for k in (128 * b - 81, 128 * b - 80, 128 * b - 79, 128 * b - 65,
+                                                   128 * b - 64, 128 * b - 63) if 0 <= k <= 4200} | {0, 1, 15, 16, 17})
+    for t, mlen in enumerate(lens + [rng.randrange(0, 4200) for _ in range(60)]):
+        pre = bytes(rng.getrandbits(8) for _ in range(64))
+        m = bytes(rng.getrandbits(8) for _ in range(mlen))
+        off = rng.randrange(0, 16)
+        buf = ctypes.create_string_buffer(b"\0" * off + m + b"\0" * 16)
+        stride = 64 if t % 2 else 1
+        nu = hostcheck.edv_host_sha512_units_count(ctypes.c_uint64(mlen))
+        units = ctypes.create_string_buffer(16 * nu)
+        out = ctypes.create_string_buffer(64)
+        hostcheck.edv_host_sha512_units(out, pre, ctypes.byref(buf, off), ctypes.c_uint64(mlen),
+                                        ctypes.c_uint64(stride), units)
+        assert out.raw == hashlib.sha512(pre + m).digest(), (mlen, off)
+        # the units are the stream after the prefix: M || 0x80 || 0.. || 128-bit length, as u64 words
+        total = 64 + mlen
+        nblocks = (total + 16) // 128 + 1
+        assert nu == 8 * nblocks - 4
+        stream = m + b"\x80" + b"\0" * (128 * nblocks - total - 17) + (8 * total).to_bytes(16, "big")
+        words = [int.from_bytes(stream[8 * k:8 * k + 8], "big") for k in range(2 * nu)]
+        got = [int.from_bytes(units.raw[8 * k:8 * k + 8], "little") for k in range(2 * nu)]
+        assert got == words, (mlen, off)
+
+
 def test_kernel_sc_reduce_and_canonical(hostcheck):
     rng = random.Random(6)
     specials = [0, 1, L - 1, L, L + 1, 2 * L, 2**512 - 1, 2**512 - 1 - L, 2**252, 2**253 - 1, (2**256 - 1) * L % 2**512]
