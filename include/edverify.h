@@ -245,6 +245,34 @@ int edv_tally_finish_device(edv_ctx *ctx, const void *d_ballot, uint32_t n_keys,
 int edv_tally(edv_ctx *ctx, const uint32_t *key, const uint8_t *voter, const uint8_t *phase, const uint8_t *valid,
               const uint8_t *primary, uint64_t n_votes, uint32_t n_keys, uint32_t n_validators, uint32_t *counts_out, uint8_t *quorum_out);
 
+/* ------------------------------------------------ BLS multi-signatures
+ * The COMMIT / state-proof BLS check, replacing indy-crypto
+ * 0.1.6 under crypto/bls/indy_crypto/bls_crypto_indy_crypto.py:59-90 over
+ * AMCL BN254 (algorithm: oracle/bls_bn254_oracle.py).  Wire forms: G1
+ * (signatures) 128 bytes 0x04 | x | y | 63 zero bytes; G2 (generator,
+ * verkeys) 128 bytes x.a | x.b | y.a | y.b; 32-byte big-endian coordinates.
+ * A G1/G2 encoding that is off the curve decodes to the point at infinity.
+ * One GPU lane per check; host-pointer calls, synchronous. */
+
+/* BlsCryptoVerifierIndyCrypto.verify_sig (:59-70) over a batch: item i
+ * accepts iff e(sig_i, gen) == e(H(m_i), vk_i), H = indy-crypto Bls::_hash.
+ * vk_off == NULL: one verkey per item (vk128[i]); else verify_multi_sig
+ * (:72-84): item i's verkey is the sum of vk128[vk_off[i] .. vk_off[i+1]).
+ * msg_off[n + 1] as edv_verify_batch.  accept_bits: ceil(n/8) bytes. */
+int edv_bls_verify_batch(edv_ctx *ctx, const uint8_t *sig128, const uint8_t *msgs, const uint64_t *msg_off,
+                         const uint8_t *vk128, const uint64_t *vk_off, const uint8_t *gen128, uint64_t n,
+                         uint8_t *accept_bits);
+/* BlsCryptoVerifierIndyCrypto.create_multi_sig (:86-90) over a batch:
+ * out128[i] = sum of sig128[sig_off[i] .. sig_off[i+1]) (MultiSignature.new). */
+int edv_bls_aggregate(edv_ctx *ctx, const uint8_t *sig128, const uint64_t *sig_off, uint64_t m, uint8_t *out128);
+/* Test / bench data: sig128[i] = [sk_i] H(m_i) (BlsCryptoSignerIndyCrypto.sign,
+ * :112-114), vk128[i] = [sk_i] gen (VerKey.new); sk 32 bytes big-endian < r.
+ * (indy-crypto derives sk from a seed with AMCL's RAND; that derivation is
+ * not restated.) */
+int edv_bls_sign_batch(edv_ctx *ctx, const uint8_t *sk32, const uint8_t *msgs, const uint64_t *msg_off, uint64_t n,
+                       uint8_t *sig128);
+int edv_bls_keygen_batch(edv_ctx *ctx, const uint8_t *sk32, const uint8_t *gen128, uint64_t n, uint8_t *vk128);
+
 #ifdef __cplusplus
 }
 #endif

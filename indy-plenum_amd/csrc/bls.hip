@@ -1,0 +1,253 @@
+// bls.hip -- the BLS multi-signature check of Plenum's COMMIT / state-proof
+// path on MI355X, one lane per check, behind include/edverify.h.
+//
+// Replaces indy-crypto 0.1.6 under crypto/bls/indy_crypto/
+// bls_crypto_indy_crypto.py:59-90 (Bls.verify, Bls.verify_multi_sig,
+// MultiSignature.new), called from plenum/bls/bls_bft_replica_plenum.py:157,
+// :170, :205 and plenum/client/client.py:541.  Arithmetic: bn254.h.
+//   edv_bls_verify_kernel   decode sig (G1) and verkeys (G2), sum the verkeys
+//                           of a multi-signature, H(m), then
+//                           FE(ML(sig, g) * ML(-H, vk)) == 1; wave ballot
+//   edv_bls_aggregate_kernel  create_multi_sig: the sum of G1 points
+//   edv_bls_sign_kernel / edv_bls_keygen_kernel  [sk]H(m), [sk]g (test data)
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+#include "../../include/edverify.h"
+#include "bn254.h"
+#include "edv_internal.h"
+
+using namespace edv::bn;
+using edv_internal::set_err;
+
+#define BLS_TRY(expr)                                                                              \
+  do {                                                                                             \
+    hipError_t e_ = (expr);                                                                        \
+    if (e_ != hipSuccess) return set_err(EDV_EHIP, "%s: %s", #expr, hipGetErrorString(e_));        \
+  } while (0)
+
+namespace {
+
+constexpr int kBlsBlock = 64;
+
+__global__ __launch_bounds__(kBlsBlock) void edv_bls_verify_kernel(const uint8_t* __restrict__ sig128,
+                                                                  const uint8_t* __restrict__ msgs,
+                                                                  const uint64_t* __restrict__ moff,
+                                                                  const uint8_t* __restrict__ vk128,
+                                                                  const uint64_t* __restrict__ vk_off,
+                                                                  const uint8_t* __restrict__ gen128, uint64_t n,
+                                                                  unsigned long long* __restrict__ words) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool ok = false;
+  if (i < n) {
+    g1 s, h;
+    g2 v, g;
+    g1_from_bytes(s, sig128 + 128 * i);
+    g1_hash(h, msgs + moff[i], moff[i + 1] - moff[i]);
+    const uint64_t k0 = vk_off ? vk_off[i] : i, k1 = vk_off ? vk_off[i + 1] : i + 1;
+    g2_inf(v);
+    for (uint64_t k = k0; k < k1; ++k) {  // Bls.verify_multi_sig: the verkeys' sum
+      g2 t;
+      g2_from_bytes(t, vk128 + 128 * k);
+      g2_add(v, v, t);
+    }
+    g2_from_bytes(g, gen128);
+    ok = bls_check(s, h, v, g);
+  }
+  const unsigned long long b = __ballot(ok);  // every lane of the wave takes part
+  if ((threadIdx.x & 63) == 0 && i < n) words[i >> 6] = b;
+}
+
+__global__ __launch_bounds__(kBlsBlock) void edv_bls_aggregate_kernel(const uint8_t* __restrict__ sig128,
+                                                                     const uint64_t* __restrict__ off, uint64_t m,
+                                                                     uint8_t* __restrict__ out128) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  g1 acc;
+  g1_inf(acc);
+  for (uint64_t k = off[i]; k < off[i + 1]; ++k) {
+    g1 t;
+    g1_from_bytes(t, sig128 + 128 * k);
+    g1_add(acc, acc, t);
+  }
+  g1_to_bytes(out128 + 128 * i, acc);
+}
+
+__global__ __launch_bounds__(kBlsBlock) void edv_bls_sign_kernel(const uint8_t* __restrict__ sk32,
+                                                                const uint8_t* __restrict__ msgs,
+                                                                const uint64_t* __restrict__ moff, uint64_t n,
+                                                                uint8_t* __restrict__ sig128) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t k[8];
+  words_from_be(k, sk32 + 32 * i);
+  g1 h, s;
+  g1_hash(h, msgs + moff[i], moff[i + 1] - moff[i]);
+  g1_mul(s, h, k);
+  g1_to_bytes(sig128 + 128 * i, s);
+}
+
+__global__ __launch_bounds__(kBlsBlock) void edv_bls_keygen_kernel(const uint8_t* __restrict__ sk32,
+                                                                  const uint8_t* __restrict__ gen128, uint64_t n,
+                                                                  uint8_t* __restrict__ vk128) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t k[8];
+  words_from_be(k, sk32 + 32 * i);
+  g2 g, v;
+  g2_from_bytes(g, gen128);
+  g2_mul(v, g, k);
+  g2_to_bytes(vk128 + 128 * i, v);
+}
+
+// Device buffers of one host-pointer call, freed on every exit.
+struct Scratch {
+  std::vector<void*> p;
+  ~Scratch() {
+    for (void* q : p) (void)hipFree(q);
+  }
+  template <class T>
+  int alloc(T** out, size_t bytes) {
+    void* q = nullptr;
+    hipError_t e = hipMalloc(&q, bytes ? bytes : 16);
+    if (e != hipSuccess) return set_err(EDV_ENOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+    p.push_back(q);
+    *out = (T*)q;
+    return 0;
+  }
+};
+
+int check_offsets(const uint64_t* off, uint64_t n, const char* what) {
+  if (!off) return set_err(EDV_EINVAL, "null %s", what);
+  for (uint64_t i = 0; i < n; ++i)
+    if (off[i + 1] < off[i]) return set_err(EDV_EINVAL, "%s[%llu] decreasing", what, (unsigned long long)i);
+  return 0;
+}
+
+// Messages [off[0], off[n]) to the device, offsets rebased to 0.
+int upload_msgs(Scratch& sc, hipStream_t st, const uint8_t* msgs, const uint64_t* off, uint64_t n, uint8_t** d_msgs,
+                uint64_t** d_off) {
+  const uint64_t m0 = off[0], mbytes = off[n] - m0;
+  if (mbytes && !msgs) return set_err(EDV_EINVAL, "null msgs");
+  int r;
+  if ((r = sc.alloc(d_msgs, mbytes + 16)) || (r = sc.alloc(d_off, 8 * (n + 1)))) return r;
+  std::vector<uint64_t> o(n + 1);
+  for (uint64_t i = 0; i <= n; ++i) o[i] = off[i] - m0;
+  if (mbytes) BLS_TRY(hipMemcpyAsync(*d_msgs, msgs + m0, mbytes, hipMemcpyHostToDevice, st));
+  BLS_TRY(hipMemcpyAsync(*d_off, o.data(), 8 * (n + 1), hipMemcpyHostToDevice, st));
+  BLS_TRY(hipStreamSynchronize(st));  // o is freed on return
+  return 0;
+}
+
+uint32_t grid_of(uint64_t n) { return (uint32_t)((n + kBlsBlock - 1) / kBlsBlock); }
+
+}  // namespace
+
+extern "C" {
+
+int edv_bls_verify_batch(edv_ctx* ctx, const uint8_t* sig128, const uint8_t* msgs, const uint64_t* msg_off,
+                         const uint8_t* vk128, const uint64_t* vk_off, const uint8_t* gen128, uint64_t n,
+                         uint8_t* accept_bits) {
+  hipStream_t st;
+  int r = edv_internal::begin(ctx, &st);
+  if (r) return r;
+  if (n == 0) return 0;
+  if (!sig128 || !vk128 || !gen128 || !accept_bits) return set_err(EDV_EINVAL, "null pointer");
+  if ((r = check_offsets(msg_off, n, "msg_off"))) return r;
+  if (vk_off && (r = check_offsets(vk_off, n, "vk_off"))) return r;
+  const uint64_t nvk = vk_off ? vk_off[n] - vk_off[0] : n, vk0 = vk_off ? vk_off[0] : 0;
+  Scratch sc;
+  uint8_t *d_sig, *d_vk, *d_gen, *d_msgs;
+  uint64_t *d_off, *d_vkoff = nullptr;
+  unsigned long long* d_words;
+  const uint64_t nwords = (n + 63) / 64;
+  if ((r = sc.alloc(&d_sig, 128 * n)) || (r = sc.alloc(&d_vk, 128 * nvk)) || (r = sc.alloc(&d_gen, 128)) ||
+      (r = sc.alloc(&d_words, 8 * nwords)) || (r = upload_msgs(sc, st, msgs, msg_off, n, &d_msgs, &d_off)))
+    return r;
+  BLS_TRY(hipMemcpyAsync(d_sig, sig128, 128 * n, hipMemcpyHostToDevice, st));
+  BLS_TRY(hipMemcpyAsync(d_vk, vk128 + 128 * vk0, 128 * nvk, hipMemcpyHostToDevice, st));
+  BLS_TRY(hipMemcpyAsync(d_gen, gen128, 128, hipMemcpyHostToDevice, st));
+  std::vector<uint64_t> vo;
+  if (vk_off) {
+    if ((r = sc.alloc(&d_vkoff, 8 * (n + 1)))) return r;
+    vo.resize(n + 1);
+    for (uint64_t i = 0; i <= n; ++i) vo[i] = vk_off[i] - vk0;
+    BLS_TRY(hipMemcpyAsync(d_vkoff, vo.data(), 8 * (n + 1), hipMemcpyHostToDevice, st));
+  }
+  hipLaunchKernelGGL(edv_bls_verify_kernel, dim3(grid_of(n)), dim3(kBlsBlock), 0, st, d_sig, d_msgs, d_off, d_vk,
+                     d_vkoff, d_gen, n, d_words);
+  BLS_TRY(hipGetLastError());
+  std::vector<unsigned long long> w(nwords);
+  BLS_TRY(hipMemcpyAsync(w.data(), d_words, 8 * nwords, hipMemcpyDeviceToHost, st));
+  BLS_TRY(hipStreamSynchronize(st));
+  for (uint64_t b = 0; b < (n + 7) / 8; ++b) accept_bits[b] = (uint8_t)(w[b / 8] >> (8 * (b % 8)));
+  if (n & 7) accept_bits[n / 8] &= (uint8_t)((1u << (n & 7)) - 1);
+  return 0;
+}
+
+int edv_bls_aggregate(edv_ctx* ctx, const uint8_t* sig128, const uint64_t* sig_off, uint64_t m, uint8_t* out128) {
+  hipStream_t st;
+  int r = edv_internal::begin(ctx, &st);
+  if (r) return r;
+  if (m == 0) return 0;
+  if (!sig128 || !out128) return set_err(EDV_EINVAL, "null pointer");
+  if ((r = check_offsets(sig_off, m, "sig_off"))) return r;
+  const uint64_t s0 = sig_off[0], ns = sig_off[m] - s0;
+  Scratch sc;
+  uint8_t *d_sig, *d_out;
+  uint64_t* d_off;
+  if ((r = sc.alloc(&d_sig, 128 * ns)) || (r = sc.alloc(&d_out, 128 * m)) || (r = sc.alloc(&d_off, 8 * (m + 1))))
+    return r;
+  std::vector<uint64_t> o(m + 1);
+  for (uint64_t i = 0; i <= m; ++i) o[i] = sig_off[i] - s0;
+  BLS_TRY(hipMemcpyAsync(d_sig, sig128 + 128 * s0, 128 * ns, hipMemcpyHostToDevice, st));
+  BLS_TRY(hipMemcpyAsync(d_off, o.data(), 8 * (m + 1), hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(edv_bls_aggregate_kernel, dim3(grid_of(m)), dim3(kBlsBlock), 0, st, d_sig, d_off, m, d_out);
+  BLS_TRY(hipGetLastError());
+  BLS_TRY(hipMemcpyAsync(out128, d_out, 128 * m, hipMemcpyDeviceToHost, st));
+  BLS_TRY(hipStreamSynchronize(st));
+  return 0;
+}
+
+int edv_bls_sign_batch(edv_ctx* ctx, const uint8_t* sk32, const uint8_t* msgs, const uint64_t* msg_off, uint64_t n,
+                       uint8_t* sig128) {
+  hipStream_t st;
+  int r = edv_internal::begin(ctx, &st);
+  if (r) return r;
+  if (n == 0) return 0;
+  if (!sk32 || !sig128) return set_err(EDV_EINVAL, "null pointer");
+  if ((r = check_offsets(msg_off, n, "msg_off"))) return r;
+  Scratch sc;
+  uint8_t *d_sk, *d_msgs, *d_sig;
+  uint64_t* d_off;
+  if ((r = sc.alloc(&d_sk, 32 * n)) || (r = sc.alloc(&d_sig, 128 * n)) ||
+      (r = upload_msgs(sc, st, msgs, msg_off, n, &d_msgs, &d_off)))
+    return r;
+  BLS_TRY(hipMemcpyAsync(d_sk, sk32, 32 * n, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(edv_bls_sign_kernel, dim3(grid_of(n)), dim3(kBlsBlock), 0, st, d_sk, d_msgs, d_off, n, d_sig);
+  BLS_TRY(hipGetLastError());
+  BLS_TRY(hipMemcpyAsync(sig128, d_sig, 128 * n, hipMemcpyDeviceToHost, st));
+  BLS_TRY(hipStreamSynchronize(st));
+  return 0;
+}
+
+int edv_bls_keygen_batch(edv_ctx* ctx, const uint8_t* sk32, const uint8_t* gen128, uint64_t n, uint8_t* vk128) {
+  hipStream_t st;
+  int r = edv_internal::begin(ctx, &st);
+  if (r) return r;
+  if (n == 0) return 0;
+  if (!sk32 || !gen128 || !vk128) return set_err(EDV_EINVAL, "null pointer");
+  Scratch sc;
+  uint8_t *d_sk, *d_gen, *d_vk;
+  if ((r = sc.alloc(&d_sk, 32 * n)) || (r = sc.alloc(&d_gen, 128)) || (r = sc.alloc(&d_vk, 128 * n))) return r;
+  BLS_TRY(hipMemcpyAsync(d_sk, sk32, 32 * n, hipMemcpyHostToDevice, st));
+  BLS_TRY(hipMemcpyAsync(d_gen, gen128, 128, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(edv_bls_keygen_kernel, dim3(grid_of(n)), dim3(kBlsBlock), 0, st, d_sk, d_gen, n, d_vk);
+  BLS_TRY(hipGetLastError());
+  BLS_TRY(hipMemcpyAsync(vk128, d_vk, 128 * n, hipMemcpyDeviceToHost, st));
+  BLS_TRY(hipStreamSynchronize(st));
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,960 @@
+// bn254.h -- BN254 (AMCL) arithmetic and the reduced optimal ate pairing for
+// the BLS multi-signature check of Plenum's COMMIT messages.
+//
+// Restates what the reference reaches through indy-crypto 0.1.6
+// (crypto/bls/indy_crypto/bls_crypto_indy_crypto.py:59-90: Bls.verify,
+// Bls.verify_multi_sig, MultiSignature.new) over AMCL BN254; the published
+// algorithm is written out in oracle/bls_bn254_oracle.py, which this code is
+// tested against (tests/test_bls.py).  One lane per signature check:
+//   Fp    8 x 32-bit limbs, Montgomery (R = 2^256), CIOS multiplication on
+//         v_mad_u64_u32; p < 2^254 so sums of two reduced values never carry
+//         out of 256 bits
+//   Fp2   Fp[i]/(i^2 + 1);  Fp6 = Fp2[v]/(v^3 - xi), xi = 1 + i;
+//   Fp12  Fp6[w]/(w^2 - v)  (w^6 = xi: the D-type twist of the generator)
+//   G1    y^2 = x^3 + 2 over Fp (signatures, H(m)); Jacobian coordinates
+//   G2    y^2 = x^3 + 2/xi over Fp2 (generator, verkeys); Jacobian
+//   pairing  Miller loop over |6x+2| with lines scaled by Fp2 factors (the
+//         final exponentiation removes them), conjugation for x < 0, the
+//         lines through pi(Q) and -pi^2(Q); final exponentiation
+//         (p^6 - 1)(p^2 + 1) by conjugation, inversion and Frobenius, then
+//         the hard part (p^4 - p^2 + 1)/r by square-and-multiply.
+#pragma once
+#include "bn254_constants.h"
+#include "fe25519.h"  // EDV_HD
+#include "sha256.h"
+
+// The large routines are real calls on the device (a fully inlined pairing
+// is hundreds of thousands of instructions); the small ones stay inline.
+#if defined(__HIPCC__)
+#define EDV_BN_NI static __host__ __device__ __attribute__((noinline))
+#else
+#define EDV_BN_NI static __attribute__((noinline))
+#endif
+
+namespace edv {
+namespace bn {
+
+struct fp {
+  uint32_t v[8];
+};
+struct fp2 {
+  fp a, b;
+};
+struct fp6 {
+  fp2 c0, c1, c2;
+};
+struct fp12 {
+  fp6 c0, c1;
+};
+struct g1 {  // Jacobian; Z = 0: infinity
+  fp X, Y, Z;
+};
+struct g2 {
+  fp2 X, Y, Z;
+};
+
+// ------------------------------------------------------------------ Fp
+EDV_HD void fp_load(fp& r, const uint32_t* c) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r.v[k] = c[k];
+}
+EDV_HD void fp_zero(fp& r) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r.v[k] = 0;
+}
+EDV_HD void fp_one(fp& r) { fp_load(r, kOne); }
+EDV_HD bool fp_iszero(const fp& a) {
+  uint32_t o = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) o |= a.v[k];
+  return o == 0;
+}
+EDV_HD bool fp_eq(const fp& a, const fp& b) {
+  uint32_t o = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) o |= a.v[k] ^ b.v[k];
+  return o == 0;
+}
+// a >= p (plain integers)
+EDV_HD bool fp_geq_p(const uint32_t a[8]) {
+  for (int k = 7; k >= 0; --k) {
+    if (a[k] != kP[k]) return a[k] > kP[k];
+  }
+  return true;
+}
+// r = a - p if a >= p (a < 2p)
+EDV_HD void fp_reduce_once(fp& r, const uint32_t a[8]) {
+  uint32_t t[8];
+  uint64_t br = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint64_t d = (uint64_t)a[k] - kP[k] - br;
+    t[k] = (uint32_t)d;
+    br = (d >> 32) & 1;
+  }
+  const bool keep = br != 0;  // a < p
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r.v[k] = keep ? a[k] : t[k];
+}
+EDV_HD void fp_add(fp& r, const fp& a, const fp& b) {
+  uint32_t s[8];
+  uint64_t c = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint64_t t = (uint64_t)a.v[k] + b.v[k] + c;
+    s[k] = (uint32_t)t;
+    c = t >> 32;
+  }
+  fp_reduce_once(r, s);
+}
+EDV_HD void fp_sub(fp& r, const fp& a, const fp& b) {
+  uint32_t d[8];
+  uint64_t br = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint64_t t = (uint64_t)a.v[k] - b.v[k] - br;
+    d[k] = (uint32_t)t;
+    br = (t >> 32) & 1;
+  }
+  const uint32_t m = 0u - (uint32_t)br;  // add p back on borrow
+  uint64_t c = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint64_t t = (uint64_t)d[k] + (kP[k] & m) + c;
+    r.v[k] = (uint32_t)t;
+    c = t >> 32;
+  }
+}
+EDV_HD void fp_neg(fp& r, const fp& a) {
+  fp z;
+  fp_zero(z);
+  fp_sub(r, z, a);
+}
+EDV_HD void fp_dbl(fp& r, const fp& a) { fp_add(r, a, a); }
+
+// Montgomery product a * b / 2^256 mod p (CIOS; inputs < p, output < p).
+EDV_BN_NI void fp_mul(fp& r, const fp& a, const fp& b) {
+  uint32_t t[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) t[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint64_t s = (uint64_t)a.v[j] * b.v[i] + t[j] + c;
+      t[j] = (uint32_t)s;
+      c = s >> 32;
+    }
+    uint64_t s = (uint64_t)t[8] + c;
+    t[8] = (uint32_t)s;
+    t[9] = (uint32_t)(s >> 32);
+    const uint32_t m = t[0] * kNP0;
+    s = (uint64_t)m * kP[0] + t[0];
+    c = s >> 32;
+#pragma unroll
+    for (int j = 1; j < 8; ++j) {
+      s = (uint64_t)m * kP[j] + t[j] + c;
+      t[j - 1] = (uint32_t)s;
+      c = s >> 32;
+    }
+    s = (uint64_t)t[8] + c;
+    t[7] = (uint32_t)s;
+    t[8] = t[9] + (uint32_t)(s >> 32);
+  }
+  fp_reduce_once(r, t);
+}
+EDV_HD void fp_sqr(fp& r, const fp& a) { fp_mul(r, a, a); }
+
+// a^e for a plain exponent of nw little-endian words (square and multiply, MSB first)
+EDV_BN_NI void fp_pow(fp& r, const fp& a, const uint32_t* e, int nw) {
+  fp acc;
+  fp_one(acc);
+  for (int w = nw - 1; w >= 0; --w) {
+    const uint32_t word = e[w];
+    for (int bit = 31; bit >= 0; --bit) {
+      fp_sqr(acc, acc);
+      if ((word >> bit) & 1u) fp_mul(acc, acc, a);
+    }
+  }
+  r = acc;
+}
+EDV_HD void fp_inv(fp& r, const fp& a) { fp_pow(r, a, kPm2, 8); }
+
+// 32 big-endian bytes -> plain limbs
+EDV_HD void words_from_be(uint32_t w[8], const uint8_t* b) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint8_t* q = b + 28 - 4 * k;
+    w[k] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+  }
+}
+EDV_HD void words_to_be(uint8_t* b, const uint32_t w[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    uint8_t* q = b + 28 - 4 * k;
+    q[0] = (uint8_t)(w[k] >> 24);
+    q[1] = (uint8_t)(w[k] >> 16);
+    q[2] = (uint8_t)(w[k] >> 8);
+    q[3] = (uint8_t)w[k];
+  }
+}
+// plain (< p) -> Montgomery
+EDV_HD void fp_from_plain(fp& r, const uint32_t w[8]) {
+  fp a, r2;
+  fp_load(a, w);
+  fp_load(r2, kR2);
+  fp_mul(r, a, r2);
+}
+// Montgomery -> plain
+EDV_HD void fp_to_plain(uint32_t w[8], const fp& a) {
+  fp one;
+  fp_zero(one);
+  one.v[0] = 1;
+  fp t;
+  fp_mul(t, a, one);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) w[k] = t.v[k];
+}
+// 32 BE bytes -> Fp; false if the integer is >= p
+EDV_HD bool fp_from_be(fp& r, const uint8_t* b) {
+  uint32_t w[8];
+  words_from_be(w, b);
+  if (fp_geq_p(w)) return false;
+  fp_from_plain(r, w);
+  return true;
+}
+
+// ------------------------------------------------------------------ Fp2
+EDV_HD void fp2_zero(fp2& r) {
+  fp_zero(r.a);
+  fp_zero(r.b);
+}
+EDV_HD void fp2_one(fp2& r) {
+  fp_one(r.a);
+  fp_zero(r.b);
+}
+EDV_HD void fp2_load(fp2& r, const uint32_t* c) {
+  fp_load(r.a, c);
+  fp_load(r.b, c + 8);
+}
+EDV_HD bool fp2_iszero(const fp2& x) { return fp_iszero(x.a) && fp_iszero(x.b); }
+EDV_HD bool fp2_eq(const fp2& x, const fp2& y) { return fp_eq(x.a, y.a) && fp_eq(x.b, y.b); }
+EDV_HD void fp2_add(fp2& r, const fp2& x, const fp2& y) {
+  fp_add(r.a, x.a, y.a);
+  fp_add(r.b, x.b, y.b);
+}
+EDV_HD void fp2_sub(fp2& r, const fp2& x, const fp2& y) {
+  fp_sub(r.a, x.a, y.a);
+  fp_sub(r.b, x.b, y.b);
+}
+EDV_HD void fp2_neg(fp2& r, const fp2& x) {
+  fp_neg(r.a, x.a);
+  fp_neg(r.b, x.b);
+}
+EDV_HD void fp2_dbl(fp2& r, const fp2& x) { fp2_add(r, x, x); }
+EDV_HD void fp2_conj(fp2& r, const fp2& x) {
+  r.a = x.a;
+  fp_neg(r.b, x.b);
+}
+// (a + b i)(c + d i), Karatsuba: 3 Fp products
+EDV_BN_NI void fp2_mul(fp2& r, const fp2& x, const fp2& y) {
+  fp t0, t1, s0, s1, t2;
+  fp_mul(t0, x.a, y.a);
+  fp_mul(t1, x.b, y.b);
+  fp_add(s0, x.a, x.b);
+  fp_add(s1, y.a, y.b);
+  fp_mul(t2, s0, s1);
+  fp_sub(r.a, t0, t1);
+  fp_sub(t2, t2, t0);
+  fp_sub(r.b, t2, t1);
+}
+EDV_BN_NI void fp2_sqr(fp2& r, const fp2& x) {  // (a+b)(a-b) + 2ab i
+  fp s, d, ab;
+  fp_add(s, x.a, x.b);
+  fp_sub(d, x.a, x.b);
+  fp_mul(ab, x.a, x.b);
+  fp_mul(r.a, s, d);
+  fp_dbl(r.b, ab);
+}
+EDV_HD void fp2_mul_fp(fp2& r, const fp2& x, const fp& k) {
+  fp_mul(r.a, x.a, k);
+  fp_mul(r.b, x.b, k);
+}
+EDV_HD void fp2_mul_xi(fp2& r, const fp2& x) {  // (a + b i)(1 + i) = (a - b) + (a + b) i
+  fp t;
+  fp_sub(t, x.a, x.b);
+  fp_add(r.b, x.a, x.b);
+  r.a = t;
+}
+EDV_BN_NI void fp2_inv(fp2& r, const fp2& x) {  // (a - b i) / (a^2 + b^2)
+  fp t0, t1;
+  fp_sqr(t0, x.a);
+  fp_sqr(t1, x.b);
+  fp_add(t0, t0, t1);
+  fp_inv(t1, t0);
+  fp_mul(r.a, x.a, t1);
+  fp_mul(t0, x.b, t1);
+  fp_neg(r.b, t0);
+}
+
+// ------------------------------------------------------------------ Fp6
+EDV_HD void fp6_zero(fp6& r) {
+  fp2_zero(r.c0);
+  fp2_zero(r.c1);
+  fp2_zero(r.c2);
+}
+EDV_HD void fp6_add(fp6& r, const fp6& x, const fp6& y) {
+  fp2_add(r.c0, x.c0, y.c0);
+  fp2_add(r.c1, x.c1, y.c1);
+  fp2_add(r.c2, x.c2, y.c2);
+}
+EDV_HD void fp6_sub(fp6& r, const fp6& x, const fp6& y) {
+  fp2_sub(r.c0, x.c0, y.c0);
+  fp2_sub(r.c1, x.c1, y.c1);
+  fp2_sub(r.c2, x.c2, y.c2);
+}
+EDV_HD void fp6_neg(fp6& r, const fp6& x) {
+  fp2_neg(r.c0, x.c0);
+  fp2_neg(r.c1, x.c1);
+  fp2_neg(r.c2, x.c2);
+}
+// Karatsuba over v^3 = xi: 6 Fp2 products
+EDV_BN_NI void fp6_mul(fp6& r, const fp6& x, const fp6& y) {
+  fp2 t0, t1, t2, s, u, c0, c1, c2;
+  fp2_mul(t0, x.c0, y.c0);
+  fp2_mul(t1, x.c1, y.c1);
+  fp2_mul(t2, x.c2, y.c2);
+  fp2_add(s, x.c1, x.c2);
+  fp2_add(u, y.c1, y.c2);
+  fp2_mul(c0, s, u);
+  fp2_sub(c0, c0, t1);
+  fp2_sub(c0, c0, t2);
+  fp2_mul_xi(c0, c0);
+  fp2_add(c0, c0, t0);
+  fp2_add(s, x.c0, x.c1);
+  fp2_add(u, y.c0, y.c1);
+  fp2_mul(c1, s, u);
+  fp2_sub(c1, c1, t0);
+  fp2_sub(c1, c1, t1);
+  fp2_mul_xi(s, t2);
+  fp2_add(c1, c1, s);
+  fp2_add(s, x.c0, x.c2);
+  fp2_add(u, y.c0, y.c2);
+  fp2_mul(c2, s, u);
+  fp2_sub(c2, c2, t0);
+  fp2_sub(c2, c2, t2);
+  fp2_add(c2, c2, t1);
+  r.c0 = c0;
+  r.c1 = c1;
+  r.c2 = c2;
+}
+EDV_HD void fp6_mul_v(fp6& r, const fp6& x) {  // (c0 + c1 v + c2 v^2) v = xi c2 + c0 v + c1 v^2
+  fp2 t;
+  fp2_mul_xi(t, x.c2);
+  r.c2 = x.c1;
+  r.c1 = x.c0;
+  r.c0 = t;
+}
+EDV_BN_NI void fp6_inv(fp6& r, const fp6& x) {
+  fp2 t0, t1, t2, s, d;
+  fp2_sqr(t0, x.c0);  // t0 = c0^2 - xi c1 c2
+  fp2_mul(s, x.c1, x.c2);
+  fp2_mul_xi(s, s);
+  fp2_sub(t0, t0, s);
+  fp2_sqr(t1, x.c2);  // t1 = xi c2^2 - c0 c1
+  fp2_mul_xi(t1, t1);
+  fp2_mul(s, x.c0, x.c1);
+  fp2_sub(t1, t1, s);
+  fp2_sqr(t2, x.c1);  // t2 = c1^2 - c0 c2
+  fp2_mul(s, x.c0, x.c2);
+  fp2_sub(t2, t2, s);
+  fp2_mul(d, x.c2, t1);  // d = c0 t0 + xi (c2 t1 + c1 t2)
+  fp2_mul(s, x.c1, t2);
+  fp2_add(d, d, s);
+  fp2_mul_xi(d, d);
+  fp2_mul(s, x.c0, t0);
+  fp2_add(d, d, s);
+  fp2_inv(d, d);
+  fp2_mul(r.c0, t0, d);
+  fp2_mul(r.c1, t1, d);
+  fp2_mul(r.c2, t2, d);
+}
+
+// ------------------------------------------------------------------ Fp12
+EDV_HD void fp12_one(fp12& r) {
+  fp6_zero(r.c0);
+  fp6_zero(r.c1);
+  fp2_one(r.c0.c0);
+}
+EDV_HD bool fp12_isone(const fp12& x) {
+  fp2 one;
+  fp2_one(one);
+  return fp2_eq(x.c0.c0, one) && fp2_iszero(x.c0.c1) && fp2_iszero(x.c0.c2) && fp2_iszero(x.c1.c0) &&
+         fp2_iszero(x.c1.c1) && fp2_iszero(x.c1.c2);
+}
+EDV_BN_NI void fp12_mul(fp12& r, const fp12& x, const fp12& y) {  // 3 Fp6 products
+  fp6 t0, t1, s, u;
+  fp6_mul(t0, x.c0, y.c0);
+  fp6_mul(t1, x.c1, y.c1);
+  fp6_add(s, x.c0, x.c1);
+  fp6_add(u, y.c0, y.c1);
+  fp6_mul(s, s, u);
+  fp6_sub(s, s, t0);
+  fp6_sub(r.c1, s, t1);
+  fp6_mul_v(t1, t1);
+  fp6_add(r.c0, t0, t1);
+}
+EDV_BN_NI void fp12_sqr(fp12& r, const fp12& x) {  // complex squaring: 2 Fp6 products
+  fp6 t, s, u, ab;
+  fp6_mul(ab, x.c0, x.c1);
+  fp6_add(s, x.c0, x.c1);
+  fp6_mul_v(t, x.c1);
+  fp6_add(u, x.c0, t);
+  fp6_mul(s, s, u);  // (a + b)(a + v b) = a^2 + v b^2 + (1 + v) ab
+  fp6_sub(s, s, ab);
+  fp6_mul_v(t, ab);
+  fp6_sub(r.c0, s, t);
+  fp6_add(r.c1, ab, ab);
+}
+EDV_HD void fp12_conj(fp12& r, const fp12& x) {
+  r.c0 = x.c0;
+  fp6_neg(r.c1, x.c1);
+}
+EDV_BN_NI void fp12_inv(fp12& r, const fp12& x) {  // (a - b w) / (a^2 - v b^2)
+  fp6 t0, t1;
+  fp6_mul(t0, x.c0, x.c0);
+  fp6_mul(t1, x.c1, x.c1);
+  fp6_mul_v(t1, t1);
+  fp6_sub(t0, t0, t1);
+  fp6_inv(t1, t0);
+  fp6_mul(r.c0, x.c0, t1);
+  fp6_mul(t0, x.c1, t1);
+  fp6_neg(r.c1, t0);
+}
+// Frobenius x -> x^p: the Fp2 coefficient of w^e is conjugated and
+// multiplied by gamma_e = xi^(e (p-1) / 6) (e = 2j + k for c_k.c_j)
+EDV_BN_NI void fp12_frob(fp12& r, const fp12& x) {
+  fp2 g, t;
+  fp2_conj(r.c0.c0, x.c0.c0);  // gamma_0 = 1
+  fp2_load(g, kGamma2);
+  fp2_conj(t, x.c0.c1);
+  fp2_mul(r.c0.c1, t, g);
+  fp2_load(g, kGamma4);
+  fp2_conj(t, x.c0.c2);
+  fp2_mul(r.c0.c2, t, g);
+  fp2_load(g, kGamma1);
+  fp2_conj(t, x.c1.c0);
+  fp2_mul(r.c1.c0, t, g);
+  fp2_load(g, kGamma3);
+  fp2_conj(t, x.c1.c1);
+  fp2_mul(r.c1.c1, t, g);
+  fp2_load(g, kGamma5);
+  fp2_conj(t, x.c1.c2);
+  fp2_mul(r.c1.c2, t, g);
+}
+
+// f * line, line = l0 + (l1 + l2 v) w, l0, l1, l2 in Fp2: the sparse
+// product (15 Fp2 products instead of the 18 of fp12_mul)
+EDV_BN_NI void fp6_mul_01(fp6& r, const fp6& a, const fp2& b0, const fp2& b1) {  // a * (b0 + b1 v)
+  fp2 t0, t1, u, w2, c0, c1, c2;
+  fp2_mul(t0, a.c0, b0);
+  fp2_mul(t1, a.c1, b1);
+  fp2_mul(u, a.c2, b1);  // c0 = t0 + xi a2 b1
+  fp2_mul_xi(u, u);
+  fp2_add(c0, t0, u);
+  fp2_add(u, a.c0, a.c1);  // c1 = (a0 + a1)(b0 + b1) - t0 - t1
+  fp2_add(w2, b0, b1);
+  fp2_mul(c1, u, w2);
+  fp2_sub(c1, c1, t0);
+  fp2_sub(c1, c1, t1);
+  fp2_mul(u, a.c2, b0);  // c2 = a2 b0 + t1
+  fp2_add(c2, u, t1);
+  r.c0 = c0;
+  r.c1 = c1;
+  r.c2 = c2;
+}
+EDV_BN_NI void fp12_mul_line(fp12& f, const fp2& l0, const fp2& l1, const fp2& l2) {
+  fp6 aA, bB, s;
+  fp2_mul(aA.c0, f.c0.c0, l0);  // a * (l0, 0, 0)
+  fp2_mul(aA.c1, f.c0.c1, l0);
+  fp2_mul(aA.c2, f.c0.c2, l0);
+  fp6_mul_01(bB, f.c1, l1, l2);  // b * (l1, l2, 0)
+  fp6_add(s, f.c0, f.c1);       // (a + b)(l0 + l1, l2, 0) - aA - bB
+  fp2 m0;
+  fp2_add(m0, l0, l1);
+  fp6_mul_01(s, s, m0, l2);
+  fp6_sub(s, s, aA);
+  fp6_sub(f.c1, s, bB);
+  fp6_mul_v(bB, bB);
+  fp6_add(f.c0, aA, bB);
+}
+
+// ------------------------------------------------------------------ G1 (Jacobian, a = 0)
+EDV_HD void g1_inf(g1& r) {
+  fp_one(r.X);
+  fp_one(r.Y);
+  fp_zero(r.Z);
+}
+EDV_HD bool g1_isinf(const g1& p) { return fp_iszero(p.Z); }
+EDV_BN_NI void g1_dbl(g1& r, const g1& p) {
+  if (g1_isinf(p)) {
+    r = p;
+    return;
+  }
+  fp A, B, C, D, E, F, t;
+  fp_sqr(A, p.X);
+  fp_sqr(B, p.Y);
+  fp_sqr(C, B);
+  fp_add(t, p.X, B);
+  fp_sqr(t, t);
+  fp_sub(t, t, A);
+  fp_sub(t, t, C);
+  fp_dbl(D, t);
+  fp_dbl(E, A);
+  fp_add(E, E, A);
+  fp_sqr(F, E);
+  fp Z3;
+  fp_mul(Z3, p.Y, p.Z);
+  fp_dbl(r.Z, Z3);
+  fp_sub(t, F, D);
+  fp_sub(r.X, t, D);
+  fp_sub(t, D, r.X);
+  fp_mul(t, E, t);
+  fp_dbl(C, C);
+  fp_dbl(C, C);
+  fp_dbl(C, C);
+  fp_sub(r.Y, t, C);
+}
+// general Jacobian addition (handles infinity and doubling)
+EDV_BN_NI void g1_add(g1& r, const g1& p, const g1& q) {
+  if (g1_isinf(p)) {
+    r = q;
+    return;
+  }
+  if (g1_isinf(q)) {
+    r = p;
+    return;
+  }
+  fp Z1Z1, Z2Z2, U1, U2, S1, S2, H, Rr, t;
+  fp_sqr(Z1Z1, p.Z);
+  fp_sqr(Z2Z2, q.Z);
+  fp_mul(U1, p.X, Z2Z2);
+  fp_mul(U2, q.X, Z1Z1);
+  fp_mul(t, q.Z, Z2Z2);
+  fp_mul(S1, p.Y, t);
+  fp_mul(t, p.Z, Z1Z1);
+  fp_mul(S2, q.Y, t);
+  fp_sub(H, U2, U1);
+  fp_sub(Rr, S2, S1);
+  if (fp_iszero(H)) {
+    if (fp_iszero(Rr)) {
+      g1_dbl(r, p);
+    } else {
+      g1_inf(r);
+    }
+    return;
+  }
+  fp HH, HHH, V;
+  fp_sqr(HH, H);
+  fp_mul(HHH, HH, H);
+  fp_mul(V, U1, HH);
+  fp X3, Y3, Z3;
+  fp_sqr(X3, Rr);
+  fp_sub(X3, X3, HHH);
+  fp_sub(X3, X3, V);
+  fp_sub(X3, X3, V);
+  fp_sub(t, V, X3);
+  fp_mul(Y3, Rr, t);
+  fp_mul(t, S1, HHH);
+  fp_sub(Y3, Y3, t);
+  fp_mul(t, p.Z, q.Z);
+  fp_mul(Z3, t, H);
+  r.X = X3;
+  r.Y = Y3;
+  r.Z = Z3;
+}
+// affine (x, y) of a finite point
+EDV_BN_NI void g1_affine(fp& x, fp& y, const g1& p) {
+  fp zi, z2, z3;
+  fp_inv(zi, p.Z);
+  fp_sqr(z2, zi);
+  fp_mul(z3, z2, zi);
+  fp_mul(x, p.X, z2);
+  fp_mul(y, p.Y, z3);
+}
+EDV_HD bool g1_on_curve_affine(const fp& x, const fp& y) {
+  fp l, r, b;
+  fp_sqr(l, y);
+  fp_sqr(r, x);
+  fp_mul(r, r, x);
+  fp_load(b, kB1);
+  fp_add(r, r, b);
+  return fp_eq(l, r);
+}
+// [k]P, k = 8 little-endian words (plain), MSB first
+EDV_BN_NI void g1_mul(g1& r, const g1& p, const uint32_t k[8]) {
+  g1 acc;
+  g1_inf(acc);
+  for (int w = 7; w >= 0; --w)
+    for (int bit = 31; bit >= 0; --bit) {
+      g1_dbl(acc, acc);
+      if ((k[w] >> bit) & 1u) g1_add(acc, acc, p);
+    }
+  r = acc;
+}
+
+// ------------------------------------------------------------------ G2 (Jacobian over Fp2)
+EDV_HD void g2_inf(g2& r) {
+  fp2_one(r.X);
+  fp2_one(r.Y);
+  fp2_zero(r.Z);
+}
+EDV_HD bool g2_isinf(const g2& p) { return fp2_iszero(p.Z); }
+EDV_BN_NI void g2_dbl(g2& r, const g2& p) {
+  if (g2_isinf(p)) {
+    r = p;
+    return;
+  }
+  fp2 A, B, C, D, E, F, t, Z3;
+  fp2_sqr(A, p.X);
+  fp2_sqr(B, p.Y);
+  fp2_sqr(C, B);
+  fp2_add(t, p.X, B);
+  fp2_sqr(t, t);
+  fp2_sub(t, t, A);
+  fp2_sub(t, t, C);
+  fp2_dbl(D, t);
+  fp2_dbl(E, A);
+  fp2_add(E, E, A);
+  fp2_sqr(F, E);
+  fp2_mul(Z3, p.Y, p.Z);
+  fp2_dbl(r.Z, Z3);
+  fp2_sub(t, F, D);
+  fp2_sub(r.X, t, D);
+  fp2_sub(t, D, r.X);
+  fp2_mul(t, E, t);
+  fp2_dbl(C, C);
+  fp2_dbl(C, C);
+  fp2_dbl(C, C);
+  fp2_sub(r.Y, t, C);
+}
+EDV_BN_NI void g2_add(g2& r, const g2& p, const g2& q) {
+  if (g2_isinf(p)) {
+    r = q;
+    return;
+  }
+  if (g2_isinf(q)) {
+    r = p;
+    return;
+  }
+  fp2 Z1Z1, Z2Z2, U1, U2, S1, S2, H, Rr, t;
+  fp2_sqr(Z1Z1, p.Z);
+  fp2_sqr(Z2Z2, q.Z);
+  fp2_mul(U1, p.X, Z2Z2);
+  fp2_mul(U2, q.X, Z1Z1);
+  fp2_mul(t, q.Z, Z2Z2);
+  fp2_mul(S1, p.Y, t);
+  fp2_mul(t, p.Z, Z1Z1);
+  fp2_mul(S2, q.Y, t);
+  fp2_sub(H, U2, U1);
+  fp2_sub(Rr, S2, S1);
+  if (fp2_iszero(H)) {
+    if (fp2_iszero(Rr)) {
+      g2_dbl(r, p);
+    } else {
+      g2_inf(r);
+    }
+    return;
+  }
+  fp2 HH, HHH, V, X3, Y3, Z3;
+  fp2_sqr(HH, H);
+  fp2_mul(HHH, HH, H);
+  fp2_mul(V, U1, HH);
+  fp2_sqr(X3, Rr);
+  fp2_sub(X3, X3, HHH);
+  fp2_sub(X3, X3, V);
+  fp2_sub(X3, X3, V);
+  fp2_sub(t, V, X3);
+  fp2_mul(Y3, Rr, t);
+  fp2_mul(t, S1, HHH);
+  fp2_sub(Y3, Y3, t);
+  fp2_mul(t, p.Z, q.Z);
+  fp2_mul(Z3, t, H);
+  r.X = X3;
+  r.Y = Y3;
+  r.Z = Z3;
+}
+EDV_BN_NI void g2_affine(fp2& x, fp2& y, const g2& p) {
+  fp2 zi, z2, z3;
+  fp2_inv(zi, p.Z);
+  fp2_sqr(z2, zi);
+  fp2_mul(z3, z2, zi);
+  fp2_mul(x, p.X, z2);
+  fp2_mul(y, p.Y, z3);
+}
+EDV_HD bool g2_on_curve_affine(const fp2& x, const fp2& y) {
+  fp2 l, r, b;
+  fp2_sqr(l, y);
+  fp2_sqr(r, x);
+  fp2_mul(r, r, x);
+  fp2_load(b, kB2);
+  fp2_add(r, r, b);
+  return fp2_eq(l, r);
+}
+EDV_BN_NI void g2_mul(g2& r, const g2& p, const uint32_t k[8]) {
+  g2 acc;
+  g2_inf(acc);
+  for (int w = 7; w >= 0; --w)
+    for (int bit = 31; bit >= 0; --bit) {
+      g2_dbl(acc, acc);
+      if ((k[w] >> bit) & 1u) g2_add(acc, acc, p);
+    }
+  r = acc;
+}
+
+// ------------------------------------------------------------------ encodings (oracle header)
+// G2: x.a | x.b | y.a | y.b, 32-byte big-endian each; off-curve or a
+// coordinate >= p decodes to infinity.
+EDV_BN_NI void g2_from_bytes(g2& r, const uint8_t* b) {
+  fp2 x, y;
+  const bool ok = fp_from_be(x.a, b) && fp_from_be(x.b, b + 32) && fp_from_be(y.a, b + 64) && fp_from_be(y.b, b + 96);
+  if (!ok || !g2_on_curve_affine(x, y)) {
+    g2_inf(r);
+    return;
+  }
+  r.X = x;
+  r.Y = y;
+  fp2_one(r.Z);
+}
+EDV_BN_NI void g2_to_bytes(uint8_t* b, const g2& p) {
+  if (g2_isinf(p)) {
+    for (int k = 0; k < 128; ++k) b[k] = 0;
+    return;
+  }
+  fp2 x, y;
+  g2_affine(x, y, p);
+  uint32_t w[8];
+  fp_to_plain(w, x.a);
+  words_to_be(b, w);
+  fp_to_plain(w, x.b);
+  words_to_be(b + 32, w);
+  fp_to_plain(w, y.a);
+  words_to_be(b + 64, w);
+  fp_to_plain(w, y.b);
+  words_to_be(b + 96, w);
+}
+// y = sqrt(v) = v^((p+1)/4) if v is a nonzero square (AMCL ECP::new_big's test)
+EDV_BN_NI bool fp_sqrt(fp& y, const fp& v) {
+  if (fp_iszero(v)) return false;
+  fp_pow(y, v, kSqrtExp, 8);
+  fp c;
+  fp_sqr(c, y);
+  return fp_eq(c, v);
+}
+// G1: 0x04 | x | y (| 63 bytes ignored); another first byte: y = sqrt(x^3 + 2)
+EDV_BN_NI void g1_from_bytes(g1& r, const uint8_t* b) {
+  fp x, y;
+  g1_inf(r);
+  if (!fp_from_be(x, b + 1)) return;
+  if (b[0] == 4) {
+    if (!fp_from_be(y, b + 33) || !g1_on_curve_affine(x, y)) return;
+  } else {
+    fp rhs, bb;
+    fp_sqr(rhs, x);
+    fp_mul(rhs, rhs, x);
+    fp_load(bb, kB1);
+    fp_add(rhs, rhs, bb);
+    if (!fp_sqrt(y, rhs)) return;
+  }
+  r.X = x;
+  r.Y = y;
+  fp_one(r.Z);
+}
+EDV_BN_NI void g1_to_bytes(uint8_t* b, const g1& p) {
+  for (int k = 0; k < 128; ++k) b[k] = 0;
+  if (g1_isinf(p)) return;
+  fp x, y;
+  g1_affine(x, y, p);
+  uint32_t w[8];
+  b[0] = 4;
+  fp_to_plain(w, x);
+  words_to_be(b + 1, w);
+  fp_to_plain(w, y);
+  words_to_be(b + 33, w);
+}
+
+// H(m) = indy-crypto Bls::_hash: SHA-256(m) as a big-endian integer h, then
+// x = h mod p, y = (x^3 + 2)^((p+1)/4) if x^3 + 2 is a nonzero square, else
+// h + 1 and again (AMCL ECP::new_big / PointG1::from_hash).
+EDV_BN_NI void g1_hash(g1& r, const uint8_t* msg, uint64_t mlen) {
+  uint32_t d[8];
+  sha256_msg(d, msg, mlen);  // digest bytes in order, little-endian words
+  uint8_t hb[32];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    hb[4 * k] = (uint8_t)d[k];
+    hb[4 * k + 1] = (uint8_t)(d[k] >> 8);
+    hb[4 * k + 2] = (uint8_t)(d[k] >> 16);
+    hb[4 * k + 3] = (uint8_t)(d[k] >> 24);
+  }
+  uint32_t h[8];
+  words_from_be(h, hb);
+  for (int tries = 0; tries < 1024; ++tries) {
+    uint32_t x[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = h[k];
+    while (fp_geq_p(x)) {  // h mod p (h < 2^256 < 5p)
+      fp t;
+      fp_reduce_once(t, x);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) x[k] = t.v[k];
+    }
+    fp X, rhs, bb, Y;
+    fp_from_plain(X, x);
+    fp_sqr(rhs, X);
+    fp_mul(rhs, rhs, X);
+    fp_load(bb, kB1);
+    fp_add(rhs, rhs, bb);
+    if (fp_sqrt(Y, rhs)) {
+      r.X = X;
+      r.Y = Y;
+      fp_one(r.Z);
+      return;
+    }
+    for (int k = 0; k < 8; ++k)  // h += 1
+      if (++h[k] != 0) break;
+  }
+  g1_inf(r);  // unreachable in practice (each try succeeds with probability 1/2)
+}
+
+// ------------------------------------------------------------------ pairing
+// Lines for the D-type twist, P = (xP, yP) affine in G1, T Jacobian on the
+// twist.  The line through psi(T) (tangent) or psi(T), psi(Q) evaluated at P
+// is yP - lambda' xP w + (lambda' x1 - y1) w^3, w^3 = v w; each is scaled by
+// an Fp2 factor the final exponentiation removes:
+//   doubling: 2YZ^3 yP - 3X^2 Z^2 xP w + (3X^3 - 2Y^2) v w
+//   addition: Z eps yP - theta xP w + (theta xQ - Z eps yQ) v w
+//             with theta = yQ Z^3 - Y, eps = xQ Z^2 - X.
+EDV_BN_NI void miller_dbl(fp12& f, g2& T, const fp& xP, const fp& yP) {
+  fp2 XX, YY, ZZ, u, l0, l1, l2, t;
+  fp2_sqr(XX, T.X);
+  fp2_sqr(YY, T.Y);
+  fp2_sqr(ZZ, T.Z);
+  fp2_mul(l0, T.Y, T.Z);  // 2 Y Z^3 yP
+  fp2_mul(l0, l0, ZZ);
+  fp2_dbl(l0, l0);
+  fp2_mul_fp(l0, l0, yP);
+  fp2_dbl(u, XX);  // 3 X^2
+  fp2_add(u, u, XX);
+  fp2_mul(l1, u, ZZ);  // -3 X^2 Z^2 xP
+  fp2_mul_fp(l1, l1, xP);
+  fp2_neg(l1, l1);
+  fp2_mul(l2, u, T.X);  // 3 X^3 - 2 Y^2
+  fp2_dbl(t, YY);
+  fp2_sub(l2, l2, t);
+  fp12_mul_line(f, l0, l1, l2);
+  g2_dbl(T, T);
+}
+EDV_BN_NI void miller_add(fp12& f, g2& T, const fp2& xQ, const fp2& yQ, const fp& xP, const fp& yP) {
+  fp2 ZZ, ZZZ, theta, eps, k, t, l0, l1, l2;
+  fp2_sqr(ZZ, T.Z);
+  fp2_mul(ZZZ, ZZ, T.Z);
+  fp2_mul(theta, yQ, ZZZ);  // theta = yQ Z^3 - Y
+  fp2_sub(theta, theta, T.Y);
+  fp2_mul(eps, xQ, ZZ);  // eps = xQ Z^2 - X
+  fp2_sub(eps, eps, T.X);
+  fp2_mul(k, T.Z, eps);
+  fp2_mul_fp(l0, k, yP);  // k yP
+  fp2_mul_fp(l1, theta, xP);  // -theta xP
+  fp2_neg(l1, l1);
+  fp2_mul(l2, theta, xQ);  // theta xQ - k yQ
+  fp2_mul(t, k, yQ);
+  fp2_sub(l2, l2, t);
+  fp12_mul_line(f, l0, l1, l2);
+  g2 Q;
+  Q.X = xQ;
+  Q.Y = yQ;
+  fp2_one(Q.Z);
+  g2_add(T, T, Q);
+}
+// pi on the twist: (conj(x) gamma_2, conj(y) gamma_3)
+EDV_HD void twist_frob(fp2& xo, fp2& yo, const fp2& x, const fp2& y) {
+  fp2 g, t;
+  fp2_conj(t, x);
+  fp2_load(g, kGamma2);
+  fp2_mul(xo, t, g);
+  fp2_conj(t, y);
+  fp2_load(g, kGamma3);
+  fp2_mul(yo, t, g);
+}
+
+// f *= (Miller function of Q at P) for the optimal ate pairing; P, Q affine.
+EDV_BN_NI void miller_loop_acc(fp12& f, const fp& xP, const fp& yP, const fp2& xQ, const fp2& yQ) {
+  g2 T;
+  T.X = xQ;
+  T.Y = yQ;
+  fp2_one(T.Z);
+  fp12 g;
+  fp12_one(g);
+  // |6x + 2| = 2^64 + kAteLoop: bits 63..0 after the leading one
+  for (int bit = kAteLoopBits - 2; bit >= 0; --bit) {
+    fp12_sqr(g, g);
+    miller_dbl(g, T, xP, yP);
+    if ((kAteLoop >> bit) & 1ull) miller_add(g, T, xQ, yQ, xP, yP);
+  }
+  fp12_conj(g, g);  // x < 0
+  fp2_neg(T.Y, T.Y);
+  fp2 x1, y1, x2, y2;
+  twist_frob(x1, y1, xQ, yQ);
+  twist_frob(x2, y2, x1, y1);
+  fp2_neg(y2, y2);
+  miller_add(g, T, x1, y1, xP, yP);
+  miller_add(g, T, x2, y2, xP, yP);
+  fp12_mul(f, f, g);
+}
+
+EDV_BN_NI void final_exp(fp12& r, const fp12& f) {
+  fp12 t, u;
+  fp12_conj(t, f);  // f^(p^6 - 1)
+  fp12_inv(u, f);
+  fp12_mul(t, t, u);
+  fp12_frob(u, t);  // ^(p^2 + 1)
+  fp12_frob(u, u);
+  fp12_mul(t, u, t);
+  fp12 acc;
+  fp12_one(acc);
+  for (int bit = kHardExpBits - 1; bit >= 0; --bit) {  // ^((p^4 - p^2 + 1) / r)
+    fp12_sqr(acc, acc);
+    if ((kHardExp[bit >> 5] >> (bit & 31)) & 1u) fp12_mul(acc, acc, t);
+  }
+  r = acc;
+}
+
+// e(sig, gen) == e(H, vk)  <=>  FE(ML(sig, gen) * ML(-H, vk)) == 1;
+// an infinite point contributes 1 (its Miller function is constant).
+EDV_BN_NI bool bls_check(const g1& sig, const g1& H, const g2& vk, const g2& gen) {
+  fp12 f;
+  fp12_one(f);
+  if (!g1_isinf(sig) && !g2_isinf(gen)) {
+    fp x, y;
+    fp2 qx, qy;
+    g1_affine(x, y, sig);
+    g2_affine(qx, qy, gen);
+    miller_loop_acc(f, x, y, qx, qy);
+  }
+  if (!g1_isinf(H) && !g2_isinf(vk)) {
+    fp x, y;
+    fp2 qx, qy;
+    g1_affine(x, y, H);
+    fp_neg(y, y);
+    g2_affine(qx, qy, vk);
+    miller_loop_acc(f, x, y, qx, qy);
+  }
+  fp12 e;
+  final_exp(e, f);
+  return fp12_isone(e);
+}
+
+}  // namespace bn
+}  // namespace edv

@@ -33,6 +33,7 @@
 #include <rocprim/iterator/counting_iterator.hpp>
 
 #include "../../include/edverify.h"
+#include "edv_internal.h"
 #include "batch_encode.h"
 #include "comb.h"
 #include "sha256.h"
@@ -1446,6 +1447,24 @@ static int host_verify(edv_ctx* ctx, bool keyed, const uint8_t* sig64, const uin
   if (n & 7) accept_bits[n / 8] &= (uint8_t)((1u << (n & 7)) - 1);
   return 0;
 }
+
+namespace edv_internal {
+int begin(edv_ctx* ctx, hipStream_t* stream) {
+  int r = set_device(ctx);
+  if (r) return r;
+  *stream = ctx->stream;
+  return 0;
+}
+int set_err(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+}  // namespace edv_internal
 
 extern "C" {
 

@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "batch_encode.h"
+#include "bn254.h"
 #include "comb.h"
 #include "sha256.h"
 #include "verify_core.h"
@@ -335,6 +336,73 @@ int edv_host_verify_batch_comb(const uint8_t* sig64, const uint8_t* pk32, const 
     encode_batch<16>(a);
   }
   return 0;
+}
+
+}  // extern "C"
+
+// ---- BLS (bn254.h) on the CPU, for tests/test_bls.py against the oracle.
+extern "C" {
+
+// H(m) as 128 G1 bytes
+void edv_host_bls_hash(const uint8_t* msg, uint64_t mlen, uint8_t out128[128]) {
+  edv::bn::g1 h;
+  edv::bn::g1_hash(h, msg, mlen);
+  edv::bn::g1_to_bytes(out128, h);
+}
+// [sk]H(m) (sk 32 big-endian bytes, < r)
+void edv_host_bls_sign(const uint8_t sk32[32], const uint8_t* msg, uint64_t mlen, uint8_t out128[128]) {
+  uint32_t k[8];
+  edv::bn::words_from_be(k, sk32);
+  edv::bn::g1 h, s;
+  edv::bn::g1_hash(h, msg, mlen);
+  edv::bn::g1_mul(s, h, k);
+  edv::bn::g1_to_bytes(out128, s);
+}
+void edv_host_bls_keygen(const uint8_t sk32[32], const uint8_t gen128[128], uint8_t out128[128]) {
+  uint32_t k[8];
+  edv::bn::words_from_be(k, sk32);
+  edv::bn::g2 g, v;
+  edv::bn::g2_from_bytes(g, gen128);
+  edv::bn::g2_mul(v, g, k);
+  edv::bn::g2_to_bytes(out128, v);
+}
+// the reduced pairing e(P, Q) as 12 Fp values (tower order c0.c0.a, c0.c0.b,
+// c0.c1.a, ..., c1.c2.b), 32 big-endian bytes each
+int edv_host_bls_pairing(const uint8_t p128[128], const uint8_t q128[128], uint8_t out[384]) {
+  using namespace edv::bn;
+  g1 P;
+  g2 Q;
+  g1_from_bytes(P, p128);
+  g2_from_bytes(Q, q128);
+  if (g1_isinf(P) || g2_isinf(Q)) return -1;
+  fp x, y;
+  fp2 qx, qy;
+  g1_affine(x, y, P);
+  g2_affine(qx, qy, Q);
+  fp12 f, e;
+  fp12_one(f);
+  miller_loop_acc(f, x, y, qx, qy);
+  final_exp(e, f);
+  const fp* c[12] = {&e.c0.c0.a, &e.c0.c0.b, &e.c0.c1.a, &e.c0.c1.b, &e.c0.c2.a, &e.c0.c2.b,
+                     &e.c1.c0.a, &e.c1.c0.b, &e.c1.c1.a, &e.c1.c1.b, &e.c1.c2.a, &e.c1.c2.b};
+  for (int k = 0; k < 12; ++k) {
+    uint32_t w[8];
+    fp_to_plain(w, *c[k]);
+    words_to_be(out + 32 * k, w);
+  }
+  return 0;
+}
+// Bls.verify over wire bytes: 1 accept, 0 reject
+int edv_host_bls_verify(const uint8_t sig128[128], const uint8_t* msg, uint64_t mlen, const uint8_t vk128[128],
+                        const uint8_t gen128[128]) {
+  using namespace edv::bn;
+  g1 s, h;
+  g2 v, g;
+  g1_from_bytes(s, sig128);
+  g1_hash(h, msg, mlen);
+  g2_from_bytes(v, vk128);
+  g2_from_bytes(g, gen128);
+  return bls_check(s, h, v, g) ? 1 : 0;
 }
 
 }  // extern "C"

@@ -54,6 +54,10 @@ SIGNATURES = {
     "edv_tally_device": (_I, [_P, _P, _P, _P, _P, _P, _U64, _U32, _U32, _P, _P, _P, _P]),
     "edv_tally_finish_device": (_I, [_P, _P, _U32, _U32, _P, _P, _P]),
     "edv_tally": (_I, [_P, _P, _P, _P, _P, _P, _U64, _U32, _U32, _P, _P]),
+    "edv_bls_verify_batch": (_I, [_P, _P, _P, _P, _P, _P, _P, _U64, _P]),
+    "edv_bls_aggregate": (_I, [_P, _P, _P, _U64, _P]),
+    "edv_bls_sign_batch": (_I, [_P, _P, _P, _P, _U64, _P]),
+    "edv_bls_keygen_batch": (_I, [_P, _P, _P, _U64, _P]),
 }
 
 

@@ -205,6 +205,65 @@ class EdVerifyEngine:
         hashed in place)."""
         check(self._lib.edv_set_unit_arena(self._ctx, int(nbytes)))
 
+    # ------------------------------------------------------------------ BLS
+    # BN254 BLS (indy-crypto's Bls, bls_crypto_indy_crypto.py:59-90); G1 / G2
+    # points as the 128-byte wire forms of edverify.h.
+    def bls_verify_batch(self, sig128, msgs, msg_off, vk128, gen128, vk_off=None):
+        """Bool array: e(sig_i, gen) == e(H(m_i), vk_i); with vk_off, vk_i is the
+        sum of vk128[vk_off[i]:vk_off[i+1]] (verify_multi_sig)."""
+        sig128 = _u8(sig128, 128)
+        n = sig128.shape[0]
+        vk128 = _u8(vk128, 128)
+        gen128 = _u8(gen128)
+        msgs = _u8(msgs)
+        msg_off = np.ascontiguousarray(msg_off, dtype=np.uint64)
+        if msg_off.shape[0] != n + 1 or gen128.size != 128:
+            raise ValueError("msg_off needs n + 1 entries and gen 128 bytes")
+        if vk_off is not None:
+            vk_off = np.ascontiguousarray(vk_off, dtype=np.uint64)
+            if vk_off.shape[0] != n + 1 or int(vk_off[-1]) > vk128.shape[0]:
+                raise ValueError("vk_off needs n + 1 entries within vk128")
+        elif vk128.shape[0] != n:
+            raise ValueError("one verkey per item without vk_off")
+        bits = np.zeros((n + 7) // 8, dtype=np.uint8)
+        if n:
+            check(self._lib.edv_bls_verify_batch(self._ctx, _ptr(sig128), _ptr(msgs) if msgs.size else None,
+                                                 _ptr(msg_off), _ptr(vk128), _ptr(vk_off), _ptr(gen128), n,
+                                                 _ptr(bits)))
+        return unpack_bits(bits, n)
+
+    def bls_aggregate(self, sig128, sig_off):
+        """out[i] = sum of sig128[sig_off[i]:sig_off[i+1]] (create_multi_sig)."""
+        sig128 = _u8(sig128, 128)
+        sig_off = np.ascontiguousarray(sig_off, dtype=np.uint64)
+        m = sig_off.shape[0] - 1
+        out = np.zeros((m, 128), dtype=np.uint8)
+        if m > 0:
+            check(self._lib.edv_bls_aggregate(self._ctx, _ptr(sig128), _ptr(sig_off), m, _ptr(out)))
+        return out
+
+    def bls_sign_batch(self, sk32, msgs, msg_off):
+        """[sk_i] H(m_i) as 128-byte G1 (sk: 32-byte big-endian scalars < r)."""
+        sk32 = _u8(sk32, 32)
+        n = sk32.shape[0]
+        msgs = _u8(msgs)
+        msg_off = np.ascontiguousarray(msg_off, dtype=np.uint64)
+        out = np.zeros((n, 128), dtype=np.uint8)
+        if n:
+            check(self._lib.edv_bls_sign_batch(self._ctx, _ptr(sk32), _ptr(msgs) if msgs.size else None,
+                                               _ptr(msg_off), n, _ptr(out)))
+        return out
+
+    def bls_keygen_batch(self, sk32, gen128):
+        """[sk_i] gen as 128-byte G2 verkeys."""
+        sk32 = _u8(sk32, 32)
+        gen128 = _u8(gen128)
+        n = sk32.shape[0]
+        out = np.zeros((n, 128), dtype=np.uint8)
+        if n:
+            check(self._lib.edv_bls_keygen_batch(self._ctx, _ptr(sk32), _ptr(gen128), n, _ptr(out)))
+        return out
+
     # ------------------------------------------------------------ key tables
     def keys_set_window(self, w):
         """Comb window of the key tables: 4 (64 KiB/key, 64 additions per

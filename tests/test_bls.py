@@ -1,0 +1,109 @@
+"""BLS multi-signatures on the CPU: the oracle's pinning, the
+device arithmetic (bn254.h compiled into libedv_hostcheck.so) against the
+oracle and the committed vectors, and the drop-in's string handling.
+Reference: crypto/bls/indy_crypto/bls_crypto_indy_crypto.py (indy-crypto
+0.1.6, absent here; parity beyond the generator literal is unpinned)."""
+import ctypes
+import json
+import os
+import random
+import sys
+
+import pytest
+
+from conftest import GOLDEN, ROOT
+
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import bls_bn254_oracle as o  # noqa: E402
+
+V = json.load(open(os.path.join(GOLDEN, "bls_vectors.json")))
+
+
+def test_generator_literal_pins_curve_and_twist():
+    """The reference's only BLS literal (bls_crypto_indy_crypto.py:14-15)
+    decodes to a point of order r on y^2 = x^3 + 2/(1+i) over AMCL BN254's
+    Fp2 -- and on no other candidate twist / coordinate order."""
+    raw = o.b58decode(o.G2_GEN_B58)
+    assert len(raw) == 128
+    g = o.g2_from_bytes(raw)
+    assert g is not None and o.g2_mul(g, o.R) is None
+    assert o.g2_to_bytes(g) == raw
+    v = [int.from_bytes(raw[32 * k:32 * k + 32], "big") for k in range(4)]
+    others = [o.F2(2) * o.F2(1, 1), o.F2(2) * o.F2(1, -1).inv(), o.F2(0, 2), o.F2(2) * o.F2(0, 1).inv()]
+    for x, y in (((v[0], v[1]), (v[2], v[3])), ((v[1], v[0]), (v[3], v[2]))):
+        X, Y = o.F2(*x), o.F2(*y)
+        for b in others:
+            assert not (Y * Y == X * X * X + b)
+    assert V["generator"] == raw.hex()
+
+
+def test_oracle_pairing_is_bilinear():
+    rng = random.Random(11)
+    g = o.generator()
+    h = o.hash_to_g1(b"bilinear")
+    e = o.pairing(h, g)
+    assert not e.isone() and (e ** o.R).isone()
+    a, b = rng.randrange(1, o.R), rng.randrange(1, o.R)
+    assert o.pairing(o.g1_mul(h, a), o.g2_mul(g, b)) == e ** (a * b % o.R)
+
+
+def _hc_bls(hostcheck):
+    hostcheck.edv_host_bls_verify.restype = ctypes.c_int
+    return hostcheck
+
+
+def test_device_arithmetic_matches_vectors(hostcheck):
+    """bn254.h on the CPU: H(m), [sk]H(m), [sk]g and the verdict of every
+    committed case equal the oracle's vectors."""
+    hc = _hc_bls(hostcheck)
+    gen = bytes.fromhex(V["generator"])
+    msgs = [bytes.fromhex(m) for m in V["messages"]]
+    for h in V["hashes"]:
+        out = ctypes.create_string_buffer(128)
+        m = msgs[h["msg"]]
+        hc.edv_host_bls_hash(m, ctypes.c_uint64(len(m)), out)
+        assert out.raw.hex() == h["h"]
+    for k in V["keys"]:
+        out = ctypes.create_string_buffer(128)
+        hc.edv_host_bls_keygen(bytes.fromhex(k["sk"]), gen, out)
+        assert out.raw.hex() == k["vk"]
+    for s in V["signatures"][::3]:
+        out = ctypes.create_string_buffer(128)
+        m = msgs[s["msg"]]
+        hc.edv_host_bls_sign(bytes.fromhex(V["keys"][s["key"]]["sk"]), m, ctypes.c_uint64(len(m)), out)
+        assert out.raw.hex() == s["sig"]
+    for c in V["cases"]:
+        if len(c["vks"]) != 1:
+            continue
+        m = msgs[c["msg"]]
+        got = hc.edv_host_bls_verify(bytes.fromhex(c["sig"]), m, ctypes.c_uint64(len(m)),
+                                     bytes.fromhex(c["vks"][0]), gen)
+        assert got == int(c["expect"]), c["name"]
+
+
+def test_device_pairing_value_bit_exact(hostcheck):
+    """The reduced pairing computed by bn254.h (tower Fp12, Jacobian twist
+    lines) equals the oracle's (Fp[w]/(w^12 - 2w^6 + 2), affine) exactly."""
+    rng = random.Random(12)
+    g = o.generator()
+    for t in range(2):
+        p1 = o.g1_mul(o.hash_to_g1(b"pair %d" % t), rng.randrange(1, o.R))
+        q2 = o.g2_mul(g, rng.randrange(1, o.R))
+        out = ctypes.create_string_buffer(384)
+        assert hostcheck.edv_host_bls_pairing(o.g1_to_bytes(p1), o.g2_to_bytes(q2), out) == 0
+        got = [int.from_bytes(out.raw[32 * k:32 * k + 32], "big") for k in range(12)]
+        assert got == o.f12_to_tower(o.pairing(p1, q2))
+
+
+def test_dropin_string_handling():
+    """IndyCryptoBlsUtils.bls_from_str (bls_crypto_indy_crypto.py:28-40):
+    undecodable base58 or a length other than 32 / 128 -> None."""
+    from plenum_amd.bls import GpuBlsUtils, BlsGroupParamsLoaderGpu
+    assert GpuBlsUtils.bls_from_str("0OIl") is None  # not base58
+    assert GpuBlsUtils.bls_from_str(o.b58encode(b"\x01" * 10)) is None
+    assert GpuBlsUtils.bls_from_str(o.b58encode(b"\x01" * 500)) is None
+    assert len(GpuBlsUtils.bls_from_str(o.b58encode(b"\x01" * 128))) == 128
+    assert GpuBlsUtils.prepare_seed("abc") == b"abc" + b"0" * 45
+    assert GpuBlsUtils.prepare_seed(b"x" * 48) == b"x" * 48
+    params = BlsGroupParamsLoaderGpu().load_group_params()
+    assert params.group_name == "generator" and o.b58decode(params.g).hex() == V["generator"]

@@ -1,0 +1,34 @@
+"""Throughput probe of the GPU BLS verify (edv_bls_verify_batch): n signed
+items (distinct keys and messages), one call, wall time incl. H2D."""
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "indy-plenum_amd"))
+from plenum_amd import EdVerifyEngine, pack_messages  # noqa: E402
+from plenum_amd.bls import GENERATOR, ORDER  # noqa: E402
+from plenum_amd.base58 import b58decode  # noqa: E402
+
+eng = EdVerifyEngine(0)
+gen = np.frombuffer(b58decode(GENERATOR), np.uint8)
+rng = np.random.default_rng(1)
+for n in (64, 1024, 16384, 65536):
+    sks = np.frombuffer(b"".join((int.from_bytes(rng.bytes(32), "big") % ORDER).to_bytes(32, "big")
+                                 for _ in range(n)), np.uint8).reshape(n, 32)
+    t = time.time()
+    vks = eng.bls_keygen_batch(sks, gen)
+    tk = time.time() - t
+    msgs = [rng.bytes(96) for _ in range(n)]
+    buf, off = pack_messages(msgs)
+    t = time.time()
+    sigs = eng.bls_sign_batch(sks, buf, off)
+    ts = time.time() - t
+    t = time.time()
+    ok = eng.bls_verify_batch(sigs, buf, off, vks, gen)
+    tv = time.time() - t
+    print("n=%6d keygen %.3f s  sign %.3f s  verify %.3f s = %.0f verifies/s  all_ok=%s" % (
+        n, tk, ts, tv, n / tv, bool(ok.all())), flush=True)
+    if tv > 60:
+        break
