@@ -210,3 +210,41 @@ class BlsCryptoSignerGpu(BlsCryptoSigner):
         buf, off = pack_messages([msg])
         sig = _engine(self._engine).bls_sign_batch(np.frombuffer(self._sk_bytes, np.uint8).reshape(1, 32), buf, off)
         return GpuBlsUtils.bls_to_str(sig[0].tobytes())
+
+
+try:
+    from crypto.bls.bls_factory import BlsFactoryCrypto as _FactoryBase
+except Exception:  # standalone: the same template methods, no base class
+    _FactoryBase = object
+
+
+class BlsFactoryGpu(_FactoryBase):
+    """BlsFactoryIndyCrypto (plenum/bls/bls_crypto_factory.py:31-52) with the
+    GPU classes: a node built with this factory (create_default_bls_crypto_factory's
+    replacement) signs and verifies COMMIT BLS signatures here."""
+
+    def __init__(self, basedir=None, node_name=None, engine=None):
+        self._basedir = basedir
+        self._node_name = node_name
+        self._engine = engine
+
+    def _create_group_params_loader(self):
+        return BlsGroupParamsLoaderGpu()
+
+    def _get_bls_crypto_signer_class(self):
+        return BlsCryptoSignerGpu
+
+    def _create_bls_crypto_signer(self, sk, pk, group_params):
+        return BlsCryptoSignerGpu(sk=sk, pk=pk, params=group_params, engine=self._engine)
+
+    def _create_bls_crypto_verifier(self, group_params):
+        return BlsCryptoVerifierGpu(group_params, engine=self._engine)
+
+    def _create_key_manager(self, group_params):
+        from plenum.bls.bls_key_manager_file import BlsKeyManagerFile
+        assert self._basedir
+        assert self._node_name
+        return BlsKeyManagerFile(self._basedir, self._node_name)
+
+    def create_bls_crypto_verifier(self):
+        return self._create_bls_crypto_verifier(self._create_group_params_loader().load_group_params())

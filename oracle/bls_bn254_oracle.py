@@ -31,8 +31,10 @@ tests generate keys and signatures at run time).
 
 Arithmetic here is deliberately different from the device code (bn254.h):
 Fp12 is Fp[w]/(w^12 - 2 w^6 + 2) (w^6 = 1 + i) with schoolbook polynomial
-products, points are affine, the Miller loop runs on the untwisted point
-in E(Fp12) and the final exponentiation is one plain power.
+products, points are affine, every line is evaluated in Fp12 from the
+affine twist slope (psi(x', y') = (x' w^2, y' w^3)) without scaling, and the
+final exponentiation is one plain power; the device's reduced pairing must
+equal this one bit for bit (tests/test_bls.py).
 Only tests/ and bench.py's checker may import this."""
 import hashlib
 

@@ -81,3 +81,60 @@ class OracleEngine:
         return np.array([self.lib.oracle_verify_detached(sig64[i].tobytes(), msgs[off[i]:off[i + 1]],
                                                          off[i + 1] - off[i], pk32[i].tobytes()) == 0
                          for i in range(len(off) - 1)], dtype=bool)
+
+
+class OracleBlsEngine:
+    """The BLS half of EdVerifyEngine (bls_verify_batch, bls_aggregate,
+    bls_sign_batch, bls_keygen_batch) answered by oracle/bls_bn254_oracle.py
+    (pure Python, ~0.5 s per check).  `calls` counts launches."""
+
+    def __init__(self):
+        import sys
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import bls_bn254_oracle
+        self.o = bls_bn254_oracle
+        self.calls = 0
+
+    def bls_verify_batch(self, sig128, msgs, msg_off, vk128, gen128, vk_off=None):
+        o = self.o
+        self.calls += 1
+        sig128 = np.asarray(sig128, np.uint8).reshape(-1, 128)
+        vk128 = np.asarray(vk128, np.uint8).reshape(-1, 128)
+        msgs = np.asarray(msgs, np.uint8)
+        gen = o.g2_from_bytes(np.asarray(gen128, np.uint8).tobytes())
+        out = []
+        for i in range(sig128.shape[0]):
+            k0, k1 = (int(vk_off[i]), int(vk_off[i + 1])) if vk_off is not None else (i, i + 1)
+            acc = None
+            for k in range(k0, k1):
+                acc = o.g2_add(acc, o.g2_from_bytes(vk128[k].tobytes()))
+            m = msgs[int(msg_off[i]):int(msg_off[i + 1])].tobytes()
+            out.append(o.verify(o.g1_from_bytes(sig128[i].tobytes()), m, acc, gen))
+        return np.asarray(out, bool)
+
+    def bls_aggregate(self, sig128, sig_off):
+        o = self.o
+        self.calls += 1
+        sig128 = np.asarray(sig128, np.uint8).reshape(-1, 128)
+        out = []
+        for i in range(len(sig_off) - 1):
+            pts = [o.g1_from_bytes(sig128[k].tobytes()) for k in range(int(sig_off[i]), int(sig_off[i + 1]))]
+            out.append(np.frombuffer(o.g1_to_bytes(o.aggregate(pts)), np.uint8))
+        return np.asarray(out, np.uint8).reshape(-1, 128)
+
+    def bls_sign_batch(self, sk32, msgs, msg_off):
+        o = self.o
+        self.calls += 1
+        sk32 = np.asarray(sk32, np.uint8).reshape(-1, 32)
+        msgs = np.asarray(msgs, np.uint8)
+        return np.asarray([np.frombuffer(o.g1_to_bytes(o.sign(msgs[int(msg_off[i]):int(msg_off[i + 1])].tobytes(),
+                                                               int.from_bytes(sk32[i].tobytes(), "big"))), np.uint8)
+                           for i in range(sk32.shape[0])], np.uint8)
+
+    def bls_keygen_batch(self, sk32, gen128):
+        o = self.o
+        self.calls += 1
+        sk32 = np.asarray(sk32, np.uint8).reshape(-1, 32)
+        gen = o.g2_from_bytes(np.asarray(gen128, np.uint8).tobytes())
+        return np.asarray([np.frombuffer(o.g2_to_bytes(o.keygen(int.from_bytes(sk32[i].tobytes(), "big"), gen)),
+                                         np.uint8) for i in range(sk32.shape[0])], np.uint8)

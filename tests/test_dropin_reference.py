@@ -33,3 +33,20 @@ def test_committed_record():
     assert rec["ok"] and rec["matched"] == rec["cases"] == 50
     assert rec["libsodium_crypto_sign_open_calls"] == 0
     assert rec["forged_propagate"].startswith("SuspiciousNode")
+
+
+@pytest.mark.skipif(not (os.path.exists(PY39) and os.path.isdir("/root/reference/crypto")),
+                    reason="needs the reference tree and Python 3.9 (container only)")
+def test_bls_classes_over_reference_abcs():
+    """plenum_amd.bls against the reference's crypto.bls.bls_crypto ABCs and
+    the reference's own BLS test scenarios (tests/golden/check_bls_dropin_ref.py)."""
+    out = subprocess.run([PY39, os.path.join(GOLDEN, "check_bls_dropin_ref.py")], cwd=ROOT, capture_output=True,
+                         text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    got = json.loads(out.stdout.strip().splitlines()[-1])
+    assert got["ok"] and all(got["checks"].values()) and got["engine_calls"] > 0
+
+
+def test_bls_committed_record():
+    rec = json.load(open(os.path.join(GOLDEN, "bls_dropin_ref_check.json")))
+    assert rec["ok"] and len(rec["checks"]) == 8
