@@ -17,7 +17,8 @@
 //         final exponentiation removes them), conjugation for x < 0, the
 //         lines through pi(Q) and -pi^2(Q); final exponentiation
 //         (p^6 - 1)(p^2 + 1) by conjugation, inversion and Frobenius, then
-//         the hard part (p^4 - p^2 + 1)/r by square-and-multiply.
+//         the hard part (p^4 - p^2 + 1)/r through its exact BN decomposition
+//         in x (three powers by x and Frobenius maps).
 #pragma once
 #include "bn254_constants.h"
 #include "fe25519.h"  // EDV_HD
@@ -914,6 +915,32 @@ EDV_BN_NI void miller_loop_acc(fp12& f, const fp& xP, const fp& yP, const fp2& x
   fp12_mul(f, f, g);
 }
 
+// f^x for f in the cyclotomic subgroup (x = -|x| < 0: the conjugate of
+// f^|x|, |x| = 2^62 + 2^55 + 1)
+EDV_BN_NI void fp12_pow_x(fp12& r, const fp12& f) {
+  fp12 acc = f;
+  for (int bit = 61; bit >= 0; --bit) {
+    fp12_sqr(acc, acc);
+    if (bit == 55 || bit == 0) fp12_mul(acc, acc, f);
+  }
+  fp12_conj(r, acc);
+}
+// f^k for a small constant k >= 1
+EDV_BN_NI void fp12_pow_small(fp12& r, const fp12& f, uint32_t k) {
+  fp12 acc = f;
+  int top = 31;
+  while (!((k >> top) & 1u)) --top;
+  for (int bit = top - 1; bit >= 0; --bit) {
+    fp12_sqr(acc, acc);
+    if ((k >> bit) & 1u) fp12_mul(acc, acc, f);
+  }
+  r = acc;
+}
+// f^((p^12 - 1) / r): the easy part (p^6 - 1)(p^2 + 1) by conjugation,
+// inversion and Frobenius; the hard part (p^4 - p^2 + 1) / r =
+// l0 + l1 p + l2 p^2 + p^3 exactly, with l0 = -36x^3 - 30x^2 - 18x - 2,
+// l1 = -36x^3 - 18x^2 - 12x + 1, l2 = 6x^2 + 1 (BN), from t^x, t^(x^2),
+// t^(x^3) -- 186 squarings instead of the 760 of a plain power.
 EDV_BN_NI void final_exp(fp12& r, const fp12& f) {
   fp12 t, u;
   fp12_conj(t, f);  // f^(p^6 - 1)
@@ -922,13 +949,40 @@ EDV_BN_NI void final_exp(fp12& r, const fp12& f) {
   fp12_frob(u, t);  // ^(p^2 + 1)
   fp12_frob(u, u);
   fp12_mul(t, u, t);
-  fp12 acc;
-  fp12_one(acc);
-  for (int bit = kHardExpBits - 1; bit >= 0; --bit) {  // ^((p^4 - p^2 + 1) / r)
-    fp12_sqr(acc, acc);
-    if ((kHardExp[bit >> 5] >> (bit & 31)) & 1u) fp12_mul(acc, acc, t);
-  }
-  r = acc;
+  fp12 a, b, c, c36, y, z;
+  fp12_pow_x(a, t);  // t^x
+  fp12_pow_x(b, a);  // t^(x^2)
+  fp12_pow_x(c, b);  // t^(x^3)
+  fp12_pow_small(c36, c, 36);
+  // t^l0 = conj(c^36 b^30 a^18 t^2)
+  fp12_pow_small(y, b, 30);
+  fp12_mul(y, y, c36);
+  fp12_pow_small(z, a, 18);
+  fp12_mul(y, y, z);
+  fp12_sqr(z, t);
+  fp12_mul(y, y, z);
+  fp12 res;
+  fp12_conj(res, y);
+  // (t^l1)^p, t^l1 = conj(c^36 b^18 a^12) t
+  fp12_pow_small(y, b, 18);
+  fp12_mul(y, y, c36);
+  fp12_pow_small(z, a, 12);
+  fp12_mul(y, y, z);
+  fp12_conj(y, y);
+  fp12_mul(y, y, t);
+  fp12_frob(y, y);
+  fp12_mul(res, res, y);
+  // (t^l2)^(p^2), t^l2 = b^6 t
+  fp12_pow_small(y, b, 6);
+  fp12_mul(y, y, t);
+  fp12_frob(y, y);
+  fp12_frob(y, y);
+  fp12_mul(res, res, y);
+  // t^(p^3)
+  fp12_frob(y, t);
+  fp12_frob(y, y);
+  fp12_frob(y, y);
+  fp12_mul(r, res, y);
 }
 
 // e(sig, gen) == e(H, vk)  <=>  FE(ML(sig, gen) * ML(-H, vk)) == 1;
