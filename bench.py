@@ -258,7 +258,11 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(args.dist_backend)
+    t_create = time.perf_counter()
     eng = EdVerifyEngine(local)
+    create_s = time.perf_counter() - t_create  # includes the base comb's build (kBaseW)
+    if hasattr(eng._lib, "edv_base_window"):
+        RL.set_base_window(eng._lib.edv_base_window())
     eng.set_pipeline(args.pipeline)
     n = args.n if not (args.config == "c4" and args.n == 1_000_000) else 2_000_000
 
@@ -427,6 +431,33 @@ def main():
         elapsed = float(e.item())
 
     tally_result = tally_check() if tally_check else None
+
+    # the exchange step alone (RCCL cost reported apart from the
+    # verify): the bitmask all-gather (+ the ballot all-reduce MAX on configs[4])
+    # on the same buffers, timed with events on the compute stream, max over ranks
+    collective = None
+    if world > 1:
+        reps = 20
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        dist.barrier()
+        ev0.record(stream)
+        for _ in range(reps):
+            dist.all_gather(gathered, d_words)
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        ag = torch.tensor([ev0.elapsed_time(ev1) / reps], dtype=torch.float64, device=dev)
+        dist.all_reduce(ag, op=dist.ReduceOp.MAX)
+        collective = {"all_gather_bitmask_ms": float(ag.item()), "bitmask_bytes_per_rank": int(d_words.numel() * 8)}
+        if args.config == "c4":
+            dist.barrier()
+            ev0.record(stream)
+            for _ in range(reps):
+                dist.all_reduce(d_ballot, op=dist.ReduceOp.MAX)
+            ev1.record(stream)
+            torch.cuda.synchronize()
+            ar = torch.tensor([ev0.elapsed_time(ev1) / reps], dtype=torch.float64, device=dev)
+            dist.all_reduce(ar, op=dist.ReduceOp.MAX)
+            collective.update({"all_reduce_max_ballots_ms": float(ar.item()), "ballot_bytes": int(d_ballot.numel())})
 
     # ---- parity of the timed output against the construction
     words = d_words.cpu().numpy().view(np.uint64)
@@ -608,6 +639,7 @@ def main():
                                  "%d-request chunk" % (launches, n_chunk)},
             "length_buckets": "packed" if args.length_buckets == "packed" else bool(buckets),
             "key_window": args.key_window, "key_table_build_ms": key_build_ms, "keys": int(reg_pks.shape[0]),
+            "base_window": RL.BASE_W, "engine_create_s": create_s,
             "value_incl_key_build_one_step": (n * world / (ms_per_step * 1e-3 + key_build_ms * 1e-3)
                                               if args.path == "keyed" else None),
             "ref10_equivalent_frac": (n * RL.MAD_PER_VERIFY / (ms_per_step * 1e-3)) / RL.PEAK_MAD_PER_S,
@@ -617,6 +649,7 @@ def main():
             "cpu_baseline": cpu,
             "parity": {"mismatches_vs_construction": mismatches, "accepted": int(got.sum()), "expected": int(expect.sum())},
             "tally": tally_result,
+            "collective": collective,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

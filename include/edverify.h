@@ -52,6 +52,10 @@ typedef struct edv_ctx edv_ctx;
 
 /* Library/version info. */
 const char *edv_version(void);
+/* Window of the base-point comb table built by edv_create (rows =
+ * ceil(254 / w) mixed additions per [S]B): the bench's roofline prices the
+ * comb kernel's work from it. */
+int edv_base_window(void);
 const char *edv_last_error(void);
 int edv_device_count(void);
 

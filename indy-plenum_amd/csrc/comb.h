@@ -16,7 +16,7 @@
 //       W = 10: 26 rows x 512 entries x 128 B = 1.6 MiB per key, 26 additions
 //       W = 13: 20 rows x 4096 entries x 128 B = 10 MiB per key, 20 additions
 //   B = the base point, one table per context (kBaseW, verify_core.h):
-//       W = 22: 12 rows x 2^21 entries x 128 B = 3 GiB (a 256 MiB slab per row).
+//       W = 24: 11 rows x 2^23 entries x 128 B = 11 GiB (a 1 GiB slab per row).
 // Entries are 32 u32 words (30 limbs + 2 pad) so one entry is 8 dwordx4 loads.
 #pragma once
 #include "ge25519.h"
@@ -27,11 +27,11 @@ constexpr int kEntryWords = 32;
 
 template <int W>
 struct Window {
-  static_assert(W >= 4 && W <= 22, "comb window width 4..22");
+  static_assert(W >= 4 && W <= 26, "comb window width 4..26");
   // x < L < 2^253 plus the digit bias must stay below 2^(W * kRows): W * kRows >= 254
   static constexpr int kRows = (254 + W - 1) / W;
   static constexpr int kEntries = 1 << (W - 1);
-  static constexpr int kTableWords = kRows * kEntries * kEntryWords;
+  static constexpr uint64_t kTableWords = (uint64_t)kRows * kEntries * kEntryWords;
   // word k of bias = sum_{i < kRows} 2^(W-1) * 2^(W*i)   (9 words: W*kRows may exceed 256)
   static constexpr uint32_t bias_word(int k) {
     uint32_t w = 0;

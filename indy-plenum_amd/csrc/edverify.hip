@@ -525,7 +525,7 @@ __global__ __launch_bounds__(kBlock) void edv_encode_kernel(const uint8_t* __res
 #ifndef EDV_COMB_MIN_WAVES
 #define EDV_COMB_MIN_WAVES 4  // 128 VGPRs: 1M lanes = 3.8 rounds of 262k (3 waves: 5.1 rounds -> 15% tail); -11% vs 3 (tools/ab_keyed.py)
 #endif
-constexpr int kBaseTabWords = Window<kBaseW>::kTableWords;  // 805M words at W = 22
+constexpr uint64_t kBaseTabWords = Window<kBaseW>::kTableWords;  // 2.95G words at W = 24
 constexpr int kRowWords = 40;
 
 // One lane per key: decode -A, libsodium's key checks, the row bases.
@@ -964,7 +964,7 @@ struct edv_ctx {
   int max_sub = 1;  // edv_set_pipeline (1, 2 and 4 sub-batches measure within 1% at 1M: profiles/r02b)
   bool timed = false;
   // key-table store (registered public keys)
-  uint32_t* d_btab_comb32 = nullptr;  // base-point comb table (kBaseW; 3 GiB at W = 22)
+  uint32_t* d_btab_comb32 = nullptr;  // base-point comb table (kBaseW; 11 GiB at W = 24)
   uint32_t* d_ident = nullptr;        // identity niels entry (comb accessors' j = -1)
   uint8_t* d_key_pk = nullptr;
   uint8_t* d_key_valid = nullptr;
@@ -1585,6 +1585,7 @@ int edv_verify_batch_keyed(edv_ctx* ctx, const uint8_t* sig64, const uint32_t* k
 extern "C" {
 
 const char* edv_version(void) { return EDV_VERSION; }
+int edv_base_window(void) { return kBaseW; }
 const char* edv_last_error(void) { return g_err.c_str(); }
 
 int edv_device_count(void) {

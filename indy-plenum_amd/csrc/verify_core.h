@@ -130,9 +130,11 @@ EDV_HD bool verify_phase_table(const uint32_t pk[8], TA& ta) {
 // W = 8 fixed-base comb of B (CB::load(row, j, ge_niels&), comb.h), 32 mixed
 // additions and no doublings of its own.
 #ifndef EDV_BASE_W
-#define EDV_BASE_W 22  // 16: 16 rows (64 MiB); 18: 15; 20: 13 (832 MiB) -- comb -8% vs 16; 22: 12 rows, +1.5% vs 20
+#define EDV_BASE_W 24  // 16: 16 rows (64 MiB); 20: 13 (832 MiB), comb -8% vs 16; 22: 12 (3 GiB), +1.5% vs 20;
+                       // 24: 11 rows (11 GiB, 1 GiB row slabs), comb -4..7% vs 22; 26: 10 rows (40 GiB, 4 GiB
+                       // slabs), comb +6..15% vs 24 (profiles/r02i/ab_b24, ab_b26)
 #endif                  // (tools/gpu_basew.sh, tools/gpu_ab_b22.sh)
-constexpr int kBaseW = EDV_BASE_W;  // base-point comb window: 12 rows x 2^21 entries (3 GiB) at W = 22
+constexpr int kBaseW = EDV_BASE_W;  // base-point comb window: 11 rows x 2^23 entries (11 GiB) at W = 24
 template <class TA, class CB>
 EDV_HD uint32_t verify_phase_dsm_point(ge_p3& Q, const uint32_t h[8], const uint32_t S[8], const TA& ta,
                                        const CB& cb) {

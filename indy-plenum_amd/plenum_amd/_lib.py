@@ -19,6 +19,7 @@ _U32 = _c.c_uint32
 _I = _c.c_int
 SIGNATURES = {
     "edv_version": (_c.c_char_p, []),
+    "edv_base_window": (_c.c_int, []),
     "edv_last_error": (_c.c_char_p, []),
     "edv_device_count": (_I, []),
     "edv_create": (_P, [_I]),

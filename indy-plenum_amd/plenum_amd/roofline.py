@@ -29,10 +29,11 @@ MAD_TABLE_KERNEL = FE_DECODE * MAD_PER_FE
 # The implementation's edv_dsm_kernel with K split tables per distinct key
 # (verify_core.h verify_phase_dsm_split_point): 64/K - 1 steps of 4 doublings
 # (3 x (4 sq + 3 mul) + (4 sq + 4 mul) = 29 field ops), 64 cached additions
-# (4 + 4 field ops), 12 base-comb mixed additions (7).  K = 1: 2,423 field ops
-# (ref10's 2,510 less its sliding-window bookkeeping); K = 4: 1,031; K = 8: 799.
+# (4 + 4 field ops), ceil(254 / kBaseW) = 11 base-comb mixed additions (7).
+# K = 1: 2,416 field ops (ref10's 2,510 less its sliding-window bookkeeping);
+# K = 4: 1,024; K = 8: 792.
 def fe_dsm_split(k):
-    return (64 // k - 1) * 29 + 64 * 8 + BASE_ROWS_DSM * 7
+    return (64 // k - 1) * 29 + 64 * 8 + BASE_ROWS * 7
 
 
 def mad_dsm_kernel(k):
@@ -43,12 +44,12 @@ def split_of(distinct, n):
     """edverify.hip split_of: tables per distinct key of a sub-batch."""
     return 8 if 16 * distinct <= n else 4 if 4 * distinct <= n else 1
 # Key-table path (keys registered once): edv_comb_kernel<W> = fixed-base combs
-# over both tables -- ceil(254 / W) rows of the key table + ceil(254 / 22) = 12
-# rows of the W = 22 base table (verify_core.h kBaseW) -- one mixed addition
-# (7 multiplications) per row, except the key comb's row 0, which is set with
-# one multiplication (comb.h comb_set).
-BASE_W = 22
-BASE_ROWS_DSM = (254 + BASE_W - 1) // BASE_W
+# over both tables -- ceil(254 / W) rows of the key table + ceil(254 / kBaseW)
+# rows of the base table (verify_core.h kBaseW = 24: 11 rows) -- one mixed
+# addition (7 multiplications) per row, except the key comb's row 0, which is
+# set with one multiplication (comb.h comb_set).  The base window is the
+# library's (edv_base_window; set_base_window), so the price follows the build.
+BASE_W = 24
 
 
 def key_rows(w):
@@ -58,8 +59,14 @@ def key_rows(w):
 BASE_ROWS = key_rows(BASE_W)
 
 
+def set_base_window(w):
+    """Price the base comb at the window the loaded library was built with."""
+    global BASE_W, BASE_ROWS
+    BASE_W, BASE_ROWS = int(w), key_rows(int(w))
+
+
 def mad_comb_kernel(w):
-    return ((key_rows(w) - 1 + BASE_ROWS) * 7 + 1) * MAD_PER_FE  # W=13: 21,800; W=10: 26,000; W=8: 30,200
+    return ((key_rows(w) - 1 + BASE_ROWS) * 7 + 1) * MAD_PER_FE  # base 24, W=14: 20,400; W=10: 25,300
 
 
 # edv_encode_kernel<M>: per request 3 multiplications of Montgomery's trick +
@@ -68,16 +75,13 @@ def mad_encode_kernel(m):
     return (5 + FE_ENCODE / m) * MAD_PER_FE
 
 
-MAD_COMB_KERNEL = mad_comb_kernel(10)
-
-
 def kernel_work(name, w=8):
     if name == "edv_comb_kernel":
         return ("((%d - 1 key rows (W=%d; row 0 set with 1 field op) + %d base rows (W=%d)) mixed additions "
                 "x 7 field ops + 1) x 100 MAD" % (key_rows(w), w, BASE_ROWS, BASE_W))
     if name == "edv_dsm_kernel":
-        return ("((64/K - 1) x 29 + 64 x 8 + 12 x 7) field ops x 100 MAD (K split tables per distinct key, "
-                "roofline.fe_dsm_split)")
+        return ("((64/K - 1) x 29 + 64 x 8 + %d x 7) field ops x 100 MAD (K split tables per distinct key, "
+                "roofline.fe_dsm_split)" % BASE_ROWS)
     return ""
 
 
