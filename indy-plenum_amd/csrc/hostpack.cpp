@@ -28,7 +28,11 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <string>
+#include <string_view>
+#include <thread>
+#include <unordered_map>
 #include <vector>
 
 namespace {
@@ -181,6 +185,113 @@ PyObject* py_serialize_for_signing(PyObject*, PyObject* args) {
   Py_XDECREF(ign);
   if (!ok) Py_RETURN_NONE;
   return PyBytes_FromStringAndSize(out.data(), (Py_ssize_t)out.size());
+}
+
+// ------------------------------------------------ serializer for worker threads
+// scan_batch's worker threads serialize while the calling thread holds the GIL
+// and waits for them: no Python code runs and no object changes meanwhile.
+// The workers touch objects through pure reads only (exact-type checks,
+// PyDict_Next, the data of one-byte strings, the digits of an exact int) -- no
+// allocation, no reference counts, no error state (PyDict_GetItem would touch
+// the GIL holder's error state, so the values come from PyDict_Next).  What
+// needs more -- str() of a float or a big int, non-ASCII text, keys that are
+// not one-byte strings -- is kDefer: ser_obj redoes that item under the GIL.
+// kOk bytes equal ser_obj's; kFail exactly where ser_obj returns false.
+enum WRes { kOk = 0, kFail = 1, kDefer = 2 };
+
+WRes wser_obj(PyObject* o, int level, PyObject* ignore, std::string& out);
+
+bool w_str_eq(PyObject* a, PyObject* b) {  // canonical kinds: equal strings have equal kinds
+  const Py_ssize_t n = PyUnicode_GET_LENGTH(a);
+  return PyUnicode_KIND(a) == PyUnicode_KIND(b) && n == PyUnicode_GET_LENGTH(b) &&
+         memcmp(PyUnicode_DATA(a), PyUnicode_DATA(b), (size_t)n * PyUnicode_KIND(a)) == 0;
+}
+
+bool w_ignored(PyObject* k, PyObject* ignore) {
+  if (!ignore) return false;
+  const Py_ssize_t n = PySequence_Fast_GET_SIZE(ignore);
+  PyObject** items = PySequence_Fast_ITEMS(ignore);
+  for (Py_ssize_t i = 0; i < n; ++i)
+    if (PyUnicode_CheckExact(items[i]) && w_str_eq(k, items[i])) return true;
+  return false;
+}
+
+bool w_less(PyObject* a, PyObject* b) {  // both one-byte kind (checked by the caller)
+  const Py_ssize_t na = PyUnicode_GET_LENGTH(a), nb = PyUnicode_GET_LENGTH(b);
+  const int c = memcmp(PyUnicode_1BYTE_DATA(a), PyUnicode_1BYTE_DATA(b), (size_t)(na < nb ? na : nb));
+  return c < 0 || (c == 0 && na < nb);
+}
+
+WRes w_append_str(PyObject* s, std::string& out) {
+  if (!PyUnicode_IS_ASCII(s)) return kDefer;  // UTF-8 encoding may allocate
+  out.append((const char*)PyUnicode_1BYTE_DATA(s), (size_t)PyUnicode_GET_LENGTH(s));
+  return kOk;
+}
+
+WRes wser_dict(PyObject* d, int level, PyObject* ignore, std::string& out) {
+  constexpr Py_ssize_t kSmall = 24;
+  struct KV {
+    PyObject *k, *v;
+  };
+  KV small[kSmall];
+  std::vector<KV> big;
+  const Py_ssize_t nd = PyDict_GET_SIZE(d);
+  KV* kv = small;
+  if (nd > kSmall) {
+    big.resize((size_t)nd);
+    kv = big.data();
+  }
+  Py_ssize_t nk = 0, pos = 0;
+  PyObject *k, *v;
+  bool one_byte = true;
+  while (PyDict_Next(d, &pos, &k, &v)) {
+    if (!PyUnicode_CheckExact(k)) return kFail;  // as ser_dict
+    if (level == 0 && w_ignored(k, ignore)) continue;
+    one_byte = one_byte && PyUnicode_KIND(k) == PyUnicode_1BYTE_KIND;
+    kv[nk++] = KV{k, v};
+  }
+  if (!one_byte) return kDefer;  // PyUnicode_Compare order for wider kinds: ser_dict
+  std::sort(kv, kv + nk, [](const KV& a, const KV& b) { return w_less(a.k, b.k); });
+  for (Py_ssize_t i = 0; i < nk; ++i) {
+    if (i) out.push_back('|');
+    WRes r = w_append_str(kv[i].k, out);
+    if (r != kOk) return r;
+    out.push_back(':');
+    r = wser_obj(kv[i].v, level + 1, nullptr, out);
+    if (r != kOk) return r;
+  }
+  return kOk;
+}
+
+WRes wser_obj(PyObject* o, int level, PyObject* ignore, std::string& out) {
+  if (level > kMaxDepth) return kFail;
+  if (PyUnicode_CheckExact(o)) return w_append_str(o, out);
+  if (PyDict_CheckExact(o)) return wser_dict(o, level, ignore, out);
+  if (PyList_CheckExact(o)) {
+    const Py_ssize_t n = PyList_GET_SIZE(o);
+    for (Py_ssize_t i = 0; i < n; ++i) {
+      if (i) out.push_back(',');
+      const WRes r = wser_obj(PyList_GET_ITEM(o, i), level + 1, nullptr, out);
+      if (r != kOk) return r;
+    }
+    return kOk;
+  }
+  if (o == Py_None) return kOk;
+  if (PyBool_Check(o)) {
+    out.append(o == Py_True ? "True" : "False");
+    return kOk;
+  }
+  if (PyLong_CheckExact(o)) {
+    int overflow = 0;
+    const long long x = PyLong_AsLongLongAndOverflow(o, &overflow);  // an exact int never errors
+    if (overflow) return kDefer;
+    char b[24];
+    const int len = snprintf(b, sizeof b, "%lld", x);
+    out.append(b, (size_t)len);
+    return kOk;
+  }
+  if (PyFloat_CheckExact(o)) return kDefer;  // Python's repr: str() under the GIL
+  return kFail;
 }
 
 // ------------------------------------------------------------------- base58
@@ -412,7 +523,8 @@ PyObject* py_pack_sm(PyObject*, PyObject* args) {
   return ret;
 }
 
-// scan_batch(msgs, ignore) -> (fast, idrs, sig64, msgbuf, off, short)
+// scan_batch(msgs, ignore[, threads]) -> (fast, idrs, sig64, msgbuf, off, short)
+// scan_batch_u(msgs, ignore[, threads]) -> (fast, uidx, uniq, sig64, msgbuf, off, short)
 // The host half of NaclAuthNr.authenticate for a batch of request dicts
 // (client_authn.py:72-92) where every step succeeds without a decision the
 // Python code must make: msg[signature] is a non-empty str, msg[identifier] a
@@ -421,11 +533,55 @@ PyObject* py_pack_sm(PyObject*, PyObject* args) {
 // sm = b58decode(sig) || ser is split at byte 64 like crypto_sign_open
 // (nacl_wrappers.py:108): sig64 (n * 64), messages (msgbuf + off[n + 1],
 // uint64 LE), short[i] = len(sm) < 64.  idrs[i] is the identifier (fast items)
-// or None.  Every other item (fast[i] = 0, zero-length slots) takes the
-// Python _prepare, which raises the reference's exception.
-PyObject* py_scan_batch(PyObject*, PyObject* args) {
+// or None; the _u form gives instead uidx[i] (uint32 LE, 0xffffffff for
+// non-fast items) into uniq, the batch's distinct identifiers in first-seen
+// order, so the caller resolves each verkey once without a per-item loop.
+// Every other item (fast[i] = 0, zero-length slots) takes the Python
+// _prepare, which raises the reference's exception.
+//
+// Phases: (1) under the GIL, per item: the dict / type checks and the
+// identifier's slot; (2) `threads` workers (0 = auto) split the items into
+// ranges and do the base58 decode and the serialization (wser_obj) into
+// buffers of their own; (3) under the GIL, the deferred serializations
+// (ser_obj); (4) offsets by prefix sum; (5) the workers write sig64 and the
+// message buffer straight into the result bytes objects.
+struct ScanItem {
+  PyObject* m = nullptr;
+  const unsigned char* sp = nullptr;
+  Py_ssize_t ns = 0;
+  uint32_t uid = 0xffffffffu;
+  uint8_t state = 0;  // 0 Python path, 1 fast, 2 serialization deferred
+  uint16_t buf = 0;   // which buffer holds its decoded signature / serialization
+  uint32_t sig_len = 0, ser_len = 0;
+  uint64_t sig_at = 0, ser_at = 0;
+};
+struct ScanBuf {
+  std::string sig, ser;
+};
+
+int scan_threads(Py_ssize_t n, int want) {
+  if (want > 0) return std::min(want, 64);
+  const unsigned hc = std::thread::hardware_concurrency();
+  const Py_ssize_t by_size = n / 8192 + 1;
+  return (int)std::max<Py_ssize_t>(1, std::min<Py_ssize_t>({(Py_ssize_t)(hc ? hc : 1), (Py_ssize_t)16, by_size}));
+}
+
+template <class F>
+void run_ranges(Py_ssize_t n, int t, F&& f) {  // f(worker, begin, end), t workers
+  if (t <= 1) {
+    f(0, (Py_ssize_t)0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve((size_t)t);
+  for (int w = 0; w < t; ++w) th.emplace_back([&, w] { f(w, n * w / t, n * (w + 1) / t); });
+  for (auto& x : th) x.join();
+}
+
+PyObject* scan_impl(PyObject* args, bool unique_form) {
   PyObject *msgs, *ignore = Py_None;
-  if (!PyArg_ParseTuple(args, "O|O", &msgs, &ignore)) return nullptr;
+  int want_threads = 0;
+  if (!PyArg_ParseTuple(args, "O|Oi", &msgs, &ignore, &want_threads)) return nullptr;
   PyObject* fm = PySequence_Fast(msgs, "msgs must be a sequence");
   if (!fm) return nullptr;
   PyObject* ign = nullptr;
@@ -439,66 +595,216 @@ PyObject* py_scan_batch(PyObject*, PyObject* args) {
   static PyObject* k_sig = PyUnicode_InternFromString("signature");
   static PyObject* k_idr = PyUnicode_InternFromString("identifier");
   const Py_ssize_t n = PySequence_Fast_GET_SIZE(fm);
-  std::string fast((size_t)n, '\0'), shortv((size_t)n, '\0'), sig64((size_t)n * 64, '\0'), buf;
-  std::vector<uint64_t> off((size_t)n + 1, 0);
-  PyObject* idrs = PyList_New(n);
-  if (!idrs) {
-    Py_DECREF(fm);
-    Py_XDECREF(ign);
-    return nullptr;
-  }
-  std::vector<uint8_t> sig;
-  std::string ser;
-  buf.reserve((size_t)n * 160);
+  std::vector<ScanItem> it((size_t)n);
+  std::vector<PyObject*> idr_of((size_t)n, nullptr);  // borrowed (the dicts hold them)
+  std::vector<PyObject*> uniq;
+  std::unordered_map<std::string_view, uint32_t> slot;
+  const bool prof = getenv("EDV_SCAN_PROFILE") != nullptr;
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  auto t_start = now();
+  // (1) checks and identifier slots, under the GIL
   for (Py_ssize_t i = 0; i < n; ++i) {
     PyObject* m = PySequence_Fast_GET_ITEM(fm, i);
-    PyObject* idr = Py_None;
-    bool ok = PyDict_CheckExact(m);
-    PyObject *sv = nullptr, *iv = nullptr;
-    if (ok) {
-      sv = PyDict_GetItemWithError(m, k_sig);
-      iv = sv ? PyDict_GetItemWithError(m, k_idr) : nullptr;
-      if (PyErr_Occurred()) PyErr_Clear();
-      ok = sv && iv && PyUnicode_CheckExact(sv) && PyUnicode_GET_LENGTH(sv) > 0 && PyUnicode_CheckExact(iv) &&
-           PyUnicode_GET_LENGTH(iv) > 0 && PyUnicode_IS_ASCII(sv);
+    ScanItem& x = it[(size_t)i];
+    if (!PyDict_CheckExact(m)) continue;
+    PyObject* sv = PyDict_GetItemWithError(m, k_sig);
+    PyObject* iv = sv ? PyDict_GetItemWithError(m, k_idr) : nullptr;
+    if (PyErr_Occurred()) PyErr_Clear();
+    if (!(sv && iv && PyUnicode_CheckExact(sv) && PyUnicode_GET_LENGTH(sv) > 0 && PyUnicode_CheckExact(iv) &&
+          PyUnicode_GET_LENGTH(iv) > 0 && PyUnicode_IS_ASCII(sv)))
+      continue;
+    Py_ssize_t ni = 0;
+    const char* ip = PyUnicode_AsUTF8AndSize(iv, &ni);
+    if (!ip) {
+      PyErr_Clear();
+      continue;
     }
-    if (ok) {
-      Py_ssize_t ns = 0;
-      const unsigned char* sp = (const unsigned char*)PyUnicode_AsUTF8AndSize(sv, &ns);
-      ok = sp && b58decode_raw(sp, (size_t)ns, sig);
-      if (!sp) PyErr_Clear();
-    }
-    if (ok) {
-      ser.clear();
-      ok = ser_obj(m, 0, ign, ser);
-    }
-    if (ok) {
-      fast[(size_t)i] = 1;
-      idr = iv;
-      const size_t ls = sig.size(), lm = ser.size();
-      char* dst = &sig64[(size_t)i * 64];
-      if (ls + lm < 64) {
-        shortv[(size_t)i] = 1;  // crypto_sign_open: smlen < 64 rejects
-      } else if (ls >= 64) {
-        memcpy(dst, sig.data(), 64);
-        buf.append((const char*)sig.data() + 64, ls - 64);
-        buf.append(ser);
+    x.m = m;
+    x.sp = (const unsigned char*)PyUnicode_1BYTE_DATA(sv);
+    x.ns = PyUnicode_GET_LENGTH(sv);
+    x.state = 1;
+    idr_of[(size_t)i] = iv;
+    auto ins = slot.emplace(std::string_view(ip, (size_t)ni), (uint32_t)uniq.size());
+    if (ins.second) uniq.push_back(iv);
+    x.uid = ins.first->second;
+  }
+  auto t_p1 = now();
+  // (2) base58 decode + serialization on the workers
+  const int t = scan_threads(n, want_threads);
+  std::vector<ScanBuf> bufs((size_t)t + 1);  // bufs[t]: the deferred serializations
+  run_ranges(n, t, [&](int w, Py_ssize_t a, Py_ssize_t b) {
+    ScanBuf& sb = bufs[(size_t)w];
+    sb.sig.reserve((size_t)(b - a) * 64);
+    sb.ser.reserve((size_t)(b - a) * 200);
+    std::vector<uint8_t> sig;
+    for (Py_ssize_t i = a; i < b; ++i) {
+      ScanItem& x = it[(size_t)i];
+      if (x.state != 1) continue;
+      if (!b58decode_raw(x.sp, (size_t)x.ns, sig)) {
+        x.state = 0;
+        continue;
+      }
+      x.buf = (uint16_t)w;
+      x.sig_at = sb.sig.size();
+      x.sig_len = (uint32_t)sig.size();
+      sb.sig.append((const char*)sig.data(), sig.size());
+      const size_t at = sb.ser.size();
+      const WRes r = wser_obj(x.m, 0, ign, sb.ser);
+      if (r == kOk) {
+        x.ser_at = at;
+        x.ser_len = (uint32_t)(sb.ser.size() - at);
       } else {
-        memcpy(dst, sig.data(), ls);
-        memcpy(dst + ls, ser.data(), 64 - ls);
-        buf.append(ser, 64 - ls, std::string::npos);
+        sb.ser.resize(at);
+        x.state = r == kDefer ? 2 : 0;
       }
     }
-    off[(size_t)i + 1] = buf.size();
-    Py_INCREF(idr);
-    PyList_SET_ITEM(idrs, i, idr);
+  });
+  auto t_p2 = now();
+  // (3) the deferred serializations, under the GIL
+  {
+    ScanBuf& sb = bufs[(size_t)t];
+    std::string tmp;
+    for (Py_ssize_t i = 0; i < n; ++i) {
+      ScanItem& x = it[(size_t)i];
+      if (x.state != 2) continue;
+      tmp.clear();
+      if (!ser_obj(x.m, 0, ign, tmp)) {
+        x.state = 0;
+        continue;
+      }
+      // the signature moves too, so one buffer index describes the item
+      const std::string& from = bufs[x.buf].sig;
+      const uint64_t sig_at = sb.sig.size();
+      sb.sig.append(from, (size_t)x.sig_at, x.sig_len);
+      x.sig_at = sig_at;
+      x.ser_at = sb.ser.size();
+      x.ser_len = (uint32_t)tmp.size();
+      sb.ser.append(tmp);
+      x.buf = (uint16_t)t;
+      x.state = 1;
+    }
   }
+  auto t_p3 = now();
+  // (4) crypto_sign_open's split at byte 64: message lengths -> offsets
+  std::string fast((size_t)n, '\0'), shortv((size_t)n, '\0');
+  std::vector<uint64_t> off((size_t)n + 1, 0);
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    const ScanItem& x = it[(size_t)i];
+    uint64_t len = 0;
+    if (x.state == 1) {
+      fast[(size_t)i] = 1;
+      const uint64_t ls = x.sig_len, lm = x.ser_len;
+      if (ls + lm < 64)
+        shortv[(size_t)i] = 1;  // crypto_sign_open: smlen < 64 rejects
+      else
+        len = ls + lm - 64;
+    }
+    off[(size_t)i + 1] = off[(size_t)i] + len;
+  }
+  // (5) sig64 and the messages, written by the workers into the result objects
+  PyObject* o_sig = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)n * 64);
+  PyObject* o_msg = o_sig ? PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)off[(size_t)n]) : nullptr;
+  PyObject* ret = nullptr;
+  if (o_msg) {
+    char* dsig = PyBytes_AS_STRING(o_sig);
+    char* dmsg = PyBytes_AS_STRING(o_msg);
+    run_ranges(n, t, [&](int, Py_ssize_t a, Py_ssize_t b) {
+      for (Py_ssize_t i = a; i < b; ++i) {
+        const ScanItem& x = it[(size_t)i];
+        char* ds = dsig + (size_t)i * 64;
+        if (x.state != 1 || shortv[(size_t)i]) {
+          memset(ds, 0, 64);
+          continue;
+        }
+        const ScanBuf& sb = bufs[x.buf];
+        const char* sg = sb.sig.data() + x.sig_at;
+        const char* sr = sb.ser.data() + x.ser_at;
+        const size_t ls = x.sig_len, lm = x.ser_len;
+        char* dm = dmsg + off[(size_t)i];
+        if (ls >= 64) {  // sm[64:] = sig[64:] || ser
+          memcpy(ds, sg, 64);
+          memcpy(dm, sg + 64, ls - 64);
+          memcpy(dm + (ls - 64), sr, lm);
+        } else {
+          memcpy(ds, sg, ls);
+          memcpy(ds + ls, sr, 64 - ls);
+          memcpy(dm, sr + (64 - ls), lm - (64 - ls));
+        }
+      }
+    });
+    if (prof) {
+      auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+      fprintf(stderr, "scan: n=%zd threads=%d  checks %.0f us, decode+ser %.0f us, deferred %.0f us, pack %.0f us\n",
+              n, t, us(t_start, t_p1), us(t_p1, t_p2), us(t_p2, t_p3), us(t_p3, now()));
+    }
+    if (unique_form) {
+      std::vector<uint32_t> uidx((size_t)n, 0xffffffffu);
+      for (Py_ssize_t i = 0; i < n; ++i)
+        if (it[(size_t)i].state == 1) uidx[(size_t)i] = it[(size_t)i].uid;
+      PyObject* ul = PyList_New((Py_ssize_t)uniq.size());
+      if (ul) {
+        for (size_t u = 0; u < uniq.size(); ++u) {
+          Py_INCREF(uniq[u]);
+          PyList_SET_ITEM(ul, (Py_ssize_t)u, uniq[u]);
+        }
+        ret = Py_BuildValue("(y#y#OOOy#y#)", fast.data(), (Py_ssize_t)n, (const char*)uidx.data(),
+                            (Py_ssize_t)(uidx.size() * 4), ul, o_sig, o_msg, (const char*)off.data(),
+                            (Py_ssize_t)(off.size() * 8), shortv.data(), (Py_ssize_t)n);
+        Py_DECREF(ul);
+      }
+    } else {
+      PyObject* idrs = PyList_New(n);
+      if (idrs) {
+        for (Py_ssize_t i = 0; i < n; ++i) {
+          PyObject* idr = it[(size_t)i].state == 1 ? idr_of[(size_t)i] : Py_None;
+          Py_INCREF(idr);
+          PyList_SET_ITEM(idrs, i, idr);
+        }
+        ret = Py_BuildValue("(y#OOOy#y#)", fast.data(), (Py_ssize_t)n, idrs, o_sig, o_msg, (const char*)off.data(),
+                            (Py_ssize_t)(off.size() * 8), shortv.data(), (Py_ssize_t)n);
+        Py_DECREF(idrs);
+      }
+    }
+  }
+  Py_XDECREF(o_sig);
+  Py_XDECREF(o_msg);
   Py_DECREF(fm);
   Py_XDECREF(ign);
-  PyObject* ret = Py_BuildValue("(y#Oy#y#y#y#)", fast.data(), (Py_ssize_t)n, idrs, sig64.data(),
-                                (Py_ssize_t)sig64.size(), buf.data(), (Py_ssize_t)buf.size(), (const char*)off.data(),
-                                (Py_ssize_t)(off.size() * 8), shortv.data(), (Py_ssize_t)n);
-  Py_DECREF(idrs);
+  return ret;
+}
+
+PyObject* py_scan_batch(PyObject*, PyObject* args) { return scan_impl(args, false); }
+PyObject* py_scan_batch_u(PyObject*, PyObject* args) { return scan_impl(args, true); }
+
+// results_from(codes, uidx, uniq) -> list: item i is uniq[uidx[i]] where
+// codes[i] == 1 (verified: authenticate() returns the identifier), None
+// elsewhere (the caller fills those in).
+PyObject* py_results_from(PyObject*, PyObject* args) {
+  Py_buffer bc, bu;
+  PyObject* uniq;
+  if (!PyArg_ParseTuple(args, "y*y*O", &bc, &bu, &uniq)) return nullptr;
+  PyObject* ret = nullptr;
+  const Py_ssize_t n = bc.len;
+  if (!PyList_CheckExact(uniq) || bu.len != n * 4) {
+    PyErr_SetString(PyExc_ValueError, "results_from: codes / uidx / uniq mismatch");
+  } else {
+    const uint8_t* c = (const uint8_t*)bc.buf;
+    const uint32_t* u = (const uint32_t*)bu.buf;
+    const Py_ssize_t nu = PyList_GET_SIZE(uniq);
+    bool ok = true;
+    for (Py_ssize_t i = 0; i < n && ok; ++i) ok = c[i] != 1 || (Py_ssize_t)u[i] < nu;
+    if (!ok) {
+      PyErr_SetString(PyExc_ValueError, "results_from: identifier index out of range");
+    } else if ((ret = PyList_New(n))) {
+      for (Py_ssize_t i = 0; i < n; ++i) {
+        PyObject* o = c[i] == 1 ? PyList_GET_ITEM(uniq, u[i]) : Py_None;
+        Py_INCREF(o);
+        PyList_SET_ITEM(ret, i, o);
+      }
+    }
+  }
+  PyBuffer_Release(&bc);
+  PyBuffer_Release(&bu);
   return ret;
 }
 
@@ -537,7 +843,13 @@ PyObject* py_gather_items(PyObject*, PyObject* args) {
 
 PyMethodDef kMethods[] = {
     {"scan_batch", py_scan_batch, METH_VARARGS,
-     "scan_batch(msgs, ignore) -> (fast, idrs, sig64, msgbuf, off, short): authenticate()'s host steps for a batch"},
+     "scan_batch(msgs, ignore, threads=0) -> (fast, idrs, sig64, msgbuf, off, short): authenticate()'s host steps "
+     "for a batch"},
+    {"scan_batch_u", py_scan_batch_u, METH_VARARGS,
+     "scan_batch_u(msgs, ignore, threads=0) -> (fast, uidx_u32, uniq, sig64, msgbuf, off, short): scan_batch with "
+     "the identifiers as indices into the batch's distinct identifiers"},
+    {"results_from", py_results_from, METH_VARARGS,
+     "results_from(codes_u8, uidx_u32, uniq) -> list: uniq[uidx[i]] where codes[i] == 1, else None"},
     {"gather_items", py_gather_items, METH_VARARGS,
      "gather_items(sig64, msgbuf, off, idx_u32) -> (sig64, msgbuf, off) of the selected items"},
     {"serialize_for_signing", py_serialize_for_signing, METH_VARARGS,

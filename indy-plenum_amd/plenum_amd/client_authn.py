@@ -59,9 +59,9 @@ from .serialization import serialize_msg_for_signing
 from .verifier import DidVerifier, VerkeyCache
 
 try:  # native batch scan (csrc/hostpack.cpp): authenticate()'s host steps for a whole batch
-    from ._hostpack import gather_items as _gather_items, scan_batch as _scan_batch
+    from ._hostpack import gather_items as _gather_items, results_from as _results_from, scan_batch_u as _scan_batch
 except ImportError:  # pragma: no cover - the per-message path below
-    _scan_batch = _gather_items = None
+    _scan_batch = _gather_items = _results_from = None
 
 try:  # native packing (csrc/hostpack.cpp)
     from ._hostpack import pack_sm as _pack_sm, pack_split64 as _pack_split64
@@ -106,13 +106,6 @@ KEY_STORE_BYTES = 32 << 30  # HBM for key tables: the window is the widest that 
 _MISSING = object()
 
 
-class _KeyOnly:
-    __slots__ = ("key",)
-
-    def __init__(self, key):
-        self.key = key
-
-
 class _Prepared:
     __slots__ = ("identifier", "sig", "ser", "key")
 
@@ -124,7 +117,7 @@ class _GpuState:
     """Per-authenticator GPU state (created on first use)."""
 
     def __init__(self, engine=None, device=0, devices=None, verdict_cache_size=1 << 20, key_window="auto",
-                 max_keys=16384, hot_key_uses=2, key_store_bytes=KEY_STORE_BYTES):
+                 max_keys=16384, hot_key_uses=2, key_store_bytes=KEY_STORE_BYTES, scan_threads=0):
         self.engine = engine
         self.device = device
         self.devices = devices
@@ -138,6 +131,7 @@ class _GpuState:
         self.key_uses_max = 1 << 16
         self.pending = OrderedDict()    # addIdr keys waiting for a free slot
         self.hot = OrderedDict()        # keys that earned a slot (hot_key_uses verified requests)
+        self.scan_threads = scan_threads  # host threads of the native batch scan (0 = auto)
         self.stats = {"batches": 0, "batch_items": 0, "cache_hits": 0, "single_verifies": 0, "keyed_items": 0,
                       "keys_registered": 0}
 
@@ -153,7 +147,9 @@ class GpuAuthMixin:
         devices=[...] or "all": a MultiEngine sharding every batch over them).
         options (_GpuState): verdict_cache_size; key_window ('auto' = widest
         comb whose max_keys tables fit key_store_bytes, e.g. 16,384 keys in
-        32 GiB -> W=10, 1,000 keys -> W=14); max_keys; hot_key_uses."""
+        32 GiB -> W=10, 1,000 keys -> W=14); max_keys; hot_key_uses;
+        scan_threads (host threads of authenticate_batch's native scan, 0 =
+        auto: up to 16, one per 8k requests)."""
         self._edv = _GpuState(engine=engine, device=device, **options)
 
     @property
@@ -300,6 +296,25 @@ class GpuAuthMixin:
         while len(uses) > g.key_uses_max:
             uses.popitem(last=False)
 
+    def _count_verified_keys(self, keys, counts):
+        """_count_verified for c[j] verified requests of key j at once (the
+        same final state as counting them one by one)."""
+        g = self._g
+        if g.max_keys <= 0:
+            return
+        uses, h = g.key_uses, g.hot_key_uses
+        for key, c in zip(keys, counts):
+            if not c:
+                continue
+            u = uses.pop(key, 0) + int(c)
+            if u >= h:
+                g.hot[key] = None
+                u %= h
+            if u:
+                uses[key] = u
+        while len(uses) > g.key_uses_max:
+            uses.popitem(last=False)
+
     def _verify_keyed(self, items, ids):
         """crypto_sign_open(sig || ser) against registered keys: the split at
         byte 64 done on the host (nacl_wrappers.py:108), len < 64 rejects."""
@@ -394,57 +409,59 @@ class GpuAuthMixin:
 
     def _authenticate_batch_scanned(self, msgs):
         """authenticate_batch with the host steps in native code: one
-        _hostpack.scan_batch over the dicts (signature / identifier checks,
-        b58decode, serialization, crypto_sign_open's split at byte 64), the
-        verkey resolved once per identifier of the batch, one GPU launch per
-        path.  Messages the scan leaves to Python (odd types, missing fields,
-        bad base58 ...) go through _prepare, which raises the reference's
-        exception."""
+        _hostpack.scan_batch_u over the dicts (signature / identifier checks,
+        b58decode, serialization, crypto_sign_open's split at byte 64, on
+        scan_threads host threads), the verkey resolved once per distinct
+        identifier of the batch, one GPU launch per path, the result list built
+        natively.  Messages the scan leaves to Python (odd types, missing
+        fields, bad base58 ...) go through _prepare, which raises the
+        reference's exception."""
         import numpy as np
         n = len(msgs)
-        fast, idrs, sig64, mbuf, off, short = _scan_batch(msgs, [SIG])
-        results = [None] * n
-        key_of = {}
-        keys = [None] * n
-        fast_idx = []
-        for i, idr in enumerate(idrs):
-            if idr is None:
-                continue
-            k = key_of.get(idr, _MISSING)
-            if k is _MISSING:
-                k = key_of[idr] = self._key_for(idr)
-            if k is None or k.__class__ is bytes:
-                keys[i] = k
-                fast_idx.append(i)
-            else:
-                results[i] = self._fresh(k)
-        if fast_idx:
-            ok = self._verify_split(fast_idx, keys, sig64, mbuf, off, short)
-            for i, v in zip(fast_idx, ok):
-                results[i] = idrs[i] if v else InvalidSignature()
-        slow = [i for i in range(n) if not fast[i]]
+        fast_b, uidx_b, uniq, sig64, mbuf, off, short = _scan_batch(msgs, [SIG], self._g.scan_threads)
+        fast = np.frombuffer(fast_b, np.uint8).astype(bool)
+        uidx = np.frombuffer(uidx_b, np.uint32)
+        ukeys = [self._key_for(idr) for idr in uniq]  # authenticate():93-99, once per identifier
+        # per distinct identifier: 0 = key bytes, 1 = no key (the verify fails), 2 = exception
+        ucls = np.fromiter((0 if k.__class__ is bytes else 1 if k is None else 2 for k in ukeys), np.uint8,
+                           len(ukeys))
+        fidx = np.nonzero(fast)[0]
+        icls = ucls[uidx[fidx]] if len(fidx) else np.zeros(0, np.uint8)
+        vidx = fidx[icls != 2]  # the items that reach the verify
+        codes = np.zeros(n, np.uint8)
+        ok = self._verify_scanned(vidx, uidx, ukeys, ucls, sig64, mbuf, off, short) if len(vidx) else \
+            np.zeros(0, bool)
+        codes[vidx[ok]] = 1
+        results = _results_from(codes.tobytes(), uidx_b, uniq)  # the identifier where verified
+        for i in vidx[~ok].tolist():
+            results[i] = InvalidSignature()
+        for i in fidx[icls == 2].tolist():
+            results[i] = self._fresh(ukeys[uidx[i]])
+        slow = np.nonzero(~fast)[0].tolist()
         if slow:
             for i, r in zip(slow, self._authenticate_batch_each([msgs[i] for i in slow])):
                 results[i] = r
         return results
 
-    def _verify_split(self, idx, keys, sig64, mbuf, off, short):
-        """Verdicts of the scanned items idx (split sig64 / messages of the
-        whole batch): registered keys on the key-table path, the rest one
-        general launch, no key -> False."""
+    def _verify_scanned(self, vidx, uidx, ukeys, ucls, sig64, mbuf, off, short):
+        """Verdicts of the scanned items vidx (split sig64 / messages of the
+        whole batch; item i's key = ukeys[uidx[i]]): registered keys on the
+        key-table path, the rest one general launch, no key -> False."""
         import numpy as np
         g = self._g
-        m = len(idx)
-        idx_a = np.asarray(idx, np.uint32)
-        short_a = np.frombuffer(short, np.uint8)[idx_a] != 0
+        m = len(vidx)
+        item_u = uidx[vidx].astype(np.int64)
+        short_a = np.frombuffer(short, np.uint8)[vidx] != 0
         ok = np.zeros(m, bool)
-        item_keys = [keys[i] for i in idx]
-        uniq = list(dict.fromkeys(k for k in item_keys if k))
+        has_key = np.nonzero(ucls == 0)[0]
+        ukey_list = [ukeys[u] for u in has_key.tolist()]
+        uniq_keys = list(dict.fromkeys(ukey_list))
+        kid_u = np.full(len(ukeys), -2, np.int64)  # -2: no key, -1: general path, >= 0: key-store id
+        kid_u[has_key] = -1
         ks = self._key_store()
-        kid_of = {}
-        if ks is not None and uniq:
+        if ks is not None and uniq_keys:
             if g.hot:
-                got = ks.register(list(g.hot), pinned=uniq, evict=True)
+                got = ks.register(list(g.hot), pinned=uniq_keys, evict=True)
                 g.stats["keys_registered"] += len(got)
                 g.hot.clear()
             if g.pending:
@@ -453,34 +470,39 @@ class GpuAuthMixin:
                     got = ks.register([k for k in g.pending if k not in ks][:room], evict=False)
                     g.stats["keys_registered"] += len(got)
                 g.pending.clear()
-            kid_of = {k: i for k, i in zip(uniq, ks.lookup(uniq)) if i is not None}
-        kid = np.fromiter((kid_of.get(k, -1) if k else -2 for k in item_keys), np.int64, m)
+            id_of = {k: i for k, i in zip(uniq_keys, ks.lookup(uniq_keys)) if i is not None}
+            kid_u[has_key] = [id_of.get(k, -1) for k in ukey_list]
+        kid = kid_u[item_u]
         keyed = np.nonzero(kid >= 0)[0]
         general = np.nonzero(kid == -1)[0]
         eng = self._engine()
-        full = len(idx) == len(keys)
+        whole = m == len(uidx)
         for sel, is_keyed in ((keyed, True), (general, False)):
             if not len(sel):
                 continue
-            if full and len(sel) == m:
+            if whole and len(sel) == m:
                 s_sig, s_msg, s_off = sig64, mbuf, off
             else:
-                s_sig, s_msg, s_off = _gather_items(sig64, mbuf, off, idx_a[sel].tobytes())
+                s_sig, s_msg, s_off = _gather_items(sig64, mbuf, off, vidx[sel].astype(np.uint32).tobytes())
             s_sig = np.frombuffer(s_sig, np.uint8).reshape(-1, 64)
             s_msg, s_off = np.frombuffer(s_msg, np.uint8), np.frombuffer(s_off, np.uint64)
             if is_keyed:
                 v = eng.verify_batch_keyed(s_sig, kid[sel].astype(np.uint32), s_msg, s_off)
                 g.stats["keyed_items"] += len(sel)
             else:
-                pk = np.frombuffer(b"".join(item_keys[j] for j in sel), np.uint8).reshape(-1, 32)
-                v = eng.verify_batch(s_sig, pk, s_msg, s_off)
+                ukey_arr = np.zeros((len(ukeys), 32), np.uint8)
+                ukey_arr[has_key] = np.frombuffer(b"".join(ukey_list), np.uint8).reshape(-1, 32)
+                v = eng.verify_batch(s_sig, ukey_arr[item_u[sel]], s_msg, s_off)
             ok[sel] = np.asarray(v, bool)
             g.stats["batches"] += 1
             g.stats["batch_items"] += len(sel)
         ok &= ~short_a
-        if len(general):
-            gen_ok = ok[general]
-            self._count_verified([_KeyOnly(item_keys[j]) for j in general[gen_ok]], [True] * int(gen_ok.sum()))
+        if len(general):  # general-path keys earn a slot by verified requests
+            verified_u = np.bincount(item_u[general[ok[general]]], minlength=len(ukeys))
+            per_key = {}
+            for u in np.nonzero(verified_u)[0].tolist():
+                per_key[ukeys[u]] = per_key.get(ukeys[u], 0) + int(verified_u[u])
+            self._count_verified_keys(list(per_key), list(per_key.values()))
         return ok
 
     def _authenticate_batch_each(self, msgs, identifiers=None, signatures=None):

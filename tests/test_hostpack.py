@@ -127,3 +127,71 @@ def test_pack_sm_layout():
     assert pk == b"k" * 32 + b"q" * 32
     with pytest.raises(ValueError):
         H.pack_sm([b"a"], [b"b"], [b"short"])
+
+
+def _scan_pool(r, n):
+    """Request-shaped dicts over the fuzz scalars/objects: every item kind the
+    scan must get exactly right (fast, deferred to the GIL, Python path)."""
+    msgs = []
+    idrs = ["idr%d" % k for k in range(7)] + ["ключ", "é"]
+    for i in range(n):
+        k = r.randrange(12)
+        sig = b58encode(bytes(r.getrandbits(8) for _ in range(r.choice([64, 64, 64, 0, 10, 63, 65, 100]))))
+        m = {"identifier": r.choice(idrs), "reqId": r.randrange(10**18), "operation": _rand_obj(r),
+             "signature": sig}
+        if k == 0:
+            m["signature"] = r.choice(["", "0OIl", "é", 17, None])
+        elif k == 1:
+            del m["identifier"]
+        elif k == 2:
+            m["identifier"] = r.choice(["", 5, None])
+        elif k == 3:
+            m = [m]
+        elif k == 4:
+            m[r.choice(["ключ", "z中"])] = r.random()  # wider-kind keys: ordered under the GIL
+        elif k == 5:
+            m[3] = "non-str key"
+        msgs.append(m)
+    return msgs
+
+
+@pytest.mark.parametrize("threads", [2, 3, 7])
+def test_scan_batch_threads_equal_serial(threads):
+    """The worker-thread scan (csrc/hostpack.cpp scan_impl: wser_obj on the
+    workers, deferred items by ser_obj under the GIL) returns exactly the
+    single-threaded result, and the single-threaded result is the Python
+    restatement's split of b58decode(sig) || serialize(msg)."""
+    r = random.Random(21)
+    msgs = _scan_pool(r, 3000)
+    one = H.scan_batch(msgs, ["signature"], 1)
+    many = H.scan_batch(msgs, ["signature"], threads)
+    assert one == many
+    fast, idrs, sig64, mbuf, off, short = one
+    offs = struct.unpack("<%dQ" % (len(msgs) + 1), off)
+    nfast = 0
+    for i, m in enumerate(msgs):
+        if not fast[i]:
+            assert idrs[i] is None and offs[i + 1] == offs[i]
+            continue
+        nfast += 1
+        sm = b58decode_py(m["signature"]) + py_ser(m, ["signature"])
+        assert idrs[i] == m["identifier"]
+        if len(sm) < 64:
+            assert short[i] == 1 and offs[i + 1] == offs[i]
+        else:
+            assert sig64[64 * i:64 * i + 64] == sm[:64] and mbuf[offs[i]:offs[i + 1]] == sm[64:]
+    assert nfast > 1000
+    fu, uidx, uniq, *rest = H.scan_batch_u(msgs, ["signature"], threads)
+    assert fu == fast and tuple(rest) == (sig64, mbuf, off, short)
+    u = struct.unpack("<%dI" % len(msgs), uidx)
+    for i in range(len(msgs)):
+        assert (uniq[u[i]] == idrs[i]) if fast[i] else u[i] == 0xffffffff
+    assert len(set(uniq)) == len(uniq)
+
+
+def test_results_from():
+    codes = bytes([1, 0, 1, 2])
+    got = H.results_from(codes, struct.pack("<4I", 1, 0xffffffff, 0, 0), ["a", "b"])
+    assert got == ["b", None, "a", None]
+    with pytest.raises(ValueError):
+        H.results_from(bytes([1]), struct.pack("<I", 5), ["a"])
