@@ -28,6 +28,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <charconv>
 #include <chrono>
 #include <string>
 #include <string_view>
@@ -163,8 +164,8 @@ bool ser_obj(PyObject* o, int level, PyObject* ignore, std::string& out) {
       return append_text_of(o, out);
     }
     char b[24];
-    const int len = snprintf(b, sizeof b, "%lld", x);
-    out.append(b, (size_t)len);
+    const auto r = std::to_chars(b, b + sizeof b, x);  // str(int) for 64-bit values
+    out.append(b, (size_t)(r.ptr - b));
     return true;
   }
   if (PyFloat_CheckExact(o)) return append_text_of(o, out);
@@ -286,8 +287,8 @@ WRes wser_obj(PyObject* o, int level, PyObject* ignore, std::string& out) {
     const long long x = PyLong_AsLongLongAndOverflow(o, &overflow);  // an exact int never errors
     if (overflow) return kDefer;
     char b[24];
-    const int len = snprintf(b, sizeof b, "%lld", x);
-    out.append(b, (size_t)len);
+    const auto r = std::to_chars(b, b + sizeof b, x);
+    out.append(b, (size_t)(r.ptr - b));
     return kOk;
   }
   if (PyFloat_CheckExact(o)) return kDefer;  // Python's repr: str() under the GIL
@@ -338,15 +339,16 @@ bool b58decode_raw(const unsigned char* s, size_t n, std::vector<uint8_t>& out) 
     }
     if (carry) limb[nl++] = (uint64_t)carry;
   }
-  out.assign(nz, 0);
-  bool lead = true;
+  // big-endian bytes of the number without its leading zero bytes, after nz zero bytes
+  size_t top = nl ? 8 - (size_t)(__builtin_clzll(limb[nl - 1]) >> 3) : 0;  // bytes of the top limb
+  const size_t len = nl ? top + (nl - 1) * 8 : 0;
+  out.resize(nz + len);
+  uint8_t* o = out.data();
+  memset(o, 0, nz);
+  o += nz;
   for (size_t j = nl; j-- > 0;) {
-    for (int sh = 56; sh >= 0; sh -= 8) {
-      const uint8_t byte = (uint8_t)(limb[j] >> sh);
-      if (lead && byte == 0) continue;
-      lead = false;
-      out.push_back(byte);
-    }
+    const size_t nb = j == nl - 1 ? top : 8;
+    for (size_t b = 0; b < nb; ++b) *o++ = (uint8_t)(limb[j] >> (8 * (nb - 1 - b)));
   }
   return true;
 }
@@ -534,17 +536,18 @@ PyObject* py_pack_sm(PyObject*, PyObject* args) {
 // (nacl_wrappers.py:108): sig64 (n * 64), messages (msgbuf + off[n + 1],
 // uint64 LE), short[i] = len(sm) < 64.  idrs[i] is the identifier (fast items)
 // or None; the _u form gives instead uidx[i] (uint32 LE, 0xffffffff for
-// non-fast items) into uniq, the batch's distinct identifiers in first-seen
-// order, so the caller resolves each verkey once without a per-item loop.
+// non-fast items) into uniq, the batch's distinct identifiers, so the caller
+// resolves each verkey once without a per-item loop.
 // Every other item (fast[i] = 0, zero-length slots) takes the Python
 // _prepare, which raises the reference's exception.
 //
-// Phases: (1) under the GIL, per item: the dict / type checks and the
-// identifier's slot; (2) `threads` workers (0 = auto) split the items into
-// ranges and do the base58 decode and the serialization (wser_obj) into
-// buffers of their own; (3) under the GIL, the deferred serializations
-// (ser_obj); (4) offsets by prefix sum; (5) the workers write sig64 and the
-// message buffer straight into the result bytes objects.
+// Phases: (1) `threads` workers (0 = auto) split the items into ranges and do
+// the checks, the base58 decode, the serialization (wser_obj) and the
+// identifier's slot into tables of their own, reading objects only as
+// wser_obj does; (2) the identifier tables merged; (3) under the GIL, the
+// items the workers could not finish (ser_obj); (4) offsets by prefix sum;
+// (5) the workers write sig64 and the message buffer straight into the result
+// bytes objects.
 struct ScanItem {
   PyObject* m = nullptr;
   const unsigned char* sp = nullptr;
@@ -597,91 +600,136 @@ PyObject* scan_impl(PyObject* args, bool unique_form) {
   const Py_ssize_t n = PySequence_Fast_GET_SIZE(fm);
   std::vector<ScanItem> it((size_t)n);
   std::vector<PyObject*> idr_of((size_t)n, nullptr);  // borrowed (the dicts hold them)
-  std::vector<PyObject*> uniq;
-  std::unordered_map<std::string_view, uint32_t> slot;
   const bool prof = getenv("EDV_SCAN_PROFILE") != nullptr;
   auto now = [] { return std::chrono::steady_clock::now(); };
   auto t_start = now();
-  // (1) checks and identifier slots, under the GIL
-  for (Py_ssize_t i = 0; i < n; ++i) {
-    PyObject* m = PySequence_Fast_GET_ITEM(fm, i);
-    ScanItem& x = it[(size_t)i];
-    if (!PyDict_CheckExact(m)) continue;
-    PyObject* sv = PyDict_GetItemWithError(m, k_sig);
-    PyObject* iv = sv ? PyDict_GetItemWithError(m, k_idr) : nullptr;
-    if (PyErr_Occurred()) PyErr_Clear();
-    if (!(sv && iv && PyUnicode_CheckExact(sv) && PyUnicode_GET_LENGTH(sv) > 0 && PyUnicode_CheckExact(iv) &&
-          PyUnicode_GET_LENGTH(iv) > 0 && PyUnicode_IS_ASCII(sv)))
-      continue;
-    Py_ssize_t ni = 0;
-    const char* ip = PyUnicode_AsUTF8AndSize(iv, &ni);
-    if (!ip) {
-      PyErr_Clear();
-      continue;
-    }
-    x.m = m;
-    x.sp = (const unsigned char*)PyUnicode_1BYTE_DATA(sv);
-    x.ns = PyUnicode_GET_LENGTH(sv);
-    x.state = 1;
-    idr_of[(size_t)i] = iv;
-    auto ins = slot.emplace(std::string_view(ip, (size_t)ni), (uint32_t)uniq.size());
-    if (ins.second) uniq.push_back(iv);
-    x.uid = ins.first->second;
-  }
-  auto t_p1 = now();
-  // (2) base58 decode + serialization on the workers
+  PyObject** items = PySequence_Fast_ITEMS(fm);
+  // (1) on the workers, per item: the checks of authenticate():72-91 (fields
+  // found by PyDict_Next: a dict with a key that is not an exact str takes the
+  // Python path), base58 decode, serialization, and the identifier's slot in
+  // the worker's own table of distinct identifiers
   const int t = scan_threads(n, want_threads);
-  std::vector<ScanBuf> bufs((size_t)t + 1);  // bufs[t]: the deferred serializations
+  std::vector<ScanBuf> bufs((size_t)t + 1);  // bufs[t]: items redone under the GIL
+  struct IdrTable {
+    std::unordered_map<std::string_view, uint32_t> slot;
+    std::vector<PyObject*> obj;
+  };
+  std::vector<IdrTable> tabs((size_t)t);
   run_ranges(n, t, [&](int w, Py_ssize_t a, Py_ssize_t b) {
     ScanBuf& sb = bufs[(size_t)w];
+    IdrTable& tab = tabs[(size_t)w];
     sb.sig.reserve((size_t)(b - a) * 64);
     sb.ser.reserve((size_t)(b - a) * 200);
     std::vector<uint8_t> sig;
     for (Py_ssize_t i = a; i < b; ++i) {
+      PyObject* m = items[i];
       ScanItem& x = it[(size_t)i];
-      if (x.state != 1) continue;
-      if (!b58decode_raw(x.sp, (size_t)x.ns, sig)) {
-        x.state = 0;
+      if (!PyDict_CheckExact(m)) continue;
+      PyObject *sv = nullptr, *iv = nullptr, *k, *v;
+      Py_ssize_t pos = 0;
+      bool str_keys = true;
+      while (PyDict_Next(m, &pos, &k, &v)) {
+        if (!PyUnicode_CheckExact(k)) {
+          str_keys = false;
+          break;
+        }
+        if (k == k_sig || w_str_eq(k, k_sig))
+          sv = v;
+        else if (k == k_idr || w_str_eq(k, k_idr))
+          iv = v;
+      }
+      if (!str_keys || !(sv && iv && PyUnicode_CheckExact(sv) && PyUnicode_GET_LENGTH(sv) > 0 &&
+                         PyUnicode_CheckExact(iv) && PyUnicode_GET_LENGTH(iv) > 0 && PyUnicode_IS_ASCII(sv)))
+        continue;  // the Python path raises the reference's exception
+      x.m = m;
+      if (!PyUnicode_IS_ASCII(iv)) {  // its UTF-8 form may need allocating: under the GIL
+        x.state = 2;
         continue;
       }
+      x.sp = (const unsigned char*)PyUnicode_1BYTE_DATA(sv);
+      x.ns = PyUnicode_GET_LENGTH(sv);
+      if (!b58decode_raw(x.sp, (size_t)x.ns, sig)) continue;
+      const size_t at = sb.ser.size();
+      const WRes r = wser_obj(m, 0, ign, sb.ser);
+      if (r != kOk) {
+        sb.ser.resize(at);
+        x.state = r == kDefer ? 2 : 0;
+        continue;
+      }
+      x.state = 1;
       x.buf = (uint16_t)w;
+      x.ser_at = at;
+      x.ser_len = (uint32_t)(sb.ser.size() - at);
       x.sig_at = sb.sig.size();
       x.sig_len = (uint32_t)sig.size();
       sb.sig.append((const char*)sig.data(), sig.size());
-      const size_t at = sb.ser.size();
-      const WRes r = wser_obj(x.m, 0, ign, sb.ser);
-      if (r == kOk) {
-        x.ser_at = at;
-        x.ser_len = (uint32_t)(sb.ser.size() - at);
-      } else {
-        sb.ser.resize(at);
-        x.state = r == kDefer ? 2 : 0;
-      }
+      idr_of[(size_t)i] = iv;
+      auto ins = tab.slot.emplace(
+          std::string_view((const char*)PyUnicode_1BYTE_DATA(iv), (size_t)PyUnicode_GET_LENGTH(iv)),
+          (uint32_t)tab.obj.size());
+      if (ins.second) tab.obj.push_back(iv);
+      x.uid = ins.first->second;
     }
   });
+  auto t_p1 = now();
+  // (2) the workers' identifier tables merged into the batch's (worker order)
+  std::vector<PyObject*> uniq;
+  std::unordered_map<std::string_view, uint32_t> slot;
+  std::vector<std::vector<uint32_t>> to_global((size_t)t);
+  for (int w = 0; w < t; ++w) {
+    for (PyObject* o : tabs[(size_t)w].obj) {
+      auto ins = slot.emplace(
+          std::string_view((const char*)PyUnicode_1BYTE_DATA(o), (size_t)PyUnicode_GET_LENGTH(o)),
+          (uint32_t)uniq.size());
+      if (ins.second) uniq.push_back(o);
+      to_global[(size_t)w].push_back(ins.first->second);
+    }
+  }
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    ScanItem& x = it[(size_t)i];
+    if (x.state == 1) x.uid = to_global[x.buf][x.uid];
+  }
   auto t_p2 = now();
-  // (3) the deferred serializations, under the GIL
+  // (3) the items the workers left (non-ASCII identifiers, floats / big ints /
+  // wide-kind keys in the payload), redone under the GIL
   {
     ScanBuf& sb = bufs[(size_t)t];
-    std::string tmp;
+    std::vector<uint8_t> sig;
     for (Py_ssize_t i = 0; i < n; ++i) {
       ScanItem& x = it[(size_t)i];
       if (x.state != 2) continue;
-      tmp.clear();
-      if (!ser_obj(x.m, 0, ign, tmp)) {
-        x.state = 0;
+      x.state = 0;
+      PyObject* m = x.m;
+      PyObject* sv = PyDict_GetItemWithError(m, k_sig);
+      PyObject* iv = sv ? PyDict_GetItemWithError(m, k_idr) : nullptr;
+      if (PyErr_Occurred()) PyErr_Clear();
+      if (!(sv && iv && PyUnicode_CheckExact(sv) && PyUnicode_GET_LENGTH(sv) > 0 && PyUnicode_CheckExact(iv) &&
+            PyUnicode_GET_LENGTH(iv) > 0 && PyUnicode_IS_ASCII(sv)))
+        continue;
+      Py_ssize_t ni = 0;
+      const char* ip = PyUnicode_AsUTF8AndSize(iv, &ni);
+      if (!ip) {
+        PyErr_Clear();
         continue;
       }
-      // the signature moves too, so one buffer index describes the item
-      const std::string& from = bufs[x.buf].sig;
-      const uint64_t sig_at = sb.sig.size();
-      sb.sig.append(from, (size_t)x.sig_at, x.sig_len);
-      x.sig_at = sig_at;
-      x.ser_at = sb.ser.size();
-      x.ser_len = (uint32_t)tmp.size();
-      sb.ser.append(tmp);
-      x.buf = (uint16_t)t;
+      if (!b58decode_raw((const unsigned char*)PyUnicode_1BYTE_DATA(sv), (size_t)PyUnicode_GET_LENGTH(sv), sig))
+        continue;
+      const size_t at = sb.ser.size();
+      if (!ser_obj(m, 0, ign, sb.ser)) {
+        sb.ser.resize(at);
+        continue;
+      }
       x.state = 1;
+      x.buf = (uint16_t)t;
+      x.ser_at = at;
+      x.ser_len = (uint32_t)(sb.ser.size() - at);
+      x.sig_at = sb.sig.size();
+      x.sig_len = (uint32_t)sig.size();
+      sb.sig.append((const char*)sig.data(), sig.size());
+      idr_of[(size_t)i] = iv;
+      auto ins = slot.emplace(std::string_view(ip, (size_t)ni), (uint32_t)uniq.size());
+      if (ins.second) uniq.push_back(iv);
+      x.uid = ins.first->second;
     }
   }
   auto t_p3 = now();
@@ -734,7 +782,7 @@ PyObject* scan_impl(PyObject* args, bool unique_form) {
     });
     if (prof) {
       auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
-      fprintf(stderr, "scan: n=%zd threads=%d  checks %.0f us, decode+ser %.0f us, deferred %.0f us, pack %.0f us\n",
+      fprintf(stderr, "scan: n=%zd threads=%d  workers %.0f us, merge %.0f us, under the GIL %.0f us, pack %.0f us\n",
               n, t, us(t_start, t_p1), us(t_p1, t_p2), us(t_p2, t_p3), us(t_p3, now()));
     }
     if (unique_form) {

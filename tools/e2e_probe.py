@@ -1,0 +1,36 @@
+"""Where the drop-in's end-to-end time goes on the GPU box: GpuAuthNr.authenticate_batch
+over configs[1]-shaped request dicts (1M NYMs, 1,000 signers), timed whole and under
+cProfile, with the native scan's phase times (EDV_SCAN_PROFILE=1).
+usage: EDV_SCAN_PROFILE=1 python tools/e2e_probe.py [n]"""
+import cProfile
+import os
+import pstats
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "indy-plenum_amd"))
+import bench  # noqa: E402
+from plenum_amd import EdVerifyEngine  # noqa: E402
+from plenum_amd.client_authn import GpuAuthNr  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
+eng = EdVerifyEngine(0)
+t0 = time.perf_counter()
+reqs, idrs, vks = bench.e2e_requests(eng, n, 1000, 43)
+print("built %d requests in %.1f s" % (n, time.perf_counter() - t0), flush=True)
+a = GpuAuthNr(engine=eng)
+for idr, vk in zip(idrs, vks):
+    a.addIdr(idr, vk)
+a.authenticate_batch(reqs[:2048])
+for rep in range(3):
+    t0 = time.perf_counter()
+    res = a.authenticate_batch(reqs)
+    el = time.perf_counter() - t0
+    print("authenticate_batch: %.3f s = %.2f M requests/s, ok %d" % (el, n / el / 1e6,
+                                                                     sum(1 for r in res[:1000] if isinstance(r, str))),
+          flush=True)
+cProfile.run("a.authenticate_batch(reqs)", "/tmp/e2e.prof")
+pstats.Stats("/tmp/e2e.prof").sort_stats("tottime").print_stats(15)
+eng.close()

@@ -16,7 +16,7 @@ class FakeEngine:
     def verify_batch_keyed(self, sig, ids, msgs, off): return np.ones(len(ids), bool)
     def sign_open_batch(self, sm, off, pk): return np.ones(len(off) - 1, bool)
 
-n = 20000
+n = int(os.environ.get("PROF_N", "20000"))
 rng = np.random.default_rng(0)
 pks = [bytes(rng.integers(0,256,32,dtype=np.uint8)) for _ in range(100)]
 msgs_b, kidx, spec = synth.nym_messages(n, pks, alias_len=43)
