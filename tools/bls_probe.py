@@ -14,7 +14,7 @@ from plenum_amd.base58 import b58decode  # noqa: E402
 eng = EdVerifyEngine(0)
 gen = np.frombuffer(b58decode(GENERATOR), np.uint8)
 rng = np.random.default_rng(1)
-for n in (64, 1024, 16384, 65536):
+for n in [int(x) for x in os.environ.get("BLS_SIZES", "64,1024,16384,65536,262144").split(",")]:
     sks = np.frombuffer(b"".join((int.from_bytes(rng.bytes(32), "big") % ORDER).to_bytes(32, "big")
                                  for _ in range(n)), np.uint8).reshape(n, 32)
     t = time.time()
