@@ -191,7 +191,8 @@ EDV_HD void mad_acc5(uint64_t& acc, const uint32_t a[5], const uint32_t b[5]) {
 #ifndef EDV_FE_MUL_ORDER
 #define EDV_FE_MUL_ORDER 2  // 2: -3% comb time vs 0 and 1 (tools/ab_keyed.py)
 #endif
-EDV_HD void fe_mul(fe& h, const fe& f, const fe& g) {
+template <int ORDER>
+EDV_HD void fe_mul_o(fe& h, const fe& f, const fe& g) {
   EDV_ASSERT(EDV_IS_W(f) && EDV_IS_L(g));
   uint32_t g19[10], f2[10];
 #pragma unroll
@@ -199,80 +200,82 @@ EDV_HD void fe_mul(fe& h, const fe& f, const fe& g) {
     g19[k] = 19u * g.v[k];
     f2[k] = (k & 1) ? 2u * f.v[k] : f.v[k];
   }
-#if EDV_FE_MUL_ORDER == 2
-  uint64_t c = 0;
-  uint32_t o[10];  // h may alias f or g
-#pragma unroll
-  for (int k = 0; k < 10; ++k) {
-#if EDV_MAD_CHAIN
-    // the chain starts from the carry of limb k - 1 (one v_mad_u64_u32 per
-    // product, no separate 64-bit add of the carry, which the compiler's
-    // reassociation otherwise emits)
-    uint64_t a = c;
-    uint32_t fa[10], gb[10];
-#pragma unroll
-    for (int i = 0; i < 10; ++i) {
-      const int j = k - i;
-      fa[i] = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
-      gb[i] = j >= 0 ? g.v[j] : g19[j + 10];
-    }
-    mad_acc10(a, fa, gb);
-#else
-    uint64_t a = c;
-#pragma unroll
-    for (int i = 0; i < 10; ++i) {
-      const int j = k - i;
-      const uint32_t fi = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
-      const uint32_t gj = j >= 0 ? g.v[j] : g19[j + 10];
-      a += (uint64_t)fi * gj;
-    }
-#endif
-    o[k] = (uint32_t)a & fe_mask(k);
-    c = a >> fe_width(k);
-  }
-  {
-    const uint64_t t = (uint64_t)o[0] + c * 19u;  // carry out of limb 9 wraps as 19 * 2^0
-    o[0] = (uint32_t)t & M26;
-    o[1] += (uint32_t)(t >> 26);
-  }
-#pragma unroll
-  for (int k = 0; k < 10; ++k) h.v[k] = o[k];
-  return;
-#endif
-  uint64_t acc[10];
-#if EDV_FE_MUL_ORDER == 1
-#pragma unroll
-  for (int k = 0; k < 10; ++k) acc[k] = 0;
-#pragma unroll
-  for (int i = 0; i < 10; ++i) {
+  if constexpr (ORDER == 2) {
+    uint64_t c = 0;
+    uint32_t o[10];  // h may alias f or g
 #pragma unroll
     for (int k = 0; k < 10; ++k) {
-      const int j = k - i;
-      const uint32_t fi = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
-      const uint32_t gj = j >= 0 ? g.v[j] : g19[j + 10];
-      acc[k] += (uint64_t)fi * gj;
-    }
-  }
+#if EDV_MAD_CHAIN
+      // the chain starts from the carry of limb k - 1 (one v_mad_u64_u32 per
+      // product, no separate 64-bit add of the carry, which the compiler's
+      // reassociation otherwise emits)
+      uint64_t a = c;
+      uint32_t fa[10], gb[10];
+#pragma unroll
+      for (int i = 0; i < 10; ++i) {
+        const int j = k - i;
+        fa[i] = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
+        gb[i] = j >= 0 ? g.v[j] : g19[j + 10];
+      }
+      mad_acc10(a, fa, gb);
 #else
+      uint64_t a = c;
 #pragma unroll
-  for (int k = 0; k < 10; ++k) {
-    uint64_t a = 0;
-#pragma unroll
-    for (int i = 0; i < 10; ++i) {
-      const int j = k - i;
-      const uint32_t fi = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
-      const uint32_t gj = j >= 0 ? g.v[j] : g19[j + 10];
-      a += (uint64_t)fi * gj;
-    }
-    acc[k] = a;
-  }
+      for (int i = 0; i < 10; ++i) {
+        const int j = k - i;
+        const uint32_t fi = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
+        const uint32_t gj = j >= 0 ? g.v[j] : g19[j + 10];
+        a += (uint64_t)fi * gj;
+      }
 #endif
-  fe_carry64(h, acc);
+      o[k] = (uint32_t)a & fe_mask(k);
+      c = a >> fe_width(k);
+    }
+    {
+      const uint64_t t = (uint64_t)o[0] + c * 19u;  // carry out of limb 9 wraps as 19 * 2^0
+      o[0] = (uint32_t)t & M26;
+      o[1] += (uint32_t)(t >> 26);
+    }
+#pragma unroll
+    for (int k = 0; k < 10; ++k) h.v[k] = o[k];
+  } else {
+    uint64_t acc[10];
+    if constexpr (ORDER == 1) {
+#pragma unroll
+      for (int k = 0; k < 10; ++k) acc[k] = 0;
+#pragma unroll
+      for (int i = 0; i < 10; ++i) {
+#pragma unroll
+        for (int k = 0; k < 10; ++k) {
+          const int j = k - i;
+          const uint32_t fi = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
+          const uint32_t gj = j >= 0 ? g.v[j] : g19[j + 10];
+          acc[k] += (uint64_t)fi * gj;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 10; ++k) {
+        uint64_t a = 0;
+#pragma unroll
+        for (int i = 0; i < 10; ++i) {
+          const int j = k - i;
+          const uint32_t fi = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
+          const uint32_t gj = j >= 0 ? g.v[j] : g19[j + 10];
+          a += (uint64_t)fi * gj;
+        }
+        acc[k] = a;
+      }
+    }
+    fe_carry64(h, acc);
+  }
 }
+EDV_HD void fe_mul(fe& h, const fe& f, const fe& g) { fe_mul_o<EDV_FE_MUL_ORDER>(h, f, g); }
 
 // h = f^2.  f in L; h in C.  55 multiply-adds.  With EDV_FE_MUL_ORDER 2 the
 // carry of limb k-1 is the initial addend of limb k's chain (as fe_mul).
-EDV_HD void fe_sq(fe& h, const fe& f) {
+template <int ORDER>
+EDV_HD void fe_sq_o(fe& h, const fe& f) {
   EDV_ASSERT(EDV_IS_L(f));
   uint32_t d[10], d2[10], d19[10], d38[10];
 #pragma unroll
@@ -287,7 +290,7 @@ EDV_HD void fe_sq(fe& h, const fe& f) {
   uint32_t o[10];
 #pragma unroll
   for (int k = 0; k < 10; ++k) {
-    uint64_t a = EDV_FE_MUL_ORDER == 2 ? c : 0;
+    uint64_t a = ORDER == 2 ? c : 0;
     uint32_t pa[6], pb[6];
     int np = 0;
 #pragma unroll
@@ -299,7 +302,7 @@ EDV_HD void fe_sq(fe& h, const fe& f) {
         const bool wrap = i + j >= 10;
         const uint32_t fi = (i != j) ? d2[i] : d[i];
         const uint32_t fj = wrap ? (both_odd ? d38[j] : d19[j]) : (both_odd ? d2[j] : d[j]);
-        if (EDV_FE_MUL_ORDER == 2 && EDV_MAD_CHAIN) {
+        if (ORDER == 2 && EDV_MAD_CHAIN) {
           pa[np] = fi;  // carry-started chain, one asm block per limb
           pb[np] = fj;
           ++np;
@@ -308,19 +311,19 @@ EDV_HD void fe_sq(fe& h, const fe& f) {
         }
       }
     }
-    if (EDV_FE_MUL_ORDER == 2 && EDV_MAD_CHAIN) {
+    if (ORDER == 2 && EDV_MAD_CHAIN) {
       if (k & 1)
         mad_acc5(a, pa, pb);
       else
         mad_acc6(a, pa, pb);
     }
     acc[k] = a;
-    if (EDV_FE_MUL_ORDER == 2) {
+    if (ORDER == 2) {
       o[k] = (uint32_t)a & fe_mask(k);
       c = a >> fe_width(k);
     }
   }
-  if (EDV_FE_MUL_ORDER == 2) {
+  if (ORDER == 2) {
     const uint64_t t = (uint64_t)o[0] + c * 19u;
     o[0] = (uint32_t)t & M26;
     o[1] += (uint32_t)(t >> 26);
@@ -330,12 +333,14 @@ EDV_HD void fe_sq(fe& h, const fe& f) {
     fe_carry64(h, acc);
   }
 }
+EDV_HD void fe_sq(fe& h, const fe& f) { fe_sq_o<EDV_FE_MUL_ORDER>(h, f); }
 
 // h = f^(2^n), n >= 1.
+template <int ORDER = EDV_FE_MUL_ORDER>
 EDV_HDNI void fe_sqn(fe& h, const fe& f, int n) {
-  fe_sq(h, f);
+  fe_sq_o<ORDER>(h, f);
 #pragma unroll 1
-  for (int i = 1; i < n; ++i) fe_sq(h, h);
+  for (int i = 1; i < n; ++i) fe_sq_o<ORDER>(h, h);
 }
 
 // One 32-bit carry pass: any class up to 2^31 per limb -> C.
@@ -418,30 +423,33 @@ EDV_HD uint32_t fe_isnegative(const fe& f) {
 }
 
 // z^(2^255 - 21) = z^-1 (ref10 addition chain: 254 squarings, 11 multiplies).
+// ORDER as fe_mul_o: 1 gives ten independent accumulator chains per product
+// (for latency-bound callers at low occupancy, e.g. the batched encode).
+template <int ORDER = EDV_FE_MUL_ORDER>
 EDV_HDNI void fe_invert(fe& out, const fe& z) {
   fe t0, t1, t2, t3;
-  fe_sq(t0, z);
-  fe_sqn(t1, t0, 2);
-  fe_mul(t1, z, t1);
-  fe_mul(t0, t0, t1);
-  fe_sq(t2, t0);
-  fe_mul(t1, t1, t2);
-  fe_sqn(t2, t1, 5);
-  fe_mul(t1, t2, t1);
-  fe_sqn(t2, t1, 10);
-  fe_mul(t2, t2, t1);
-  fe_sqn(t3, t2, 20);
-  fe_mul(t2, t3, t2);
-  fe_sqn(t2, t2, 10);
-  fe_mul(t1, t2, t1);
-  fe_sqn(t2, t1, 50);
-  fe_mul(t2, t2, t1);
-  fe_sqn(t3, t2, 100);
-  fe_mul(t2, t3, t2);
-  fe_sqn(t2, t2, 50);
-  fe_mul(t1, t2, t1);
-  fe_sqn(t1, t1, 5);
-  fe_mul(out, t1, t0);
+  fe_sq_o<ORDER>(t0, z);
+  fe_sqn<ORDER>(t1, t0, 2);
+  fe_mul_o<ORDER>(t1, z, t1);
+  fe_mul_o<ORDER>(t0, t0, t1);
+  fe_sq_o<ORDER>(t2, t0);
+  fe_mul_o<ORDER>(t1, t1, t2);
+  fe_sqn<ORDER>(t2, t1, 5);
+  fe_mul_o<ORDER>(t1, t2, t1);
+  fe_sqn<ORDER>(t2, t1, 10);
+  fe_mul_o<ORDER>(t2, t2, t1);
+  fe_sqn<ORDER>(t3, t2, 20);
+  fe_mul_o<ORDER>(t2, t3, t2);
+  fe_sqn<ORDER>(t2, t2, 10);
+  fe_mul_o<ORDER>(t1, t2, t1);
+  fe_sqn<ORDER>(t2, t1, 50);
+  fe_mul_o<ORDER>(t2, t2, t1);
+  fe_sqn<ORDER>(t3, t2, 100);
+  fe_mul_o<ORDER>(t2, t3, t2);
+  fe_sqn<ORDER>(t2, t2, 50);
+  fe_mul_o<ORDER>(t1, t2, t1);
+  fe_sqn<ORDER>(t1, t1, 5);
+  fe_mul_o<ORDER>(out, t1, t0);
 }
 
 // z^(2^252 - 3) (for square roots; 250 squarings, 11 multiplies).
