@@ -581,10 +581,53 @@ void run_ranges(Py_ssize_t n, int t, F&& f) {  // f(worker, begin, end), t worke
   for (auto& x : th) x.join();
 }
 
+// Scratch kept across calls.  A fresh 1M-request batch would otherwise touch
+// ~600 MB of newly mapped memory per call (page faults on first touch, unmaps
+// on free), which measured ~25 % of the scan.  The scan holds the GIL from
+// start to end, so calls never overlap.
+struct ScanScratch {
+  std::vector<ScanItem> it;
+  std::vector<PyObject*> idr_of;
+  std::vector<ScanBuf> bufs;
+  std::vector<uint64_t> off;
+  std::string fast, shortv;
+  std::vector<uint32_t> uidx;
+};
+ScanScratch& scan_scratch() {
+  static ScanScratch* s = new ScanScratch;  // never destroyed (interpreter teardown order)
+  return *s;
+}
+
+// Output buffer for (5): the caller's bytearray grown to `need` bytes (never
+// shrunk, so its pages stay mapped from call to call), or a fresh bytes object
+// when no bytearray is given or it cannot be resized (a live export).
+PyObject* out_buffer(PyObject* ba, Py_ssize_t need, char** data) {
+  if (ba && PyByteArray_CheckExact(ba)) {
+    if (PyByteArray_GET_SIZE(ba) >= need || PyByteArray_Resize(ba, need) == 0) {
+      Py_INCREF(ba);
+      *data = PyByteArray_AS_STRING(ba);
+      return ba;
+    }
+    PyErr_Clear();
+  }
+  PyObject* b = PyBytes_FromStringAndSize(nullptr, need);
+  if (b) *data = PyBytes_AS_STRING(b);
+  return b;
+}
+
 PyObject* scan_impl(PyObject* args, bool unique_form) {
-  PyObject *msgs, *ignore = Py_None;
+  PyObject *msgs, *ignore = Py_None, *out = Py_None;
   int want_threads = 0;
-  if (!PyArg_ParseTuple(args, "O|Oi", &msgs, &ignore, &want_threads)) return nullptr;
+  if (!PyArg_ParseTuple(args, "O|OiO", &msgs, &ignore, &want_threads, &out)) return nullptr;
+  PyObject *out_sig = nullptr, *out_msg = nullptr;
+  if (out != Py_None) {
+    if (!PyList_CheckExact(out) || PyList_GET_SIZE(out) != 2) {
+      PyErr_SetString(PyExc_TypeError, "out must be a list [bytearray, bytearray]");
+      return nullptr;
+    }
+    out_sig = PyList_GET_ITEM(out, 0);
+    out_msg = PyList_GET_ITEM(out, 1);
+  }
   PyObject* fm = PySequence_Fast(msgs, "msgs must be a sequence");
   if (!fm) return nullptr;
   PyObject* ign = nullptr;
@@ -598,8 +641,11 @@ PyObject* scan_impl(PyObject* args, bool unique_form) {
   static PyObject* k_sig = PyUnicode_InternFromString("signature");
   static PyObject* k_idr = PyUnicode_InternFromString("identifier");
   const Py_ssize_t n = PySequence_Fast_GET_SIZE(fm);
-  std::vector<ScanItem> it((size_t)n);
-  std::vector<PyObject*> idr_of((size_t)n, nullptr);  // borrowed (the dicts hold them)
+  ScanScratch& S = scan_scratch();
+  std::vector<ScanItem>& it = S.it;
+  std::vector<PyObject*>& idr_of = S.idr_of;  // borrowed (the dicts hold them)
+  it.resize((size_t)n);                       // entries reset by the workers
+  idr_of.resize((size_t)n);
   const bool prof = getenv("EDV_SCAN_PROFILE") != nullptr;
   auto now = [] { return std::chrono::steady_clock::now(); };
   auto t_start = now();
@@ -609,7 +655,12 @@ PyObject* scan_impl(PyObject* args, bool unique_form) {
   // Python path), base58 decode, serialization, and the identifier's slot in
   // the worker's own table of distinct identifiers
   const int t = scan_threads(n, want_threads);
-  std::vector<ScanBuf> bufs((size_t)t + 1);  // bufs[t]: items redone under the GIL
+  std::vector<ScanBuf>& bufs = S.bufs;  // bufs[t]: items redone under the GIL
+  if (bufs.size() < (size_t)t + 1) bufs.resize((size_t)t + 1);
+  for (ScanBuf& b : bufs) {
+    b.sig.clear();
+    b.ser.clear();
+  }
   struct IdrTable {
     std::unordered_map<std::string_view, uint32_t> slot;
     std::vector<PyObject*> obj;
@@ -624,6 +675,8 @@ PyObject* scan_impl(PyObject* args, bool unique_form) {
     for (Py_ssize_t i = a; i < b; ++i) {
       PyObject* m = items[i];
       ScanItem& x = it[(size_t)i];
+      x = ScanItem{};
+      idr_of[(size_t)i] = nullptr;
       if (!PyDict_CheckExact(m)) continue;
       PyObject *sv = nullptr, *iv = nullptr, *k, *v;
       Py_ssize_t pos = 0;
@@ -734,8 +787,13 @@ PyObject* scan_impl(PyObject* args, bool unique_form) {
   }
   auto t_p3 = now();
   // (4) crypto_sign_open's split at byte 64: message lengths -> offsets
-  std::string fast((size_t)n, '\0'), shortv((size_t)n, '\0');
-  std::vector<uint64_t> off((size_t)n + 1, 0);
+  std::string& fast = S.fast;
+  std::string& shortv = S.shortv;
+  std::vector<uint64_t>& off = S.off;
+  fast.assign((size_t)n, '\0');
+  shortv.assign((size_t)n, '\0');
+  off.resize((size_t)n + 1);
+  off[0] = 0;
   for (Py_ssize_t i = 0; i < n; ++i) {
     const ScanItem& x = it[(size_t)i];
     uint64_t len = 0;
@@ -750,12 +808,11 @@ PyObject* scan_impl(PyObject* args, bool unique_form) {
     off[(size_t)i + 1] = off[(size_t)i] + len;
   }
   // (5) sig64 and the messages, written by the workers into the result objects
-  PyObject* o_sig = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)n * 64);
-  PyObject* o_msg = o_sig ? PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)off[(size_t)n]) : nullptr;
+  char *dsig = nullptr, *dmsg = nullptr;
+  PyObject* o_sig = out_buffer(out_sig, (Py_ssize_t)n * 64, &dsig);
+  PyObject* o_msg = o_sig ? out_buffer(out_msg, (Py_ssize_t)off[(size_t)n], &dmsg) : nullptr;
   PyObject* ret = nullptr;
   if (o_msg) {
-    char* dsig = PyBytes_AS_STRING(o_sig);
-    char* dmsg = PyBytes_AS_STRING(o_msg);
     run_ranges(n, t, [&](int, Py_ssize_t a, Py_ssize_t b) {
       for (Py_ssize_t i = a; i < b; ++i) {
         const ScanItem& x = it[(size_t)i];
@@ -786,7 +843,8 @@ PyObject* scan_impl(PyObject* args, bool unique_form) {
               n, t, us(t_start, t_p1), us(t_p1, t_p2), us(t_p2, t_p3), us(t_p3, now()));
     }
     if (unique_form) {
-      std::vector<uint32_t> uidx((size_t)n, 0xffffffffu);
+      std::vector<uint32_t>& uidx = S.uidx;
+      uidx.assign((size_t)n, 0xffffffffu);
       for (Py_ssize_t i = 0; i < n; ++i)
         if (it[(size_t)i].state == 1) uidx[(size_t)i] = it[(size_t)i].uid;
       PyObject* ul = PyList_New((Py_ssize_t)uniq.size());
@@ -891,11 +949,12 @@ PyObject* py_gather_items(PyObject*, PyObject* args) {
 
 PyMethodDef kMethods[] = {
     {"scan_batch", py_scan_batch, METH_VARARGS,
-     "scan_batch(msgs, ignore, threads=0) -> (fast, idrs, sig64, msgbuf, off, short): authenticate()'s host steps "
-     "for a batch"},
+     "scan_batch(msgs, ignore, threads=0, out=None) -> (fast, idrs, sig64, msgbuf, off, short): authenticate()'s "
+     "host steps for a batch.  out = [bytearray, bytearray]: sig64 / msgbuf are written into them (grown, never "
+     "shrunk: slice to n * 64 and off[n] bytes) and returned"},
     {"scan_batch_u", py_scan_batch_u, METH_VARARGS,
-     "scan_batch_u(msgs, ignore, threads=0) -> (fast, uidx_u32, uniq, sig64, msgbuf, off, short): scan_batch with "
-     "the identifiers as indices into the batch's distinct identifiers"},
+     "scan_batch_u(msgs, ignore, threads=0, out=None) -> (fast, uidx_u32, uniq, sig64, msgbuf, off, short): "
+     "scan_batch with the identifiers as indices into the batch's distinct identifiers"},
     {"results_from", py_results_from, METH_VARARGS,
      "results_from(codes_u8, uidx_u32, uniq) -> list: uniq[uidx[i]] where codes[i] == 1, else None"},
     {"gather_items", py_gather_items, METH_VARARGS,

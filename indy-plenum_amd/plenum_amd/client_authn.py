@@ -132,6 +132,9 @@ class _GpuState:
         self.pending = OrderedDict()    # addIdr keys waiting for a free slot
         self.hot = OrderedDict()        # keys that earned a slot (hot_key_uses verified requests)
         self.scan_threads = scan_threads  # host threads of the native batch scan (0 = auto)
+        # the scan's sig64 / message output, reused from batch to batch (grown, never shrunk:
+        # fresh buffers cost a page fault per 4 KiB on every batch)
+        self.scan_out = [bytearray(), bytearray()]
         self.stats = {"batches": 0, "batch_items": 0, "cache_hits": 0, "single_verifies": 0, "keyed_items": 0,
                       "keys_registered": 0}
 
@@ -418,7 +421,12 @@ class GpuAuthMixin:
         reference's exception."""
         import numpy as np
         n = len(msgs)
-        fast_b, uidx_b, uniq, sig64, mbuf, off, short = _scan_batch(msgs, [SIG], self._g.scan_threads)
+        g = self._g
+        fast_b, uidx_b, uniq, sig_o, msg_o, off, short = _scan_batch(msgs, [SIG], g.scan_threads, g.scan_out)
+        # views of exactly this batch's bytes (released when the batch returns, so the next
+        # batch may grow the buffers again)
+        sig64 = memoryview(sig_o)[:64 * n]
+        mbuf = memoryview(msg_o)[:int(np.frombuffer(off, np.uint64)[-1])]
         fast = np.frombuffer(fast_b, np.uint8).astype(bool)
         uidx = np.frombuffer(uidx_b, np.uint32)
         ukeys = [self._key_for(idr) for idr in uniq]  # authenticate():93-99, once per identifier

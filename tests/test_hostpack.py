@@ -189,6 +189,30 @@ def test_scan_batch_threads_equal_serial(threads):
     assert len(set(uniq)) == len(uniq)
 
 
+def test_scan_batch_out_buffers_reused():
+    """scan_batch(..., out=[bytearray, bytearray]) (the authenticator's reused
+    output buffers): the same bytes as fresh output in the first n * 64 /
+    off[n] bytes, buffers grown and never shrunk across a large then a small
+    batch, and a buffer with a live export falls back to fresh bytes."""
+    r = random.Random(5)
+    big, small = _scan_pool(r, 2000), _scan_pool(r, 300)
+    out = [bytearray(), bytearray()]
+    for msgs in (big, small, big):
+        want = H.scan_batch_u(msgs, ["signature"], 3)
+        got = H.scan_batch_u(msgs, ["signature"], 3, out)
+        n = len(msgs)
+        end = struct.unpack_from("<Q", want[5], 8 * n)[0]
+        assert got[3] is out[0] and got[4] is out[1]
+        assert bytes(got[3][:64 * n]) == want[3] and bytes(got[4][:end]) == want[4]
+        assert got[:3] == want[:3] and got[5:] == want[5:]
+    assert len(out[0]) >= 64 * len(big)
+    held = memoryview(out[0])  # a live export: out[0] cannot be resized
+    bigger = _scan_pool(r, 2500)
+    got = H.scan_batch_u(bigger, ["signature"], 2, out)
+    assert isinstance(got[3], bytes) and got[3] == H.scan_batch_u(bigger, ["signature"], 2)[3]
+    held.release()
+
+
 def test_results_from():
     codes = bytes([1, 0, 1, 2])
     got = H.results_from(codes, struct.pack("<4I", 1, 0xffffffff, 0, 0), ["a", "b"])
