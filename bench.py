@@ -138,9 +138,18 @@ def time_e2e(eng, reqs, idrs, vks):
         a.addIdr(idr, vk)
     a.authenticate_batch(reqs[:2048])  # first batch registers the addIdr keys (key tables built)
     t0 = time.perf_counter()
-    res = a.authenticate_batch(reqs)
-    total = time.perf_counter() - t0
+    res = a.authenticate_batch(reqs)  # first full-size batch: the scan's reused buffers grow (page faults)
+    first = time.perf_counter() - t0
     ok = sum(1 for r, m in zip(res, reqs) if r == m["identifier"])
+    del res
+    reps = []
+    for _ in range(3):  # steady state: a node authenticates batch after batch
+        t0 = time.perf_counter()
+        res = a.authenticate_batch(reqs)
+        reps.append(time.perf_counter() - t0)
+        assert sum(1 for r, m in zip(res, reqs) if r == m["identifier"]) == ok
+        del res
+    total = sorted(reps)[1]
     from plenum_amd import _hostpack
     t1 = time.perf_counter()
     _hostpack.scan_batch(reqs, ["signature"], 1)
@@ -158,6 +167,7 @@ def time_e2e(eng, reqs, idrs, vks):
     t_ver = time.perf_counter() - t2
     g = a._g
     return {"requests": len(reqs), "value": len(reqs) / total, "seconds": total, "accepted": ok,
+            "first_batch_seconds": first, "first_batch_value": len(reqs) / first,
             "host_scan_us_per_request": t_scan / len(reqs) * 1e6,
             "host_scan_us_per_request_1_thread": t_scan1 / len(reqs) * 1e6,
             "gpu_call_ms": t_ver * 1e3, "gpu_call_rate": len(reqs) / t_ver,
@@ -167,7 +177,9 @@ def time_e2e(eng, reqs, idrs, vks):
                     "requests) while the node thread waits. Breakdown (separate passes): host_scan = "
                     "hostpack.scan_batch (signature/identifier checks, b58decode, serialization, split at byte "
                     "64); gpu_call = edv_verify_batch_keyed on the packed batch (pinned H2D + kernels + D2H); "
-                    "the rest of value's time is per-identifier key resolution and the result list"}
+                    "the rest of value's time is per-identifier key resolution and the result list. value = "
+                    "the median of 3 batches after the first full-size one (steady state); first_batch_* = "
+                    "that first batch, whose scan output buffers are still growing"}
 
 
 def reference_path_baseline(eng, n, host):

@@ -427,12 +427,20 @@ class GpuAuthMixin:
         # batch may grow the buffers again)
         sig64 = memoryview(sig_o)[:64 * n]
         mbuf = memoryview(msg_o)[:int(np.frombuffer(off, np.uint64)[-1])]
-        fast = np.frombuffer(fast_b, np.uint8).astype(bool)
+        fast = np.frombuffer(fast_b, np.uint8).view(bool)
         uidx = np.frombuffer(uidx_b, np.uint32)
         ukeys = [self._key_for(idr) for idr in uniq]  # authenticate():93-99, once per identifier
         # per distinct identifier: 0 = key bytes, 1 = no key (the verify fails), 2 = exception
         ucls = np.fromiter((0 if k.__class__ is bytes else 1 if k is None else 2 for k in ukeys), np.uint8,
                            len(ukeys))
+        if n and fast_b.count(0) == 0 and not (ucls == 2).any():
+            # every item scanned and every identifier resolved (the node's steady state): no index
+            # arrays over the batch
+            ok = self._verify_scanned(None, uidx, ukeys, ucls, sig64, mbuf, off, short)
+            results = _results_from(ok.view(np.uint8).tobytes(), uidx_b, uniq)
+            for i in np.flatnonzero(~ok).tolist():
+                results[i] = InvalidSignature()
+            return results
         fidx = np.nonzero(fast)[0]
         icls = ucls[uidx[fidx]] if len(fidx) else np.zeros(0, np.uint8)
         vidx = fidx[icls != 2]  # the items that reach the verify
@@ -452,14 +460,17 @@ class GpuAuthMixin:
         return results
 
     def _verify_scanned(self, vidx, uidx, ukeys, ucls, sig64, mbuf, off, short):
-        """Verdicts of the scanned items vidx (split sig64 / messages of the
-        whole batch; item i's key = ukeys[uidx[i]]): registered keys on the
-        key-table path, the rest one general launch, no key -> False."""
+        """Verdicts of the scanned items vidx (None: every item; split sig64 /
+        messages of the whole batch; item i's key = ukeys[uidx[i]]): registered
+        keys on the key-table path, the rest one general launch, no key -> False."""
         import numpy as np
         g = self._g
-        m = len(vidx)
-        item_u = uidx[vidx].astype(np.int64)
-        short_a = np.frombuffer(short, np.uint8)[vidx] != 0
+        everything = vidx is None
+        m = len(uidx) if everything else len(vidx)
+        item_u = uidx if everything else uidx[vidx]
+        short_a = np.frombuffer(short, np.uint8).view(bool)
+        if not everything:
+            short_a = short_a[vidx]
         ok = np.zeros(m, bool)
         has_key = np.nonzero(ucls == 0)[0]
         ukey_list = [ukeys[u] for u in has_key.tolist()]
@@ -480,30 +491,39 @@ class GpuAuthMixin:
                 g.pending.clear()
             id_of = {k: i for k, i in zip(uniq_keys, ks.lookup(uniq_keys)) if i is not None}
             kid_u[has_key] = [id_of.get(k, -1) for k in ukey_list]
-        kid = kid_u[item_u]
-        keyed = np.nonzero(kid >= 0)[0]
-        general = np.nonzero(kid == -1)[0]
+        # the items of each path: a whole-batch slice when one path takes them all
+        if (kid_u >= 0).all():
+            groups, general = [(slice(None), True)], np.zeros(0, np.int64)
+        elif (kid_u == -1).all():
+            groups, general = [(slice(None), False)], np.arange(m)
+        else:
+            kid = kid_u[item_u]
+            general = np.nonzero(kid == -1)[0]
+            groups = [(np.nonzero(kid >= 0)[0], True), (general, False)]
         eng = self._engine()
         whole = m == len(uidx)
-        for sel, is_keyed in ((keyed, True), (general, False)):
-            if not len(sel):
+        for sel, is_keyed in groups:
+            cnt = m if isinstance(sel, slice) else len(sel)
+            if not cnt:
                 continue
-            if whole and len(sel) == m:
+            if whole and cnt == m:
                 s_sig, s_msg, s_off = sig64, mbuf, off
             else:
-                s_sig, s_msg, s_off = _gather_items(sig64, mbuf, off, vidx[sel].astype(np.uint32).tobytes())
+                s_sig, s_msg, s_off = _gather_items(sig64, mbuf, off,
+                                                    (np.arange(m) if everything else vidx)[sel].astype(np.uint32)
+                                                    .tobytes())
             s_sig = np.frombuffer(s_sig, np.uint8).reshape(-1, 64)
             s_msg, s_off = np.frombuffer(s_msg, np.uint8), np.frombuffer(s_off, np.uint64)
             if is_keyed:
-                v = eng.verify_batch_keyed(s_sig, kid[sel].astype(np.uint32), s_msg, s_off)
-                g.stats["keyed_items"] += len(sel)
+                v = eng.verify_batch_keyed(s_sig, kid_u.astype(np.uint32)[item_u[sel]], s_msg, s_off)
+                g.stats["keyed_items"] += cnt
             else:
                 ukey_arr = np.zeros((len(ukeys), 32), np.uint8)
                 ukey_arr[has_key] = np.frombuffer(b"".join(ukey_list), np.uint8).reshape(-1, 32)
                 v = eng.verify_batch(s_sig, ukey_arr[item_u[sel]], s_msg, s_off)
             ok[sel] = np.asarray(v, bool)
             g.stats["batches"] += 1
-            g.stats["batch_items"] += len(sel)
+            g.stats["batch_items"] += cnt
         ok &= ~short_a
         if len(general):  # general-path keys earn a slot by verified requests
             verified_u = np.bincount(item_u[general[ok[general]]], minlength=len(ukeys))
