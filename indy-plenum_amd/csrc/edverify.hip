@@ -26,6 +26,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <rocprim/device/device_radix_sort.hpp>
@@ -1391,6 +1392,33 @@ static int launch_verify_keyed(edv_ctx* ctx, const void* d_sig, const void* d_ki
 // on the context stream after the H2D event.  So the CPU copy and H2D of chunk
 // c + 1 run while chunk c's kernels do.  key_bytes: 32 (pk32) or 4 (key ids).
 constexpr uint64_t kHostChunk = 1ull << 18;
+
+// memcpy into the pinned staging on up to 8 host threads (8 MiB or more each):
+// one thread copies a pageable source at ~15 GB/s, below the H2D rate, so a
+// 2^18-request chunk of 200-byte messages (~70 MB) would otherwise take longer
+// to stage than to transfer and verify.
+static void stage_copy(void* dst, const void* src, size_t n) {
+  constexpr size_t kPerThread = 8u << 20;
+  const unsigned hw = std::thread::hardware_concurrency();
+  size_t t = n / kPerThread;
+  if (t > 8) t = 8;
+  if (hw && t > hw) t = hw;
+  if (t <= 1) {
+    memcpy(dst, src, n);
+    return;
+  }
+  const size_t per = (n / t + 63) & ~(size_t)63;
+  std::vector<std::thread> th;
+  th.reserve(t - 1);
+  for (size_t i = 1; i < t; ++i) {
+    const size_t a = i * per, b = (i + 1) * per < n ? (i + 1) * per : n;
+    if (a >= b) break;
+    th.emplace_back([=] { memcpy((char*)dst + a, (const char*)src + a, b - a); });
+  }
+  memcpy(dst, src, per < n ? per : n);
+  for (auto& x : th) x.join();
+}
+
 static int host_verify(edv_ctx* ctx, bool keyed, const uint8_t* sig64, const uint8_t* keys, const uint8_t* msgs,
                        const uint64_t* msg_off, uint64_t n, uint8_t* accept_bits) {
   const uint64_t key_bytes = keyed ? 4 : 32;
@@ -1422,9 +1450,9 @@ static int host_verify(edv_ctx* ctx, bool keyed, const uint8_t* sig64, const uin
       return r;
     uint64_t* off = (uint64_t*)ctx->h_off[sl].p;
     for (uint64_t i = 0; i <= cn; ++i) off[i] = msg_off[c0 + i] - m0;
-    memcpy(ctx->h_sig[sl].p, sig64 + 64 * c0, 64 * cn);
+    stage_copy(ctx->h_sig[sl].p, sig64 + 64 * c0, 64 * cn);
     memcpy(ctx->h_key[sl].p, keys + key_bytes * c0, key_bytes * cn);
-    if (mbytes) memcpy(ctx->h_msg[sl].p, msgs + m0, mbytes);
+    if (mbytes) stage_copy(ctx->h_msg[sl].p, msgs + m0, mbytes);
     set_bucketing(ctx, ctx->bucket_mode == 2 && lengths_mixed(off, cn));
     hipStream_t cs = ctx->stream_copy;
     HIP_TRY(hipMemcpyAsync(ctx->d_sig[sl].p, ctx->h_sig[sl].p, 64 * cn, hipMemcpyHostToDevice, cs));
