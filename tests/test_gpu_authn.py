@@ -150,3 +150,32 @@ def test_multi_engine_one_device(gpu_engine):
         assert rc == rb and c.stats["keyed_items"] == len(reqs)
     finally:
         auto.close()
+
+
+def test_reused_scan_buffers_on_gpu(gpu_engine):
+    """authenticate_batch over a large, a small and a large batch again on one
+    authenticator (the scan writes into the same grown output buffers each
+    time; csrc/hostpack.cpp scan_impl), with different forgeries per batch
+    and one batch that leaves the whole-batch fast path (a request without a
+    signature): every verdict is the construction's."""
+    import copy
+    reqs, rx, idrs, vks, pks, sers, sig = _drain(gpu_engine, n_req=3000, n_nodes=1)
+    a = GpuAuthNr(engine=gpu_engine)
+    for idr, vk in zip(idrs, vks):
+        a.addIdr(idr, vk)
+    base_bad = {i for i in range(3000) if i % 10 == 3}  # forged after signing by _drain
+    for size, extra_bad, drop_sig in ((3000, (7, 2999), None), (500, (11,), 42), (3000, (1, 1500), None)):
+        batch = [copy.deepcopy(r) for r in reqs[:size]]
+        for i in extra_bad:
+            batch[i]["reqId"] += 1
+        if drop_sig is not None:
+            del batch[drop_sig]["signature"]
+        res = a.authenticate_batch(batch)
+        for i, r in enumerate(res):
+            if i == drop_sig:
+                assert type(r).__name__ == "MissingSignature"
+            elif i in base_bad or i in extra_bad:
+                assert type(r).__name__ == "InvalidSignature", (size, i)
+            else:
+                assert r == batch[i]["identifier"], (size, i)
+    assert len(a._g.scan_out[0]) >= 64 * 3000
