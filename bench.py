@@ -378,7 +378,7 @@ def main():
         # Step += unpack bits -> ballot scatter -> RCCL all-reduce(MAX) of the
         # ballots (set union) -> counts + Quorums(25) flags (quorums.py:15-32).
         V = 25
-        n_keys = n * world // 100
+        n_keys = -(-(n // 2) * world // (2 * V))  # every vote g // (2V) has its key (ceil)
         nv = n // 2
         g = np.arange(nv, dtype=np.int64) + rank * nv
         v_key = (g // (2 * V)).astype(np.uint32)
@@ -481,6 +481,16 @@ def main():
     words = d_words.cpu().numpy().view(np.uint64)
     got = np.unpackbits(words.view(np.uint8), bitorder="little")[:n].astype(bool)
     mismatches = int((got != expect).sum())
+    accepted, expected = int(got.sum()), int(expect.sum())
+    gathered_accepted = None
+    if world > 1:  # every rank's parity, and the bitmask as the all-gather delivers it
+        red = torch.tensor([mismatches, accepted, expected], dtype=torch.int64, device=dev)
+        dist.all_reduce(red)
+        mismatches, accepted, expected = (int(x) for x in red.tolist())
+        parts = [torch.empty_like(d_words) for _ in range(world)]
+        dist.all_gather(parts, d_words)
+        gathered_accepted = sum(int(np.unpackbits(t.cpu().numpy().view(np.uint8), bitorder="little")[:n].sum())
+                                for t in parts)
 
     # secondary: the other path on the same resident batch (same verdicts required)
     other = None
@@ -665,7 +675,8 @@ def main():
             "dropin_window": dropin,
             "end_to_end": e2e,
             "cpu_baseline": cpu,
-            "parity": {"mismatches_vs_construction": mismatches, "accepted": int(got.sum()), "expected": int(expect.sum())},
+            "parity": {"mismatches_vs_construction": mismatches, "accepted": accepted, "expected": expected,
+                       "ranks": world, "accepted_in_gathered_bitmask": gathered_accepted},
             "tally": tally_result,
             "collective": collective,
         }

@@ -1,0 +1,45 @@
+"""The N > 1 bench path with the HIP engine on every rank (test_dist_gloo.py
+covers the sharding and collectives with the CPU oracle per rank): two ranks
+of bench.py under torch.distributed.run, gloo, both on cuda:0 (the box's one
+GPU), configs[4]'s step at a small size (160,000 requests per rank: a multiple of 64, and
+of 100 / world so the 3PC keys cover every vote).  The all-gathered bitmask equals the
+construction (every request valid) and the MAX-unioned ballots give the
+expected per-key counts and quorum flags, primary-PREPARE rule included
+(bench.py tally_check)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def test_bench_two_ranks_one_gpu():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--dist-backend", "gloo", "--same-device", "--config", "c4", "--requests", "160000",
+           "--signers", "64", "--key-window", "10", "--steps", "2", "--warmup", "1", "--no-cpu",
+           "--general-steps", "0", "--dropin-steps", "0", "--e2e-n", "0", "--e2e-c0", "0"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="4")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=ROOT, env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-8000:])
+    d = json.loads([x for x in r.stdout.splitlines() if x.startswith('{"metric')][-1])
+    assert d["n_gpus"] == 2 and d["config"]["requests_per_gpu"] == 160000
+    p = d["parity"]
+    assert p["mismatches_vs_construction"] == 0 and p["accepted"] == p["expected"] == 2 * 160000
+    assert p["accepted_in_gathered_bitmask"] == 2 * 160000
+    assert d["tally"]["counts_match"] and d["tally"]["quorum_match"]
+    assert d["tally"]["prepare_quorums"] > 0 and d["tally"]["commit_quorums"] > 0
