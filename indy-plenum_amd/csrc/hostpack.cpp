@@ -597,6 +597,10 @@ ScanScratch& scan_scratch() {
   static ScanScratch* s = new ScanScratch;  // never destroyed (interpreter teardown order)
   return *s;
 }
+// A scan entered while another is still running (only reachable through a
+// finalizer run by a garbage collection inside the outer scan's allocations)
+// gets scratch of its own.
+bool g_scan_busy = false;
 
 // Output buffer for (5): the caller's bytearray grown to `need` bytes (never
 // shrunk, so its pages stay mapped from call to call), or a fresh bytes object
@@ -641,7 +645,13 @@ PyObject* scan_impl(PyObject* args, bool unique_form) {
   static PyObject* k_sig = PyUnicode_InternFromString("signature");
   static PyObject* k_idr = PyUnicode_InternFromString("identifier");
   const Py_ssize_t n = PySequence_Fast_GET_SIZE(fm);
-  ScanScratch& S = scan_scratch();
+  ScanScratch own;
+  ScanScratch& S = g_scan_busy ? own : scan_scratch();
+  struct Busy {
+    bool was;
+    Busy() : was(g_scan_busy) { g_scan_busy = true; }
+    ~Busy() { g_scan_busy = was; }
+  } busy;
   std::vector<ScanItem>& it = S.it;
   std::vector<PyObject*>& idr_of = S.idr_of;  // borrowed (the dicts hold them)
   it.resize((size_t)n);                       // entries reset by the workers
