@@ -558,7 +558,7 @@ struct ScanItem {
   uint32_t sig_len = 0, ser_len = 0;
   uint64_t sig_at = 0, ser_at = 0;
 };
-struct ScanBuf {
+struct alignas(64) ScanBuf {  // one cache line per worker: the string headers change on every append
   std::string sig, ser;
 };
 
@@ -671,7 +671,7 @@ PyObject* scan_impl(PyObject* args, bool unique_form) {
     b.sig.clear();
     b.ser.clear();
   }
-  struct IdrTable {
+  struct alignas(64) IdrTable {  // a cache line (or more) of its own per worker
     std::unordered_map<std::string_view, uint32_t> slot;
     std::vector<PyObject*> obj;
   };
