@@ -173,7 +173,7 @@ def time_e2e(eng, reqs, idrs, vks):
             "gpu_call_ms": t_ver * 1e3, "gpu_call_rate": len(reqs) / t_ver,
             "key_window": g.key_window, "keyed_items_share": g.stats["keyed_items"] / max(1, g.stats["batch_items"]),
             "note": "one Python thread (a Plenum node is single-threaded asyncio); the native scan inside it runs "
-                    "its base58 decode and serialization on up to 16 host threads (scan_threads=0: one per 8k "
+                    "its base58 decode and serialization on up to 16 host threads (scan_threads=0: one per 2k "
                     "requests) while the node thread waits. Breakdown (separate passes): host_scan = "
                     "hostpack.scan_batch (signature/identifier checks, b58decode, serialization, split at byte "
                     "64); gpu_call = edv_verify_batch_keyed on the packed batch (pinned H2D + kernels + D2H); "

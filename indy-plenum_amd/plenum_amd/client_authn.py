@@ -152,7 +152,7 @@ class GpuAuthMixin:
         comb whose max_keys tables fit key_store_bytes, e.g. 16,384 keys in
         32 GiB -> W=10, 1,000 keys -> W=14); max_keys; hot_key_uses;
         scan_threads (host threads of authenticate_batch's native scan, 0 =
-        auto: up to 16, one per 8k requests)."""
+        auto: up to 16, one per 2k requests)."""
         self._edv = _GpuState(engine=engine, device=device, **options)
 
     @property

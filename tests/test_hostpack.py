@@ -183,6 +183,8 @@ def test_scan_batch_threads_equal_serial(threads):
     assert nfast > 1000
     fu, uidx, uniq, *rest = H.scan_batch_u(msgs, ["signature"], threads)
     assert fu == fast and tuple(rest) == (sig64, mbuf, off, short)
+    # distinct identifiers in order of first occurrence, whichever worker took which chunk
+    assert H.scan_batch_u(msgs, ["signature"], 1) == (fu, uidx, uniq, *rest)
     u = struct.unpack("<%dI" % len(msgs), uidx)
     for i in range(len(msgs)):
         assert (uniq[u[i]] == idrs[i]) if fast[i] else u[i] == 0xffffffff
