@@ -135,8 +135,6 @@ class _GpuState:
         # the scan's sig64 / message output, reused from batch to batch (grown, never shrunk:
         # fresh buffers cost a page fault per 4 KiB on every batch)
         self.scan_out = [bytearray(), bytearray()]
-        self.scan_out2 = None  # the second set of a pipelined batch (created on first use)
-        self.pipe_chunk = 1 << 18  # batches of 2 chunks or more: scan of chunk k + 1 || GPU call of chunk k
         self.stats = {"batches": 0, "batch_items": 0, "cache_hits": 0, "single_verifies": 0, "keyed_items": 0,
                       "keys_registered": 0}
 
@@ -420,89 +418,25 @@ class GpuAuthMixin:
         identifier of the batch, one GPU launch per path, the result list built
         natively.  Messages the scan leaves to Python (odd types, missing
         fields, bad base58 ...) go through _prepare, which raises the
-        reference's exception.  Batches of two pipeline chunks or more are
-        scanned chunk by chunk, overlapped with the GPU calls
-        (_authenticate_batch_pipelined)."""
-        g = self._g
-        if len(msgs) >= 2 * g.pipe_chunk and not getattr(self._engine(), "host_threads", False):
-            return self._authenticate_batch_pipelined(msgs)
-        return self._finish_scanned(msgs, _scan_batch(msgs, [SIG], g.scan_threads, g.scan_out))
-
-    def _authenticate_batch_pipelined(self, msgs):
-        """authenticate_batch in chunks of pipe_chunk messages: the native scan
-        of chunk k + 1 runs on a helper thread while this thread waits in the
-        engine call of chunk k (ctypes releases the GIL there; the scan holds
-        it from start to end, so the helper is released by `go` right before
-        the engine call, once this thread's Python work for chunk k is done).
-        Two sets of scan output buffers alternate between the chunks.  The
-        results are those of the unchunked batch (verkeys resolved once per
-        identifier across the chunks)."""
-        import threading
-        g = self._g
-        if g.scan_out2 is None:
-            g.scan_out2 = [bytearray(), bytearray()]
-        outs = (g.scan_out, g.scan_out2)
-        n, step = len(msgs), g.pipe_chunk
-        chunks = [msgs[a:a + step] for a in range(0, n, step)]
-        key_cache = {}
-        results = []
-        sc = _scan_batch(chunks[0], [SIG], g.scan_threads, outs[0])
-        for k, chunk in enumerate(chunks):
-            nxt, go, th = {}, None, None
-            if k + 1 < len(chunks):
-                go = threading.Event()
-
-                def scan_next(k1=k + 1, go=go, nxt=nxt):
-                    go.wait()
-                    try:
-                        nxt["sc"] = _scan_batch(chunks[k1], [SIG], g.scan_threads, outs[k1 % 2])
-                    except BaseException as e:  # re-raised on this thread
-                        nxt["err"] = e
-
-                th = threading.Thread(target=scan_next, name="edv-scan", daemon=True)
-                th.start()
-            try:
-                results.extend(self._finish_scanned(chunk, sc, key_cache, go.set if go is not None else None))
-            finally:
-                if th is not None:
-                    go.set()  # (no engine call in a chunk without verifiable items)
-                    th.join()
-            if th is not None:
-                if "err" in nxt:
-                    raise nxt["err"]
-                sc = nxt["sc"]
-        return results
-
-    def _finish_scanned(self, msgs, sc, key_cache=None, before_verify=None):
-        """The rest of authenticate_batch after the scan sc of msgs: verkeys,
-        the verify (before_verify() right before the first engine call), the
-        result list.  key_cache: identifier -> _key_for result across the
-        chunks of one batch."""
+        reference's exception."""
         import numpy as np
         n = len(msgs)
-        fast_b, uidx_b, uniq, sig_o, msg_o, off, short = sc
+        g = self._g
+        fast_b, uidx_b, uniq, sig_o, msg_o, off, short = _scan_batch(msgs, [SIG], g.scan_threads, g.scan_out)
         # views of exactly this batch's bytes (released when the batch returns, so the next
         # batch may grow the buffers again)
         sig64 = memoryview(sig_o)[:64 * n]
         mbuf = memoryview(msg_o)[:int(np.frombuffer(off, np.uint64)[-1])]
         fast = np.frombuffer(fast_b, np.uint8).view(bool)
         uidx = np.frombuffer(uidx_b, np.uint32)
-        if key_cache is None:
-            ukeys = [self._key_for(idr) for idr in uniq]  # authenticate():93-99, once per identifier
-        else:
-            ukeys = []
-            for idr in uniq:
-                k = key_cache.get(idr, key_cache)
-                if k is key_cache:
-                    k = key_cache[idr] = self._key_for(idr)
-                ukeys.append(k)
+        ukeys = [self._key_for(idr) for idr in uniq]  # authenticate():93-99, once per identifier
         # per distinct identifier: 0 = key bytes, 1 = no key (the verify fails), 2 = exception
         ucls = np.fromiter((0 if k.__class__ is bytes else 1 if k is None else 2 for k in ukeys), np.uint8,
                            len(ukeys))
         if n and fast_b.count(0) == 0 and not (ucls == 2).any():
             # every item scanned and every identifier resolved (the node's steady state): no index
             # arrays over the batch
-            ok = self._verify_scanned(None, uidx, ukeys, ucls, sig64, mbuf, off, short, before_verify)
+            ok = self._verify_scanned(None, uidx, ukeys, ucls, sig64, mbuf, off, short)
             results = _results_from(ok.view(np.uint8).tobytes(), uidx_b, uniq)
             for i in np.flatnonzero(~ok).tolist():
                 results[i] = InvalidSignature()
@@ -511,8 +445,8 @@ class GpuAuthMixin:
         icls = ucls[uidx[fidx]] if len(fidx) else np.zeros(0, np.uint8)
         vidx = fidx[icls != 2]  # the items that reach the verify
         codes = np.zeros(n, np.uint8)
-        ok = self._verify_scanned(vidx, uidx, ukeys, ucls, sig64, mbuf, off, short, before_verify) \
-            if len(vidx) else np.zeros(0, bool)
+        ok = self._verify_scanned(vidx, uidx, ukeys, ucls, sig64, mbuf, off, short) if len(vidx) else \
+            np.zeros(0, bool)
         codes[vidx[ok]] = 1
         results = _results_from(codes.tobytes(), uidx_b, uniq)  # the identifier where verified
         for i in vidx[~ok].tolist():
@@ -525,7 +459,7 @@ class GpuAuthMixin:
                 results[i] = r
         return results
 
-    def _verify_scanned(self, vidx, uidx, ukeys, ucls, sig64, mbuf, off, short, before_verify=None):
+    def _verify_scanned(self, vidx, uidx, ukeys, ucls, sig64, mbuf, off, short):
         """Verdicts of the scanned items vidx (None: every item; split sig64 /
         messages of the whole batch; item i's key = ukeys[uidx[i]]): registered
         keys on the key-table path, the rest one general launch, no key -> False."""
@@ -580,8 +514,6 @@ class GpuAuthMixin:
                                                     .tobytes())
             s_sig = np.frombuffer(s_sig, np.uint8).reshape(-1, 64)
             s_msg, s_off = np.frombuffer(s_msg, np.uint8), np.frombuffer(s_off, np.uint64)
-            if before_verify is not None:
-                before_verify()
             if is_keyed:
                 v = eng.verify_batch_keyed(s_sig, kid_u.astype(np.uint32)[item_u[sel]], s_msg, s_off)
                 g.stats["keyed_items"] += cnt

@@ -29,10 +29,6 @@ def shard_bounds(n, world, rank):
 
 
 class MultiEngine:
-    # its calls run Python on per-device threads: the authenticator does not overlap them with
-    # a native scan that holds the GIL (client_authn._authenticate_batch_pipelined)
-    host_threads = True
-
     def __init__(self, devices=None, engines=None, min_shard=4096):
         """devices: device indices ("all" / None = every visible device);
         engines: ready engines (e.g. test doubles) instead.  Batches smaller

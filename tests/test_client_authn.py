@@ -373,14 +373,3 @@ def test_scanned_batch_fuzz(oracle):
                 want.append(_outcome(ex))
         assert got == want
         assert sum(isinstance(x, str) for x in got) > 10
-        # the pipelined form (scan of chunk k + 1 overlapped with the engine call of chunk k):
-        # chunks of 7 -> 9 chunks, a partial last one; alternating output buffer sets
-        eng = OracleEngine(oracle)
-        c = GpuAuthNr(engine=eng, max_keys=max_keys)
-        for idr, vk in zip(idrs, vks):
-            c.addIdr(idr, vk)
-        c._g.pipe_chunk = 7
-        calls = eng.calls
-        assert [_outcome(r) for r in c.authenticate_batch(pool)] == want
-        assert eng.calls - calls >= 9 and c._g.scan_out2 is not None
-        assert [_outcome(r) for r in c.authenticate_batch(pool[:20])] == want[:20]
