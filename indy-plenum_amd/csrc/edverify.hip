@@ -21,8 +21,6 @@
 #include <hip/hip_runtime.h>
 
 #include <mutex>
-#include <pthread.h>
-#include <sched.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -1399,9 +1397,6 @@ constexpr uint64_t kHostChunk = 1ull << 18;
 // one thread copies a pageable source at ~15 GB/s, below the H2D rate, so a
 // 2^18-request chunk of 200-byte messages (~70 MB) would otherwise take longer
 // to stage than to transfer and verify.
-// The copy threads are pinned to their own CPUs (the calling thread's CPU's
-// successors in the affinity mask): short-lived threads otherwise start next to
-// the spawning thread and share its CPU.
 static void stage_copy(void* dst, const void* src, size_t n) {
   constexpr size_t kPerThread = 8u << 20;
   const unsigned hw = std::thread::hardware_concurrency();
@@ -1412,14 +1407,6 @@ static void stage_copy(void* dst, const void* src, size_t n) {
     memcpy(dst, src, n);
     return;
   }
-  std::vector<int> cpus;
-  cpu_set_t set;
-  if (sched_getaffinity(0, sizeof set, &set) == 0)
-    for (int c = 0; c < CPU_SETSIZE; ++c)
-      if (CPU_ISSET(c, &set)) cpus.push_back(c);
-  size_t at = 0;
-  const int cur = sched_getcpu();
-  while (at < cpus.size() && cpus[at] != cur) ++at;
   const size_t per = (n / t + 63) & ~(size_t)63;
   std::vector<std::thread> th;
   th.reserve(t - 1);
@@ -1427,12 +1414,6 @@ static void stage_copy(void* dst, const void* src, size_t n) {
     const size_t a = i * per, b = (i + 1) * per < n ? (i + 1) * per : n;
     if (a >= b) break;
     th.emplace_back([=] { memcpy((char*)dst + a, (const char*)src + a, b - a); });
-    if (!cpus.empty()) {
-      cpu_set_t one;
-      CPU_ZERO(&one);
-      CPU_SET(cpus[(at + i) % cpus.size()], &one);
-      (void)pthread_setaffinity_np(th.back().native_handle(), sizeof one, &one);  // best effort
-    }
   }
   memcpy(dst, src, per < n ? per : n);
   for (auto& x : th) x.join();
