@@ -590,13 +590,16 @@ std::vector<int> worker_cpus(int t) {
 }
 
 // Host workers of the scan and the pack: the calling thread (worker 0, left
-// where it is) plus t - 1 new threads, each pinned to its own CPU
-// (worker_cpus; EDV_SCAN_PIN=0: not pinned).  A new thread starts next to the
-// thread that spawned it and the scheduler spreads short-lived threads only
-// after milliseconds: on an 8-CPU host 2 and 4 unpinned workers ran no faster
-// than 1, pinned ones 2.0x and 4.1x.  Items go out in chunks of kScanChunk
-// from a shared counter, so a worker whose CPU is busy with other work takes
-// fewer.  f(worker, begin, end) per chunk.
+// where it is) plus t - 1 new threads.  EDV_SCAN_PIN=1 pins each new thread
+// to its own CPU (worker_cpus): a new thread starts next to the thread that
+// spawned it and the scheduler spreads short-lived threads only after
+// milliseconds, so on a dedicated 8-CPU host 2 and 4 unpinned workers ran no
+// faster than 1 and pinned ones 2.0x and 4.1x; on the shared GPU box
+// (16-CPU quota out of 256 CPUs) unpinned workers were faster (1M requests end
+// to end 17.7-19.7 vs 15.3-16.5 M/s pinned: the scheduler finds idle CPUs), so
+// pinning is off by default.  Items go out in chunks of kScanChunk from a
+// shared counter, so a worker whose CPU is busy with other work takes fewer.
+// f(worker, begin, end) per chunk.
 constexpr Py_ssize_t kScanChunk = 1024;
 template <class F>
 void run_chunks(Py_ssize_t n, int t, F&& f) {
@@ -613,7 +616,7 @@ void run_chunks(Py_ssize_t n, int t, F&& f) {
     }
   };
   const char* pin_env = getenv("EDV_SCAN_PIN");
-  const std::vector<int> cpus = (pin_env && pin_env[0] == '0') ? std::vector<int>() : worker_cpus(t);
+  const std::vector<int> cpus = (pin_env && pin_env[0] == '1') ? worker_cpus(t) : std::vector<int>();
   std::vector<std::thread> th;
   th.reserve((size_t)t);
   for (int w = 1; w < t; ++w) {
