@@ -101,6 +101,19 @@ def test_b58decode_native():
         assert H.b58decode(bad) is None
 
 
+def test_b58decode_every_length():
+    """Random base58 strings of every length 0..130 (the native decoder takes
+    its independent-products path up to 90 digits, Horner passes beyond),
+    with and without leading '1's (zero bytes), against the Python decoder."""
+    from plenum_amd.base58 import alphabet as ALPHABET
+    r = random.Random(8)
+    for n in range(131):
+        for lead in (0, 1, 3):
+            s = "1" * lead + "".join(r.choice(ALPHABET) for _ in range(n))
+            assert H.b58decode(s) == b58decode_py(s), s
+        assert H.b58decode("z" * n) == b58decode_py("z" * n)  # the largest value of each length
+
+
 def test_pack_split64_is_crypto_sign_open_split():
     r = random.Random(4)
     for _ in range(200):
