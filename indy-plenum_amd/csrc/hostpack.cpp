@@ -24,6 +24,7 @@
 #include <Python.h>
 #include <pthread.h>
 #include <sched.h>
+#include <unistd.h>
 
 #include <stdint.h>
 #include <stdio.h>
@@ -31,6 +32,9 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <charconv>
 #include <chrono>
 #include <string>
@@ -590,7 +594,7 @@ std::vector<int> worker_cpus(int t) {
 }
 
 // Host workers of the scan and the pack: the calling thread (worker 0, left
-// where it is) plus t - 1 new threads.  EDV_SCAN_PIN=1 pins each new thread
+// where it is) plus t - 1 pool threads (ScanPool).  EDV_SCAN_PIN=1 pins each helper
 // to its own CPU (worker_cpus): a new thread starts next to the thread that
 // spawned it and the scheduler spreads short-lived threads only after
 // milliseconds, so on a dedicated 8-CPU host 2 and 4 unpinned workers ran no
@@ -601,6 +605,78 @@ std::vector<int> worker_cpus(int t) {
 // shared counter, so a worker whose CPU is busy with other work takes fewer.
 // f(worker, begin, end) per chunk.
 constexpr Py_ssize_t kScanChunk = 1024;
+
+// Helper threads kept from call to call (the scan's workers 1..t-1; the caller
+// is worker 0): asleep on a condition variable between calls, so a call wakes
+// threads the scheduler has already spread over the CPUs instead of creating
+// threads next to the caller.  A child process after fork() (which has none
+// of the parent's threads) builds a pool of its own.
+class ScanPool {
+ public:
+  // f(w) for w in [1, t) on the helpers while the caller runs f(0); returns
+  // when every f has returned.
+  void run(int t, const std::function<void(int)>& f) {
+    std::unique_lock<std::mutex> lk(mu_);
+    while ((int)th_.size() < t - 1) {
+      const int w = (int)th_.size() + 1;
+      th_.emplace_back([this, w, seen = gen_] { helper(w, seen); });
+      const char* pin_env = getenv("EDV_SCAN_PIN");
+      if (pin_env && pin_env[0] == '1') {
+        const std::vector<int> cpus = worker_cpus(w + 1);
+        if ((size_t)w < cpus.size()) {
+          cpu_set_t one;
+          CPU_ZERO(&one);
+          CPU_SET(cpus[(size_t)w], &one);
+          (void)pthread_setaffinity_np(th_.back().native_handle(), sizeof one, &one);  // best effort
+        }
+      }
+    }
+    job_ = &f;
+    active_ = t;
+    pending_ = t - 1;
+    ++gen_;
+    lk.unlock();
+    cv_work_.notify_all();
+    f(0);
+    lk.lock();
+    cv_done_.wait(lk, [this] { return pending_ == 0; });
+    job_ = nullptr;
+  }
+  static ScanPool& get() {
+    static ScanPool* pool = nullptr;
+    static pid_t owner = 0;
+    if (!pool || owner != getpid()) {  // (after fork the old pool's threads do not exist: leak it)
+      pool = new ScanPool;
+      owner = getpid();
+    }
+    return *pool;
+  }
+
+ private:
+  void helper(int w, uint64_t seen) {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_work_.wait(lk, [&] { return gen_ != seen; });
+      seen = gen_;
+      if (w >= active_) continue;
+      const std::function<void(int)>* f = job_;
+      lk.unlock();
+      (*f)(w);
+      lk.lock();
+      if (--pending_ == 0) cv_done_.notify_one();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_work_, cv_done_;
+  std::vector<std::thread> th_;  // never joined: the helpers live as long as the process
+  const std::function<void(int)>* job_ = nullptr;
+  uint64_t gen_ = 0;
+  int active_ = 0, pending_ = 0;
+};
+
+// f(worker, begin, end) per chunk of kScanChunk items, chunks taken from a
+// shared counter by the caller and t - 1 pool helpers, so a worker whose CPU
+// is busy with other work takes fewer.
 template <class F>
 void run_chunks(Py_ssize_t n, int t, F&& f) {
   if (t <= 1 || n <= kScanChunk) {
@@ -608,28 +684,14 @@ void run_chunks(Py_ssize_t n, int t, F&& f) {
     return;
   }
   std::atomic<Py_ssize_t> next{0};
-  auto body = [&](int w) {
+  const std::function<void(int)> body = [&](int w) {
     for (;;) {
       const Py_ssize_t a = next.fetch_add(kScanChunk, std::memory_order_relaxed);
       if (a >= n) break;
       f(w, a, std::min(n, a + kScanChunk));
     }
   };
-  const char* pin_env = getenv("EDV_SCAN_PIN");
-  const std::vector<int> cpus = (pin_env && pin_env[0] == '1') ? worker_cpus(t) : std::vector<int>();
-  std::vector<std::thread> th;
-  th.reserve((size_t)t);
-  for (int w = 1; w < t; ++w) {
-    th.emplace_back(body, w);
-    if ((size_t)w < cpus.size()) {
-      cpu_set_t one;
-      CPU_ZERO(&one);
-      CPU_SET(cpus[(size_t)w], &one);
-      (void)pthread_setaffinity_np(th.back().native_handle(), sizeof one, &one);  // best effort
-    }
-  }
-  body(0);
-  for (auto& x : th) x.join();
+  ScanPool::get().run(t, body);
 }
 
 // Scratch kept across calls.  A fresh 1M-request batch would otherwise touch
