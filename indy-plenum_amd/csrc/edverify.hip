@@ -35,6 +35,7 @@
 
 #include "../../include/edverify.h"
 #include "edv_internal.h"
+#include "host_pool.h"
 #include "batch_encode.h"
 #include "comb.h"
 #include "sha256.h"
@@ -1393,10 +1394,11 @@ static int launch_verify_keyed(edv_ctx* ctx, const void* d_sig, const void* d_ki
 // c + 1 run while chunk c's kernels do.  key_bytes: 32 (pk32) or 4 (key ids).
 constexpr uint64_t kHostChunk = 1ull << 18;
 
-// memcpy into the pinned staging on up to 8 host threads (8 MiB or more each):
-// one thread copies a pageable source at ~15 GB/s, below the H2D rate, so a
-// 2^18-request chunk of 200-byte messages (~70 MB) would otherwise take longer
-// to stage than to transfer and verify.
+// memcpy into the pinned staging on up to 8 host threads (8 MiB or more each;
+// the caller and pooled helpers, host_pool.h): one thread copies a pageable
+// source at ~15 GB/s, below the H2D rate, so a 2^18-request chunk of 200-byte
+// messages (~70 MB) would otherwise take longer to stage than to transfer and
+// verify.
 static void stage_copy(void* dst, const void* src, size_t n) {
   constexpr size_t kPerThread = 8u << 20;
   const unsigned hw = std::thread::hardware_concurrency();
@@ -1408,15 +1410,10 @@ static void stage_copy(void* dst, const void* src, size_t n) {
     return;
   }
   const size_t per = (n / t + 63) & ~(size_t)63;
-  std::vector<std::thread> th;
-  th.reserve(t - 1);
-  for (size_t i = 1; i < t; ++i) {
-    const size_t a = i * per, b = (i + 1) * per < n ? (i + 1) * per : n;
-    if (a >= b) break;
-    th.emplace_back([=] { memcpy((char*)dst + a, (const char*)src + a, b - a); });
-  }
-  memcpy(dst, src, per < n ? per : n);
-  for (auto& x : th) x.join();
+  HostPool::get().run((int)t, [&](int w) {
+    const size_t a = (size_t)w * per, b = ((size_t)w + 1) * per < n ? ((size_t)w + 1) * per : n;
+    if (a < b) memcpy((char*)dst + a, (const char*)src + a, b - a);
+  });
 }
 
 static int host_verify(edv_ctx* ctx, bool keyed, const uint8_t* sig64, const uint8_t* keys, const uint8_t* msgs,

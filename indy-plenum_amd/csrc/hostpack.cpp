@@ -22,6 +22,8 @@
 //   pack_sm(sigs, sers, keys) -> (sm, off, pk32)   (edv_sign_open_batch layout)
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
+
+#include "host_pool.h"
 #include <pthread.h>
 #include <sched.h>
 #include <unistd.h>
@@ -576,25 +578,8 @@ int scan_threads(Py_ssize_t n, int want) {
   return (int)std::max<Py_ssize_t>(1, std::min<Py_ssize_t>({(Py_ssize_t)(hc ? hc : 1), (Py_ssize_t)16, by_size}));
 }
 
-// CPUs for t workers: the calling thread's CPU, then the next t - 1 CPUs of
-// the process's affinity mask (wrapping).
-std::vector<int> worker_cpus(int t) {
-  std::vector<int> all, out;
-  cpu_set_t set;
-  if (sched_getaffinity(0, sizeof set, &set) == 0)
-    for (int c = 0; c < CPU_SETSIZE; ++c)
-      if (CPU_ISSET(c, &set)) all.push_back(c);
-  if (all.empty()) return out;
-  const int cur = sched_getcpu();
-  size_t at = 0;
-  while (at < all.size() && all[at] != cur) ++at;
-  if (at == all.size()) at = 0;
-  for (int w = 0; w < t; ++w) out.push_back(all[(at + (size_t)w) % all.size()]);
-  return out;
-}
-
 // Host workers of the scan and the pack: the calling thread (worker 0, left
-// where it is) plus t - 1 pool threads (ScanPool).  EDV_SCAN_PIN=1 pins each helper
+// where it is) plus t - 1 pool threads (host_pool.h).  EDV_SCAN_PIN=1 pins each helper
 // to its own CPU (worker_cpus): a new thread starts next to the thread that
 // spawned it and the scheduler spreads short-lived threads only after
 // milliseconds, so on a dedicated 8-CPU host 2 and 4 unpinned workers ran no
@@ -605,74 +590,6 @@ std::vector<int> worker_cpus(int t) {
 // shared counter, so a worker whose CPU is busy with other work takes fewer.
 // f(worker, begin, end) per chunk.
 constexpr Py_ssize_t kScanChunk = 1024;
-
-// Helper threads kept from call to call (the scan's workers 1..t-1; the caller
-// is worker 0): asleep on a condition variable between calls, so a call wakes
-// threads the scheduler has already spread over the CPUs instead of creating
-// threads next to the caller.  A child process after fork() (which has none
-// of the parent's threads) builds a pool of its own.
-class ScanPool {
- public:
-  // f(w) for w in [1, t) on the helpers while the caller runs f(0); returns
-  // when every f has returned.
-  void run(int t, const std::function<void(int)>& f) {
-    std::unique_lock<std::mutex> lk(mu_);
-    while ((int)th_.size() < t - 1) {
-      const int w = (int)th_.size() + 1;
-      th_.emplace_back([this, w, seen = gen_] { helper(w, seen); });
-      const char* pin_env = getenv("EDV_SCAN_PIN");
-      if (pin_env && pin_env[0] == '1') {
-        const std::vector<int> cpus = worker_cpus(w + 1);
-        if ((size_t)w < cpus.size()) {
-          cpu_set_t one;
-          CPU_ZERO(&one);
-          CPU_SET(cpus[(size_t)w], &one);
-          (void)pthread_setaffinity_np(th_.back().native_handle(), sizeof one, &one);  // best effort
-        }
-      }
-    }
-    job_ = &f;
-    active_ = t;
-    pending_ = t - 1;
-    ++gen_;
-    lk.unlock();
-    cv_work_.notify_all();
-    f(0);
-    lk.lock();
-    cv_done_.wait(lk, [this] { return pending_ == 0; });
-    job_ = nullptr;
-  }
-  static ScanPool& get() {
-    static ScanPool* pool = nullptr;
-    static pid_t owner = 0;
-    if (!pool || owner != getpid()) {  // (after fork the old pool's threads do not exist: leak it)
-      pool = new ScanPool;
-      owner = getpid();
-    }
-    return *pool;
-  }
-
- private:
-  void helper(int w, uint64_t seen) {
-    std::unique_lock<std::mutex> lk(mu_);
-    for (;;) {
-      cv_work_.wait(lk, [&] { return gen_ != seen; });
-      seen = gen_;
-      if (w >= active_) continue;
-      const std::function<void(int)>* f = job_;
-      lk.unlock();
-      (*f)(w);
-      lk.lock();
-      if (--pending_ == 0) cv_done_.notify_one();
-    }
-  }
-  std::mutex mu_;
-  std::condition_variable cv_work_, cv_done_;
-  std::vector<std::thread> th_;  // never joined: the helpers live as long as the process
-  const std::function<void(int)>* job_ = nullptr;
-  uint64_t gen_ = 0;
-  int active_ = 0, pending_ = 0;
-};
 
 // f(worker, begin, end) per chunk of kScanChunk items, chunks taken from a
 // shared counter by the caller and t - 1 pool helpers, so a worker whose CPU
@@ -691,7 +608,7 @@ void run_chunks(Py_ssize_t n, int t, F&& f) {
       f(w, a, std::min(n, a + kScanChunk));
     }
   };
-  ScanPool::get().run(t, body);
+  HostPool::get().run(t, body);
 }
 
 // Scratch kept across calls.  A fresh 1M-request batch would otherwise touch
