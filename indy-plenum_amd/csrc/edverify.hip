@@ -150,7 +150,7 @@ __device__ __forceinline__ void load_words(uint32_t* dst, const uint8_t* src, in
 // register budget; intermediates are SoA in the context scratch).
 
 #ifndef EDV_HASH_MIN_WAVES
-#define EDV_HASH_MIN_WAVES 4  // 115 VGPRs since the branch-free schedule (sha512.h)
+#define EDV_HASH_MIN_WAVES 4  // 94 VGPRs = 5 waves / SIMD; 6 (80 VGPRs + 36 B spill) measured no faster (profiles/r03a_ab_hash_occupancy)
 #endif
 
 // Length buckets: the lanes of a wave should hash messages of equal SHA-512
