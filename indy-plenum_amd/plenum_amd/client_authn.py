@@ -45,6 +45,7 @@ message from Node.verifySignature, node.py:2294-2318):
 authenticators (names from BASELINE.json's north star).
 """
 import copy
+import threading
 from abc import abstractmethod
 from collections import OrderedDict
 from copy import deepcopy
@@ -135,6 +136,9 @@ class _GpuState:
         # the scan's sig64 / message output, reused from batch to batch (grown, never shrunk:
         # fresh buffers cost a page fault per 4 KiB on every batch)
         self.scan_out = [bytearray(), bytearray()]
+        # held while a batch uses scan_out (scan through verify): a batch from another thread
+        # meanwhile gets fresh buffers instead of overwriting bytes the first one's GPU call reads
+        self.scan_out_lock = threading.Lock()
         self.stats = {"batches": 0, "batch_items": 0, "cache_hits": 0, "single_verifies": 0, "keyed_items": 0,
                       "keys_registered": 0}
 
@@ -419,10 +423,19 @@ class GpuAuthMixin:
         natively.  Messages the scan leaves to Python (odd types, missing
         fields, bad base58 ...) go through _prepare, which raises the
         reference's exception."""
+        g = self._g
+        mine = g.scan_out_lock.acquire(blocking=False)
+        try:
+            return self._authenticate_batch_scanned_into(msgs, g.scan_out if mine else None)
+        finally:
+            if mine:
+                g.scan_out_lock.release()
+
+    def _authenticate_batch_scanned_into(self, msgs, out):
         import numpy as np
         n = len(msgs)
         g = self._g
-        fast_b, uidx_b, uniq, sig_o, msg_o, off, short = _scan_batch(msgs, [SIG], g.scan_threads, g.scan_out)
+        fast_b, uidx_b, uniq, sig_o, msg_o, off, short = _scan_batch(msgs, [SIG], g.scan_threads, out)
         # views of exactly this batch's bytes (released when the batch returns, so the next
         # batch may grow the buffers again)
         sig64 = memoryview(sig_o)[:64 * n]

@@ -327,6 +327,27 @@ def test_scanned_batch_equals_single_on_kats(oracle):
         assert got == want
 
 
+def test_scan_buffers_not_shared_by_concurrent_batches(oracle):
+    """While one batch holds the authenticator's reused scan buffers (scan
+    through GPU call), a batch from another thread gets fresh buffers, and
+    both are right."""
+    idrs, vks, msgs = _signed(2, 30, seed=4)
+    a = GpuAuthNr(engine=OracleEngine(oracle))
+    for idr, vk in zip(idrs, vks):
+        a.addIdr(idr, vk)
+    want = [_outcome(r) for r in a.authenticate_batch(msgs)]
+    used = len(a._g.scan_out[0])
+    assert used >= 64 * len(msgs) and all(isinstance(x, str) for x in want)
+    a._g.scan_out[0][:] = b"\0" * used  # what a first batch's GPU call would still be reading
+    assert a._g.scan_out_lock.acquire(blocking=False)  # that first batch
+    try:
+        assert [_outcome(r) for r in a.authenticate_batch(msgs)] == want
+        assert bytes(a._g.scan_out[0]) == b"\0" * used  # untouched
+    finally:
+        a._g.scan_out_lock.release()
+    assert [_outcome(r) for r in a.authenticate_batch(msgs)] == want
+
+
 def test_scanned_batch_fuzz(oracle):
     """Random request dicts (valid, tampered, odd field types, missing / empty
     fields, non-base58, short signatures): scanned batch == per-message."""
