@@ -800,10 +800,7 @@ PyObject* scan_impl(PyObject* args, bool unique_form) {
       to_global[(size_t)c.w][c.local] = ins.first->second;
     }
   }
-  for (Py_ssize_t i = 0; i < n; ++i) {
-    ScanItem& x = it[(size_t)i];
-    if (x.state == 1) x.uid = to_global[x.buf][x.uid];
-  }
+  // (the items' worker-local ids are mapped in (4), on the workers)
   auto t_p2 = now();
   // (3) the items the workers left (non-ASCII identifiers, floats / big ints /
   // wide-kind keys in the payload), redone under the GIL
@@ -848,27 +845,49 @@ PyObject* scan_impl(PyObject* args, bool unique_form) {
     }
   }
   auto t_p3 = now();
-  // (4) crypto_sign_open's split at byte 64: message lengths -> offsets
+  // (4) on the workers, per item: the fast / short flags, the batch-wide
+  // identifier id, crypto_sign_open's split at byte 64 (message length);
+  // offsets by a prefix sum over the kScanChunk chunks (chunk sums, a short
+  // serial pass over them, then each chunk's offsets)
   std::string& fast = S.fast;
   std::string& shortv = S.shortv;
   std::vector<uint64_t>& off = S.off;
-  fast.assign((size_t)n, '\0');
-  shortv.assign((size_t)n, '\0');
+  std::vector<uint32_t>& uidx = S.uidx;
+  fast.resize((size_t)n);
+  shortv.resize((size_t)n);
   off.resize((size_t)n + 1);
   off[0] = 0;
-  for (Py_ssize_t i = 0; i < n; ++i) {
-    const ScanItem& x = it[(size_t)i];
-    uint64_t len = 0;
-    if (x.state == 1) {
-      fast[(size_t)i] = 1;
-      const uint64_t ls = x.sig_len, lm = x.ser_len;
-      if (ls + lm < 64)
-        shortv[(size_t)i] = 1;  // crypto_sign_open: smlen < 64 rejects
-      else
-        len = ls + lm - 64;
+  if (unique_form) uidx.resize((size_t)n);
+  std::vector<uint64_t> csum((size_t)((n + kScanChunk - 1) / kScanChunk) + 1, 0);
+  run_chunks(n, t, [&](int, Py_ssize_t a, Py_ssize_t b) {
+    uint64_t sum = 0;
+    for (Py_ssize_t i = a; i < b; ++i) {
+      const ScanItem& x = it[(size_t)i];
+      uint64_t len = 0;
+      uint32_t u = 0xffffffffu;
+      char f = 0, sh = 0;
+      if (x.state == 1) {
+        f = 1;
+        u = x.buf < t ? to_global[x.buf][x.uid] : x.uid;  // bufs[t]: redone under the GIL, id already global
+        const uint64_t ls = x.sig_len, lm = x.ser_len;
+        if (ls + lm < 64)
+          sh = 1;  // crypto_sign_open: smlen < 64 rejects
+        else
+          len = ls + lm - 64;
+      }
+      fast[(size_t)i] = f;
+      shortv[(size_t)i] = sh;
+      if (unique_form) uidx[(size_t)i] = u;
+      off[(size_t)i + 1] = len;
+      sum += len;
     }
-    off[(size_t)i + 1] = off[(size_t)i] + len;
-  }
+    csum[(size_t)(a / kScanChunk) + 1] = sum;  // (one call over [0, n) when not chunked: csum[1])
+  });
+  for (size_t c = 1; c < csum.size(); ++c) csum[c] += csum[c - 1];
+  run_chunks(n, t, [&](int, Py_ssize_t a, Py_ssize_t b) {
+    uint64_t at = csum[(size_t)(a / kScanChunk)];
+    for (Py_ssize_t i = a; i < b; ++i) off[(size_t)i + 1] = at += off[(size_t)i + 1];
+  });
   // (5) sig64 and the messages, written by the workers into the result objects
   char *dsig = nullptr, *dmsg = nullptr;
   PyObject* o_sig = out_buffer(out_sig, (Py_ssize_t)n * 64, &dsig);
@@ -905,10 +924,6 @@ PyObject* scan_impl(PyObject* args, bool unique_form) {
               n, t, us(t_start, t_p1), us(t_p1, t_p2), us(t_p2, t_p3), us(t_p3, now()));
     }
     if (unique_form) {
-      std::vector<uint32_t>& uidx = S.uidx;
-      uidx.assign((size_t)n, 0xffffffffu);
-      for (Py_ssize_t i = 0; i < n; ++i)
-        if (it[(size_t)i].state == 1) uidx[(size_t)i] = it[(size_t)i].uid;
       PyObject* ul = PyList_New((Py_ssize_t)uniq.size());
       if (ul) {
         for (size_t u = 0; u < uniq.size(); ++u) {
