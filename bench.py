@@ -645,8 +645,13 @@ def main():
                 mlen_mean, args.signers,
                 ", 10% corrupted/non-canonical/small-order" if args.config == "c2" else ", all valid",
                 req_desc + (" + PREPARE/COMMIT tally of %d keys x 25 validators in the step (RCCL all-reduce MAX "
-                            "of the ballots)" % (n * world // 100) if args.config == "c4" else "")),
-                       "requests_per_gpu": n, "signers": args.signers, "parallelism": "dp%d (request-index shards)" % world},
+                            "of the ballots)" % (-(-(n // 2) * world // 50)) if args.config == "c4" else "")),
+                       "requests_per_gpu": n, "signers": args.signers, "parallelism": "dp%d (request-index shards)" % world,
+                       "path": ("keyed: the signers' verkeys registered once (comb tables of key window %d, base "
+                                "window %d), inputs HBM-resident; the drop-in's own window and its end-to-end rate "
+                                "are the dropin_window / end_to_end fields" % (args.key_window, RL.BASE_W)
+                                if args.path == "keyed" else
+                                "general: every request carries its key bytes, inputs HBM-resident")},
             "roofline": {"bound": "valu", "kernel": kernel_name, "achieved": achieved, "peak": peak,
                          "unit": "TMAD/s", "frac": achieved / peak, "traffic": traffic,
                          "algorithmic": "%d MAD per verify (%s), %d launches per chunk of %d requests (n=%d each; "
