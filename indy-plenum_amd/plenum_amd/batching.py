@@ -4,36 +4,66 @@ Reference: ZStack.processReceived (stp_zmq/zstack.py:528-549) pops
 (json_text, ident) pairs from rxMsgs -- up to LISTENER_MESSAGE_QUOTA = 100 per
 listener per cycle (plenum/config.py:179) -- and hands each to the node, which
 authenticates client REQUESTs (node.py:1439-1440) and the request inside each
-PROPAGATE (node.py:1313-1316, 2304-2306) one at a time.  `requests_in_drain`
-pulls those requests out of a drain so one GPU batch (`prefetch`) covers them;
-the unchanged per-message authenticate() then hits the verdict cache."""
+PROPAGATE (node.py:1313-1316, 2304-2306) one at a time.
+
+Under load the node-to-node traffic does not arrive as bare messages: a
+sender's outbox of more than one message is flushed as ONE signed BATCH
+(Batched.flushOutBoxes -> _make_batch, plenum/common/batched.py:99-125,
+141-144; Batch = {"op": "BATCH", "messages": [serialized message, ...],
+"signature": ...}, node_messages.py:30-36), kept whole by doProcessReceived
+(batched.py:149-162, which only drops pings / pongs) and unpacked by
+Node.unpackNodeMsg, which deserializes every entry of `messages` with
+nodestack.deserializeMsg and re-enters handleOneNodeMsg for it
+(node.py:1333-1337).  So the n - 1 PROPAGATE copies of a request mostly sit
+INSIDE BATCH entries.  `requests_in_drain` descends into them the same way, so
+one GPU batch (`prefetch`) covers client REQUESTs, bare PROPAGATEs and batched
+PROPAGATEs alike; the unchanged per-message authenticate() then hits the
+verdict cache."""
 import json
 
 PROPAGATE = "PROPAGATE"
+BATCH = "BATCH"
+_MAX_BATCH_DEPTH = 2  # the reference never nests batches; bounded anyway
+
+
+def _decode(raw, deserialize):
+    try:
+        return deserialize(raw) if isinstance(raw, (str, bytes)) else raw
+    except Exception:
+        return None
+
+
+def _collect(m, deserialize, out, depth):
+    if not isinstance(m, dict):
+        return
+    op = m.get("op")
+    if op == BATCH:  # node.py:1333-1337: each entry re-enters handleOneNodeMsg
+        inner = m.get("messages")
+        if depth < _MAX_BATCH_DEPTH and isinstance(inner, list):
+            for raw in inner:
+                _collect(_decode(raw, deserialize), deserialize, out, depth + 1)
+        return
+    if op == PROPAGATE:
+        m = m.get("request")
+        if not isinstance(m, dict):
+            return
+    if "signature" in m:
+        out.append(m)
 
 
 def requests_in_drain(raw_msgs, deserialize=json.loads, limit=None):
     """Signed request dicts inside a list of raw rxMsgs entries
-    ((text, ident) pairs or bare texts): client requests themselves and the
-    `request` of PROPAGATE messages.  Undecodable entries are skipped (the
-    reference logs and drops them, zstack.py:541-545)."""
+    ((text, ident) pairs or bare texts): client requests themselves, the
+    `request` of PROPAGATE messages, and both of those inside BATCH messages.
+    `limit` counts rxMsgs entries (a BATCH is one entry, as in
+    processReceived).  Undecodable entries are skipped (the reference logs and
+    drops them, zstack.py:541-545)."""
     out = []
     for n, item in enumerate(raw_msgs):
         if limit is not None and n >= limit:
             break
         raw = item[0] if isinstance(item, tuple) else item
-        try:
-            m = deserialize(raw) if isinstance(raw, (str, bytes)) else raw
-        except Exception:
-            continue
-        if not isinstance(m, dict):
-            continue
-        if m.get("op") == PROPAGATE:
-            m = m.get("request")
-            if not isinstance(m, dict):
-                continue
-        if "signature" in m:
-            out.append(m)
+        _collect(_decode(raw, deserialize), deserialize, out, 0)
     return out
 
 
@@ -45,11 +75,34 @@ def prefetch_drain(authnr, raw_msgs, deserialize=json.loads, limit=None):
 
 class VerifyAheadMixin:
     """Mix in front of a ZStack subclass (e.g. plenum.common.stacks.ClientZStack
-    / NodeZStack) constructed with `authnr=<GpuAuthMixin instance>`."""
+    / NodeZStack).  The authenticator is the class attribute `authnr`
+    (verify_ahead_stack binds it) or a constructor keyword `authnr=`."""
 
     authnr = None
+
+    def __init__(self, *args, authnr=None, **kwargs):
+        if authnr is not None:
+            self.authnr = authnr
+        super().__init__(*args, **kwargs)
 
     def processReceived(self, limit):
         if self.authnr is not None and limit > 0:
             prefetch_drain(self.authnr, list(self.rxMsgs), self.deserializeMsg, limit)
         return super().processReceived(limit)
+
+
+_stack_classes = {}
+
+
+def verify_ahead_stack(base, authnr):
+    """A subclass of the stack class `base` whose processReceived prefetches
+    for `authnr`: what a Node subclass returns from its nodeStackClass /
+    clientStackClass properties (node.py:536-541; the node constructs its
+    stacks as cls(**kwargs) at node.py:182-196, after clientAuthNr is set at
+    :168), see INTEGRATION.md section 4."""
+    key = (base, id(authnr))
+    cls = _stack_classes.get(key)
+    if cls is None or cls.authnr is not authnr:
+        cls = type("VerifyAhead" + base.__name__, (VerifyAheadMixin, base), {"authnr": authnr})
+        _stack_classes[key] = cls
+    return cls

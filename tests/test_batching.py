@@ -46,3 +46,54 @@ def test_verify_ahead_mixin_prefetches_then_processes():
     assert st.processReceived(2) == 2
     assert st.authnr.batches == [[req, req]]
     assert prefetch_drain(st.authnr, st.rxMsgs) == 3
+
+
+def _batch(msgs):
+    """A node's flushed outbox as the reference frames it: Batched._make_batch
+    (plenum/common/batched.py:141-144) wraps the already-serialized messages in
+    Batch(msgs, None) (node_messages.py:30-36), serialized by ZStack.serializeMsg."""
+    return json.dumps({"op": "BATCH", "messages": [json.dumps(m) for m in msgs], "signature": None})
+
+
+def test_requests_inside_batch_messages():
+    """node.py:1333-1337: each entry of a BATCH re-enters handleOneNodeMsg, so
+    PROPAGATEs inside a BATCH are authenticated like bare ones."""
+    r1 = {"identifier": "a", "reqId": 1, "operation": {"type": "1"}, "signature": "s1"}
+    r2 = {"identifier": "b", "reqId": 2, "operation": {"type": "1"}, "signature": "s2"}
+    prop = [{"op": "PROPAGATE", "request": r, "senderClient": "c"} for r in (r1, r2)]
+    other = {"op": "PREPARE", "instId": 0, "viewNo": 0, "ppSeqNo": 1}
+    drain = [(json.dumps(r1), b"c1"),
+             (_batch([prop[0], other, prop[1]]), b"Node2"),
+             (json.dumps({"op": "BATCH", "messages": ["not json", json.dumps(prop[1])], "signature": None}), b"N3"),
+             (json.dumps({"op": "BATCH", "messages": "oops", "signature": None}), b"N4"),
+             (json.dumps({"op": "BATCH", "messages": [_batch([prop[0]])], "signature": None}), b"N5")]
+    assert requests_in_drain(drain) == [r1, r1, r2, r2, r1]
+    # a BATCH is one rxMsgs entry for processReceived's limit
+    assert requests_in_drain(drain, limit=2) == [r1, r1, r2]
+    # bytes entries (the wire form) decode like str ones
+    assert requests_in_drain([(_batch(prop).encode(), b"n")], deserialize=lambda m: json.loads(m)) == [r1, r2]
+
+
+def test_verify_ahead_stack_binds_authenticator():
+    """verify_ahead_stack(base, authnr): the class a Node subclass returns from
+    nodeStackClass / clientStackClass (node.py:536-541); the node constructs it
+    as cls(**kwargs) (node.py:182-196)."""
+    from plenum_amd.batching import verify_ahead_stack
+
+    class Base(_Stack):
+        def __init__(self, msgs=(), **kw):
+            _Stack.__init__(self, msgs)
+            self.kw = kw
+
+    auth = _Auth()
+    cls = verify_ahead_stack(Base, auth)
+    assert verify_ahead_stack(Base, auth) is cls and issubclass(cls, Base)
+    req = {"identifier": "a", "signature": "s"}
+    st = cls(msgs=[(_batch([{"op": "PROPAGATE", "request": req}] * 2), b"n")], stackParams={"name": "x"})
+    assert st.kw == {"stackParams": {"name": "x"}}
+    st.processReceived(100)
+    assert auth.batches == [[req, req]]
+    other = _Auth()
+    st2 = verify_ahead_stack(Base, auth)(msgs=[(json.dumps(req), 1)], authnr=other)
+    st2.processReceived(1)
+    assert other.batches == [[req]] and len(auth.batches) == 1

@@ -127,6 +127,48 @@ def test_verify_ahead_drain_on_gpu(gpu_engine, oracle):
     assert eng.launches == 1 and a.stats["single_verifies"] == 0 and a.stats["cache_hits"] == 100
 
 
+def test_verify_ahead_batch_framed_drain_on_gpu(gpu_engine, oracle):
+    """The drain as it looks under load: 100 client REQUESTs plus, from each of
+    the 24 other nodes, ONE BATCH message wrapping that node's serialized
+    PROPAGATEs (Batched.flushOutBoxes -> _make_batch, batched.py:99-125,
+    141-144) interleaved with a 3PC message, unpacked by the node with
+    nodestack.deserializeMsg per entry (node.py:1333-1337).  One engine
+    launch, 0 single verifies, verdicts == the oracle's."""
+    import json
+    from plenum_amd.batching import prefetch_drain
+    reqs, _rx, idrs, vks, pks, sers, sig = _drain(gpu_engine, n_nodes=1)
+    rx = [(json.dumps(r), b"client%d" % i) for i, r in enumerate(reqs)]
+    for node in range(1, 25):
+        inner = []
+        for i, r in enumerate(reqs):
+            inner.append(json.dumps({"op": "PROPAGATE", "request": r, "senderClient": "client%d" % i}))
+            if i % 25 == 0:
+                inner.append(json.dumps({"op": "PREPARE", "instId": 0, "viewNo": 0, "ppSeqNo": i}))
+        rx.append((json.dumps({"op": "BATCH", "messages": inner, "signature": None}).encode(), b"Node%d" % node))
+    eng = _Counting(gpu_engine)
+    a = GpuAuthNr(engine=eng)
+    for idr, vk in zip(idrs, vks):
+        a.addIdr(idr, vk)
+    assert prefetch_drain(a, rx) == 100
+    assert eng.launches == 1 and a.stats["keyed_items"] == 100
+    # the requests as the node authenticates them after unpacking one node's BATCH
+    unpacked = [json.loads(m) for m in json.loads(rx[100 + 5][0])["messages"]]
+    props = [m["request"] for m in unpacked if m["op"] == "PROPAGATE"]
+    assert len(props) == 100
+    for i, r in enumerate(reqs):
+        ser = sers[i] if i % 10 != 3 else None
+        want = ser is not None and oracle.oracle_verify_detached(sig[i].tobytes(), ser, len(ser),
+                                                                 pks[i % 10].tobytes()) == 0
+        for m in (r, props[i]):
+            if want:
+                assert a.authenticate(m) == r["identifier"]
+            else:
+                with pytest.raises(Exception) as ei:
+                    a.authenticate(m)
+                assert type(ei.value).__name__ == "InvalidSignature"
+    assert eng.launches == 1 and a.stats["single_verifies"] == 0 and a.stats["cache_hits"] == 200
+
+
 def test_multi_engine_one_device(gpu_engine):
     """The single-process multi-GPU path with the devices of this box (one
     here): MultiEngine through the authenticator == the plain engine."""
