@@ -1000,12 +1000,18 @@ EDV_BN_NI void final_exp(fp12& r, const fp12& f) {
   fp12_mul(r, res, y);
 }
 
-// e(sig, gen) == e(H, vk)  <=>  FE(ML(sig, gen) * ML(-H, vk)) == 1;
-// an infinite point contributes 1 (its Miller function is constant).
+// e(sig, gen) == e(H, vk)  <=>  FE(ML(sig, gen) * ML(-H, vk)) == 1.
+// A signature, (summed) verkey or generator at infinity never verifies: its
+// pairing is 1, so an all-zero or off-curve signature with an empty or
+// infinite verkey sum would otherwise pass as 1 == 1 -- a forged state-root
+// multi-signature with participants = [] (bls_bft_replica_plenum.py:159-172
+// drops participants without a key and checks no count).  What AMCL returns
+// for these inputs is not pinned by any fixture; rejecting is the safe side.
 EDV_BN_NI bool bls_check(const g1& sig, const g1& H, const g2& vk, const g2& gen) {
+  if (g1_isinf(sig) || g2_isinf(vk) || g2_isinf(gen)) return false;
   fp12 f;
   fp12_one(f);
-  if (!g1_isinf(sig) && !g2_isinf(gen)) {
+  {
     fp x, y;
     fp2 qx, qy;
     g1_affine(x, y, sig);

@@ -15,6 +15,7 @@
 #include <unistd.h>
 
 #include <condition_variable>
+#include <exception>
 #include <cstdint>
 #include <functional>
 #include <mutex>
@@ -46,22 +47,48 @@ inline std::vector<int> worker_cpus(int t) {
 class HostPool {
  public:
   // f(w) for w in [1, t) on the helpers while the caller runs f(0); returns
-  // when every f has returned.
+  // when every f has returned.  An exception thrown by any f (e.g. bad_alloc
+  // from a worker's buffer growth) is caught where it is thrown, every helper
+  // is still waited for, and the first one is rethrown on the caller -- so no
+  // helper calls std::terminate and the caller never unwinds while helpers
+  // still run the job.
   // A call while another is running (engines of several devices staging at
   // once) runs on threads of its own.
   void run(int t, const std::function<void(int)>& f) {
+    std::exception_ptr err;
+    std::mutex err_mu;
+    const std::function<void(int)> g = [&](int w) {
+      try {
+        f(w);
+      } catch (...) {
+        std::lock_guard<std::mutex> l(err_mu);
+        if (!err) err = std::current_exception();
+      }
+    };
     std::unique_lock<std::mutex> busy(run_mu_, std::try_to_lock);
     if (!busy.owns_lock()) {
       std::vector<std::thread> th;
-      for (int w = 1; w < t; ++w) th.emplace_back(f, w);
-      f(0);
+      for (int w = 1; w < t; ++w) {
+        try {
+          th.emplace_back(g, w);
+        } catch (...) {  // no thread: run its share here
+          g(w);
+        }
+      }
+      g(0);
       for (auto& x : th) x.join();
+      if (err) std::rethrow_exception(err);
       return;
     }
     std::unique_lock<std::mutex> lk(mu_);
     while ((int)th_.size() < t - 1) {
       const int w = (int)th_.size() + 1;
-      th_.emplace_back([this, w, seen = gen_] { helper(w, seen); });
+      try {
+        th_.emplace_back([this, w, seen = gen_] { helper(w, seen); });
+      } catch (...) {
+        t = w;  // fewer helpers: workers 0..w-1 (run_chunks' shared counter covers every item)
+        break;
+      }
       const char* pin_env = getenv("EDV_SCAN_PIN");
       if (pin_env && pin_env[0] == '1') {
         const std::vector<int> cpus = worker_cpus(w + 1);
@@ -73,16 +100,18 @@ class HostPool {
         }
       }
     }
-    job_ = &f;
+    job_ = &g;
     active_ = t;
     pending_ = t - 1;
     ++gen_;
     lk.unlock();
     cv_work_.notify_all();
-    f(0);
+    g(0);
     lk.lock();
     cv_done_.wait(lk, [this] { return pending_ == 0; });
     job_ = nullptr;
+    lk.unlock();
+    if (err) std::rethrow_exception(err);
   }
   static HostPool& get() {
     static std::mutex m;

@@ -649,7 +649,21 @@ PyObject* out_buffer(PyObject* ba, Py_ssize_t need, char** data) {
   return b;
 }
 
-PyObject* scan_impl(PyObject* args, bool unique_form) {
+// Owned references released on every exit, an exception's unwinding included.
+struct PyRefs {
+  PyObject* fm = nullptr;
+  PyObject* ign = nullptr;
+  PyObject* o_sig = nullptr;
+  PyObject* o_msg = nullptr;
+  ~PyRefs() {
+    Py_XDECREF(o_sig);
+    Py_XDECREF(o_msg);
+    Py_XDECREF(fm);
+    Py_XDECREF(ign);
+  }
+};
+
+PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
   PyObject *msgs, *ignore = Py_None, *out = Py_None;
   int want_threads = 0;
   if (!PyArg_ParseTuple(args, "O|OiO", &msgs, &ignore, &want_threads, &out)) return nullptr;
@@ -662,15 +676,12 @@ PyObject* scan_impl(PyObject* args, bool unique_form) {
     out_sig = PyList_GET_ITEM(out, 0);
     out_msg = PyList_GET_ITEM(out, 1);
   }
-  PyObject* fm = PySequence_Fast(msgs, "msgs must be a sequence");
+  PyObject* fm = refs.fm = PySequence_Fast(msgs, "msgs must be a sequence");
   if (!fm) return nullptr;
   PyObject* ign = nullptr;
   if (ignore != Py_None) {
-    ign = PySequence_Fast(ignore, "ignore must be a sequence");
-    if (!ign) {
-      Py_DECREF(fm);
-      return nullptr;
-    }
+    ign = refs.ign = PySequence_Fast(ignore, "ignore must be a sequence");
+    if (!ign) return nullptr;
   }
   static PyObject* k_sig = PyUnicode_InternFromString("signature");
   static PyObject* k_idr = PyUnicode_InternFromString("identifier");
@@ -890,8 +901,8 @@ PyObject* scan_impl(PyObject* args, bool unique_form) {
   });
   // (5) sig64 and the messages, written by the workers into the result objects
   char *dsig = nullptr, *dmsg = nullptr;
-  PyObject* o_sig = out_buffer(out_sig, (Py_ssize_t)n * 64, &dsig);
-  PyObject* o_msg = o_sig ? out_buffer(out_msg, (Py_ssize_t)off[(size_t)n], &dmsg) : nullptr;
+  PyObject* o_sig = refs.o_sig = out_buffer(out_sig, (Py_ssize_t)n * 64, &dsig);
+  PyObject* o_msg = refs.o_msg = o_sig ? out_buffer(out_msg, (Py_ssize_t)off[(size_t)n], &dmsg) : nullptr;
   PyObject* ret = nullptr;
   if (o_msg) {
     run_chunks(n, t, [&](int, Py_ssize_t a, Py_ssize_t b) {
@@ -949,11 +960,25 @@ PyObject* scan_impl(PyObject* args, bool unique_form) {
       }
     }
   }
-  Py_XDECREF(o_sig);
-  Py_XDECREF(o_msg);
-  Py_DECREF(fm);
-  Py_XDECREF(ign);
   return ret;
+}
+
+// No C++ exception reaches the interpreter: a worker's bad_alloc (buffers of a
+// very large batch) becomes MemoryError once every worker has stopped
+// (HostPool::run rethrows on the caller only after the helpers are done).
+PyObject* scan_impl(PyObject* args, bool unique_form) {
+  PyRefs refs;
+  try {
+    return scan_impl_body(args, unique_form, refs);
+  } catch (const std::bad_alloc&) {
+    return PyErr_NoMemory();
+  } catch (const std::exception& e) {
+    PyErr_Format(PyExc_RuntimeError, "scan_batch: %s", e.what());
+    return nullptr;
+  } catch (...) {
+    PyErr_SetString(PyExc_RuntimeError, "scan_batch: native error");
+    return nullptr;
+  }
 }
 
 PyObject* py_scan_batch(PyObject*, PyObject* args) { return scan_impl(args, false); }

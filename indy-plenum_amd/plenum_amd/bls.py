@@ -148,6 +148,8 @@ class BlsCryptoVerifierGpu(BlsCryptoVerifier):
             keys = [_point128(GpuBlsUtils.bls_from_str(p)) for p in pks]
             if s is None or any(k is None for k in keys):
                 continue  # bls_from_str returned None: False (:61-66, :73-80)
+            if not keys:
+                continue  # no verkeys: the sum is infinity, never verifies (bn254.h bls_check)
             sigs.append(s)
             msgs.append(bytes(message_bytes(msg)))
             vks.extend(keys)

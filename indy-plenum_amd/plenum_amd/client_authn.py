@@ -114,6 +114,27 @@ class _Prepared:
         self.identifier, self.sig, self.ser, self.key = identifier, sig, ser, key
 
 
+_LOCKS_LOCK = threading.Lock()
+
+
+def _engine_lock(eng):
+    """One re-entrant lock per engine, shared by every authenticator on it:
+    held from key routing (KeyStore lookup / register, whose evictions rebuild
+    slots) through the verify launch, so a batch on another thread can neither
+    rebind a key id this batch already resolved nor share the engine's
+    staging buffers and stream with it.  (The reference is single-threaded
+    asyncio, looper.py:141-151; this makes concurrent callers safe, not
+    parallel.)"""
+    lk = getattr(eng, "_authn_lock", None)
+    if lk is None:
+        with _LOCKS_LOCK:
+            lk = getattr(eng, "_authn_lock", None)
+            if lk is None:
+                lk = threading.RLock()
+                eng._authn_lock = lk
+    return lk
+
+
 class _GpuState:
     """Per-authenticator GPU state (created on first use)."""
 
@@ -134,11 +155,9 @@ class _GpuState:
         self.hot = OrderedDict()        # keys that earned a slot (hot_key_uses verified requests)
         self.scan_threads = scan_threads  # host threads of the native batch scan (0 = auto)
         # the scan's sig64 / message output, reused from batch to batch (grown, never shrunk:
-        # fresh buffers cost a page fault per 4 KiB on every batch)
+        # fresh buffers cost a page fault per 4 KiB on every batch); a batch holds the engine
+        # lock (_engine_lock) from the scan through the verify, so no other batch writes them
         self.scan_out = [bytearray(), bytearray()]
-        # held while a batch uses scan_out (scan through verify): a batch from another thread
-        # meanwhile gets fresh buffers instead of overwriting bytes the first one's GPU call reads
-        self.scan_out_lock = threading.Lock()
         self.stats = {"batches": 0, "batch_items": 0, "cache_hits": 0, "single_verifies": 0, "keyed_items": 0,
                       "keys_registered": 0}
 
@@ -362,6 +381,10 @@ class GpuAuthMixin:
         """GPU launches over prepared items (crypto_sign_open semantics): items
         whose key is registered take the key-table path, the rest one general
         launch; items without a usable key are False without touching the GPU."""
+        with _engine_lock(self._engine()):
+            return self._verify_many_locked(prepared)
+
+    def _verify_many_locked(self, prepared):
         g = self._g
         todo = [p for p in prepared if p.key]
         out = {}
@@ -387,9 +410,16 @@ class GpuAuthMixin:
     def authenticate_batch(self, msgs, identifiers=None, signatures=None):
         """Per message: the identifier authenticate() would return, or the
         exception instance it would raise (same class, args and __cause__)."""
-        if _scan_batch is not None and not identifiers and not signatures:
+        if _scan_batch is not None and not identifiers and not signatures and self._native_host_steps():
             return self._authenticate_batch_scanned(msgs)
         return self._authenticate_batch_each(msgs, identifiers, signatures)
+
+    def _native_host_steps(self):
+        """The native scan restates GpuAuthMixin._prepare / serializeForSig;
+        a subclass that overrides either keeps its own (per-message) path, so
+        authenticate() and authenticate_batch() always agree."""
+        cls = type(self)
+        return cls.serializeForSig is GpuAuthMixin.serializeForSig and cls._prepare is GpuAuthMixin._prepare
 
     def _key_for(self, identifier):
         """getVerkey + DidVerifier for one identifier (authenticate()'s
@@ -419,17 +449,13 @@ class GpuAuthMixin:
         _hostpack.scan_batch_u over the dicts (signature / identifier checks,
         b58decode, serialization, crypto_sign_open's split at byte 64, on
         scan_threads host threads), the verkey resolved once per distinct
-        identifier of the batch, one GPU launch per path, the result list built
+        identifier of the batch (getVerkey is called once per identifier, not
+        once per message), one GPU launch per path, the result list built
         natively.  Messages the scan leaves to Python (odd types, missing
         fields, bad base58 ...) go through _prepare, which raises the
         reference's exception."""
-        g = self._g
-        mine = g.scan_out_lock.acquire(blocking=False)
-        try:
-            return self._authenticate_batch_scanned_into(msgs, g.scan_out if mine else None)
-        finally:
-            if mine:
-                g.scan_out_lock.release()
+        with _engine_lock(self._engine()):
+            return self._authenticate_batch_scanned_into(msgs, self._g.scan_out)
 
     def _authenticate_batch_scanned_into(self, msgs, out):
         import numpy as np

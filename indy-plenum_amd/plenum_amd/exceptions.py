@@ -13,6 +13,10 @@ to the authenticate_multi extension, which the reference snapshot does not
 have (parity unpinned); they derive from SigningException either
 way."""
 
+import re
+
+_NODE_NAME = re.compile(r'(\b\w+)(:(\d+))?')  # exceptions.py:125 ("Alpha-1:9701" -> "Alpha")
+
 _NAMES = ("ReqInfo", "BaseExc", "SigningException", "CouldNotAuthenticate", "MissingSignature", "EmptySignature",
           "InvalidSignatureFormat", "InvalidSignature", "MissingIdentifier", "EmptyIdentifier",
           "UnknownIdentifier", "InvalidIdentifier", "InvalidKey", "SuspiciousNode")
@@ -67,10 +71,14 @@ if not REFERENCE:
 
         def __init__(self, node, suspicion, offendingMsg):
             node = node.decode() if isinstance(node, bytes) else node
-            self.code = getattr(suspicion, "code", None) if suspicion else None
-            self.reason = getattr(suspicion, "reason", None) if suspicion else None
-            self.node = node.split(":", 1)[0]
+            self.code = suspicion.code if suspicion else None
+            self.reason = suspicion.reason if suspicion else None
+            m = _NODE_NAME.match(node)
+            self.node = m.groups()[0] if m else node
             self.offendingMsg = offendingMsg
+
+        def __repr__(self):
+            return "Error code: {}. {}".format(self.code, self.reason)
 
 
 # --- authenticate_multi extension (not in the reference snapshot) ----------

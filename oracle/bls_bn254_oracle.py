@@ -403,8 +403,13 @@ def aggregate(sigs):
 
 
 def verify(sig, msg, vk, gen=None):
-    """Bls.verify: e(sig, g) == e(H(m), vk)."""
+    """Bls.verify: e(sig, g) == e(H(m), vk).  A signature, verkey (sum) or
+    generator at infinity is rejected (the product's policy, bn254.h
+    bls_check: 1 == 1 would accept a forged multi-signature with no
+    participants; AMCL's own answer for these inputs is unpinned)."""
     gen = gen or generator()
+    if sig is None or vk is None or gen is None:
+        return False
     lhs = final_exp(miller_loop(sig, gen) * miller_loop(g1_neg(hash_to_g1(msg)), vk))
     return lhs.isone()
 

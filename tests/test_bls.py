@@ -107,3 +107,30 @@ def test_dropin_string_handling():
     assert GpuBlsUtils.prepare_seed(b"x" * 48) == b"x" * 48
     params = BlsGroupParamsLoaderGpu().load_group_params()
     assert params.group_name == "generator" and o.b58decode(params.g).hex() == V["generator"]
+
+
+def test_identity_points_never_verify(hostcheck):
+    """A signature, summed verkey or generator at infinity is rejected
+    (bn254.h bls_check), on the CPU build of the device code, through the
+    drop-in (an empty participant list never reaches the engine) and by the
+    oracle: e(inf, g) == e(H, inf) == 1 would accept a forged multi-signature
+    with participants = [] (bls_bft_replica_plenum.py:159-172)."""
+    from plenum_amd.bls import BlsCryptoVerifierGpu, BlsGroupParamsLoaderGpu
+    from engine_double import OracleBlsEngine
+    hc = _hc_bls(hostcheck)
+    gen = bytes.fromhex(V["generator"])
+    vk0 = bytes.fromhex(V["keys"][0]["vk"])
+    m = b"pool state root"
+    zero = b"\0" * 128
+    assert hc.edv_host_bls_verify(zero, m, ctypes.c_uint64(len(m)), zero, gen) == 0
+    assert hc.edv_host_bls_verify(zero, m, ctypes.c_uint64(len(m)), vk0, gen) == 0
+    assert hc.edv_host_bls_verify(zero, m, ctypes.c_uint64(len(m)), vk0, zero) == 0
+    assert not o.verify(None, m, None) and not o.verify_multi(None, m, [])
+    eng = OracleBlsEngine()
+    v = BlsCryptoVerifierGpu(BlsGroupParamsLoaderGpu().load_group_params(), engine=eng)
+    inf = o.b58encode(zero)
+    assert v.verify_multi_sig(inf, m, []) is False
+    assert v.verify_multi_sig_batch([(inf, m, []), (inf, m, [])]) == [False, False]
+    assert eng.calls == 0
+    assert v.verify_sig(inf, m, o.b58encode(zero)) is False
+    assert v.verify_multi_sig(inf, m, [o.b58encode(zero)] * 2) is False

@@ -327,25 +327,82 @@ def test_scanned_batch_equals_single_on_kats(oracle):
         assert got == want
 
 
-def test_scan_buffers_not_shared_by_concurrent_batches(oracle):
-    """While one batch holds the authenticator's reused scan buffers (scan
-    through GPU call), a batch from another thread gets fresh buffers, and
-    both are right."""
+def test_concurrent_batches_serialised_on_the_engine(oracle):
+    """A batch from another thread waits for the engine lock (held from key
+    routing through the verify), so it neither overwrites the reused scan
+    buffers nor rebinds key ids an in-flight batch resolved."""
+    import threading
+    import time
+    from plenum_amd.client_authn import _engine_lock
     idrs, vks, msgs = _signed(2, 30, seed=4)
-    a = GpuAuthNr(engine=OracleEngine(oracle))
+    eng = OracleEngine(oracle)
+    a = GpuAuthNr(engine=eng)
     for idr, vk in zip(idrs, vks):
         a.addIdr(idr, vk)
     want = [_outcome(r) for r in a.authenticate_batch(msgs)]
-    used = len(a._g.scan_out[0])
-    assert used >= 64 * len(msgs) and all(isinstance(x, str) for x in want)
-    a._g.scan_out[0][:] = b"\0" * used  # what a first batch's GPU call would still be reading
-    assert a._g.scan_out_lock.acquire(blocking=False)  # that first batch
-    try:
-        assert [_outcome(r) for r in a.authenticate_batch(msgs)] == want
-        assert bytes(a._g.scan_out[0]) == b"\0" * used  # untouched
-    finally:
-        a._g.scan_out_lock.release()
-    assert [_outcome(r) for r in a.authenticate_batch(msgs)] == want
+    assert all(isinstance(x, str) for x in want)
+    got = []
+    with _engine_lock(eng):  # a first batch in flight
+        t = threading.Thread(target=lambda: got.append([_outcome(r) for r in a.authenticate_batch(msgs)]))
+        t.start()
+        time.sleep(0.3)
+        assert t.is_alive() and not got
+    t.join(30)
+    assert got == [want]
+
+
+def test_concurrent_batches_with_evictions(oracle):
+    """Threads on two authenticators sharing one engine whose key store holds
+    2 keys of 6 hot signers (every batch evicts): every verdict stays right."""
+    import threading
+    idrs, vks, msgs = _signed(6, 36, seed=8)
+    bad = [dict(m, reqId=m["reqId"] + 1) if i % 5 == 0 else m for i, m in enumerate(msgs)]
+    eng = OracleEngine(oracle)
+    auths = [GpuAuthNr(engine=eng, max_keys=2, hot_key_uses=1) for _ in range(2)]
+    for a in auths:
+        for idr, vk in zip(idrs, vks):
+            a.addIdr(idr, vk)
+    ref = GpuAuthNr(engine=OracleEngine(oracle), max_keys=0)
+    for idr, vk in zip(idrs, vks):
+        ref.addIdr(idr, vk)
+    want = [_outcome(r) for r in ref.authenticate_batch(bad)]
+    assert sum(1 for w in want if w[0] == "InvalidSignature") == 8
+    errors = []
+
+    def work(a, k):
+        for it in range(6):
+            batch = bad[k % 6:] + bad[:k % 6]
+            got = [_outcome(r) for r in a.authenticate_batch(batch)]
+            if got != want[k % 6:] + want[:k % 6]:
+                errors.append((k, it))
+            k += 1
+
+    th = [threading.Thread(target=work, args=(auths[i % 2], i)) for i in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    assert not errors and eng.keyed_calls > 0
+
+
+def test_overridden_serializer_keeps_the_per_message_path(oracle):
+    """A host class with its own serializeForSig: authenticate_batch uses it
+    (the native scan would restate the mixin's), so batch == per-message."""
+    idrs, vks, msgs = _signed(1, 4, seed=2)
+
+    class Custom(GpuAuthNr):
+        def serializeForSig(self, msg, topLevelKeysToIgnore=None):
+            return b"custom" + super().serializeForSig(msg, topLevelKeysToIgnore)
+
+    a = Custom(engine=OracleEngine(oracle))
+    a.addIdr(idrs[0], vks[0])
+    assert not a._native_host_steps() and GpuAuthNr(engine=OracleEngine(oracle))._native_host_steps()
+    got = [_outcome(r)[0] for r in a.authenticate_batch(msgs)]
+    assert got == ["InvalidSignature"] * 4  # signed over the plain bytes
+    for m in msgs:
+        with pytest.raises(Exception) as ei:
+            a.authenticate(m)
+        assert type(ei.value).__name__ == "InvalidSignature"
 
 
 def test_scanned_batch_fuzz(oracle):
