@@ -178,6 +178,33 @@ int edv_verify_batch_keyed(edv_ctx *ctx, const uint8_t *sig64, const uint32_t *k
 int edv_verify_batch_keyed_device(edv_ctx *ctx, const void *d_sig64, const void *d_key_idx, const void *d_msgs,
                                   const void *d_msg_off, uint64_t n, void *d_accept_words, void *stream);
 
+/* Signature slots: the host-pointer verifies below take, instead of sig64,
+ * n slots of EDV_SIG_SLOT96 bytes, so that the base58 decode of the request
+ * signature (client_authn.py:89, b58decode) runs on the GPU:
+ *   slot[95] = t > 0 : slot[0 .. t) is the signature's base58 text, which the
+ *                      caller has checked decodes to exactly 64 bytes (value
+ *                      < 2^512; the split of sig || ser at byte 64 then is the
+ *                      plain one);
+ *   slot[95] = 0     : slot[0 .. 64) is R || S, decoded by the caller.
+ * Same verdicts as the sig64 forms on the decoded signatures. */
+#define EDV_SIG_SLOT96 96
+int edv_verify_batch_slots(edv_ctx *ctx, const uint8_t *sig_slots, const uint8_t *pk32, const uint8_t *msgs,
+                           const uint64_t *msg_off, uint64_t n, uint8_t *accept_bits);
+int edv_verify_batch_keyed_slots(edv_ctx *ctx, const uint8_t *sig_slots, const uint32_t *key_idx, const uint8_t *msgs,
+                                 const uint64_t *msg_off, uint64_t n, uint8_t *accept_bits);
+
+/* Pinned host memory (hipHostMalloc, portable to every device).  A host-
+ * pointer verify whose inputs (signatures, keys, messages, offsets) lie in
+ * such blocks copies them to the device straight from there, with no CPU
+ * staging copy -- the authenticator's batch scan writes its output into them.
+ * edv_host_free only after the verifies reading the block have returned. */
+int edv_host_alloc(edv_ctx *ctx, uint64_t bytes, void **out);
+int edv_host_free(void *p);
+/* The last host-pointer verify on ctx: out4 = {call ms, CPU staging-copy ms,
+ * bytes copied host -> device, direct mask (bit 0 signatures, 1 keys,
+ * 2 messages, 3 offsets copied straight from pinned memory)}. */
+int edv_last_host_stats(edv_ctx *ctx, double *out4);
+
 /* Either path with message spans instead of contiguous offsets: item i's
  * message is d_msgs[d_msg_start[i] .. d_msg_end[i]) (uint64 each), so the k
  * signatures of a multi-signature request (authenticate_multi, configs[3])

@@ -20,6 +20,7 @@
 //   edv_tally_*          distinct-voter ballots -> counts -> quorum flags.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <mutex>
 #include <stdarg.h>
 #include <stdio.h>
@@ -164,6 +165,70 @@ __device__ __forceinline__ void load_words(uint32_t* dst, const uint8_t* src, in
 constexpr int kLenKeyBits = 6;  // block counts 0..62; 63 = longer
 __device__ __forceinline__ uint64_t hash_lane_request(uint64_t t, const uint32_t* __restrict__ perm) {
   return perm ? perm[t] : t;
+}
+
+// ---- signature slots (edverify.h EDV_SIG_SLOT96): the authenticator's
+// base58 decode of the request signature (client_authn.py:89) moved off the
+// host.  Slot i is 96 bytes; byte 95 = t > 0: bytes 0..t-1 are the base58
+// text of a signature that the host checked decodes to exactly 64 bytes
+// (hostpack.cpp b58_len64), so its value is < 2^512 and the decode is the
+// 512-bit big-endian value of the text; t == 0: bytes 0..63 are R || S
+// (decoded on the host: other lengths, which move bytes across the split at
+// 64).  HBM: 96 B read + 64 B written per request.
+__device__ __forceinline__ uint32_t b58_digit(uint32_t c) {
+  // '1'-'9' 0-8, 'A'-'H' 9-16, 'J'-'N' 17-21, 'P'-'Z' 22-32, 'a'-'k' 33-43, 'm'-'z' 44-57
+  uint32_t d = c - '1';
+  d = c >= 'A' ? c - 'A' + 9 - (c > 'H') - (c > 'N') : d;
+  d = c >= 'a' ? c - 'a' + 33 - (c > 'k') : d;
+  return d;
+}
+
+constexpr uint32_t kPow58[6] = {1u, 58u, 3364u, 195112u, 11316496u, 656356768u};
+
+__global__ __launch_bounds__(kBlock) void edv_b58_sig_kernel(const uint8_t* __restrict__ slots, uint64_t n,
+                                                            uint8_t* __restrict__ sig64) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t w[24];
+  load_words(w, slots + 96 * i, 24);
+  const uint32_t t = w[23] >> 24;
+  uint32_t out[16];
+  if (t == 0) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) out[j] = w[j];
+  } else {
+    // Horner over groups of five digits (58^5 < 2^32): acc = acc * 58^k + chunk,
+    // k = the group's digits inside the text (0..5, per lane)
+    uint32_t acc[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[j] = 0;
+#pragma unroll
+    for (int g = 0; g < 19; ++g) {
+      uint32_t chunk = 0, k = 0;
+#pragma unroll
+      for (int q = 0; q < 5; ++q) {
+        const int p = 5 * g + q;
+        if (p < 95 && (uint32_t)p < t) {
+          chunk = chunk * 58u + b58_digit((w[p >> 2] >> (8 * (p & 3))) & 0xffu);
+          ++k;
+        }
+      }
+      const uint32_t mul = k == 5 ? kPow58[5] : k == 4 ? kPow58[4] : k == 3 ? kPow58[3] : k == 2 ? kPow58[2]
+                         : k == 1 ? kPow58[1] : kPow58[0];
+      uint64_t carry = chunk;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const uint64_t v = (uint64_t)acc[j] * mul + carry;
+        acc[j] = (uint32_t)v;
+        carry = v >> 32;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) out[j] = __builtin_bswap32(acc[15 - j]);  // big-endian bytes
+  }
+  uint4* o = (uint4*)(sig64 + 64 * i);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) o[k] = make_uint4(out[4 * k], out[4 * k + 1], out[4 * k + 2], out[4 * k + 3]);
 }
 
 // Message i = msgs[ms[i] .. me[i]): me = msg_off + 1 for contiguous offsets,
@@ -988,6 +1053,12 @@ struct edv_ctx {
   hipEvent_t ev_h2d[kSlots] = {}, ev_done[kSlots] = {};
   Buf h_sig[kSlots], h_key[kSlots], h_msg[kSlots], h_off[kSlots], h_bits[kSlots];
   Buf d_sig[kSlots], d_key[kSlots], d_msg[kSlots], d_off[kSlots], d_bits[kSlots];
+  Buf d_slot[kSlots];  // EDV_SIG_SLOT96 input of edv_b58_sig_kernel
+  // what the last host-pointer verify did (edv_last_host_stats)
+  double last_stage_ms = 0.0;   // CPU copies into the pinned staging (0 when every source was pinned)
+  double last_call_ms = 0.0;    // the whole call
+  uint64_t last_h2d_bytes = 0;  // bytes copied host -> device
+  int last_direct = 0;          // bit 0 sig, 1 keys, 2 msgs, 3 offsets: DMA straight from the caller's pinned memory
 };
 
 namespace {
@@ -1387,11 +1458,36 @@ static int launch_verify_keyed(edv_ctx* ctx, const void* d_sig, const void* d_ki
   return launch_pipeline(ctx, true, d_sig, d_kidx, d_msgs, off, off + 1, n, d_words, st);
 }
 
-// Host-pointer verify: chunks of kHostChunk requests staged through pinned
-// memory in two slots.  Chunk c: CPU copy into pinned slot c % 2 (after the
-// slot's previous chunk finished), H2D on stream_copy, kernels + bitmask D2H
-// on the context stream after the H2D event.  So the CPU copy and H2D of chunk
-// c + 1 run while chunk c's kernels do.  key_bytes: 32 (pk32) or 4 (key ids).
+// Pinned host memory handed out by edv_host_alloc (process-wide: the blocks
+// are allocated portable, so every context's copy engine can read them).  A
+// host-pointer verify whose source range lies inside one block copies it to
+// the device straight from there, with no CPU staging copy.
+struct PinnedBlock {
+  const uint8_t* p;
+  size_t n;
+};
+std::mutex g_pinned_mu;
+std::vector<PinnedBlock> g_pinned;
+
+static bool pinned_range(const void* p, size_t n) {
+  if (!p) return false;
+  const uint8_t* a = (const uint8_t*)p;
+  std::lock_guard<std::mutex> g(g_pinned_mu);
+  for (const PinnedBlock& b : g_pinned)
+    if (a >= b.p && a + n <= b.p + b.n) return true;
+  return false;
+}
+
+// Host-pointer verify: chunks of kHostChunk requests, two slots of device
+// buffers.  Chunk c: its inputs go to the device on stream_copy -- straight
+// from the caller's memory when it lies in edv_host_alloc'd pinned blocks,
+// otherwise through a CPU copy into the slot's pinned staging first -- then
+// (after the H2D event) the signature-slot decode if any, the kernels and the
+// bitmask D2H on the context stream.  So the copies of chunk c + 1 run while
+// chunk c's kernels do.  Offsets are copied as given: the kernels see the
+// device message buffer at (base - msg_off[c0]), so no offset is rebased on
+// the host.  key_bytes: 32 (pk32) or 4 (key ids); sig_stride: 64 (R || S) or
+// EDV_SIG_SLOT96.
 constexpr uint64_t kHostChunk = 1ull << 18;
 
 // memcpy into the pinned staging on up to 8 host threads (8 MiB or more each;
@@ -1416,13 +1512,23 @@ static void stage_copy(void* dst, const void* src, size_t n) {
   });
 }
 
-static int host_verify(edv_ctx* ctx, bool keyed, const uint8_t* sig64, const uint8_t* keys, const uint8_t* msgs,
-                       const uint64_t* msg_off, uint64_t n, uint8_t* accept_bits) {
+static int host_verify(edv_ctx* ctx, bool keyed, const uint8_t* sig, uint64_t sig_stride, const uint8_t* keys,
+                       const uint8_t* msgs, const uint64_t* msg_off, uint64_t n, uint8_t* accept_bits) {
+  using clk = std::chrono::steady_clock;
+  const auto t_call = clk::now();
+  double stage_s = 0.0;
   const uint64_t key_bytes = keyed ? 4 : 32;
+  const bool slots = sig_stride == EDV_SIG_SLOT96;
   for (uint64_t i = 0; i < n; ++i)
     if (msg_off[i + 1] < msg_off[i]) return set_err(EDV_EINVAL, "msg_off[%llu] decreasing", (unsigned long long)i);
   if (msg_off[n] > msg_off[0] && !msgs) return set_err(EDV_EINVAL, "null msgs");
   if (keyed && ctx->key_count == 0) return set_err(EDV_EINVAL, "no registered keys");
+  const bool sig_direct = pinned_range(sig, sig_stride * n);
+  const bool key_direct = pinned_range(keys, key_bytes * n);
+  const bool msg_direct = msg_off[n] == msg_off[0] || pinned_range(msgs + msg_off[0], msg_off[n] - msg_off[0]);
+  const bool off_direct = pinned_range(msg_off, 8 * (n + 1));
+  ctx->last_direct = (sig_direct ? 1 : 0) | (key_direct ? 2 : 0) | (msg_direct ? 4 : 0) | (off_direct ? 8 : 0);
+  ctx->last_h2d_bytes = 0;
   const uint64_t nchunks = div_up(n, kHostChunk);
   uint64_t pend[edv_ctx::kSlots] = {};  // chunk index + 1 whose bits sit in the slot (0 = none)
   auto drain = [&](int sl) -> int {     // wait for the slot's chunk, copy its bits out
@@ -1433,34 +1539,61 @@ static int host_verify(edv_ctx* ctx, bool keyed, const uint8_t* sig64, const uin
     pend[sl] = 0;
     return 0;
   };
+  // a source the copy engine reads: the caller's pinned memory, or the slot's staging after a CPU copy
+  auto source = [&](bool direct, edv_ctx::Buf& stage, const uint8_t* src, uint64_t bytes, bool threaded,
+                    const uint8_t** out) -> int {
+    if (direct || !bytes) {
+      *out = src;
+      return 0;
+    }
+    int r = ensure_pinned(stage, bytes + 16);
+    if (r) return r;
+    const auto t0 = clk::now();
+    if (threaded)
+      stage_copy(stage.p, src, bytes);
+    else
+      memcpy(stage.p, src, bytes);
+    stage_s += std::chrono::duration<double>(clk::now() - t0).count();
+    *out = (const uint8_t*)stage.p;
+    return 0;
+  };
   int r;
   for (uint64_t c = 0; c < nchunks; ++c) {
     const int sl = (int)(c % edv_ctx::kSlots);
     if ((r = drain(sl))) return r;
     const uint64_t c0 = c * kHostChunk, cn = (n - c0) < kHostChunk ? (n - c0) : kHostChunk;
     const uint64_t m0 = msg_off[c0], mbytes = msg_off[c0 + cn] - m0, nwords = div_up(cn, 64);
-    if ((r = ensure_pinned(ctx->h_sig[sl], 64 * cn)) || (r = ensure_pinned(ctx->h_key[sl], key_bytes * cn)) ||
-        (r = ensure_pinned(ctx->h_msg[sl], mbytes + 16)) || (r = ensure_pinned(ctx->h_off[sl], 8 * (cn + 1))) ||
-        (r = ensure_pinned(ctx->h_bits[sl], 8 * nwords)) || (r = ensure(ctx->d_sig[sl], 64 * cn)) ||
+    if ((r = ensure_pinned(ctx->h_bits[sl], 8 * nwords)) || (r = ensure(ctx->d_sig[sl], 64 * cn)) ||
         (r = ensure(ctx->d_key[sl], key_bytes * cn)) || (r = ensure(ctx->d_msg[sl], mbytes + 16)) ||
-        (r = ensure(ctx->d_off[sl], 8 * (cn + 1))) || (r = ensure(ctx->d_bits[sl], 8 * nwords)))
+        (r = ensure(ctx->d_off[sl], 8 * (cn + 1))) || (r = ensure(ctx->d_bits[sl], 8 * nwords)) ||
+        (slots && (r = ensure(ctx->d_slot[sl], sig_stride * cn))))
       return r;
-    uint64_t* off = (uint64_t*)ctx->h_off[sl].p;
-    for (uint64_t i = 0; i <= cn; ++i) off[i] = msg_off[c0 + i] - m0;
-    stage_copy(ctx->h_sig[sl].p, sig64 + 64 * c0, 64 * cn);
-    memcpy(ctx->h_key[sl].p, keys + key_bytes * c0, key_bytes * cn);
-    if (mbytes) stage_copy(ctx->h_msg[sl].p, msgs + m0, mbytes);
-    set_bucketing(ctx, ctx->bucket_mode == 2 && lengths_mixed(off, cn));
+    const uint8_t *s_sig, *s_key, *s_msg, *s_off;
+    if ((r = source(sig_direct, ctx->h_sig[sl], sig + sig_stride * c0, sig_stride * cn, true, &s_sig)) ||
+        (r = source(key_direct, ctx->h_key[sl], keys + key_bytes * c0, key_bytes * cn, false, &s_key)) ||
+        (r = source(msg_direct, ctx->h_msg[sl], msgs ? msgs + m0 : nullptr, mbytes, true, &s_msg)) ||
+        (r = source(off_direct, ctx->h_off[sl], (const uint8_t*)(msg_off + c0), 8 * (cn + 1), false, &s_off)))
+      return r;
+    set_bucketing(ctx, ctx->bucket_mode == 2 && lengths_mixed(msg_off + c0, cn));
     hipStream_t cs = ctx->stream_copy;
-    HIP_TRY(hipMemcpyAsync(ctx->d_sig[sl].p, ctx->h_sig[sl].p, 64 * cn, hipMemcpyHostToDevice, cs));
-    HIP_TRY(hipMemcpyAsync(ctx->d_key[sl].p, ctx->h_key[sl].p, key_bytes * cn, hipMemcpyHostToDevice, cs));
-    if (mbytes) HIP_TRY(hipMemcpyAsync(ctx->d_msg[sl].p, ctx->h_msg[sl].p, mbytes, hipMemcpyHostToDevice, cs));
-    HIP_TRY(hipMemcpyAsync(ctx->d_off[sl].p, off, 8 * (cn + 1), hipMemcpyHostToDevice, cs));
+    void* d_sig_in = slots ? ctx->d_slot[sl].p : ctx->d_sig[sl].p;
+    HIP_TRY(hipMemcpyAsync(d_sig_in, s_sig, sig_stride * cn, hipMemcpyHostToDevice, cs));
+    HIP_TRY(hipMemcpyAsync(ctx->d_key[sl].p, s_key, key_bytes * cn, hipMemcpyHostToDevice, cs));
+    if (mbytes) HIP_TRY(hipMemcpyAsync(ctx->d_msg[sl].p, s_msg, mbytes, hipMemcpyHostToDevice, cs));
+    HIP_TRY(hipMemcpyAsync(ctx->d_off[sl].p, s_off, 8 * (cn + 1), hipMemcpyHostToDevice, cs));
     HIP_TRY(hipEventRecord(ctx->ev_h2d[sl], cs));
+    ctx->last_h2d_bytes += sig_stride * cn + key_bytes * cn + mbytes + 8 * (cn + 1);
     hipStream_t st = ctx->stream;
     HIP_TRY(hipStreamWaitEvent(st, ctx->ev_h2d[sl], 0));
+    if (slots) {
+      hipLaunchKernelGGL(edv_b58_sig_kernel, dim3((uint32_t)div_up(cn, kBlock)), dim3(kBlock), 0, st,
+                         (const uint8_t*)ctx->d_slot[sl].p, cn, (uint8_t*)ctx->d_sig[sl].p);
+      HIP_TRY(hipGetLastError());
+    }
     const uint64_t* d_off = (const uint64_t*)ctx->d_off[sl].p;
-    if ((r = launch_pipeline(ctx, keyed, ctx->d_sig[sl].p, ctx->d_key[sl].p, ctx->d_msg[sl].p, d_off, d_off + 1, cn,
+    // the offsets are the caller's (starting at m0): the kernels address msgs + off[i]
+    const uint8_t* d_msg_base = (const uint8_t*)ctx->d_msg[sl].p - m0;
+    if ((r = launch_pipeline(ctx, keyed, ctx->d_sig[sl].p, ctx->d_key[sl].p, d_msg_base, d_off, d_off + 1, cn,
                              ctx->d_bits[sl].p, st)))
       return r;
     HIP_TRY(hipMemcpyAsync(ctx->h_bits[sl].p, ctx->d_bits[sl].p, 8 * nwords, hipMemcpyDeviceToHost, st));
@@ -1470,6 +1603,8 @@ static int host_verify(edv_ctx* ctx, bool keyed, const uint8_t* sig64, const uin
   for (int sl = 0; sl < edv_ctx::kSlots; ++sl)
     if ((r = drain(sl))) return r;
   if (n & 7) accept_bits[n / 8] &= (uint8_t)((1u << (n & 7)) - 1);
+  ctx->last_stage_ms = stage_s * 1e3;
+  ctx->last_call_ms = std::chrono::duration<double, std::milli>(clk::now() - t_call).count();
   return 0;
 }
 
@@ -1602,7 +1737,64 @@ int edv_verify_batch_keyed(edv_ctx* ctx, const uint8_t* sig64, const uint32_t* k
   if (r) return r;
   if (n == 0) return 0;
   if (!sig64 || !key_idx || !msg_off || !accept_bits) return set_err(EDV_EINVAL, "null pointer");
-  return host_verify(ctx, true, sig64, (const uint8_t*)key_idx, msgs, msg_off, n, accept_bits);
+  return host_verify(ctx, true, sig64, 64, (const uint8_t*)key_idx, msgs, msg_off, n, accept_bits);
+}
+
+int edv_verify_batch_keyed_slots(edv_ctx* ctx, const uint8_t* sig_slots, const uint32_t* key_idx, const uint8_t* msgs,
+                                 const uint64_t* msg_off, uint64_t n, uint8_t* accept_bits) {
+  int r = set_device(ctx);
+  if (r) return r;
+  if (n == 0) return 0;
+  if (!sig_slots || !key_idx || !msg_off || !accept_bits) return set_err(EDV_EINVAL, "null pointer");
+  return host_verify(ctx, true, sig_slots, EDV_SIG_SLOT96, (const uint8_t*)key_idx, msgs, msg_off, n, accept_bits);
+}
+
+int edv_verify_batch_slots(edv_ctx* ctx, const uint8_t* sig_slots, const uint8_t* pk32, const uint8_t* msgs,
+                           const uint64_t* msg_off, uint64_t n, uint8_t* accept_bits) {
+  int r = set_device(ctx);
+  if (r) return r;
+  if (n == 0) return 0;
+  if (!sig_slots || !pk32 || !msg_off || !accept_bits) return set_err(EDV_EINVAL, "null pointer");
+  return host_verify(ctx, false, sig_slots, EDV_SIG_SLOT96, pk32, msgs, msg_off, n, accept_bits);
+}
+
+int edv_host_alloc(edv_ctx* ctx, uint64_t bytes, void** out) {
+  int r = set_device(ctx);
+  if (r) return r;
+  if (!out) return set_err(EDV_EINVAL, "null out");
+  *out = nullptr;
+  if (bytes == 0) return set_err(EDV_EINVAL, "zero bytes");
+  void* p = nullptr;
+  hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocPortable);
+  if (e != hipSuccess) return set_err(EDV_ENOMEM, "hipHostMalloc(%llu): %s", (unsigned long long)bytes, hipGetErrorString(e));
+  {
+    std::lock_guard<std::mutex> g(g_pinned_mu);
+    g_pinned.push_back(PinnedBlock{(const uint8_t*)p, (size_t)bytes});
+  }
+  *out = p;
+  return 0;
+}
+
+int edv_host_free(void* p) {
+  if (!p) return 0;
+  {
+    std::lock_guard<std::mutex> g(g_pinned_mu);
+    size_t k = 0;
+    while (k < g_pinned.size() && g_pinned[k].p != p) ++k;
+    if (k == g_pinned.size()) return set_err(EDV_EINVAL, "not an edv_host_alloc block");
+    g_pinned.erase(g_pinned.begin() + (long)k);
+  }
+  HIP_TRY(hipHostFree(p));
+  return 0;
+}
+
+int edv_last_host_stats(edv_ctx* ctx, double* out4) {
+  if (!ctx || !out4) return set_err(EDV_EINVAL, "null argument");
+  out4[0] = ctx->last_call_ms;
+  out4[1] = ctx->last_stage_ms;
+  out4[2] = (double)ctx->last_h2d_bytes;
+  out4[3] = (double)ctx->last_direct;
+  return 0;
 }
 
 }  // extern "C"
@@ -1726,7 +1918,8 @@ void edv_destroy(edv_ctx* ctx) {
   for (edv_ctx::Buf* b : {&ctx->b_sig, &ctx->b_pk, &ctx->b_msg, &ctx->b_off, &ctx->b_bits, &ctx->b_aux}) free_buf(*b);
   for (int k = 0; k < edv_ctx::kSlots; ++k) {
     for (edv_ctx::Buf* b : {&ctx->h_sig[k], &ctx->h_key[k], &ctx->h_msg[k], &ctx->h_off[k], &ctx->h_bits[k],
-                            &ctx->d_sig[k], &ctx->d_key[k], &ctx->d_msg[k], &ctx->d_off[k], &ctx->d_bits[k]})
+                            &ctx->d_sig[k], &ctx->d_key[k], &ctx->d_msg[k], &ctx->d_off[k], &ctx->d_bits[k],
+                            &ctx->d_slot[k]})
       free_buf(*b);
     if (ctx->ev_h2d[k]) (void)hipEventDestroy(ctx->ev_h2d[k]);
     if (ctx->ev_done[k]) (void)hipEventDestroy(ctx->ev_done[k]);
@@ -1846,7 +2039,7 @@ int edv_verify_batch(edv_ctx* ctx, const uint8_t* sig64, const uint8_t* pk32, co
   if (r) return r;
   if (n == 0) return 0;
   if (!sig64 || !pk32 || !msg_off || !accept_bits) return set_err(EDV_EINVAL, "null pointer");
-  return host_verify(ctx, false, sig64, pk32, msgs, msg_off, n, accept_bits);
+  return host_verify(ctx, false, sig64, 64, pk32, msgs, msg_off, n, accept_bits);
 }
 
 int edv_sign_open_batch(edv_ctx* ctx, const uint8_t* sm, const uint64_t* sm_off, const uint8_t* pk32, uint64_t n,

@@ -384,6 +384,58 @@ std::string b58encode_raw(const uint8_t* v, size_t n) {
   return std::string(nz, '1') + std::string(digits.rbegin(), digits.rend());
 }
 
+// Signature slots (edverify.h EDV_SIG_SLOT96): a signature whose base58 text
+// decodes to exactly 64 bytes travels as its text and is decoded on the GPU
+// (edv_b58_sig_kernel); the host only needs to know that the decoded length
+// is 64, because crypto_sign_open's split of sig || ser at byte 64
+// (nacl_wrappers.py:108) depends on it.  The text after its nz leading '1's
+// (zero bytes) is a number whose byte length must be L = 64 - nz, i.e.
+// 256^(L-1) <= value < 256^L; base58 digits are in ASCII order, so for texts
+// of equal length the numeric comparison is memcmp against the encodings of
+// those powers.
+struct B58Len64 {
+  std::string lo[65], hi[65];  // L = 1..64: b58(256^(L-1)), b58(256^L)
+  B58Len64() {
+    std::vector<uint8_t> v(66, 0);
+    v[0] = 1;
+    for (size_t L = 1; L <= 64; ++L) {
+      lo[L] = b58encode_raw(v.data(), L);
+      hi[L] = b58encode_raw(v.data(), L + 1);
+    }
+  }
+};
+const B58Len64& b58_len64_table() {
+  static const B58Len64 t;
+  return t;
+}
+
+// 1: b58decode(s) is valid and exactly 64 bytes; 0: valid, another length;
+// -1: a character outside the alphabet (b58decode raises).
+int b58_len64(const unsigned char* s, size_t n) {
+  for (size_t i = 0; i < n; ++i)
+    if (kIndex.v[s[i]] < 0) return -1;
+  size_t nz = 0;
+  while (nz < n && s[nz] == '1') ++nz;
+  if (nz > 64) return 0;
+  const size_t L = 64 - nz, d = n - nz;
+  if (L == 0) return d == 0 ? 1 : 0;
+  if (d == 0) return 0;  // the value is 0: nz < 64 zero bytes
+  const B58Len64& t = b58_len64_table();
+  const std::string &lo = t.lo[L], &hi = t.hi[L];
+  const unsigned char* r = s + nz;
+  const bool ge = d > lo.size() || (d == lo.size() && memcmp(r, lo.data(), d) >= 0);
+  const bool lt = d < hi.size() || (d == hi.size() && memcmp(r, hi.data(), d) < 0);
+  return ge && lt ? 1 : 0;
+}
+
+PyObject* py_b58_len64(PyObject*, PyObject* v) {
+  if (!PyUnicode_CheckExact(v) || !PyUnicode_IS_ASCII(v)) {
+    PyErr_SetString(PyExc_TypeError, "ASCII str expected");
+    return nullptr;
+  }
+  return PyLong_FromLong(b58_len64(PyUnicode_1BYTE_DATA(v), (size_t)PyUnicode_GET_LENGTH(v)));
+}
+
 // b58encode_rows(buf, width) -> [b58encode(buf[i*width:(i+1)*width]) ...]
 PyObject* py_b58encode_rows(PyObject*, PyObject* args) {
   Py_buffer b;
@@ -557,12 +609,15 @@ PyObject* py_pack_sm(PyObject*, PyObject* args) {
 // items the workers could not finish (ser_obj); (4) offsets by prefix sum;
 // (5) the workers write sig64 and the message buffer straight into the result
 // bytes objects.
+constexpr int kSigSlot = 96;  // edverify.h EDV_SIG_SLOT96
+
 struct ScanItem {
   PyObject* m = nullptr;
   const unsigned char* sp = nullptr;
   Py_ssize_t ns = 0;
   uint32_t uid = 0xffffffffu;
   uint8_t state = 0;  // 0 Python path, 1 fast, 2 serialization deferred
+  uint8_t text = 0;   // slot mode: the signature's base58 text goes to the GPU (decodes to 64 bytes)
   uint16_t buf = 0;   // which buffer holds its decoded signature / serialization
   uint32_t sig_len = 0, ser_len = 0;
   uint64_t sig_at = 0, ser_at = 0;
@@ -633,8 +688,12 @@ ScanScratch& scan_scratch() {
 bool g_scan_busy = false;
 
 // Output buffer for (5): the caller's bytearray grown to `need` bytes (never
-// shrunk, so its pages stay mapped from call to call), or a fresh bytes object
-// when no bytearray is given or it cannot be resized (a live export).
+// shrunk, so its pages stay mapped from call to call); or any other writable
+// C-contiguous buffer of at least `need` bytes -- the authenticator passes the
+// engine's pinned host memory (edv_host_alloc), so the GPU call copies from it
+// without staging; or a fresh bytes object when neither fits (a bytearray with
+// a live export, a buffer that is too small).  The object is returned as the
+// result and the pointer stays valid while the caller holds it.
 PyObject* out_buffer(PyObject* ba, Py_ssize_t need, char** data) {
   if (ba && PyByteArray_CheckExact(ba)) {
     if (PyByteArray_GET_SIZE(ba) >= need || PyByteArray_Resize(ba, need) == 0) {
@@ -643,6 +702,22 @@ PyObject* out_buffer(PyObject* ba, Py_ssize_t need, char** data) {
       return ba;
     }
     PyErr_Clear();
+  } else if (ba && ba != Py_None && PyObject_CheckBuffer(ba)) {
+    Py_buffer view;
+    if (PyObject_GetBuffer(ba, &view, PyBUF_WRITABLE | PyBUF_C_CONTIGUOUS) == 0) {
+      const bool fits = view.len >= need;
+      char* p = (char*)view.buf;
+      // a buffer with a memory owner outside Python (ctypes over pinned host memory): the
+      // caller keeps the owner alive while it uses the result
+      PyBuffer_Release(&view);
+      if (fits) {
+        Py_INCREF(ba);
+        *data = p;
+        return ba;
+      }
+    } else {
+      PyErr_Clear();
+    }
   }
   PyObject* b = PyBytes_FromStringAndSize(nullptr, need);
   if (b) *data = PyBytes_AS_STRING(b);
@@ -665,12 +740,17 @@ struct PyRefs {
 
 PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
   PyObject *msgs, *ignore = Py_None, *out = Py_None;
-  int want_threads = 0;
-  if (!PyArg_ParseTuple(args, "O|OiO", &msgs, &ignore, &want_threads, &out)) return nullptr;
+  int want_threads = 0, sig_slot = 64;
+  if (!PyArg_ParseTuple(args, "O|OiOi", &msgs, &ignore, &want_threads, &out, &sig_slot)) return nullptr;
+  if (sig_slot != 64 && sig_slot != kSigSlot) {
+    PyErr_Format(PyExc_ValueError, "slot must be 64 (raw signatures) or %d (base58 slots)", kSigSlot);
+    return nullptr;
+  }
+  const bool slots = sig_slot == kSigSlot;
   PyObject *out_sig = nullptr, *out_msg = nullptr;
   if (out != Py_None) {
     if (!PyList_CheckExact(out) || PyList_GET_SIZE(out) != 2) {
-      PyErr_SetString(PyExc_TypeError, "out must be a list [bytearray, bytearray]");
+      PyErr_SetString(PyExc_TypeError, "out must be a list of two writable buffers (bytearray, pinned memory)");
       return nullptr;
     }
     out_sig = PyList_GET_ITEM(out, 0);
@@ -756,7 +836,12 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
       }
       x.sp = (const unsigned char*)PyUnicode_1BYTE_DATA(sv);
       x.ns = PyUnicode_GET_LENGTH(sv);
-      if (!b58decode_raw(x.sp, (size_t)x.ns, sig)) continue;
+      int len64 = 0;
+      if (slots) {  // decoded on the GPU when the text decodes to exactly 64 bytes
+        len64 = x.ns <= kSigSlot - 1 ? b58_len64(x.sp, (size_t)x.ns) : 0;
+        if (len64 < 0) continue;  // b58decode raises: the Python path (InvalidSignatureFormat)
+      }
+      if (len64 == 0 && !b58decode_raw(x.sp, (size_t)x.ns, sig)) continue;
       const size_t at = sb.ser.size();
       const WRes r = wser_obj(m, 0, ign, sb.ser);
       if (r != kOk) {
@@ -768,9 +853,14 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
       x.buf = (uint16_t)w;
       x.ser_at = at;
       x.ser_len = (uint32_t)(sb.ser.size() - at);
-      x.sig_at = sb.sig.size();
-      x.sig_len = (uint32_t)sig.size();
-      sb.sig.append((const char*)sig.data(), sig.size());
+      if (len64 == 1) {
+        x.text = 1;
+        x.sig_len = 64;
+      } else {
+        x.sig_at = sb.sig.size();
+        x.sig_len = (uint32_t)sig.size();
+        sb.sig.append((const char*)sig.data(), sig.size());
+      }
       idr_of[(size_t)i] = iv;
       auto ins = tab.slot.emplace(
           std::string_view((const char*)PyUnicode_1BYTE_DATA(iv), (size_t)PyUnicode_GET_LENGTH(iv)),
@@ -901,23 +991,31 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
   });
   // (5) sig64 and the messages, written by the workers into the result objects
   char *dsig = nullptr, *dmsg = nullptr;
-  PyObject* o_sig = refs.o_sig = out_buffer(out_sig, (Py_ssize_t)n * 64, &dsig);
+  PyObject* o_sig = refs.o_sig = out_buffer(out_sig, (Py_ssize_t)n * sig_slot, &dsig);
   PyObject* o_msg = refs.o_msg = o_sig ? out_buffer(out_msg, (Py_ssize_t)off[(size_t)n], &dmsg) : nullptr;
   PyObject* ret = nullptr;
   if (o_msg) {
     run_chunks(n, t, [&](int, Py_ssize_t a, Py_ssize_t b) {
       for (Py_ssize_t i = a; i < b; ++i) {
         const ScanItem& x = it[(size_t)i];
-        char* ds = dsig + (size_t)i * 64;
+        char* ds = dsig + (size_t)i * sig_slot;
+        if (slots) memset(ds + 64, 0, (size_t)sig_slot - 64);  // slot[95] = 0: raw R || S in bytes 0..63
         if (x.state != 1 || shortv[(size_t)i]) {
           memset(ds, 0, 64);
           continue;
         }
         const ScanBuf& sb = bufs[x.buf];
-        const char* sg = sb.sig.data() + x.sig_at;
         const char* sr = sb.ser.data() + x.ser_at;
         const size_t ls = x.sig_len, lm = x.ser_len;
         char* dm = dmsg + off[(size_t)i];
+        if (x.text) {  // slot: the base58 text, its length in the last byte
+          memcpy(ds, x.sp, (size_t)x.ns);
+          memset(ds + x.ns, 0, 64 - std::min<size_t>(64, (size_t)x.ns));
+          ds[sig_slot - 1] = (char)x.ns;
+          memcpy(dm, sr, lm);
+          continue;
+        }
+        const char* sg = sb.sig.data() + x.sig_at;
         if (ls >= 64) {  // sm[64:] = sig[64:] || ser
           memcpy(ds, sg, 64);
           memcpy(dm, sg + 64, ls - 64);
@@ -1016,24 +1114,28 @@ PyObject* py_results_from(PyObject*, PyObject* args) {
   return ret;
 }
 
-// gather_items(sig64, msgbuf, off, idx) -> (sig64', msgbuf', off'): the items
-// idx (uint32 LE) of a split batch, repacked contiguously.
+// gather_items(sig, msgbuf, off, idx, stride=64) -> (sig', msgbuf', off'): the
+// items idx (uint32 LE) of a split batch, repacked contiguously; stride is the
+// signature record size (64 = R || S, 96 = edverify.h signature slots).
 PyObject* py_gather_items(PyObject*, PyObject* args) {
   Py_buffer bs, bm, bo, bi;
-  if (!PyArg_ParseTuple(args, "y*y*y*y*", &bs, &bm, &bo, &bi)) return nullptr;
+  Py_ssize_t stride = 64;
+  if (!PyArg_ParseTuple(args, "y*y*y*y*|n", &bs, &bm, &bo, &bi, &stride)) return nullptr;
   const uint64_t* off = (const uint64_t*)bo.buf;
   const uint32_t* idx = (const uint32_t*)bi.buf;
   const Py_ssize_t n = bo.len / 8 - 1, k = bi.len / 4;
-  std::string sig((size_t)k * 64, '\0'), msg;
+  bool ok = stride == 64 || stride == kSigSlot;
+  std::string sig, msg;
   std::vector<uint64_t> o((size_t)k + 1, 0);
-  bool ok = n >= 0 && bs.len >= n * 64;
+  if (ok) sig.assign((size_t)k * (size_t)stride, '\0');
+  ok = ok && n >= 0 && bs.len >= n * stride;
   for (Py_ssize_t j = 0; j < k && ok; ++j) {
     const uint32_t i = idx[j];
     if ((Py_ssize_t)i >= n || off[i + 1] < off[i] || off[i + 1] > (uint64_t)bm.len) {
       ok = false;
       break;
     }
-    memcpy(&sig[(size_t)j * 64], (const char*)bs.buf + (size_t)i * 64, 64);
+    memcpy(&sig[(size_t)j * stride], (const char*)bs.buf + (size_t)i * stride, (size_t)stride);
     msg.append((const char*)bm.buf + off[i], off[i + 1] - off[i]);
     o[(size_t)j + 1] = msg.size();
   }
@@ -1042,7 +1144,7 @@ PyObject* py_gather_items(PyObject*, PyObject* args) {
   PyBuffer_Release(&bo);
   PyBuffer_Release(&bi);
   if (!ok) {
-    PyErr_SetString(PyExc_ValueError, "gather_items: index or offsets out of range");
+    PyErr_SetString(PyExc_ValueError, "gather_items: stride, index or offsets out of range");
     return nullptr;
   }
   return Py_BuildValue("(y#y#y#)", sig.data(), (Py_ssize_t)sig.size(), msg.data(), (Py_ssize_t)msg.size(),
@@ -1055,15 +1157,19 @@ PyMethodDef kMethods[] = {
      "host steps for a batch.  out = [bytearray, bytearray]: sig64 / msgbuf are written into them (grown, never "
      "shrunk: slice to n * 64 and off[n] bytes) and returned"},
     {"scan_batch_u", py_scan_batch_u, METH_VARARGS,
-     "scan_batch_u(msgs, ignore, threads=0, out=None) -> (fast, uidx_u32, uniq, sig64, msgbuf, off, short): "
-     "scan_batch with the identifiers as indices into the batch's distinct identifiers"},
+     "scan_batch_u(msgs, ignore, threads=0, out=None, slot=64) -> (fast, uidx_u32, uniq, sig, msgbuf, off, short): "
+     "scan_batch with the identifiers as indices into the batch's distinct identifiers; slot=96: sig is n "
+     "96-byte signature slots (edverify.h EDV_SIG_SLOT96: base58 text decoded on the GPU, or raw R||S); out "
+     "items may be any writable buffers large enough (e.g. the engine's pinned host memory)"},
     {"results_from", py_results_from, METH_VARARGS,
      "results_from(codes_u8, uidx_u32, uniq) -> list: uniq[uidx[i]] where codes[i] == 1, else None"},
     {"gather_items", py_gather_items, METH_VARARGS,
-     "gather_items(sig64, msgbuf, off, idx_u32) -> (sig64, msgbuf, off) of the selected items"},
+     "gather_items(sig, msgbuf, off, idx_u32, stride=64) -> (sig, msgbuf, off) of the selected items"},
     {"serialize_for_signing", py_serialize_for_signing, METH_VARARGS,
      "serialize_for_signing(obj, ignore=None) -> bytes, or None for the Python path"},
     {"b58decode", py_b58decode, METH_O, "b58decode(str | bytes) -> bytes, or None for the Python path"},
+    {"b58_len64", py_b58_len64, METH_O,
+     "b58_len64(text) -> 1 if b58decode(text) is exactly 64 bytes, 0 if another length, -1 if not base58"},
     {"b58encode_rows", py_b58encode_rows, METH_VARARGS,
      "b58encode_rows(buf, width) -> list of b58encode(row) for each width-byte row (synthetic loads)"},
     {"pack_split64", py_pack_split64, METH_VARARGS,

@@ -46,6 +46,11 @@ SIGNATURES = {
     "edv_verify_batch_keyed": (_I, [_P, _P, _P, _P, _P, _U64, _P]),
     "edv_verify_batch_keyed_device": (_I, [_P, _P, _P, _P, _P, _U64, _P, _P]),
     "edv_verify_spans_device": (_I, [_P, _P, _P, _I, _P, _P, _P, _U64, _P, _P]),
+    "edv_verify_batch_slots": (_I, [_P, _P, _P, _P, _P, _U64, _P]),
+    "edv_verify_batch_keyed_slots": (_I, [_P, _P, _P, _P, _P, _U64, _P]),
+    "edv_host_alloc": (_I, [_P, _U64, _P]),
+    "edv_host_free": (_I, [_P]),
+    "edv_last_host_stats": (_I, [_P, _P]),
     "edv_seed_keypair_batch": (_I, [_P, _P, _U64, _P, _P]),
     "edv_sign_batch_device": (_I, [_P, _P, _P, _P, _P, _U64, _P, _P]),
     "edv_sign_spans_device": (_I, [_P, _P, _P, _P, _P, _P, _U64, _P, _P]),

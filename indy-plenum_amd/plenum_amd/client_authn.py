@@ -102,6 +102,8 @@ VERKEY = 'verkey'
 ROLE = 'role'
 
 KEY_STORE_BYTES = 32 << 30  # HBM for key tables: the window is the widest that fits max_keys
+_SIG_SLOT = 96  # edverify.h EDV_SIG_SLOT96: signatures as base58 text, decoded on the GPU
+_PINNED_MIN_BATCH = 4096  # smaller batches keep the bytearrays (the library stages them cheaply)
 
 
 _MISSING = object()
@@ -158,6 +160,10 @@ class _GpuState:
         # fresh buffers cost a page fault per 4 KiB on every batch); a batch holds the engine
         # lock (_engine_lock) from the scan through the verify, so no other batch writes them
         self.scan_out = [bytearray(), bytearray()]
+        # ... or, on an engine with pinned host memory, these (engine.host_alloc): the GPU call
+        # then copies straight from them; sized from the last batch's message bytes per item
+        self.pinned_out = None
+        self.msg_bytes_per_item = 256.0
         self.stats = {"batches": 0, "batch_items": 0, "cache_hits": 0, "single_verifies": 0, "keyed_items": 0,
                       "keys_registered": 0}
 
@@ -454,18 +460,43 @@ class GpuAuthMixin:
         natively.  Messages the scan leaves to Python (odd types, missing
         fields, bad base58 ...) go through _prepare, which raises the
         reference's exception."""
-        with _engine_lock(self._engine()):
-            return self._authenticate_batch_scanned_into(msgs, self._g.scan_out)
+        eng = self._engine()
+        with _engine_lock(eng):
+            slot = _SIG_SLOT if getattr(eng, "supports_sig_slots", False) else 64
+            return self._authenticate_batch_scanned_into(msgs, self._scan_buffers(eng, len(msgs), slot), slot)
 
-    def _authenticate_batch_scanned_into(self, msgs, out):
+    def _scan_buffers(self, eng, n, slot):
+        """The scan's output buffers for an n-request batch: the engine's pinned
+        host memory (host_alloc) when it has some -- the GPU call then copies
+        from them with no staging copy -- grown ahead of need (never shrunk),
+        else the reused bytearrays."""
+        g = self._g
+        alloc = getattr(eng, "host_alloc", None)
+        if alloc is None or n < _PINNED_MIN_BATCH:
+            return g.scan_out
+        need = (n * slot, int(n * g.msg_bytes_per_item * 1.25) + (64 << 10))
+        bufs = g.pinned_out
+        if bufs is None or any(len(b) < k for b, k in zip(bufs, need)):
+            old = [len(b) for b in bufs] if bufs else [0, 0]
+            try:
+                bufs = [alloc(max(k, int(o * 1.5))) for k, o in zip(need, old)]
+            except Exception:
+                return g.scan_out  # no pinned memory: the library stages (correct, slower)
+            g.pinned_out = bufs
+        return bufs
+
+    def _authenticate_batch_scanned_into(self, msgs, out, slot=64):
         import numpy as np
         n = len(msgs)
         g = self._g
-        fast_b, uidx_b, uniq, sig_o, msg_o, off, short = _scan_batch(msgs, [SIG], g.scan_threads, out)
+        fast_b, uidx_b, uniq, sig_o, msg_o, off, short = _scan_batch(msgs, [SIG], g.scan_threads, out, slot)
         # views of exactly this batch's bytes (released when the batch returns, so the next
         # batch may grow the buffers again)
-        sig64 = memoryview(sig_o)[:64 * n]
-        mbuf = memoryview(msg_o)[:int(np.frombuffer(off, np.uint64)[-1])]
+        mlen = int(np.frombuffer(off, np.uint64)[-1])
+        if n:
+            g.msg_bytes_per_item = max(g.msg_bytes_per_item * 0.5, mlen / n)  # sizes the next batch's buffer
+        sig64 = memoryview(sig_o)[:slot * n]
+        mbuf = memoryview(msg_o)[:mlen]
         fast = np.frombuffer(fast_b, np.uint8).view(bool)
         uidx = np.frombuffer(uidx_b, np.uint32)
         ukeys = [self._key_for(idr) for idr in uniq]  # authenticate():93-99, once per identifier
@@ -475,7 +506,7 @@ class GpuAuthMixin:
         if n and fast_b.count(0) == 0 and not (ucls == 2).any():
             # every item scanned and every identifier resolved (the node's steady state): no index
             # arrays over the batch
-            ok = self._verify_scanned(None, uidx, ukeys, ucls, sig64, mbuf, off, short)
+            ok = self._verify_scanned(None, uidx, ukeys, ucls, sig64, mbuf, off, short, slot)
             results = _results_from(ok.view(np.uint8).tobytes(), uidx_b, uniq)
             for i in np.flatnonzero(~ok).tolist():
                 results[i] = InvalidSignature()
@@ -484,7 +515,7 @@ class GpuAuthMixin:
         icls = ucls[uidx[fidx]] if len(fidx) else np.zeros(0, np.uint8)
         vidx = fidx[icls != 2]  # the items that reach the verify
         codes = np.zeros(n, np.uint8)
-        ok = self._verify_scanned(vidx, uidx, ukeys, ucls, sig64, mbuf, off, short) if len(vidx) else \
+        ok = self._verify_scanned(vidx, uidx, ukeys, ucls, sig64, mbuf, off, short, slot) if len(vidx) else \
             np.zeros(0, bool)
         codes[vidx[ok]] = 1
         results = _results_from(codes.tobytes(), uidx_b, uniq)  # the identifier where verified
@@ -498,10 +529,12 @@ class GpuAuthMixin:
                 results[i] = r
         return results
 
-    def _verify_scanned(self, vidx, uidx, ukeys, ucls, sig64, mbuf, off, short):
+    def _verify_scanned(self, vidx, uidx, ukeys, ucls, sig64, mbuf, off, short, slot=64):
         """Verdicts of the scanned items vidx (None: every item; split sig64 /
         messages of the whole batch; item i's key = ukeys[uidx[i]]): registered
-        keys on the key-table path, the rest one general launch, no key -> False."""
+        keys on the key-table path, the rest one general launch, no key -> False.
+        slot = 96: sig64 holds the scan's signature slots (base58 text decoded
+        on the GPU, edverify.h EDV_SIG_SLOT96)."""
         import numpy as np
         g = self._g
         everything = vidx is None
@@ -550,16 +583,17 @@ class GpuAuthMixin:
             else:
                 s_sig, s_msg, s_off = _gather_items(sig64, mbuf, off,
                                                     (np.arange(m) if everything else vidx)[sel].astype(np.uint32)
-                                                    .tobytes())
-            s_sig = np.frombuffer(s_sig, np.uint8).reshape(-1, 64)
+                                                    .tobytes(), slot)
+            s_sig = np.frombuffer(s_sig, np.uint8).reshape(-1, slot)
             s_msg, s_off = np.frombuffer(s_msg, np.uint8), np.frombuffer(s_off, np.uint64)
+            kw = {"sig_slot": slot} if slot != 64 else {}
             if is_keyed:
-                v = eng.verify_batch_keyed(s_sig, kid_u.astype(np.uint32)[item_u[sel]], s_msg, s_off)
+                v = eng.verify_batch_keyed(s_sig, kid_u.astype(np.uint32)[item_u[sel]], s_msg, s_off, **kw)
                 g.stats["keyed_items"] += cnt
             else:
                 ukey_arr = np.zeros((len(ukeys), 32), np.uint8)
                 ukey_arr[has_key] = np.frombuffer(b"".join(ukey_list), np.uint8).reshape(-1, 32)
-                v = eng.verify_batch(s_sig, ukey_arr[item_u[sel]], s_msg, s_off)
+                v = eng.verify_batch(s_sig, ukey_arr[item_u[sel]], s_msg, s_off, **kw)
             ok[sel] = np.asarray(v, bool)
             g.stats["batches"] += 1
             g.stats["batch_items"] += cnt

@@ -79,6 +79,23 @@ def lengths_mixed(msg_start, msg_end):
     return 4 * int((w.max(axis=1) * cnt).sum()) > 5 * int(blocks.sum())
 
 
+SIG_SLOT = 96  # edverify.h EDV_SIG_SLOT96
+
+
+class _PinnedOwner:
+    """Frees an edv_host_alloc block when the last array over it is gone."""
+    __slots__ = ("lib", "ptr")
+
+    def __init__(self, lib, ptr):
+        self.lib, self.ptr = lib, ptr
+
+    def __del__(self):
+        try:
+            self.lib.edv_host_free(ctypes.c_void_p(self.ptr))
+        except Exception:
+            pass
+
+
 def unpack_bits(bits, n):
     return np.unpackbits(np.asarray(bits, dtype=np.uint8), bitorder="little")[:n].astype(bool)
 
@@ -141,10 +158,53 @@ class EdVerifyEngine:
                                              _ptr(msg_off), n, _ptr(bits)))
         return bits
 
-    def verify_batch(self, sig64, pk32, msgs, msg_off):
-        """Bool array: accepted[i] == (crypto_sign_verify_detached(...) == 0)."""
+    def verify_batch(self, sig64, pk32, msgs, msg_off, sig_slot=64):
+        """Bool array: accepted[i] == (crypto_sign_verify_detached(...) == 0).
+        sig_slot=96: sig64 holds EDV_SIG_SLOT96 slots (base58 text decoded on
+        the GPU, edverify.h)."""
+        if sig_slot == SIG_SLOT:
+            return self._verify_slots(False, sig64, pk32, msgs, msg_off)
         sig64 = _u8(sig64, 64)
         return unpack_bits(self.verify_bits(sig64, pk32, msgs, msg_off), sig64.shape[0])
+
+    supports_sig_slots = True
+
+    def _verify_slots(self, keyed, slots, keys, msgs, msg_off):
+        slots = _u8(slots, SIG_SLOT)
+        keys = np.ascontiguousarray(keys, dtype=np.uint32) if keyed else _u8(keys, 32)
+        msgs = _u8(msgs)
+        msg_off = np.ascontiguousarray(msg_off, dtype=np.uint64)
+        n = slots.shape[0]
+        if keys.shape[0] != n or msg_off.shape[0] != n + 1:
+            raise ValueError("shape mismatch: slots %d, keys %d, off %d" % (n, keys.shape[0], msg_off.shape[0]))
+        if n and int(msg_off[-1]) > msgs.shape[0]:
+            raise ValueError("msg_off exceeds message buffer")
+        bits = np.zeros((n + 7) // 8, dtype=np.uint8)
+        if n:
+            fn = self._lib.edv_verify_batch_keyed_slots if keyed else self._lib.edv_verify_batch_slots
+            check(fn(self._ctx, _ptr(slots), _ptr(keys), _ptr(msgs) if msgs.size else None, _ptr(msg_off), n,
+                     _ptr(bits)))
+        return unpack_bits(bits, n)
+
+    def host_alloc(self, nbytes):
+        """nbytes of pinned host memory (edv_host_alloc) as a writable ctypes
+        array; host-pointer verifies copy inputs inside it to the device with no
+        staging copy.  Freed when the array (and every view of it) is gone."""
+        p = ctypes.c_void_p()
+        check(self._lib.edv_host_alloc(self._ctx, int(nbytes), ctypes.byref(p)))
+        arr = (ctypes.c_ubyte * int(nbytes)).from_address(p.value)
+        arr._owner = _PinnedOwner(self._lib, p.value)
+        return arr
+
+    def last_host_stats(self):
+        """The last host-pointer verify: dict(call_ms, stage_ms, h2d_bytes,
+        direct) -- stage_ms is the CPU copy into pinned staging (0 when every
+        input came from host_alloc memory)."""
+        out = (ctypes.c_double * 4)()
+        check(self._lib.edv_last_host_stats(self._ctx, out))
+        d = int(out[3])
+        return {"call_ms": out[0], "stage_ms": out[1], "h2d_bytes": int(out[2]),
+                "direct": {"sig": bool(d & 1), "keys": bool(d & 2), "msgs": bool(d & 4), "offsets": bool(d & 8)}}
 
     def sign_open_batch(self, sm, sm_off, pk32):
         """crypto_sign_open verdicts over signed messages sm_i = sig || msg
@@ -304,8 +364,11 @@ class EdVerifyEngine:
         check(self._lib.edv_keys_reset(self._ctx))
         self.keys_generation += 1
 
-    def verify_batch_keyed(self, sig64, key_idx, msgs, msg_off):
-        """Verdicts against registered key ids (same predicate as verify_batch)."""
+    def verify_batch_keyed(self, sig64, key_idx, msgs, msg_off, sig_slot=64):
+        """Verdicts against registered key ids (same predicate as verify_batch);
+        sig_slot=96 as verify_batch."""
+        if sig_slot == SIG_SLOT:
+            return self._verify_slots(True, sig64, key_idx, msgs, msg_off)
         sig64 = _u8(sig64, 64)
         key_idx = np.ascontiguousarray(key_idx, dtype=np.uint32)
         msgs = _u8(msgs)

@@ -74,23 +74,33 @@ class MultiEngine:
         return np.concatenate([np.asarray(p, bool) for p in parts])
 
     # -------------------------------------------------------------- verify
-    def verify_batch(self, sig64, pk32, msgs, msg_off):
-        sig64, pk32, msgs = _u8(sig64, 64), _u8(pk32, 32), _u8(msgs)
+    @property
+    def supports_sig_slots(self):
+        return all(getattr(e, "supports_sig_slots", False) for e in self.engines)
+
+    def host_alloc(self, nbytes):
+        """Pinned host memory (portable: every device's copy engine reads it)."""
+        return self.engines[0].host_alloc(nbytes)
+
+    def verify_batch(self, sig64, pk32, msgs, msg_off, sig_slot=64):
+        sig64, pk32, msgs = _u8(sig64, sig_slot), _u8(pk32, 32), _u8(msgs)
         off = np.ascontiguousarray(msg_off, dtype=np.uint64)
+        kw = {"sig_slot": sig_slot} if sig_slot != 64 else {}
         return self._run(sig64.shape[0], lambda e, lo, hi: e.verify_batch(sig64[lo:hi], pk32[lo:hi], msgs,
-                                                                          off[lo:hi + 1]))
+                                                                          off[lo:hi + 1], **kw))
 
     def sign_open_batch(self, sm, sm_off, pk32):
         sm, pk32 = _u8(sm), _u8(pk32, 32)
         off = np.ascontiguousarray(sm_off, dtype=np.uint64)
         return self._run(pk32.shape[0], lambda e, lo, hi: e.sign_open_batch(sm, off[lo:hi + 1], pk32[lo:hi]))
 
-    def verify_batch_keyed(self, sig64, key_idx, msgs, msg_off):
-        sig64, msgs = _u8(sig64, 64), _u8(msgs)
+    def verify_batch_keyed(self, sig64, key_idx, msgs, msg_off, sig_slot=64):
+        sig64, msgs = _u8(sig64, sig_slot), _u8(msgs)
         kidx = np.ascontiguousarray(key_idx, dtype=np.uint32)
         off = np.ascontiguousarray(msg_off, dtype=np.uint64)
+        kw = {"sig_slot": sig_slot} if sig_slot != 64 else {}
         return self._run(sig64.shape[0], lambda e, lo, hi: e.verify_batch_keyed(sig64[lo:hi], kidx[lo:hi], msgs,
-                                                                                off[lo:hi + 1]))
+                                                                                off[lo:hi + 1], **kw))
 
     # ---------------------------------------------------- replicated key store
     def keys_reset(self):
@@ -102,15 +112,24 @@ class MultiEngine:
         for e in self.engines:
             e.keys_set_window(w)
 
+    def _each(self, fn):
+        """fn(engine) on every device at once (a host thread per device; the
+        ctypes calls release the GIL, so the table builds run concurrently)."""
+        if self._pool is None:
+            return [fn(e) for e in self.engines]
+        futs = [self._pool.submit(fn, e) for e in self.engines]
+        return [f.result() for f in futs]
+
     def keys_add(self, pk32):
-        firsts = {e.keys_add(pk32) for e in self.engines}
+        pk32 = _u8(pk32, 32)
+        firsts = set(self._each(lambda e: e.keys_add(pk32)))
         if len(firsts) != 1:
             raise RuntimeError("key stores of the devices diverged (first ids %s)" % sorted(firsts))
         return firsts.pop()
 
     def keys_set(self, first_id, pk32):
-        for e in self.engines:
-            e.keys_set(first_id, pk32)
+        pk32 = _u8(pk32, 32)
+        self._each(lambda e: e.keys_set(first_id, pk32))
 
     def keys_count(self):
         return self.engines[0].keys_count()

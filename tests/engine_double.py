@@ -52,7 +52,38 @@ class OracleEngine:
     def keys_count(self):
         return len(self.keys)
 
-    def verify_batch_keyed(self, sig64, key_idx, msgs, msg_off):
+    # signature slots (edverify.h EDV_SIG_SLOT96), decoded here the way the
+    # slot contract states: text -> its 512-bit big-endian base58 value
+    supports_sig_slots = True
+    slot_text_items = 0
+    _B58 = "123456789ABCDEFGHJKLMNPQRSTUVWXYZabcdefghijkmnopqrstuvwxyz"
+
+    def host_alloc(self, nbytes):
+        """Plain host memory standing in for edv_host_alloc's pinned blocks."""
+        self.host_allocs = getattr(self, "host_allocs", 0) + 1
+        return (ctypes.c_ubyte * int(nbytes))()
+
+    def _sig64(self, sig, sig_slot):
+        if sig_slot == 64:
+            return sig
+        assert sig_slot == 96
+        slots = np.asarray(sig, np.uint8).reshape(-1, 96)
+        out = np.zeros((slots.shape[0], 64), np.uint8)
+        for i, s in enumerate(slots):
+            t = int(s[95])
+            if t == 0:
+                out[i] = s[:64]
+                continue
+            v = 0
+            for c in bytes(s[:t]).decode("ascii"):
+                v = v * 58 + self._B58.index(c)
+            assert v < 1 << 512, "slot text beyond 64 bytes"
+            out[i] = np.frombuffer(v.to_bytes(64, "big"), np.uint8)
+            self.slot_text_items += 1
+        return out
+
+    def verify_batch_keyed(self, sig64, key_idx, msgs, msg_off, sig_slot=64):
+        sig64 = self._sig64(sig64, sig_slot)
         self.keyed_calls += 1
         pk = np.frombuffer(b"".join(self.keys[int(k)] if int(k) < len(self.keys) else b"\0" * 32
                                     for k in key_idx), np.uint8).reshape(-1, 32)
@@ -69,9 +100,9 @@ class OracleEngine:
         return np.array([self.lib.oracle_sign_open(sm[off[i]:off[i + 1]], off[i + 1] - off[i], pk32[i].tobytes()) == 0
                          for i in range(len(off) - 1)], dtype=bool)
 
-    def verify_batch(self, sig64, pk32, msgs, msg_off):
+    def verify_batch(self, sig64, pk32, msgs, msg_off, sig_slot=64):
         self.calls += 1
-        return self._verify(sig64, pk32, msgs, msg_off)
+        return self._verify(self._sig64(sig64, sig_slot), pk32, msgs, msg_off)
 
     def _verify(self, sig64, pk32, msgs, msg_off):
         msgs = bytes(msgs) if not isinstance(msgs, np.ndarray) else msgs.tobytes()

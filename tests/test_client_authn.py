@@ -451,3 +451,49 @@ def test_scanned_batch_fuzz(oracle):
                 want.append(_outcome(ex))
         assert got == want
         assert sum(isinstance(x, str) for x in got) > 10
+
+
+def test_scan_slots_into_engine_buffers(oracle):
+    """A batch large enough for the engine's (pinned) host buffers: the scan
+    writes signature slots (base58 text for signatures that decode to 64
+    bytes, raw R || S otherwise) straight into host_alloc memory; verdicts ==
+    authenticate() per message, including 63- / 65-byte signatures (split at
+    byte 64 on the host) and non-base58 ones."""
+    from plenum_amd.base58 import b58decode, b58encode
+    idrs, vks, msgs = _signed(4, 64, seed=6)
+    pool = []
+    for k in range(4200):
+        m = dict(msgs[k % 64])
+        r = k % 50
+        if r == 1:
+            m["reqId"] += 7  # tampered
+        elif r == 2:
+            m["signature"] = b58encode(b58decode(m["signature"])[:63])  # 63 bytes: ser[0] joins the signature
+        elif r == 3:
+            m["signature"] = b58encode(b58decode(m["signature"]) + b"\x01")  # 65 bytes: spills into M
+        elif r == 4:
+            m["signature"] = "0OIl" + m["signature"][4:]  # not base58
+        elif r == 5:
+            m["signature"] = b58encode(b"\0\0" + b58decode(m["signature"])[2:])  # leading '1's, 64 bytes
+        pool.append(m)
+    eng = OracleEngine(oracle)
+    a = GpuAuthNr(engine=eng)
+    for idr, vk in zip(idrs, vks):
+        a.addIdr(idr, vk)
+    got = [_outcome(r) for r in a.authenticate_batch(pool)]
+    assert getattr(eng, "host_allocs", 0) == 2 and eng.slot_text_items > 3800
+    ref = GpuAuthNr(engine=OracleEngine(oracle), max_keys=0)
+    for idr, vk in zip(idrs, vks):
+        ref.addIdr(idr, vk)
+    want = []
+    for m in pool[:400]:
+        try:
+            want.append(_outcome(ref.authenticate(m)))
+        except Exception as ex:
+            want.append(_outcome(ex))
+    assert got[:400] == want
+    assert got == got[:200] * 21
+    # a second, larger batch grows the buffers; a smaller one reuses them
+    a.authenticate_batch(pool + pool[:3000])
+    a.authenticate_batch(pool[:4100])
+    assert eng.host_allocs == 4

@@ -484,3 +484,46 @@ def test_spans_share_messages(gpu_engine):
         gpu_engine.set_length_buckets("auto")
         got = np.unpackbits(words.cpu().numpy().view(np.uint8), bitorder="little")[:n].astype(bool)
         assert (got == want).all(), (keyed, mode)
+
+
+def test_sig_slots_match_sig64(gpu_engine, oracle):
+    """EDV_SIG_SLOT96: the same batch as 64-byte signatures and as slots
+    (base58 text where it decodes to 64 bytes, else raw) gives identical
+    verdicts on both paths; texts with leading '1's (R with leading zero
+    bytes), the all-'1' text (64 zero bytes), raw slots and corrupted texts
+    included; a sample agrees with the oracle."""
+    from plenum_amd import _hostpack, pack_messages
+    rng = np.random.default_rng(31)
+    n = 40000
+    seeds = rng.integers(0, 256, size=(16, 32), dtype=np.uint8)
+    pk, sk = gpu_engine.seed_keypair_batch(seeds)
+    msgs = [bytes(rng.integers(0, 256, size=int(rng.integers(0, 300)), dtype=np.uint8)) for _ in range(n)]
+    buf, off = pack_messages(msgs)
+    kidx = (np.arange(n) % 16).astype(np.uint32)
+    sig = gpu_engine.sign_batch(sk, kidx, buf, off)
+    sig[::7, 50] ^= 4                      # corrupted S
+    sig[1] = 0                             # all zero: the text is 64 '1's
+    sig[2, :3] = 0                         # leading zero bytes
+    texts = _hostpack.b58encode_rows(sig.tobytes(), 64)
+    slots = np.zeros((n, 96), np.uint8)
+    raw = np.zeros(n, bool)
+    raw[::13] = True                       # host-decoded slots
+    for i, t in enumerate(texts):
+        assert _hostpack.b58_len64(t) == 1
+        if raw[i]:
+            slots[i, :64] = sig[i]
+        else:
+            slots[i, :len(t)] = np.frombuffer(t.encode(), np.uint8)
+            slots[i, 95] = len(t)
+    assert (slots[:, 95] > 0).sum() > 30000 and texts[1] == "1" * 64 and texts[2].startswith("111")
+    want = gpu_engine.verify_batch(sig, pk[kidx], buf, off)
+    got = gpu_engine.verify_batch(slots, pk[kidx], buf, off, sig_slot=96)
+    assert (got == want).all() and want.sum() > n * 0.8
+    uniq_ids = gpu_engine.keys_add(pk)
+    try:
+        gotk = gpu_engine.verify_batch_keyed(slots, kidx + uniq_ids, buf, off, sig_slot=96)
+        assert (gotk == want).all()
+    finally:
+        gpu_engine.keys_reset()
+    idx = rng.choice(n, 500, replace=False)
+    assert (_oracle_sample(oracle, sig, pk[kidx], buf, off, idx) == got[idx]).all()
