@@ -422,16 +422,14 @@ def main():
         n_keys = -(-(n // 2) * world // (2 * V))  # every vote g // (2V) has its key (ceil)
         nv = n // 2
         g = np.arange(nv, dtype=np.int64) + rank * nv
-        v_key = (g // (2 * V)).astype(np.uint32)
-        v_phase = ((g % (2 * V)) // V).astype(np.uint8)
-        v_voter = (g % V).astype(np.uint8)
-        keep = np.random.default_rng(40 + rank).random(nv) >= 0.05
+        # which votes are present: per-key classes (synth.c4_votes) -- half the keys ~5% random drops,
+        # the rest exactly at / one below the prepare (16) or commit (17) quorum of n = 25, the
+        # prepare ones with the primary's PREPARE present (it must not count, replica.py:1289-1291)
+        v_key, v_phase, v_voter, keep, _ = synth.c4_votes(g, V)
         d_vkey, d_vphase, d_vvoter = (torch.from_numpy(a).to(dev) for a in
-                                      (v_key.astype(np.int32), v_phase, v_voter))
+                                      (v_key.astype(np.int32), v_phase.astype(np.uint8), v_voter.astype(np.uint8)))
         d_keep = torch.from_numpy(keep.astype(np.uint8)).to(dev)
-        # the primary of each key's view (view = key // 1000, primary = view % V):
-        # its PREPARE never counts (replica.py:1289-1291)
-        primary = ((np.arange(n_keys) // 1000) % V).astype(np.uint8)
+        primary = synth.c4_primary(n_keys, V)
         d_primary = torch.from_numpy(primary).to(dev)
         d_ballot = torch.zeros(n_keys * 2 * V, dtype=torch.uint8, device=dev)
         d_counts = torch.zeros(n_keys * 2, dtype=torch.int32, device=dev)
@@ -452,21 +450,34 @@ def main():
         step = step_c4
 
         def tally_check():
-            # expected: every rank's kept votes (all signatures valid here)
+            # expected: every rank's present votes (all signatures valid here), the primary's PREPARE dropped
             cnt = np.zeros(n_keys * 2, np.int64)
+            cnt_naive = np.zeros(n_keys, np.int64)
+            cls_of = np.zeros(n_keys, np.int64)
             for r in range(world):
-                gr = np.arange(nv, dtype=np.int64) + r * nv
-                kr = np.random.default_rng(40 + r).random(nv) >= 0.05
-                kk, ph, vv = gr // (2 * V), (gr % (2 * V)) // V, gr % V
+                kk, ph, vv, kr, cl = synth.c4_votes(np.arange(nv, dtype=np.int64) + r * nv, V)
+                np.add.at(cnt_naive, kk[ph == 0], kr[ph == 0].astype(np.int64))
+                cls_of[kk] = cl
                 kr &= ~((ph == 0) & (vv == primary[kk]))
                 np.add.at(cnt, kk * 2 + ph, kr.astype(np.int64))
             f = (V - 1) // 3
             q = ((cnt[0::2] >= V - f - 1).astype(np.uint8) | ((cnt[1::2] >= V - f).astype(np.uint8) << 1))
             got_c = d_counts.cpu().numpy().astype(np.int64)
             got_q = d_quorum.cpu().numpy()
+            by_class = {}
+            for c, name in enumerate(synth.C4_CLASSES):
+                sel = cls_of == c
+                d = by_class.setdefault(name, {"keys": 0, "prepare_quorums": 0, "commit_quorums": 0})
+                d["keys"] += int(sel.sum())
+                d["prepare_quorums"] += int((got_q[sel] & 1).sum())
+                d["commit_quorums"] += int((got_q[sel] >> 1 & 1).sum())
             return {"keys": n_keys, "votes_per_gpu": nv, "validators": V,
                     "counts_match": bool((got_c == cnt).all()), "quorum_match": bool((got_q == q).all()),
-                    "prepare_quorums": int((got_q & 1).sum()), "commit_quorums": int((got_q >> 1 & 1).sum())}
+                    "prepare_quorums": int((got_q & 1).sum()), "commit_quorums": int((got_q >> 1 & 1).sum()),
+                    "keys_below_prepare_quorum": int((q & 1 == 0).sum()),
+                    "keys_below_commit_quorum": int((q >> 1 & 1 == 0).sum()),
+                    "keys_decided_by_primary_rule": int(((cnt_naive >= V - f - 1) != (cnt[0::2] >= V - f - 1)).sum()),
+                    "by_class": by_class}
 
     for _ in range(args.warmup):
         step()

@@ -146,3 +146,60 @@ def corrupt_configs2(sig, pk, msgs, off, rng):
     expect = np.ones(n, dtype=bool)
     expect[bad] = False
     return expect
+
+
+# ---- configs[4] votes -------------------------------------------------------
+def _mix64(x):
+    """splitmix64 finalizer over uint64 arrays (a deterministic per-vote hash,
+    the same on every rank)."""
+    x = np.asarray(x, np.uint64)
+    with np.errstate(over="ignore"):
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return x ^ (x >> np.uint64(31))
+
+
+C4_CLASSES = ("random", "random", "random", "random", "prepare_below", "prepare_at", "commit_below", "commit_at")
+
+
+def c4_votes(g, n_validators, view_len=1000):
+    """configs[4] vote g (global index over all ranks): key g // (2V), phase
+    (g % 2V) // V (0 PREPARE, 1 COMMIT), voter g % V; the primary of the key's
+    view (view = key // view_len, primary = view % V) -- its PREPARE never
+    counts (replica.py:1289-1291).  Which votes are present is decided per key
+    class (hash of the key, C4_CLASSES) so the tally has decisions to make at
+    full size (n = 25: prepare quorum 16, commit quorum 17, quorums.py:15-32):
+      random         each vote present with p = 0.95;
+      prepare_below  15 non-primary PREPAREs + the primary's (16 if the
+                     primary were counted: the rule decides the quorum);
+      prepare_at     16 non-primary PREPAREs + the primary's;
+      commit_below   16 COMMITs;  commit_at  17 COMMITs;
+    (the other phase of those keys random).  Returns (key, phase, voter,
+    present, primary_of_key_fn) as arrays over g."""
+    V = n_validators
+    g = np.asarray(g, np.int64)
+    key = g // (2 * V)
+    phase = (g % (2 * V)) // V
+    voter = g % V
+    prim = (key // view_len) % V
+    cls = (_mix64(key.astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15)) % np.uint64(8)).astype(np.int64)
+    u = (_mix64(g.astype(np.uint64) + np.uint64(0x51ED2701)) >> np.uint64(11)).astype(np.float64) / float(1 << 53)
+    present = u >= 0.05
+    o_prep = (voter - prim - 1) % V                      # 0..V-2 for the other voters, V-1 for the primary
+    o_com = (voter - (key * 7) % V) % V                  # a window of committers per key
+    is_p, is_c = phase == 0, phase == 1
+    for c, name in enumerate(C4_CLASSES):
+        sel = cls == c
+        if name == "prepare_below":
+            present = np.where(sel & is_p, (o_prep < 15) | (voter == prim), present)
+        elif name == "prepare_at":
+            present = np.where(sel & is_p, (o_prep < 16) | (voter == prim), present)
+        elif name == "commit_below":
+            present = np.where(sel & is_c, o_com < 16, present)
+        elif name == "commit_at":
+            present = np.where(sel & is_c, o_com < 17, present)
+    return key, phase, voter, present, cls
+
+
+def c4_primary(n_keys, n_validators, view_len=1000):
+    return ((np.arange(n_keys) // view_len) % n_validators).astype(np.uint8)

@@ -43,3 +43,7 @@ def test_bench_two_ranks_one_gpu():
     assert p["accepted_in_gathered_bitmask"] == 2 * 160000
     assert d["tally"]["counts_match"] and d["tally"]["quorum_match"]
     assert d["tally"]["prepare_quorums"] > 0 and d["tally"]["commit_quorums"] > 0
+    # near-threshold keys (synth.c4_votes): quorums missed by one vote, and keys whose prepare quorum
+    # the primary-PREPARE rule decides, checked across the two ranks' unioned ballots
+    assert d["tally"]["keys_below_prepare_quorum"] > 0 and d["tally"]["keys_below_commit_quorum"] > 0
+    assert d["tally"]["keys_decided_by_primary_rule"] > 0

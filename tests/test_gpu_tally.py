@@ -48,6 +48,36 @@ def test_tally_c4_shape(gpu_engine):
     assert (counts == c2).all() and (prep == p2).all() and (com == m2).all()
 
 
+def test_tally_c4_near_threshold_160k(gpu_engine):
+    """configs[4] at one GPU's full size (160,000 keys x 25 validators x 2
+    phases, 8M votes) with the bench's vote classes (synth.c4_votes): keys
+    exactly at and one vote below the prepare (16) and commit (17) quorums,
+    the primary's PREPARE present on the prepare ones.  GPU == tally_oracle,
+    and every class decides as constructed (prepare_below would reach quorum
+    if the primary's PREPARE counted)."""
+    from plenum_amd import synth
+    n_keys, nv = 160_000, 25
+    key, ph, v, present, cls = synth.c4_votes(np.arange(n_keys * 2 * nv), nv)
+    primary = synth.c4_primary(n_keys, nv)
+    counts, prep, com = gpu_engine.tally(key, v, ph, present.astype(np.uint8), n_keys, nv, primary=primary)
+    c2, p2, m2 = tally_oracle.tally(key, v, ph, present.astype(np.uint8), n_keys, nv, primary=primary)
+    assert (counts == c2).all() and (prep == p2).all() and (com == m2).all()
+    kcls = cls[::2 * nv]
+    want = {"prepare_below": (False, None, 15), "prepare_at": (True, None, 16),
+            "commit_below": (None, False, 16), "commit_at": (None, True, 17)}
+    for c, name in enumerate(synth.C4_CLASSES):
+        sel = kcls == c
+        assert sel.sum() > 10000, name
+        if name in want:
+            wp, wc, cnt = want[name]
+            if wp is not None:
+                assert (prep[sel] == wp).all() and (counts[sel, 0] == cnt).all(), name
+            if wc is not None:
+                assert (com[sel] == wc).all() and (counts[sel, 1] == cnt).all(), name
+    naive_c, naive_p, _ = tally_oracle.tally(key, v, ph, present.astype(np.uint8), n_keys, nv)
+    assert naive_p[kcls == synth.C4_CLASSES.index("prepare_below")].all()
+
+
 def _kat():
     import json
     from conftest import GOLDEN

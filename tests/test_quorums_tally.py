@@ -98,3 +98,23 @@ def test_ballot_union_equals_set_union():
                    tally_oracle.ballots_from_votes(k[half:], v[half:], p[half:], ok[half:], n_keys, nv))
     counts, _, _ = tally_oracle.tally(k, v, p, ok, n_keys, nv)
     assert (b.sum(axis=2) == counts).all()
+
+
+def test_c4_vote_classes_decide_at_the_thresholds():
+    """synth.c4_votes (bench configs[4], tests/test_gpu_tally.py): on the CPU
+    oracle every class decides as constructed at n = 25, identically on any
+    split of the global vote range into ranks."""
+    import numpy as np
+    import tally_oracle
+    from plenum_amd import synth
+    n_keys, V = 4000, 25
+    g = np.arange(n_keys * 2 * V)
+    k, ph, v, pres, cls = synth.c4_votes(g, V)
+    prim = synth.c4_primary(n_keys, V)
+    c, p, m = tally_oracle.tally(k, v, ph, pres.astype(np.uint8), n_keys, V, primary=prim)
+    kc = cls[::2 * V]
+    names = synth.C4_CLASSES
+    assert not p[kc == names.index("prepare_below")].any() and p[kc == names.index("prepare_at")].all()
+    assert not m[kc == names.index("commit_below")].any() and m[kc == names.index("commit_at")].all()
+    halves = [synth.c4_votes(part, V) for part in np.array_split(g, 3)]
+    assert all((np.concatenate([h[i] for h in halves]) == x).all() for i, x in enumerate((k, ph, v, pres, cls)))
