@@ -193,6 +193,19 @@ int edv_verify_batch_slots(edv_ctx *ctx, const uint8_t *sig_slots, const uint8_t
 int edv_verify_batch_keyed_slots(edv_ctx *ctx, const uint8_t *sig_slots, const uint32_t *key_idx, const uint8_t *msgs,
                                  const uint64_t *msg_off, uint64_t n, uint8_t *accept_bits);
 
+/* Asynchronous form of the host-pointer verifies (the authenticator overlaps
+ * its scan of the next part of a batch with the GPU work of this one).
+ * edv_verify_submit queues the copies, kernels and bitmask read-back and
+ * returns a ticket; inputs outside edv_host_alloc memory are copied before it
+ * returns, inputs inside it are read by DMA later and must stay unchanged
+ * until edv_verify_collect(ticket) has returned, which waits and writes the
+ * (n + 7) / 8 accept bytes.  keyed: keys = uint32 key ids, else n * 32 key
+ * bytes; sig_format: 64 (R || S) or EDV_SIG_SLOT96.  Submissions complete in
+ * order; every ticket should be collected (the 64 most recent are kept). */
+int edv_verify_submit(edv_ctx *ctx, int keyed, const uint8_t *sig, int sig_format, const uint8_t *keys,
+                      const uint8_t *msgs, const uint64_t *msg_off, uint64_t n, uint64_t *ticket);
+int edv_verify_collect(edv_ctx *ctx, uint64_t ticket, uint8_t *accept_bits);
+
 /* Pinned host memory (hipHostMalloc, portable to every device).  A host-
  * pointer verify whose inputs (signatures, keys, messages, offsets) lie in
  * such blocks copies them to the device straight from there, with no CPU

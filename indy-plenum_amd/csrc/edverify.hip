@@ -1054,6 +1054,19 @@ struct edv_ctx {
   Buf h_sig[kSlots], h_key[kSlots], h_msg[kSlots], h_off[kSlots], h_bits[kSlots];
   Buf d_sig[kSlots], d_key[kSlots], d_msg[kSlots], d_off[kSlots], d_bits[kSlots];
   Buf d_slot[kSlots];  // EDV_SIG_SLOT96 input of edv_b58_sig_kernel
+  // Asynchronous host-pointer verifies (edv_verify_submit / edv_verify_collect): which
+  // submission's chunk each slot holds, and per submission its accept bits so far.
+  struct SlotUse {
+    uint64_t ticket = 0;  // 0 = free
+    uint64_t c0 = 0, cn = 0;
+  } slot_use[kSlots];
+  struct Pending {
+    uint64_t ticket = 0, n = 0;
+    std::vector<uint8_t> bits;
+  };
+  std::vector<Pending> pending;
+  uint64_t next_ticket = 1;
+  uint64_t next_slot = 0;  // round robin over the slots, across submissions
   // what the last host-pointer verify did (edv_last_host_stats)
   double last_stage_ms = 0.0;   // CPU copies into the pinned staging (0 when every source was pinned)
   double last_call_ms = 0.0;    // the whole call
@@ -1512,8 +1525,22 @@ static void stage_copy(void* dst, const void* src, size_t n) {
   });
 }
 
-static int host_verify(edv_ctx* ctx, bool keyed, const uint8_t* sig, uint64_t sig_stride, const uint8_t* keys,
-                       const uint8_t* msgs, const uint64_t* msg_off, uint64_t n, uint8_t* accept_bits) {
+// A slot's chunk done: its bits into its submission's buffer, the slot free.
+static int drain_slot(edv_ctx* ctx, int sl) {
+  edv_ctx::SlotUse& u = ctx->slot_use[sl];
+  if (!u.ticket) return 0;
+  HIP_TRY(hipEventSynchronize(ctx->ev_done[sl]));
+  for (edv_ctx::Pending& p : ctx->pending)
+    if (p.ticket == u.ticket) {
+      memcpy(p.bits.data() + u.c0 / 8, ctx->h_bits[sl].p, (u.cn + 7) / 8);
+      break;
+    }
+  u.ticket = 0;
+  return 0;
+}
+
+static int host_submit(edv_ctx* ctx, bool keyed, const uint8_t* sig, uint64_t sig_stride, const uint8_t* keys,
+                       const uint8_t* msgs, const uint64_t* msg_off, uint64_t n, uint64_t* ticket_out) {
   using clk = std::chrono::steady_clock;
   const auto t_call = clk::now();
   double stage_s = 0.0;
@@ -1529,16 +1556,10 @@ static int host_verify(edv_ctx* ctx, bool keyed, const uint8_t* sig, uint64_t si
   const bool off_direct = pinned_range(msg_off, 8 * (n + 1));
   ctx->last_direct = (sig_direct ? 1 : 0) | (key_direct ? 2 : 0) | (msg_direct ? 4 : 0) | (off_direct ? 8 : 0);
   ctx->last_h2d_bytes = 0;
-  const uint64_t nchunks = div_up(n, kHostChunk);
-  uint64_t pend[edv_ctx::kSlots] = {};  // chunk index + 1 whose bits sit in the slot (0 = none)
-  auto drain = [&](int sl) -> int {     // wait for the slot's chunk, copy its bits out
-    if (!pend[sl]) return 0;
-    HIP_TRY(hipEventSynchronize(ctx->ev_done[sl]));
-    const uint64_t c = pend[sl] - 1, c0 = c * kHostChunk, cn = (n - c0) < kHostChunk ? (n - c0) : kHostChunk;
-    memcpy(accept_bits + c0 / 8, ctx->h_bits[sl].p, (cn + 7) / 8);
-    pend[sl] = 0;
-    return 0;
-  };
+  const uint64_t ticket = ctx->next_ticket++;
+  // submissions never collected (a caller that went away) are forgotten after a while
+  while (ctx->pending.size() >= 64) ctx->pending.erase(ctx->pending.begin());
+  ctx->pending.push_back(edv_ctx::Pending{ticket, n, std::vector<uint8_t>((size_t)((n + 7) / 8), 0)});
   // a source the copy engine reads: the caller's pinned memory, or the slot's staging after a CPU copy
   auto source = [&](bool direct, edv_ctx::Buf& stage, const uint8_t* src, uint64_t bytes, bool threaded,
                     const uint8_t** out) -> int {
@@ -1557,55 +1578,96 @@ static int host_verify(edv_ctx* ctx, bool keyed, const uint8_t* sig, uint64_t si
     *out = (const uint8_t*)stage.p;
     return 0;
   };
-  int r;
-  for (uint64_t c = 0; c < nchunks; ++c) {
-    const int sl = (int)(c % edv_ctx::kSlots);
-    if ((r = drain(sl))) return r;
-    const uint64_t c0 = c * kHostChunk, cn = (n - c0) < kHostChunk ? (n - c0) : kHostChunk;
-    const uint64_t m0 = msg_off[c0], mbytes = msg_off[c0 + cn] - m0, nwords = div_up(cn, 64);
-    if ((r = ensure_pinned(ctx->h_bits[sl], 8 * nwords)) || (r = ensure(ctx->d_sig[sl], 64 * cn)) ||
-        (r = ensure(ctx->d_key[sl], key_bytes * cn)) || (r = ensure(ctx->d_msg[sl], mbytes + 16)) ||
-        (r = ensure(ctx->d_off[sl], 8 * (cn + 1))) || (r = ensure(ctx->d_bits[sl], 8 * nwords)) ||
-        (slots && (r = ensure(ctx->d_slot[sl], sig_stride * cn))))
-      return r;
-    const uint8_t *s_sig, *s_key, *s_msg, *s_off;
-    if ((r = source(sig_direct, ctx->h_sig[sl], sig + sig_stride * c0, sig_stride * cn, true, &s_sig)) ||
-        (r = source(key_direct, ctx->h_key[sl], keys + key_bytes * c0, key_bytes * cn, false, &s_key)) ||
-        (r = source(msg_direct, ctx->h_msg[sl], msgs ? msgs + m0 : nullptr, mbytes, true, &s_msg)) ||
-        (r = source(off_direct, ctx->h_off[sl], (const uint8_t*)(msg_off + c0), 8 * (cn + 1), false, &s_off)))
-      return r;
-    set_bucketing(ctx, ctx->bucket_mode == 2 && lengths_mixed(msg_off + c0, cn));
-    hipStream_t cs = ctx->stream_copy;
-    void* d_sig_in = slots ? ctx->d_slot[sl].p : ctx->d_sig[sl].p;
-    HIP_TRY(hipMemcpyAsync(d_sig_in, s_sig, sig_stride * cn, hipMemcpyHostToDevice, cs));
-    HIP_TRY(hipMemcpyAsync(ctx->d_key[sl].p, s_key, key_bytes * cn, hipMemcpyHostToDevice, cs));
-    if (mbytes) HIP_TRY(hipMemcpyAsync(ctx->d_msg[sl].p, s_msg, mbytes, hipMemcpyHostToDevice, cs));
-    HIP_TRY(hipMemcpyAsync(ctx->d_off[sl].p, s_off, 8 * (cn + 1), hipMemcpyHostToDevice, cs));
-    HIP_TRY(hipEventRecord(ctx->ev_h2d[sl], cs));
-    ctx->last_h2d_bytes += sig_stride * cn + key_bytes * cn + mbytes + 8 * (cn + 1);
-    hipStream_t st = ctx->stream;
-    HIP_TRY(hipStreamWaitEvent(st, ctx->ev_h2d[sl], 0));
-    if (slots) {
-      hipLaunchKernelGGL(edv_b58_sig_kernel, dim3((uint32_t)div_up(cn, kBlock)), dim3(kBlock), 0, st,
-                         (const uint8_t*)ctx->d_slot[sl].p, cn, (uint8_t*)ctx->d_sig[sl].p);
-      HIP_TRY(hipGetLastError());
+  auto run = [&]() -> int {
+    int r;
+    for (uint64_t c0 = 0; c0 < n; c0 += kHostChunk) {
+      const int sl = (int)(ctx->next_slot++ % edv_ctx::kSlots);
+      if ((r = drain_slot(ctx, sl))) return r;  // the slot's previous chunk (this or an earlier submission)
+      const uint64_t cn = (n - c0) < kHostChunk ? (n - c0) : kHostChunk;
+      const uint64_t m0 = msg_off[c0], mbytes = msg_off[c0 + cn] - m0, nwords = div_up(cn, 64);
+      if ((r = ensure_pinned(ctx->h_bits[sl], 8 * nwords)) || (r = ensure(ctx->d_sig[sl], 64 * cn)) ||
+          (r = ensure(ctx->d_key[sl], key_bytes * cn)) || (r = ensure(ctx->d_msg[sl], mbytes + 16)) ||
+          (r = ensure(ctx->d_off[sl], 8 * (cn + 1))) || (r = ensure(ctx->d_bits[sl], 8 * nwords)) ||
+          (slots && (r = ensure(ctx->d_slot[sl], sig_stride * cn))))
+        return r;
+      const uint8_t *s_sig, *s_key, *s_msg, *s_off;
+      if ((r = source(sig_direct, ctx->h_sig[sl], sig + sig_stride * c0, sig_stride * cn, true, &s_sig)) ||
+          (r = source(key_direct, ctx->h_key[sl], keys + key_bytes * c0, key_bytes * cn, false, &s_key)) ||
+          (r = source(msg_direct, ctx->h_msg[sl], msgs ? msgs + m0 : nullptr, mbytes, true, &s_msg)) ||
+          (r = source(off_direct, ctx->h_off[sl], (const uint8_t*)(msg_off + c0), 8 * (cn + 1), false, &s_off)))
+        return r;
+      set_bucketing(ctx, ctx->bucket_mode == 2 && lengths_mixed(msg_off + c0, cn));
+      hipStream_t cs = ctx->stream_copy;
+      void* d_sig_in = slots ? ctx->d_slot[sl].p : ctx->d_sig[sl].p;
+      HIP_TRY(hipMemcpyAsync(d_sig_in, s_sig, sig_stride * cn, hipMemcpyHostToDevice, cs));
+      HIP_TRY(hipMemcpyAsync(ctx->d_key[sl].p, s_key, key_bytes * cn, hipMemcpyHostToDevice, cs));
+      if (mbytes) HIP_TRY(hipMemcpyAsync(ctx->d_msg[sl].p, s_msg, mbytes, hipMemcpyHostToDevice, cs));
+      HIP_TRY(hipMemcpyAsync(ctx->d_off[sl].p, s_off, 8 * (cn + 1), hipMemcpyHostToDevice, cs));
+      HIP_TRY(hipEventRecord(ctx->ev_h2d[sl], cs));
+      ctx->last_h2d_bytes += sig_stride * cn + key_bytes * cn + mbytes + 8 * (cn + 1);
+      hipStream_t st = ctx->stream;
+      HIP_TRY(hipStreamWaitEvent(st, ctx->ev_h2d[sl], 0));
+      if (slots) {
+        hipLaunchKernelGGL(edv_b58_sig_kernel, dim3((uint32_t)div_up(cn, kBlock)), dim3(kBlock), 0, st,
+                           (const uint8_t*)ctx->d_slot[sl].p, cn, (uint8_t*)ctx->d_sig[sl].p);
+        HIP_TRY(hipGetLastError());
+      }
+      const uint64_t* d_off = (const uint64_t*)ctx->d_off[sl].p;
+      // the offsets are the caller's (starting at m0): the kernels address msgs + off[i]
+      const uint8_t* d_msg_base = (const uint8_t*)ctx->d_msg[sl].p - m0;
+      if ((r = launch_pipeline(ctx, keyed, ctx->d_sig[sl].p, ctx->d_key[sl].p, d_msg_base, d_off, d_off + 1, cn,
+                               ctx->d_bits[sl].p, st)))
+        return r;
+      HIP_TRY(hipMemcpyAsync(ctx->h_bits[sl].p, ctx->d_bits[sl].p, 8 * nwords, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipEventRecord(ctx->ev_done[sl], st));
+      ctx->slot_use[sl] = edv_ctx::SlotUse{ticket, c0, cn};
     }
-    const uint64_t* d_off = (const uint64_t*)ctx->d_off[sl].p;
-    // the offsets are the caller's (starting at m0): the kernels address msgs + off[i]
-    const uint8_t* d_msg_base = (const uint8_t*)ctx->d_msg[sl].p - m0;
-    if ((r = launch_pipeline(ctx, keyed, ctx->d_sig[sl].p, ctx->d_key[sl].p, d_msg_base, d_off, d_off + 1, cn,
-                             ctx->d_bits[sl].p, st)))
-      return r;
-    HIP_TRY(hipMemcpyAsync(ctx->h_bits[sl].p, ctx->d_bits[sl].p, 8 * nwords, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipEventRecord(ctx->ev_done[sl], st));
-    pend[sl] = c + 1;
-  }
-  for (int sl = 0; sl < edv_ctx::kSlots; ++sl)
-    if ((r = drain(sl))) return r;
-  if (n & 7) accept_bits[n / 8] &= (uint8_t)((1u << (n & 7)) - 1);
+    return 0;
+  };
+  int r = run();
   ctx->last_stage_ms = stage_s * 1e3;
   ctx->last_call_ms = std::chrono::duration<double, std::milli>(clk::now() - t_call).count();
+  if (r) {  // nothing of a failed submission stays queued
+    for (int sl = 0; sl < edv_ctx::kSlots; ++sl)
+      if (ctx->slot_use[sl].ticket == ticket) (void)drain_slot(ctx, sl);
+    for (size_t k = 0; k < ctx->pending.size(); ++k)
+      if (ctx->pending[k].ticket == ticket) {
+        ctx->pending.erase(ctx->pending.begin() + (long)k);
+        break;
+      }
+    return r;
+  }
+  *ticket_out = ticket;
   return 0;
+}
+
+static int host_collect(edv_ctx* ctx, uint64_t ticket, uint8_t* accept_bits) {
+  size_t k = 0;
+  while (k < ctx->pending.size() && ctx->pending[k].ticket != ticket) ++k;
+  if (k == ctx->pending.size()) return set_err(EDV_EINVAL, "no pending submission %llu", (unsigned long long)ticket);
+  int r;
+  for (int sl = 0; sl < edv_ctx::kSlots; ++sl)
+    if (ctx->slot_use[sl].ticket == ticket && (r = drain_slot(ctx, sl))) return r;
+  edv_ctx::Pending& p = ctx->pending[k];
+  const uint64_t n = p.n;
+  if (n) {
+    memcpy(accept_bits, p.bits.data(), (size_t)((n + 7) / 8));
+    if (n & 7) accept_bits[n / 8] &= (uint8_t)((1u << (n & 7)) - 1);
+  }
+  ctx->pending.erase(ctx->pending.begin() + (long)k);
+  return 0;
+}
+
+static int host_verify(edv_ctx* ctx, bool keyed, const uint8_t* sig, uint64_t sig_stride, const uint8_t* keys,
+                       const uint8_t* msgs, const uint64_t* msg_off, uint64_t n, uint8_t* accept_bits) {
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  uint64_t ticket = 0;
+  int r = host_submit(ctx, keyed, sig, sig_stride, keys, msgs, msg_off, n, &ticket);
+  if (r) return r;
+  r = host_collect(ctx, ticket, accept_bits);
+  ctx->last_call_ms = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+  return r;
 }
 
 namespace edv_internal {
@@ -1756,6 +1818,22 @@ int edv_verify_batch_slots(edv_ctx* ctx, const uint8_t* sig_slots, const uint8_t
   if (n == 0) return 0;
   if (!sig_slots || !pk32 || !msg_off || !accept_bits) return set_err(EDV_EINVAL, "null pointer");
   return host_verify(ctx, false, sig_slots, EDV_SIG_SLOT96, pk32, msgs, msg_off, n, accept_bits);
+}
+
+int edv_verify_submit(edv_ctx* ctx, int keyed, const uint8_t* sig, int sig_format, const uint8_t* keys,
+                      const uint8_t* msgs, const uint64_t* msg_off, uint64_t n, uint64_t* ticket) {
+  int r = set_device(ctx);
+  if (r) return r;
+  if (!ticket || !msg_off || (n && (!sig || !keys))) return set_err(EDV_EINVAL, "null pointer");
+  if (sig_format != 64 && sig_format != EDV_SIG_SLOT96) return set_err(EDV_EINVAL, "sig_format %d", sig_format);
+  return host_submit(ctx, keyed != 0, sig, (uint64_t)sig_format, keys, msgs, msg_off, n, ticket);
+}
+
+int edv_verify_collect(edv_ctx* ctx, uint64_t ticket, uint8_t* accept_bits) {
+  int r = set_device(ctx);
+  if (r) return r;
+  if (!accept_bits) return set_err(EDV_EINVAL, "null accept_bits");
+  return host_collect(ctx, ticket, accept_bits);
 }
 
 int edv_host_alloc(edv_ctx* ctx, uint64_t bytes, void** out) {

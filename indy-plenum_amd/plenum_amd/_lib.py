@@ -48,6 +48,8 @@ SIGNATURES = {
     "edv_verify_spans_device": (_I, [_P, _P, _P, _I, _P, _P, _P, _U64, _P, _P]),
     "edv_verify_batch_slots": (_I, [_P, _P, _P, _P, _P, _U64, _P]),
     "edv_verify_batch_keyed_slots": (_I, [_P, _P, _P, _P, _P, _U64, _P]),
+    "edv_verify_submit": (_I, [_P, _I, _P, _I, _P, _P, _P, _U64, _P]),
+    "edv_verify_collect": (_I, [_P, _U64, _P]),
     "edv_host_alloc": (_I, [_P, _U64, _P]),
     "edv_host_free": (_I, [_P]),
     "edv_last_host_stats": (_I, [_P, _P]),

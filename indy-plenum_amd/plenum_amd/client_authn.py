@@ -141,7 +141,8 @@ class _GpuState:
     """Per-authenticator GPU state (created on first use)."""
 
     def __init__(self, engine=None, device=0, devices=None, verdict_cache_size=1 << 20, key_window="auto",
-                 max_keys=16384, hot_key_uses=2, key_store_bytes=KEY_STORE_BYTES, scan_threads=0):
+                 max_keys=16384, hot_key_uses=2, key_store_bytes=KEY_STORE_BYTES, scan_threads=0,
+                 pipeline_part=1 << 18):
         self.engine = engine
         self.device = device
         self.devices = devices
@@ -164,6 +165,9 @@ class _GpuState:
         # then copies straight from them; sized from the last batch's message bytes per item
         self.pinned_out = None
         self.msg_bytes_per_item = 256.0
+        # batches of 2 * pipeline_part requests or more are scanned in parts whose GPU work
+        # overlaps the next part's scan (0 = never)
+        self.pipeline_part = pipeline_part
         self.stats = {"batches": 0, "batch_items": 0, "cache_hits": 0, "single_verifies": 0, "keyed_items": 0,
                       "keys_registered": 0}
 
@@ -181,7 +185,9 @@ class GpuAuthMixin:
         comb whose max_keys tables fit key_store_bytes, e.g. 16,384 keys in
         32 GiB -> W=10, 1,000 keys -> W=14); max_keys; hot_key_uses;
         scan_threads (host threads of authenticate_batch's native scan, 0 =
-        auto: up to 16, one per 2k requests)."""
+        auto: up to 16, one per 2k requests); pipeline_part (batches of twice
+        this many requests or more are scanned in parts whose GPU work
+        overlaps the next part's scan; 0 = off)."""
         self._edv = _GpuState(engine=engine, device=device, **options)
 
     @property
@@ -463,7 +469,75 @@ class GpuAuthMixin:
         eng = self._engine()
         with _engine_lock(eng):
             slot = _SIG_SLOT if getattr(eng, "supports_sig_slots", False) else 64
-            return self._authenticate_batch_scanned_into(msgs, self._scan_buffers(eng, len(msgs), slot), slot)
+            bufs = self._scan_buffers(eng, len(msgs), slot)
+            part = self._g.pipeline_part
+            if part and len(msgs) >= 2 * part and hasattr(eng, "verify_submit") and bufs is not self._g.scan_out:
+                return self._authenticate_pipelined(msgs, eng, slot, bufs, part)
+            return self._authenticate_batch_scanned_into(msgs, bufs, slot)
+
+    def _authenticate_pipelined(self, msgs, eng, slot, bufs, part):
+        """A large batch in parts of `part` requests: the scan of part k + 1
+        (host threads) runs while part k's copies and kernels run on the GPU
+        (edv_verify_submit / edv_verify_collect).  Each part's scan writes into
+        its own stretch of the pinned buffers.  A part in the node's steady
+        state (every item scanned, every identifier resolved to a registered
+        key) is submitted asynchronously; any other part takes the ordinary
+        path synchronously (same verdicts either way).  getVerkey is called
+        once per distinct identifier of the whole batch."""
+        import numpy as np
+        g = self._g
+        n = len(msgs)
+        ks = self._key_store()
+        memo = {}
+        sig_mv = memoryview(bufs[0]).cast("B")
+        msg_mv = memoryview(bufs[1]).cast("B")
+        mpos, mtotal = 0, 0
+        parts = []
+        for lo in range(0, n, part):
+            hi = min(n, lo + part)
+            chunk = msgs[lo:hi]
+            out = [sig_mv[lo * slot:hi * slot], msg_mv[mpos:]]
+            scan = _scan_batch(chunk, [SIG], g.scan_threads, out, slot)
+            fast_b, uidx_b, uniq, sig_o, msg_o, off, short = scan
+            mlen = int(np.frombuffer(off, np.uint64)[-1])
+            mtotal += mlen
+            if msg_o is out[1]:
+                mpos += mlen
+            ukeys = []
+            for idr in uniq:
+                k = memo.get(idr, _MISSING)
+                if k is _MISSING:
+                    k = memo[idr] = self._key_for(idr)  # authenticate():93-99, once per identifier
+                ukeys.append(k)
+            ids = None
+            if ks is not None and fast_b.count(0) == 0 and all(k.__class__ is bytes for k in ukeys):
+                ids = ks.lookup(ukeys)
+                if any(i is None for i in ids):
+                    ids = None
+            if ids is None:  # not the steady state: this part the ordinary way
+                parts.append(("done", self._finish_scanned(chunk, scan, slot, ukeys)))
+                continue
+            kid = np.asarray(ids, np.uint32)[np.frombuffer(uidx_b, np.uint32)]
+            handle = eng.verify_submit(np.frombuffer(sig_o, np.uint8, count=slot * (hi - lo)).reshape(-1, slot),
+                                       kid, np.frombuffer(msg_o, np.uint8, count=mlen),
+                                       np.frombuffer(off, np.uint64), True, slot)
+            parts.append(("async", (handle, uidx_b, uniq, short)))
+            g.stats["batches"] += 1
+            g.stats["batch_items"] += hi - lo
+            g.stats["keyed_items"] += hi - lo
+        if n:
+            g.msg_bytes_per_item = max(g.msg_bytes_per_item * 0.5, mtotal / n)
+        results = []
+        for kind, payload in parts:
+            if kind == "async":
+                handle, uidx_b, uniq, short = payload
+                ok = np.asarray(eng.verify_collect(handle), bool) & (np.frombuffer(short, np.uint8) == 0)
+                res = _results_from(ok.view(np.uint8).tobytes(), uidx_b, uniq)
+                for i in np.flatnonzero(~ok).tolist():
+                    res[i] = InvalidSignature()
+                payload = res
+            results += payload
+        return results
 
     def _scan_buffers(self, eng, n, slot):
         """The scan's output buffers for an n-request batch: the engine's pinned
@@ -489,17 +563,27 @@ class GpuAuthMixin:
         import numpy as np
         n = len(msgs)
         g = self._g
-        fast_b, uidx_b, uniq, sig_o, msg_o, off, short = _scan_batch(msgs, [SIG], g.scan_threads, out, slot)
+        scan = _scan_batch(msgs, [SIG], g.scan_threads, out, slot)
+        mlen = int(np.frombuffer(scan[5], np.uint64)[-1])
+        if n:
+            g.msg_bytes_per_item = max(g.msg_bytes_per_item * 0.5, mlen / n)  # sizes the next batch's buffer
+        return self._finish_scanned(msgs, scan, slot)
+
+    def _finish_scanned(self, msgs, scan, slot, ukeys=None):
+        """Everything after the native scan of msgs: key resolution, the
+        verify launches, the result list."""
+        import numpy as np
+        n = len(msgs)
+        fast_b, uidx_b, uniq, sig_o, msg_o, off, short = scan
         # views of exactly this batch's bytes (released when the batch returns, so the next
         # batch may grow the buffers again)
         mlen = int(np.frombuffer(off, np.uint64)[-1])
-        if n:
-            g.msg_bytes_per_item = max(g.msg_bytes_per_item * 0.5, mlen / n)  # sizes the next batch's buffer
         sig64 = memoryview(sig_o)[:slot * n]
         mbuf = memoryview(msg_o)[:mlen]
         fast = np.frombuffer(fast_b, np.uint8).view(bool)
         uidx = np.frombuffer(uidx_b, np.uint32)
-        ukeys = [self._key_for(idr) for idr in uniq]  # authenticate():93-99, once per identifier
+        if ukeys is None:
+            ukeys = [self._key_for(idr) for idr in uniq]  # authenticate():93-99, once per identifier
         # per distinct identifier: 0 = key bytes, 1 = no key (the verify fails), 2 = exception
         ucls = np.fromiter((0 if k.__class__ is bytes else 1 if k is None else 2 for k in ukeys), np.uint8,
                            len(ukeys))

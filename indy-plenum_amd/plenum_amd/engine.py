@@ -186,6 +186,33 @@ class EdVerifyEngine:
                      _ptr(bits)))
         return unpack_bits(bits, n)
 
+    def verify_submit(self, sig, keys, msgs, msg_off, keyed, sig_slot=64):
+        """Queue a host-pointer verify and return a handle for verify_collect
+        (edv_verify_submit): inputs in host_alloc memory are read by DMA later
+        and must not change until then (the handle keeps the arrays alive).
+        keyed: keys are uint32 key ids, else n x 32 key bytes."""
+        sig = _u8(sig, sig_slot)
+        keys = np.ascontiguousarray(keys, dtype=np.uint32) if keyed else _u8(keys, 32)
+        msgs = _u8(msgs)
+        msg_off = np.ascontiguousarray(msg_off, dtype=np.uint64)
+        n = sig.shape[0]
+        if keys.shape[0] != n or msg_off.shape[0] != n + 1:
+            raise ValueError("shape mismatch: sig %d, keys %d, off %d" % (n, keys.shape[0], msg_off.shape[0]))
+        if n and int(msg_off[-1]) > msgs.shape[0]:
+            raise ValueError("msg_off exceeds message buffer")
+        ticket = ctypes.c_uint64()
+        check(self._lib.edv_verify_submit(self._ctx, 1 if keyed else 0, _ptr(sig), int(sig_slot), _ptr(keys),
+                                          _ptr(msgs) if msgs.size else None, _ptr(msg_off), n,
+                                          ctypes.byref(ticket)))
+        return (ticket.value, n, (sig, keys, msgs, msg_off))
+
+    def verify_collect(self, handle):
+        """Wait for a verify_submit and return its bool verdicts."""
+        ticket, n, _keep = handle
+        bits = np.zeros((n + 7) // 8, dtype=np.uint8)
+        check(self._lib.edv_verify_collect(self._ctx, ticket, _ptr(bits) if n else ctypes.c_void_p(1)))
+        return unpack_bits(bits, n)
+
     def host_alloc(self, nbytes):
         """nbytes of pinned host memory (edv_host_alloc) as a writable ctypes
         array; host-pointer verifies copy inputs inside it to the device with no

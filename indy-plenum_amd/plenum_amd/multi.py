@@ -102,6 +102,20 @@ class MultiEngine:
         return self._run(sig64.shape[0], lambda e, lo, hi: e.verify_batch_keyed(sig64[lo:hi], kidx[lo:hi], msgs,
                                                                                 off[lo:hi + 1], **kw))
 
+    def verify_submit(self, sig, keys, msgs, msg_off, keyed, sig_slot=64):
+        """Each device's shard queued (edv_verify_submit); verify_collect
+        concatenates the shards' verdicts in request order."""
+        sig, msgs = _u8(sig, sig_slot), _u8(msgs)
+        keys = np.ascontiguousarray(keys, dtype=np.uint32) if keyed else _u8(keys, 32)
+        off = np.ascontiguousarray(msg_off, dtype=np.uint64)
+        shards = [(e, lo, hi) for e, (lo, hi) in zip(self.engines, self._shards(sig.shape[0])) if hi > lo]
+        return [(e, e.verify_submit(sig[lo:hi], keys[lo:hi], msgs, off[lo:hi + 1], keyed, sig_slot))
+                for e, lo, hi in shards]
+
+    def verify_collect(self, handle):
+        parts = [e.verify_collect(h) for e, h in handle]
+        return np.concatenate(parts) if parts else np.zeros(0, bool)
+
     # ---------------------------------------------------- replicated key store
     def keys_reset(self):
         for e in self.engines:

@@ -100,6 +100,15 @@ class OracleEngine:
         return np.array([self.lib.oracle_sign_open(sm[off[i]:off[i + 1]], off[i + 1] - off[i], pk32[i].tobytes()) == 0
                          for i in range(len(off) - 1)], dtype=bool)
 
+    def verify_submit(self, sig, keys, msgs, msg_off, keyed, sig_slot=64):
+        self.submits = getattr(self, "submits", 0) + 1
+        if keyed:
+            return self.verify_batch_keyed(sig, keys, msgs, msg_off, sig_slot=sig_slot)
+        return self.verify_batch(sig, keys, msgs, msg_off, sig_slot=sig_slot)
+
+    def verify_collect(self, handle):
+        return handle
+
     def verify_batch(self, sig64, pk32, msgs, msg_off, sig_slot=64):
         self.calls += 1
         return self._verify(self._sig64(sig64, sig_slot), pk32, msgs, msg_off)

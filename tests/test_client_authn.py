@@ -497,3 +497,46 @@ def test_scan_slots_into_engine_buffers(oracle):
     a.authenticate_batch(pool + pool[:3000])
     a.authenticate_batch(pool[:4100])
     assert eng.host_allocs == 4
+
+
+def test_pipelined_parts_equal_per_message(oracle):
+    """A batch scanned in parts (pipeline_part): steady-state parts are
+    submitted asynchronously (verify_submit / verify_collect), a part with an
+    unknown identifier, a non-base58 signature, a missing field and a
+    registered-later key takes the ordinary path; verdicts == authenticate()
+    per message, and getVerkey runs once per identifier of the whole batch."""
+    idrs, vks, msgs = _signed(5, 80, seed=11)
+    pool = []
+    for k in range(6000):
+        m = dict(msgs[k % 80])
+        if k % 37 == 0:
+            m["reqId"] += 1
+        pool.append(m)
+    pool[2500] = dict(pool[2500], identifier="UnknownIdr1111111111")
+    pool[2600] = dict(pool[2600], signature="0OIl" + pool[2600]["signature"][4:])
+    del pool[2700]["identifier"]
+    eng = OracleEngine(oracle)
+    a = GpuAuthNr(engine=eng, pipeline_part=1024)
+    for idr, vk in zip(idrs[:4], vks[:4]):
+        a.addIdr(idr, vk)
+    a.clients[idrs[4]] = {"verkey": vks[4], "role": None}  # known, not queued for a key slot
+    calls = []
+    orig = a.getVerkey
+    a.getVerkey = lambda idr: calls.append(idr) or orig(idr)
+    got = [_outcome(r) for r in a.authenticate_batch(pool)]
+    ref = GpuAuthNr(engine=OracleEngine(oracle), max_keys=0)
+    for idr, vk in zip(idrs, vks):
+        ref.addIdr(idr, vk)
+    want = []
+    for m in pool:
+        try:
+            want.append(_outcome(ref.authenticate(m)))
+        except Exception as ex:
+            want.append(_outcome(ex))
+    assert got == want
+    assert getattr(eng, "submits", 0) >= 2
+    assert sorted(calls) == sorted(set(calls))  # once per identifier
+    # the next batch: idrs[4] promoted by use earlier, everything steady -> every part asynchronous
+    eng.submits = 0
+    got2 = [_outcome(r) for r in a.authenticate_batch(pool[:4096])]
+    assert got2 == want[:4096] and eng.submits >= 3

@@ -259,3 +259,30 @@ def test_pinned_slots_end_to_end_on_gpu(gpu_engine):
         # (4 + 8 B per request, made by numpy / the scan's result bytes) are staged: microseconds
         assert st["direct"]["sig"] and st["direct"]["msgs"] and st["stage_ms"] < 1.0, st
     assert a._g.pinned_out is not None and len(a._g.pinned_out[0]) >= 96 * n
+
+
+def test_pipelined_parts_on_gpu(gpu_engine):
+    """authenticate_batch in parts (pipeline_part = 4096 on 20,000 requests:
+    5 parts, more submissions than the library's two copy slots, so slots are
+    reused across pending submissions): edv_verify_submit / collect give the
+    construction's verdicts, the same as one synchronous call."""
+    import copy
+    n = 20000
+    reqs, rx, idrs, vks, pks, sers, sig = _drain(gpu_engine, n_req=n, n_nodes=1, n_signers=16)
+    bad = {i for i in range(n) if i % 10 == 3}
+    whole = GpuAuthNr(engine=gpu_engine, pipeline_part=0)
+    parts = GpuAuthNr(engine=gpu_engine, pipeline_part=4096)
+    for a in (whole, parts):
+        for idr, vk in zip(idrs, vks):
+            a.addIdr(idr, vk)
+    batch = [copy.deepcopy(r) for r in reqs]
+    batch[9000]["reqId"] += 1
+    bad.add(9000)
+    r1 = whole.authenticate_batch(batch)
+    for rep in range(2):
+        r2 = parts.authenticate_batch(batch)
+        assert [type(x).__name__ if not isinstance(x, str) else x for x in r2] == \
+               [type(x).__name__ if not isinstance(x, str) else x for x in r1]
+        for i, r in enumerate(r2):
+            assert (type(r).__name__ == "InvalidSignature") if i in bad else (r == batch[i]["identifier"]), i
+    assert parts.stats["keyed_items"] >= n
