@@ -40,3 +40,32 @@ a._g.pipeline_part = parts[-1]
 cProfile.run("a.authenticate_batch(reqs)", "/tmp/e2e.prof")
 pstats.Stats("/tmp/e2e.prof").sort_stats("tottime").print_stats(15)
 eng.close()
+
+# one request not in the verdict cache: authenticate() vs the engine call alone
+import numpy as np  # noqa: E402
+eng = EdVerifyEngine(0)
+a = GpuAuthNr(engine=eng)
+for idr, vk in zip(idrs, vks):
+    a.addIdr(idr, vk)
+a.authenticate_batch(reqs[:4096])
+lat, lat_eng, lat_prep = [], [], []
+for r in reqs[:330]:
+    a.clear_verdicts()
+    t0 = time.perf_counter()
+    a.authenticate(r)
+    lat.append(time.perf_counter() - t0)
+    t0 = time.perf_counter()
+    p = a._prepare(r)
+    lat_prep.append(time.perf_counter() - t0)
+    ks = a._key_store()
+    kid = np.asarray(ks.lookup([p.key]), np.uint32)
+    from plenum_amd.client_authn import _pack_split64
+    s64, m, off, short = _pack_split64([p.sig], [p.ser])
+    t0 = time.perf_counter()
+    eng.verify_batch_keyed(np.frombuffer(s64, np.uint8).reshape(-1, 64), kid, np.frombuffer(m, np.uint8),
+                           np.frombuffer(off, np.uint64))
+    lat_eng.append(time.perf_counter() - t0)
+for name, v in (("authenticate", lat), ("_prepare", lat_prep), ("engine call n=1", lat_eng)):
+    v = np.array(v[30:]) * 1e6
+    print("single %-16s p50 %.1f us  p99 %.1f us" % (name, np.percentile(v, 50), np.percentile(v, 99)))
+print("phases of the last n=1 call (ms):", eng.last_phases_ms(), eng.last_host_stats())
