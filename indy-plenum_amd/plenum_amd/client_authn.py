@@ -142,7 +142,7 @@ class _GpuState:
 
     def __init__(self, engine=None, device=0, devices=None, verdict_cache_size=1 << 20, key_window="auto",
                  max_keys=16384, hot_key_uses=2, key_store_bytes=KEY_STORE_BYTES, scan_threads=0,
-                 pipeline_part=1 << 18):
+                 pipeline_part=0):
         self.engine = engine
         self.device = device
         self.devices = devices
@@ -166,7 +166,10 @@ class _GpuState:
         self.pinned_out = None
         self.msg_bytes_per_item = 256.0
         # batches of 2 * pipeline_part requests or more are scanned in parts whose GPU work
-        # overlaps the next part's scan (0 = never)
+        # overlaps the next part's scan (0 = never, the default: on the box's 16-CPU share the
+        # per-part scan costs -- helper wake-ups, the identifier merge, the result list assembly --
+        # exceeded the ~7 ms per 1M of GPU work hidden: 1M requests 23-25 M/s unparted against
+        # 14 M/s in 2^17 parts and 17-18 M/s in 2^18 parts, profiles/r04c)
         self.pipeline_part = pipeline_part
         self.stats = {"batches": 0, "batch_items": 0, "cache_hits": 0, "single_verifies": 0, "keyed_items": 0,
                       "keys_registered": 0}
