@@ -136,7 +136,10 @@ def time_e2e(eng, reqs, idrs, vks):
     a = GpuAuthNr(engine=eng)
     for idr, vk in zip(idrs, vks):
         a.addIdr(idr, vk)
-    a.authenticate_batch(reqs[:2048])  # first batch registers the addIdr keys (key tables built)
+    # genesis NYMs' key tables built before traffic (registrations on the request path build in the
+    # background, their requests on the general path until built)
+    a.keys_settle()
+    a.authenticate_batch(reqs[:2048])
     t0 = time.perf_counter()
     res = a.authenticate_batch(reqs)  # first full-size batch: the scan's reused buffers grow (page faults)
     first = time.perf_counter() - t0
@@ -596,14 +599,30 @@ def main():
     # tools/pmc_summary.py): 2 x FETCH_SIZE + WRITE_SIZE per request (gfx950
     # FETCH_SIZE correction), times the requests of one launch
     traffic = None
+    utilisation = None
+    key = "%s<%d>" % (kernel_name, args.key_window) if args.path == "keyed" else kernel_name
     tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tpath):
         with open(tpath) as f:
             tj = json.load(f)
-        key = "%s<%d>" % (kernel_name, args.key_window) if args.path == "keyed" else kernel_name
-        row = tj.get("kernels", {}).get(key)
+        kern = tj.get("kernels", {})
+        row = kern.get(key)
         if row and "traffic_bytes_per_request" in row:
             traffic = row["traffic_bytes_per_request"] * (n_chunk / launches)
+        # VALU busy / clock / HBM GB/s of the step's kernels: counters of the committed PMC pass
+        # (same binary, same workload), durations from this run's HIP events
+        per = n_chunk / launches
+        hash_key = "edv_hash_keyed_kernel<false>" if args.path == "keyed" else "edv_hash_kernel<false>"
+        legs = ((key, float(ph[2]) / launches, kernel_mad), (hash_key, float(ph[0]) / launches, None),
+                ("edv_encode_kernel<16>", float(ph[3]) / launches, RL.mad_encode_kernel(16)))
+        utilisation = {k: RL.pmc_utilisation(kern[k], ms, per, mad) for k, ms, mad in legs
+                       if k in kern and ms > 0}
+        utilisation["source"] = ("%s (run %s): counters per launch from the PMC passes, durations from this run's "
+                                 "HIP events. clock = GRBM_GUI_ACTIVE/8/duration; valu_busy = SQ_ACTIVE_INST_VALU*4/"
+                                 "(1024 SIMDs * GRBM_GUI_ACTIVE/8) (rocprof gfx94x VALUBusy); hbm_GBps = (2*FETCH_SIZE"
+                                 " + WRITE_SIZE) bytes per request * requests / duration; mad_share_of_valu = MAD per "
+                                 "request / VALU lane-instructions per request (roofline.pmc_utilisation)"
+                                 % (os.path.relpath(tpath, ROOT), tj.get("run", "?")))
 
     # the dominant kernel alone on the GPU (one sub-batch, no overlap), one
     # untimed step: its own roofline fraction beside the overlapped one above
@@ -711,6 +730,10 @@ def main():
                              kernel_mad, RL.kernel_work(kernel_name, args.key_window), launches, n_chunk,
                              n_chunk // launches, n, dsm_avg),
                          "standalone": standalone,
+                         "valu_busy": (utilisation or {}).get(key, {}).get("valu_busy"),
+                         "hbm_GBps": (utilisation or {}).get(key, {}).get("hbm_GBps"),
+                         "clock_GHz": (utilisation or {}).get(key, {}).get("clock_GHz"),
+                         "utilisation": utilisation,
                          "frac_survey": (n * RL.MAD_PER_VERIFY / (ms_per_step * 1e-3)) / RL.PEAK_MAD_PER_S,
                          "frac_survey_note": "SURVEY 8(d)'s a-priori 305,000 MAD per verify (ref10: decode A + 253 "
                                              "doublings + ~86 additions + inversion) x requests / step time / peak; "

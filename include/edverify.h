@@ -162,8 +162,26 @@ int edv_keys_add_device(edv_ctx *ctx, const void *d_pk32, uint64_t nkeys, uint64
  * registered count): the caller's LRU eviction.  Waits for in-flight work on
  * the device first, so no verify reads a half-rebuilt table. */
 int edv_keys_set(edv_ctx *ctx, uint64_t first_id, const uint8_t *pk32, uint64_t nkeys);
+/* Asynchronous forms, for registrations made on the request path (a key that
+ * earned a slot by use, an addIdr key): the pk upload and the table builds
+ * are queued on the context's build stream and the call returns at once with
+ * a ticket (tickets complete in order).  The ids are assigned immediately,
+ * but a keyed verify of an id whose build has not finished reads a
+ * half-built table: the caller routes those requests to the general path
+ * (edv_verify_batch / edv_sign_open_batch, same verdicts) until
+ * edv_keys_ready(ticket) returns 1.  edv_keys_set_async's rebuild starts
+ * after the work already queued on the context's own streams (a verify still
+ * reading the old table); the host never waits for it.  Replaces the
+ * synchronous registration inside plenum/server/client_authn.py:133-140's
+ * addIdr path (SimpleAuthNr keeps its dict; the tables are this library's). */
+int edv_keys_add_async(edv_ctx *ctx, const uint8_t *pk32, uint64_t nkeys, uint64_t *first_id, uint64_t *ticket);
+int edv_keys_set_async(edv_ctx *ctx, uint64_t first_id, const uint8_t *pk32, uint64_t nkeys, uint64_t *ticket);
+/* 1 when every build up to `ticket` has finished, 0 while one still runs, < 0 on error. */
+int edv_keys_ready(edv_ctx *ctx, uint64_t ticket);
+/* Wait for every queued build. */
+int edv_keys_sync(edv_ctx *ctx);
 uint64_t edv_keys_count(edv_ctx *ctx);
-/* Forget all registered keys (device memory is kept for reuse). */
+/* Forget all registered keys (device memory is kept for reuse; waits for queued builds). */
 int edv_keys_reset(edv_ctx *ctx);
 /* Set the key window (4, 6, 8, 10, 12, 13, 14 or 16; environment EDV_KEY_WINDOW sets the
  * context default).  Only with no keys registered; frees the key store. */

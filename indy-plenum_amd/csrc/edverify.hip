@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <deque>
 #include <mutex>
 #include <stdarg.h>
 #include <stdio.h>
@@ -1072,6 +1073,17 @@ struct edv_ctx {
   double last_call_ms = 0.0;    // the whole call
   uint64_t last_h2d_bytes = 0;  // bytes copied host -> device
   int last_direct = 0;          // bit 0 sig, 1 keys, 2 msgs, 3 offsets: DMA straight from the caller's pinned memory
+  // Asynchronous key-table builds (edv_keys_add_async / edv_keys_set_async): serialized on
+  // stream_build with scratch of their own; build k records builds[k].ev; tickets complete in order
+  hipStream_t stream_build = nullptr;
+  Buf b_build;
+  struct BuildEv {
+    uint64_t ticket;
+    hipEvent_t ev;
+  };
+  std::deque<BuildEv> builds;
+  uint64_t build_ticket = 0, build_done = 0;
+  hipEvent_t ev_fence[4] = {};  // in-flight work of the context's streams, awaited by a slot rebuild
 };
 
 namespace {
@@ -1427,15 +1439,18 @@ static int keys_reserve(edv_ctx* ctx, uint64_t need) {
 constexpr uint64_t kKeyBuildScratch = 1ull << 30;  // bytes of row bases + prefix products per slice (the row
                                                    // kernel is one lane per key: fewer, larger slices)
 template <int W>
-static int keys_build_w(edv_ctx* ctx, uint64_t first, uint64_t nkeys, hipStream_t st) {
+static int keys_build_w(edv_ctx* ctx, uint64_t first, uint64_t nkeys, hipStream_t st, edv_ctx::Buf& aux) {
   constexpr int R = Window<W>::kRows, E = Window<W>::kEntries;
   constexpr uint64_t per_key = (uint64_t)R * kRowWords * 4 + (uint64_t)R * E * 10 * 4;
   const uint64_t max_slice = kKeyBuildScratch / per_key > 0 ? kKeyBuildScratch / per_key : 1;
   const uint64_t slice = nkeys < max_slice ? nkeys : max_slice;
   int r;
   // rows: R p3 bases per key; pre: E prefix products per row
-  if ((r = ensure(ctx->b_aux, slice * R * kRowWords * 4 + slice * R * E * 10 * 4))) return r;
-  uint32_t* rows = (uint32_t*)ctx->b_aux.p;
+  const size_t need = slice * R * kRowWords * 4 + slice * R * E * 10 * 4;
+  // an earlier build on this stream may still read the scratch: it finishes before a regrowth frees it
+  if (aux.cap < need) HIP_TRY(hipStreamSynchronize(st));
+  if ((r = ensure(aux, need))) return r;
+  uint32_t* rows = (uint32_t*)aux.p;
   uint32_t* pre = rows + slice * R * kRowWords;
   for (uint64_t k0 = 0; k0 < nkeys; k0 += slice) {
     const uint64_t kn = nkeys - k0 < slice ? nkeys - k0 : slice;
@@ -1452,9 +1467,10 @@ static int keys_build_w(edv_ctx* ctx, uint64_t first, uint64_t nkeys, hipStream_
 
 static int keys_build(edv_ctx* ctx, uint64_t first, uint64_t nkeys, hipStream_t st) {
   if (!nkeys) return 0;
+  edv_ctx::Buf& aux = st == ctx->stream_build ? ctx->b_build : ctx->b_aux;
 #define EDV_BUILD_CASE(W) \
   case W:                 \
-    return keys_build_w<W>(ctx, first, nkeys, st);
+    return keys_build_w<W>(ctx, first, nkeys, st, aux);
   switch (ctx->key_w) {
     EDV_KEY_WINDOWS(EDV_BUILD_CASE)
     default:
@@ -1741,10 +1757,91 @@ int edv_keys_set(edv_ctx* ctx, uint64_t first_id, const uint8_t* pk32, uint64_t 
   return 0;
 }
 
+// Asynchronous registration.  The pk upload and the table builds go on stream_build (its own
+// scratch, b_build), an event closes each call, and the host returns at once; the caller routes a
+// building id's requests elsewhere until edv_keys_ready says its ticket is done.
+static int build_ticket(edv_ctx* ctx, uint64_t* ticket) {
+  hipEvent_t ev = nullptr;
+  HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  const hipError_t e = hipEventRecord(ev, ctx->stream_build);
+  if (e != hipSuccess) {
+    (void)hipEventDestroy(ev);
+    return set_err(EDV_EHIP, "hipEventRecord: %s", hipGetErrorString(e));
+  }
+  ctx->builds.push_back(edv_ctx::BuildEv{++ctx->build_ticket, ev});
+  if (ticket) *ticket = ctx->build_ticket;
+  return 0;
+}
+
+int edv_keys_add_async(edv_ctx* ctx, const uint8_t* pk32, uint64_t nkeys, uint64_t* first_id, uint64_t* ticket) {
+  int r = set_device(ctx);
+  if (r) return r;
+  if (nkeys && !pk32) return set_err(EDV_EINVAL, "null pk32");
+  if (ctx->key_count + nkeys > 0xffffffffull) return set_err(EDV_EINVAL, "too many keys");
+  // a regrowth of the store waits for everything (it copies the built tables); rare: capacity doubles
+  if ((r = keys_reserve(ctx, ctx->key_count + nkeys))) return r;
+  const uint64_t first = ctx->key_count;
+  if (nkeys) {
+    HIP_TRY(hipMemcpyAsync(ctx->d_key_pk + 32 * first, pk32, 32 * nkeys, hipMemcpyHostToDevice, ctx->stream_build));
+    if ((r = keys_build(ctx, first, nkeys, ctx->stream_build))) return r;
+  }
+  if ((r = build_ticket(ctx, ticket))) return r;
+  ctx->key_count += nkeys;
+  if (first_id) *first_id = first;
+  return 0;
+}
+
+int edv_keys_set_async(edv_ctx* ctx, uint64_t first_id, const uint8_t* pk32, uint64_t nkeys, uint64_t* ticket) {
+  int r = set_device(ctx);
+  if (r) return r;
+  if (nkeys && !pk32) return set_err(EDV_EINVAL, "null pk32");
+  if (first_id > ctx->key_count || nkeys > ctx->key_count - first_id)
+    return set_err(EDV_EINVAL, "keys [%llu, %llu) outside the %llu registered", (unsigned long long)first_id,
+                   (unsigned long long)(first_id + nkeys), (unsigned long long)ctx->key_count);
+  if (nkeys) {
+    // the rebuild starts after the work already queued on the context's streams (verifies that may
+    // still read these slots' old tables); the host does not wait
+    hipStream_t qs[4] = {ctx->stream, ctx->stream2, ctx->stream_copy, ctx->stream_key};
+    for (int k = 0; k < 4; ++k) {
+      HIP_TRY(hipEventRecord(ctx->ev_fence[k], qs[k]));
+      HIP_TRY(hipStreamWaitEvent(ctx->stream_build, ctx->ev_fence[k], 0));
+    }
+    HIP_TRY(hipMemcpyAsync(ctx->d_key_pk + 32 * first_id, pk32, 32 * nkeys, hipMemcpyHostToDevice,
+                           ctx->stream_build));
+    if ((r = keys_build(ctx, first_id, nkeys, ctx->stream_build))) return r;
+  }
+  return build_ticket(ctx, ticket);
+}
+
+int edv_keys_ready(edv_ctx* ctx, uint64_t ticket) {
+  int r = set_device(ctx);
+  if (r) return r;
+  while (ticket > ctx->build_done && !ctx->builds.empty()) {
+    const hipError_t e = hipEventQuery(ctx->builds.front().ev);
+    if (e == hipErrorNotReady) return 0;
+    if (e != hipSuccess) return set_err(EDV_EHIP, "key-table build: %s", hipGetErrorString(e));
+    ctx->build_done = ctx->builds.front().ticket;
+    (void)hipEventDestroy(ctx->builds.front().ev);
+    ctx->builds.pop_front();
+  }
+  return ticket <= ctx->build_done ? 1 : 0;
+}
+
+int edv_keys_sync(edv_ctx* ctx) {
+  int r = set_device(ctx);
+  if (r) return r;
+  if (ctx->builds.empty()) return 0;
+  HIP_TRY(hipStreamSynchronize(ctx->stream_build));
+  return edv_keys_ready(ctx, ctx->build_ticket) == 1 ? 0 : set_err(EDV_EHIP, "key-table builds did not drain");
+}
+
 uint64_t edv_keys_count(edv_ctx* ctx) { return ctx ? ctx->key_count : 0; }
 
 int edv_keys_reset(edv_ctx* ctx) {
-  if (!ctx) return set_err(EDV_EINVAL, "null context");
+  int r = set_device(ctx);
+  if (r) return r;
+  // a pending asynchronous build must not write a slot the next registration reuses
+  if ((r = edv_keys_sync(ctx))) return r;
   ctx->key_count = 0;
   return 0;
 }
@@ -1757,6 +1854,7 @@ int edv_keys_set_window(edv_ctx* ctx, int w) {
                                      (unsigned long long)ctx->key_count);
   if (w == ctx->key_w) return 0;
   HIP_TRY(hipStreamSynchronize(ctx->stream));
+  if ((r = edv_keys_sync(ctx))) return r;
   if (ctx->d_key_tab) (void)hipFree(ctx->d_key_tab);
   if (ctx->d_key_pk) (void)hipFree(ctx->d_key_pk);
   if (ctx->d_key_valid) (void)hipFree(ctx->d_key_valid);
@@ -1918,6 +2016,10 @@ edv_ctx* edv_create(int device) {
     return fail("hipStreamCreate", e);
   if ((e = hipStreamCreateWithFlags(&ctx->stream_key, hipStreamNonBlocking)) != hipSuccess)
     return fail("hipStreamCreate", e);
+  if ((e = hipStreamCreateWithFlags(&ctx->stream_build, hipStreamNonBlocking)) != hipSuccess)
+    return fail("hipStreamCreate", e);
+  for (hipEvent_t& f : ctx->ev_fence)
+    if ((e = hipEventCreateWithFlags(&f, hipEventDisableTiming)) != hipSuccess) return fail("hipEventCreate", e);
   for (int sb = 0; sb < edv_ctx::kSub; ++sb)
     if ((e = hipEventCreateWithFlags(&ctx->ev_kfork[sb], hipEventDisableTiming)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&ctx->ev_kjoin[sb], hipEventDisableTiming)) != hipSuccess)
@@ -1993,7 +2095,12 @@ void edv_destroy(edv_ctx* ctx) {
   if (ctx->stream_copy) (void)hipStreamSynchronize(ctx->stream_copy);
   if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
   if (ctx->stream_key) (void)hipStreamSynchronize(ctx->stream_key);
-  for (edv_ctx::Buf* b : {&ctx->b_sig, &ctx->b_pk, &ctx->b_msg, &ctx->b_off, &ctx->b_bits, &ctx->b_aux}) free_buf(*b);
+  if (ctx->stream_build) (void)hipStreamSynchronize(ctx->stream_build);
+  for (edv_ctx::Buf* b : {&ctx->b_sig, &ctx->b_pk, &ctx->b_msg, &ctx->b_off, &ctx->b_bits, &ctx->b_aux, &ctx->b_build})
+    free_buf(*b);
+  for (edv_ctx::BuildEv& b : ctx->builds) (void)hipEventDestroy(b.ev);
+  for (hipEvent_t f : ctx->ev_fence)
+    if (f) (void)hipEventDestroy(f);
   for (int k = 0; k < edv_ctx::kSlots; ++k) {
     for (edv_ctx::Buf* b : {&ctx->h_sig[k], &ctx->h_key[k], &ctx->h_msg[k], &ctx->h_off[k], &ctx->h_bits[k],
                             &ctx->d_sig[k], &ctx->d_key[k], &ctx->d_msg[k], &ctx->d_off[k], &ctx->d_bits[k],
@@ -2034,6 +2141,7 @@ void edv_destroy(edv_ctx* ctx) {
   if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
   if (ctx->stream_key) (void)hipStreamDestroy(ctx->stream_key);
   if (ctx->stream_copy) (void)hipStreamDestroy(ctx->stream_copy);
+  if (ctx->stream_build) (void)hipStreamDestroy(ctx->stream_build);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }

@@ -39,6 +39,10 @@ SIGNATURES = {
     "edv_keys_add": (_I, [_P, _P, _U64, _P]),
     "edv_keys_add_device": (_I, [_P, _P, _U64, _P, _P]),
     "edv_keys_set": (_I, [_P, _U64, _P, _U64]),
+    "edv_keys_add_async": (_I, [_P, _P, _U64, _P, _P]),
+    "edv_keys_set_async": (_I, [_P, _U64, _P, _U64, _P]),
+    "edv_keys_ready": (_I, [_P, _U64]),
+    "edv_keys_sync": (_I, [_P]),
     "edv_keys_count": (_U64, [_P]),
     "edv_keys_reset": (_I, [_P]),
     "edv_keys_set_window": (_I, [_P, _I]),

@@ -142,7 +142,7 @@ class _GpuState:
 
     def __init__(self, engine=None, device=0, devices=None, verdict_cache_size=1 << 20, key_window="auto",
                  max_keys=16384, hot_key_uses=2, key_store_bytes=KEY_STORE_BYTES, scan_threads=0,
-                 pipeline_part=0):
+                 pipeline_part=0, async_key_builds=True):
         self.engine = engine
         self.device = device
         self.devices = devices
@@ -171,6 +171,10 @@ class _GpuState:
         # exceeded the ~7 ms per 1M of GPU work hidden: 1M requests 23-25 M/s unparted against
         # 14 M/s in 2^17 parts and 17-18 M/s in 2^18 parts, profiles/r04c)
         self.pipeline_part = pipeline_part
+        # key tables registered on the request path (addIdr keys, keys that earned a slot) build on
+        # the engine's build stream while batches go on; their requests take the general path until
+        # the build completes (engines without edv_keys_add_async build synchronously)
+        self.async_key_builds = async_key_builds
         self.stats = {"batches": 0, "batch_items": 0, "cache_hits": 0, "single_verifies": 0, "keyed_items": 0,
                       "keys_registered": 0}
 
@@ -190,7 +194,9 @@ class GpuAuthMixin:
         scan_threads (host threads of authenticate_batch's native scan, 0 =
         auto: up to 16, one per 2k requests); pipeline_part (batches of twice
         this many requests or more are scanned in parts whose GPU work
-        overlaps the next part's scan; 0 = off)."""
+        overlaps the next part's scan; 0 = off); async_key_builds (key
+        tables registered on the request path build in the background, their
+        requests on the general path until built; default True)."""
         self._edv = _GpuState(engine=engine, device=device, **options)
 
     @property
@@ -296,6 +302,25 @@ class GpuAuthMixin:
             return None
         return KeyStore.attach(self._engine(), g.key_window, g.max_keys)
 
+    def keys_settle(self):
+        """Register the addIdr keys waiting for a slot and wait until every
+        queued key-table build has finished (e.g. after genesis NYMs, before a
+        timed run); batches never need this for correctness."""
+        g = self._g
+        ks = self._key_store()
+        if ks is None:
+            return 0
+        with _engine_lock(self._engine()):
+            if g.pending:
+                room = ks.free_slots()
+                if room > 0:
+                    got = ks.register([k for k in g.pending if k not in ks][:room], evict=False,
+                                      asynchronous=g.async_key_builds)
+                    g.stats["keys_registered"] += len(got)
+                g.pending.clear()
+            ks.settle()
+        return len(ks)
+
     def _route(self, todo):
         """Register waiting keys, then split items into (keyed + ids, general)."""
         g = self._g
@@ -304,14 +329,14 @@ class GpuAuthMixin:
             return [], [], todo
         batch_keys = [p.key for p in todo]
         if g.hot:  # earned a slot: may evict least-recently-used keys not in this batch
-            got = ks.register(list(g.hot), pinned=batch_keys, evict=True)
+            got = ks.register(list(g.hot), pinned=batch_keys, evict=True, asynchronous=g.async_key_builds)
             g.stats["keys_registered"] += len(got)
             g.hot.clear()
         if g.pending:  # addIdr keys: free slots only
             room = ks.free_slots()
             if room > 0:
                 take = [k for k in g.pending if k not in ks][:room]
-                got = ks.register(take, evict=False)
+                got = ks.register(take, evict=False, asynchronous=g.async_key_builds)
                 g.stats["keys_registered"] += len(got)
             g.pending.clear()  # registered, or no room: later keys get in by use (hot)
         ids = ks.lookup(batch_keys)
@@ -639,13 +664,14 @@ class GpuAuthMixin:
         ks = self._key_store()
         if ks is not None and uniq_keys:
             if g.hot:
-                got = ks.register(list(g.hot), pinned=uniq_keys, evict=True)
+                got = ks.register(list(g.hot), pinned=uniq_keys, evict=True, asynchronous=g.async_key_builds)
                 g.stats["keys_registered"] += len(got)
                 g.hot.clear()
             if g.pending:
                 room = ks.free_slots()
                 if room > 0:
-                    got = ks.register([k for k in g.pending if k not in ks][:room], evict=False)
+                    got = ks.register([k for k in g.pending if k not in ks][:room], evict=False,
+                                      asynchronous=g.async_key_builds)
                     g.stats["keys_registered"] += len(got)
                 g.pending.clear()
             id_of = {k: i for k, i in zip(uniq_keys, ks.lookup(uniq_keys)) if i is not None}

@@ -382,6 +382,32 @@ class EdVerifyEngine:
         pk32 = _u8(pk32, 32)
         check(self._lib.edv_keys_set(self._ctx, int(first_id), _ptr(pk32), pk32.shape[0]))
 
+    def keys_add_async(self, pk32):
+        """Register keys without waiting for their tables (edv_keys_add_async):
+        returns (first id, ticket); the ids may be used by keyed verifies only
+        once keys_ready(ticket)."""
+        pk32 = _u8(pk32, 32)
+        first, ticket = ctypes.c_uint64(), ctypes.c_uint64()
+        check(self._lib.edv_keys_add_async(self._ctx, _ptr(pk32), pk32.shape[0], ctypes.byref(first),
+                                           ctypes.byref(ticket)))
+        return first.value, ticket.value
+
+    def keys_set_async(self, first_id, pk32):
+        """Rebuild slots first_id.. with new keys without waiting; returns the ticket."""
+        pk32 = _u8(pk32, 32)
+        ticket = ctypes.c_uint64()
+        check(self._lib.edv_keys_set_async(self._ctx, int(first_id), _ptr(pk32), pk32.shape[0],
+                                           ctypes.byref(ticket)))
+        return ticket.value
+
+    def keys_ready(self, ticket):
+        r = self._lib.edv_keys_ready(self._ctx, int(ticket))
+        check(min(r, 0))
+        return r == 1
+
+    def keys_sync(self):
+        check(self._lib.edv_keys_sync(self._ctx))
+
     def keys_count(self):
         return int(self._lib.edv_keys_count(self._ctx))
 

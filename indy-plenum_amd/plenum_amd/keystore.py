@@ -16,6 +16,12 @@ policy (client_authn.GpuAuthMixin): keys given to addIdr while there is free
 room, and keys that verified successfully hot_key_uses times.  A key whose
 registration fails (allocation, HIP error) is remembered as unregistrable and
 its requests keep taking the general path, which gives the same verdicts.
+
+Registrations made on the request path are asynchronous when the engine has
+edv_keys_add_async (register(..., asynchronous=True)): the ids are assigned at
+once, the tables build on the engine's build stream while batches go on, and
+lookup() answers None for an id whose build ticket has not completed, so its
+requests take the general path until then (same verdicts, no stall).
 """
 from collections import OrderedDict
 
@@ -52,6 +58,8 @@ class KeyStore:
         self._slot_key = []           # id -> key bytes
         self._failed = OrderedDict()  # keys that could not be registered
         self._generation = None
+        self._building = {}           # id -> ticket of its latest build (asynchronous registrations)
+        self._tickets = OrderedDict()  # ticket -> ids, ascending (tickets complete in order)
 
     @classmethod
     def attach(cls, engine, window, capacity):
@@ -75,7 +83,37 @@ class KeyStore:
             self.engine.keys_set_window(self.window)
         self._ids.clear()
         self._slot_key = []
+        self._building.clear()
+        self._tickets.clear()
         self._generation = getattr(self.engine, "keys_generation", 0)
+
+    def _refresh(self):
+        """Drop the ids whose builds have completed from the building set
+        (one edv_keys_ready query per completed ticket, oldest first)."""
+        while self._tickets:
+            t = next(iter(self._tickets))
+            if not self.engine.keys_ready(t):
+                return
+            for i in self._tickets.pop(t):
+                if self._building.get(i) == t:
+                    del self._building[i]
+
+    def building(self):
+        """Ids whose tables are still being built."""
+        self._refresh()
+        return len(self._building)
+
+    def settle(self):
+        """Wait for every queued build (e.g. before a timed run)."""
+        if self._tickets and hasattr(self.engine, "keys_sync"):
+            self.engine.keys_sync()
+        self._building.clear()
+        self._tickets.clear()
+
+    def _mark_building(self, ids, ticket):
+        for i in ids:
+            self._building[i] = ticket
+        self._tickets.setdefault(ticket, []).extend(ids)
 
     def __len__(self):
         return len(self._ids)
@@ -88,21 +126,30 @@ class KeyStore:
         return self.capacity - len(self._ids)
 
     def lookup(self, keys):
-        """Ids of keys (None for unregistered), marking them recently used."""
+        """Ids of keys (None for unregistered keys and for keys whose tables
+        are still building), marking them recently used."""
         self._sync()
+        if self._building:
+            self._refresh()
+        building = self._building
         out = []
         for k in keys:
             i = self._ids.get(k)
             if i is not None:
                 self._ids.move_to_end(k)
+                if building and i in building:
+                    i = None
             out.append(i)
         return out
 
-    def register(self, keys, pinned=(), evict=True):
+    def register(self, keys, pinned=(), evict=True, asynchronous=False):
         """Register keys not yet in the store: into free slots, then (evict)
         over least-recently-used keys outside `pinned`.  Returns the keys
-        registered."""
+        registered.  asynchronous: queue the table builds and return at once
+        (engines with keys_add_async; lookup() hides the ids until built)."""
         self._sync()
+        use_async = asynchronous and getattr(self.engine, "supports_async_keys",
+                                             hasattr(self.engine, "keys_add_async"))
         fresh = [k for k in OrderedDict.fromkeys(keys) if k not in self._ids and k not in self._failed]
         if not fresh:
             return []
@@ -110,14 +157,21 @@ class KeyStore:
         new, over = fresh[:room], fresh[room:]
         done = []
         if new:
+            pk = np.frombuffer(b"".join(new), np.uint8).reshape(-1, 32)
+            ticket = None
             try:
-                first = self.engine.keys_add(np.frombuffer(b"".join(new), np.uint8).reshape(-1, 32))
+                if use_async:
+                    first, ticket = self.engine.keys_add_async(pk)
+                else:
+                    first = self.engine.keys_add(pk)
             except Exception:
                 self._fail(new)
                 new = []
             for j, k in enumerate(new):
                 self._ids[k] = first + j
                 self._slot_key.append(k)
+            if ticket is not None and new:
+                self._mark_building(range(first, first + len(new)), ticket)
             done += new
         if over and evict and hasattr(self.engine, "keys_set"):
             pinned = set(pinned)
@@ -125,7 +179,11 @@ class KeyStore:
             for k_new, k_old in zip(over, victims):
                 slot = self._ids.pop(k_old)
                 try:
-                    self.engine.keys_set(slot, np.frombuffer(k_new, np.uint8).reshape(1, 32))
+                    pk = np.frombuffer(k_new, np.uint8).reshape(1, 32)
+                    if use_async and hasattr(self.engine, "keys_set_async"):
+                        self._mark_building([slot], self.engine.keys_set_async(slot, pk))
+                    else:
+                        self.engine.keys_set(slot, pk)
                 except Exception:
                     # the slot's old table may be half rewritten: retire the slot
                     self._slot_key[slot] = None

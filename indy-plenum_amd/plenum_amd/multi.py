@@ -145,6 +145,30 @@ class MultiEngine:
         pk32 = _u8(pk32, 32)
         self._each(lambda e: e.keys_set(first_id, pk32))
 
+    @property
+    def supports_async_keys(self):
+        return all(hasattr(e, "keys_add_async") for e in self.engines)
+
+    def keys_add_async(self, pk32):
+        """Queued on every device at once; the ticket is the tuple of the
+        devices' tickets (ready when every device's build is)."""
+        pk32 = _u8(pk32, 32)
+        res = self._each(lambda e: e.keys_add_async(pk32))
+        firsts = {f for f, _ in res}
+        if len(firsts) != 1:
+            raise RuntimeError("key stores of the devices diverged (first ids %s)" % sorted(firsts))
+        return firsts.pop(), tuple(t for _, t in res)
+
+    def keys_set_async(self, first_id, pk32):
+        pk32 = _u8(pk32, 32)
+        return tuple(self._each(lambda e: e.keys_set_async(first_id, pk32)))
+
+    def keys_ready(self, ticket):
+        return all(e.keys_ready(t) for e, t in zip(self.engines, ticket))
+
+    def keys_sync(self):
+        self._each(lambda e: e.keys_sync())
+
     def keys_count(self):
         return self.engines[0].keys_count()
 

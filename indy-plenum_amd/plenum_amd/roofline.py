@@ -94,6 +94,50 @@ PEAK_MAD_PER_S = CUS * MAD_LANE_OPS_PER_CLK_CU * CLOCK_HZ  # 39.32e12
 MEASURED_MAD_PER_S = 36.1e12  # tools/microbench/ubench_int: 58.75 lane-ops/clk/CU at 16 waves/CU
 
 
+SIMDS = CUS * 4
+XCDS = 8
+
+
+def pmc_utilisation(row, launch_ms, n_per_launch, mad_per_request=None):
+    """VALU utilisation, clock and HBM rate of one kernel: its counters from the
+    committed PMC pass (tools/pmc_passes.sh -> tools/pmc_summary.py; `row` is
+    one kernel of pmc_traffic.json, counters per launch over n_req requests)
+    and its launch duration measured live (HIP events).
+
+      clock      = GRBM_GUI_ACTIVE / 8 / duration   (GRBM sums the 8 XCDs;
+                   MI355X_MICROARCH.md 'DVFS give-back')
+      valu_busy  = SQ_ACTIVE_INST_VALU * 4 / (SIMDs * GRBM_GUI_ACTIVE / 8)
+                   (rocprof's gfx94x VALUBusy: SQ counts quad-cycles, one per
+                   wave64 VALU issue; 1.0 = every SIMD issued a VALU op every
+                   4 cycles of the kernel)
+      hbm_GBps   = (2 * FETCH_SIZE + WRITE_SIZE) bytes per request (gfx950
+                   FETCH_SIZE correction) * requests of the launch / duration
+      mad_share  = v_mad_u64_u32 per request / 64 over VALU instructions per
+                   request (wave64 instructions)
+    """
+    m = row.get("mean", {})
+    n_req = float(row.get("n_requests", 1_000_000))
+    sec = launch_ms * 1e-3
+    # the PMC launch covered n_req requests; scale its cycle counts to this launch's size
+    scale = n_per_launch / n_req
+    out = {"launch_ms": launch_ms, "n_per_launch": n_per_launch}
+    if "GRBM_GUI_ACTIVE" in m:
+        gui = m["GRBM_GUI_ACTIVE"] * scale
+        out["clock_GHz"] = gui / XCDS / sec / 1e9
+        if "SQ_ACTIVE_INST_VALU" in m:
+            out["valu_busy"] = m["SQ_ACTIVE_INST_VALU"] * scale * 4 / (SIMDS * gui / XCDS)
+    if "traffic_bytes_per_request" in row:
+        out["hbm_bytes_per_request"] = row["traffic_bytes_per_request"]
+        out["hbm_GBps"] = row["traffic_bytes_per_request"] * n_per_launch / sec / 1e9
+        out["hbm_frac_of_8TBps"] = out["hbm_GBps"] / 8000.0
+    if "SQ_INSTS_VALU" in m:
+        vpr = m["SQ_INSTS_VALU"] / n_req  # wave64 instructions per request
+        out["valu_insts_per_request"] = vpr * 64  # lane-instructions
+        if mad_per_request:
+            out["mad_share_of_valu"] = mad_per_request / (vpr * 64)
+    return out
+
+
 def sha_blocks(mlen):
     return (mlen + 81 + 127) // 128
 

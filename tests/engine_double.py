@@ -178,3 +178,58 @@ class OracleBlsEngine:
         gen = o.g2_from_bytes(np.asarray(gen128, np.uint8).tobytes())
         return np.asarray([np.frombuffer(o.g2_to_bytes(o.keygen(int.from_bytes(sk32[i].tobytes(), "big"), gen)),
                                          np.uint8) for i in range(sk32.shape[0])], np.uint8)
+
+
+class AsyncOracleEngine(OracleEngine):
+    """OracleEngine with edv_keys_add_async's contract: a registration returns
+    at once with a ticket and its build stays in flight until finish_builds()
+    (or keys_sync); a keyed verify of an id still building fails the test (the
+    product must route it to the general path), and the synchronous
+    keys_add / keys_set raise (the request path must never wait on a build)."""
+
+    def __init__(self, lib=None):
+        super().__init__(lib)
+        self.issued = 0
+        self.done = 0
+        self.building = {}  # id -> ticket
+        self.sync_calls = 0
+
+    def keys_add(self, pk32):
+        raise AssertionError("synchronous keys_add on the request path")
+
+    def keys_set(self, first_id, pk32):
+        raise AssertionError("synchronous keys_set on the request path")
+
+    def keys_add_async(self, pk32):
+        first = OracleEngine.keys_add(self, pk32)
+        self.issued += 1
+        for i in range(first, len(self.keys)):
+            self.building[i] = self.issued
+        return first, self.issued
+
+    def keys_set_async(self, first_id, pk32):
+        OracleEngine.keys_set(self, first_id, pk32)
+        self.issued += 1
+        for i in range(first_id, first_id + np.asarray(pk32, np.uint8).reshape(-1, 32).shape[0]):
+            self.building[i] = self.issued
+        return self.issued
+
+    def keys_ready(self, ticket):
+        return ticket <= self.done
+
+    def finish_builds(self):
+        self.done = self.issued
+        self.building.clear()
+
+    def keys_sync(self):
+        self.sync_calls += 1
+        self.finish_builds()
+
+    def keys_reset(self):
+        super().keys_reset()
+        self.finish_builds()
+
+    def verify_batch_keyed(self, sig64, key_idx, msgs, msg_off, sig_slot=64):
+        busy = [int(k) for k in key_idx if int(k) in self.building]
+        assert not busy, "keyed verify of ids still building: %s" % sorted(set(busy))[:8]
+        return super().verify_batch_keyed(sig64, key_idx, msgs, msg_off, sig_slot)

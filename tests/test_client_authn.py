@@ -540,3 +540,58 @@ def test_pipelined_parts_equal_per_message(oracle):
     eng.submits = 0
     got2 = [_outcome(r) for r in a.authenticate_batch(pool[:4096])]
     assert got2 == want[:4096] and eng.submits >= 3
+
+
+def _ref_outcomes(oracle, batches, lookup=None):
+    """The same batches through an authenticator with no key store (general path only)."""
+    ref = GpuAuthNr(engine=OracleEngine(oracle), nym_lookup=lookup, max_keys=0)
+    return [[_outcome(r) for r in ref.authenticate_batch(b)] for b in batches]
+
+
+def test_async_key_builds_stay_off_the_request_path(oracle):
+    """VERDICT r2 'keep hot-key table builds off the request path': an addIdr
+    key and a key promoted by use register with keys_add_async / keys_set_async
+    (the double raises on the synchronous forms); until a build completes its
+    requests take the general path, and the verdicts are the general path's at
+    every step, across an eviction too."""
+    from engine_double import AsyncOracleEngine
+    eng = AsyncOracleEngine(oracle)
+    idrs, vks, msgs = _signed(3, 48)
+    table = dict(zip(idrs, vks))
+    a = GpuAuthNr(engine=eng, nym_lookup=lambda st, idr: {"verkey": table[idr]}, max_keys=2, hot_key_uses=1)
+    a.addIdr(idrs[0], vks[0])
+    batches = [[msgs[k + s] for k in range(j, j + 12, 3) for s in range(2)] for j in range(0, 48, 12)]
+    lookup = lambda st, idr: {"verkey": table[idr]}  # noqa: E731
+    want = _ref_outcomes(oracle, batches + [[m for m in msgs if m["identifier"] == idrs[2]][:4]], lookup)
+    # batch 1: idrs[0]'s key (addIdr) is queued, not built: everything general; idrs[1] earns a slot
+    assert [_outcome(r) for r in a.authenticate_batch(batches[0])] == want[0]
+    assert a.stats["keyed_items"] == 0 and eng.issued == 1
+    # batch 2: idrs[1]'s build is queued in this batch, idrs[0]'s still running: still general
+    assert [_outcome(r) for r in a.authenticate_batch(batches[1])] == want[1]
+    assert a.stats["keyed_items"] == 0 and eng.issued == 2
+    eng.finish_builds()
+    # batch 3: both built -> keyed
+    assert [_outcome(r) for r in a.authenticate_batch(batches[2])] == want[2]
+    assert a.stats["keyed_items"] == len(batches[2])
+    # idrs[2] earns a slot with the store full: an eviction rebuild (keys_set_async), its requests general
+    third = [m for m in msgs if m["identifier"] == idrs[2]][:4]
+    assert [_outcome(r) for r in a.authenticate_batch(third)] == want[4]
+    before = a.stats["keyed_items"]
+    assert [_outcome(r) for r in a.authenticate_batch(third)] == want[4]
+    assert eng.issued == 3 and a.stats["keyed_items"] == before  # evicted into, still building
+    assert eng.sync_calls == 0  # no batch ever waited on a build
+    eng.finish_builds()
+    assert [_outcome(r) for r in a.authenticate_batch(third)] == want[4]
+    assert a.stats["keyed_items"] == before + len(third)
+
+
+def test_keys_settle_waits_for_queued_builds(oracle):
+    from engine_double import AsyncOracleEngine
+    eng = AsyncOracleEngine(oracle)
+    idrs, vks, msgs = _signed(2, 8)
+    a = GpuAuthNr(engine=eng)
+    for i, v in zip(idrs, vks):
+        a.addIdr(i, v)
+    assert a.keys_settle() == 2 and eng.sync_calls == 1 and not eng.building
+    assert a.authenticate_batch(msgs) == [m["identifier"] for m in msgs]
+    assert a.stats["keyed_items"] == len(msgs)

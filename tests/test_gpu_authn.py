@@ -110,6 +110,7 @@ def test_verify_ahead_drain_on_gpu(gpu_engine, oracle):
     a = GpuAuthNr(engine=eng)
     for idr, vk in zip(idrs, vks):
         a.addIdr(idr, vk)
+    a.keys_settle()  # genesis NYMs: their tables built before traffic (batches never wait on builds)
     assert prefetch_drain(a, rx) == 100
     assert eng.launches == 1 and a.stats["keyed_items"] == 100
     for i, r in enumerate(reqs):
@@ -149,6 +150,7 @@ def test_verify_ahead_batch_framed_drain_on_gpu(gpu_engine, oracle):
     a = GpuAuthNr(engine=eng)
     for idr, vk in zip(idrs, vks):
         a.addIdr(idr, vk)
+    a.keys_settle()  # genesis NYMs: their tables built before traffic (batches never wait on builds)
     assert prefetch_drain(a, rx) == 100
     assert eng.launches == 1 and a.stats["keyed_items"] == 100
     # the requests as the node authenticates them after unpacking one node's BATCH
@@ -188,6 +190,7 @@ def test_multi_engine_one_device(gpu_engine):
         c = GpuAuthNr(engine=auto)
         for idr, vk in zip(idrs, vks):
             c.addIdr(idr, vk)
+        c.keys_settle()
         rc = [r if isinstance(r, str) else type(r).__name__ for r in c.authenticate_batch(reqs)]
         assert rc == rb and c.stats["keyed_items"] == len(reqs)
     finally:
@@ -275,6 +278,7 @@ def test_pipelined_parts_on_gpu(gpu_engine):
     for a in (whole, parts):
         for idr, vk in zip(idrs, vks):
             a.addIdr(idr, vk)
+        a.keys_settle()
     batch = [copy.deepcopy(r) for r in reqs]
     batch[9000]["reqId"] += 1
     bad.add(9000)
@@ -286,3 +290,44 @@ def test_pipelined_parts_on_gpu(gpu_engine):
         for i, r in enumerate(r2):
             assert (type(r).__name__ == "InvalidSignature") if i in bad else (r == batch[i]["identifier"]), i
     assert parts.stats["keyed_items"] >= n
+
+
+@pytest.mark.gpu
+def test_async_key_promotion_on_gpu(gpu_engine):
+    """Hot-key promotion with the table builds off the request path
+    (edv_keys_add_async / edv_keys_set_async on the engine's build stream):
+    10 signers with room for 4 keys and hot_key_uses = 1, so batches keep
+    promoting and evicting while earlier builds still run.  A building key's
+    requests take the general path; every verdict is the construction's, in
+    every batch; once the builds drain, the store's keys are verified on the
+    key-table path."""
+    import copy
+    from plenum_amd.engine import EdVerifyEngine
+    reqs, rx, idrs, vks, pks, sers, sig = _drain(gpu_engine, n_req=2000, n_nodes=1, n_signers=10)
+    table = dict(zip(idrs, vks))
+    eng = EdVerifyEngine(0)  # a store of its own (4 slots at W = 16: 64 MiB tables, builds take ms)
+    try:
+        a = GpuAuthNr(engine=eng, nym_lookup=lambda st, idr: {"verkey": table[idr]}, max_keys=4, hot_key_uses=1)
+        bad = {i for i in range(2000) if i % 10 == 3}
+        seen_building = 0
+        for rep in range(6):
+            lo = (rep * 700) % 1500
+            batch = [copy.deepcopy(r) for r in reqs[lo:lo + 500]]
+            res = a.authenticate_batch(batch)
+            for j, r in enumerate(res):
+                if lo + j in bad:
+                    assert type(r).__name__ == "InvalidSignature", (rep, j)
+                else:
+                    assert r == batch[j]["identifier"], (rep, j)
+            seen_building = max(seen_building, a._key_store().building())
+        assert a.stats["keys_registered"] >= 4 and seen_building > 0
+        a.keys_settle()
+        ks = a._key_store()
+        assert ks.building() == 0 and len(ks) == 4
+        before = a.stats["keyed_items"]
+        res = a.authenticate_batch(reqs[:500])
+        assert [r if isinstance(r, str) else type(r).__name__ for r in res] == \
+               ["InvalidSignature" if i in bad else reqs[i]["identifier"] for i in range(500)]
+        assert a.stats["keyed_items"] > before
+    finally:
+        eng.close()

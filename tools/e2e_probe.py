@@ -25,6 +25,7 @@ print("built %d requests in %.1f s" % (n, time.perf_counter() - t0), flush=True)
 a = GpuAuthNr(engine=eng)
 for idr, vk in zip(idrs, vks):
     a.addIdr(idr, vk)
+a.keys_settle()
 a.authenticate_batch(reqs[:2048])
 a.authenticate_batch(reqs)  # buffers grown
 for part in parts:
@@ -47,6 +48,7 @@ eng = EdVerifyEngine(0)
 a = GpuAuthNr(engine=eng)
 for idr, vk in zip(idrs, vks):
     a.addIdr(idr, vk)
+a.keys_settle()
 a.authenticate_batch(reqs[:4096])
 lat, lat_eng, lat_prep = [], [], []
 for r in reqs[:330]:

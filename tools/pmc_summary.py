@@ -17,7 +17,7 @@ import sys
 
 
 def short(name):
-    m = re.search(r"(edv_\w+?)(?:<(\d+)>)?\(", name)
+    m = re.search(r"(edv_\w+?)(?:<(\w+)>)?\(", name)
     if m:
         return m.group(1) + ("<%s>" % m.group(2) if m.group(2) else "")
     return name[:60]
@@ -40,10 +40,10 @@ def main():
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 1_000_000
     out_json = sys.argv[3] if len(sys.argv) > 3 else None
     acc, grid = load(root)
-    summary = {"n": n, "kernels": {}}
+    summary = {"n": n, "kernels": {}, "run": sys.argv[4] if len(sys.argv) > 4 else os.path.basename(root)}
     for k in sorted(acc):
         c = {name: sum(v) / len(v) for name, v in acc[k].items()}
-        row = {"grid": grid[k], "dispatches": max(len(v) for v in acc[k].values()), "mean": c}
+        row = {"grid": grid[k], "dispatches": max(len(v) for v in acc[k].values()), "mean": c, "n_requests": n}
         if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
             row["traffic_bytes"] = (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
             row["traffic_bytes_per_request"] = row["traffic_bytes"] / n
