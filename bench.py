@@ -77,6 +77,9 @@ def parse():
     ap.add_argument("--e2e-n", type=int, default=1_000_000,
                     help="requests of the end-to-end authenticate_batch leg over configs[1] (0 = skip)")
     ap.add_argument("--e2e-c0", type=int, default=10_000, help="configs[0] end-to-end requests (0 = skip)")
+    ap.add_argument("--e2e-devices", type=int, default=1,
+                    help="1: also run the end-to-end leg through MultiEngine over 1/2/4/8 of the visible devices "
+                         "(one node process; rank 0 at world 1)")
     return ap.parse_args()
 
 
@@ -224,6 +227,51 @@ def time_e2e(eng, reqs, idrs, vks):
                     "value = the median of 3 batches after the first full-size one (steady state); first_batch_* "
                     "= that first batch (buffers allocated). single_authenticate_us: authenticate() of one "
                     "request not in the verdict cache (300 calls after 30 warm-up)"}
+
+
+def time_e2e_devices(eng, reqs, idrs, vks, counts):
+    """The node-shaped multi-GPU leg: one node process (looper.py:141-151),
+    GpuAuthNr over MultiEngine with k engines (multi.py: every batch split by
+    64-aligned request index, one host thread per device, key store
+    replicated on every device), k in `counts`.  Per k: the steady-state
+    authenticate_batch rate (median of 3 after two warm batches), the scan
+    and the GPU call in the same process as configs1.  Engine 0 is this
+    process's engine; the others are created here and closed after."""
+    from plenum_amd.client_authn import GpuAuthNr
+    from plenum_amd.multi import MultiEngine
+    out = {}
+    n = len(reqs)
+    for k in counts:
+        extra = [EdVerifyEngine(d) for d in range(1, k)]
+        me = MultiEngine(engines=[eng] + extra)
+        try:
+            a = GpuAuthNr(engine=me)
+            for idr, vk in zip(idrs, vks):
+                a.addIdr(idr, vk)
+            t0 = time.perf_counter()
+            a.keys_settle()  # the signers' tables on every device (built concurrently, one thread each)
+            keys_s = time.perf_counter() - t0
+            a.authenticate_batch(reqs)
+            a.authenticate_batch(reqs)
+            reps = []
+            for _ in range(3):
+                t0 = time.perf_counter()
+                res = a.authenticate_batch(reqs)
+                reps.append(time.perf_counter() - t0)
+            ok = sum(1 for r, m in zip(res, reqs) if r == m["identifier"])
+            del res
+            t = sorted(reps)[1]
+            out[str(k)] = {"engines": k, "value": n / t, "seconds": t, "accepted": ok,
+                           "keyed_items_share": a.stats["keyed_items"] / max(1, a.stats["batch_items"]),
+                           "keys_build_s_all_devices": keys_s}
+        finally:
+            for e in extra:
+                e.close()
+            if me._pool:
+                me._pool.shutdown()
+        if eng.keys_count():
+            eng.keys_reset()
+    return out
 
 
 def reference_path_baseline(eng, n, host):
@@ -703,6 +751,14 @@ def main():
             reqs, idrs, vks = e2e_requests(eng, m, args.signers, args.alias_len, spec=nym_spec, sig=sig_all,
                                            pks=pks)
             e2e["configs1"] = time_e2e(eng, reqs, idrs, vks)
+            if args.e2e_devices:
+                ndev = torch.cuda.device_count()
+                counts = [k for k in (1, 2, 4, 8) if k <= ndev]
+                e2e["by_devices"] = time_e2e_devices(eng, reqs, idrs, vks, counts)
+                e2e["by_devices"]["note"] = (
+                    "one node process over MultiEngine(k engines): configs1's %d requests per batch split by "
+                    "64-aligned request index across k devices (one host thread each), the native scan as in "
+                    "configs1 (up to 16 host threads); %d device(s) visible" % (m, ndev))
             del reqs
 
     if rank == 0:

@@ -611,6 +611,75 @@ PyObject* py_pack_sm(PyObject*, PyObject* args) {
 // bytes objects.
 constexpr int kSigSlot = 96;  // edverify.h EDV_SIG_SLOT96
 
+// The batch's distinct identifiers: an open-addressing table over the
+// identifier text (a 64-bit multiply-xor hash of 8-byte words, linear
+// probing, grown at half load).  Every request carries its identifier as its
+// own str object (json-decoded from the wire), so the lookup is by content.
+// A node-based std::unordered_map<std::string_view> here allocated a node per
+// emplace and cost ~30 % of a worker's time per request.
+struct IdrTable {
+  struct E {
+    uint64_t h;
+    const char* p;  // the identifier's bytes (the str object's data; owned by the batch's dicts)
+    size_t n;
+    uint32_t id;
+  };
+  std::vector<E> e;
+  size_t mask = 0, used = 0;
+  static uint64_t hash(const char* p, size_t n) {
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)n;
+    size_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+      uint64_t w;
+      memcpy(&w, p + i, 8);
+      h = (h ^ w) * 0xff51afd7ed558ccdull;
+      h ^= h >> 32;
+    }
+    uint64_t w = 0;
+    memcpy(&w, p + i, n - i);
+    h = (h ^ w) * 0xc4ceb9fe1a85ec53ull;
+    return h ^ (h >> 29);
+  }
+  void reset(size_t expect) {
+    size_t cap = 64;
+    while (cap < 2 * expect) cap <<= 1;
+    e.assign(cap, E{0, nullptr, 0, 0});
+    mask = cap - 1;
+    used = 0;
+  }
+  // the id of text (p, n), or `next` (fresh = true) when it is new
+  uint32_t find_or_add(const char* p, size_t n, uint32_t next, bool& fresh) {
+    if (2 * (used + 1) > e.size()) grow();
+    const uint64_t h = hash(p, n);
+    for (size_t s = h & mask;; s = (s + 1) & mask) {
+      E& x = e[s];
+      if (!x.p) {
+        x = E{h, p, n, next};
+        ++used;
+        fresh = true;
+        return next;
+      }
+      if (x.h == h && x.n == n && (x.p == p || memcmp(x.p, p, n) == 0)) {
+        fresh = false;
+        return x.id;
+      }
+    }
+  }
+  void grow() {
+    std::vector<E> old;
+    old.swap(e);
+    e.assign(old.empty() ? 64 : old.size() * 2, E{0, nullptr, 0, 0});
+    mask = e.size() - 1;
+    for (const E& x : old)
+      if (x.p)
+        for (size_t s = x.h & mask;; s = (s + 1) & mask)
+          if (!e[s].p) {
+            e[s] = x;
+            break;
+          }
+  }
+};
+
 struct ScanItem {
   PyObject* m = nullptr;
   const unsigned char* sp = nullptr;
@@ -792,12 +861,14 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
     b.sig.clear();
     b.ser.clear();
   }
-  struct alignas(64) IdrTable {  // a cache line (or more) of its own per worker
-    std::unordered_map<std::string_view, uint32_t> slot;
+  struct alignas(64) WorkerIdrs {  // a cache line (or more) of its own per worker
+    IdrTable slot;
     std::vector<PyObject*> obj;
     std::vector<Py_ssize_t> first;  // the item where the worker met it first
+    size_t deferred = 0;            // items left for the GIL pass (3)
   };
-  std::vector<IdrTable> tabs((size_t)t);
+  std::vector<WorkerIdrs> tabs((size_t)t);
+  for (WorkerIdrs& w : tabs) w.slot.reset(1024);
   std::vector<std::vector<uint8_t>> sigs((size_t)t);
   for (int w = 0; w < t; ++w) {  // no-ops once a batch of this size has been seen
     bufs[(size_t)w].sig.reserve((size_t)(n / t + kScanChunk) * 64);
@@ -805,7 +876,7 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
   }
   run_chunks(n, t, [&](int w, Py_ssize_t a, Py_ssize_t b) {
     ScanBuf& sb = bufs[(size_t)w];
-    IdrTable& tab = tabs[(size_t)w];
+    WorkerIdrs& tab = tabs[(size_t)w];
     std::vector<uint8_t>& sig = sigs[(size_t)w];
     for (Py_ssize_t i = a; i < b; ++i) {
       PyObject* m = items[i];
@@ -832,6 +903,7 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
       x.m = m;
       if (!PyUnicode_IS_ASCII(iv)) {  // its UTF-8 form may need allocating: under the GIL
         x.state = 2;
+        ++tab.deferred;
         continue;
       }
       x.sp = (const unsigned char*)PyUnicode_1BYTE_DATA(sv);
@@ -847,6 +919,7 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
       if (r != kOk) {
         sb.ser.resize(at);
         x.state = r == kDefer ? 2 : 0;
+        tab.deferred += r == kDefer;
         continue;
       }
       x.state = 1;
@@ -862,14 +935,13 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
         sb.sig.append((const char*)sig.data(), sig.size());
       }
       idr_of[(size_t)i] = iv;
-      auto ins = tab.slot.emplace(
-          std::string_view((const char*)PyUnicode_1BYTE_DATA(iv), (size_t)PyUnicode_GET_LENGTH(iv)),
-          (uint32_t)tab.obj.size());
-      if (ins.second) {
+      bool fresh = false;
+      x.uid = tab.slot.find_or_add((const char*)PyUnicode_1BYTE_DATA(iv), (size_t)PyUnicode_GET_LENGTH(iv),
+                                   (uint32_t)tab.obj.size(), fresh);
+      if (fresh) {
         tab.obj.push_back(iv);
         tab.first.push_back(i);
       }
-      x.uid = ins.first->second;
     }
   });
   auto t_p1 = now();
@@ -877,8 +949,11 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
   // first occurrence in the batch (the single-thread order, whichever worker
   // took which chunk)
   std::vector<PyObject*> uniq;
-  std::unordered_map<std::string_view, uint32_t> slot;
+  IdrTable slot;
+  slot.reset(tabs.empty() ? 64 : tabs[0].obj.size() + 64);
   std::vector<std::vector<uint32_t>> to_global((size_t)t);
+  size_t deferred = 0;
+  for (const WorkerIdrs& w : tabs) deferred += w.deferred;
   {
     struct Cand {
       Py_ssize_t first;
@@ -887,25 +962,26 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
     };
     std::vector<Cand> cand;
     for (int w = 0; w < t; ++w) {
-      const IdrTable& tb = tabs[(size_t)w];
+      const WorkerIdrs& tb = tabs[(size_t)w];
       to_global[(size_t)w].resize(tb.obj.size());
       for (size_t u = 0; u < tb.obj.size(); ++u) cand.push_back(Cand{tb.first[u], w, (uint32_t)u});
     }
     std::sort(cand.begin(), cand.end(), [](const Cand& a, const Cand& b) { return a.first < b.first; });
     for (const Cand& c : cand) {
       PyObject* o = tabs[(size_t)c.w].obj[c.local];
-      auto ins = slot.emplace(
-          std::string_view((const char*)PyUnicode_1BYTE_DATA(o), (size_t)PyUnicode_GET_LENGTH(o)),
-          (uint32_t)uniq.size());
-      if (ins.second) uniq.push_back(o);
-      to_global[(size_t)c.w][c.local] = ins.first->second;
+      bool fresh = false;
+      const uint32_t g = slot.find_or_add((const char*)PyUnicode_1BYTE_DATA(o), (size_t)PyUnicode_GET_LENGTH(o),
+                                          (uint32_t)uniq.size(), fresh);
+      if (fresh) uniq.push_back(o);
+      to_global[(size_t)c.w][c.local] = g;
     }
   }
   // (the items' worker-local ids are mapped in (4), on the workers)
   auto t_p2 = now();
   // (3) the items the workers left (non-ASCII identifiers, floats / big ints /
-  // wide-kind keys in the payload), redone under the GIL
-  {
+  // wide-kind keys in the payload), redone under the GIL; none in the steady
+  // state, which then skips this pass over the batch
+  if (deferred) {
     ScanBuf& sb = bufs[(size_t)t];
     std::vector<uint8_t> sig;
     for (Py_ssize_t i = 0; i < n; ++i) {
@@ -940,9 +1016,9 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
       x.sig_len = (uint32_t)sig.size();
       sb.sig.append((const char*)sig.data(), sig.size());
       idr_of[(size_t)i] = iv;
-      auto ins = slot.emplace(std::string_view(ip, (size_t)ni), (uint32_t)uniq.size());
-      if (ins.second) uniq.push_back(iv);
-      x.uid = ins.first->second;
+      bool fresh = false;
+      x.uid = slot.find_or_add(ip, (size_t)ni, (uint32_t)uniq.size(), fresh);
+      if (fresh) uniq.push_back(iv);
     }
   }
   auto t_p3 = now();

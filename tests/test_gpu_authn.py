@@ -296,38 +296,75 @@ def test_pipelined_parts_on_gpu(gpu_engine):
 def test_async_key_promotion_on_gpu(gpu_engine):
     """Hot-key promotion with the table builds off the request path
     (edv_keys_add_async / edv_keys_set_async on the engine's build stream):
-    10 signers with room for 4 keys and hot_key_uses = 1, so batches keep
-    promoting and evicting while earlier builds still run.  A building key's
-    requests take the general path; every verdict is the construction's, in
-    every batch; once the builds drain, the store's keys are verified on the
-    key-table path."""
+    10 signers with room for 4 keys and hot_key_uses = 1; each batch carries 5
+    of the signers, rotating, so batches keep promoting keys and evicting the
+    ones the batch does not use while earlier builds may still run.  A
+    building key's requests take the general path (the proxy records, at each
+    verify launch, how many ids were still building); every verdict is the
+    construction's, in every batch; once the builds drain, the store's keys
+    verify on the key-table path."""
     import copy
     from plenum_amd.engine import EdVerifyEngine
-    reqs, rx, idrs, vks, pks, sers, sig = _drain(gpu_engine, n_req=2000, n_nodes=1, n_signers=10)
+    reqs, rx, idrs, vks, pks, sers, sig = _drain(gpu_engine, n_req=3000, n_nodes=1, n_signers=10)
     table = dict(zip(idrs, vks))
-    eng = EdVerifyEngine(0)  # a store of its own (4 slots at W = 16: 64 MiB tables, builds take ms)
+    bad = {i for i in range(3000) if i % 10 == 3}
+
+    class Probe(_Counting):
+        seen = 0
+
+        def __getattr__(self, name):
+            attr = super().__getattr__(name)
+            if name in ("verify_batch", "verify_batch_keyed"):
+                def probed(*a, **k):
+                    ks = self.__dict__.get("_edv_key_store")
+                    if ks is not None:
+                        Probe.seen = max(Probe.seen, ks.building())
+                    return attr(*a, **k)
+                return probed
+            return attr
+
+    real = EdVerifyEngine(0)  # a store of its own (4 slots at W = 16: 64 MiB tables per key)
     try:
+        eng = Probe(real)
         a = GpuAuthNr(engine=eng, nym_lookup=lambda st, idr: {"verkey": table[idr]}, max_keys=4, hot_key_uses=1)
-        bad = {i for i in range(2000) if i % 10 == 3}
-        seen_building = 0
-        for rep in range(6):
-            lo = (rep * 700) % 1500
-            batch = [copy.deepcopy(r) for r in reqs[lo:lo + 500]]
+        for rep in range(8):
+            signers = {(rep + j) % 10 for j in range(5)}
+            idx = [i for i in range(3000) if i % 10 in signers][:600]
+            batch = [copy.deepcopy(reqs[i]) for i in idx]
             res = a.authenticate_batch(batch)
-            for j, r in enumerate(res):
-                if lo + j in bad:
-                    assert type(r).__name__ == "InvalidSignature", (rep, j)
+            for i, r in zip(idx, res):
+                if i in bad:
+                    assert type(r).__name__ == "InvalidSignature", (rep, i)
                 else:
-                    assert r == batch[j]["identifier"], (rep, j)
-            seen_building = max(seen_building, a._key_store().building())
-        assert a.stats["keys_registered"] >= 4 and seen_building > 0
+                    assert r == reqs[i]["identifier"], (rep, i)
+        assert a.stats["keys_registered"] > 4, a.stats  # evictions rebuilt slots
+        assert Probe.seen > 0  # some verify ran while a table was still building
         a.keys_settle()
         ks = a._key_store()
         assert ks.building() == 0 and len(ks) == 4
         before = a.stats["keyed_items"]
-        res = a.authenticate_batch(reqs[:500])
+        last = {(7 + j) % 10 for j in range(5)}
+        idx = [i for i in range(3000) if i % 10 in last][:600]
+        res = a.authenticate_batch([reqs[i] for i in idx])
         assert [r if isinstance(r, str) else type(r).__name__ for r in res] == \
-               ["InvalidSignature" if i in bad else reqs[i]["identifier"] for i in range(500)]
+               ["InvalidSignature" if i in bad else reqs[i]["identifier"] for i in idx]
         assert a.stats["keyed_items"] > before
     finally:
-        eng.close()
+        real.close()
+
+
+@pytest.mark.gpu
+def test_bench_e2e_devices_leg_on_gpu(gpu_engine):
+    """bench.py's node-shaped multi-GPU leg (end_to_end.by_devices: GpuAuthNr
+    over MultiEngine with k engines, one node process) at k = 1 on this box:
+    every request of a configs[1]-shaped batch accepted, on the key-table
+    path after keys_settle."""
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if root not in sys.path:
+        sys.path.insert(0, root)
+    import bench
+    reqs, idrs, vks = bench.e2e_requests(gpu_engine, 8192, 16, 43)
+    out = bench.time_e2e_devices(gpu_engine, reqs, idrs, vks, [1])
+    assert out["1"]["accepted"] == 8192 and out["1"]["keyed_items_share"] == 1.0, out
