@@ -77,6 +77,9 @@ def parse():
     ap.add_argument("--e2e-n", type=int, default=1_000_000,
                     help="requests of the end-to-end authenticate_batch leg over configs[1] (0 = skip)")
     ap.add_argument("--e2e-c0", type=int, default=10_000, help="configs[0] end-to-end requests (0 = skip)")
+    ap.add_argument("--key-order", choices=["arrival", "sorted"], default="arrival",
+                    help="arrival: request i signed by signer i %% signers (the keys of a wave all differ); "
+                         "sorted: requests grouped by signer (A/B of the comb's gather locality)")
     ap.add_argument("--e2e-devices", type=int, default=1,
                     help="1: also run the end-to-end leg through MultiEngine over 1/2/4/8 of the visible devices "
                          "(one node process; rank 0 at world 1)")
@@ -407,6 +410,10 @@ def main():
         item_start, item_end = roff[:-1][item_req], roff[1:][item_req]
         req_desc = ", %d requests x 1-5 signatures (mean %.2f), payload %d-%d B log-uniform" % (
             nreq, n / nreq, int(lens.min()), int(lens.max()))
+    if args.key_order == "sorted":
+        # requests grouped by signer (a batch sorted by key id; the messages stay, spans reordered)
+        order = np.argsort(key_idx, kind="stable")
+        key_idx, item_start, item_end = key_idx[order], item_start[order], item_end[order]
     mlen_mean = float(np.mean(item_end - item_start))
     buckets = args.length_buckets in ("on", "packed") or (args.length_buckets == "auto" and
                                                            lengths_mixed(item_start, item_end))
@@ -739,7 +746,7 @@ def main():
             cpu["reference_path_configs0"] = reference_path_baseline(eng, args.e2e_c0, host)
 
     e2e = None
-    if rank == 0 and world == 1 and args.config == "c1":
+    if rank == 0 and world == 1 and args.config == "c1" and args.key_order == "arrival":
         e2e = {}
         if args.e2e_c0 > 0:
             reqs, idrs, vks = e2e_requests(eng, args.e2e_c0, 100, 0, seed=11)

@@ -21,7 +21,11 @@ parts = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0, 1
 eng = EdVerifyEngine(0)
 t0 = time.perf_counter()
 reqs, idrs, vks = bench.e2e_requests(eng, n, 1000, 43)
-print("built %d requests in %.1f s" % (n, time.perf_counter() - t0), flush=True)
+if os.environ.get("WIRE"):  # every request json-decoded on its own, as the node receives it (own str objects)
+    import json
+    reqs = [json.loads(json.dumps(r)) for r in reqs]
+print("built %d requests in %.1f s (wire=%s)" % (n, time.perf_counter() - t0, bool(os.environ.get("WIRE"))),
+      flush=True)
 a = GpuAuthNr(engine=eng)
 for idr, vk in zip(idrs, vks):
     a.addIdr(idr, vk)
