@@ -80,6 +80,8 @@ def parse():
     ap.add_argument("--key-order", choices=["arrival", "sorted"], default="arrival",
                     help="arrival: request i signed by signer i %% signers (the keys of a wave all differ); "
                          "sorted: requests grouped by signer (A/B of the comb's gather locality)")
+    ap.add_argument("--key-sort", choices=["auto", "on", "off"], default="auto",
+                    help="comb lanes in key-sorted order (edv_set_key_sort; auto = sub-batches >= 4096)")
     ap.add_argument("--e2e-devices", type=int, default=1,
                     help="1: also run the end-to-end leg through MultiEngine over 1/2/4/8 of the visible devices "
                          "(one node process; rank 0 at world 1)")
@@ -377,6 +379,7 @@ def main():
     if hasattr(eng._lib, "edv_base_window"):
         RL.set_base_window(eng._lib.edv_base_window())
     eng.set_pipeline(args.pipeline)
+    eng.set_key_sort(args.key_sort)
     n = args.n if not (args.config == "c4" and args.n == 1_000_000) else 2_000_000
 
     # ---- synthetic signed batch (not timed)

@@ -132,6 +132,16 @@ int edv_set_pipeline(edv_ctx *ctx, int sub_batches);
  * chunk).  Groups that do not fit the arena are read in place.  The accept
  * bits do not depend on the mode. */
 int edv_set_length_buckets(edv_ctx *ctx, int mode);
+/* Key order of the comb (key-table path): mode 0 off, 1 on, 2 auto (default:
+ * sub-batches of 4,096 requests or more at key windows of 15 and up).  A
+ * counting sort of the sub-batch's key ids (the keyed path's "table" phase)
+ * makes the requests of one key neighbours, so a wave's 64 comb lanes gather
+ * from one key's rows instead of 64 keys' rows spread over the key store;
+ * the encode reads the permutation back and the accept bits are unchanged.
+ * Applies when the registered key count is below 16,384 (LDS cursors).
+ * Measured (profiles/r05e): key window 16 with key ids in a random order
+ * (configs[2]) comb 1.70 -> 1.02 ms per 1M; at window 14 no gain. */
+int edv_set_key_sort(edv_ctx *ctx, int mode);
 /* Size of the unit arena of mode 3 in bytes (default 1.25 GiB = 1,280 B per
  * lane of a 2^20-request chunk; allocated on first use; 0 = none).  Takes
  * effect at the next mode-3 launch. */

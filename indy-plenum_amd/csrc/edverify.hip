@@ -20,6 +20,7 @@
 //   edv_tally_*          distinct-voter ballots -> counts -> quorum flags.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <deque>
 #include <mutex>
@@ -516,6 +517,9 @@ __global__ __launch_bounds__(kBlock, EDV_DSM_MIN_WAVES) void edv_dsm_kernel(cons
 
 // Batched encode + compare + ballot.  Lane l of wave v owns requests
 // v*64*M + 64*j + l (j < M): every j is one coalesced 64-request word.
+// With perm (the comb ran in key-sorted order): slot r of pt / pre is request
+// perm[r], whose R and flags are read there and whose verdict goes to
+// ok8[perm[r]] (edv_ok_pack_kernel makes the words).
 struct DevEncode {
   const uint32_t* __restrict__ pt;
   uint32_t* __restrict__ pre;
@@ -524,6 +528,8 @@ struct DevEncode {
   unsigned long long* __restrict__ words;
   uint64_t stride, n, base, wbase;  // base = this lane's request for j = 0; wbase = word for j = 0
   uint32_t lane;
+  const uint32_t* __restrict__ perm;
+  uint8_t* __restrict__ ok8;
   __device__ uint64_t req(int j) const { return base + 64ull * j; }
   __device__ bool valid(int j) const { return req(j) < n; }
   __device__ void z(int j, fe& f) const {
@@ -554,12 +560,17 @@ struct DevEncode {
   }
   __device__ void emit(int j, const uint32_t enc[8], bool zero_z) const {
     bool ok = false;
+    uint64_t r = 0;
     if (valid(j)) {
-      const uint64_t r = req(j);
+      r = perm ? perm[req(j)] : req(j);
       const uint4* R = (const uint4*)(sig64 + 64 * r);
       const uint4 a = R[0], b = R[1];
       ok = !zero_z && flags[r] && enc[0] == a.x && enc[1] == a.y && enc[2] == a.z && enc[3] == a.w &&
            enc[4] == b.x && enc[5] == b.y && enc[6] == b.z && enc[7] == b.w;
+    }
+    if (perm) {
+      if (valid(j)) ok8[r] = ok ? 1 : 0;
+      return;
     }
     const unsigned long long bits = __ballot(ok);
     if (lane == 0 && valid(j)) words[wbase + j] = bits;
@@ -577,13 +588,78 @@ __global__ __launch_bounds__(kBlock) void edv_encode_kernel(const uint8_t* __res
                                                            uint32_t* __restrict__ pre,
                                                            const uint8_t* __restrict__ flags,
                                                            unsigned long long* __restrict__ accept_words,
-                                                           uint64_t stride) {
+                                                           uint64_t stride, const uint32_t* __restrict__ perm,
+                                                           uint8_t* __restrict__ ok8) {
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t wave = g >> 6;
   const uint32_t lane = (uint32_t)(g & 63);
   if (wave * 64ull * M >= n) return;  // whole wave past the end (wave-uniform)
-  DevEncode a{pt, pre, sig64, flags, accept_words, stride, n, wave * 64ull * M + lane, wave * M, lane};
+  DevEncode a{pt, pre, sig64, flags, accept_words, stride, n, wave * 64ull * M + lane, wave * M, lane, perm, ok8};
   encode_batch<M>(a);
+}
+
+// Accept words from per-request verdict bytes (the key-sorted path): one lane per request.
+__global__ __launch_bounds__(kBlock) void edv_ok_pack_kernel(const uint8_t* __restrict__ ok8, uint64_t n,
+                                                            unsigned long long* __restrict__ words) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if ((i & ~63ull) >= n) return;  // whole wave past the end (wave-uniform)
+  const unsigned long long bits = __ballot(i < n && ok8[i] != 0);
+  if ((i & 63) == 0) words[i >> 6] = bits;
+}
+
+// ---- key order of the comb (edv_set_key_sort) ------------------------------
+// A counting sort of a sub-batch's key ids: requests of one key become
+// neighbours, so a wave's 64 comb lanes gather from one key's rows (a few
+// pages) instead of 64 keys' rows spread over the key store -- what lets the
+// wide key window (16: 4 MiB rows, 64 MiB per key) run at its row count when
+// the batch arrives in any key order.  Bins = ids, the last bin for
+// out-of-range ids.  (1) each block histograms a contiguous range of the
+// requests in LDS and adds its bins into the global totals; (2) an exclusive
+// scan of the totals gives each bin's base, copied into the cursors; (3) each
+// block histograms its range again, reserves a stretch of every bin it uses
+// with one global atomic on the bin's cursor, and places its requests there
+// with LDS cursors.  Order within a key is arbitrary (verdicts are per
+// request).
+constexpr uint32_t kSortBlocks = 256, kSortThreads = 1024;
+constexpr uint32_t kSortMaxBins = 16384;  // 64 KiB of LDS per block
+__device__ __forceinline__ void sort_range(uint64_t n, uint64_t& lo, uint64_t& hi) {
+  const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+  lo = blockIdx.x * per;
+  hi = lo + per < n ? lo + per : n;
+}
+__device__ __forceinline__ void block_hist(const uint32_t* __restrict__ kidx, uint64_t lo, uint64_t hi, uint32_t nb,
+                                           uint32_t* h) {
+  for (uint32_t k = threadIdx.x; k < nb; k += blockDim.x) h[k] = 0;
+  __syncthreads();
+  for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    const uint32_t k = kidx[i];
+    atomicAdd(&h[k < nb - 1 ? k : nb - 1], 1u);
+  }
+  __syncthreads();
+}
+__global__ __launch_bounds__(kSortThreads) void edv_key_hist_kernel(const uint32_t* __restrict__ kidx, uint64_t n,
+                                                                   uint32_t nb, uint32_t* __restrict__ total) {
+  extern __shared__ uint32_t h[];
+  uint64_t lo, hi;
+  sort_range(n, lo, hi);
+  block_hist(kidx, lo, hi, nb, h);
+  for (uint32_t k = threadIdx.x; k < nb; k += blockDim.x)
+    if (h[k]) atomicAdd(&total[k], h[k]);
+}
+__global__ __launch_bounds__(kSortThreads) void edv_key_scatter_kernel(const uint32_t* __restrict__ kidx, uint64_t n,
+                                                                      uint32_t nb, uint32_t* __restrict__ cursor,
+                                                                      uint32_t* __restrict__ perm) {
+  extern __shared__ uint32_t h[];
+  uint64_t lo, hi;
+  sort_range(n, lo, hi);
+  block_hist(kidx, lo, hi, nb, h);
+  for (uint32_t k = threadIdx.x; k < nb; k += blockDim.x)
+    if (h[k]) h[k] = atomicAdd(&cursor[k], h[k]);  // this block's stretch of bin k
+  __syncthreads();
+  for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    const uint32_t k = kidx[i];
+    perm[atomicAdd(&h[k < nb - 1 ? k : nb - 1], 1u)] = (uint32_t)i;
+  }
 }
 
 // ---- key-table path (comb.h) ---------------------------------------------
@@ -766,9 +842,13 @@ __global__ __launch_bounds__(kBlock, EDV_COMB_MIN_WAVES) void edv_comb_kernel(co
                                                          const uint32_t* __restrict__ key_tab, uint64_t key_cap,
                                                          const uint32_t* __restrict__ btab,
                                                          const uint32_t* __restrict__ ident,
-                                                         uint32_t* __restrict__ pt, uint64_t stride) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+                                                         uint32_t* __restrict__ pt, uint64_t stride,
+                                                         const uint32_t* __restrict__ kperm) {
+  // lane t runs request i = kperm[t] (key-sorted order, edv_set_key_sort) and
+  // leaves R' in slot t for the encode, which reads kperm back
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const uint64_t i = kperm ? kperm[t] : t;
   uint32_t S[8], h[8];
   load_words(S, sig64 + 64 * i + 32, 8);
 #pragma unroll
@@ -791,8 +871,8 @@ __global__ __launch_bounds__(kBlock, EDV_COMB_MIN_WAVES) void edv_comb_kernel(co
   uint32_t sink = comb_mul_add<W>(Q, h, ta);
   sink ^= comb_mul_add<kBaseW>(Q, S, tb);
 #endif
-  store_point_soa(pt, stride, i, Q);
-  if (sink == 0x9e3779b9u && key0 == 0xffffffffu && key_count == 0) pt[i] = sink;  // keeps the prefetches live
+  store_point_soa(pt, stride, t, Q);
+  if (sink == 0x9e3779b9u && key0 == 0xffffffffu && key_count == 0) pt[t] = sink;  // keeps the prefetches live
 }
 
 // Fixed-base comb: [x]B with x < 2^253, 64 madds over BASE_COMB (global).
@@ -1030,6 +1110,15 @@ struct edv_ctx {
   int last_nsub = 0;
   uint64_t last_chunk_n = 0;  // requests in the last chunk (what edv_last_phases_ms covers)
   int max_sub = 1;  // edv_set_pipeline (1, 2 and 4 sub-batches measure within 1% at 1M: profiles/r02b)
+  // key-sorted comb order (edv_set_key_sort): the permutation and the verdict bytes [kMaxLanes];
+  // per sub-batch: block offsets [kSortBlocks][bins], bin totals / bases [bins] x 2, scan scratch
+  int key_sort = 2;
+  uint32_t* d_kperm = nullptr;
+  uint8_t* d_ok8 = nullptr;
+  uint32_t* d_kbin = nullptr;
+  uint64_t kbin_cap = 0;  // bins allocated per sub-batch
+  void* d_kscan_tmp = nullptr;
+  size_t kscan_tmp_bytes = 0;  // per sub-batch
   bool timed = false;
   // key-table store (registered public keys)
   uint32_t* d_btab_comb32 = nullptr;  // base-point comb table (kBaseW; 11 GiB at W = 24)
@@ -1159,11 +1248,65 @@ uint32_t key_tab_words(int w) {
 }
 
 int launch_encode(edv_ctx* ctx, const uint8_t* sig, uint64_t cn, unsigned long long* words, uint64_t off,
-                  uint64_t chunk, hipStream_t st) {
+                  uint64_t chunk, hipStream_t st, const uint32_t* perm = nullptr) {
   const uint64_t waves = div_up(cn, 64ull * kEncodeM);
   const uint32_t grid = (uint32_t)div_up(waves * 64, kBlock);
+  uint8_t* ok8 = perm ? ctx->d_ok8 + off : nullptr;
   hipLaunchKernelGGL(edv_encode_kernel<kEncodeM>, dim3(grid), dim3(kBlock), 0, st, sig, cn, ctx->d_pt + off,
-                     ctx->d_pre + off, ctx->d_flags + off, words, chunk);
+                     ctx->d_pre + off, ctx->d_flags + off, words, chunk, perm, ok8);
+  HIP_TRY(hipGetLastError());
+  if (perm) {
+    hipLaunchKernelGGL(edv_ok_pack_kernel, dim3((uint32_t)div_up(cn, kBlock)), dim3(kBlock), 0, st, ok8, cn, words);
+    HIP_TRY(hipGetLastError());
+  }
+  return 0;
+}
+
+// The key-sort scratch for `bins` bins (grown when the key count passes it; in-flight launches
+// may read the old one, so a regrowth waits for the device).
+int ensure_key_sort(edv_ctx* ctx, uint64_t bins) {
+  if (bins <= ctx->kbin_cap) return 0;
+  uint64_t cap = ctx->kbin_cap ? ctx->kbin_cap : 1024;
+  while (cap < bins) cap *= 2;
+  if (cap > kSortMaxBins) cap = kSortMaxBins;
+  if (ctx->d_kbin) {
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipFree(ctx->d_kbin));
+    ctx->d_kbin = nullptr;
+  }
+  if (ctx->d_kscan_tmp) {
+    HIP_TRY(hipFree(ctx->d_kscan_tmp));
+    ctx->d_kscan_tmp = nullptr;
+  }
+  ctx->kbin_cap = 0;
+  const uint64_t per_sub = 2 * cap;
+  hipError_t e = hipMalloc(&ctx->d_kbin, edv_ctx::kSub * per_sub * sizeof(uint32_t));
+  if (e != hipSuccess) return set_err(EDV_ENOMEM, "key-sort scratch: %s", hipGetErrorString(e));
+  size_t bytes = 0;
+  HIP_TRY(rocprim::exclusive_scan(nullptr, bytes, ctx->d_kbin, ctx->d_kbin, 0u, (size_t)cap, rocprim::plus<uint32_t>(),
+                                  ctx->stream));
+  ctx->kscan_tmp_bytes = (bytes + 255) & ~(size_t)255;
+  e = hipMalloc(&ctx->d_kscan_tmp, edv_ctx::kSub * (ctx->kscan_tmp_bytes ? ctx->kscan_tmp_bytes : 256));
+  if (e != hipSuccess) return set_err(EDV_ENOMEM, "key-sort scan scratch: %s", hipGetErrorString(e));
+  ctx->kbin_cap = cap;
+  return 0;
+}
+
+// kperm of a keyed sub-batch: its requests in key-id order (edv_key_*_kernel).
+int launch_key_sort(edv_ctx* ctx, const uint32_t* kidx, uint64_t cn, uint32_t bins, uint32_t* kperm, int sub,
+                    hipStream_t q) {
+  uint32_t* total = ctx->d_kbin + sub * 2 * ctx->kbin_cap;
+  uint32_t* cursor = total + ctx->kbin_cap;
+  const size_t lds = (size_t)bins * sizeof(uint32_t);
+  // blocks of at least 2,048 requests (a block's LDS histogram costs its bins)
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>(kSortBlocks, div_up(cn, 2048));
+  HIP_TRY(hipMemsetAsync(total, 0, (size_t)bins * sizeof(uint32_t), q));
+  hipLaunchKernelGGL(edv_key_hist_kernel, dim3(blocks), dim3(kSortThreads), lds, q, kidx, cn, bins, total);
+  HIP_TRY(hipGetLastError());
+  size_t tmp = ctx->kscan_tmp_bytes;
+  HIP_TRY(rocprim::exclusive_scan((char*)ctx->d_kscan_tmp + (size_t)sub * tmp, tmp, total, cursor, 0u, (size_t)bins,
+                                  rocprim::plus<uint32_t>(), q));
+  hipLaunchKernelGGL(edv_key_scatter_kernel, dim3(blocks), dim3(kSortThreads), lds, q, kidx, cn, bins, cursor, kperm);
   HIP_TRY(hipGetLastError());
   return 0;
 }
@@ -1243,6 +1386,7 @@ int launch_sub(edv_ctx* ctx, bool keyed, const SubBatch& b, const uint8_t* msgs,
   uint8_t* fl = ctx->d_flags + b.soff;
   uint32_t* pt = ctx->d_pt + b.soff;
   uint32_t* perm = nullptr;
+  uint32_t* kperm = nullptr;  // keyed path: the comb's key-sorted lane order (nullptr = request order)
   UnitArena ua = {nullptr, nullptr, nullptr, 0};
   HIP_TRY(hipEventRecord(ev[0], q));
   if (ctx->bucket_now && (b.cn > 64 || ctx->pack_now)) {
@@ -1270,10 +1414,20 @@ int launch_sub(edv_ctx* ctx, bool keyed, const SubBatch& b, const uint8_t* msgs,
                          ctx->d_key_pk, ctx->d_key_valid, msgs, b.ms, b.me, b.cn, hs, fl, chunk, perm, ua);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ev[1], q));
+    // key order of the comb lanes (the keyed path's "table" phase): auto sorts sub-batches of
+    // 4,096 requests or more at key windows of 15 and up (rows of 2 MiB and more) whose ids fit
+    // the LDS cursors (kSortMaxBins)
+    const uint64_t bins = (uint64_t)kc + 1;
+    if ((ctx->key_sort == 1 || (ctx->key_sort == 2 && b.cn >= 4096 && ctx->key_w >= 15)) && bins <= kSortMaxBins) {
+      int r = ensure_key_sort(ctx, bins);
+      if (r) return r;
+      kperm = ctx->d_kperm + b.soff;
+      if ((r = launch_key_sort(ctx, b.kidx, b.cn, (uint32_t)bins, kperm, sub, q))) return r;
+    }
     HIP_TRY(hipEventRecord(ev[2], q));
 #define EDV_COMB_LAUNCH(W)                                                                                   \
   hipLaunchKernelGGL(edv_comb_kernel<W>, dim3(grid), dim3(kBlock), 0, q, b.sig, b.kidx, kc, b.cn, hs,        \
-                     ctx->d_key_tab, ctx->key_cap, ctx->d_btab_comb32, ctx->d_ident, pt, chunk)
+                     ctx->d_key_tab, ctx->key_cap, ctx->d_btab_comb32, ctx->d_ident, pt, chunk, kperm)
 #define EDV_COMB_CASE(W) \
   case W:                \
     EDV_COMB_LAUNCH(W);  \
@@ -1327,7 +1481,7 @@ int launch_sub(edv_ctx* ctx, bool keyed, const SubBatch& b, const uint8_t* msgs,
     HIP_TRY(hipGetLastError());
   }
   HIP_TRY(hipEventRecord(ev[3], q));
-  int r = launch_encode(ctx, b.sig, b.cn, b.words, b.soff, chunk, q);
+  int r = launch_encode(ctx, b.sig, b.cn, b.words, b.soff, chunk, q, kperm);
   if (r) return r;
   HIP_TRY(hipEventRecord(ev[4], q));
   return 0;
@@ -2068,6 +2222,9 @@ edv_ctx* edv_create(int device) {
     return fail("hipMalloc(pre)", e);
   if ((e = hipMalloc(&ctx->d_perm, ctx->scratch_lanes * sizeof(uint32_t))) != hipSuccess)
     return fail("hipMalloc(perm)", e);
+  if ((e = hipMalloc(&ctx->d_kperm, ctx->scratch_lanes * sizeof(uint32_t))) != hipSuccess)
+    return fail("hipMalloc(kperm)", e);
+  if ((e = hipMalloc(&ctx->d_ok8, ctx->scratch_lanes)) != hipSuccess) return fail("hipMalloc(ok8)", e);
   if ((e = hipMalloc(&ctx->d_lenkey, 2 * ctx->scratch_lanes)) != hipSuccess) return fail("hipMalloc(lenkey)", e);
   if ((e = hipMalloc(&ctx->d_dedup, 6 * ctx->scratch_lanes * sizeof(uint32_t))) != hipSuccess)
     return fail("hipMalloc(dedup)", e);
@@ -2114,6 +2271,10 @@ void edv_destroy(edv_ctx* ctx) {
   if (ctx->d_flags) (void)hipFree(ctx->d_flags);
   if (ctx->d_pt) (void)hipFree(ctx->d_pt);
   if (ctx->d_perm) (void)hipFree(ctx->d_perm);
+  if (ctx->d_kperm) (void)hipFree(ctx->d_kperm);
+  if (ctx->d_ok8) (void)hipFree(ctx->d_ok8);
+  if (ctx->d_kbin) (void)hipFree(ctx->d_kbin);
+  if (ctx->d_kscan_tmp) (void)hipFree(ctx->d_kscan_tmp);
   if (ctx->d_gunits) (void)hipFree(ctx->d_gunits);
   if (ctx->d_goff) (void)hipFree(ctx->d_goff);
   if (ctx->d_scan_tmp) (void)hipFree(ctx->d_scan_tmp);
@@ -2192,6 +2353,13 @@ int edv_set_length_buckets(edv_ctx* ctx, int mode) {
 int edv_set_unit_arena(edv_ctx* ctx, uint64_t bytes) {
   if (!ctx) return set_err(EDV_EINVAL, "null context");
   ctx->arena_want = bytes / sizeof(Chunk16);
+  return 0;
+}
+
+int edv_set_key_sort(edv_ctx* ctx, int mode) {
+  if (!ctx) return set_err(EDV_EINVAL, "null context");
+  if (mode < 0 || mode > 2) return set_err(EDV_EINVAL, "key-sort mode %d (0 off, 1 on, 2 auto)", mode);
+  ctx->key_sort = mode;
   return 0;
 }
 

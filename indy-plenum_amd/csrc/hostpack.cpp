@@ -869,6 +869,11 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
   };
   std::vector<WorkerIdrs> tabs((size_t)t);
   for (WorkerIdrs& w : tabs) w.slot.reset(1024);
+  // the signature output (n slots) is sized before the scan: in slot mode the workers write an
+  // item's base58 text slot while its text is still in cache (phase 5 writes the rest)
+  char* dsig = nullptr;
+  PyObject* o_sig = refs.o_sig = out_buffer(out_sig, (Py_ssize_t)n * sig_slot, &dsig);
+  if (!o_sig) return nullptr;
   std::vector<std::vector<uint8_t>> sigs((size_t)t);
   for (int w = 0; w < t; ++w) {  // no-ops once a batch of this size has been seen
     bufs[(size_t)w].sig.reserve((size_t)(n / t + kScanChunk) * 64);
@@ -929,6 +934,10 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
       if (len64 == 1) {
         x.text = 1;
         x.sig_len = 64;
+        char* ds = dsig + (size_t)i * sig_slot;  // slot: the text, zero padding, its length in the last byte
+        memcpy(ds, x.sp, (size_t)x.ns);
+        memset(ds + x.ns, 0, (size_t)sig_slot - 1 - (size_t)x.ns);
+        ds[sig_slot - 1] = (char)x.ns;
       } else {
         x.sig_at = sb.sig.size();
         x.sig_len = (uint32_t)sig.size();
@@ -1066,15 +1075,18 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
     for (Py_ssize_t i = a; i < b; ++i) off[(size_t)i + 1] = at += off[(size_t)i + 1];
   });
   // (5) sig64 and the messages, written by the workers into the result objects
-  char *dsig = nullptr, *dmsg = nullptr;
-  PyObject* o_sig = refs.o_sig = out_buffer(out_sig, (Py_ssize_t)n * sig_slot, &dsig);
-  PyObject* o_msg = refs.o_msg = o_sig ? out_buffer(out_msg, (Py_ssize_t)off[(size_t)n], &dmsg) : nullptr;
+  char* dmsg = nullptr;
+  PyObject* o_msg = refs.o_msg = out_buffer(out_msg, (Py_ssize_t)off[(size_t)n], &dmsg);
   PyObject* ret = nullptr;
   if (o_msg) {
     run_chunks(n, t, [&](int, Py_ssize_t a, Py_ssize_t b) {
       for (Py_ssize_t i = a; i < b; ++i) {
         const ScanItem& x = it[(size_t)i];
         char* ds = dsig + (size_t)i * sig_slot;
+        if (x.state == 1 && x.text) {  // slot written by the worker in (1)
+          memcpy(dmsg + off[(size_t)i], bufs[x.buf].ser.data() + x.ser_at, x.ser_len);
+          continue;
+        }
         if (slots) memset(ds + 64, 0, (size_t)sig_slot - 64);  // slot[95] = 0: raw R || S in bytes 0..63
         if (x.state != 1 || shortv[(size_t)i]) {
           memset(ds, 0, 64);
@@ -1084,13 +1096,6 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
         const char* sr = sb.ser.data() + x.ser_at;
         const size_t ls = x.sig_len, lm = x.ser_len;
         char* dm = dmsg + off[(size_t)i];
-        if (x.text) {  // slot: the base58 text, its length in the last byte
-          memcpy(ds, x.sp, (size_t)x.ns);
-          memset(ds + x.ns, 0, 64 - std::min<size_t>(64, (size_t)x.ns));
-          ds[sig_slot - 1] = (char)x.ns;
-          memcpy(dm, sr, lm);
-          continue;
-        }
         const char* sg = sb.sig.data() + x.sig_at;
         if (ls >= 64) {  // sm[64:] = sig[64:] || ser
           memcpy(ds, sg, 64);

@@ -280,6 +280,12 @@ class EdVerifyEngine:
         """Sub-batches per chunk (1..4; 1 = kernels run one at a time)."""
         check(self._lib.edv_set_pipeline(self._ctx, int(sub_batches)))
 
+    def set_key_sort(self, mode):
+        """Key-sorted comb order on the key-table path: False/0 off, True/1
+        on, "auto"/2 (the default: sub-batches of 4,096 requests or more)."""
+        m = {"auto": 2, "on": 1, "off": 0}.get(mode, mode)
+        check(self._lib.edv_set_key_sort(self._ctx, int(m)))
+
     def set_length_buckets(self, mode):
         """Hash lanes sorted by SHA-512 block count: False/0 off, True/1 on,
         "auto"/2 (the default; host-offset calls decide per batch, edverify.h),

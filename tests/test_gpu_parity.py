@@ -200,10 +200,12 @@ def test_large_batch_properties(gpu_engine, nym_1m):
     assert digests[0] == digests[1]
 
 
-@pytest.mark.parametrize("config", ["c1", "c2"])
-def test_keyed_headline_1m(gpu_engine, oracle, nym_1m, config):
+@pytest.mark.parametrize("config,w,sort", [("c1", 14, "auto"), ("c2", 14, "auto"), ("c2", 16, "auto"),
+                                           ("c2", 16, "off")])
+def test_keyed_headline_1m(gpu_engine, oracle, nym_1m, config, w, sort):
     """The headline configuration as bench.py times it: key-table path at key
-    window 14, 1M requests, message spans, 4 sub-batches.  c1: all valid ->
+    window 14 / 16, 1M requests, message spans, 4 sub-batches, the comb in
+    key-sorted order (edv_set_key_sort auto) or request order.  c1: all valid ->
     every bit set.  c2: the configs[2] 10% corruption mix (synth.corrupt_configs2:
     R/S/M bit flips, S+L, S|2^255, small-order and non-canonical A, R = identity,
     R+T8; corrupted keys registered as keys of their own) -> the construction's
@@ -219,7 +221,8 @@ def test_keyed_headline_1m(gpu_engine, oracle, nym_1m, config):
     uniq, inv = np.unique(pk, axis=0, return_inverse=True)
     try:
         gpu_engine.keys_reset()
-        gpu_engine.keys_set_window(14)
+        gpu_engine.keys_set_window(w)
+        gpu_engine.set_key_sort(sort)
         assert gpu_engine.keys_add(uniq) == 0
         d_sig = torch.from_numpy(sig).to(dev)
         d_k = torch.from_numpy(inv.reshape(-1).astype(np.int32)).to(dev)
@@ -232,6 +235,7 @@ def test_keyed_headline_1m(gpu_engine, oracle, nym_1m, config):
         torch.cuda.synchronize()
         got = _bits(words, n)
     finally:
+        gpu_engine.set_key_sort("auto")
         gpu_engine.keys_reset()
         gpu_engine.keys_set_window(10)
     wrong = np.nonzero(got != expect)[0]
@@ -270,6 +274,47 @@ def test_keyed_random_vs_oracle_and_out_of_range(gpu_engine, oracle):
     kidx[::5] = gpu_engine.keys_count() + 7  # unregistered ids reject
     got = gpu_engine.verify_batch_keyed(sig, kidx, buf, off)
     assert not got[::5].any() and (got[1::5] == want[1::5]).all()
+
+
+@pytest.mark.parametrize("pipeline", [1, 3])
+def test_key_sorted_comb_matches_request_order(gpu_engine, oracle, pipeline):
+    """edv_set_key_sort: the comb in key-sorted lane order (counting sort of
+    the key ids; the encode reads the permutation back and packs verdict
+    bytes) gives the request-order verdicts bit for bit: 20,011 requests
+    (not a multiple of 64), 1,500 keys in random order, 5% of the ids
+    unregistered, 10% of the signatures corrupted, 1 or 3 sub-batches (each
+    sorts with its own scratch); == the general path with the same keys."""
+    n = 20011
+    rng = np.random.default_rng(31)
+    seeds = rng.integers(0, 256, size=(1500, 32), dtype=np.uint8)
+    pks, sks = gpu_engine.seed_keypair_batch(seeds)
+    msgs = [bytes(rng.integers(0, 256, size=int(rng.integers(0, 400)), dtype=np.uint8)) for _ in range(n)]
+    buf, off = pack_messages(msgs)
+    kid = rng.integers(0, 1500, size=n).astype(np.uint32)
+    sig = gpu_engine.sign_batch(sks, kid, buf, off)
+    bad = rng.random(n) < 0.10
+    sig[bad, rng.integers(0, 64, size=int(bad.sum()))] ^= 1
+    want = gpu_engine.verify_batch(sig, pks[kid], buf, off)
+    try:
+        gpu_engine.keys_reset()
+        first = gpu_engine.keys_add(pks)
+        ids = kid + np.uint32(first)
+        drop = rng.random(n) < 0.05
+        ids[drop] = gpu_engine.keys_count() + 3
+        gpu_engine.set_pipeline(pipeline)
+        got = {}
+        for mode in ("off", "on", "auto"):
+            gpu_engine.set_key_sort(mode)
+            got[mode] = gpu_engine.verify_batch_keyed(sig, ids, buf, off)
+    finally:
+        gpu_engine.set_key_sort("auto")
+        gpu_engine.set_pipeline(1)
+        gpu_engine.keys_reset()
+    exp = want & ~drop
+    for mode, g in got.items():
+        assert (g == exp).all(), (mode, np.nonzero(g != exp)[0][:8])
+    idx = np.nonzero(~drop)[0][:300]
+    assert (_oracle_sample(oracle, sig, pks[kid], buf, off, idx) == got["on"][idx]).all()
 
 
 @pytest.mark.parametrize("w", [4, 6, 8, 12, 13, 14, 16])
