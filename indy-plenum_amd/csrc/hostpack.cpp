@@ -695,11 +695,35 @@ struct alignas(64) ScanBuf {  // one cache line per worker: the string headers c
   std::string sig, ser;
 };
 
+// CPUs this process may use: its affinity mask, capped by a cgroup v2 CPU quota
+// (cpu.max "quota period"; the GPU box shows 256 CPUs but grants 16 of them).
+int cpu_budget() {
+  static const int budget = [] {
+    cpu_set_t set;
+    int aff = sched_getaffinity(0, sizeof set, &set) == 0 ? CPU_COUNT(&set) : 0;
+    if (aff <= 0) aff = (int)std::max(1u, std::thread::hardware_concurrency());
+    int quota = aff;
+    if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+      char q[32] = {0};
+      long period = 0;
+      if (fscanf(f, "%31s %ld", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0)
+        quota = (int)std::max(1L, atol(q) / period);
+      fclose(f);
+    }
+    return std::max(1, std::min(aff, quota));
+  }();
+  return budget;
+}
+
+// Scan workers for n items: one per 2k items (two kScanChunk chunks or more each), up to the
+// CPUs this process may use and at most kMaxScanThreads (a node host with more CPUs than the GPU
+// box's 16-CPU share scans a large batch on more of them).
+constexpr int kMaxScanThreads = 48;
 int scan_threads(Py_ssize_t n, int want) {
   if (want > 0) return std::min(want, 64);
-  const unsigned hc = std::thread::hardware_concurrency();
-  const Py_ssize_t by_size = n / 2048 + 1;  // two kScanChunk chunks or more per worker
-  return (int)std::max<Py_ssize_t>(1, std::min<Py_ssize_t>({(Py_ssize_t)(hc ? hc : 1), (Py_ssize_t)16, by_size}));
+  const Py_ssize_t by_size = n / 2048 + 1;
+  return (int)std::max<Py_ssize_t>(
+      1, std::min<Py_ssize_t>({(Py_ssize_t)cpu_budget(), (Py_ssize_t)kMaxScanThreads, by_size}));
 }
 
 // Host workers of the scan and the pack: the calling thread (worker 0, left
@@ -747,14 +771,42 @@ struct ScanScratch {
   std::string fast, shortv;
   std::vector<uint32_t> uidx;
 };
-ScanScratch& scan_scratch() {
-  static ScanScratch* s = new ScanScratch;  // never destroyed (interpreter teardown order)
-  return *s;
+// One spare scratch kept across calls (taken by a scan, given back when it --
+// or the pack handle of a deferred scan -- is done); a scan entered while the
+// spare is out (a garbage collection's finalizer inside a scan, a second
+// deferred batch) gets a fresh one.  Touched only under the GIL.
+ScanScratch* g_spare = nullptr;
+ScanScratch* take_scratch() {
+  ScanScratch* s = g_spare ? g_spare : new ScanScratch;
+  g_spare = nullptr;
+  return s;
 }
-// A scan entered while another is still running (only reachable through a
-// finalizer run by a garbage collection inside the outer scan's allocations)
-// gets scratch of its own.
-bool g_scan_busy = false;
+void give_scratch(ScanScratch* s) {
+  if (!s) return;
+  if (!g_spare)
+    g_spare = s;
+  else
+    delete s;
+}
+
+// A deferred scan's state for pack_range: the scratch (items, worker buffers,
+// offsets), the output pointers and references to the output objects.
+struct PackState {
+  ScanScratch* S = nullptr;
+  PyObject *o_sig = nullptr, *o_msg = nullptr;
+  char *dsig = nullptr, *dmsg = nullptr;
+  int sig_slot = 64, t = 1;
+  Py_ssize_t n = 0;
+};
+void pack_items(const PackState& P, Py_ssize_t lo, Py_ssize_t hi);
+void pack_capsule_free(PyObject* cap) {
+  PackState* P = (PackState*)PyCapsule_GetPointer(cap, "edv.pack");
+  if (!P) return;
+  give_scratch(P->S);
+  Py_XDECREF(P->o_sig);
+  Py_XDECREF(P->o_msg);
+  delete P;
+}
 
 // Output buffer for (5): the caller's bytearray grown to `need` bytes (never
 // shrunk, so its pages stay mapped from call to call); or any other writable
@@ -809,8 +861,12 @@ struct PyRefs {
 
 PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
   PyObject *msgs, *ignore = Py_None, *out = Py_None;
-  int want_threads = 0, sig_slot = 64;
-  if (!PyArg_ParseTuple(args, "O|OiOi", &msgs, &ignore, &want_threads, &out, &sig_slot)) return nullptr;
+  int want_threads = 0, sig_slot = 64, defer = 0;
+  if (!PyArg_ParseTuple(args, "O|OiOii", &msgs, &ignore, &want_threads, &out, &sig_slot, &defer)) return nullptr;
+  if (defer && !unique_form) {
+    PyErr_SetString(PyExc_ValueError, "defer needs scan_batch_u");
+    return nullptr;
+  }
   if (sig_slot != 64 && sig_slot != kSigSlot) {
     PyErr_Format(PyExc_ValueError, "slot must be 64 (raw signatures) or %d (base58 slots)", kSigSlot);
     return nullptr;
@@ -835,13 +891,11 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
   static PyObject* k_sig = PyUnicode_InternFromString("signature");
   static PyObject* k_idr = PyUnicode_InternFromString("identifier");
   const Py_ssize_t n = PySequence_Fast_GET_SIZE(fm);
-  ScanScratch own;
-  ScanScratch& S = g_scan_busy ? own : scan_scratch();
-  struct Busy {
-    bool was;
-    Busy() : was(g_scan_busy) { g_scan_busy = true; }
-    ~Busy() { g_scan_busy = was; }
-  } busy;
+  struct Held {  // the scratch goes back to the spare slot on every exit unless a pack handle takes it
+    ScanScratch* s = take_scratch();
+    ~Held() { give_scratch(s); }
+  } held;
+  ScanScratch& S = *held.s;
   std::vector<ScanItem>& it = S.it;
   std::vector<PyObject*>& idr_of = S.idr_of;  // borrowed (the dicts hold them)
   it.resize((size_t)n);                       // entries reset by the workers
@@ -1074,40 +1128,36 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
     uint64_t at = csum[(size_t)(a / kScanChunk)];
     for (Py_ssize_t i = a; i < b; ++i) off[(size_t)i + 1] = at += off[(size_t)i + 1];
   });
-  // (5) sig64 and the messages, written by the workers into the result objects
+  // (5) sig64 and the messages, written by the workers into the result objects (a deferred
+  // scan leaves this to pack_range, stretch by stretch, so the caller can queue each stretch's
+  // DMA while the next one packs)
   char* dmsg = nullptr;
   PyObject* o_msg = refs.o_msg = out_buffer(out_msg, (Py_ssize_t)off[(size_t)n], &dmsg);
   PyObject* ret = nullptr;
   if (o_msg) {
-    run_chunks(n, t, [&](int, Py_ssize_t a, Py_ssize_t b) {
-      for (Py_ssize_t i = a; i < b; ++i) {
-        const ScanItem& x = it[(size_t)i];
-        char* ds = dsig + (size_t)i * sig_slot;
-        if (x.state == 1 && x.text) {  // slot written by the worker in (1)
-          memcpy(dmsg + off[(size_t)i], bufs[x.buf].ser.data() + x.ser_at, x.ser_len);
-          continue;
-        }
-        if (slots) memset(ds + 64, 0, (size_t)sig_slot - 64);  // slot[95] = 0: raw R || S in bytes 0..63
-        if (x.state != 1 || shortv[(size_t)i]) {
-          memset(ds, 0, 64);
-          continue;
-        }
-        const ScanBuf& sb = bufs[x.buf];
-        const char* sr = sb.ser.data() + x.ser_at;
-        const size_t ls = x.sig_len, lm = x.ser_len;
-        char* dm = dmsg + off[(size_t)i];
-        const char* sg = sb.sig.data() + x.sig_at;
-        if (ls >= 64) {  // sm[64:] = sig[64:] || ser
-          memcpy(ds, sg, 64);
-          memcpy(dm, sg + 64, ls - 64);
-          memcpy(dm + (ls - 64), sr, lm);
-        } else {
-          memcpy(ds, sg, ls);
-          memcpy(ds + ls, sr, 64 - ls);
-          memcpy(dm, sr + (64 - ls), lm - (64 - ls));
-        }
+    PackState P;
+    P.S = &S;
+    P.dsig = dsig;
+    P.dmsg = dmsg;
+    P.sig_slot = sig_slot;
+    P.t = t;
+    P.n = n;
+    PyObject* handle = nullptr;
+    if (defer) {
+      PackState* hp = new PackState(P);
+      handle = PyCapsule_New(hp, "edv.pack", pack_capsule_free);
+      if (!handle) {
+        delete hp;
+        return nullptr;
       }
-    });
+      hp->o_sig = o_sig;
+      hp->o_msg = o_msg;
+      Py_INCREF(o_sig);
+      Py_INCREF(o_msg);
+      held.s = nullptr;  // the handle owns the scratch now
+    } else {
+      pack_items(P, 0, n);
+    }
     if (prof) {
       auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
       fprintf(stderr, "scan: n=%zd threads=%d  workers %.0f us, merge %.0f us, under the GIL %.0f us, pack %.0f us\n",
@@ -1120,10 +1170,17 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
           Py_INCREF(uniq[u]);
           PyList_SET_ITEM(ul, (Py_ssize_t)u, uniq[u]);
         }
-        ret = Py_BuildValue("(y#y#OOOy#y#)", fast.data(), (Py_ssize_t)n, (const char*)uidx.data(),
-                            (Py_ssize_t)(uidx.size() * 4), ul, o_sig, o_msg, (const char*)off.data(),
-                            (Py_ssize_t)(off.size() * 8), shortv.data(), (Py_ssize_t)n);
+        if (handle)
+          ret = Py_BuildValue("(y#y#OOOy#y#N)", fast.data(), (Py_ssize_t)n, (const char*)uidx.data(),
+                              (Py_ssize_t)(uidx.size() * 4), ul, o_sig, o_msg, (const char*)off.data(),
+                              (Py_ssize_t)(off.size() * 8), shortv.data(), (Py_ssize_t)n, handle);
+        else
+          ret = Py_BuildValue("(y#y#OOOy#y#)", fast.data(), (Py_ssize_t)n, (const char*)uidx.data(),
+                              (Py_ssize_t)(uidx.size() * 4), ul, o_sig, o_msg, (const char*)off.data(),
+                              (Py_ssize_t)(off.size() * 8), shortv.data(), (Py_ssize_t)n);
         Py_DECREF(ul);
+      } else {
+        Py_XDECREF(handle);
       }
     } else {
       PyObject* idrs = PyList_New(n);
@@ -1162,6 +1219,71 @@ PyObject* scan_impl(PyObject* args, bool unique_form) {
 
 PyObject* py_scan_batch(PyObject*, PyObject* args) { return scan_impl(args, false); }
 PyObject* py_scan_batch_u(PyObject*, PyObject* args) { return scan_impl(args, true); }
+
+// Phase (5) for items [lo, hi): their messages at off[i] and the signature slots the workers did
+// not write (raw signatures, zeroed slots of items that take the Python path or are short).
+void pack_items(const PackState& P, Py_ssize_t lo, Py_ssize_t hi) {
+  const ScanScratch& S = *P.S;
+  const std::vector<ScanItem>& it = S.it;
+  const std::vector<ScanBuf>& bufs = S.bufs;
+  const std::vector<uint64_t>& off = S.off;
+  const std::string& shortv = S.shortv;
+  const int sig_slot = P.sig_slot;
+  const bool slots = sig_slot == kSigSlot;
+  char* dsig = P.dsig;
+  char* dmsg = P.dmsg;
+  run_chunks(hi - lo, P.t, [&](int, Py_ssize_t a0, Py_ssize_t b0) {
+    for (Py_ssize_t i = lo + a0; i < lo + b0; ++i) {
+      const ScanItem& x = it[(size_t)i];
+      char* ds = dsig + (size_t)i * sig_slot;
+      if (x.state == 1 && x.text) {  // slot written by the worker in (1)
+        memcpy(dmsg + off[(size_t)i], bufs[x.buf].ser.data() + x.ser_at, x.ser_len);
+        continue;
+      }
+      if (slots) memset(ds + 64, 0, (size_t)sig_slot - 64);  // slot[95] = 0: raw R || S in bytes 0..63
+      if (x.state != 1 || shortv[(size_t)i]) {
+        memset(ds, 0, 64);
+        continue;
+      }
+      const ScanBuf& sb = bufs[x.buf];
+      const char* sr = sb.ser.data() + x.ser_at;
+      const size_t ls = x.sig_len, lm = x.ser_len;
+      char* dm = dmsg + off[(size_t)i];
+      const char* sg = sb.sig.data() + x.sig_at;
+      if (ls >= 64) {  // sm[64:] = sig[64:] || ser
+        memcpy(ds, sg, 64);
+        memcpy(dm, sg + 64, ls - 64);
+        memcpy(dm + (ls - 64), sr, lm);
+      } else {
+        memcpy(ds, sg, ls);
+        memcpy(ds + ls, sr, 64 - ls);
+        memcpy(dm, sr + (64 - ls), lm - (64 - ls));
+      }
+    }
+  });
+}
+
+// pack_range(handle, lo, hi): phase (5) of a deferred scan_batch_u for items [lo, hi).
+PyObject* py_pack_range(PyObject*, PyObject* args) {
+  PyObject* cap;
+  Py_ssize_t lo, hi;
+  if (!PyArg_ParseTuple(args, "Onn", &cap, &lo, &hi)) return nullptr;
+  PackState* P = (PackState*)PyCapsule_GetPointer(cap, "edv.pack");
+  if (!P) return nullptr;
+  if (lo < 0 || hi > P->n || lo > hi) {
+    PyErr_SetString(PyExc_ValueError, "pack_range: range outside the batch");
+    return nullptr;
+  }
+  try {
+    pack_items(*P, lo, hi);
+  } catch (const std::bad_alloc&) {
+    return PyErr_NoMemory();
+  } catch (...) {
+    PyErr_SetString(PyExc_RuntimeError, "pack_range: native error");
+    return nullptr;
+  }
+  Py_RETURN_NONE;
+}
 
 // results_from(codes, uidx, uniq) -> list: item i is uniq[uidx[i]] where
 // codes[i] == 1 (verified: authenticate() returns the identifier), None
@@ -1242,6 +1364,9 @@ PyMethodDef kMethods[] = {
      "scan_batch with the identifiers as indices into the batch's distinct identifiers; slot=96: sig is n "
      "96-byte signature slots (edverify.h EDV_SIG_SLOT96: base58 text decoded on the GPU, or raw R||S); out "
      "items may be any writable buffers large enough (e.g. the engine's pinned host memory)"},
+    {"pack_range", py_pack_range, METH_VARARGS,
+     "pack_range(handle, lo, hi): write items [lo, hi) of a deferred scan_batch_u (defer=1 returns the handle as "
+     "an 8th element) into its output buffers"},
     {"results_from", py_results_from, METH_VARARGS,
      "results_from(codes_u8, uidx_u32, uniq) -> list: uniq[uidx[i]] where codes[i] == 1, else None"},
     {"gather_items", py_gather_items, METH_VARARGS,

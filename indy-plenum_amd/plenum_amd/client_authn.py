@@ -63,6 +63,10 @@ try:  # native batch scan (csrc/hostpack.cpp): authenticate()'s host steps for a
     from ._hostpack import gather_items as _gather_items, results_from as _results_from, scan_batch_u as _scan_batch
 except ImportError:  # pragma: no cover - the per-message path below
     _scan_batch = _gather_items = _results_from = None
+try:
+    from ._hostpack import pack_range as _pack_range
+except ImportError:  # pragma: no cover
+    _pack_range = None
 
 try:  # native packing (csrc/hostpack.cpp)
     from ._hostpack import pack_sm as _pack_sm, pack_split64 as _pack_split64
@@ -104,6 +108,7 @@ ROLE = 'role'
 KEY_STORE_BYTES = 32 << 30  # HBM for key tables: the window is the widest that fits max_keys
 _SIG_SLOT = 96  # edverify.h EDV_SIG_SLOT96: signatures as base58 text, decoded on the GPU
 _PINNED_MIN_BATCH = 4096  # smaller batches keep the bytearrays (the library stages them cheaply)
+_STREAM_CHUNK = 1 << 18   # edverify.hip kHostChunk: the library's copy / kernel chunk
 
 
 _MISSING = object()
@@ -142,7 +147,7 @@ class _GpuState:
 
     def __init__(self, engine=None, device=0, devices=None, verdict_cache_size=1 << 20, key_window="auto",
                  max_keys=16384, hot_key_uses=2, key_store_bytes=KEY_STORE_BYTES, scan_threads=0,
-                 pipeline_part=0, async_key_builds=True):
+                 pipeline_part=0, async_key_builds=True, stream=True):
         self.engine = engine
         self.device = device
         self.devices = devices
@@ -175,6 +180,9 @@ class _GpuState:
         # the engine's build stream while batches go on; their requests take the general path until
         # the build completes (engines without edv_keys_add_async build synchronously)
         self.async_key_builds = async_key_builds
+        # batches of 2 library chunks (2^19 requests) or more pack chunk by chunk, each chunk's DMA and
+        # kernels overlapping the next chunk's pack (_authenticate_streamed)
+        self.stream = stream
         self.stats = {"batches": 0, "batch_items": 0, "cache_hits": 0, "single_verifies": 0, "keyed_items": 0,
                       "keys_registered": 0}
 
@@ -196,7 +204,9 @@ class GpuAuthMixin:
         this many requests or more are scanned in parts whose GPU work
         overlaps the next part's scan; 0 = off); async_key_builds (key
         tables registered on the request path build in the background, their
-        requests on the general path until built; default True)."""
+        requests on the general path until built; default True); stream
+        (batches of 2^19 requests or more pack chunk by chunk under the
+        previous chunk's DMA; default True)."""
         self._edv = _GpuState(engine=engine, device=device, **options)
 
     @property
@@ -301,6 +311,23 @@ class GpuAuthMixin:
         if g.max_keys <= 0:
             return None
         return KeyStore.attach(self._engine(), g.key_window, g.max_keys)
+
+    def _register_waiting(self, ks, batch_keys):
+        """Keys that earned a slot (may evict least-recently-used keys not in
+        this batch) and addIdr keys (free slots only), registered before the
+        batch routes its items (asynchronous builds by default)."""
+        g = self._g
+        if g.hot:
+            got = ks.register(list(g.hot), pinned=batch_keys, evict=True, asynchronous=g.async_key_builds)
+            g.stats["keys_registered"] += len(got)
+            g.hot.clear()
+        if g.pending:
+            room = ks.free_slots()
+            if room > 0:
+                got = ks.register([k for k in g.pending if k not in ks][:room], evict=False,
+                                  asynchronous=g.async_key_builds)
+                g.stats["keys_registered"] += len(got)
+            g.pending.clear()
 
     def keys_settle(self):
         """Register the addIdr keys waiting for a slot and wait until every
@@ -501,7 +528,57 @@ class GpuAuthMixin:
             part = self._g.pipeline_part
             if part and len(msgs) >= 2 * part and hasattr(eng, "verify_submit") and bufs is not self._g.scan_out:
                 return self._authenticate_pipelined(msgs, eng, slot, bufs, part)
+            if (self._g.stream and _pack_range is not None and len(msgs) >= 2 * _STREAM_CHUNK
+                    and hasattr(eng, "verify_submit") and bufs is not self._g.scan_out):
+                return self._authenticate_streamed(msgs, eng, slot, bufs)
             return self._authenticate_batch_scanned_into(msgs, bufs, slot)
+
+    def _authenticate_streamed(self, msgs, eng, slot, bufs):
+        """A large batch whose pack overlaps its DMA: one scan of the whole
+        batch with the pack deferred (scan_batch_u defer=1), then per
+        library chunk of 2^18 requests the pack of its messages into pinned
+        memory (pack_range) and edv_verify_submit, so chunk c's copy engine
+        and kernels run while chunk c + 1 packs; one collect per chunk.  In
+        the node's steady state (every item scanned, every identifier
+        resolved to a built key); any other batch packs whole and takes the
+        ordinary path (same verdicts)."""
+        import numpy as np
+        g = self._g
+        n = len(msgs)
+        scan = _scan_batch(msgs, [SIG], g.scan_threads, bufs, slot, 1)
+        fast_b, uidx_b, uniq, sig_o, msg_o, off, short, handle = scan
+        off_a = np.frombuffer(off, np.uint64)
+        mlen = int(off_a[-1])
+        g.msg_bytes_per_item = max(g.msg_bytes_per_item * 0.5, mlen / n)
+        ukeys = [self._key_for(idr) for idr in uniq]  # authenticate():93-99, once per identifier
+        ids = None
+        ks = self._key_store()
+        if ks is not None and fast_b.count(0) == 0 and all(k.__class__ is bytes for k in ukeys):
+            self._register_waiting(ks, list(dict.fromkeys(ukeys)))
+            ids = ks.lookup(ukeys)
+            if any(i is None for i in ids):
+                ids = None
+        if ids is None:  # not the steady state: the whole batch packed, the ordinary path
+            _pack_range(handle, 0, n)
+            return self._finish_scanned(msgs, scan[:7], slot, ukeys)
+        kid = np.asarray(ids, np.uint32)[np.frombuffer(uidx_b, np.uint32)]
+        sig_a = np.frombuffer(sig_o, np.uint8, count=slot * n).reshape(-1, slot)
+        msg_a = np.frombuffer(msg_o, np.uint8, count=mlen)
+        handles = []
+        for c0 in range(0, n, _STREAM_CHUNK):
+            c1 = min(n, c0 + _STREAM_CHUNK)
+            _pack_range(handle, c0, c1)
+            handles.append(eng.verify_submit(sig_a[c0:c1], kid[c0:c1], msg_a, off_a[c0:c1 + 1], True, slot))
+        ok = np.concatenate([np.asarray(eng.verify_collect(h), bool) for h in handles])
+        del handles, sig_a, msg_a
+        ok &= np.frombuffer(short, np.uint8) == 0
+        g.stats["batches"] += 1
+        g.stats["batch_items"] += n
+        g.stats["keyed_items"] += n
+        results = _results_from(ok.view(np.uint8).tobytes(), uidx_b, uniq)
+        for i in np.flatnonzero(~ok).tolist():
+            results[i] = InvalidSignature()
+        return results
 
     def _authenticate_pipelined(self, msgs, eng, slot, bufs, part):
         """A large batch in parts of `part` requests: the scan of part k + 1
@@ -663,17 +740,7 @@ class GpuAuthMixin:
         kid_u[has_key] = -1
         ks = self._key_store()
         if ks is not None and uniq_keys:
-            if g.hot:
-                got = ks.register(list(g.hot), pinned=uniq_keys, evict=True, asynchronous=g.async_key_builds)
-                g.stats["keys_registered"] += len(got)
-                g.hot.clear()
-            if g.pending:
-                room = ks.free_slots()
-                if room > 0:
-                    got = ks.register([k for k in g.pending if k not in ks][:room], evict=False,
-                                      asynchronous=g.async_key_builds)
-                    g.stats["keys_registered"] += len(got)
-                g.pending.clear()
+            self._register_waiting(ks, uniq_keys)
             id_of = {k: i for k, i in zip(uniq_keys, ks.lookup(uniq_keys)) if i is not None}
             kid_u[has_key] = [id_of.get(k, -1) for k in ukey_list]
         # the items of each path: a whole-batch slice when one path takes them all

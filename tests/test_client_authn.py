@@ -595,3 +595,32 @@ def test_keys_settle_waits_for_queued_builds(oracle):
     assert a.keys_settle() == 2 and eng.sync_calls == 1 and not eng.building
     assert a.authenticate_batch(msgs) == [m["identifier"] for m in msgs]
     assert a.stats["keyed_items"] == len(msgs)
+
+
+def test_streamed_batch_equals_whole(oracle, monkeypatch):
+    """authenticate_batch's streamed path (scan with the pack deferred, then per
+    library chunk pack_range + verify_submit, so a chunk's DMA overlaps the
+    next chunk's pack): the same outcome per message as the unstreamed path,
+    in the steady state (keys registered) and when the batch leaves it (an
+    unknown identifier, a missing signature, a forgery)."""
+    from plenum_amd import client_authn as CA
+    idrs, vks, msgs = _signed(3, 5000)
+    monkeypatch.setattr(CA, "_STREAM_CHUNK", 1024)
+    eng = OracleEngine(oracle)
+    a = GpuAuthNr(engine=eng)
+    ref = GpuAuthNr(engine=OracleEngine(oracle), max_keys=0)
+    for i, v in zip(idrs, vks):
+        a.addIdr(i, v)
+        ref.addIdr(i, v)
+    a.keys_settle()
+    batch = [dict(m) for m in msgs]
+    batch[17]["reqId"] += 1  # forged
+    subs = getattr(eng, "submits", 0)
+    got = [_outcome(r) for r in a.authenticate_batch(batch)]
+    assert got == [_outcome(r) for r in ref.authenticate_batch(batch)]
+    assert eng.submits - subs == 5 and a.stats["keyed_items"] == 5000  # 5 chunks streamed, all keyed
+    odd = [dict(m) for m in msgs]
+    odd[3]["identifier"] = "UnknownIdentifier1111"
+    del odd[4000]["signature"]
+    got = [_outcome(r) for r in a.authenticate_batch(odd)]
+    assert got == [_outcome(r) for r in ref.authenticate_batch(odd)]
