@@ -142,6 +142,14 @@ int edv_set_length_buckets(edv_ctx *ctx, int mode);
  * Measured (profiles/r05e): key window 16 with key ids in a random order
  * (configs[2]) comb 1.70 -> 1.02 ms per 1M; at window 14 no gain. */
 int edv_set_key_sort(edv_ctx *ctx, int mode);
+/* Small keyed batches (a message that missed the verify-ahead cache): host-
+ * pointer keyed verifies of at most max_requests requests (default 256; 0 =
+ * never) run one workgroup of three waves per request -- the hash, the two
+ * combs' rows on separate lanes summed as trees, and R decoded beside them
+ * instead of inverting R' afterwards (encode(R') == R iff X' = x_R Z',
+ * Y' = y_R Z' with R canonical and decodable) -- for latency; same verdicts
+ * as the batch kernels. */
+int edv_set_small_batch(edv_ctx *ctx, uint64_t max_requests);
 /* Size of the unit arena of mode 3 in bytes (default 1.25 GiB = 1,280 B per
  * lane of a 2^20-request chunk; allocated on first use; 0 = none).  Takes
  * effect at the next mode-3 launch. */

@@ -621,6 +621,7 @@ __global__ __launch_bounds__(kBlock) void edv_ok_pack_kernel(const uint8_t* __re
 // with LDS cursors.  Order within a key is arbitrary (verdicts are per
 // request).
 constexpr uint32_t kSortBlocks = 256, kSortThreads = 1024;
+constexpr uint64_t kCompactBytes = 256 << 10;  // host_submit: small chunks in one pinned block, one copy
 constexpr uint32_t kSortMaxBins = 16384;  // 64 KiB of LDS per block
 __device__ __forceinline__ void sort_range(uint64_t n, uint64_t& lo, uint64_t& hi) {
   const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
@@ -875,6 +876,236 @@ __global__ __launch_bounds__(kBlock, EDV_COMB_MIN_WAVES) void edv_comb_kernel(co
   if (sink == 0x9e3779b9u && key0 == 0xffffffffu && key_count == 0) pt[t] = sink;  // keeps the prefetches live
 }
 
+// ---- low-latency keyed verify for small batches (edv_set_small_batch) -------
+// A batch of a few requests (authenticate() of a message the verify-ahead did
+// not cover) is latency-bound: the three-kernel path runs each request's 29
+// mixed additions and its own ~265-product inversion as serial chains on one
+// lane (hash 35 + comb 90 + encode 85 us).  Here each request gets a workgroup
+// of three waves:
+//   wave 0: prechecks + h = SHA-512(R || A || M) mod L (lane 0), then the key
+//           comb's rows on lanes 0..RK-1 -- each lane fetches its row's signed
+//           entry and sets it as a point (one product) -- summed as a tree of
+//           full additions across lanes (log2 levels, points moved by
+//           shuffles), then the base sum added and the result compared;
+//   wave 1: the base comb's rows the same way ([S]B needs only S);
+//   wave 2: R decoded (libsodium's frombytes: the x of R's sign from y, one
+//           exponentiation), so no inversion of R' is needed:
+//             encode(R') == R  <=>  y_R < p, (x_R, y_R) on the curve, and
+//             X' == x_R Z', Y' == y_R Z'  (x_R = 0 with the sign bit set never
+//             matches: libsodium encodes x = 0 with sign 0).
+// The exponentiation runs beside the hash instead of after the comb.  Same
+// verdicts as the batch path (tests/test_gpu_parity.py: small batches == the
+// large path on golden, edge and random items).
+__device__ __forceinline__ void shfl_fe(fe& out, const fe& in, int delta) {
+#pragma unroll
+  for (int l = 0; l < 10; ++l) out.v[l] = (uint32_t)__shfl_down((int)in.v[l], delta, 64);
+}
+// Sum of the p3 points of lanes 0..width-1 of this wave (width a power of two
+// <= 64; lanes >= rows hold the identity) into lane 0: log2(width) levels of
+// p + q (q as cached).
+__device__ void lane_tree_sum(ge_p3& P, int lane, int width) {
+#pragma unroll 1
+  for (int step = 1; step < width; step <<= 1) {
+    ge_p3 Q;
+    shfl_fe(Q.X, P.X, step);
+    shfl_fe(Q.Y, P.Y, step);
+    shfl_fe(Q.Z, P.Z, step);
+    shfl_fe(Q.T, P.T, step);
+    if ((lane & (2 * step - 1)) == 0 && lane < width) {
+      ge_cached c;
+      ge_p1p1 t;
+      ge_p3_to_cached(c, Q);
+      ge_add(t, P, c);
+      ge_p1p1_to_p3_addlike(P, t);
+    }
+  }
+}
+// The point of row `row` of a comb for the signed digit of y (comb_recode'd scalar).
+template <int W, class T>
+__device__ void comb_row_point(ge_p3& P, const uint32_t y[9], int row, const T& tab) {
+  const int e = comb_digit<W>(y, row);
+  ge_niels nb;
+  tab.load(row, (e < 0 ? -e : e) - 1, nb);
+  comb_set_entry(P, nb, e);
+}
+
+// libsodium's frombytes of R (ge_frombytes, negate = false) cut in two at a
+// point of its exponentiation, so the first ~145 products run beside the hash
+// and the rest beside the key comb's tree: part 1 leaves u = y^2 - 1,
+// v = d y^2 + 1, v3 = v^3, t0, t1 and t2 = t1^(2^30) of fe_pow22523(u v^7).
+struct RDecode {
+  fe y, u, v, v3, t0, t1, t2;
+};
+__device__ void r_decode_part1(RDecode& d, const uint32_t s[8]) {
+  fe one, x, z;
+  fe_1(one);
+  fe_frombytes(d.y, s);
+  fe_sq(d.u, d.y);
+  fe_mul(d.v, d.u, fe_const_d());
+  fe_sub(d.u, d.u, one);
+  fe_carry(d.u);
+  fe_add(d.v, d.v, one);
+  fe_sq(d.v3, d.v);
+  fe_mul(d.v3, d.v3, d.v);
+  fe_sq(x, d.v3);
+  fe_mul(x, x, d.v);
+  fe_mul(z, x, d.u);  // u v^7: fe_pow22523's input, its chain up to t1 = z^(2^100 - 1) then 30 squarings
+  fe_sq(d.t0, z);
+  fe_sqn(d.t1, d.t0, 2);
+  fe_mul(d.t1, z, d.t1);
+  fe_mul(d.t0, d.t0, d.t1);
+  fe_sq(d.t0, d.t0);
+  fe_mul(d.t0, d.t1, d.t0);
+  fe_sqn(d.t1, d.t0, 5);
+  fe_mul(d.t0, d.t1, d.t0);
+  fe_sqn(d.t1, d.t0, 10);
+  fe_mul(d.t1, d.t1, d.t0);
+  fe_sqn(d.t2, d.t1, 20);
+  fe_mul(d.t1, d.t2, d.t1);
+  fe_sqn(d.t1, d.t1, 10);
+  fe_mul(d.t0, d.t1, d.t0);
+  fe_sqn(d.t1, d.t0, 50);
+  fe_mul(d.t1, d.t1, d.t0);
+  fe_sqn(d.t2, d.t1, 30);
+}
+// The rest: x of R with R's sign (false: no square root).  Same value as ge_frombytes.
+__device__ bool r_decode_part2(fe& x, RDecode& d, const uint32_t s[8]) {
+  fe_sqn(d.t2, d.t2, 70);
+  fe_mul(d.t1, d.t2, d.t1);
+  fe_sqn(d.t1, d.t1, 50);
+  fe_mul(d.t0, d.t1, d.t0);
+  fe_sqn(d.t0, d.t0, 2);
+  fe z;
+  fe_sq(x, d.v3);
+  fe_mul(x, x, d.v);
+  fe_mul(z, x, d.u);
+  fe_mul(x, d.t0, z);  // (u v^7)^((p-5)/8)
+  fe_mul(x, x, d.v3);
+  fe_mul(x, x, d.u);   // u v^3 (u v^7)^((p-5)/8)
+  fe vxx, chk;
+  fe_sq(vxx, x);
+  fe_mul(vxx, vxx, d.v);
+  fe_sub(chk, vxx, d.u);
+  if (!fe_iszero(chk)) {
+    fe_add(chk, vxx, d.u);
+    if (!fe_iszero(chk)) return false;
+    fe_mul(x, x, fe_const_sqrtm1());
+  }
+  if (fe_isnegative(x) != (s[7] >> 31)) {
+    fe_neg(x, x);
+    fe_carry(x);
+  }
+  return true;
+}
+
+constexpr int kSmallThreads = 192;
+struct SmallShared {
+  uint32_t h[8];
+  uint32_t xr[10], yr[10];  // R decoded (wave 2)
+  uint32_t base[40];        // [S]B (wave 1): X, Y, Z, T
+  int ok_hash, ok_r;
+};
+template <int W>
+__global__ __launch_bounds__(kSmallThreads) void edv_verify_small_kernel(
+    const uint8_t* __restrict__ sig64, const uint32_t* __restrict__ key_idx, uint32_t key_count,
+    const uint8_t* __restrict__ key_pk, const uint8_t* __restrict__ key_valid, const uint8_t* __restrict__ msgs,
+    const uint64_t* __restrict__ ms, const uint64_t* __restrict__ me, uint64_t n,
+    const uint32_t* __restrict__ key_tab, uint64_t key_cap, const uint32_t* __restrict__ btab,
+    const uint32_t* __restrict__ ident, uint8_t* __restrict__ ok8) {
+  constexpr int RK = Window<W>::kRows, RB = Window<kBaseW>::kRows;
+  static_assert(RK <= 64 && RB <= 64, "one lane per row");
+  constexpr int WK = RK <= 16 ? 16 : RK <= 32 ? 32 : 64, WB = RB <= 16 ? 16 : RB <= 32 ? 32 : 64;
+  __shared__ SmallShared sh;
+  const uint64_t i = blockIdx.x;
+  if (i >= n) return;  // block-uniform
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  RDecode rd;  // wave 2, lane 0: R's decode, across the first barrier
+  const uint32_t key0 = key_idx[i];
+  const bool in_range = key0 < key_count;
+  const uint64_t key = in_range ? key0 : 0;
+  uint32_t sig[16];
+  load_words(sig, sig64 + 64 * i, 16);
+  if (wave == 0) {
+    if (lane == 0) {
+      uint32_t pk[8], h[8];
+      load_words(pk, key_pk + 32 * key, 8);
+      const bool ok = verify_phase_hash(h, sig, pk, msgs + ms[i], me[i] - ms[i]) && in_range && key_valid[key];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) sh.h[k] = h[k];
+      sh.ok_hash = ok ? 1 : 0;
+    }
+  } else if (wave == 1) {
+    uint32_t y[9];
+    comb_recode<kBaseW>(y, sig + 8);
+    ge_p3 P;
+    if (lane < RB) {
+      const DevComb<kBaseW> tb{btab, ident};
+      comb_row_point<kBaseW>(P, y, lane, tb);
+    } else {
+      ge_p3_0(P);
+    }
+    lane_tree_sum(P, lane, WB);
+    if (lane == 0) {
+      store_fe(sh.base, P.X);
+      store_fe(sh.base + 10, P.Y);
+      store_fe(sh.base + 20, P.Z);
+      store_fe(sh.base + 30, P.T);
+    }
+  } else if (lane == 0) {
+    r_decode_part1(rd, sig);
+  }
+  __syncthreads();
+  if (wave == 2) {
+    if (lane == 0) {
+      fe x;
+      const bool dec = r_decode_part2(x, rd, sig);  // false: y^2 - 1 / (d y^2 + 1) has no root
+      const bool zero_signed = (sig[7] >> 31) && fe_iszero(x);
+      store_fe(sh.xr, x);
+      store_fe(sh.yr, rd.y);
+      sh.ok_r = (dec && is_canonical_point(sig) && !zero_signed) ? 1 : 0;
+    }
+  }
+  ge_p3 P;
+  if (wave == 0) {  // [h](-A): the key comb's rows on lanes, summed as a tree
+    uint32_t h[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) h[k] = sh.h[k];
+    uint32_t y[9];
+    comb_recode<W>(y, h);
+    if (lane < RK) {
+      constexpr uint64_t kRowWordsW = (uint64_t)Window<W>::kEntries * kEntryWords;
+      const DevComb<W> ta{key_tab + key * kRowWordsW, ident, key_cap * kRowWordsW};  // row-major store
+      comb_row_point<W>(P, y, lane, ta);
+    } else {
+      ge_p3_0(P);
+    }
+    lane_tree_sum(P, lane, WK);
+  }
+  __syncthreads();  // R's decode (wave 2) done
+  if (wave != 0 || lane != 0) return;
+  ge_p3 B;
+  load_fe(B.X, sh.base);
+  load_fe(B.Y, sh.base + 10);
+  load_fe(B.Z, sh.base + 20);
+  load_fe(B.T, sh.base + 30);
+  ge_cached c;
+  ge_p1p1 t;
+  ge_p2 Q;
+  ge_p3_to_cached(c, B);
+  ge_add(t, P, c);
+  ge_p1p1_to_p2_addlike(Q, t);  // R' = [h](-A) + [S]B, classes C
+  fe xr, yr, u, d;
+  load_fe(xr, sh.xr);
+  load_fe(yr, sh.yr);
+  fe_mul(u, xr, Q.Z);
+  fe_sub(d, Q.X, u);  // X' - x_R Z'  (L)
+  bool ok = sh.ok_hash && sh.ok_r && fe_iszero(d);
+  fe_mul(u, yr, Q.Z);
+  fe_sub(d, Q.Y, u);
+  ok = ok && fe_iszero(d);
+  ok8[i] = ok ? 1 : 0;
+}
+
 // Fixed-base comb: [x]B with x < 2^253, 64 madds over BASE_COMB (global).
 __device__ void ge_scalarmult_base(ge_p3& Q, const uint32_t x[8], const uint32_t* __restrict__ comb) {
   uint32_t y[8];
@@ -1113,6 +1344,8 @@ struct edv_ctx {
   // key-sorted comb order (edv_set_key_sort): the permutation and the verdict bytes [kMaxLanes];
   // per sub-batch: block offsets [kSortBlocks][bins], bin totals / bases [bins] x 2, scan scratch
   int key_sort = 2;
+  uint64_t small_max = 256;  // edv_set_small_batch: keyed host-pointer chunks of at most this many requests take
+                             // edv_verify_small_kernel (0 = never)
   uint32_t* d_kperm = nullptr;
   uint8_t* d_ok8 = nullptr;
   uint32_t* d_kbin = nullptr;
@@ -1540,6 +1773,40 @@ int launch_pipeline(edv_ctx* ctx, bool keyed, const void* d_sig, const void* d_k
   return 0;
 }
 
+// A small keyed batch through edv_verify_small_kernel (one workgroup per request) and the
+// verdict-byte pack; its duration lands in the comb phase of edv_last_phases_ms.
+int launch_small(edv_ctx* ctx, const void* d_sig, const void* d_kidx, const void* d_msgs, const uint64_t* ms,
+                 const uint64_t* me, uint64_t n, void* d_words, hipStream_t st) {
+  if (n == 0) return 0;
+  if (ctx->key_count == 0) return set_err(EDV_EINVAL, "no registered keys");
+  hipEvent_t* ev = ctx->ev_sub[0];
+  for (int k = 0; k < 3; ++k) HIP_TRY(hipEventRecord(ev[k], st));
+  const uint32_t kc = (uint32_t)ctx->key_count;
+#define EDV_SMALL_CASE(W)                                                                                        \
+  case W:                                                                                                        \
+    hipLaunchKernelGGL(edv_verify_small_kernel<W>, dim3((uint32_t)n), dim3(kSmallThreads), 0, st,                \
+                       (const uint8_t*)d_sig, (const uint32_t*)d_kidx, kc, ctx->d_key_pk, ctx->d_key_valid,      \
+                       (const uint8_t*)d_msgs, ms, me, n, ctx->d_key_tab, ctx->key_cap, ctx->d_btab_comb32,     \
+                       ctx->d_ident, ctx->d_ok8);                                                                \
+    break;
+  switch (ctx->key_w) {
+    EDV_KEY_WINDOWS(EDV_SMALL_CASE)
+    default:
+      return set_err(EDV_EINVAL, "key window %d", ctx->key_w);
+  }
+#undef EDV_SMALL_CASE
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(ev[3], st));
+  hipLaunchKernelGGL(edv_ok_pack_kernel, dim3((uint32_t)div_up(n, kBlock)), dim3(kBlock), 0, st, ctx->d_ok8, n,
+                     (unsigned long long*)d_words);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(ev[4], st));
+  ctx->last_nsub = 1;
+  ctx->last_chunk_n = n;
+  ctx->timed = true;
+  return 0;
+}
+
 int launch_verify(edv_ctx* ctx, const void* d_sig, const void* d_pk, const void* d_msgs, const void* d_off, uint64_t n,
                   void* d_words, hipStream_t st) {
   const uint64_t* off = (const uint64_t*)d_off;
@@ -1760,6 +2027,46 @@ static int host_submit(edv_ctx* ctx, bool keyed, const uint8_t* sig, uint64_t si
           (r = ensure(ctx->d_off[sl], 8 * (cn + 1))) || (r = ensure(ctx->d_bits[sl], 8 * nwords)) ||
           (slots && (r = ensure(ctx->d_slot[sl], sig_stride * cn))))
         return r;
+      // a small chunk (a message the verify-ahead missed): its four inputs packed into one pinned
+      // block and ONE copy on the compute stream, instead of four copies on the copy stream and a
+      // cross-stream wait -- each small DMA costs microseconds of latency, not bandwidth
+      const uint64_t a16 = 16;
+      const uint64_t o_key = div_up(sig_stride * cn, a16) * a16, o_off = o_key + div_up(key_bytes * cn, a16) * a16,
+                     o_msg = o_off + div_up(8 * (cn + 1), a16) * a16, c_bytes = o_msg + mbytes;
+      if (cn <= ctx->small_max && c_bytes <= kCompactBytes) {
+        if ((r = ensure_pinned(ctx->h_msg[sl], c_bytes + 16)) || (r = ensure(ctx->d_msg[sl], c_bytes + 16))) return r;
+        char* hb = (char*)ctx->h_msg[sl].p;
+        const auto t0 = clk::now();
+        memcpy(hb, sig + sig_stride * c0, sig_stride * cn);
+        memcpy(hb + o_key, keys + key_bytes * c0, key_bytes * cn);
+        memcpy(hb + o_off, msg_off + c0, 8 * (cn + 1));
+        if (mbytes) memcpy(hb + o_msg, msgs + m0, mbytes);
+        stage_s += std::chrono::duration<double>(clk::now() - t0).count();
+        hipStream_t st = ctx->stream;
+        char* db = (char*)ctx->d_msg[sl].p;
+        HIP_TRY(hipMemcpyAsync(db, hb, c_bytes, hipMemcpyHostToDevice, st));
+        ctx->last_h2d_bytes += c_bytes;
+        void* d_sig_use = db;
+        if (slots) {
+          hipLaunchKernelGGL(edv_b58_sig_kernel, dim3((uint32_t)div_up(cn, kBlock)), dim3(kBlock), 0, st,
+                             (const uint8_t*)db, cn, (uint8_t*)ctx->d_sig[sl].p);
+          HIP_TRY(hipGetLastError());
+          d_sig_use = ctx->d_sig[sl].p;
+        }
+        const uint64_t* d_off = (const uint64_t*)(db + o_off);
+        const uint8_t* d_msg_base = (const uint8_t*)db + o_msg - m0;
+        set_bucketing(ctx, ctx->bucket_mode == 2 && lengths_mixed(msg_off + c0, cn));
+        if (keyed)
+          r = launch_small(ctx, d_sig_use, db + o_key, d_msg_base, d_off, d_off + 1, cn, ctx->d_bits[sl].p, st);
+        else
+          r = launch_pipeline(ctx, keyed, d_sig_use, db + o_key, d_msg_base, d_off, d_off + 1, cn, ctx->d_bits[sl].p,
+                              st);
+        if (r) return r;
+        HIP_TRY(hipMemcpyAsync(ctx->h_bits[sl].p, ctx->d_bits[sl].p, 8 * nwords, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipEventRecord(ctx->ev_done[sl], st));
+        ctx->slot_use[sl] = edv_ctx::SlotUse{ticket, c0, cn};
+        continue;
+      }
       const uint8_t *s_sig, *s_key, *s_msg, *s_off;
       if ((r = source(sig_direct, ctx->h_sig[sl], sig + sig_stride * c0, sig_stride * cn, true, &s_sig)) ||
           (r = source(key_direct, ctx->h_key[sl], keys + key_bytes * c0, key_bytes * cn, false, &s_key)) ||
@@ -1785,9 +2092,13 @@ static int host_submit(edv_ctx* ctx, bool keyed, const uint8_t* sig, uint64_t si
       const uint64_t* d_off = (const uint64_t*)ctx->d_off[sl].p;
       // the offsets are the caller's (starting at m0): the kernels address msgs + off[i]
       const uint8_t* d_msg_base = (const uint8_t*)ctx->d_msg[sl].p - m0;
-      if ((r = launch_pipeline(ctx, keyed, ctx->d_sig[sl].p, ctx->d_key[sl].p, d_msg_base, d_off, d_off + 1, cn,
-                               ctx->d_bits[sl].p, st)))
-        return r;
+      if (keyed && cn <= ctx->small_max)
+        r = launch_small(ctx, ctx->d_sig[sl].p, ctx->d_key[sl].p, d_msg_base, d_off, d_off + 1, cn, ctx->d_bits[sl].p,
+                         st);
+      else
+        r = launch_pipeline(ctx, keyed, ctx->d_sig[sl].p, ctx->d_key[sl].p, d_msg_base, d_off, d_off + 1, cn,
+                            ctx->d_bits[sl].p, st);
+      if (r) return r;
       HIP_TRY(hipMemcpyAsync(ctx->h_bits[sl].p, ctx->d_bits[sl].p, 8 * nwords, hipMemcpyDeviceToHost, st));
       HIP_TRY(hipEventRecord(ctx->ev_done[sl], st));
       ctx->slot_use[sl] = edv_ctx::SlotUse{ticket, c0, cn};
@@ -2353,6 +2664,14 @@ int edv_set_length_buckets(edv_ctx* ctx, int mode) {
 int edv_set_unit_arena(edv_ctx* ctx, uint64_t bytes) {
   if (!ctx) return set_err(EDV_EINVAL, "null context");
   ctx->arena_want = bytes / sizeof(Chunk16);
+  return 0;
+}
+
+int edv_set_small_batch(edv_ctx* ctx, uint64_t max_requests) {
+  if (!ctx) return set_err(EDV_EINVAL, "null context");
+  if (max_requests > 65536) return set_err(EDV_EINVAL, "small-batch limit %llu (at most 65536)",
+                                            (unsigned long long)max_requests);
+  ctx->small_max = max_requests;
   return 0;
 }
 

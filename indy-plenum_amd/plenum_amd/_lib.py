@@ -34,6 +34,7 @@ SIGNATURES = {
     "edv_set_pipeline": (_I, [_P, _I]),
     "edv_set_length_buckets": (_I, [_P, _I]),
     "edv_set_key_sort": (_I, [_P, _I]),
+    "edv_set_small_batch": (_I, [_P, _U64]),
     "edv_set_unit_arena": (_I, [_P, _U64]),
     "edv_last_phase_ms": (_I, [_P, _P, _P, _P]),
     "edv_last_kernel_ms": (_c.c_double, [_P]),

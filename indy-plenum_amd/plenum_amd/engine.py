@@ -280,6 +280,11 @@ class EdVerifyEngine:
         """Sub-batches per chunk (1..4; 1 = kernels run one at a time)."""
         check(self._lib.edv_set_pipeline(self._ctx, int(sub_batches)))
 
+    def set_small_batch(self, max_requests):
+        """Keyed host-pointer verifies of at most max_requests requests take the
+        low-latency kernel (edv_set_small_batch; default 256, 0 = never)."""
+        check(self._lib.edv_set_small_batch(self._ctx, int(max_requests)))
+
     def set_key_sort(self, mode):
         """Key-sorted comb order on the key-table path: False/0 off, True/1
         on, "auto"/2 (the default: sub-batches of 4,096 requests or more)."""

@@ -572,3 +572,55 @@ def test_sig_slots_match_sig64(gpu_engine, oracle):
         gpu_engine.keys_reset()
     idx = rng.choice(n, 500, replace=False)
     assert (_oracle_sample(oracle, sig, pk[kidx], buf, off, idx) == got[idx]).all()
+
+
+@pytest.mark.parametrize("w", [4, 6, 10, 14, 16])
+def test_small_batch_kernel_matches_batch_path(gpu_engine, oracle, w):
+    """edv_verify_small_kernel (keyed host-pointer batches of <= 256 requests:
+    rows on lanes summed as trees, R decoded instead of R' inverted) gives the
+    batch kernels' verdicts bit for bit: every golden edge item (small-order
+    and non-canonical R, A and S, R + T8, mixed-order keys) and valid item in
+    chunks of 1 / 7 / 64 / 256 requests, unregistered ids, and random
+    corrupted signatures, at every comb window shape (64 / 43 / 26 / 19 / 16
+    key rows)."""
+    e, v = load_npz("ed25519_edge.npz"), load_npz("ed25519_valid.npz")
+    try:
+        gpu_engine.keys_reset()
+        gpu_engine.keys_set_window(w)
+        for d in (e, v):
+            gpu_engine.keys_reset()
+            first = gpu_engine.keys_add(d["pk"])
+            kidx = np.arange(first, first + len(d["pk"]), dtype=np.uint32)
+            kidx[5::11] = gpu_engine.keys_count() + 1  # unregistered
+            want = d["expect"].astype(bool).copy()
+            want[5::11] = False
+            gpu_engine.set_small_batch(0)
+            big = gpu_engine.verify_batch_keyed(d["sig"], kidx, d["msgs"], d["off"])
+            assert (big == want).all(), (w, np.nonzero(big != want)[0][:8])
+            gpu_engine.set_small_batch(256)
+            for step in (1, 7, 64, 256):
+                for a in range(0, len(kidx), step):
+                    b = min(len(kidx), a + step)
+                    off = d["off"][a:b + 1]
+                    got = gpu_engine.verify_batch_keyed(d["sig"][a:b], kidx[a:b], d["msgs"], off)
+                    assert (got == want[a:b]).all(), (w, step, a, np.nonzero(got != want[a:b])[0][:8])
+                if step == 1 and len(kidx) > 300:
+                    break  # one request per call over the edge set only (hundreds of launches)
+        # random batch with corrupted S / R / M bits and shared keys
+        n = 200
+        sig, pks, msgs, buf, off = _random_batch(gpu_engine, n, 41)
+        gpu_engine.keys_reset()
+        uniq, inv = np.unique(pks, axis=0, return_inverse=True)
+        first = gpu_engine.keys_add(uniq)
+        kidx = (inv.reshape(-1) + first).astype(np.uint32)
+        gpu_engine.set_small_batch(0)
+        big = gpu_engine.verify_batch_keyed(sig, kidx, buf, off)
+        gpu_engine.set_small_batch(256)
+        small = gpu_engine.verify_batch_keyed(sig, kidx, buf, off)
+        assert (small == big).all()
+        idx = np.arange(0, n, 7)
+        assert (_oracle_sample(oracle, sig, pks, buf, off, idx) == small[idx]).all()
+    finally:
+        gpu_engine.set_small_batch(256)
+        gpu_engine.keys_reset()
+        gpu_engine.keys_set_window(10)
