@@ -78,3 +78,10 @@ for name, v in (("authenticate", lat), ("_prepare", lat_prep), ("engine call n=1
     v = np.array(v[30:]) * 1e6
     print("single %-16s p50 %.1f us  p99 %.1f us" % (name, np.percentile(v, 50), np.percentile(v, 99)))
 print("phases of the last n=1 call (ms):", eng.last_phases_ms(), eng.last_host_stats())
+# where a single authenticate()'s time goes (Python frames vs the library call)
+def _singles():
+    for r in reqs[:300]:
+        a.clear_verdicts()
+        a.authenticate(r)
+cProfile.run("_singles()", "/tmp/single.prof")
+pstats.Stats("/tmp/single.prof").sort_stats("tottime").print_stats(12)
