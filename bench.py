@@ -116,9 +116,12 @@ def host_cpus():
     return {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "cgroup_cpu_quota": quota}
 
 
-def e2e_requests(eng, n, signers, alias_len, seed=1, spec=None, sig=None, pks=None):
+def e2e_requests(eng, n, signers, alias_len, seed=1, spec=None, sig=None, pks=None, wire=True):
     """Signed NYM request dicts (the shape Node hands authenticate(),
-    plenum/common/request.py:27-39) plus the signers' (identifier, '~'verkey)."""
+    plenum/common/request.py:27-39) plus the signers' (identifier, '~'verkey).
+    wire: each request json-encoded and decoded on its own, as the node gets
+    it off the wire (ZStack -> json.loads per message), so every request owns
+    its str / int objects like in a running node."""
     from plenum_amd import _hostpack
     from plenum_amd.base58 import b58encode
     if spec is None:
@@ -128,10 +131,11 @@ def e2e_requests(eng, n, signers, alias_len, seed=1, spec=None, sig=None, pks=No
         sig = eng.sign_batch(sks, kidx, b, o)
     sig_b58 = _hostpack.b58encode_rows(np.ascontiguousarray(sig[:n]).tobytes(), 64)
     reqs = []
+    dumps, loads = json.dumps, json.loads
     for i in range(n):
         r = synth.nym_request_dict(spec, i, signers)
         r["signature"] = sig_b58[i]
-        reqs.append(r)
+        reqs.append(loads(dumps(r)) if wire else r)
     vks = ["~" + b58encode(bytes(pk[16:])) for pk in pks]
     return reqs, spec["idrs"], vks
 
@@ -221,9 +225,10 @@ def time_e2e(eng, reqs, idrs, vks):
             "single_authenticate_us": {"p50": float(np.percentile(lat, 50)), "p99": float(np.percentile(lat, 99)),
                                        "calls": int(len(lat))},
             "key_window": g.key_window, "keyed_items_share": g.stats["keyed_items"] / max(1, g.stats["batch_items"]),
-            "note": "one Python thread (a Plenum node is single-threaded asyncio); the native scan inside it runs "
-                    "its checks, base58 length check and serialization on up to 16 host threads (scan_threads=0: "
-                    "one per 2k requests) while the node thread waits, writing signature slots (base58 text, "
+            "note": "requests json-decoded one by one as the node receives them; one Python thread (a Plenum node "
+                    "is single-threaded asyncio); the native scan inside it runs "
+                    "its checks, base58 length check and serialization on the process's CPU budget (scan_threads=0: one "
+                    "per 2k requests, at most min(affinity, cgroup quota, 48); 16 on the GPU box) while the node thread waits, writing signature slots (base58 text, "
                     "decoded on the GPU) and messages into the engine's pinned host memory. Breakdown (separate "
                     "passes): host_scan = hostpack.scan_batch_u; gpu_call = edv_verify_batch_keyed_slots on its "
                     "output (H2D straight from pinned memory, stage_ms = CPU staging copies, 0 when every input "
