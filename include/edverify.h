@@ -214,6 +214,27 @@ int edv_verify_batch_keyed(edv_ctx *ctx, const uint8_t *sig64, const uint32_t *k
 int edv_verify_batch_keyed_device(edv_ctx *ctx, const void *d_sig64, const void *d_key_idx, const void *d_msgs,
                                   const void *d_msg_off, uint64_t n, void *d_accept_words, void *stream);
 
+/* Staged inputs: the caller DMAs its inputs piece by piece while it is still
+ * producing the rest (the authenticator's batch scan queues each 4k-request
+ * chunk's signature slots and messages as soon as its workers have written
+ * them, so the PCIe transfer runs under the host work instead of after it).
+ *   edv_stage_reserve(ctx, bytes): a device staging buffer of >= bytes (kept
+ *     across calls; clears the put error state).
+ *   edv_stage_put(ctx, src, nbytes, off): queue the copy of nbytes of pinned
+ *     memory (edv_host_alloc) to staging offset off; returns at once; any
+ *     thread (serialized inside); src must not change until the verify.
+ *   edv_verify_staged(ctx, keyed, keys, slot_off, msg_base, msg_start,
+ *     msg_end, n, accept_bits): n EDV_SIG_SLOT96 signature slots at staging
+ *     offset slot_off, message i at staging msg_base + [msg_start[i],
+ *     msg_end[i]) (any order, any gaps), keys as edv_verify_batch_keyed /
+ *     edv_verify_batch (host arrays): waits for every put queued before it,
+ *     then the same kernels and verdicts as the slot forms.  Fails if any put
+ *     since the last reserve failed. */
+int edv_stage_reserve(edv_ctx *ctx, uint64_t bytes);
+int edv_stage_put(edv_ctx *ctx, const void *src, uint64_t nbytes, uint64_t off);
+int edv_verify_staged(edv_ctx *ctx, int keyed, const uint8_t *keys, uint64_t slot_off, uint64_t msg_base,
+                      const uint64_t *msg_start, const uint64_t *msg_end, uint64_t n, uint8_t *accept_bits);
+
 /* Signature slots: the host-pointer verifies below take, instead of sig64,
  * n slots of EDV_SIG_SLOT96 bytes, so that the base58 decode of the request
  * signature (client_authn.py:89, b58decode) runs on the GPU:

@@ -1406,6 +1406,13 @@ struct edv_ctx {
   std::deque<BuildEv> builds;
   uint64_t build_ticket = 0, build_done = 0;
   hipEvent_t ev_fence[4] = {};  // in-flight work of the context's streams, awaited by a slot rebuild
+  // Staged inputs (edv_stage_reserve / edv_stage_put / edv_verify_staged): a device buffer the
+  // caller fills piece by piece from pinned memory while it still produces the rest; the puts
+  // queue on stream_copy (any thread, under stage_mu) and edv_verify_staged orders after them
+  Buf d_stage;
+  std::mutex stage_mu;
+  int stage_err = 0;  // first failed put since the last reserve (reported by edv_verify_staged)
+  Buf d_spans;        // message starts and ends of a staged verify [2][n]
 };
 
 namespace {
@@ -2383,6 +2390,88 @@ int edv_verify_batch_slots(edv_ctx* ctx, const uint8_t* sig_slots, const uint8_t
   return host_verify(ctx, false, sig_slots, EDV_SIG_SLOT96, pk32, msgs, msg_off, n, accept_bits);
 }
 
+int edv_stage_reserve(edv_ctx* ctx, uint64_t bytes) {
+  int r = set_device(ctx);
+  if (r) return r;
+  std::lock_guard<std::mutex> lk(ctx->stage_mu);
+  ctx->stage_err = 0;
+  if (ctx->d_stage.cap < bytes) {
+    HIP_TRY(hipStreamSynchronize(ctx->stream_copy));  // earlier puts may still write the old buffer
+    HIP_TRY(hipStreamSynchronize(ctx->stream));       // ... and earlier verifies read it
+    if ((r = ensure(ctx->d_stage, bytes))) return r;
+  }
+  return 0;
+}
+
+int edv_stage_put(edv_ctx* ctx, const void* src, uint64_t nbytes, uint64_t off) {
+  if (!ctx) return set_err(EDV_EINVAL, "null context");
+  std::lock_guard<std::mutex> lk(ctx->stage_mu);
+  if (!nbytes) return 0;
+  int r = 0;
+  if (!src || off > ctx->d_stage.cap || nbytes > ctx->d_stage.cap - off)
+    r = set_err(EDV_EINVAL, "stage_put [%llu, +%llu) outside the %llu-byte staging buffer", (unsigned long long)off,
+                (unsigned long long)nbytes, (unsigned long long)ctx->d_stage.cap);
+  else if (!pinned_range(src, nbytes))
+    r = set_err(EDV_EINVAL, "stage_put source is not edv_host_alloc memory");
+  else if (hipSetDevice(ctx->device) != hipSuccess ||
+           hipMemcpyAsync((char*)ctx->d_stage.p + off, src, nbytes, hipMemcpyHostToDevice, ctx->stream_copy) !=
+               hipSuccess)
+    r = set_err(EDV_EHIP, "stage_put copy failed");
+  if (r && !ctx->stage_err) ctx->stage_err = r;
+  return r;
+}
+
+int edv_verify_staged(edv_ctx* ctx, int keyed, const uint8_t* keys, uint64_t slot_off, uint64_t msg_base,
+                      const uint64_t* msg_start, const uint64_t* msg_end, uint64_t n, uint8_t* accept_bits) {
+  int r = set_device(ctx);
+  if (r) return r;
+  if (n && (!keys || !msg_start || !msg_end || !accept_bits)) return set_err(EDV_EINVAL, "null pointer");
+  {
+    std::lock_guard<std::mutex> lk(ctx->stage_mu);
+    if (ctx->stage_err) return set_err(ctx->stage_err, "an earlier stage_put failed");
+  }
+  if (!n) return 0;
+  if (keyed && ctx->key_count == 0) return set_err(EDV_EINVAL, "no registered keys");
+  const uint64_t cap = ctx->d_stage.cap;
+  if (slot_off > cap || n > (cap - slot_off) / EDV_SIG_SLOT96) return set_err(EDV_EINVAL, "slots outside staging");
+  for (uint64_t i = 0; i < n; ++i)  // the kernels read msg_base + [start, end): inside the staging buffer
+    if (msg_start[i] > msg_end[i] || msg_end[i] > cap - msg_base)
+      return set_err(EDV_EINVAL, "message span %llu outside staging", (unsigned long long)i);
+  const uint64_t key_bytes = keyed ? 4 : 32, nwords = div_up(n, 64);
+  if ((r = ensure_pinned(ctx->h_key[0], key_bytes * n)) || (r = ensure_pinned(ctx->h_off[0], 16 * n)) ||
+      (r = ensure(ctx->d_key[0], key_bytes * n)) || (r = ensure(ctx->d_spans, 16 * n)) ||
+      (r = ensure(ctx->b_sig, 64 * n)) || (r = ensure(ctx->d_bits[0], 8 * nwords)) ||
+      (r = ensure_pinned(ctx->h_bits[0], 8 * nwords)))
+    return r;
+  for (int sl = 0; sl < edv_ctx::kSlots; ++sl)  // submissions still holding the slot-0 buffers
+    if ((r = drain_slot(ctx, sl))) return r;
+  memcpy(ctx->h_key[0].p, keys, key_bytes * n);
+  memcpy(ctx->h_off[0].p, msg_start, 8 * n);
+  memcpy((char*)ctx->h_off[0].p + 8 * n, msg_end, 8 * n);
+  hipStream_t cs = ctx->stream_copy, st = ctx->stream;
+  HIP_TRY(hipMemcpyAsync(ctx->d_key[0].p, ctx->h_key[0].p, key_bytes * n, hipMemcpyHostToDevice, cs));
+  HIP_TRY(hipMemcpyAsync(ctx->d_spans.p, ctx->h_off[0].p, 16 * n, hipMemcpyHostToDevice, cs));
+  HIP_TRY(hipEventRecord(ctx->ev_h2d[0], cs));  // after every put queued before this call
+  HIP_TRY(hipStreamWaitEvent(st, ctx->ev_h2d[0], 0));
+  const uint8_t* stage = (const uint8_t*)ctx->d_stage.p;
+  hipLaunchKernelGGL(edv_b58_sig_kernel, dim3((uint32_t)div_up(n, kBlock)), dim3(kBlock), 0, st, stage + slot_off, n,
+                     (uint8_t*)ctx->b_sig.p);
+  HIP_TRY(hipGetLastError());
+  const uint64_t* ms = (const uint64_t*)ctx->d_spans.p;
+  set_bucketing(ctx, false);
+  if (keyed && n <= ctx->small_max)
+    r = launch_small(ctx, ctx->b_sig.p, ctx->d_key[0].p, stage + msg_base, ms, ms + n, n, ctx->d_bits[0].p, st);
+  else
+    r = launch_pipeline(ctx, keyed != 0, ctx->b_sig.p, ctx->d_key[0].p, stage + msg_base, ms, ms + n, n,
+                        ctx->d_bits[0].p, st);
+  if (r) return r;
+  HIP_TRY(hipMemcpyAsync(ctx->h_bits[0].p, ctx->d_bits[0].p, 8 * nwords, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  memcpy(accept_bits, ctx->h_bits[0].p, (size_t)((n + 7) / 8));
+  if (n & 7) accept_bits[n / 8] &= (uint8_t)((1u << (n & 7)) - 1);
+  return 0;
+}
+
 int edv_verify_submit(edv_ctx* ctx, int keyed, const uint8_t* sig, int sig_format, const uint8_t* keys,
                       const uint8_t* msgs, const uint64_t* msg_off, uint64_t n, uint64_t* ticket) {
   int r = set_device(ctx);
@@ -2564,7 +2653,8 @@ void edv_destroy(edv_ctx* ctx) {
   if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
   if (ctx->stream_key) (void)hipStreamSynchronize(ctx->stream_key);
   if (ctx->stream_build) (void)hipStreamSynchronize(ctx->stream_build);
-  for (edv_ctx::Buf* b : {&ctx->b_sig, &ctx->b_pk, &ctx->b_msg, &ctx->b_off, &ctx->b_bits, &ctx->b_aux, &ctx->b_build})
+  for (edv_ctx::Buf* b : {&ctx->b_sig, &ctx->b_pk, &ctx->b_msg, &ctx->b_off, &ctx->b_bits, &ctx->b_aux, &ctx->b_build,
+                          &ctx->d_stage, &ctx->d_spans})
     free_buf(*b);
   for (edv_ctx::BuildEv& b : ctx->builds) (void)hipEventDestroy(b.ev);
   for (hipEvent_t f : ctx->ev_fence)

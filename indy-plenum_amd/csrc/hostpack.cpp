@@ -743,17 +743,17 @@ constexpr Py_ssize_t kScanChunk = 1024;
 // shared counter by the caller and t - 1 pool helpers, so a worker whose CPU
 // is busy with other work takes fewer.
 template <class F>
-void run_chunks(Py_ssize_t n, int t, F&& f) {
-  if (t <= 1 || n <= kScanChunk) {
+void run_chunks(Py_ssize_t n, int t, F&& f, Py_ssize_t chunk = kScanChunk) {
+  if (t <= 1 || n <= chunk) {
     if (n) f(0, (Py_ssize_t)0, n);
     return;
   }
   std::atomic<Py_ssize_t> next{0};
   const std::function<void(int)> body = [&](int w) {
     for (;;) {
-      const Py_ssize_t a = next.fetch_add(kScanChunk, std::memory_order_relaxed);
+      const Py_ssize_t a = next.fetch_add(chunk, std::memory_order_relaxed);
       if (a >= n) break;
-      f(w, a, std::min(n, a + kScanChunk));
+      f(w, a, std::min(n, a + chunk));
     }
   };
   HostPool::get().run(t, body);
@@ -770,7 +770,12 @@ struct ScanScratch {
   std::vector<uint64_t> off;
   std::string fast, shortv;
   std::vector<uint32_t> uidx;
+  std::vector<uint64_t> spans;  // staged mode: message starts [n] then ends [n]
 };
+
+// Staged mode (defer = 2): edverify.h edv_stage_put, called by the workers.
+using StageFn = int (*)(void*, const void*, uint64_t, uint64_t);
+constexpr Py_ssize_t kStageChunk = 4096;  // items per staged chunk: ~0.8 MB of messages + 0.4 MB of slots per copy
 // One spare scratch kept across calls (taken by a scan, given back when it --
 // or the pack handle of a deferred scan -- is done); a scan entered while the
 // spare is out (a garbage collection's finalizer inside a scan, a second
@@ -860,12 +865,33 @@ struct PyRefs {
 };
 
 PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
-  PyObject *msgs, *ignore = Py_None, *out = Py_None;
+  PyObject *msgs, *ignore = Py_None, *out = Py_None, *stager = Py_None;
   int want_threads = 0, sig_slot = 64, defer = 0;
-  if (!PyArg_ParseTuple(args, "O|OiOii", &msgs, &ignore, &want_threads, &out, &sig_slot, &defer)) return nullptr;
+  unsigned long long slot_base = 0;
+  if (!PyArg_ParseTuple(args, "O|OiOiiOK", &msgs, &ignore, &want_threads, &out, &sig_slot, &defer, &stager,
+                        &slot_base))
+    return nullptr;
   if (defer && !unique_form) {
     PyErr_SetString(PyExc_ValueError, "defer needs scan_batch_u");
     return nullptr;
+  }
+  // staged mode: (edv_stage_put address, context address); messages at staging offset 0, slots
+  // at slot_base; both output buffers must be the engine's pinned memory
+  const bool staged = defer == 2;
+  StageFn stage_fn = nullptr;
+  void* stage_ctx = nullptr;
+  if (staged) {
+    unsigned long long fa = 0, ca = 0;
+    if (!PyTuple_Check(stager) || !PyArg_ParseTuple(stager, "KK", &fa, &ca) || !fa || !ca) {
+      if (!PyErr_Occurred()) PyErr_SetString(PyExc_ValueError, "staged scan: stager = (edv_stage_put, ctx)");
+      return nullptr;
+    }
+    stage_fn = (StageFn)(uintptr_t)fa;
+    stage_ctx = (void*)(uintptr_t)ca;
+    if (sig_slot != kSigSlot) {
+      PyErr_SetString(PyExc_ValueError, "staged scan needs signature slots");
+      return nullptr;
+    }
   }
   if (sig_slot != 64 && sig_slot != kSigSlot) {
     PyErr_Format(PyExc_ValueError, "slot must be 64 (raw signatures) or %d (base58 slots)", kSigSlot);
@@ -928,11 +954,85 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
   char* dsig = nullptr;
   PyObject* o_sig = refs.o_sig = out_buffer(out_sig, (Py_ssize_t)n * sig_slot, &dsig);
   if (!o_sig) return nullptr;
+  // staged mode: the message buffer is the caller's pinned buffer, filled by a bump cursor chunk
+  // by chunk (each chunk's bytes contiguous, chunks in completion order; item spans say where)
+  char* smsg = nullptr;
+  uint64_t smsg_cap = 0;
+  std::atomic<uint64_t> scursor{0};
+  std::atomic<bool> staged_ok{true};
+  if (staged) {
+    Py_buffer view;
+    if (!out_msg || PyObject_GetBuffer(out_msg, &view, PyBUF_WRITABLE | PyBUF_C_CONTIGUOUS) != 0) {
+      PyErr_Clear();
+      PyErr_SetString(PyExc_ValueError, "staged scan: out[1] must be a writable buffer");
+      return nullptr;
+    }
+    smsg = (char*)view.buf;
+    smsg_cap = (uint64_t)view.len;
+    PyBuffer_Release(&view);  // the caller keeps the owner alive
+    S.spans.resize(2 * (size_t)n);
+  }
   std::vector<std::vector<uint8_t>> sigs((size_t)t);
   for (int w = 0; w < t; ++w) {  // no-ops once a batch of this size has been seen
     bufs[(size_t)w].sig.reserve((size_t)(n / t + kScanChunk) * 64);
     bufs[(size_t)w].ser.reserve((size_t)(n / t + kScanChunk) * 200);
   }
+  // staged mode, at the end of each chunk [a, b) of phase (1): the chunk's messages (crypto_sign_open's
+  // sm[64:]) at the bump cursor, the slots the worker has not written (raw signatures, zeroed slots),
+  // the item spans, and the two copies queued -- so the DMA runs while the scan goes on
+  const auto stage_chunk = [&](int w, Py_ssize_t a, Py_ssize_t b) {
+    const ScanBuf& sb = bufs[(size_t)w];
+    uint64_t total = 0;
+    for (Py_ssize_t i = a; i < b; ++i) {
+      const ScanItem& x = it[(size_t)i];
+      if (x.state != 1) continue;
+      const uint64_t ls = x.sig_len, lm = x.ser_len;
+      total += x.text ? lm : (ls + lm >= 64 ? ls + lm - 64 : 0);
+    }
+    const uint64_t pos = scursor.fetch_add(total, std::memory_order_relaxed);
+    if (pos + total > smsg_cap) {
+      staged_ok = false;  // the buffer was sized from earlier batches: the caller re-scans unstaged
+      return;
+    }
+    uint64_t at = pos;
+    uint64_t* st0 = S.spans.data();
+    uint64_t* en0 = st0 + n;
+    for (Py_ssize_t i = a; i < b; ++i) {
+      const ScanItem& x = it[(size_t)i];
+      char* ds = dsig + (size_t)i * sig_slot;
+      st0[i] = en0[i] = at;
+      if (x.state == 1 && x.text) {  // the slot was written in the item loop
+        memcpy(smsg + at, sb.ser.data() + x.ser_at, x.ser_len);
+        at += x.ser_len;
+        en0[i] = at;
+        continue;
+      }
+      memset(ds + 64, 0, (size_t)sig_slot - 64);  // slot[95] = 0: raw R || S in bytes 0..63
+      const uint64_t ls = x.sig_len, lm = x.ser_len;
+      if (x.state != 1 || ls + lm < 64) {
+        memset(ds, 0, 64);
+        continue;
+      }
+      const char* sr = sb.ser.data() + x.ser_at;
+      const char* sg = sb.sig.data() + x.sig_at;
+      char* dm = smsg + at;
+      if (ls >= 64) {  // sm[64:] = sig[64:] || ser
+        memcpy(ds, sg, 64);
+        memcpy(dm, sg + 64, ls - 64);
+        memcpy(dm + (ls - 64), sr, lm);
+      } else {
+        memcpy(ds, sg, ls);
+        memcpy(ds + ls, sr, 64 - ls);
+        memcpy(dm, sr + (64 - ls), lm - (64 - ls));
+      }
+      at += ls + lm - 64;
+      en0[i] = at;
+    }
+    if (stage_fn(stage_ctx, smsg + pos, total, pos) != 0 ||
+        stage_fn(stage_ctx, dsig + (size_t)a * sig_slot, (uint64_t)(b - a) * sig_slot,
+                 slot_base + (uint64_t)a * sig_slot) != 0)
+      staged_ok = false;
+  };
   run_chunks(n, t, [&](int w, Py_ssize_t a, Py_ssize_t b) {
     ScanBuf& sb = bufs[(size_t)w];
     WorkerIdrs& tab = tabs[(size_t)w];
@@ -1006,7 +1106,8 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
         tab.first.push_back(i);
       }
     }
-  });
+    if (staged) stage_chunk(w, a, b);
+  }, staged ? kStageChunk : kScanChunk);
   auto t_p1 = now();
   // (2) the workers' identifier tables merged into the batch's, in order of
   // first occurrence in the batch (the single-thread order, whichever worker
@@ -1044,7 +1145,8 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
   // (3) the items the workers left (non-ASCII identifiers, floats / big ints /
   // wide-kind keys in the payload), redone under the GIL; none in the steady
   // state, which then skips this pass over the batch
-  if (deferred) {
+  if (deferred && staged) staged_ok = false;  // rare items redone under the GIL: the caller re-scans unstaged
+  if (deferred && !staged) {
     ScanBuf& sb = bufs[(size_t)t];
     std::vector<uint8_t> sig;
     for (Py_ssize_t i = 0; i < n; ++i) {
@@ -1132,6 +1234,25 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
   // scan leaves this to pack_range, stretch by stretch, so the caller can queue each stretch's
   // DMA while the next one packs)
   char* dmsg = nullptr;
+  if (staged) {  // the messages are in place; the spans say where
+    Py_INCREF(out_msg);
+    refs.o_msg = out_msg;
+    PyObject* ul = PyList_New((Py_ssize_t)uniq.size());
+    if (!ul) return nullptr;
+    for (size_t u = 0; u < uniq.size(); ++u) {
+      Py_INCREF(uniq[u]);
+      PyList_SET_ITEM(ul, (Py_ssize_t)u, uniq[u]);
+    }
+    if (prof) {
+      auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+      fprintf(stderr, "scan (staged): n=%zd threads=%d  workers %.0f us, merge %.0f us, bookkeeping %.0f us\n", n, t,
+              us(t_start, t_p1), us(t_p1, t_p2), us(t_p3, now()));
+    }
+    return Py_BuildValue("(y#y#NOOy#y#O)", fast.data(), (Py_ssize_t)n, (const char*)uidx.data(),
+                         (Py_ssize_t)(uidx.size() * 4), ul, o_sig, out_msg, (const char*)S.spans.data(),
+                         (Py_ssize_t)(S.spans.size() * 8), shortv.data(), (Py_ssize_t)n,
+                         staged_ok.load() ? Py_True : Py_False);
+  }
   PyObject* o_msg = refs.o_msg = out_buffer(out_msg, (Py_ssize_t)off[(size_t)n], &dmsg);
   PyObject* ret = nullptr;
   if (o_msg) {
@@ -1285,6 +1406,36 @@ PyObject* py_pack_range(PyObject*, PyObject* args) {
   Py_RETURN_NONE;
 }
 
+// repack_spans(buf, spans) -> (msgs, off): a staged scan's messages (item i at buf[start[i]:end[i]],
+// spans = starts[n] then ends[n], uint64) laid out contiguously with offsets, for the ordinary path.
+PyObject* py_repack_spans(PyObject*, PyObject* args) {
+  Py_buffer bb, bs;
+  if (!PyArg_ParseTuple(args, "y*y*", &bb, &bs)) return nullptr;
+  PyObject* ret = nullptr;
+  const Py_ssize_t n = bs.len / 16;
+  const uint64_t* st = (const uint64_t*)bs.buf;
+  const uint64_t* en = st + n;
+  std::vector<uint64_t> off((size_t)n + 1, 0);
+  bool ok = bs.len % 16 == 0;
+  for (Py_ssize_t i = 0; i < n && ok; ++i) {
+    ok = st[i] <= en[i] && en[i] <= (uint64_t)bb.len;
+    off[(size_t)i + 1] = off[(size_t)i] + (ok ? en[i] - st[i] : 0);
+  }
+  if (!ok) {
+    PyErr_SetString(PyExc_ValueError, "repack_spans: span outside the buffer");
+  } else {
+    PyObject* m = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)off[(size_t)n]);
+    if (m) {
+      char* d = PyBytes_AS_STRING(m);
+      for (Py_ssize_t i = 0; i < n; ++i) memcpy(d + off[(size_t)i], (const char*)bb.buf + st[i], en[i] - st[i]);
+      ret = Py_BuildValue("(Ny#)", m, (const char*)off.data(), (Py_ssize_t)(off.size() * 8));
+    }
+  }
+  PyBuffer_Release(&bb);
+  PyBuffer_Release(&bs);
+  return ret;
+}
+
 // results_from(codes, uidx, uniq) -> list: item i is uniq[uidx[i]] where
 // codes[i] == 1 (verified: authenticate() returns the identifier), None
 // elsewhere (the caller fills those in).
@@ -1367,6 +1518,8 @@ PyMethodDef kMethods[] = {
     {"pack_range", py_pack_range, METH_VARARGS,
      "pack_range(handle, lo, hi): write items [lo, hi) of a deferred scan_batch_u (defer=1 returns the handle as "
      "an 8th element) into its output buffers"},
+    {"repack_spans", py_repack_spans, METH_VARARGS,
+     "repack_spans(buf, spans) -> (msgs, off): a staged scan's messages laid out contiguously with offsets"},
     {"results_from", py_results_from, METH_VARARGS,
      "results_from(codes_u8, uidx_u32, uniq) -> list: uniq[uidx[i]] where codes[i] == 1, else None"},
     {"gather_items", py_gather_items, METH_VARARGS,

@@ -64,9 +64,9 @@ try:  # native batch scan (csrc/hostpack.cpp): authenticate()'s host steps for a
 except ImportError:  # pragma: no cover - the per-message path below
     _scan_batch = _gather_items = _results_from = None
 try:
-    from ._hostpack import pack_range as _pack_range
+    from ._hostpack import pack_range as _pack_range, repack_spans as _repack_spans
 except ImportError:  # pragma: no cover
-    _pack_range = None
+    _pack_range = _repack_spans = None
 
 try:  # native packing (csrc/hostpack.cpp)
     from ._hostpack import pack_sm as _pack_sm, pack_split64 as _pack_split64
@@ -109,6 +109,7 @@ KEY_STORE_BYTES = 32 << 30  # HBM for key tables: the window is the widest that 
 _SIG_SLOT = 96  # edverify.h EDV_SIG_SLOT96: signatures as base58 text, decoded on the GPU
 _PINNED_MIN_BATCH = 4096  # smaller batches keep the bytearrays (the library stages them cheaply)
 _STREAM_CHUNK = 1 << 18   # edverify.hip kHostChunk: the library's copy / kernel chunk
+_STAGE_MIN_BATCH = 1 << 16  # batches staged while scanned (edv_stage_put from the scan's workers)
 
 
 _MISSING = object()
@@ -147,7 +148,7 @@ class _GpuState:
 
     def __init__(self, engine=None, device=0, devices=None, verdict_cache_size=1 << 20, key_window="auto",
                  max_keys=16384, hot_key_uses=2, key_store_bytes=KEY_STORE_BYTES, scan_threads=0,
-                 pipeline_part=0, async_key_builds=True, stream=True):
+                 pipeline_part=0, async_key_builds=True, stream=True, stage=True):
         self.engine = engine
         self.device = device
         self.devices = devices
@@ -183,6 +184,8 @@ class _GpuState:
         # batches of 2 library chunks (2^19 requests) or more pack chunk by chunk, each chunk's DMA and
         # kernels overlapping the next chunk's pack (_authenticate_streamed)
         self.stream = stream
+        # batches of 2^16 requests or more are staged while scanned (_authenticate_staged)
+        self.stage = stage
         self.stats = {"batches": 0, "batch_items": 0, "cache_hits": 0, "single_verifies": 0, "keyed_items": 0,
                       "keys_registered": 0}
 
@@ -528,10 +531,65 @@ class GpuAuthMixin:
             part = self._g.pipeline_part
             if part and len(msgs) >= 2 * part and hasattr(eng, "verify_submit") and bufs is not self._g.scan_out:
                 return self._authenticate_pipelined(msgs, eng, slot, bufs, part)
+            if (self._g.stage and _repack_spans is not None and len(msgs) >= _STAGE_MIN_BATCH
+                    and getattr(eng, "supports_staging", False) and slot == _SIG_SLOT and bufs is not self._g.scan_out):
+                res = self._authenticate_staged(msgs, eng, slot, bufs)
+                if res is not None:
+                    return res
+                bufs = self._scan_buffers(eng, len(msgs), slot)  # regrown from the new size estimate
             if (self._g.stream and _pack_range is not None and len(msgs) >= 2 * _STREAM_CHUNK
                     and hasattr(eng, "verify_submit") and bufs is not self._g.scan_out):
                 return self._authenticate_streamed(msgs, eng, slot, bufs)
             return self._authenticate_batch_scanned_into(msgs, bufs, slot)
+
+    def _authenticate_staged(self, msgs, eng, slot, bufs):
+        """A large batch whose PCIe copy runs under its scan: the native scan's
+        workers place each 4k-request chunk's messages at a bump cursor in the
+        engine's pinned memory and queue that chunk's messages and signature
+        slots to the device (edv_stage_put) as soon as they are written, so
+        by the time the scan returns most of the batch is already in HBM;
+        edv_verify_staged then waits for the rest and runs the kernels over
+        the item spans.  In the node's steady state (every item scanned,
+        every identifier resolved to a built key); a batch with other items
+        repacks its messages contiguously and takes the ordinary path (same
+        verdicts).  None when the scan could not stage (the pinned buffer
+        was too small for this batch, or items needed the interpreter): the
+        caller scans again the ordinary way."""
+        import numpy as np
+        g = self._g
+        n = len(msgs)
+        msg_cap = len(bufs[1])
+        slot_base = (msg_cap + 255) // 256 * 256
+        eng.stage_reserve(slot_base + n * slot)
+        scan = _scan_batch(msgs, [SIG], g.scan_threads, bufs, slot, 2, eng.stager(), slot_base)
+        fast_b, uidx_b, uniq, sig_o, msg_o, spans_b, short, staged_ok = scan
+        spans = np.frombuffer(spans_b, np.uint64)
+        ms, me = spans[:n], spans[n:]
+        if not staged_ok:
+            g.msg_bytes_per_item *= 1.5  # the next buffers are sized larger
+            return None
+        g.msg_bytes_per_item = max(g.msg_bytes_per_item * 0.5, float((me - ms).sum()) / n)
+        ukeys = [self._key_for(idr) for idr in uniq]  # authenticate():93-99, once per identifier
+        ids = None
+        ks = self._key_store()
+        if ks is not None and fast_b.count(0) == 0 and all(k.__class__ is bytes for k in ukeys):
+            self._register_waiting(ks, list(dict.fromkeys(ukeys)))
+            ids = ks.lookup(ukeys)
+            if any(i is None for i in ids):
+                ids = None
+        if ids is None:  # not the steady state: contiguous messages, the ordinary path
+            msg_c, off_c = _repack_spans(msg_o, spans_b)
+            return self._finish_scanned(msgs, (fast_b, uidx_b, uniq, sig_o, msg_c, off_c, short), slot, ukeys)
+        kid = np.asarray(ids, np.uint32)[np.frombuffer(uidx_b, np.uint32)]
+        ok = np.asarray(eng.verify_staged(True, kid, slot_base, 0, ms, me), bool)
+        ok &= np.frombuffer(short, np.uint8) == 0
+        g.stats["batches"] += 1
+        g.stats["batch_items"] += n
+        g.stats["keyed_items"] += n
+        results = _results_from(ok.view(np.uint8).tobytes(), uidx_b, uniq)
+        for i in np.flatnonzero(~ok).tolist():
+            results[i] = InvalidSignature()
+        return results
 
     def _authenticate_streamed(self, msgs, eng, slot, bufs):
         """A large batch whose pack overlaps its DMA: one scan of the whole

@@ -213,6 +213,32 @@ class EdVerifyEngine:
         check(self._lib.edv_verify_collect(self._ctx, ticket, _ptr(bits) if n else ctypes.c_void_p(1)))
         return unpack_bits(bits, n)
 
+    # ------------------------------------------------------- staged inputs
+    supports_staging = True
+
+    def stage_reserve(self, nbytes):
+        """A device staging buffer of >= nbytes (edv_stage_reserve)."""
+        check(self._lib.edv_stage_reserve(self._ctx, int(nbytes)))
+
+    def stager(self):
+        """(edv_stage_put address, context address): what the native scan
+        calls from its workers to queue each chunk's copies."""
+        return (ctypes.cast(self._lib.edv_stage_put, ctypes.c_void_p).value, self._ctx.value)
+
+    def verify_staged(self, keyed, keys, slot_off, msg_base, msg_start, msg_end):
+        """Verdicts of n staged requests (edv_verify_staged): slots at staging
+        offset slot_off, message i at msg_base + [msg_start[i], msg_end[i])."""
+        keys = np.ascontiguousarray(keys, dtype=np.uint32) if keyed else _u8(keys, 32)
+        ms = np.ascontiguousarray(msg_start, dtype=np.uint64)
+        me = np.ascontiguousarray(msg_end, dtype=np.uint64)
+        n = ms.shape[0]
+        if keys.shape[0] != n or me.shape[0] != n:
+            raise ValueError("shape mismatch: keys %d, starts %d, ends %d" % (keys.shape[0], n, me.shape[0]))
+        bits = np.zeros((n + 7) // 8, dtype=np.uint8)
+        check(self._lib.edv_verify_staged(self._ctx, 1 if keyed else 0, _ptr(keys), int(slot_off), int(msg_base),
+                                          _ptr(ms), _ptr(me), n, _ptr(bits) if n else ctypes.c_void_p(1)))
+        return unpack_bits(bits, n)
+
     def host_alloc(self, nbytes):
         """nbytes of pinned host memory (edv_host_alloc) as a writable ctypes
         array; host-pointer verifies copy inputs inside it to the device with no

@@ -233,3 +233,37 @@ class AsyncOracleEngine(OracleEngine):
         busy = [int(k) for k in key_idx if int(k) in self.building]
         assert not busy, "keyed verify of ids still building: %s" % sorted(set(busy))[:8]
         return super().verify_batch_keyed(sig64, key_idx, msgs, msg_off, sig_slot)
+
+
+class StagingOracleEngine(OracleEngine):
+    """OracleEngine with edv_stage_reserve / edv_stage_put / edv_verify_staged:
+    the staging buffer is host memory and the put a memcpy done by
+    oracle/_build/libstage_double.so, which the native scan calls from its
+    worker threads exactly as it calls the library's edv_stage_put."""
+    supports_staging = True
+
+    def __init__(self, lib=None):
+        super().__init__(lib)
+        self._put = ctypes.CDLL(os.path.join(ROOT, "oracle", "_build", "libstage_double.so")).stage_double_put
+        self.stage = (ctypes.c_ubyte * 0)()
+        self.staged_calls = 0
+
+    def stage_reserve(self, nbytes):
+        if len(self.stage) < nbytes:
+            self.stage = (ctypes.c_ubyte * int(nbytes))()
+
+    def stager(self):
+        return (ctypes.cast(self._put, ctypes.c_void_p).value, ctypes.addressof(self.stage))
+
+    def verify_staged(self, keyed, keys, slot_off, msg_base, msg_start, msg_end):
+        self.staged_calls += 1
+        st = np.frombuffer(self.stage, np.uint8)
+        n = len(msg_start)
+        slots = st[slot_off:slot_off + 96 * n].reshape(-1, 96)
+        parts = [st[msg_base + int(a):msg_base + int(b)].tobytes() for a, b in zip(msg_start, msg_end)]
+        off = np.zeros(n + 1, np.uint64)
+        off[1:] = np.cumsum([len(p) for p in parts])
+        buf = np.frombuffer(b"".join(parts), np.uint8)
+        if keyed:
+            return self.verify_batch_keyed(slots, keys, buf, off, sig_slot=96)
+        return self.verify_batch(slots, keys, buf, off, sig_slot=96)

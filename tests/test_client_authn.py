@@ -624,3 +624,43 @@ def test_streamed_batch_equals_whole(oracle, monkeypatch):
     del odd[4000]["signature"]
     got = [_outcome(r) for r in a.authenticate_batch(odd)]
     assert got == [_outcome(r) for r in ref.authenticate_batch(odd)]
+
+
+def test_staged_batch_equals_whole(oracle, monkeypatch):
+    """authenticate_batch's staged path (the scan's workers place each chunk's
+    messages at a bump cursor and queue its messages and slots to the device
+    with edv_stage_put -- here the CPU stand-in, called from the same worker
+    threads -- then edv_verify_staged over the item spans): the same outcome
+    per message as the unstaged path in the steady state, when the batch
+    leaves it (messages repacked from the spans), and when the pinned message
+    buffer is too small (the batch is scanned again the ordinary way)."""
+    from engine_double import StagingOracleEngine
+    from plenum_amd import client_authn as CA
+    idrs, vks, msgs = _signed(3, 5000)
+    monkeypatch.setattr(CA, "_STAGE_MIN_BATCH", 1000)
+    monkeypatch.setattr(CA, "_PINNED_MIN_BATCH", 1000)
+    eng = StagingOracleEngine(oracle)
+    a = GpuAuthNr(engine=eng)
+    ref = GpuAuthNr(engine=OracleEngine(oracle), max_keys=0)
+    for i, v in zip(idrs, vks):
+        a.addIdr(i, v)
+        ref.addIdr(i, v)
+    a.keys_settle()
+    batch = [dict(m) for m in msgs]
+    batch[17]["reqId"] += 1                       # forged
+    batch[99]["signature"] = batch[99]["signature"][:-2]   # decodes to < 64 bytes: raw slot, split at 64
+    assert [_outcome(r) for r in a.authenticate_batch(batch)] == [_outcome(r) for r in ref.authenticate_batch(batch)]
+    assert eng.staged_calls == 1 and a.stats["keyed_items"] == 5000
+    odd = [dict(m) for m in msgs]
+    odd[3]["identifier"] = "UnknownIdentifier1111"
+    del odd[4000]["signature"]
+    assert [_outcome(r) for r in a.authenticate_batch(odd)] == [_outcome(r) for r in ref.authenticate_batch(odd)]
+    assert eng.staged_calls == 1  # left the steady state: repacked, ordinary path
+    small = GpuAuthNr(engine=StagingOracleEngine(oracle))
+    for i, v in zip(idrs, vks):
+        small.addIdr(i, v)
+    small.keys_settle()
+    small._g.msg_bytes_per_item = 10.0           # pinned message buffer far too small for this batch
+    assert [_outcome(r) for r in small.authenticate_batch(batch)] == \
+        [_outcome(r) for r in ref.authenticate_batch(batch)]
+    assert small.engine.staged_calls == 0

@@ -368,3 +368,37 @@ def test_bench_e2e_devices_leg_on_gpu(gpu_engine):
     reqs, idrs, vks = bench.e2e_requests(gpu_engine, 8192, 16, 43)
     out = bench.time_e2e_devices(gpu_engine, reqs, idrs, vks, [1])
     assert out["1"]["accepted"] == 8192 and out["1"]["keyed_items_share"] == 1.0, out
+
+
+@pytest.mark.gpu
+def test_staged_batch_on_gpu(gpu_engine):
+    """The staged path on the device (edv_stage_put from the scan's workers,
+    edv_verify_staged over the item spans): 70,000 requests (above the 2^16
+    staging threshold), every 10th forged, 63- and 65-byte signatures, R with
+    leading zero bytes -- every verdict is the construction's, over two
+    batches on one authenticator (reused pinned and staging buffers)."""
+    import copy
+    from plenum_amd.base58 import b58decode, b58encode
+    n = 70000
+    reqs, rx, idrs, vks, pks, sers, sig = _drain(gpu_engine, n_req=n, n_nodes=1)
+    a = GpuAuthNr(engine=gpu_engine)
+    for idr, vk in zip(idrs, vks):
+        a.addIdr(idr, vk)
+    a.keys_settle()
+    bad = {i for i in range(n) if i % 10 == 3}
+    batch = [copy.deepcopy(r) for r in reqs]
+    for i in range(5, n, 4999):
+        batch[i]["signature"] = b58encode(b58decode(batch[i]["signature"])[:63])
+        bad.add(i)
+    for i in range(6, n, 7001):
+        batch[i]["signature"] = b58encode(b58decode(batch[i]["signature"]) + b"\x07")
+        bad.add(i)
+    before = a.stats["keyed_items"]
+    for rep in range(2):
+        res = a.authenticate_batch(batch)
+        for i, r in enumerate(res):
+            if i in bad:
+                assert type(r).__name__ == "InvalidSignature", (rep, i)
+            else:
+                assert r == batch[i]["identifier"], (rep, i)
+    assert a.stats["keyed_items"] - before == 2 * n

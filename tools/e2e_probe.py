@@ -32,19 +32,21 @@ for idr, vk in zip(idrs, vks):
 a.keys_settle()
 a.authenticate_batch(reqs[:2048])
 a.authenticate_batch(reqs)  # buffers grown
-runs = [(p, True) for p in parts] + ([(0, False)] if 0 in parts else [])
-for part, stream in runs:
+runs = [(p, True, True) for p in parts] + ([(0, True, False), (0, False, False)] if 0 in parts else [])
+for part, stream, stage in runs:
     a._g.pipeline_part = part
     a._g.stream = stream
+    a._g.stage = stage
     for rep in range(3):
         t0 = time.perf_counter()
         res = a.authenticate_batch(reqs)
         el = time.perf_counter() - t0
-        print("authenticate_batch part=%d stream=%d: %.3f s = %.2f M requests/s, ok %d" % (
-            part, stream, el, n / el / 1e6, sum(1 for r in res[:1000] if isinstance(r, str))), flush=True)
+        print("authenticate_batch part=%d stream=%d stage=%d: %.3f s = %.2f M requests/s, ok %d" % (
+            part, stream, stage, el, n / el / 1e6, sum(1 for r in res[:1000] if isinstance(r, str))), flush=True)
         del res
 a._g.pipeline_part = parts[-1]
 a._g.stream = True
+a._g.stage = True
 cProfile.run("a.authenticate_batch(reqs)", "/tmp/e2e.prof")
 pstats.Stats("/tmp/e2e.prof").sort_stats("tottime").print_stats(15)
 eng.close()
