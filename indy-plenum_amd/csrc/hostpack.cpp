@@ -36,6 +36,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <charconv>
 #include <chrono>
@@ -775,7 +776,70 @@ struct ScanScratch {
 
 // Staged mode (defer = 2): edverify.h edv_stage_put, called by the workers.
 using StageFn = int (*)(void*, const void*, uint64_t, uint64_t);
-constexpr Py_ssize_t kStageChunk = 4096;  // items per staged chunk: ~0.8 MB of messages + 0.4 MB of slots per copy
+constexpr Py_ssize_t kStageChunk = 4096;  // items per staged chunk: ~0.8 MB of messages, 0.4 MB of slots
+
+// The copies of a staged scan, issued by one thread of their own so no worker ever waits on the
+// runtime: workers publish each finished chunk (its message reservation, by reservation order,
+// and its slot range, by chunk index); the copier advances over the contiguous done prefix of
+// each and queues one edv_stage_put per >= kCopyGrain bytes (and the remainder at the end).
+constexpr uint64_t kCopyGrain = 4ull << 20;
+constexpr int kSeqShift = 44;  // message cursor: reservation number << 44 | byte position
+struct StageCopier {
+  StageFn fn = nullptr;
+  void* ctx = nullptr;
+  const char* smsg = nullptr;
+  const char* dsig = nullptr;
+  uint64_t slot_base = 0, slot_bytes_per_chunk = 0, slot_bytes_total = 0;
+  size_t nchunks = 0;
+  std::unique_ptr<std::atomic<uint64_t>[]> res_end;  // by reservation number: end byte + 1 once written (0 = not yet)
+  std::unique_ptr<std::atomic<uint8_t>[]> slot_done;  // by chunk index
+  std::atomic<bool> finished{false};
+  std::atomic<bool> failed{false};
+  std::thread th;
+  uint64_t msg_sent = 0, msg_ready = 0;
+  size_t next_res = 0, next_chunk = 0, slot_sent_chunk = 0;
+
+  void put(const char* src, uint64_t nbytes, uint64_t off) {
+    if (nbytes && fn(ctx, src, nbytes, off) != 0) failed = true;
+  }
+  // one pass over what became ready; `flush` sends every ready byte
+  void pump(bool flush) {
+    while (next_res < nchunks) {
+      const uint64_t e = res_end[next_res].load(std::memory_order_acquire);
+      if (!e) break;
+      msg_ready = e - 1;
+      ++next_res;
+    }
+    if (msg_ready > msg_sent && (flush || msg_ready - msg_sent >= kCopyGrain)) {
+      put(smsg + msg_sent, msg_ready - msg_sent, msg_sent);
+      msg_sent = msg_ready;
+    }
+    while (next_chunk < nchunks && slot_done[next_chunk].load(std::memory_order_acquire)) ++next_chunk;
+    const uint64_t s0 = slot_sent_chunk * slot_bytes_per_chunk;
+    const uint64_t s1 = std::min<uint64_t>(next_chunk * slot_bytes_per_chunk, slot_bytes_total);
+    if (s1 > s0 && (flush || s1 - s0 >= kCopyGrain)) {
+      put(dsig + s0, s1 - s0, slot_base + s0);
+      slot_sent_chunk = next_chunk;
+    }
+  }
+  void start() {
+    th = std::thread([this] {
+      while (!finished.load(std::memory_order_acquire)) {
+        pump(false);
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+      }
+    });
+  }
+  void finish() {  // after every worker is done: join, then send the rest
+    finished = true;
+    if (th.joinable()) th.join();
+    pump(true);
+  }
+  ~StageCopier() {
+    finished = true;
+    if (th.joinable()) th.join();
+  }
+};
 // One spare scratch kept across calls (taken by a scan, given back when it --
 // or the pack handle of a deferred scan -- is done); a scan entered while the
 // spare is out (a garbage collection's finalizer inside a scan, a second
@@ -960,6 +1024,7 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
   uint64_t smsg_cap = 0;
   std::atomic<uint64_t> scursor{0};
   std::atomic<bool> staged_ok{true};
+  StageCopier copier;
   if (staged) {
     Py_buffer view;
     if (!out_msg || PyObject_GetBuffer(out_msg, &view, PyBUF_WRITABLE | PyBUF_C_CONTIGUOUS) != 0) {
@@ -989,9 +1054,13 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
       const uint64_t ls = x.sig_len, lm = x.ser_len;
       total += x.text ? lm : (ls + lm >= 64 ? ls + lm - 64 : 0);
     }
-    const uint64_t pos = scursor.fetch_add(total, std::memory_order_relaxed);
+    const uint64_t got = scursor.fetch_add(total + (1ull << kSeqShift), std::memory_order_relaxed);
+    const size_t seq = (size_t)(got >> kSeqShift);
+    const uint64_t pos = got & ((1ull << kSeqShift) - 1);
     if (pos + total > smsg_cap) {
       staged_ok = false;  // the buffer was sized from earlier batches: the caller re-scans unstaged
+      copier.res_end[seq].store(pos + 1, std::memory_order_release);  // (nothing of it is copied)
+      copier.slot_done[(size_t)(a / kStageChunk)].store(1, std::memory_order_release);
       return;
     }
     uint64_t at = pos;
@@ -1028,11 +1097,26 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
       at += ls + lm - 64;
       en0[i] = at;
     }
-    if (stage_fn(stage_ctx, smsg + pos, total, pos) != 0 ||
-        stage_fn(stage_ctx, dsig + (size_t)a * sig_slot, (uint64_t)(b - a) * sig_slot,
-                 slot_base + (uint64_t)a * sig_slot) != 0)
-      staged_ok = false;
+    copier.res_end[seq].store(pos + total + 1, std::memory_order_release);
+    copier.slot_done[(size_t)(a / kStageChunk)].store(1, std::memory_order_release);
   };
+  if (staged) {
+    copier.fn = stage_fn;
+    copier.ctx = stage_ctx;
+    copier.smsg = smsg;
+    copier.dsig = dsig;
+    copier.slot_base = slot_base;
+    copier.slot_bytes_per_chunk = (uint64_t)kStageChunk * sig_slot;
+    copier.slot_bytes_total = (uint64_t)n * sig_slot;
+    copier.nchunks = (size_t)((n + kStageChunk - 1) / kStageChunk);
+    copier.res_end.reset(new std::atomic<uint64_t>[copier.nchunks]);
+    copier.slot_done.reset(new std::atomic<uint8_t>[copier.nchunks]);
+    for (size_t c = 0; c < copier.nchunks; ++c) {
+      copier.res_end[c].store(0, std::memory_order_relaxed);
+      copier.slot_done[c].store(0, std::memory_order_relaxed);
+    }
+    copier.start();
+  }
   run_chunks(n, t, [&](int w, Py_ssize_t a, Py_ssize_t b) {
     ScanBuf& sb = bufs[(size_t)w];
     WorkerIdrs& tab = tabs[(size_t)w];
@@ -1108,6 +1192,10 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
     }
     if (staged) stage_chunk(w, a, b);
   }, staged ? kStageChunk : kScanChunk);
+  if (staged) {
+    copier.finish();
+    if (copier.failed) staged_ok = false;
+  }
   auto t_p1 = now();
   // (2) the workers' identifier tables merged into the batch's, in order of
   // first occurrence in the batch (the single-thread order, whichever worker

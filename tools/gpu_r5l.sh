@@ -3,7 +3,7 @@
 # the e2e probe (staged / streamed / plain), the bench's e2e legs.
 set -o pipefail
 export TMPDIR=/tmp
-OUT=gpurun_out/r5k
+OUT=gpurun_out/r5l
 mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests/test_gpu_authn.py -x -v --timeout 300 --timeout-method thread -m gpu > $OUT/pytest_gpu.log 2>&1 || { tail -c 4000 $OUT/pytest_gpu.log; exit 1; }
 tail -n 1 $OUT/pytest_gpu.log
