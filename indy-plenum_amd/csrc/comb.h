@@ -202,6 +202,7 @@ EDV_HD uint32_t comb_mul_add(ge_p3& Q, const uint32_t x[8], const T& tab) {
 // 2y, Z = 2, T = XY / Z = 2xy = 2dxy / d -- one multiplication instead of 7.
 // -entry = (y-x, y+x, -2dxy) gives (-2x, 2y, 2, -2xy); the identity entry
 // (1, 1, 0) gives (0, 2, 2, 0).  Output classes: X, Y, Z, T all C.
+template <int ORDER = EDV_FE_MUL_ORDER>
 EDV_HD void comb_set_entry(ge_p3& Q, const ge_niels& nb, int e) {
   const bool neg = e < 0;
   fe p, m, t;
@@ -217,7 +218,7 @@ EDV_HD void comb_set_entry(ge_p3& Q, const ge_niels& nb, int e) {
   fe_carry(Q.Y);
   fe_0(Q.Z);
   Q.Z.v[0] = 2;
-  fe_mul(Q.T, t, fe_const_dinv());
+  fe_mul_o<ORDER>(Q.T, t, fe_const_dinv());
 }
 template <class T>
 EDV_HD void comb_set(ge_p3& Q, int e, const T& tab) {

@@ -903,6 +903,13 @@ __device__ __forceinline__ void shfl_fe(fe& out, const fe& in, int delta) {
 // Sum of the p3 points of lanes 0..width-1 of this wave (width a power of two
 // <= 64; lanes >= rows hold the identity) into lane 0: log2(width) levels of
 // p + q (q as cached).
+#ifndef EDV_SMALL_ORDER
+// fe_mul_o order of the small kernel's products.  One wave's serial carry-started chains
+// (2) beat ten independent accumulators (1) here too: R's decode 99.6 vs 118.2 us, the kernel
+// 103.8 vs 123.4 us (tools/small_probe.py, profiles/r05m).
+#define EDV_SMALL_ORDER 2
+#endif
+constexpr int kSO = EDV_SMALL_ORDER;
 __device__ void lane_tree_sum(ge_p3& P, int lane, int width) {
 #pragma unroll 1
   for (int step = 1; step < width; step <<= 1) {
@@ -914,9 +921,9 @@ __device__ void lane_tree_sum(ge_p3& P, int lane, int width) {
     if ((lane & (2 * step - 1)) == 0 && lane < width) {
       ge_cached c;
       ge_p1p1 t;
-      ge_p3_to_cached(c, Q);
-      ge_add(t, P, c);
-      ge_p1p1_to_p3_addlike(P, t);
+      ge_p3_to_cached<kSO>(c, Q);
+      ge_add<kSO>(t, P, c);
+      ge_p1p1_to_p3_addlike<kSO>(P, t);
     }
   }
 }
@@ -926,7 +933,7 @@ __device__ void comb_row_point(ge_p3& P, const uint32_t y[9], int row, const T& 
   const int e = comb_digit<W>(y, row);
   ge_niels nb;
   tab.load(row, (e < 0 ? -e : e) - 1, nb);
-  comb_set_entry(P, nb, e);
+  comb_set_entry<kSO>(P, nb, e);
 }
 
 // libsodium's frombytes of R (ge_frombytes, negate = false) cut in two at a
@@ -940,56 +947,56 @@ __device__ void r_decode_part1(RDecode& d, const uint32_t s[8]) {
   fe one, x, z;
   fe_1(one);
   fe_frombytes(d.y, s);
-  fe_sq(d.u, d.y);
-  fe_mul(d.v, d.u, fe_const_d());
+  fe_sq_o<kSO>(d.u, d.y);
+  fe_mul_o<kSO>(d.v, d.u, fe_const_d());
   fe_sub(d.u, d.u, one);
   fe_carry(d.u);
   fe_add(d.v, d.v, one);
-  fe_sq(d.v3, d.v);
-  fe_mul(d.v3, d.v3, d.v);
-  fe_sq(x, d.v3);
-  fe_mul(x, x, d.v);
-  fe_mul(z, x, d.u);  // u v^7: fe_pow22523's input, its chain up to t1 = z^(2^100 - 1) then 30 squarings
-  fe_sq(d.t0, z);
-  fe_sqn(d.t1, d.t0, 2);
-  fe_mul(d.t1, z, d.t1);
-  fe_mul(d.t0, d.t0, d.t1);
-  fe_sq(d.t0, d.t0);
-  fe_mul(d.t0, d.t1, d.t0);
-  fe_sqn(d.t1, d.t0, 5);
-  fe_mul(d.t0, d.t1, d.t0);
-  fe_sqn(d.t1, d.t0, 10);
-  fe_mul(d.t1, d.t1, d.t0);
-  fe_sqn(d.t2, d.t1, 20);
-  fe_mul(d.t1, d.t2, d.t1);
-  fe_sqn(d.t1, d.t1, 10);
-  fe_mul(d.t0, d.t1, d.t0);
-  fe_sqn(d.t1, d.t0, 50);
-  fe_mul(d.t1, d.t1, d.t0);
-  fe_sqn(d.t2, d.t1, 30);
+  fe_sq_o<kSO>(d.v3, d.v);
+  fe_mul_o<kSO>(d.v3, d.v3, d.v);
+  fe_sq_o<kSO>(x, d.v3);
+  fe_mul_o<kSO>(x, x, d.v);
+  fe_mul_o<kSO>(z, x, d.u);  // u v^7: fe_pow22523's input, its chain up to t1 = z^(2^100 - 1) then 30 squarings
+  fe_sq_o<kSO>(d.t0, z);
+  fe_sqn<kSO>(d.t1, d.t0, 2);
+  fe_mul_o<kSO>(d.t1, z, d.t1);
+  fe_mul_o<kSO>(d.t0, d.t0, d.t1);
+  fe_sq_o<kSO>(d.t0, d.t0);
+  fe_mul_o<kSO>(d.t0, d.t1, d.t0);
+  fe_sqn<kSO>(d.t1, d.t0, 5);
+  fe_mul_o<kSO>(d.t0, d.t1, d.t0);
+  fe_sqn<kSO>(d.t1, d.t0, 10);
+  fe_mul_o<kSO>(d.t1, d.t1, d.t0);
+  fe_sqn<kSO>(d.t2, d.t1, 20);
+  fe_mul_o<kSO>(d.t1, d.t2, d.t1);
+  fe_sqn<kSO>(d.t1, d.t1, 10);
+  fe_mul_o<kSO>(d.t0, d.t1, d.t0);
+  fe_sqn<kSO>(d.t1, d.t0, 50);
+  fe_mul_o<kSO>(d.t1, d.t1, d.t0);
+  fe_sqn<kSO>(d.t2, d.t1, 30);
 }
 // The rest: x of R with R's sign (false: no square root).  Same value as ge_frombytes.
 __device__ bool r_decode_part2(fe& x, RDecode& d, const uint32_t s[8]) {
-  fe_sqn(d.t2, d.t2, 70);
-  fe_mul(d.t1, d.t2, d.t1);
-  fe_sqn(d.t1, d.t1, 50);
-  fe_mul(d.t0, d.t1, d.t0);
-  fe_sqn(d.t0, d.t0, 2);
+  fe_sqn<kSO>(d.t2, d.t2, 70);
+  fe_mul_o<kSO>(d.t1, d.t2, d.t1);
+  fe_sqn<kSO>(d.t1, d.t1, 50);
+  fe_mul_o<kSO>(d.t0, d.t1, d.t0);
+  fe_sqn<kSO>(d.t0, d.t0, 2);
   fe z;
-  fe_sq(x, d.v3);
-  fe_mul(x, x, d.v);
-  fe_mul(z, x, d.u);
-  fe_mul(x, d.t0, z);  // (u v^7)^((p-5)/8)
-  fe_mul(x, x, d.v3);
-  fe_mul(x, x, d.u);   // u v^3 (u v^7)^((p-5)/8)
+  fe_sq_o<kSO>(x, d.v3);
+  fe_mul_o<kSO>(x, x, d.v);
+  fe_mul_o<kSO>(z, x, d.u);
+  fe_mul_o<kSO>(x, d.t0, z);  // (u v^7)^((p-5)/8)
+  fe_mul_o<kSO>(x, x, d.v3);
+  fe_mul_o<kSO>(x, x, d.u);   // u v^3 (u v^7)^((p-5)/8)
   fe vxx, chk;
-  fe_sq(vxx, x);
-  fe_mul(vxx, vxx, d.v);
+  fe_sq_o<kSO>(vxx, x);
+  fe_mul_o<kSO>(vxx, vxx, d.v);
   fe_sub(chk, vxx, d.u);
   if (!fe_iszero(chk)) {
     fe_add(chk, vxx, d.u);
     if (!fe_iszero(chk)) return false;
-    fe_mul(x, x, fe_const_sqrtm1());
+    fe_mul_o<kSO>(x, x, fe_const_sqrtm1());
   }
   if (fe_isnegative(x) != (s[7] >> 31)) {
     fe_neg(x, x);
@@ -999,6 +1006,22 @@ __device__ bool r_decode_part2(fe& x, RDecode& d, const uint32_t s[8]) {
 }
 
 constexpr int kSmallThreads = 192;
+// EDV_SMALL_PROFILE=1 (probe builds only, tools/small_probe.py): the wall clock (100 MHz) at the
+// phase boundaries of request 0, read back with edv_small_profile.
+#ifndef EDV_SMALL_PROFILE
+#define EDV_SMALL_PROFILE 0
+#endif
+#if EDV_SMALL_PROFILE
+__device__ unsigned long long g_small_prof[8];
+#define EDV_SP(k)                                                   \
+  do {                                                              \
+    if (blockIdx.x == 0 && lane == 0) g_small_prof[k] = wall_clock64(); \
+  } while (0)
+#else
+#define EDV_SP(k) \
+  do {            \
+  } while (0)
+#endif
 struct SmallShared {
   uint32_t h[8];
   uint32_t xr[10], yr[10];  // R decoded (wave 2)
@@ -1024,6 +1047,7 @@ __global__ __launch_bounds__(kSmallThreads) void edv_verify_small_kernel(
   const bool in_range = key0 < key_count;
   const uint64_t key = in_range ? key0 : 0;
   uint32_t sig[16];
+  if (wave == 0) EDV_SP(0);
   load_words(sig, sig64 + 64 * i, 16);
   if (wave == 0) {
     if (lane == 0) {
@@ -1034,6 +1058,7 @@ __global__ __launch_bounds__(kSmallThreads) void edv_verify_small_kernel(
       for (int k = 0; k < 8; ++k) sh.h[k] = h[k];
       sh.ok_hash = ok ? 1 : 0;
     }
+    EDV_SP(1);
   } else if (wave == 1) {
     uint32_t y[9];
     comb_recode<kBaseW>(y, sig + 8);
@@ -1051,8 +1076,10 @@ __global__ __launch_bounds__(kSmallThreads) void edv_verify_small_kernel(
       store_fe(sh.base + 20, P.Z);
       store_fe(sh.base + 30, P.T);
     }
+    EDV_SP(2);
   } else if (lane == 0) {
     r_decode_part1(rd, sig);
+    EDV_SP(3);
   }
   __syncthreads();
   if (wave == 2) {
@@ -1063,10 +1090,12 @@ __global__ __launch_bounds__(kSmallThreads) void edv_verify_small_kernel(
       store_fe(sh.xr, x);
       store_fe(sh.yr, rd.y);
       sh.ok_r = (dec && is_canonical_point(sig) && !zero_signed) ? 1 : 0;
+      EDV_SP(5);
     }
   }
   ge_p3 P;
   if (wave == 0) {  // [h](-A): the key comb's rows on lanes, summed as a tree
+    EDV_SP(4);
     uint32_t h[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) h[k] = sh.h[k];
@@ -1080,6 +1109,7 @@ __global__ __launch_bounds__(kSmallThreads) void edv_verify_small_kernel(
       ge_p3_0(P);
     }
     lane_tree_sum(P, lane, WK);
+    EDV_SP(6);
   }
   __syncthreads();  // R's decode (wave 2) done
   if (wave != 0 || lane != 0) return;
@@ -1091,19 +1121,20 @@ __global__ __launch_bounds__(kSmallThreads) void edv_verify_small_kernel(
   ge_cached c;
   ge_p1p1 t;
   ge_p2 Q;
-  ge_p3_to_cached(c, B);
-  ge_add(t, P, c);
-  ge_p1p1_to_p2_addlike(Q, t);  // R' = [h](-A) + [S]B, classes C
+  ge_p3_to_cached<kSO>(c, B);
+  ge_add<kSO>(t, P, c);
+  ge_p1p1_to_p2_addlike<kSO>(Q, t);  // R' = [h](-A) + [S]B, classes C
   fe xr, yr, u, d;
   load_fe(xr, sh.xr);
   load_fe(yr, sh.yr);
-  fe_mul(u, xr, Q.Z);
+  fe_mul_o<kSO>(u, xr, Q.Z);
   fe_sub(d, Q.X, u);  // X' - x_R Z'  (L)
   bool ok = sh.ok_hash && sh.ok_r && fe_iszero(d);
-  fe_mul(u, yr, Q.Z);
+  fe_mul_o<kSO>(u, yr, Q.Z);
   fe_sub(d, Q.Y, u);
   ok = ok && fe_iszero(d);
   ok8[i] = ok ? 1 : 0;
+  EDV_SP(7);
 }
 
 // Fixed-base comb: [x]B with x < 2^253, 64 madds over BASE_COMB (global).
@@ -1353,6 +1384,7 @@ struct edv_ctx {
   void* d_kscan_tmp = nullptr;
   size_t kscan_tmp_bytes = 0;  // per sub-batch
   bool timed = false;
+  bool small_timed = false;  // the last timed launch was launch_small: ev_sub[0][0] -> [3] only
   // key-table store (registered public keys)
   uint32_t* d_btab_comb32 = nullptr;  // base-point comb table (kBaseW; 11 GiB at W = 24)
   uint32_t* d_ident = nullptr;        // identity niels entry (comb accessors' j = -1)
@@ -1382,6 +1414,7 @@ struct edv_ctx {
   struct SlotUse {
     uint64_t ticket = 0;  // 0 = free
     uint64_t c0 = 0, cn = 0;
+    bool bytes = false;  // h_bits holds one verdict byte per request (the small kernel's output)
   } slot_use[kSlots];
   struct Pending {
     uint64_t ticket = 0, n = 0;
@@ -1777,24 +1810,29 @@ int launch_pipeline(edv_ctx* ctx, bool keyed, const void* d_sig, const void* d_k
   HIP_TRY(hipEventRecord(ctx->ev_join[1], ctx->stream2));
   HIP_TRY(hipStreamWaitEvent(st, ctx->ev_join[1], 0));
   ctx->timed = true;
+  ctx->small_timed = false;
   return 0;
 }
 
 // A small keyed batch through edv_verify_small_kernel (one workgroup per request) and the
 // verdict-byte pack; its duration lands in the comb phase of edv_last_phases_ms.
+// host_ok8 (pinned host memory, n bytes): the kernel stores the verdict bytes there itself and
+// no pack kernel or D2H copy follows (d_words unused) -- two fewer GPU commands on the latency
+// path of one authenticate().
 int launch_small(edv_ctx* ctx, const void* d_sig, const void* d_kidx, const void* d_msgs, const uint64_t* ms,
-                 const uint64_t* me, uint64_t n, void* d_words, hipStream_t st) {
+                 const uint64_t* me, uint64_t n, void* d_words, hipStream_t st, uint8_t* host_ok8 = nullptr) {
   if (n == 0) return 0;
   if (ctx->key_count == 0) return set_err(EDV_EINVAL, "no registered keys");
   hipEvent_t* ev = ctx->ev_sub[0];
-  for (int k = 0; k < 3; ++k) HIP_TRY(hipEventRecord(ev[k], st));
+  HIP_TRY(hipEventRecord(ev[0], st));
+  uint8_t* ok8 = host_ok8 ? host_ok8 : ctx->d_ok8;
   const uint32_t kc = (uint32_t)ctx->key_count;
 #define EDV_SMALL_CASE(W)                                                                                        \
   case W:                                                                                                        \
     hipLaunchKernelGGL(edv_verify_small_kernel<W>, dim3((uint32_t)n), dim3(kSmallThreads), 0, st,                \
                        (const uint8_t*)d_sig, (const uint32_t*)d_kidx, kc, ctx->d_key_pk, ctx->d_key_valid,      \
                        (const uint8_t*)d_msgs, ms, me, n, ctx->d_key_tab, ctx->key_cap, ctx->d_btab_comb32,     \
-                       ctx->d_ident, ctx->d_ok8);                                                                \
+                       ctx->d_ident, ok8);                                                                       \
     break;
   switch (ctx->key_w) {
     EDV_KEY_WINDOWS(EDV_SMALL_CASE)
@@ -1804,13 +1842,15 @@ int launch_small(edv_ctx* ctx, const void* d_sig, const void* d_kidx, const void
 #undef EDV_SMALL_CASE
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(ev[3], st));
-  hipLaunchKernelGGL(edv_ok_pack_kernel, dim3((uint32_t)div_up(n, kBlock)), dim3(kBlock), 0, st, ctx->d_ok8, n,
-                     (unsigned long long*)d_words);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(ev[4], st));
+  if (!host_ok8) {
+    hipLaunchKernelGGL(edv_ok_pack_kernel, dim3((uint32_t)div_up(n, kBlock)), dim3(kBlock), 0, st, ctx->d_ok8, n,
+                       (unsigned long long*)d_words);
+    HIP_TRY(hipGetLastError());
+  }
   ctx->last_nsub = 1;
   ctx->last_chunk_n = n;
   ctx->timed = true;
+  ctx->small_timed = true;
   return 0;
 }
 
@@ -1976,7 +2016,14 @@ static int drain_slot(edv_ctx* ctx, int sl) {
   HIP_TRY(hipEventSynchronize(ctx->ev_done[sl]));
   for (edv_ctx::Pending& p : ctx->pending)
     if (p.ticket == u.ticket) {
-      memcpy(p.bits.data() + u.c0 / 8, ctx->h_bits[sl].p, (u.cn + 7) / 8);
+      if (u.bytes) {  // c0 is a multiple of 64 (kHostChunk)
+        const uint8_t* b = (const uint8_t*)ctx->h_bits[sl].p;
+        uint8_t* o = p.bits.data() + u.c0 / 8;
+        for (uint64_t k = 0; k < u.cn; ++k)
+          if (b[k]) o[k >> 3] |= (uint8_t)(1u << (k & 7));
+      } else {
+        memcpy(p.bits.data() + u.c0 / 8, ctx->h_bits[sl].p, (u.cn + 7) / 8);
+      }
       break;
     }
   u.ticket = 0;
@@ -2063,15 +2110,19 @@ static int host_submit(edv_ctx* ctx, bool keyed, const uint8_t* sig, uint64_t si
         const uint64_t* d_off = (const uint64_t*)(db + o_off);
         const uint8_t* d_msg_base = (const uint8_t*)db + o_msg - m0;
         set_bucketing(ctx, ctx->bucket_mode == 2 && lengths_mixed(msg_off + c0, cn));
-        if (keyed)
-          r = launch_small(ctx, d_sig_use, db + o_key, d_msg_base, d_off, d_off + 1, cn, ctx->d_bits[sl].p, st);
-        else
+        if (keyed) {  // verdict bytes straight into the slot's pinned host buffer
+          if ((r = ensure_pinned(ctx->h_bits[sl], cn))) return r;
+          r = launch_small(ctx, d_sig_use, db + o_key, d_msg_base, d_off, d_off + 1, cn, nullptr, st,
+                           (uint8_t*)ctx->h_bits[sl].p);
+        } else {
           r = launch_pipeline(ctx, keyed, d_sig_use, db + o_key, d_msg_base, d_off, d_off + 1, cn, ctx->d_bits[sl].p,
                               st);
+        }
         if (r) return r;
-        HIP_TRY(hipMemcpyAsync(ctx->h_bits[sl].p, ctx->d_bits[sl].p, 8 * nwords, hipMemcpyDeviceToHost, st));
+        if (!keyed)
+          HIP_TRY(hipMemcpyAsync(ctx->h_bits[sl].p, ctx->d_bits[sl].p, 8 * nwords, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipEventRecord(ctx->ev_done[sl], st));
-        ctx->slot_use[sl] = edv_ctx::SlotUse{ticket, c0, cn};
+        ctx->slot_use[sl] = edv_ctx::SlotUse{ticket, c0, cn, keyed};
         continue;
       }
       const uint8_t *s_sig, *s_key, *s_msg, *s_off;
@@ -2729,6 +2780,13 @@ int edv_last_phases_ms(edv_ctx* ctx, double* out4) {
   if (!ctx || !ctx->timed) return set_err(EDV_EINVAL, "no timed verify launch yet");
   if (!out4) return set_err(EDV_EINVAL, "null output");
   for (int k = 0; k < edv_ctx::kEv - 1; ++k) out4[k] = 0.0;
+  if (ctx->small_timed) {  // launch_small: the one kernel is the comb phase
+    float t = 0.f;
+    HIP_TRY(hipEventSynchronize(ctx->ev_sub[0][3]));
+    HIP_TRY(hipEventElapsedTime(&t, ctx->ev_sub[0][0], ctx->ev_sub[0][3]));
+    out4[2] = t;
+    return 0;
+  }
   for (int sb = 0; sb < ctx->last_nsub; ++sb) {
     HIP_TRY(hipEventSynchronize(ctx->ev_sub[sb][edv_ctx::kEv - 1]));
     for (int k = 0; k < edv_ctx::kEv - 1; ++k) {
@@ -2757,6 +2815,12 @@ int edv_set_unit_arena(edv_ctx* ctx, uint64_t bytes) {
   return 0;
 }
 
+#if EDV_SMALL_PROFILE
+int edv_small_profile(uint64_t* out8) {  // probe builds only (not in include/edverify.h)
+  HIP_TRY(hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_small_prof), 8 * sizeof(uint64_t)));
+  return 0;
+}
+#endif
 int edv_set_small_batch(edv_ctx* ctx, uint64_t max_requests) {
   if (!ctx) return set_err(EDV_EINVAL, "null context");
   if (max_requests > 65536) return set_err(EDV_EINVAL, "small-batch limit %llu (at most 65536)",

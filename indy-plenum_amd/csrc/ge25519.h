@@ -68,11 +68,14 @@ EDV_HD void ge_p3_to_p2(ge_p2& r, const ge_p3& p) {
   r.Z = p.Z;
 }
 // p3 (all C) -> cached (YplusX L, YminusX L, Z C, T2d C).
+// ORDER picks fe_mul_o's product order (fe25519.h): the default for throughput, 1 (ten
+// independent accumulators) where one lane's latency is what counts (the small-batch kernel).
+template <int ORDER = EDV_FE_MUL_ORDER>
 EDV_HD void ge_p3_to_cached(ge_cached& r, const ge_p3& p) {
   fe_add(r.YplusX, p.Y, p.X);
   fe_sub(r.YminusX, p.Y, p.X);
   r.Z = p.Z;
-  fe_mul(r.T2d, p.T, fe_const_d2());
+  fe_mul_o<ORDER>(r.T2d, p.T, fe_const_d2());
 }
 
 // r = 2p.  p in C.  Output: X W, Y L, Z L, T C.
@@ -99,14 +102,15 @@ EDV_HD void ge_p3_dbl(ge_p1p1& r, const ge_p3& p) {
 }
 
 // r = p + q.  p in C, q cached.  Output: X L, Y L, Z L, T W.
+template <int ORDER = EDV_FE_MUL_ORDER>
 EDV_HD void ge_add(ge_p1p1& r, const ge_p3& p, const ge_cached& q) {
   fe s, a, b, c, d;
   fe_add(s, p.Y, p.X);
-  fe_mul(a, s, q.YplusX);
+  fe_mul_o<ORDER>(a, s, q.YplusX);
   fe_sub(s, p.Y, p.X);
-  fe_mul(b, s, q.YminusX);
-  fe_mul(c, p.T, q.T2d);
-  fe_mul(d, p.Z, q.Z);
+  fe_mul_o<ORDER>(b, s, q.YminusX);
+  fe_mul_o<ORDER>(c, p.T, q.T2d);
+  fe_mul_o<ORDER>(d, p.Z, q.Z);
   fe_add(d, d, d);            // L
   fe_sub(r.X, a, b);          // L
   fe_add(r.Y, a, b);          // L
@@ -224,11 +228,12 @@ EDV_HD void ge_add_signed(ge_p3& r, const ge_p3& p, const ge_cached& q, bool neg
 // in W, ge_sub/msub leave Z in W; ge_p2_dbl leaves X in W and T carried.
 // T3 = Y * X (not X * Y): the four products then need 2 * Y / 2 * T odd limbs
 // and 19 * X / 19 * Z premultiplies only (fe_mul's f2 / g19), not three each.
+template <int ORDER = EDV_FE_MUL_ORDER>
 EDV_HD void ge_p1p1_to_p3_addlike(ge_p3& r, const ge_p1p1& p) {  // T is W
-  fe_mul(r.X, p.T, p.X);
-  fe_mul(r.Y, p.Y, p.Z);
-  fe_mul(r.Z, p.T, p.Z);
-  fe_mul(r.T, p.Y, p.X);
+  fe_mul_o<ORDER>(r.X, p.T, p.X);
+  fe_mul_o<ORDER>(r.Y, p.Y, p.Z);
+  fe_mul_o<ORDER>(r.Z, p.T, p.Z);
+  fe_mul_o<ORDER>(r.T, p.Y, p.X);
 }
 EDV_HD void ge_p1p1_to_p3_sublike(ge_p3& r, const ge_p1p1& p) {  // Z is W
   fe_mul(r.X, p.X, p.T);
@@ -236,10 +241,11 @@ EDV_HD void ge_p1p1_to_p3_sublike(ge_p3& r, const ge_p1p1& p) {  // Z is W
   fe_mul(r.Z, p.Z, p.T);
   fe_mul(r.T, p.X, p.Y);
 }
+template <int ORDER = EDV_FE_MUL_ORDER>
 EDV_HD void ge_p1p1_to_p2_addlike(ge_p2& r, const ge_p1p1& p) {
-  fe_mul(r.X, p.T, p.X);
-  fe_mul(r.Y, p.Y, p.Z);
-  fe_mul(r.Z, p.T, p.Z);
+  fe_mul_o<ORDER>(r.X, p.T, p.X);
+  fe_mul_o<ORDER>(r.Y, p.Y, p.Z);
+  fe_mul_o<ORDER>(r.Z, p.T, p.Z);
 }
 EDV_HD void ge_p1p1_to_p2_sublike(ge_p2& r, const ge_p1p1& p) {
   fe_mul(r.X, p.X, p.T);

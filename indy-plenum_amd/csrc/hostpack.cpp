@@ -25,6 +25,7 @@
 
 #include "host_pool.h"
 #include <pthread.h>
+#include <emmintrin.h>
 #include <sched.h>
 #include <unistd.h>
 
@@ -50,9 +51,50 @@ namespace {
 
 // ------------------------------------------------------------------ serialize
 
-bool ser_obj(PyObject* o, int level, PyObject* ignore, std::string& out);
+// The scan's serialization buffers: std::string's append is an out-of-line call per piece
+// (a request's signing bytes are ~25 pieces); this one inlines to a bounds check + memcpy.
+struct OutBuf {
+  char* d = nullptr;
+  size_t n = 0, cap = 0;
+  OutBuf() = default;
+  OutBuf(const OutBuf&) = delete;
+  OutBuf& operator=(const OutBuf&) = delete;
+  OutBuf(OutBuf&& o) noexcept : d(o.d), n(o.n), cap(o.cap) { o.d = nullptr, o.n = o.cap = 0; }
+  ~OutBuf() { free(d); }
+  size_t size() const { return n; }
+  const char* data() const { return d; }
+  void clear() { n = 0; }
+  void reserve(size_t k) {
+    if (k > cap) grow_to(k);
+  }
+  void resize(size_t k) {  // (shrinks only, in its callers)
+    reserve(k);
+    n = k;
+  }
+  void grow_to(size_t k) {
+    const size_t c = std::max(k, cap * 2 + 256);
+    char* q = (char*)realloc(d, c);
+    if (!q) throw std::bad_alloc();
+    d = q;
+    cap = c;
+  }
+  void append(const char* src, size_t k) {
+    if (n + k > cap) grow_to(n + k);
+    memcpy(d + n, src, k);
+    n += k;
+  }
+  void append(const char* z) { append(z, strlen(z)); }
+  void push_back(char c) {
+    if (n + 1 > cap) grow_to(n + 1);
+    d[n++] = c;
+  }
+};
 
-bool append_str(PyObject* s, std::string& out) {
+template <class Out>
+bool ser_obj(PyObject* o, int level, PyObject* ignore, Out& out);
+
+template <class Out>
+bool append_str(PyObject* s, Out& out) {
   if (PyUnicode_IS_ASCII(s)) {
     out.append((const char*)PyUnicode_1BYTE_DATA(s), (size_t)PyUnicode_GET_LENGTH(s));
     return true;
@@ -67,7 +109,8 @@ bool append_str(PyObject* s, std::string& out) {
   return true;
 }
 
-bool append_text_of(PyObject* o, std::string& out) {  // str(o)
+template <class Out>
+bool append_text_of(PyObject* o, Out& out) {  // str(o)
   PyObject* s = PyObject_Str(o);
   if (!s) {
     PyErr_Clear();
@@ -101,7 +144,8 @@ bool str_less(PyObject* a, PyObject* b, bool& err) {
   return c < 0;
 }
 
-bool ser_dict(PyObject* d, int level, PyObject* ignore, std::string& out) {
+template <class Out>
+bool ser_dict(PyObject* d, int level, PyObject* ignore, Out& out) {
   // keys on the stack for ordinary dicts (insertion sort), a vector beyond
   constexpr Py_ssize_t kSmall = 24;
   PyObject* small[kSmall];
@@ -149,7 +193,8 @@ bool ser_dict(PyObject* d, int level, PyObject* ignore, std::string& out) {
 
 constexpr int kMaxDepth = 500;  // deeper: the Python path (which may hit RecursionError like the reference)
 
-bool ser_obj(PyObject* o, int level, PyObject* ignore, std::string& out) {
+template <class Out>
+bool ser_obj(PyObject* o, int level, PyObject* ignore, Out& out) {
   if (level > kMaxDepth) return false;
   if (PyUnicode_CheckExact(o)) return append_str(o, out);
   if (PyDict_CheckExact(o)) return ser_dict(o, level, ignore, out);
@@ -210,7 +255,7 @@ PyObject* py_serialize_for_signing(PyObject*, PyObject* args) {
 // kOk bytes equal ser_obj's; kFail exactly where ser_obj returns false.
 enum WRes { kOk = 0, kFail = 1, kDefer = 2 };
 
-WRes wser_obj(PyObject* o, int level, PyObject* ignore, std::string& out);
+WRes wser_obj(PyObject* o, int level, PyObject* ignore, OutBuf& out);
 
 bool w_str_eq(PyObject* a, PyObject* b) {  // canonical kinds: equal strings have equal kinds
   const Py_ssize_t n = PyUnicode_GET_LENGTH(a);
@@ -229,17 +274,23 @@ bool w_ignored(PyObject* k, PyObject* ignore) {
 
 bool w_less(PyObject* a, PyObject* b) {  // both one-byte kind (checked by the caller)
   const Py_ssize_t na = PyUnicode_GET_LENGTH(a), nb = PyUnicode_GET_LENGTH(b);
-  const int c = memcmp(PyUnicode_1BYTE_DATA(a), PyUnicode_1BYTE_DATA(b), (size_t)(na < nb ? na : nb));
+  const unsigned char *pa = PyUnicode_1BYTE_DATA(a), *pb = PyUnicode_1BYTE_DATA(b);
+  if (na && nb && pa[0] != pb[0]) return pa[0] < pb[0];  // most keys differ in their first byte
+  const int c = memcmp(pa, pb, (size_t)(na < nb ? na : nb));
   return c < 0 || (c == 0 && na < nb);
 }
 
-WRes w_append_str(PyObject* s, std::string& out) {
+WRes w_append_str(PyObject* s, OutBuf& out) {
   if (!PyUnicode_IS_ASCII(s)) return kDefer;  // UTF-8 encoding may allocate
   out.append((const char*)PyUnicode_1BYTE_DATA(s), (size_t)PyUnicode_GET_LENGTH(s));
   return kOk;
 }
 
-WRes wser_dict(PyObject* d, int level, PyObject* ignore, std::string& out) {
+// top != nullptr (a request's top level): also hands back the values of the keys top[0]
+// (signature) and top[1] (identifier) in found[0..1], from the same pass over the dict; both
+// null when the dict has a non-str key (the item then takes the Python path).
+WRes wser_dict(PyObject* d, int level, PyObject* ignore, OutBuf& out, PyObject* const* top = nullptr,
+               PyObject** found = nullptr) {
   constexpr Py_ssize_t kSmall = 24;
   struct KV {
     PyObject *k, *v;
@@ -256,13 +307,34 @@ WRes wser_dict(PyObject* d, int level, PyObject* ignore, std::string& out) {
   PyObject *k, *v;
   bool one_byte = true;
   while (PyDict_Next(d, &pos, &k, &v)) {
-    if (!PyUnicode_CheckExact(k)) return kFail;  // as ser_dict
+    if (!PyUnicode_CheckExact(k)) {
+      if (top) found[0] = found[1] = nullptr;
+      return kFail;  // as ser_dict
+    }
+    if (top) {
+      if (k == top[0] || w_str_eq(k, top[0]))
+        found[0] = v;
+      else if (k == top[1] || w_str_eq(k, top[1]))
+        found[1] = v;
+    }
     if (level == 0 && w_ignored(k, ignore)) continue;
     one_byte = one_byte && PyUnicode_KIND(k) == PyUnicode_1BYTE_KIND;
     kv[nk++] = KV{k, v};
   }
   if (!one_byte) return kDefer;  // PyUnicode_Compare order for wider kinds: ser_dict
-  std::sort(kv, kv + nk, [](const KV& a, const KV& b) { return w_less(a.k, b.k); });
+  if (nk <= kSmall) {  // insertion sort: a request's dicts have a handful of keys
+    for (Py_ssize_t i = 1; i < nk; ++i) {
+      const KV x = kv[i];
+      Py_ssize_t j = i;
+      while (j > 0 && w_less(x.k, kv[j - 1].k)) {
+        kv[j] = kv[j - 1];
+        --j;
+      }
+      kv[j] = x;
+    }
+  } else {
+    std::sort(kv, kv + nk, [](const KV& a, const KV& b) { return w_less(a.k, b.k); });
+  }
   for (Py_ssize_t i = 0; i < nk; ++i) {
     if (i) out.push_back('|');
     WRes r = w_append_str(kv[i].k, out);
@@ -274,7 +346,30 @@ WRes wser_dict(PyObject* d, int level, PyObject* ignore, std::string& out) {
   return kOk;
 }
 
-WRes wser_obj(PyObject* o, int level, PyObject* ignore, std::string& out) {
+// An exact int's value when it has at most two 30-bit digits (CPython's long layout up to
+// 3.11), without the out-of-line PyLong_AsLongLongAndOverflow call; false: use the API.
+inline bool w_small_long(PyObject* o, long long& x) {
+#if PY_VERSION_HEX < 0x030C0000 && PYLONG_BITS_IN_DIGIT == 30
+  const Py_ssize_t sz = Py_SIZE(o);
+  const digit* dg = ((PyLongObject*)o)->ob_digit;
+  if (sz == 0) {
+    x = 0;
+    return true;
+  }
+  const Py_ssize_t a = sz < 0 ? -sz : sz;
+  if (a > 2) return false;
+  long long v = (long long)dg[0];
+  if (a == 2) v |= (long long)dg[1] << 30;
+  x = sz < 0 ? -v : v;
+  return true;
+#else
+  (void)o;
+  (void)x;
+  return false;
+#endif
+}
+
+WRes wser_obj(PyObject* o, int level, PyObject* ignore, OutBuf& out) {
   if (level > kMaxDepth) return kFail;
   if (PyUnicode_CheckExact(o)) return w_append_str(o, out);
   if (PyDict_CheckExact(o)) return wser_dict(o, level, ignore, out);
@@ -293,9 +388,12 @@ WRes wser_obj(PyObject* o, int level, PyObject* ignore, std::string& out) {
     return kOk;
   }
   if (PyLong_CheckExact(o)) {
-    int overflow = 0;
-    const long long x = PyLong_AsLongLongAndOverflow(o, &overflow);  // an exact int never errors
-    if (overflow) return kDefer;
+    long long x;
+    if (!w_small_long(o, x)) {
+      int overflow = 0;
+      x = PyLong_AsLongLongAndOverflow(o, &overflow);  // an exact int never errors
+      if (overflow) return kDefer;
+    }
     char b[24];
     const auto r = std::to_chars(b, b + sizeof b, x);
     out.append(b, (size_t)(r.ptr - b));
@@ -410,11 +508,29 @@ const B58Len64& b58_len64_table() {
   return t;
 }
 
+// Every character in the base58 alphabet (1-9 A-H J-N P-Z a-k m-z): 16 at a time as six
+// unsigned range tests (SSE2, part of x86-64), the tail by the table.
+bool b58_chars_ok(const unsigned char* s, size_t n) {
+  size_t i = 0;
+  for (; i + 16 <= n; i += 16) {
+    const __m128i c = _mm_loadu_si128((const __m128i*)(s + i));
+    auto in = [&c](char lo, char hi) {
+      const __m128i x = _mm_sub_epi8(c, _mm_set1_epi8(lo));
+      return _mm_cmpeq_epi8(_mm_min_epu8(x, _mm_set1_epi8((char)(hi - lo))), x);  // x <= hi - lo (unsigned)
+    };
+    const __m128i ok = _mm_or_si128(_mm_or_si128(_mm_or_si128(in('1', '9'), in('A', 'H')), in('J', 'N')),
+                                    _mm_or_si128(_mm_or_si128(in('P', 'Z'), in('a', 'k')), in('m', 'z')));
+    if (_mm_movemask_epi8(ok) != 0xFFFF) return false;
+  }
+  for (; i < n; ++i)
+    if (kIndex.v[s[i]] < 0) return false;
+  return true;
+}
+
 // 1: b58decode(s) is valid and exactly 64 bytes; 0: valid, another length;
 // -1: a character outside the alphabet (b58decode raises).
 int b58_len64(const unsigned char* s, size_t n) {
-  for (size_t i = 0; i < n; ++i)
-    if (kIndex.v[s[i]] < 0) return -1;
+  if (!b58_chars_ok(s, n)) return -1;
   size_t nz = 0;
   while (nz < n && s[nz] == '1') ++nz;
   if (nz > 64) return 0;
@@ -693,7 +809,8 @@ struct ScanItem {
   uint64_t sig_at = 0, ser_at = 0;
 };
 struct alignas(64) ScanBuf {  // one cache line per worker: the string headers change on every append
-  std::string sig, ser;
+  std::string sig;
+  OutBuf ser;
 };
 
 // CPUs this process may use: its affinity mask, capped by a cgroup v2 CPU quota
@@ -980,6 +1097,7 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
   }
   static PyObject* k_sig = PyUnicode_InternFromString("signature");
   static PyObject* k_idr = PyUnicode_InternFromString("identifier");
+  PyObject* const top_keys[2] = {k_sig, k_idr};
   const Py_ssize_t n = PySequence_Fast_GET_SIZE(fm);
   struct Held {  // the scratch goes back to the spare slot on every exit unless a pack handle takes it
     ScanScratch* s = take_scratch();
@@ -1117,6 +1235,7 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
     }
     copier.start();
   }
+  const bool prefetch = getenv("EDV_SCAN_PREFETCH") != nullptr;  // (A/B switch: off by default)
   run_chunks(n, t, [&](int w, Py_ssize_t a, Py_ssize_t b) {
     ScanBuf& sb = bufs[(size_t)w];
     WorkerIdrs& tab = tabs[(size_t)w];
@@ -1126,25 +1245,38 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
       ScanItem& x = it[(size_t)i];
       x = ScanItem{};
       idr_of[(size_t)i] = nullptr;
-      if (!PyDict_CheckExact(m)) continue;
-      PyObject *sv = nullptr, *iv = nullptr, *k, *v;
-      Py_ssize_t pos = 0;
-      bool str_keys = true;
-      while (PyDict_Next(m, &pos, &k, &v)) {
-        if (!PyUnicode_CheckExact(k)) {
-          str_keys = false;
-          break;
-        }
-        if (k == k_sig || w_str_eq(k, k_sig))
-          sv = v;
-        else if (k == k_idr || w_str_eq(k, k_idr))
-          iv = v;
+      // requests' objects are scattered over the heap: the dict of request i + 4 and its key
+      // table, and the values of request i + 2 (its table fetched two items ago), ahead of use
+      if (prefetch && i + 4 < b) {
+        PyObject* m4 = items[i + 4];
+        __builtin_prefetch(m4);
+        if (PyDict_CheckExact(m4)) __builtin_prefetch(((PyDictObject*)m4)->ma_keys);
       }
-      if (!str_keys || !(sv && iv && PyUnicode_CheckExact(sv) && PyUnicode_GET_LENGTH(sv) > 0 &&
-                         PyUnicode_CheckExact(iv) && PyUnicode_GET_LENGTH(iv) > 0 && PyUnicode_IS_ASCII(sv)))
+      if (prefetch && i + 2 < b && PyDict_CheckExact(items[i + 2])) {
+        PyObject* m2 = items[i + 2];
+        Py_ssize_t p2 = 0;
+        PyObject *k2, *v2;
+        while (PyDict_Next(m2, &p2, &k2, &v2)) {
+          __builtin_prefetch(k2);
+          __builtin_prefetch(v2);
+          if (PyDict_CheckExact(v2)) __builtin_prefetch(((PyDictObject*)v2)->ma_keys);
+        }
+      }
+      if (!PyDict_CheckExact(m)) continue;
+      // one pass over the request's keys: its signing serialization (kept if the item stays on
+      // the fast path) and the signature and identifier values
+      PyObject* found[2] = {nullptr, nullptr};
+      const size_t at = sb.ser.size();
+      const WRes r = wser_dict(m, 0, ign, sb.ser, top_keys, found);
+      PyObject *sv = found[0], *iv = found[1];
+      if (!(sv && iv && PyUnicode_CheckExact(sv) && PyUnicode_GET_LENGTH(sv) > 0 && PyUnicode_CheckExact(iv) &&
+            PyUnicode_GET_LENGTH(iv) > 0 && PyUnicode_IS_ASCII(sv))) {
+        sb.ser.resize(at);
         continue;  // the Python path raises the reference's exception
+      }
       x.m = m;
       if (!PyUnicode_IS_ASCII(iv)) {  // its UTF-8 form may need allocating: under the GIL
+        sb.ser.resize(at);
         x.state = 2;
         ++tab.deferred;
         continue;
@@ -1154,11 +1286,15 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
       int len64 = 0;
       if (slots) {  // decoded on the GPU when the text decodes to exactly 64 bytes
         len64 = x.ns <= kSigSlot - 1 ? b58_len64(x.sp, (size_t)x.ns) : 0;
-        if (len64 < 0) continue;  // b58decode raises: the Python path (InvalidSignatureFormat)
+        if (len64 < 0) {
+          sb.ser.resize(at);
+          continue;  // b58decode raises: the Python path (InvalidSignatureFormat)
+        }
       }
-      if (len64 == 0 && !b58decode_raw(x.sp, (size_t)x.ns, sig)) continue;
-      const size_t at = sb.ser.size();
-      const WRes r = wser_obj(m, 0, ign, sb.ser);
+      if (len64 == 0 && !b58decode_raw(x.sp, (size_t)x.ns, sig)) {
+        sb.ser.resize(at);
+        continue;
+      }
       if (r != kOk) {
         sb.ser.resize(at);
         x.state = r == kDefer ? 2 : 0;

@@ -113,6 +113,7 @@ class EdVerifyEngine:
             raise EdVerifyUnavailable(lib.edv_last_error().decode(errors="replace"))
         self._lib = lib
         self._ctx = ctypes.c_void_p(ctx)
+        self._one = None  # verify_one_keyed's ctypes arguments
         self.device = device
 
     # ------------------------------------------------------------- lifecycle
@@ -473,6 +474,23 @@ class EdVerifyEngine:
             check(self._lib.edv_verify_batch_keyed(self._ctx, _ptr(sig64), _ptr(key_idx),
                                                    _ptr(msgs) if msgs.size else None, _ptr(msg_off), n, _ptr(bits)))
         return unpack_bits(bits, n)
+
+    def verify_one_keyed(self, sig64, key_id, msg):
+        """One request against registered key `key_id` (bytes in, bool out): the
+        per-message authenticate() path, the same library call as verify_batch_keyed
+        without the numpy packing around it."""
+        if len(sig64) != 64:
+            raise ValueError("sig64 must be 64 bytes")
+        one = self._one
+        if one is None:
+            one = self._one = (ctypes.c_uint32(0), (ctypes.c_uint64 * 2)(0, 0), ctypes.c_uint8(0))
+        kid, off, bits = one
+        kid.value = int(key_id)
+        off[1] = len(msg)
+        bits.value = 0
+        check(self._lib.edv_verify_batch_keyed(self._ctx, bytes(sig64), ctypes.byref(kid), bytes(msg) if msg else None,
+                                               off, 1, ctypes.byref(bits)))
+        return bool(bits.value & 1)
 
     def verify_batch_keyed_device(self, d_sig64, d_key_idx, d_msgs, d_msg_off, n, d_accept_words, stream=None):
         st = _stream_for(stream, d_sig64, d_accept_words)

@@ -142,6 +142,10 @@ def test_pack_sm_layout():
         H.pack_sm([b"a"], [b"b"], [b"short"])
 
 
+_EDGE_INTS = [0, 1, -1, 2**30 - 1, 2**30, -(2**30 - 1), -(2**30), 2**60 - 1, 2**60, -(2**60 - 1), -(2**60),
+              2**63 - 1, -(2**63), 2**63, -(2**63) - 1, 2**64, 10**18, -(10**18)]
+
+
 def _scan_pool(r, n):
     """Request-shaped dicts over the fuzz scalars/objects: every item kind the
     scan must get exactly right (fast, deferred to the GIL, Python path)."""
@@ -164,6 +168,9 @@ def _scan_pool(r, n):
             m[r.choice(["ключ", "z中"])] = r.random()  # wider-kind keys: ordered under the GIL
         elif k == 5:
             m[3] = "non-str key"
+        elif k == 6:  # ints at CPython's digit boundaries (the workers read 1- and 2-digit ints inline)
+            m["operation"] = {"n": r.choice(_EDGE_INTS), "x": [r.choice(_EDGE_INTS), r.choice(_EDGE_INTS)]}
+            m["reqId"] = r.choice(_EDGE_INTS)
         msgs.append(m)
     return msgs
 
