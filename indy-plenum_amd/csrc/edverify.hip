@@ -906,7 +906,8 @@ __device__ __forceinline__ void shfl_fe(fe& out, const fe& in, int delta) {
 #ifndef EDV_SMALL_ORDER
 // fe_mul_o order of the small kernel's products.  One wave's serial carry-started chains
 // (2) beat ten independent accumulators (1) here too: R's decode 99.6 vs 118.2 us, the kernel
-// 103.8 vs 123.4 us (tools/small_probe.py, profiles/r05m).
+// 103.8 vs 123.4 us (tools/small_probe.py, profiles/r05m); and two half-chains joined by a
+// carry ripple (3): decode 107.7 vs 99.0 us (profiles/r05o).
 #define EDV_SMALL_ORDER 2
 #endif
 constexpr int kSO = EDV_SMALL_ORDER;
@@ -1012,7 +1013,7 @@ constexpr int kSmallThreads = 192;
 #define EDV_SMALL_PROFILE 0
 #endif
 #if EDV_SMALL_PROFILE
-__device__ unsigned long long g_small_prof[8];
+__device__ unsigned long long g_small_prof[10];  // [8], [9]: the shader clock at stamps 0 and 7
 #define EDV_SP(k)                                                   \
   do {                                                              \
     if (blockIdx.x == 0 && lane == 0) g_small_prof[k] = wall_clock64(); \
@@ -1048,6 +1049,9 @@ __global__ __launch_bounds__(kSmallThreads) void edv_verify_small_kernel(
   const uint64_t key = in_range ? key0 : 0;
   uint32_t sig[16];
   if (wave == 0) EDV_SP(0);
+#if EDV_SMALL_PROFILE
+  if (blockIdx.x == 0 && threadIdx.x == 0) g_small_prof[8] = __builtin_amdgcn_s_memtime();
+#endif
   load_words(sig, sig64 + 64 * i, 16);
   if (wave == 0) {
     if (lane == 0) {
@@ -1135,6 +1139,9 @@ __global__ __launch_bounds__(kSmallThreads) void edv_verify_small_kernel(
   ok = ok && fe_iszero(d);
   ok8[i] = ok ? 1 : 0;
   EDV_SP(7);
+#if EDV_SMALL_PROFILE
+  if (blockIdx.x == 0) g_small_prof[9] = __builtin_amdgcn_s_memtime();
+#endif
 }
 
 // Fixed-base comb: [x]B with x < 2^253, 64 madds over BASE_COMB (global).
@@ -2816,8 +2823,8 @@ int edv_set_unit_arena(edv_ctx* ctx, uint64_t bytes) {
 }
 
 #if EDV_SMALL_PROFILE
-int edv_small_profile(uint64_t* out8) {  // probe builds only (not in include/edverify.h)
-  HIP_TRY(hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_small_prof), 8 * sizeof(uint64_t)));
+int edv_small_profile(uint64_t* out10) {  // probe builds only (not in include/edverify.h)
+  HIP_TRY(hipMemcpyFromSymbol(out10, HIP_SYMBOL(g_small_prof), 10 * sizeof(uint64_t)));
   return 0;
 }
 #endif

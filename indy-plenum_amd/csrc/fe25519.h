@@ -191,6 +191,24 @@ EDV_HD void mad_acc5(uint64_t& acc, const uint32_t a[5], const uint32_t b[5]) {
 #ifndef EDV_FE_MUL_ORDER
 #define EDV_FE_MUL_ORDER 2  // 2: -3% comb time vs 0 and 1 (tools/ab_keyed.py)
 #endif
+// EDV ORDER 3 (latency: one wave, one request): as 2, but limbs 0-4 and 5-9 run as two
+// independent carry-started chains (limb 5's starts from 0), so a lone wave can overlap them;
+// then the first chain's carry ripples through limbs 5-9 (32-bit steps) and the wrap adds
+// 19 x (both chains' final carries) to limb 0.  Output class C, as ORDER 2.
+EDV_HD void fe_join_halves(uint32_t o[10], uint64_t ca, uint64_t cb) {
+  uint64_t t = (uint64_t)o[5] + ca;
+  o[5] = (uint32_t)t & M25;
+  uint32_t c = (uint32_t)(t >> 25);  // < 2^14
+#pragma unroll
+  for (int k = 6; k < 10; ++k) {
+    const uint32_t u = o[k] + c;
+    o[k] = u & fe_mask(k);
+    c = u >> fe_width(k);
+  }
+  t = (uint64_t)o[0] + (cb + c) * 19u;  // carry out of limb 9 wraps as 19 * 2^0
+  o[0] = (uint32_t)t & M26;
+  o[1] += (uint32_t)(t >> 26);
+}
 template <int ORDER>
 EDV_HD void fe_mul_o(fe& h, const fe& f, const fe& g) {
   EDV_ASSERT(EDV_IS_W(f) && EDV_IS_L(g));
@@ -200,11 +218,15 @@ EDV_HD void fe_mul_o(fe& h, const fe& f, const fe& g) {
     g19[k] = 19u * g.v[k];
     f2[k] = (k & 1) ? 2u * f.v[k] : f.v[k];
   }
-  if constexpr (ORDER == 2) {
-    uint64_t c = 0;
+  if constexpr (ORDER == 2 || ORDER == 3) {
+    uint64_t c = 0, ca = 0;
     uint32_t o[10];  // h may alias f or g
 #pragma unroll
     for (int k = 0; k < 10; ++k) {
+      if (ORDER == 3 && k == 5) {
+        ca = c;
+        c = 0;
+      }
 #if EDV_MAD_CHAIN
       // the chain starts from the carry of limb k - 1 (one v_mad_u64_u32 per
       // product, no separate 64-bit add of the carry, which the compiler's
@@ -231,7 +253,9 @@ EDV_HD void fe_mul_o(fe& h, const fe& f, const fe& g) {
       o[k] = (uint32_t)a & fe_mask(k);
       c = a >> fe_width(k);
     }
-    {
+    if constexpr (ORDER == 3) {
+      fe_join_halves(o, ca, c);
+    } else {
       const uint64_t t = (uint64_t)o[0] + c * 19u;  // carry out of limb 9 wraps as 19 * 2^0
       o[0] = (uint32_t)t & M26;
       o[1] += (uint32_t)(t >> 26);
@@ -285,12 +309,17 @@ EDV_HD void fe_sq_o(fe& h, const fe& f) {
     d19[k] = 19u * f.v[k];
     d38[k] = 38u * f.v[k];
   }
+  constexpr bool kChain = ORDER == 2 || ORDER == 3;
   uint64_t acc[10];
-  uint64_t c = 0;
+  uint64_t c = 0, ca = 0;
   uint32_t o[10];
 #pragma unroll
   for (int k = 0; k < 10; ++k) {
-    uint64_t a = ORDER == 2 ? c : 0;
+    if (ORDER == 3 && k == 5) {
+      ca = c;
+      c = 0;
+    }
+    uint64_t a = kChain ? c : 0;
     uint32_t pa[6], pb[6];
     int np = 0;
 #pragma unroll
@@ -302,7 +331,7 @@ EDV_HD void fe_sq_o(fe& h, const fe& f) {
         const bool wrap = i + j >= 10;
         const uint32_t fi = (i != j) ? d2[i] : d[i];
         const uint32_t fj = wrap ? (both_odd ? d38[j] : d19[j]) : (both_odd ? d2[j] : d[j]);
-        if (ORDER == 2 && EDV_MAD_CHAIN) {
+        if (kChain && EDV_MAD_CHAIN) {
           pa[np] = fi;  // carry-started chain, one asm block per limb
           pb[np] = fj;
           ++np;
@@ -311,22 +340,26 @@ EDV_HD void fe_sq_o(fe& h, const fe& f) {
         }
       }
     }
-    if (ORDER == 2 && EDV_MAD_CHAIN) {
+    if (kChain && EDV_MAD_CHAIN) {
       if (k & 1)
         mad_acc5(a, pa, pb);
       else
         mad_acc6(a, pa, pb);
     }
     acc[k] = a;
-    if (ORDER == 2) {
+    if (kChain) {
       o[k] = (uint32_t)a & fe_mask(k);
       c = a >> fe_width(k);
     }
   }
-  if (ORDER == 2) {
-    const uint64_t t = (uint64_t)o[0] + c * 19u;
-    o[0] = (uint32_t)t & M26;
-    o[1] += (uint32_t)(t >> 26);
+  if (kChain) {
+    if (ORDER == 3) {
+      fe_join_halves(o, ca, c);
+    } else {
+      const uint64_t t = (uint64_t)o[0] + c * 19u;
+      o[0] = (uint32_t)t & M26;
+      o[1] += (uint32_t)(t >> 26);
+    }
 #pragma unroll
     for (int k = 0; k < 10; ++k) h.v[k] = o[k];
   } else {

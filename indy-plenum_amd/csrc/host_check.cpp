@@ -151,19 +151,42 @@ int edv_host_sc_is_canonical(const uint8_t s[32]) {
 
 // out = canonical bytes of (a * b) for field elements given as 32-byte LE
 // integers < 2^255 (exercises fe_frombytes, fe_mul, fe_sq, fe_tobytes).
-void edv_host_fe_mul(uint8_t out[32], const uint8_t a[32], const uint8_t b[32], int square) {
+// mode: bit 0 square; bits 1-2 the product order (0: the default, else fe_mul_o / fe_sq_o<order>)
+static void fe_mul_mode(fe& fo, const fe& fa, const fe& fb, int mode) {
+  const bool sq = mode & 1;
+  switch (mode >> 1) {
+    case 1:
+      sq ? fe_sq_o<1>(fo, fa) : fe_mul_o<1>(fo, fa, fb);
+      break;
+    case 2:
+      sq ? fe_sq_o<2>(fo, fa) : fe_mul_o<2>(fo, fa, fb);
+      break;
+    case 3:
+      sq ? fe_sq_o<3>(fo, fa) : fe_mul_o<3>(fo, fa, fb);
+      break;
+    default:
+      sq ? fe_sq(fo, fa) : fe_mul(fo, fa, fb);
+  }
+  EDV_ASSERT(EDV_IS_C(fo));
+}
+void edv_host_fe_mul(uint8_t out[32], const uint8_t a[32], const uint8_t b[32], int mode) {
   uint32_t wa[8], wb[8], wo[8];
   memcpy(wa, a, 32);
   memcpy(wb, b, 32);
   fe fa, fb, fo;
   fe_frombytes(fa, wa);
   fe_frombytes(fb, wb);
-  if (square)
-    fe_sq(fo, fa);
-  else
-    fe_mul(fo, fa, fb);
+  fe_mul_mode(fo, fa, fb, mode);
   fe_tobytes(wo, fo);
   memcpy(out, wo, 32);
+}
+// The same on raw limbs (a in W, b in L; a in L when squaring): out = the product's limbs (class C).
+void edv_host_fe_mul_limbs(uint32_t out[10], const uint32_t a[10], const uint32_t b[10], int mode) {
+  fe fa, fb, fo;
+  memcpy(fa.v, a, 40);
+  memcpy(fb.v, b, 40);
+  fe_mul_mode(fo, fa, fb, mode);
+  memcpy(out, fo.v, 40);
 }
 
 void edv_host_fe_invert(uint8_t out[32], const uint8_t a[32]) {

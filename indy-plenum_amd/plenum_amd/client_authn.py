@@ -148,7 +148,7 @@ class _GpuState:
 
     def __init__(self, engine=None, device=0, devices=None, verdict_cache_size=1 << 20, key_window="auto",
                  max_keys=16384, hot_key_uses=2, key_store_bytes=KEY_STORE_BYTES, scan_threads=0,
-                 pipeline_part=0, async_key_builds=True, stream=True, stage=True):
+                 pipeline_part=0, async_key_builds=True, stream=True, stage=False):
         self.engine = engine
         self.device = device
         self.devices = devices
@@ -184,7 +184,10 @@ class _GpuState:
         # batches of 2 library chunks (2^19 requests) or more pack chunk by chunk, each chunk's DMA and
         # kernels overlapping the next chunk's pack (_authenticate_streamed)
         self.stream = stream
-        # batches of 2^16 requests or more are staged while scanned (_authenticate_staged)
+        # stage=True: batches of 2^16 requests or more are staged while scanned
+        # (_authenticate_staged).  Off by default: on the box it measured level with the
+        # streamed path (r05m/r05n: 29-31 M requests/s either way; the copies it hides are
+        # not what bounds the batch -- the scan's workers are)
         self.stage = stage
         self.stats = {"batches": 0, "batch_items": 0, "cache_hits": 0, "single_verifies": 0, "keyed_items": 0,
                       "keys_registered": 0}

@@ -640,7 +640,7 @@ def test_staged_batch_equals_whole(oracle, monkeypatch):
     monkeypatch.setattr(CA, "_STAGE_MIN_BATCH", 1000)
     monkeypatch.setattr(CA, "_PINNED_MIN_BATCH", 1000)
     eng = StagingOracleEngine(oracle)
-    a = GpuAuthNr(engine=eng)
+    a = GpuAuthNr(engine=eng, stage=True)
     ref = GpuAuthNr(engine=OracleEngine(oracle), max_keys=0)
     for i, v in zip(idrs, vks):
         a.addIdr(i, v)
@@ -656,7 +656,7 @@ def test_staged_batch_equals_whole(oracle, monkeypatch):
     del odd[4000]["signature"]
     assert [_outcome(r) for r in a.authenticate_batch(odd)] == [_outcome(r) for r in ref.authenticate_batch(odd)]
     assert eng.staged_calls == 1  # left the steady state: repacked, ordinary path
-    small = GpuAuthNr(engine=StagingOracleEngine(oracle))
+    small = GpuAuthNr(engine=StagingOracleEngine(oracle), stage=True)
     for i, v in zip(idrs, vks):
         small.addIdr(i, v)
     small.keys_settle()

@@ -381,7 +381,7 @@ def test_staged_batch_on_gpu(gpu_engine):
     from plenum_amd.base58 import b58decode, b58encode
     n = 70000
     reqs, rx, idrs, vks, pks, sers, sig = _drain(gpu_engine, n_req=n, n_nodes=1)
-    a = GpuAuthNr(engine=gpu_engine)
+    a = GpuAuthNr(engine=gpu_engine, stage=True)
     for idr, vk in zip(idrs, vks):
         a.addIdr(idr, vk)
     a.keys_settle()

@@ -93,6 +93,35 @@ def test_kernel_field_ops(hostcheck):
             assert int.from_bytes(out.raw, "little") == pow(a, p - 2, p)
 
 
+_LIMB_AT = [0, 26, 51, 77, 102, 128, 153, 179, 204, 230]  # radix 2^25.5 limb positions
+
+
+@pytest.mark.parametrize("order", [1, 2, 3])
+def test_kernel_product_orders_at_class_bounds(hostcheck, order):
+    """fe_mul_o / fe_sq_o in every product order (3: the small kernel's two half-chains)
+    on limbs up to the class bounds their callers may pass (f in W = 5 x 2^26 / 5 x 2^25 +
+    2^18, g in L = 3 x 2^26 / 3 x 2^25 + 2^18): the value mod p, output limbs in class C
+    (asserted inside the -DEDV_BOUND_CHECK build)."""
+    rng = random.Random(40 + order)
+    W = [(5 << 26) if k % 2 == 0 else (5 << 25) + (1 << 18) for k in range(10)]
+    L = [(3 << 26) if k % 2 == 0 else (3 << 25) + (1 << 18) for k in range(10)]
+    val = lambda v: sum(x << s for x, s in zip(v, _LIMB_AT)) % p  # noqa: E731
+    arr = ctypes.c_uint32 * 10
+    for t in range(400):
+        if t < 4:
+            a = W if t % 2 == 0 else [x - 1 for x in W]
+            b = L
+        else:
+            a = [rng.randrange(m + 1) for m in W]
+            b = [rng.randrange(m + 1) for m in L]
+        out = arr()
+        hostcheck.edv_host_fe_mul_limbs(out, arr(*a), arr(*b), 2 * order)
+        assert val(list(out)) == val(a) * val(b) % p
+        sq_in = [min(x, m) for x, m in zip(a, L)]
+        hostcheck.edv_host_fe_mul_limbs(out, arr(*sq_in), arr(*sq_in), 2 * order + 1)
+        assert val(list(out)) == val(sq_in) ** 2 % p
+
+
 def test_kernel_point_roundtrip_and_blacklist(hostcheck, oracle):
     import edwards as E
     rng = random.Random(8)

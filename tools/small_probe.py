@@ -26,7 +26,8 @@ buf = np.frombuffer(b"".join(msgs), np.uint8)
 sig = eng.sign_batch(sks, kidx, buf, off)
 lib = ctypes.CDLL(os.environ.get("PLENUM_EDVERIFY_LIB", LIB_PATH))
 prof = getattr(lib, "edv_small_profile", None)
-names = ["hash", "base tree", "decode part 1", "(barrier)", "decode total", "key tree (after barrier)", "end"]
+names = ["hash", "base tree", "decode part 1", "(barrier)", "decode total", "key tree (after barrier)", "end",
+         "shader clock (MHz)"]
 rows, lat = [], []
 for i in range(len(msgs)):
     t0 = time.perf_counter()
@@ -34,16 +35,17 @@ for i in range(len(msgs)):
     lat.append(time.perf_counter() - t0)
     assert ok
     if prof is not None:
-        out = (ctypes.c_uint64 * 8)()
+        out = (ctypes.c_uint64 * 10)()
         assert prof(out) == 0
         t = [out[k] - out[0] for k in range(8)]
-        rows.append([t[1], t[2], t[3], t[4], t[5], t[6] - t[4], t[7]])
+        clk = (out[9] - out[8]) / max(1, t[7]) * 100.0  # shader clock over the kernel, MHz
+        rows.append([t[1], t[2], t[3], t[4], t[5], t[6] - t[4], t[7], clk * 100.0])
 lat = np.array(lat[50:]) * 1e6
 print("key window %d: engine call n=1 p50 %.1f us p99 %.1f us; phases (comb) %.1f us" % (
     kw, np.percentile(lat, 50), np.percentile(lat, 99), eng.last_phases_ms()[2] * 1e3))
 if rows:
     med = np.median(np.array(rows[50:], dtype=np.float64), axis=0) / 100.0  # 100 MHz ticks -> us
     for n_, v in zip(names, med):
-        print("  %-26s %7.1f us (from kernel start)" % (n_, v) if n_ != "key tree (after barrier)" else
-              "  %-26s %7.1f us" % (n_, v))
+        print("  %-26s %7.1f us (from kernel start)" % (n_, v) if n_ not in (names[5], names[7]) else
+              "  %-26s %7.1f" % (n_, v))
 eng.close()
