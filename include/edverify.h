@@ -353,7 +353,9 @@ int edv_tally(edv_ctx *ctx, const uint32_t *key, const uint8_t *voter, const uin
  * (signatures) 128 bytes 0x04 | x | y | 63 zero bytes; G2 (generator,
  * verkeys) 128 bytes x.a | x.b | y.a | y.b; 32-byte big-endian coordinates.
  * A G1/G2 encoding that is off the curve decodes to the point at infinity.
- * One GPU lane per check; host-pointer calls, synchronous. */
+ * One GPU lane per check, or two for batches of at most edv_bls_set_pair_lanes
+ * checks (default 32768; a COMMIT round's ~25 see the latency, not the
+ * throughput); host-pointer calls, synchronous. */
 
 /* BlsCryptoVerifierIndyCrypto.verify_sig (:59-70) over a batch: item i
  * accepts iff e(sig_i, gen) == e(H(m_i), vk_i), H = indy-crypto Bls::_hash.
@@ -373,6 +375,12 @@ int edv_bls_aggregate(edv_ctx *ctx, const uint8_t *sig128, const uint64_t *sig_o
 int edv_bls_sign_batch(edv_ctx *ctx, const uint8_t *sk32, const uint8_t *msgs, const uint64_t *msg_off, uint64_t n,
                        uint8_t *sig128);
 int edv_bls_keygen_batch(edv_ctx *ctx, const uint8_t *sk32, const uint8_t *gen128, uint64_t n, uint8_t *vk128);
+/* Verify batches of at most max_checks take two lanes per check: one Miller
+ * loop each (signature / generator on one lane, H(m) / verkey on its
+ * neighbour), the product and final exponentiation on both -- about half the
+ * serial work of the one-lane form, at half the checks per wave.  0: always
+ * one lane per check.  Same verdicts either way. */
+int edv_bls_set_pair_lanes(edv_ctx *ctx, uint64_t max_checks);
 
 #ifdef __cplusplus
 }

@@ -59,6 +59,84 @@ __global__ __launch_bounds__(kBlsBlock) void edv_bls_verify_kernel(const uint8_t
   if ((threadIdx.x & 63) == 0 && i < n) words[i >> 6] = b;
 }
 
+// The latency form (batches of at most bls_pair_max checks, e.g. a COMMIT round's ~25): two
+// lanes per check, side by side in a wave.  Even lane: the signature and the generator; odd
+// lane: H(m) and the verkey sum.  Each runs ONE Miller loop -- the same code on both lanes, so
+// the wave runs them together -- then the two Fp12 values are swapped across the pair and both
+// lanes form the product and its final exponentiation (the same value on both: no divergence);
+// the even lane's verdict is the check's.  Half the serial Miller work of the one-lane form.
+// words32[j]: the verdicts of checks 32j..32j+31 (the byte layout of the one-lane form's uint64
+// words).
+__device__ __forceinline__ void shfl_xor_fp12(fp12& o, const fp12& x) {
+  const uint32_t* a = (const uint32_t*)&x;
+  uint32_t* b = (uint32_t*)&o;
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(fp12) / 4); ++k) b[k] = (uint32_t)__shfl_xor((int)a[k], 1, 64);
+}
+__global__ __launch_bounds__(kBlsBlock) void edv_bls_verify_pair_kernel(const uint8_t* __restrict__ sig128,
+                                                                       const uint8_t* __restrict__ msgs,
+                                                                       const uint64_t* __restrict__ moff,
+                                                                       const uint8_t* __restrict__ vk128,
+                                                                       const uint64_t* __restrict__ vk_off,
+                                                                       const uint8_t* __restrict__ gen128, uint64_t n,
+                                                                       uint32_t* __restrict__ words32) {
+  const uint64_t lane_g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t i = lane_g >> 1;
+  const bool odd = lane_g & 1;
+  bool live = i < n;  // lanes past the end still take part in the shuffles and the ballot
+  const uint64_t ii = live ? i : 0;
+  fp x, y;
+  fp2 qx, qy;
+  bool inf_p = true, inf_q = true;
+  if (!odd) {
+    g1 s;
+    g2 g;
+    g1_from_bytes(s, sig128 + 128 * ii);
+    g2_from_bytes(g, gen128);
+    inf_p = g1_isinf(s);
+    inf_q = g2_isinf(g);
+    if (!inf_p) g1_affine(x, y, s);
+    if (!inf_q) g2_affine(qx, qy, g);
+  } else {
+    g1 h;
+    g2 v;
+    g1_hash(h, msgs + moff[ii], moff[ii + 1] - moff[ii]);
+    const uint64_t k0 = vk_off ? vk_off[ii] : ii, k1 = vk_off ? vk_off[ii + 1] : ii + 1;
+    g2_inf(v);
+    for (uint64_t k = k0; k < k1; ++k) {  // Bls.verify_multi_sig: the verkeys' sum
+      g2 t;
+      g2_from_bytes(t, vk128 + 128 * k);
+      g2_add(v, v, t);
+    }
+    inf_p = g1_isinf(h);
+    inf_q = g2_isinf(v);
+    if (!inf_p) {
+      g1_affine(x, y, h);
+      fp_neg(y, y);
+    }
+    if (!inf_q) g2_affine(qx, qy, v);
+  }
+  fp12 f;
+  fp12_one(f);
+  if (live && !inf_p && !inf_q) miller_loop_acc(f, x, y, qx, qy);
+  // bls_check's rejections: signature, verkey sum or generator at infinity
+  const bool bad_here = odd ? inf_q : (inf_p || inf_q);
+  const bool bad = bad_here || __shfl_xor((int)bad_here, 1, 64);
+  fp12 other, e;
+  shfl_xor_fp12(other, f);
+  fp12_mul(f, f, other);
+  final_exp(e, f);
+  const bool ok = live && !bad && fp12_isone(e) && !odd;
+  unsigned long long b = __ballot(ok);  // even lanes' verdicts
+  b &= 0x5555555555555555ull;
+  b = (b | (b >> 1)) & 0x3333333333333333ull;
+  b = (b | (b >> 2)) & 0x0f0f0f0f0f0f0f0full;
+  b = (b | (b >> 4)) & 0x00ff00ff00ff00ffull;
+  b = (b | (b >> 8)) & 0x0000ffff0000ffffull;
+  b = (b | (b >> 16)) & 0x00000000ffffffffull;
+  if ((threadIdx.x & 63) == 0 && (lane_g >> 1) < n) words32[lane_g >> 6] = (uint32_t)b;
+}
+
 __global__ __launch_bounds__(kBlsBlock) void edv_bls_aggregate_kernel(const uint8_t* __restrict__ sig128,
                                                                      const uint64_t* __restrict__ off, uint64_t m,
                                                                      uint8_t* __restrict__ out128) {
@@ -175,14 +253,24 @@ int edv_bls_verify_batch(edv_ctx* ctx, const uint8_t* sig128, const uint8_t* msg
     for (uint64_t i = 0; i <= n; ++i) vo[i] = vk_off[i] - vk0;
     BLS_TRY(hipMemcpyAsync(d_vkoff, vo.data(), 8 * (n + 1), hipMemcpyHostToDevice, st));
   }
-  hipLaunchKernelGGL(edv_bls_verify_kernel, dim3(grid_of(n)), dim3(kBlsBlock), 0, st, d_sig, d_msgs, d_off, d_vk,
-                     d_vkoff, d_gen, n, d_words);
+  if (n <= edv_internal::bls_pair_max(ctx))
+    hipLaunchKernelGGL(edv_bls_verify_pair_kernel, dim3(grid_of(2 * n)), dim3(kBlsBlock), 0, st, d_sig, d_msgs, d_off,
+                       d_vk, d_vkoff, d_gen, n, (uint32_t*)d_words);
+  else
+    hipLaunchKernelGGL(edv_bls_verify_kernel, dim3(grid_of(n)), dim3(kBlsBlock), 0, st, d_sig, d_msgs, d_off, d_vk,
+                       d_vkoff, d_gen, n, d_words);
   BLS_TRY(hipGetLastError());
   std::vector<unsigned long long> w(nwords);
   BLS_TRY(hipMemcpyAsync(w.data(), d_words, 8 * nwords, hipMemcpyDeviceToHost, st));
   BLS_TRY(hipStreamSynchronize(st));
   for (uint64_t b = 0; b < (n + 7) / 8; ++b) accept_bits[b] = (uint8_t)(w[b / 8] >> (8 * (b % 8)));
   if (n & 7) accept_bits[n / 8] &= (uint8_t)((1u << (n & 7)) - 1);
+  return 0;
+}
+
+int edv_bls_set_pair_lanes(edv_ctx* ctx, uint64_t max_checks) {
+  if (!ctx) return set_err(EDV_EINVAL, "null context");
+  edv_internal::bls_pair_max(ctx) = max_checks;
   return 0;
 }
 

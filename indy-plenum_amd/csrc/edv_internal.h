@@ -10,4 +10,6 @@ namespace edv_internal {
 int begin(edv_ctx* ctx, hipStream_t* stream);
 // Record the error text for edv_last_error() and return code.
 int set_err(int code, const char* fmt, ...);
+// BLS verify batches of at most this many checks take two lanes per check (edv_bls_set_pair_lanes).
+uint64_t& bls_pair_max(edv_ctx* ctx);
 }  // namespace edv_internal

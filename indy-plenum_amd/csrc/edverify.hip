@@ -1382,6 +1382,7 @@ struct edv_ctx {
   // key-sorted comb order (edv_set_key_sort): the permutation and the verdict bytes [kMaxLanes];
   // per sub-batch: block offsets [kSortBlocks][bins], bin totals / bases [bins] x 2, scan scratch
   int key_sort = 2;
+  uint64_t bls_pair_max = 32768;  // edv_bls_set_pair_lanes
   uint64_t small_max = 256;  // edv_set_small_batch: keyed host-pointer chunks of at most this many requests take
                              // edv_verify_small_kernel (0 = never)
   uint32_t* d_kperm = nullptr;
@@ -2223,6 +2224,7 @@ int begin(edv_ctx* ctx, hipStream_t* stream) {
   *stream = ctx->stream;
   return 0;
 }
+uint64_t& bls_pair_max(edv_ctx* ctx) { return ctx->bls_pair_max; }
 int set_err(int code, const char* fmt, ...) {
   char buf[512];
   va_list ap;

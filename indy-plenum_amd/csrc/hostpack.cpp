@@ -857,6 +857,74 @@ int scan_threads(Py_ssize_t n, int want) {
 // f(worker, begin, end) per chunk.
 constexpr Py_ssize_t kScanChunk = 1024;
 
+// Software prefetch of the requests ahead of the worker (on unless EDV_SCAN_PREFETCH=0): a request is
+// ~10 small objects scattered over the heap (each json-decoded on its own), so the scan waits on
+// one cache miss after another.  Stages, each reading only what an earlier stage fetched: the
+// dict of item i + 10; its key table (i + 7); its keys and values (i + 4); the key tables of
+// dict values (i + 2); their keys and values (i + 1).  Key-table entries are walked directly
+// on CPython 3.10's combined-table layout (elsewhere nothing past the dict is prefetched).
+inline void pf(const void* p) { __builtin_prefetch(p); }
+inline void pf_lines(const void* p, int n) {
+  for (int k = 0; k < n; ++k) __builtin_prefetch((const char*)p + 64 * k);
+}
+#if PY_VERSION_HEX >= 0x030A0000 && PY_VERSION_HEX < 0x030B0000
+struct DkEntry {
+  Py_hash_t h;
+  PyObject *k, *v;
+};
+struct DkHead {  // Objects/dict-common.h, 3.10
+  Py_ssize_t refcnt, size;
+  void* lookup;
+  Py_ssize_t usable, nentries;
+  char idx[1];
+};
+inline const DkEntry* dk_entries(PyObject* o, Py_ssize_t& n) {
+  n = 0;
+  if (Py_TYPE(o) != &PyDict_Type) return nullptr;
+  const PyDictObject* d = (const PyDictObject*)o;
+  if (d->ma_values) return nullptr;  // split table
+  const DkHead* k = (const DkHead*)d->ma_keys;
+  const Py_ssize_t sz = k->size;
+  const int ix = sz <= 0xff ? 1 : sz <= 0xffff ? 2 : sz <= 0xffffffffLL ? 4 : 8;
+  n = k->nentries;
+  return (const DkEntry*)(k->idx + sz * ix);
+}
+#define EDV_HAVE_DK 1
+#endif
+inline void prefetch_ahead(PyObject** items, Py_ssize_t i, Py_ssize_t b) {
+  if (i + 10 < b) pf(items[i + 10]);
+  if (i + 7 < b) {
+    PyObject* o = items[i + 7];
+    if (Py_TYPE(o) == &PyDict_Type) pf_lines(((PyDictObject*)o)->ma_keys, 3);
+  }
+#ifdef EDV_HAVE_DK
+  Py_ssize_t n;
+  if (i + 4 < b)
+    if (const DkEntry* e = dk_entries(items[i + 4], n))
+      for (Py_ssize_t j = 0; j < n; ++j)
+        if (e[j].v) {
+          pf(e[j].k);
+          pf_lines(e[j].v, 2);
+        }
+  if (i + 2 < b)
+    if (const DkEntry* e = dk_entries(items[i + 2], n))
+      for (Py_ssize_t j = 0; j < n; ++j)
+        if (e[j].v && Py_TYPE(e[j].v) == &PyDict_Type) pf_lines(((PyDictObject*)e[j].v)->ma_keys, 3);
+  if (i + 1 < b)
+    if (const DkEntry* e = dk_entries(items[i + 1], n))
+      for (Py_ssize_t j = 0; j < n; ++j) {
+        Py_ssize_t n2;
+        if (e[j].v)
+          if (const DkEntry* e2 = dk_entries(e[j].v, n2))
+            for (Py_ssize_t q = 0; q < n2; ++q)
+              if (e2[q].v) {
+                pf(e2[q].k);
+                pf_lines(e2[q].v, 2);
+              }
+      }
+#endif
+}
+
 // f(worker, begin, end) per chunk of kScanChunk items, chunks taken from a
 // shared counter by the caller and t - 1 pool helpers, so a worker whose CPU
 // is busy with other work takes fewer.
@@ -1235,7 +1303,11 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
     }
     copier.start();
   }
-  const bool prefetch = getenv("EDV_SCAN_PREFETCH") != nullptr;  // (A/B switch: off by default)
+  // software prefetch ahead of the workers (prefetch_ahead): the scan 18.4-19.8 vs 19.7-21.7 ms per
+  // 1M on the box's 16 CPUs, alternating in one process (profiles/r05p/scan_ab.log); EDV_SCAN_PREFETCH=0
+  // turns it off
+  const char* pf_env = getenv("EDV_SCAN_PREFETCH");
+  const bool prefetch = !(pf_env && pf_env[0] == '0');
   run_chunks(n, t, [&](int w, Py_ssize_t a, Py_ssize_t b) {
     ScanBuf& sb = bufs[(size_t)w];
     WorkerIdrs& tab = tabs[(size_t)w];
@@ -1245,23 +1317,7 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
       ScanItem& x = it[(size_t)i];
       x = ScanItem{};
       idr_of[(size_t)i] = nullptr;
-      // requests' objects are scattered over the heap: the dict of request i + 4 and its key
-      // table, and the values of request i + 2 (its table fetched two items ago), ahead of use
-      if (prefetch && i + 4 < b) {
-        PyObject* m4 = items[i + 4];
-        __builtin_prefetch(m4);
-        if (PyDict_CheckExact(m4)) __builtin_prefetch(((PyDictObject*)m4)->ma_keys);
-      }
-      if (prefetch && i + 2 < b && PyDict_CheckExact(items[i + 2])) {
-        PyObject* m2 = items[i + 2];
-        Py_ssize_t p2 = 0;
-        PyObject *k2, *v2;
-        while (PyDict_Next(m2, &p2, &k2, &v2)) {
-          __builtin_prefetch(k2);
-          __builtin_prefetch(v2);
-          if (PyDict_CheckExact(v2)) __builtin_prefetch(((PyDictObject*)v2)->ma_keys);
-        }
-      }
+      if (prefetch) prefetch_ahead(items, i, b);
       if (!PyDict_CheckExact(m)) continue;
       // one pass over the request's keys: its signing serialization (kept if the item stays on
       // the fast path) and the signature and identifier values

@@ -357,6 +357,11 @@ class EdVerifyEngine:
                                                  _ptr(bits)))
         return unpack_bits(bits, n)
 
+    def bls_set_pair_lanes(self, max_checks):
+        """Verify batches of at most max_checks use two lanes per check (lower
+        latency); 0 = one lane per check always (edv_bls_set_pair_lanes)."""
+        check(self._lib.edv_bls_set_pair_lanes(self._ctx, int(max_checks)))
+
     def bls_aggregate(self, sig128, sig_off):
         """out[i] = sum of sig128[sig_off[i]:sig_off[i+1]] (create_multi_sig)."""
         sig128 = _u8(sig128, 128)

@@ -14,11 +14,19 @@ pytestmark = pytest.mark.gpu
 V = json.load(open(os.path.join(GOLDEN, "bls_vectors.json")))
 
 
+@pytest.fixture(params=[32768, 0], ids=["pair_lanes", "one_lane"])
+def bls_mode(request, gpu_engine):
+    """Both verify forms: two lanes per check (batches up to 32768, the default) and one."""
+    gpu_engine.bls_set_pair_lanes(request.param)
+    yield request.param
+    gpu_engine.bls_set_pair_lanes(32768)
+
+
 def _u8(hexes):
     return np.frombuffer(b"".join(bytes.fromhex(h) for h in hexes), np.uint8).reshape(-1, 128)
 
 
-def test_bls_vectors_on_gpu(gpu_engine):
+def test_bls_vectors_on_gpu(gpu_engine, bls_mode):
     from plenum_amd import pack_messages
     gen = np.frombuffer(bytes.fromhex(V["generator"]), np.uint8)
     msgs = [bytes.fromhex(m) for m in V["messages"]]
@@ -48,9 +56,9 @@ def test_bls_vectors_on_gpu(gpu_engine):
     assert (out == _u8([a["out"] for a in ag])).all()
 
 
-def test_bls_random_batch_self_consistent(gpu_engine):
+def test_bls_random_batch_self_consistent(gpu_engine, bls_mode):
     """A larger batch: GPU keys and signatures verify, corrupted ones do not,
-    across wave boundaries (n = 200)."""
+    across wave boundaries (n = 200: 4 waves of 64 checks, or 7 of 32 pairs)."""
     from plenum_amd import pack_messages
     rng = np.random.default_rng(5)
     gen = np.frombuffer(bytes.fromhex(V["generator"]), np.uint8)

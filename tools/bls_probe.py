@@ -12,6 +12,8 @@ from plenum_amd.bls import GENERATOR, ORDER  # noqa: E402
 from plenum_amd.base58 import b58decode  # noqa: E402
 
 eng = EdVerifyEngine(0)
+if os.environ.get("BLS_PAIR") is not None:  # batches up to this many checks: two lanes per check
+    eng.bls_set_pair_lanes(int(os.environ["BLS_PAIR"]))
 gen = np.frombuffer(b58decode(GENERATOR), np.uint8)
 rng = np.random.default_rng(1)
 for n in [int(x) for x in os.environ.get("BLS_SIZES", "64,1024,16384,65536,262144").split(",")]:

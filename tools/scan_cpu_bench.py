@@ -34,12 +34,9 @@ for i in range(n):
 out = [bytearray(), bytearray()]
 for rep in range(reps):
     if os.environ.get("AB"):  # alternate the scan's software prefetch off / on
-        if rep % 2:
-            os.environ["EDV_SCAN_PREFETCH"] = "1"
-        else:
-            os.environ.pop("EDV_SCAN_PREFETCH", None)
+        os.environ["EDV_SCAN_PREFETCH"] = "1" if rep % 2 else "0"
     t0 = time.perf_counter()
     H.scan_batch_u(reqs, ["signature"], threads, out, 96)
     print("scan %d requests, %d threads%s: %.2f ms" % (
-        n, threads, " prefetch" if os.environ.get("EDV_SCAN_PREFETCH") else "", (time.perf_counter() - t0) * 1e3),
+        n, threads, " prefetch" if os.environ.get("EDV_SCAN_PREFETCH", "1") != "0" else "", (time.perf_counter() - t0) * 1e3),
         flush=True)
