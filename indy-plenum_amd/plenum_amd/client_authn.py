@@ -184,6 +184,7 @@ class _GpuState:
         # batches of 2 library chunks (2^19 requests) or more pack chunk by chunk, each chunk's DMA and
         # kernels overlapping the next chunk's pack (_authenticate_streamed)
         self.stream = stream
+        self.last_breakdown = None  # the last streamed batch's phases (ms)
         # stage=True: batches of 2^16 requests or more are staged while scanned
         # (_authenticate_staged).  Off by default: on the box it measured level with the
         # streamed path (r05m/r05n: 29-31 M requests/s either way; the copies it hides are
@@ -608,9 +609,12 @@ class GpuAuthMixin:
         resolved to a built key); any other batch packs whole and takes the
         ordinary path (same verdicts)."""
         import numpy as np
+        from time import perf_counter
         g = self._g
         n = len(msgs)
+        t0 = perf_counter()
         scan = _scan_batch(msgs, [SIG], g.scan_threads, bufs, slot, 1)
+        t1 = perf_counter()
         fast_b, uidx_b, uniq, sig_o, msg_o, off, short, handle = scan
         off_a = np.frombuffer(off, np.uint64)
         mlen = int(off_a[-1])
@@ -629,12 +633,15 @@ class GpuAuthMixin:
         kid = np.asarray(ids, np.uint32)[np.frombuffer(uidx_b, np.uint32)]
         sig_a = np.frombuffer(sig_o, np.uint8, count=slot * n).reshape(-1, slot)
         msg_a = np.frombuffer(msg_o, np.uint8, count=mlen)
+        t2 = perf_counter()
         handles = []
         for c0 in range(0, n, _STREAM_CHUNK):
             c1 = min(n, c0 + _STREAM_CHUNK)
             _pack_range(handle, c0, c1)
             handles.append(eng.verify_submit(sig_a[c0:c1], kid[c0:c1], msg_a, off_a[c0:c1 + 1], True, slot))
+        t3 = perf_counter()
         ok = np.concatenate([np.asarray(eng.verify_collect(h), bool) for h in handles])
+        t4 = perf_counter()
         del handles, sig_a, msg_a
         ok &= np.frombuffer(short, np.uint8) == 0
         g.stats["batches"] += 1
@@ -643,6 +650,11 @@ class GpuAuthMixin:
         results = _results_from(ok.view(np.uint8).tobytes(), uidx_b, uniq)
         for i in np.flatnonzero(~ok).tolist():
             results[i] = InvalidSignature()
+        t5 = perf_counter()
+        # where this batch's time went (bench.py end_to_end.in_batch_ms)
+        g.last_breakdown = {"scan": (t1 - t0) * 1e3, "keys_and_ids": (t2 - t1) * 1e3,
+                            "pack_and_submit": (t3 - t2) * 1e3, "collect_wait": (t4 - t3) * 1e3,
+                            "verdicts": (t5 - t4) * 1e3}
         return results
 
     def _authenticate_pipelined(self, msgs, eng, slot, bufs, part):
