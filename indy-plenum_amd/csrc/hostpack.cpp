@@ -1748,6 +1748,37 @@ PyObject* py_results_from(PyObject*, PyObject* args) {
   return ret;
 }
 
+// gather_u32(table, idx) -> bytearray: out[i] = table[idx[i]] (uint32 LE both), the key id of
+// every request from its identifier's (one pass; numpy's fancy indexing widens the index
+// array to intp first).  ValueError on an index past the table.
+PyObject* py_gather_u32(PyObject*, PyObject* args) {
+  Py_buffer bt, bi;
+  if (!PyArg_ParseTuple(args, "y*y*", &bt, &bi)) return nullptr;
+  PyObject* ret = nullptr;
+  const Py_ssize_t nt = bt.len / 4, n = bi.len / 4;
+  if (bt.len % 4 || bi.len % 4) {
+    PyErr_SetString(PyExc_ValueError, "gather_u32: buffers of uint32 expected");
+  } else if ((ret = PyByteArray_FromStringAndSize(nullptr, n * 4))) {
+    const uint32_t* t = (const uint32_t*)bt.buf;
+    const uint32_t* ix = (const uint32_t*)bi.buf;
+    uint32_t* o = (uint32_t*)PyByteArray_AS_STRING(ret);
+    uint32_t bad = 0;
+    for (Py_ssize_t i = 0; i < n; ++i) {
+      const uint32_t k = ix[i];
+      bad |= (uint32_t)(k >= (uint32_t)nt);
+      o[i] = k < (uint32_t)nt ? t[k] : 0u;
+    }
+    if (bad) {
+      Py_DECREF(ret);
+      ret = nullptr;
+      PyErr_SetString(PyExc_ValueError, "gather_u32: index out of range");
+    }
+  }
+  PyBuffer_Release(&bt);
+  PyBuffer_Release(&bi);
+  return ret;
+}
+
 // gather_items(sig, msgbuf, off, idx, stride=64) -> (sig', msgbuf', off'): the
 // items idx (uint32 LE) of a split batch, repacked contiguously; stride is the
 // signature record size (64 = R || S, 96 = edverify.h signature slots).
@@ -1800,6 +1831,7 @@ PyMethodDef kMethods[] = {
      "an 8th element) into its output buffers"},
     {"repack_spans", py_repack_spans, METH_VARARGS,
      "repack_spans(buf, spans) -> (msgs, off): a staged scan's messages laid out contiguously with offsets"},
+    {"gather_u32", py_gather_u32, METH_VARARGS, "gather_u32(table, idx) -> bytearray: table[idx[i]] (uint32)"},
     {"results_from", py_results_from, METH_VARARGS,
      "results_from(codes_u8, uidx_u32, uniq) -> list: uniq[uidx[i]] where codes[i] == 1, else None"},
     {"gather_items", py_gather_items, METH_VARARGS,

@@ -64,9 +64,9 @@ try:  # native batch scan (csrc/hostpack.cpp): authenticate()'s host steps for a
 except ImportError:  # pragma: no cover - the per-message path below
     _scan_batch = _gather_items = _results_from = None
 try:
-    from ._hostpack import pack_range as _pack_range, repack_spans as _repack_spans
+    from ._hostpack import gather_u32 as _gather_u32, pack_range as _pack_range, repack_spans as _repack_spans
 except ImportError:  # pragma: no cover
-    _pack_range = _repack_spans = None
+    _pack_range = _repack_spans = _gather_u32 = None
 
 try:  # native packing (csrc/hostpack.cpp)
     from ._hostpack import pack_sm as _pack_sm, pack_split64 as _pack_split64
@@ -588,7 +588,7 @@ class GpuAuthMixin:
         if ids is None:  # not the steady state: contiguous messages, the ordinary path
             msg_c, off_c = _repack_spans(msg_o, spans_b)
             return self._finish_scanned(msgs, (fast_b, uidx_b, uniq, sig_o, msg_c, off_c, short), slot, ukeys)
-        kid = np.asarray(ids, np.uint32)[np.frombuffer(uidx_b, np.uint32)]
+        kid = np.frombuffer(_gather_u32(np.asarray(ids, np.uint32).tobytes(), uidx_b), np.uint32)
         ok = np.asarray(eng.verify_staged(True, kid, slot_base, 0, ms, me), bool)
         ok &= np.frombuffer(short, np.uint8) == 0
         g.stats["batches"] += 1
@@ -630,7 +630,7 @@ class GpuAuthMixin:
         if ids is None:  # not the steady state: the whole batch packed, the ordinary path
             _pack_range(handle, 0, n)
             return self._finish_scanned(msgs, scan[:7], slot, ukeys)
-        kid = np.asarray(ids, np.uint32)[np.frombuffer(uidx_b, np.uint32)]
+        kid = np.frombuffer(_gather_u32(np.asarray(ids, np.uint32).tobytes(), uidx_b), np.uint32)
         sig_a = np.frombuffer(sig_o, np.uint8, count=slot * n).reshape(-1, slot)
         msg_a = np.frombuffer(msg_o, np.uint8, count=mlen)
         t2 = perf_counter()

@@ -241,3 +241,13 @@ def test_results_from():
     assert got == ["b", None, "a", None]
     with pytest.raises(ValueError):
         H.results_from(bytes([1]), struct.pack("<I", 5), ["a"])
+
+
+def test_gather_u32():
+    """gather_u32 (the per-request key ids from the per-identifier ones): table[idx[i]], and
+    ValueError past the table."""
+    t = struct.pack("<3I", 7, 8, 9)
+    assert struct.unpack("<5I", bytes(H.gather_u32(t, struct.pack("<5I", 2, 0, 1, 2, 0)))) == (9, 7, 8, 9, 7)
+    assert bytes(H.gather_u32(t, b"")) == b""
+    with pytest.raises(ValueError):
+        H.gather_u32(t, struct.pack("<I", 3))
