@@ -353,8 +353,8 @@ int edv_tally(edv_ctx *ctx, const uint32_t *key, const uint8_t *voter, const uin
  * (signatures) 128 bytes 0x04 | x | y | 63 zero bytes; G2 (generator,
  * verkeys) 128 bytes x.a | x.b | y.a | y.b; 32-byte big-endian coordinates.
  * A G1/G2 encoding that is off the curve decodes to the point at infinity.
- * One GPU lane per check, or two for batches of at most edv_bls_set_pair_lanes
- * checks (default 32768; a COMMIT round's ~25 see the latency, not the
+ * One GPU lane per check, or two / four for small batches
+ * (edv_bls_set_pair_lanes; a COMMIT round's ~25 see the latency, not the
  * throughput); host-pointer calls, synchronous. */
 
 /* BlsCryptoVerifierIndyCrypto.verify_sig (:59-70) over a batch: item i
@@ -378,8 +378,10 @@ int edv_bls_keygen_batch(edv_ctx *ctx, const uint8_t *sk32, const uint8_t *gen12
 /* Verify batches of at most max_checks take two lanes per check: one Miller
  * loop each (signature / generator on one lane, H(m) / verkey on its
  * neighbour), the product and final exponentiation on both -- about half the
- * serial work of the one-lane form, at half the checks per wave.  0: always
- * one lane per check.  Same verdicts either way. */
+ * serial work of the one-lane form, at half the checks per wave.  Batches of
+ * at most max_checks / 2 take four: the same two Miller loops, then the final
+ * exponentiation's cyclotomic squarings spread over three lanes.  0: always
+ * one lane per check.  Same verdicts in every form.  Default 32768. */
 int edv_bls_set_pair_lanes(edv_ctx *ctx, uint64_t max_checks);
 
 #ifdef __cplusplus

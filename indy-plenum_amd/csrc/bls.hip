@@ -137,6 +137,111 @@ __global__ __launch_bounds__(kBlsBlock) void edv_bls_verify_pair_kernel(const ui
   if ((threadIdx.x & 63) == 0 && (lane_g >> 1) < n) words32[lane_g >> 6] = (uint32_t)b;
 }
 
+// The four-lane form (batches of at most half of bls_pair_max checks): lanes 0 / 1 of a check's
+// quad run the two Miller loops as in the pair form, then all four hold the product and run
+// the final exponentiation together with each cyclotomic squaring spread over lanes 0-2 (one
+// Fp4 squaring each, the 2 x 2 Fp2 results gathered by shuffles; lane 3 repeats lane 0's),
+// the rest of it replicated.  words16[j]: the verdicts of checks 16j..16j+15.
+struct CycloSqQuad {
+  int q;     // lane within the quad
+  int base;  // the quad's first lane in the wave
+  __device__ void operator()(fp12& r, const fp12& x) const {
+    const fp2& a = q == 1 ? x.c1.c0 : q == 2 ? x.c0.c1 : x.c0.c0;  // (1, w^3) / (w, w^4) / (w^2, w^5)
+    const fp2& b = q == 1 ? x.c0.c2 : q == 2 ? x.c1.c2 : x.c1.c1;
+    fp2 te[2];
+    fp4_sqr(te[0], te[1], a, b);
+    fp2 t[6];  // t0..t5 of fp12_cyclo_sqr: lane base + j holds t[2j], t[2j+1]
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const uint32_t* src = (const uint32_t*)te;
+      uint32_t* dst = (uint32_t*)&t[2 * j];
+#pragma unroll
+      for (int k = 0; k < (int)(2 * sizeof(fp2) / 4); ++k) dst[k] = (uint32_t)__shfl((int)src[k], base + j, 64);
+    }
+    fp2 xt5;
+    fp2_mul_xi(xt5, t[5]);
+    fp12 o;
+    fp2_3t_m2z(o.c0.c0, t[0], x.c0.c0);
+    fp2_3t_p2z(o.c1.c1, t[1], x.c1.c1);
+    fp2_3t_p2z(o.c1.c0, xt5, x.c1.c0);
+    fp2_3t_m2z(o.c0.c2, t[4], x.c0.c2);
+    fp2_3t_m2z(o.c0.c1, t[2], x.c0.c1);
+    fp2_3t_p2z(o.c1.c2, t[3], x.c1.c2);
+    r = o;
+  }
+};
+__device__ __forceinline__ void shfl_fp12(fp12& o, const fp12& x, int src_lane) {
+  const uint32_t* a = (const uint32_t*)&x;
+  uint32_t* b = (uint32_t*)&o;
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(fp12) / 4); ++k) b[k] = (uint32_t)__shfl((int)a[k], src_lane, 64);
+}
+__global__ __launch_bounds__(kBlsBlock) void edv_bls_verify_quad_kernel(const uint8_t* __restrict__ sig128,
+                                                                       const uint8_t* __restrict__ msgs,
+                                                                       const uint64_t* __restrict__ moff,
+                                                                       const uint8_t* __restrict__ vk128,
+                                                                       const uint64_t* __restrict__ vk_off,
+                                                                       const uint8_t* __restrict__ gen128, uint64_t n,
+                                                                       uint16_t* __restrict__ words16) {
+  const uint64_t lane_g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t i = lane_g >> 2;
+  const int q = (int)(lane_g & 3), base = (int)(threadIdx.x & 63) & ~3;
+  const bool live = i < n;  // lanes past the end still take part in the shuffles and the ballot
+  const uint64_t ii = live ? i : 0;
+  fp x, y;
+  fp2 qx, qy;
+  bool inf_p = false, inf_q = false, run = false;
+  if (q == 0) {
+    g1 s;
+    g2 g;
+    g1_from_bytes(s, sig128 + 128 * ii);
+    g2_from_bytes(g, gen128);
+    inf_p = g1_isinf(s);
+    inf_q = g2_isinf(g);
+    if (!inf_p) g1_affine(x, y, s);
+    if (!inf_q) g2_affine(qx, qy, g);
+    run = !inf_p && !inf_q;
+  } else if (q == 1) {
+    g1 h;
+    g2 v;
+    g1_hash(h, msgs + moff[ii], moff[ii + 1] - moff[ii]);
+    const uint64_t k0 = vk_off ? vk_off[ii] : ii, k1 = vk_off ? vk_off[ii + 1] : ii + 1;
+    g2_inf(v);
+    for (uint64_t k = k0; k < k1; ++k) {  // Bls.verify_multi_sig: the verkeys' sum
+      g2 t;
+      g2_from_bytes(t, vk128 + 128 * k);
+      g2_add(v, v, t);
+    }
+    inf_p = g1_isinf(h);
+    inf_q = g2_isinf(v);
+    if (!inf_p) {
+      g1_affine(x, y, h);
+      fp_neg(y, y);
+    }
+    if (!inf_q) g2_affine(qx, qy, v);
+    run = !inf_p && !inf_q;
+  }
+  fp12 f;
+  fp12_one(f);
+  if (live && run) miller_loop_acc(f, x, y, qx, qy);
+  // bls_check's rejections: signature or generator (lane 0), verkey sum (lane 1) at infinity
+  const bool bad_here = q == 0 ? (inf_p || inf_q) : q == 1 ? inf_q : false;
+  const bool bad = __shfl((int)bad_here, base, 64) || __shfl((int)bad_here, base + 1, 64);
+  fp12 f0, f1, e;
+  shfl_fp12(f0, f, base);
+  shfl_fp12(f1, f, base + 1);
+  fp12_mul(f, f0, f1);
+  final_exp(e, f, CycloSqQuad{q == 3 ? 0 : q, base});
+  const bool ok = live && !bad && fp12_isone(e) && q == 0;
+  unsigned long long b = __ballot(ok);  // lane 0 of each quad
+  b &= 0x1111111111111111ull;
+  b = (b | (b >> 3)) & 0x0303030303030303ull;
+  b = (b | (b >> 6)) & 0x000f000f000f000full;
+  b = (b | (b >> 12)) & 0x000000ff000000ffull;
+  b = (b | (b >> 24)) & 0x000000000000ffffull;
+  if ((threadIdx.x & 63) == 0 && (lane_g >> 2) < n) words16[lane_g >> 6] = (uint16_t)b;
+}
+
 __global__ __launch_bounds__(kBlsBlock) void edv_bls_aggregate_kernel(const uint8_t* __restrict__ sig128,
                                                                      const uint64_t* __restrict__ off, uint64_t m,
                                                                      uint8_t* __restrict__ out128) {
@@ -253,7 +358,10 @@ int edv_bls_verify_batch(edv_ctx* ctx, const uint8_t* sig128, const uint8_t* msg
     for (uint64_t i = 0; i <= n; ++i) vo[i] = vk_off[i] - vk0;
     BLS_TRY(hipMemcpyAsync(d_vkoff, vo.data(), 8 * (n + 1), hipMemcpyHostToDevice, st));
   }
-  if (n <= edv_internal::bls_pair_max(ctx))
+  if (2 * n <= edv_internal::bls_pair_max(ctx))
+    hipLaunchKernelGGL(edv_bls_verify_quad_kernel, dim3(grid_of(4 * n)), dim3(kBlsBlock), 0, st, d_sig, d_msgs, d_off,
+                       d_vk, d_vkoff, d_gen, n, (uint16_t*)d_words);
+  else if (n <= edv_internal::bls_pair_max(ctx))
     hipLaunchKernelGGL(edv_bls_verify_pair_kernel, dim3(grid_of(2 * n)), dim3(kBlsBlock), 0, st, d_sig, d_msgs, d_off,
                        d_vk, d_vkoff, d_gen, n, (uint32_t*)d_words);
   else

@@ -975,21 +975,28 @@ EDV_BN_NI void miller_loop_acc(fp12& f, const fp& xP, const fp& yP, const fp2& x
 
 // f^x for f in the cyclotomic subgroup (x = -|x| < 0: the conjugate of
 // f^|x|, |x| = 2^62 + 2^55 + 1); squarings by fp12_cyclo_sqr
-EDV_BN_NI void fp12_pow_x(fp12& r, const fp12& f) {
+// SQ: the cyclotomic squaring used (CycloSq here; bls.hip's four-lane form spreads its three
+// Fp4 squarings over the lanes of a check)
+struct CycloSq {
+  EDV_HDM void operator()(fp12& r, const fp12& x) const { fp12_cyclo_sqr(r, x); }
+};
+template <class SQ>
+EDV_BN_NI void fp12_pow_x(fp12& r, const fp12& f, SQ sq) {
   fp12 acc = f;
   for (int bit = 61; bit >= 0; --bit) {
-    fp12_cyclo_sqr(acc, acc);
+    sq(acc, acc);
     if (bit == 55 || bit == 0) fp12_mul(acc, acc, f);
   }
   fp12_conj(r, acc);
 }
 // f^k for a small constant k >= 1, f in the cyclotomic subgroup
-EDV_BN_NI void fp12_pow_small(fp12& r, const fp12& f, uint32_t k) {
+template <class SQ>
+EDV_BN_NI void fp12_pow_small(fp12& r, const fp12& f, uint32_t k, SQ sq) {
   fp12 acc = f;
   int top = 31;
   while (!((k >> top) & 1u)) --top;
   for (int bit = top - 1; bit >= 0; --bit) {
-    fp12_cyclo_sqr(acc, acc);
+    sq(acc, acc);
     if ((k >> bit) & 1u) fp12_mul(acc, acc, f);
   }
   r = acc;
@@ -999,7 +1006,8 @@ EDV_BN_NI void fp12_pow_small(fp12& r, const fp12& f, uint32_t k) {
 // l0 + l1 p + l2 p^2 + p^3 exactly, with l0 = -36x^3 - 30x^2 - 18x - 2,
 // l1 = -36x^3 - 18x^2 - 12x + 1, l2 = 6x^2 + 1 (BN), from t^x, t^(x^2),
 // t^(x^3) -- 186 squarings instead of the 760 of a plain power.
-EDV_BN_NI void final_exp(fp12& r, const fp12& f) {
+template <class SQ = CycloSq>
+EDV_BN_NI void final_exp(fp12& r, const fp12& f, SQ sq = SQ()) {
   fp12 t, u;
   fp12_conj(t, f);  // f^(p^6 - 1)
   fp12_inv(u, f);
@@ -1008,30 +1016,30 @@ EDV_BN_NI void final_exp(fp12& r, const fp12& f) {
   fp12_frob(u, u);
   fp12_mul(t, u, t);
   fp12 a, b, c, c36, y, z;
-  fp12_pow_x(a, t);  // t^x
-  fp12_pow_x(b, a);  // t^(x^2)
-  fp12_pow_x(c, b);  // t^(x^3)
-  fp12_pow_small(c36, c, 36);
+  fp12_pow_x(a, t, sq);  // t^x
+  fp12_pow_x(b, a, sq);  // t^(x^2)
+  fp12_pow_x(c, b, sq);  // t^(x^3)
+  fp12_pow_small(c36, c, 36, sq);
   // t^l0 = conj(c^36 b^30 a^18 t^2)
-  fp12_pow_small(y, b, 30);
+  fp12_pow_small(y, b, 30, sq);
   fp12_mul(y, y, c36);
-  fp12_pow_small(z, a, 18);
+  fp12_pow_small(z, a, 18, sq);
   fp12_mul(y, y, z);
-  fp12_cyclo_sqr(z, t);
+  sq(z, t);
   fp12_mul(y, y, z);
   fp12 res;
   fp12_conj(res, y);
   // (t^l1)^p, t^l1 = conj(c^36 b^18 a^12) t
-  fp12_pow_small(y, b, 18);
+  fp12_pow_small(y, b, 18, sq);
   fp12_mul(y, y, c36);
-  fp12_pow_small(z, a, 12);
+  fp12_pow_small(z, a, 12, sq);
   fp12_mul(y, y, z);
   fp12_conj(y, y);
   fp12_mul(y, y, t);
   fp12_frob(y, y);
   fp12_mul(res, res, y);
   // (t^l2)^(p^2), t^l2 = b^6 t
-  fp12_pow_small(y, b, 6);
+  fp12_pow_small(y, b, 6, sq);
   fp12_mul(y, y, t);
   fp12_frob(y, y);
   fp12_frob(y, y);

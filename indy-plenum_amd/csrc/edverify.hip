@@ -1383,6 +1383,9 @@ struct edv_ctx {
   // per sub-batch: block offsets [kSortBlocks][bins], bin totals / bases [bins] x 2, scan scratch
   int key_sort = 2;
   uint64_t bls_pair_max = 32768;  // edv_bls_set_pair_lanes
+  // the small keyed path reads its packed inputs straight from pinned host memory (no H2D copy
+  // before the kernel); A/B switch EDV_SMALL_ZC=1
+  bool small_zero_copy = getenv("EDV_SMALL_ZC") != nullptr;
   uint64_t small_max = 256;  // edv_set_small_batch: keyed host-pointer chunks of at most this many requests take
                              // edv_verify_small_kernel (0 = never)
   uint32_t* d_kperm = nullptr;
@@ -2105,8 +2108,9 @@ static int host_submit(edv_ctx* ctx, bool keyed, const uint8_t* sig, uint64_t si
         if (mbytes) memcpy(hb + o_msg, msgs + m0, mbytes);
         stage_s += std::chrono::duration<double>(clk::now() - t0).count();
         hipStream_t st = ctx->stream;
-        char* db = (char*)ctx->d_msg[sl].p;
-        HIP_TRY(hipMemcpyAsync(db, hb, c_bytes, hipMemcpyHostToDevice, st));
+        const bool zc = keyed && !slots && ctx->small_zero_copy;  // the kernel reads hb over PCIe
+        char* db = zc ? hb : (char*)ctx->d_msg[sl].p;
+        if (!zc) HIP_TRY(hipMemcpyAsync(db, hb, c_bytes, hipMemcpyHostToDevice, st));
         ctx->last_h2d_bytes += c_bytes;
         void* d_sig_use = db;
         if (slots) {

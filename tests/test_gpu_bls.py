@@ -14,11 +14,13 @@ pytestmark = pytest.mark.gpu
 V = json.load(open(os.path.join(GOLDEN, "bls_vectors.json")))
 
 
-@pytest.fixture(params=[32768, 0], ids=["pair_lanes", "one_lane"])
+@pytest.fixture(params=["quad", "pair", "one"])
 def bls_mode(request, gpu_engine):
-    """Both verify forms: two lanes per check (batches up to 32768, the default) and one."""
-    gpu_engine.bls_set_pair_lanes(request.param)
-    yield request.param
+    """Every verify form: four lanes per check (batches up to half the pair limit), two, one.
+    Returns set(n): selects that form for an n-check batch."""
+    def set_for(n):
+        gpu_engine.bls_set_pair_lanes({"quad": 2 * n, "pair": n, "one": 0}[request.param])
+    yield set_for
     gpu_engine.bls_set_pair_lanes(32768)
 
 
@@ -40,6 +42,7 @@ def test_bls_vectors_on_gpu(gpu_engine, bls_mode):
     assert (got == _u8([s["sig"] for s in sig_items])).all()
     # every verdict, single and multi in one launch
     cases = V["cases"]
+    bls_mode(len(cases))
     buf, off = pack_messages([msgs[c["msg"]] for c in cases])
     vks, vk_off = [], [0]
     for c in cases:
@@ -58,7 +61,7 @@ def test_bls_vectors_on_gpu(gpu_engine, bls_mode):
 
 def test_bls_random_batch_self_consistent(gpu_engine, bls_mode):
     """A larger batch: GPU keys and signatures verify, corrupted ones do not,
-    across wave boundaries (n = 200: 4 waves of 64 checks, or 7 of 32 pairs)."""
+    across wave boundaries (n = 200: 4 waves of 64 checks, 7 of 32 pairs, or 13 of 16 quads)."""
     from plenum_amd import pack_messages
     rng = np.random.default_rng(5)
     gen = np.frombuffer(bytes.fromhex(V["generator"]), np.uint8)
@@ -73,6 +76,7 @@ def test_bls_random_batch_self_consistent(gpu_engine, bls_mode):
     sigs = gpu_engine.bls_sign_batch(sks, buf, off)
     sigs[::7, 50] ^= 1  # off the curve
     vks[3::11] = vks[(np.arange(3, n, 11) + 1) % n]  # someone else's key
+    bls_mode(n)
     ok = gpu_engine.bls_verify_batch(sigs, buf, off, vks, gen)
     want = np.ones(n, bool)
     want[::7] = False

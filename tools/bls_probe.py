@@ -14,6 +14,7 @@ from plenum_amd.base58 import b58decode  # noqa: E402
 eng = EdVerifyEngine(0)
 if os.environ.get("BLS_PAIR") is not None:  # batches up to this many checks: two lanes per check
     eng.bls_set_pair_lanes(int(os.environ["BLS_PAIR"]))
+FORM = os.environ.get("BLS_FORM")  # quad / pair / one: that verify form at every size
 gen = np.frombuffer(b58decode(GENERATOR), np.uint8)
 rng = np.random.default_rng(1)
 for n in [int(x) for x in os.environ.get("BLS_SIZES", "64,1024,16384,65536,262144").split(",")]:
@@ -27,6 +28,8 @@ for n in [int(x) for x in os.environ.get("BLS_SIZES", "64,1024,16384,65536,26214
     t = time.time()
     sigs = eng.bls_sign_batch(sks, buf, off)
     ts = time.time() - t
+    if FORM:
+        eng.bls_set_pair_lanes({"quad": 2 * n, "pair": n, "one": 0}[FORM])
     t = time.time()
     ok = eng.bls_verify_batch(sigs, buf, off, vks, gen)
     tv = time.time() - t
