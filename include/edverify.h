@@ -379,9 +379,9 @@ int edv_bls_keygen_batch(edv_ctx *ctx, const uint8_t *sk32, const uint8_t *gen12
  * loop each (signature / generator on one lane, H(m) / verkey on its
  * neighbour), the product and final exponentiation on both -- about half the
  * serial work of the one-lane form, at half the checks per wave.  Batches of
- * at most max_checks / 2 take four: the same two Miller loops, then the final
- * exponentiation's cyclotomic squarings spread over three lanes.  0: always
- * one lane per check.  Same verdicts in every form.  Default 32768. */
+ * at most max_checks / 2 take four: each Miller loop split over two lanes,
+ * then the final exponentiation's cyclotomic squarings spread over three.
+ * 0: always one lane per check.  Same verdicts in every form.  Default 32768. */
 int edv_bls_set_pair_lanes(edv_ctx *ctx, uint64_t max_checks);
 
 #ifdef __cplusplus

@@ -137,11 +137,12 @@ __global__ __launch_bounds__(kBlsBlock) void edv_bls_verify_pair_kernel(const ui
   if ((threadIdx.x & 63) == 0 && (lane_g >> 1) < n) words32[lane_g >> 6] = (uint32_t)b;
 }
 
-// The four-lane form (batches of at most half of bls_pair_max checks): lanes 0 / 1 of a check's
-// quad run the two Miller loops as in the pair form, then all four hold the product and run
-// the final exponentiation together with each cyclotomic squaring spread over lanes 0-2 (one
-// Fp4 squaring each, the 2 x 2 Fp2 results gathered by shuffles; lane 3 repeats lane 0's),
-// the rest of it replicated.  words16[j]: the verdicts of checks 16j..16j+15.
+// The four-lane form (batches of at most half of bls_pair_max checks): lanes 0 / 2 of a check's
+// quad run the (signature, generator) Miller loop and lanes 1 / 3 the (-H(m), verkeys) one,
+// each over its two lanes (LineSplit), then all four hold the product and run the final
+// exponentiation together with each cyclotomic squaring spread over lanes 0-2 (one Fp4
+// squaring each, the 2 x 2 Fp2 results gathered by shuffles; lane 3 repeats lane 0's), the
+// rest of it replicated.  words16[j]: the verdicts of checks 16j..16j+15.
 struct CycloSqQuad {
   int q;     // lane within the quad
   int base;  // the quad's first lane in the wave
@@ -170,6 +171,67 @@ struct CycloSqQuad {
     r = o;
   }
 };
+// The Miller loop of one pairing over two lanes (h = 0 / 1, partners lane ^ 2): each Fp12
+// squaring's two Fp6 products (a b; (a + b)(a + v b)) and each line multiply's two sparse Fp6
+// products (b (l1, l2); (a + b)(l0 + l1, l2)) go one to each lane -- the same code on both,
+// operands chosen by selects -- and are swapped by shuffles; the line evaluation and the twist
+// point's doubling / addition stay on both lanes.
+__device__ __forceinline__ void fp6_shfl_xor(fp6& o, const fp6& x, int m) {
+  const uint32_t* a = (const uint32_t*)&x;
+  uint32_t* b = (uint32_t*)&o;
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(fp6) / 4); ++k) b[k] = (uint32_t)__shfl_xor((int)a[k], m, 64);
+}
+__device__ __forceinline__ void fp6_sel(fp6& r, bool c, const fp6& x, const fp6& y) {  // c ? y : x
+  const uint32_t* a = (const uint32_t*)&x;
+  const uint32_t* b = (const uint32_t*)&y;
+  uint32_t* o = (uint32_t*)&r;
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(fp6) / 4); ++k) o[k] = c ? b[k] : a[k];
+}
+struct LineSplit {
+  int h;
+  __device__ void sqr(fp12& g) const {
+    fp6 s, u, t, X, Y, R, O, ab, sq;
+    fp6_add(s, g.c0, g.c1);
+    fp6_mul_v(t, g.c1);
+    fp6_add(u, g.c0, t);
+    fp6_sel(X, h, g.c0, s);  // lane 0: a * b; lane 1: (a + b)(a + v b)
+    fp6_sel(Y, h, g.c1, u);
+    fp6_mul(R, X, Y);
+    fp6_shfl_xor(O, R, 2);
+    fp6_sel(ab, h, R, O);
+    fp6_sel(sq, h, O, R);
+    fp6_sub(sq, sq, ab);  // a^2 + v b^2 + v ab
+    fp6_mul_v(t, ab);
+    fp6_sub(g.c0, sq, t);
+    fp6_add(g.c1, ab, ab);
+  }
+  __device__ void mul_line(fp12& f, const fp2& l0, const fp2& l1, const fp2& l2) const {
+    fp6 aA, s, X, R, O, bB, sm;
+    fp2_mul(aA.c0, f.c0.c0, l0);  // a * (l0, 0, 0), both lanes
+    fp2_mul(aA.c1, f.c0.c1, l0);
+    fp2_mul(aA.c2, f.c0.c2, l0);
+    fp6_add(s, f.c0, f.c1);
+    fp6_sel(X, h, f.c1, s);  // lane 0: b * (l1, l2, 0); lane 1: (a + b)(l0 + l1, l2, 0)
+    fp2 m0, b0;
+    fp2_add(m0, l0, l1);
+    const uint32_t* p0 = (const uint32_t*)&l1;
+    const uint32_t* p1 = (const uint32_t*)&m0;
+    uint32_t* pb = (uint32_t*)&b0;
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(fp2) / 4); ++k) pb[k] = h ? p1[k] : p0[k];
+    fp6_mul_01(R, X, b0, l2);
+    fp6_shfl_xor(O, R, 2);
+    fp6_sel(bB, h, R, O);
+    fp6_sel(sm, h, O, R);
+    fp6_sub(sm, sm, aA);
+    fp6_sub(f.c1, sm, bB);
+    fp6_mul_v(bB, bB);
+    fp6_add(f.c0, aA, bB);
+  }
+};
+
 __device__ __forceinline__ void shfl_fp12(fp12& o, const fp12& x, int src_lane) {
   const uint32_t* a = (const uint32_t*)&x;
   uint32_t* b = (uint32_t*)&o;
@@ -191,7 +253,8 @@ __global__ __launch_bounds__(kBlsBlock) void edv_bls_verify_quad_kernel(const ui
   fp x, y;
   fp2 qx, qy;
   bool inf_p = false, inf_q = false, run = false;
-  if (q == 0) {
+  // lanes 0 / 2: the (signature, generator) pairing's two halves; lanes 1 / 3: (-H(m), verkeys)
+  if ((q & 1) == 0) {
     g1 s;
     g2 g;
     g1_from_bytes(s, sig128 + 128 * ii);
@@ -201,7 +264,7 @@ __global__ __launch_bounds__(kBlsBlock) void edv_bls_verify_quad_kernel(const ui
     if (!inf_p) g1_affine(x, y, s);
     if (!inf_q) g2_affine(qx, qy, g);
     run = !inf_p && !inf_q;
-  } else if (q == 1) {
+  } else {
     g1 h;
     g2 v;
     g1_hash(h, msgs + moff[ii], moff[ii + 1] - moff[ii]);
@@ -223,7 +286,7 @@ __global__ __launch_bounds__(kBlsBlock) void edv_bls_verify_quad_kernel(const ui
   }
   fp12 f;
   fp12_one(f);
-  if (live && run) miller_loop_acc(f, x, y, qx, qy);
+  if (live && run) miller_loop_acc(f, x, y, qx, qy, LineSplit{q >> 1});
   // bls_check's rejections: signature or generator (lane 0), verkey sum (lane 1) at infinity
   const bool bad_here = q == 0 ? (inf_p || inf_q) : q == 1 ? inf_q : false;
   const bool bad = __shfl((int)bad_here, base, 64) || __shfl((int)bad_here, base + 1, 64);

@@ -895,7 +895,14 @@ EDV_BN_NI void g1_hash(g1& r, const uint8_t* msg, uint64_t mlen) {
 //   doubling: 2YZ^3 yP - 3X^2 Z^2 xP w + (3X^3 - 2Y^2) v w
 //   addition: Z eps yP - theta xP w + (theta xQ - Z eps yQ) v w
 //             with theta = yQ Z^3 - Y, eps = xQ Z^2 - X.
-EDV_BN_NI void miller_dbl(fp12& f, g2& T, const fp& xP, const fp& yP) {
+// The Miller loop's two Fp12 steps (squaring the accumulator, multiplying a line in), as a
+// policy: LineDirect here; bls.hip's LineSplit runs each over a pair of lanes.
+struct LineDirect {
+  EDV_HDM void sqr(fp12& g) const { fp12_sqr(g, g); }
+  EDV_HDM void mul_line(fp12& f, const fp2& l0, const fp2& l1, const fp2& l2) const { fp12_mul_line(f, l0, l1, l2); }
+};
+template <class SP = LineDirect>
+EDV_BN_NI void miller_dbl(fp12& f, g2& T, const fp& xP, const fp& yP, SP sp = SP()) {
   fp2 XX, YY, ZZ, u, l0, l1, l2, t;
   fp2_sqr(XX, T.X);
   fp2_sqr(YY, T.Y);
@@ -912,10 +919,11 @@ EDV_BN_NI void miller_dbl(fp12& f, g2& T, const fp& xP, const fp& yP) {
   fp2_mul(l2, u, T.X);  // 3 X^3 - 2 Y^2
   fp2_dbl(t, YY);
   fp2_sub(l2, l2, t);
-  fp12_mul_line(f, l0, l1, l2);
+  sp.mul_line(f, l0, l1, l2);
   g2_dbl(T, T);
 }
-EDV_BN_NI void miller_add(fp12& f, g2& T, const fp2& xQ, const fp2& yQ, const fp& xP, const fp& yP) {
+template <class SP = LineDirect>
+EDV_BN_NI void miller_add(fp12& f, g2& T, const fp2& xQ, const fp2& yQ, const fp& xP, const fp& yP, SP sp = SP()) {
   fp2 ZZ, ZZZ, theta, eps, k, t, l0, l1, l2;
   fp2_sqr(ZZ, T.Z);
   fp2_mul(ZZZ, ZZ, T.Z);
@@ -930,7 +938,7 @@ EDV_BN_NI void miller_add(fp12& f, g2& T, const fp2& xQ, const fp2& yQ, const fp
   fp2_mul(l2, theta, xQ);  // theta xQ - k yQ
   fp2_mul(t, k, yQ);
   fp2_sub(l2, l2, t);
-  fp12_mul_line(f, l0, l1, l2);
+  sp.mul_line(f, l0, l1, l2);
   g2 Q;
   Q.X = xQ;
   Q.Y = yQ;
@@ -949,7 +957,8 @@ EDV_HD void twist_frob(fp2& xo, fp2& yo, const fp2& x, const fp2& y) {
 }
 
 // f *= (Miller function of Q at P) for the optimal ate pairing; P, Q affine.
-EDV_BN_NI void miller_loop_acc(fp12& f, const fp& xP, const fp& yP, const fp2& xQ, const fp2& yQ) {
+template <class SP = LineDirect>
+EDV_BN_NI void miller_loop_acc(fp12& f, const fp& xP, const fp& yP, const fp2& xQ, const fp2& yQ, SP sp = SP()) {
   g2 T;
   T.X = xQ;
   T.Y = yQ;
@@ -958,9 +967,9 @@ EDV_BN_NI void miller_loop_acc(fp12& f, const fp& xP, const fp& yP, const fp2& x
   fp12_one(g);
   // |6x + 2| = 2^64 + kAteLoop: bits 63..0 after the leading one
   for (int bit = kAteLoopBits - 2; bit >= 0; --bit) {
-    fp12_sqr(g, g);
-    miller_dbl(g, T, xP, yP);
-    if ((kAteLoop >> bit) & 1ull) miller_add(g, T, xQ, yQ, xP, yP);
+    sp.sqr(g);
+    miller_dbl(g, T, xP, yP, sp);
+    if ((kAteLoop >> bit) & 1ull) miller_add(g, T, xQ, yQ, xP, yP, sp);
   }
   fp12_conj(g, g);  // x < 0
   fp2_neg(T.Y, T.Y);
@@ -968,8 +977,8 @@ EDV_BN_NI void miller_loop_acc(fp12& f, const fp& xP, const fp& yP, const fp2& x
   twist_frob(x1, y1, xQ, yQ);
   twist_frob(x2, y2, x1, y1);
   fp2_neg(y2, y2);
-  miller_add(g, T, x1, y1, xP, yP);
-  miller_add(g, T, x2, y2, xP, yP);
+  miller_add(g, T, x1, y1, xP, yP, sp);
+  miller_add(g, T, x2, y2, xP, yP, sp);
   fp12_mul(f, f, g);
 }
 
