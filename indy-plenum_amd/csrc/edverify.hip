@@ -1386,6 +1386,10 @@ struct edv_ctx {
   // the small keyed path reads its packed inputs straight from pinned host memory (no H2D copy
   // before the kernel); A/B switch EDV_SMALL_ZC=1
   bool small_zero_copy = getenv("EDV_SMALL_ZC") != nullptr;
+  // phase events around a single request's small kernel (edv_last_phases_ms): off unless
+  // EDV_SMALL_EVENTS=1 -- the two timestamps cost ~8 us of the round trip (119-126 against
+  // 128-134 us per engine call, profiles/r05y)
+  bool small_events = getenv("EDV_SMALL_EVENTS") != nullptr;
   uint64_t small_max = 256;  // edv_set_small_batch: keyed host-pointer chunks of at most this many requests take
                              // edv_verify_small_kernel (0 = never)
   uint32_t* d_kperm = nullptr;
@@ -1835,7 +1839,8 @@ int launch_small(edv_ctx* ctx, const void* d_sig, const void* d_kidx, const void
   if (n == 0) return 0;
   if (ctx->key_count == 0) return set_err(EDV_EINVAL, "no registered keys");
   hipEvent_t* ev = ctx->ev_sub[0];
-  HIP_TRY(hipEventRecord(ev[0], st));
+  const bool timed = ctx->small_events || !host_ok8;
+  if (timed) HIP_TRY(hipEventRecord(ev[0], st));
   uint8_t* ok8 = host_ok8 ? host_ok8 : ctx->d_ok8;
   const uint32_t kc = (uint32_t)ctx->key_count;
 #define EDV_SMALL_CASE(W)                                                                                        \
@@ -1852,16 +1857,18 @@ int launch_small(edv_ctx* ctx, const void* d_sig, const void* d_kidx, const void
   }
 #undef EDV_SMALL_CASE
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(ev[3], st));
+  if (timed) HIP_TRY(hipEventRecord(ev[3], st));
   if (!host_ok8) {
     hipLaunchKernelGGL(edv_ok_pack_kernel, dim3((uint32_t)div_up(n, kBlock)), dim3(kBlock), 0, st, ctx->d_ok8, n,
                        (unsigned long long*)d_words);
     HIP_TRY(hipGetLastError());
   }
-  ctx->last_nsub = 1;
-  ctx->last_chunk_n = n;
-  ctx->timed = true;
-  ctx->small_timed = true;
+  if (timed) {  // (an untimed launch leaves the previous launch's phases readable)
+    ctx->last_nsub = 1;
+    ctx->last_chunk_n = n;
+    ctx->timed = true;
+    ctx->small_timed = true;
+  }
   return 0;
 }
 

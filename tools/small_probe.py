@@ -41,8 +41,12 @@ for i in range(len(msgs)):
         clk = (out[9] - out[8]) / max(1, t[7]) * 100.0  # shader clock over the kernel, MHz
         rows.append([t[1], t[2], t[3], t[4], t[5], t[6] - t[4], t[7], clk * 100.0])
 lat = np.array(lat[50:]) * 1e6
+try:
+    comb_us = eng.last_phases_ms()[2] * 1e3
+except Exception:  # EDV_SMALL_NOEV=1: the small path records no phase events
+    comb_us = float("nan")
 print("key window %d: engine call n=1 p50 %.1f us p99 %.1f us; phases (comb) %.1f us" % (
-    kw, np.percentile(lat, 50), np.percentile(lat, 99), eng.last_phases_ms()[2] * 1e3))
+    kw, np.percentile(lat, 50), np.percentile(lat, 99), comb_us))
 if rows:
     med = np.median(np.array(rows[50:], dtype=np.float64), axis=0) / 100.0  # 100 MHz ticks -> us
     for n_, v in zip(names, med):
