@@ -1748,6 +1748,52 @@ PyObject* py_results_from(PyObject*, PyObject* args) {
   return ret;
 }
 
+// results_ok(ok, short, uidx, uniq) -> (results, failed): a steady-state batch's result list in
+// one pass -- results[i] = uniq[uidx[i]] when ok[i] and not short[i], else None, with the
+// indices of those failures (the caller puts InvalidSignature there).  ok / short: one byte
+// per request (0 / nonzero).
+PyObject* py_results_ok(PyObject*, PyObject* args) {
+  Py_buffer bo, bs, bu;
+  PyObject* uniq;
+  if (!PyArg_ParseTuple(args, "y*y*y*O", &bo, &bs, &bu, &uniq)) return nullptr;
+  PyObject* ret = nullptr;
+  const Py_ssize_t n = bo.len;
+  if (!PyList_CheckExact(uniq) || bs.len != n || bu.len != n * 4) {
+    PyErr_SetString(PyExc_ValueError, "results_ok: ok / short / uidx / uniq mismatch");
+  } else {
+    const uint8_t* ok = (const uint8_t*)bo.buf;
+    const uint8_t* sh = (const uint8_t*)bs.buf;
+    const uint32_t* u = (const uint32_t*)bu.buf;
+    const Py_ssize_t nu = PyList_GET_SIZE(uniq);
+    bool good = true;
+    for (Py_ssize_t i = 0; i < n && good; ++i) good = !(ok[i] && !sh[i]) || (Py_ssize_t)u[i] < nu;
+    PyObject* res = good ? PyList_New(n) : nullptr;
+    PyObject* failed = res ? PyList_New(0) : nullptr;
+    if (!good) PyErr_SetString(PyExc_ValueError, "results_ok: identifier index out of range");
+    bool fine = failed != nullptr;
+    for (Py_ssize_t i = 0; fine && i < n; ++i) {
+      const bool pass = ok[i] && !sh[i];
+      PyObject* o = pass ? PyList_GET_ITEM(uniq, u[i]) : Py_None;
+      Py_INCREF(o);
+      PyList_SET_ITEM(res, i, o);
+      if (!pass) {
+        PyObject* k = PyLong_FromSsize_t(i);
+        fine = k && PyList_Append(failed, k) == 0;
+        Py_XDECREF(k);
+      }
+    }
+    if (fine) {
+      ret = PyTuple_Pack(2, res, failed);
+    }
+    Py_XDECREF(res);
+    Py_XDECREF(failed);
+  }
+  PyBuffer_Release(&bo);
+  PyBuffer_Release(&bs);
+  PyBuffer_Release(&bu);
+  return ret;
+}
+
 // gather_u32(table, idx) -> bytearray: out[i] = table[idx[i]] (uint32 LE both), the key id of
 // every request from its identifier's (one pass; numpy's fancy indexing widens the index
 // array to intp first).  ValueError on an index past the table.
@@ -1832,6 +1878,8 @@ PyMethodDef kMethods[] = {
     {"repack_spans", py_repack_spans, METH_VARARGS,
      "repack_spans(buf, spans) -> (msgs, off): a staged scan's messages laid out contiguously with offsets"},
     {"gather_u32", py_gather_u32, METH_VARARGS, "gather_u32(table, idx) -> bytearray: table[idx[i]] (uint32)"},
+    {"results_ok", py_results_ok, METH_VARARGS,
+     "results_ok(ok, short, uidx, uniq) -> (results, failed indices) of a steady-state batch"},
     {"results_from", py_results_from, METH_VARARGS,
      "results_from(codes_u8, uidx_u32, uniq) -> list: uniq[uidx[i]] where codes[i] == 1, else None"},
     {"gather_items", py_gather_items, METH_VARARGS,

@@ -64,9 +64,10 @@ try:  # native batch scan (csrc/hostpack.cpp): authenticate()'s host steps for a
 except ImportError:  # pragma: no cover - the per-message path below
     _scan_batch = _gather_items = _results_from = None
 try:
-    from ._hostpack import gather_u32 as _gather_u32, pack_range as _pack_range, repack_spans as _repack_spans
+    from ._hostpack import (gather_u32 as _gather_u32, pack_range as _pack_range, repack_spans as _repack_spans,
+                            results_ok as _results_ok)
 except ImportError:  # pragma: no cover
-    _pack_range = _repack_spans = _gather_u32 = None
+    _pack_range = _repack_spans = _gather_u32 = _results_ok = None
 
 try:  # native packing (csrc/hostpack.cpp)
     from ._hostpack import pack_sm as _pack_sm, pack_split64 as _pack_split64
@@ -643,12 +644,11 @@ class GpuAuthMixin:
         ok = np.concatenate([np.asarray(eng.verify_collect(h), bool) for h in handles])
         t4 = perf_counter()
         del handles, sig_a, msg_a
-        ok &= np.frombuffer(short, np.uint8) == 0
         g.stats["batches"] += 1
         g.stats["batch_items"] += n
         g.stats["keyed_items"] += n
-        results = _results_from(ok.view(np.uint8).tobytes(), uidx_b, uniq)
-        for i in np.flatnonzero(~ok).tolist():
+        results, failed = _results_ok(ok, short, uidx_b, uniq)
+        for i in failed:
             results[i] = InvalidSignature()
         t5 = perf_counter()
         # where this batch's time went (bench.py end_to_end.in_batch_ms)

@@ -113,7 +113,6 @@ class EdVerifyEngine:
             raise EdVerifyUnavailable(lib.edv_last_error().decode(errors="replace"))
         self._lib = lib
         self._ctx = ctypes.c_void_p(ctx)
-        self._one = None  # verify_one_keyed's ctypes arguments
         self.device = device
 
     # ------------------------------------------------------------- lifecycle
@@ -486,13 +485,8 @@ class EdVerifyEngine:
         without the numpy packing around it."""
         if len(sig64) != 64:
             raise ValueError("sig64 must be 64 bytes")
-        one = self._one
-        if one is None:
-            one = self._one = (ctypes.c_uint32(0), (ctypes.c_uint64 * 2)(0, 0), ctypes.c_uint8(0))
-        kid, off, bits = one
-        kid.value = int(key_id)
-        off[1] = len(msg)
-        bits.value = 0
+        # per-call argument objects (a couple of microseconds; safe from any thread)
+        kid, off, bits = ctypes.c_uint32(int(key_id)), (ctypes.c_uint64 * 2)(0, len(msg)), ctypes.c_uint8(0)
         check(self._lib.edv_verify_batch_keyed(self._ctx, bytes(sig64), ctypes.byref(kid), bytes(msg) if msg else None,
                                                off, 1, ctypes.byref(bits)))
         return bool(bits.value & 1)

@@ -624,3 +624,25 @@ def test_small_batch_kernel_matches_batch_path(gpu_engine, oracle, w):
         gpu_engine.set_small_batch(256)
         gpu_engine.keys_reset()
         gpu_engine.keys_set_window(10)
+
+
+def test_verify_one_keyed_matches_batch(gpu_engine):
+    """EdVerifyEngine.verify_one_keyed (one authenticate() that missed the verify-ahead cache:
+    bytes in, the small kernel, its verdict byte straight into pinned host memory) gives the
+    batch path's verdict on every golden edge item and on unregistered ids."""
+    e = load_npz("ed25519_edge.npz")
+    try:
+        gpu_engine.keys_reset()
+        gpu_engine.keys_set_window(14)
+        first = gpu_engine.keys_add(e["pk"])
+        kidx = np.arange(first, first + len(e["pk"]), dtype=np.uint32)
+        kidx[5::11] = gpu_engine.keys_count() + 1  # unregistered
+        want = e["expect"].astype(bool).copy()
+        want[5::11] = False
+        msgs, off = bytes(e["msgs"]), e["off"]
+        for i in range(len(kidx)):
+            got = gpu_engine.verify_one_keyed(bytes(e["sig"][i]), int(kidx[i]), msgs[int(off[i]):int(off[i + 1])])
+            assert got == bool(want[i]), i
+    finally:
+        gpu_engine.keys_reset()
+        gpu_engine.keys_set_window(10)

@@ -251,3 +251,14 @@ def test_gather_u32():
     assert bytes(H.gather_u32(t, b"")) == b""
     with pytest.raises(ValueError):
         H.gather_u32(t, struct.pack("<I", 3))
+
+
+def test_results_ok():
+    """results_ok: identifiers where ok and not short, None elsewhere, with the failed indices."""
+    ok, short = bytes([1, 0, 1, 1]), bytes([0, 0, 1, 0])
+    res, failed = H.results_ok(ok, short, struct.pack("<4I", 1, 9, 0, 0), ["a", "b"])
+    assert res == ["b", None, None, "a"] and failed == [1, 2]
+    with pytest.raises(ValueError):
+        H.results_ok(bytes([1]), bytes([0]), struct.pack("<I", 5), ["a"])
+    with pytest.raises(ValueError):
+        H.results_ok(bytes([1, 1]), bytes([0]), struct.pack("<2I", 0, 0), ["a"])
