@@ -257,6 +257,36 @@ enum WRes { kOk = 0, kFail = 1, kDefer = 2 };
 
 WRes wser_obj(PyObject* o, int level, PyObject* ignore, OutBuf& out);
 
+// A dict's key table read directly on CPython 3.10's combined-table layout
+// (Objects/dict-common.h): the scan's workers walk a request's entries without a
+// PyDict_Next call per key, and the prefetch pipeline walks ahead with it.  nullptr
+// (and n = 0) for other layouts; elsewhere the workers use PyDict_Next.
+#if PY_VERSION_HEX >= 0x030A0000 && PY_VERSION_HEX < 0x030B0000
+struct DkEntry {
+  Py_hash_t h;
+  PyObject *k, *v;
+};
+struct DkHead {  // Objects/dict-common.h, 3.10
+  Py_ssize_t refcnt, size;
+  void* lookup;
+  Py_ssize_t usable, nentries;
+  char idx[1];
+};
+inline const DkEntry* dk_entries(PyObject* o, Py_ssize_t& n) {
+  n = 0;
+  if (Py_TYPE(o) != &PyDict_Type) return nullptr;
+  const PyDictObject* d = (const PyDictObject*)o;
+  if (d->ma_values) return nullptr;  // split table
+  const DkHead* k = (const DkHead*)d->ma_keys;
+  const Py_ssize_t sz = k->size;
+  const int ix = sz <= 0xff ? 1 : sz <= 0xffff ? 2 : sz <= 0xffffffffLL ? 4 : 8;
+  n = k->nentries;
+  return (const DkEntry*)(k->idx + sz * ix);
+}
+#define EDV_HAVE_DK 1
+#endif
+bool g_scan_direct = true;  // EDV_SCAN_DIRECT=0: PyDict_Next instead (A/B); set per scan call
+
 bool w_str_eq(PyObject* a, PyObject* b) {  // canonical kinds: equal strings have equal kinds
   const Py_ssize_t n = PyUnicode_GET_LENGTH(a);
   return PyUnicode_KIND(a) == PyUnicode_KIND(b) && n == PyUnicode_GET_LENGTH(b) &&
@@ -303,13 +333,12 @@ WRes wser_dict(PyObject* d, int level, PyObject* ignore, OutBuf& out, PyObject* 
     big.resize((size_t)nd);
     kv = big.data();
   }
-  Py_ssize_t nk = 0, pos = 0;
-  PyObject *k, *v;
+  Py_ssize_t nk = 0;
   bool one_byte = true;
-  while (PyDict_Next(d, &pos, &k, &v)) {
+  const auto take = [&](PyObject* k, PyObject* v) -> bool {  // false: a non-str key
     if (!PyUnicode_CheckExact(k)) {
       if (top) found[0] = found[1] = nullptr;
-      return kFail;  // as ser_dict
+      return false;  // as ser_dict
     }
     if (top) {
       if (k == top[0] || w_str_eq(k, top[0]))
@@ -317,9 +346,24 @@ WRes wser_dict(PyObject* d, int level, PyObject* ignore, OutBuf& out, PyObject* 
       else if (k == top[1] || w_str_eq(k, top[1]))
         found[1] = v;
     }
-    if (level == 0 && w_ignored(k, ignore)) continue;
+    if (level == 0 && w_ignored(k, ignore)) return true;
     one_byte = one_byte && PyUnicode_KIND(k) == PyUnicode_1BYTE_KIND;
     kv[nk++] = KV{k, v};
+    return true;
+  };
+#ifdef EDV_HAVE_DK
+  Py_ssize_t ne = 0;
+  const DkEntry* ent = g_scan_direct ? dk_entries(d, ne) : nullptr;
+  if (ent) {
+    for (Py_ssize_t e = 0; e < ne; ++e)  // insertion order, deleted entries (value NULL) skipped
+      if (ent[e].v && !take(ent[e].k, ent[e].v)) return kFail;
+  } else
+#endif
+  {
+    Py_ssize_t pos = 0;
+    PyObject *k, *v;
+    while (PyDict_Next(d, &pos, &k, &v))
+      if (!take(k, v)) return kFail;
   }
   if (!one_byte) return kDefer;  // PyUnicode_Compare order for wider kinds: ser_dict
   if (nk <= kSmall) {  // insertion sort: a request's dicts have a handful of keys
@@ -867,30 +911,6 @@ inline void pf(const void* p) { __builtin_prefetch(p); }
 inline void pf_lines(const void* p, int n) {
   for (int k = 0; k < n; ++k) __builtin_prefetch((const char*)p + 64 * k);
 }
-#if PY_VERSION_HEX >= 0x030A0000 && PY_VERSION_HEX < 0x030B0000
-struct DkEntry {
-  Py_hash_t h;
-  PyObject *k, *v;
-};
-struct DkHead {  // Objects/dict-common.h, 3.10
-  Py_ssize_t refcnt, size;
-  void* lookup;
-  Py_ssize_t usable, nentries;
-  char idx[1];
-};
-inline const DkEntry* dk_entries(PyObject* o, Py_ssize_t& n) {
-  n = 0;
-  if (Py_TYPE(o) != &PyDict_Type) return nullptr;
-  const PyDictObject* d = (const PyDictObject*)o;
-  if (d->ma_values) return nullptr;  // split table
-  const DkHead* k = (const DkHead*)d->ma_keys;
-  const Py_ssize_t sz = k->size;
-  const int ix = sz <= 0xff ? 1 : sz <= 0xffff ? 2 : sz <= 0xffffffffLL ? 4 : 8;
-  n = k->nentries;
-  return (const DkEntry*)(k->idx + sz * ix);
-}
-#define EDV_HAVE_DK 1
-#endif
 inline void prefetch_ahead(PyObject** items, Py_ssize_t i, Py_ssize_t b) {
   if (i + 10 < b) pf(items[i + 10]);
   if (i + 7 < b) {
@@ -1308,6 +1328,8 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
   // turns it off
   const char* pf_env = getenv("EDV_SCAN_PREFETCH");
   const bool prefetch = !(pf_env && pf_env[0] == '0');
+  const char* dir_env = getenv("EDV_SCAN_DIRECT");
+  g_scan_direct = !(dir_env && dir_env[0] == '0');
   run_chunks(n, t, [&](int w, Py_ssize_t a, Py_ssize_t b) {
     ScanBuf& sb = bufs[(size_t)w];
     WorkerIdrs& tab = tabs[(size_t)w];

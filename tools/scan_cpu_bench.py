@@ -33,10 +33,10 @@ for i in range(n):
     reqs.append(json.loads(json.dumps(r)))
 out = [bytearray(), bytearray()]
 for rep in range(reps):
-    if os.environ.get("AB"):  # alternate the scan's software prefetch off / on
-        os.environ["EDV_SCAN_PREFETCH"] = "1" if rep % 2 else "0"
+    ab = os.environ.get("AB")  # alternate a scan switch off / on (AB=1: EDV_SCAN_PREFETCH; else its name)
+    if ab:
+        os.environ["EDV_SCAN_PREFETCH" if ab == "1" else ab] = "1" if rep % 2 else "0"
     t0 = time.perf_counter()
     H.scan_batch_u(reqs, ["signature"], threads, out, 96)
-    print("scan %d requests, %d threads%s: %.2f ms" % (
-        n, threads, " prefetch" if os.environ.get("EDV_SCAN_PREFETCH", "1") != "0" else "", (time.perf_counter() - t0) * 1e3),
-        flush=True)
+    flags = "".join(" %s=%s" % (k[9:].lower(), os.environ.get(k, "1")) for k in ("EDV_SCAN_PREFETCH", "EDV_SCAN_DIRECT"))
+    print("scan %d requests, %d threads%s: %.2f ms" % (n, threads, flags, (time.perf_counter() - t0) * 1e3), flush=True)
