@@ -239,7 +239,7 @@ def time_e2e(eng, reqs, idrs, vks):
                     "+ D2H; the rest of value's time is per-identifier key resolution and the result list. "
                     "in_batch_ms: the median batch's own phases on the streamed path (scan with the pack deferred; "
                     "keys_and_ids = verkeys per distinct identifier + key ids per request; pack_and_submit = per "
-                    "2^18 chunk the pack into pinned memory and the async library call; collect_wait = waiting "
+                    "2^17-request chunk the pack into pinned memory and the async library call; collect_wait = waiting "
                     "for the last chunks' copies and kernels; verdicts = masks + the result list). "
                     "value = the median of 3 batches after the first full-size one (steady state); first_batch_* "
                     "= that first batch (buffers allocated). single_authenticate_us: authenticate() of one "
