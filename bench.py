@@ -17,7 +17,9 @@ signers, all valid.  `--config c2` adds the 10% corrupted / non-canonical /
 small-order mix of configs[2].  Signatures are made on the GPU by the library's
 own deterministic signer (bit-exact with libsodium, tests/test_gpu_parity.py).
 
-Usage: python bench.py [--gpus N --steps K --warmup W]   (N > 1 via torch.distributed.run)
+Usage: python bench.py [--gpus N --steps K --warmup W]
+  N > 1: either under torch.distributed.run (one rank per GPU, WORLD_SIZE set), or bare --
+  the process then starts the N ranks itself (launch_ranks) before anything touches the GPU.
 """
 import argparse
 import ctypes
@@ -26,11 +28,74 @@ import os
 import sys
 import time
 
-import numpy as np
-import torch
-import torch.distributed as dist
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
+
+
+def _gpus_arg(argv):
+    """--gpus N from the command line without argparse's full parse (stdlib only)."""
+    for i, a in enumerate(argv):
+        if a == "--gpus" and i + 1 < len(argv):
+            return int(argv[i + 1])
+        if a.startswith("--gpus="):
+            return int(a.split("=", 1)[1])
+    return 1
+
+
+def launch_ranks(n, argv, poll_s=0.2):
+    """`python bench.py --gpus N` with no launcher around it: start N child
+    ranks of this script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1
+    / a free MASTER_PORT in their environment, one per GPU), relay their output
+    (rank 0 prints the JSON line), and return the worst child exit code.  This
+    process imports neither torch nor the engine and never touches the GPU; if
+    one rank fails, the others are terminated rather than left waiting in a
+    collective."""
+    import signal
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL across the rank processes
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rcs = [None] * n
+    try:
+        while any(rc is None for rc in rcs):
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    rcs[i] = p.poll()
+            if any(rc not in (None, 0) for rc in rcs):  # one rank failed: the rest would wait forever
+                for i, p in enumerate(procs):
+                    if rcs[i] is None:
+                        p.send_signal(signal.SIGTERM)
+                for i, p in enumerate(procs):
+                    if rcs[i] is None:
+                        try:
+                            rcs[i] = p.wait(timeout=30)
+                        except subprocess.TimeoutExpired:
+                            p.kill()
+                            rcs[i] = p.wait()
+                break
+            time.sleep(poll_s)
+    except KeyboardInterrupt:
+        for p in procs:
+            p.kill()
+        raise
+    bad = [rc for rc in rcs if rc]
+    return max(bad, key=abs) if bad else 0
+
+
+if __name__ == "__main__" and "WORLD_SIZE" not in os.environ and _gpus_arg(sys.argv[1:]) > 1:
+    sys.exit(launch_ranks(_gpus_arg(sys.argv[1:]), sys.argv[1:]))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
 sys.path.insert(0, os.path.join(ROOT, "indy-plenum_amd"))
 
 from plenum_amd import EdVerifyEngine, pack_messages  # noqa: E402
@@ -82,6 +147,7 @@ def parse():
                          "sorted: requests grouped by signer (A/B of the comb's gather locality)")
     ap.add_argument("--key-sort", choices=["auto", "on", "off"], default="auto",
                     help="comb lanes in key-sorted order (edv_set_key_sort; auto = sub-batches >= 4096)")
+    ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--e2e-devices", type=int, default=1,
                     help="1: also run the end-to-end leg through MultiEngine over 1/2/4/8 of the visible devices "
                          "(one node process; rank 0 at world 1)")
@@ -376,6 +442,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.launch_check:  # the launcher's CPU test: what this rank was given, before any GPU call
+        print(json.dumps({"rank": rank, "local_rank": local, "world": world, "gpus": args.gpus,
+                          "master": "%s:%s" % (os.environ.get("MASTER_ADDR"), os.environ.get("MASTER_PORT")),
+                          "torch_cuda_initialized": bool(torch.cuda.is_initialized())}), flush=True)
+        return
+    assert world == args.gpus, "WORLD_SIZE=%d ranks but --gpus %d" % (world, args.gpus)
     if args.same_device:  # rehearsal of the N > 1 logic on a one-GPU box (gloo)
         local = 0
     torch.cuda.set_device(local)

@@ -621,7 +621,8 @@ __global__ __launch_bounds__(kBlock) void edv_ok_pack_kernel(const uint8_t* __re
 // with LDS cursors.  Order within a key is arbitrary (verdicts are per
 // request).
 constexpr uint32_t kSortBlocks = 256, kSortThreads = 1024;
-constexpr uint64_t kCompactBytes = 256 << 10;  // host_submit: small chunks in one pinned block, one copy
+constexpr uint64_t kCompactBytes = 256 << 10;
+constexpr size_t kMaxPending = 64;  // uncollected edv_verify_submit tickets per context  // host_submit: small chunks in one pinned block, one copy
 constexpr uint32_t kSortMaxBins = 16384;  // 64 KiB of LDS per block
 __device__ __forceinline__ void sort_range(uint64_t n, uint64_t& lo, uint64_t& hi) {
   const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
@@ -2066,8 +2067,11 @@ static int host_submit(edv_ctx* ctx, bool keyed, const uint8_t* sig, uint64_t si
   ctx->last_direct = (sig_direct ? 1 : 0) | (key_direct ? 2 : 0) | (msg_direct ? 4 : 0) | (off_direct ? 8 : 0);
   ctx->last_h2d_bytes = 0;
   const uint64_t ticket = ctx->next_ticket++;
-  // submissions never collected (a caller that went away) are forgotten after a while
-  while (ctx->pending.size() >= 64) ctx->pending.erase(ctx->pending.begin());
+  // at most kMaxPending uncollected submissions: a caller that submits more before collecting gets an
+  // error here rather than a silently dropped verdict set at collect time
+  if (ctx->pending.size() >= kMaxPending)
+    return set_err(EDV_EINVAL, "%llu submissions outstanding: collect before submitting more",
+                   (unsigned long long)ctx->pending.size());
   ctx->pending.push_back(edv_ctx::Pending{ticket, n, std::vector<uint8_t>((size_t)((n + 7) / 8), 0)});
   // a source the copy engine reads: the caller's pinned memory, or the slot's staging after a CPU copy
   auto source = [&](bool direct, edv_ctx::Buf& stage, const uint8_t* src, uint64_t bytes, bool threaded,
@@ -2509,13 +2513,15 @@ int edv_verify_staged(edv_ctx* ctx, int keyed, const uint8_t* keys, uint64_t slo
     if (msg_start[i] > msg_end[i] || msg_end[i] > cap - msg_base)
       return set_err(EDV_EINVAL, "message span %llu outside staging", (unsigned long long)i);
   const uint64_t key_bytes = keyed ? 4 : 32, nwords = div_up(n, 64);
+  // submissions still holding the slot-0 buffers finish (and hand over their verdicts) before the
+  // buffers below may be reallocated
+  for (int sl = 0; sl < edv_ctx::kSlots; ++sl)
+    if ((r = drain_slot(ctx, sl))) return r;
   if ((r = ensure_pinned(ctx->h_key[0], key_bytes * n)) || (r = ensure_pinned(ctx->h_off[0], 16 * n)) ||
       (r = ensure(ctx->d_key[0], key_bytes * n)) || (r = ensure(ctx->d_spans, 16 * n)) ||
       (r = ensure(ctx->b_sig, 64 * n)) || (r = ensure(ctx->d_bits[0], 8 * nwords)) ||
       (r = ensure_pinned(ctx->h_bits[0], 8 * nwords)))
     return r;
-  for (int sl = 0; sl < edv_ctx::kSlots; ++sl)  // submissions still holding the slot-0 buffers
-    if ((r = drain_slot(ctx, sl))) return r;
   memcpy(ctx->h_key[0].p, keys, key_bytes * n);
   memcpy(ctx->h_off[0].p, msg_start, 8 * n);
   memcpy((char*)ctx->h_off[0].p + 8 * n, msg_end, 8 * n);

@@ -951,7 +951,9 @@ inline void prefetch_ahead(PyObject** items, Py_ssize_t i, Py_ssize_t b) {
 template <class F>
 void run_chunks(Py_ssize_t n, int t, F&& f, Py_ssize_t chunk = kScanChunk) {
   if (t <= 1 || n <= chunk) {
-    if (n) f(0, (Py_ssize_t)0, n);
+    // serially, but still chunk by chunk: callers may key per-chunk state on a / chunk (the staged
+    // scan publishes one slot_done flag per kStageChunk)
+    for (Py_ssize_t a = 0; a < n; a += chunk) f(0, a, std::min(n, a + chunk));
     return;
   }
   std::atomic<Py_ssize_t> next{0};

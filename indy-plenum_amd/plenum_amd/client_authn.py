@@ -110,6 +110,7 @@ KEY_STORE_BYTES = 32 << 30  # HBM for key tables: the window is the widest that 
 _SIG_SLOT = 96  # edverify.h EDV_SIG_SLOT96: signatures as base58 text, decoded on the GPU
 _PINNED_MIN_BATCH = 4096  # smaller batches keep the bytearrays (the library stages them cheaply)
 _STREAM_CHUNK = 1 << 17  # requests per streamed submit: 2^17 beat 2^18 and 2^16 by 2-3 % (profiles/r06c)
+_STREAM_WINDOW = 16  # streamed submits in flight before the oldest is collected (edverify.hip kMaxPending = 64)
 _STAGE_MIN_BATCH = 1 << 16  # batches staged while scanned (edv_stage_put from the scan's workers)
 
 
@@ -635,15 +636,18 @@ class GpuAuthMixin:
         sig_a = np.frombuffer(sig_o, np.uint8, count=slot * n).reshape(-1, slot)
         msg_a = np.frombuffer(msg_o, np.uint8, count=mlen)
         t2 = perf_counter()
-        handles = []
+        handles, oks = [], []
         for c0 in range(0, n, _STREAM_CHUNK):
             c1 = min(n, c0 + _STREAM_CHUNK)
             _pack_range(handle, c0, c1)
+            if len(handles) - len(oks) >= _STREAM_WINDOW:  # bounded in flight (the library holds 64 tickets)
+                oks.append(np.asarray(eng.verify_collect(handles[len(oks)]), bool))
             handles.append(eng.verify_submit(sig_a[c0:c1], kid[c0:c1], msg_a, off_a[c0:c1 + 1], True, slot))
         t3 = perf_counter()
-        ok = np.concatenate([np.asarray(eng.verify_collect(h), bool) for h in handles])
+        oks += [np.asarray(eng.verify_collect(h), bool) for h in handles[len(oks):]]
+        ok = np.concatenate(oks) if oks else np.zeros(0, bool)
         t4 = perf_counter()
-        del handles, sig_a, msg_a
+        del handles, oks, sig_a, msg_a
         g.stats["batches"] += 1
         g.stats["batch_items"] += n
         g.stats["keyed_items"] += n

@@ -102,11 +102,17 @@ class OracleEngine:
 
     def verify_submit(self, sig, keys, msgs, msg_off, keyed, sig_slot=64):
         self.submits = getattr(self, "submits", 0) + 1
+        inflight = getattr(self, "in_flight", 0) + 1
+        if inflight > 64:  # edverify.hip kMaxPending: the library refuses a 65th uncollected ticket
+            raise RuntimeError("64 submissions outstanding")
+        self.in_flight = inflight
+        self.max_in_flight = max(getattr(self, "max_in_flight", 0), inflight)
         if keyed:
             return self.verify_batch_keyed(sig, keys, msgs, msg_off, sig_slot=sig_slot)
         return self.verify_batch(sig, keys, msgs, msg_off, sig_slot=sig_slot)
 
     def verify_collect(self, handle):
+        self.in_flight -= 1
         return handle
 
     def verify_batch(self, sig64, pk32, msgs, msg_off, sig_slot=64):

@@ -664,3 +664,47 @@ def test_staged_batch_equals_whole(oracle, monkeypatch):
     assert [_outcome(r) for r in small.authenticate_batch(batch)] == \
         [_outcome(r) for r in ref.authenticate_batch(batch)]
     assert small.engine.staged_calls == 0
+
+
+def test_staged_batch_one_scan_thread(oracle, monkeypatch):
+    """The staged scan with scan_threads=1 over more than one 4k-item stage
+    chunk: the serial scan still publishes every chunk's slots (run_chunks
+    walks the chunks in order instead of one call over the whole batch), so
+    items past the first chunk are verified against their own slots."""
+    from engine_double import StagingOracleEngine
+    from plenum_amd import client_authn as CA
+    idrs, vks, msgs = _signed(3, 9000)
+    monkeypatch.setattr(CA, "_STAGE_MIN_BATCH", 1000)
+    monkeypatch.setattr(CA, "_PINNED_MIN_BATCH", 1000)
+    eng = StagingOracleEngine(oracle)
+    a = GpuAuthNr(engine=eng, stage=True, scan_threads=1)
+    for i, v in zip(idrs, vks):
+        a.addIdr(i, v)
+    a.keys_settle()
+    batch = [dict(m) for m in msgs]
+    batch[8500]["reqId"] += 1  # forged, in the third stage chunk
+    got = a.authenticate_batch(batch)
+    assert eng.staged_calls == 1
+    assert [_outcome(r) for r in got] == [m["identifier"] if i != 8500 else ("InvalidSignature", (), None)
+                                          for i, m in enumerate(msgs)]
+
+
+def test_streamed_batch_bounded_in_flight(oracle, monkeypatch):
+    """More streamed chunks than the in-flight window: the oldest submissions
+    are collected before new ones go out (the library refuses a 65th
+    uncollected ticket), and the verdicts stay in request order."""
+    from plenum_amd import client_authn as CA
+    idrs, vks, msgs = _signed(3, 5000)
+    monkeypatch.setattr(CA, "_STREAM_CHUNK", 128)
+    monkeypatch.setattr(CA, "_STREAM_WINDOW", 4)
+    eng = OracleEngine(oracle)
+    a = GpuAuthNr(engine=eng)
+    for i, v in zip(idrs, vks):
+        a.addIdr(i, v)
+    a.keys_settle()
+    batch = [dict(m) for m in msgs]
+    batch[4321]["reqId"] += 1
+    got = a.authenticate_batch(batch)
+    assert eng.max_in_flight <= 4
+    assert [_outcome(r) for r in got] == [m["identifier"] if i != 4321 else ("InvalidSignature", (), None)
+                                          for i, m in enumerate(msgs)]

@@ -47,3 +47,24 @@ def test_bench_two_ranks_one_gpu():
     # the primary-PREPARE rule decides, checked across the two ranks' unioned ballots
     assert d["tally"]["keys_below_prepare_quorum"] > 0 and d["tally"]["keys_below_commit_quorum"] > 0
     assert d["tally"]["keys_decided_by_primary_rule"] > 0
+
+
+def test_bench_gpus_2_without_launcher():
+    """The driver's bare command form: `python bench.py --gpus 2` starts its two
+    ranks itself (bench.launch_ranks); both run the HIP engine (gloo, one GPU),
+    the line reports n_gpus == 2 and the all-gathered bitmask is exact."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo", "--same-device",
+           "--requests", "131072", "--signers", "64", "--key-window", "10", "--steps", "2", "--warmup", "1",
+           "--no-cpu", "--general-steps", "0", "--dropin-steps", "0", "--e2e-n", "0", "--e2e-c0", "0"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="4")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=ROOT, env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-8000:])
+    lines = [x for x in r.stdout.splitlines() if x.startswith('{"metric')]
+    assert len(lines) == 1  # rank 0 only
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["requests_per_gpu"] == 131072
+    p = d["parity"]
+    assert p["mismatches_vs_construction"] == 0 and p["accepted"] == p["expected"] == 2 * 131072
+    assert p["accepted_in_gathered_bitmask"] == 2 * 131072
+    assert d["collective"]["all_gather_bitmask_ms"] > 0
