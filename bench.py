@@ -147,6 +147,9 @@ def parse():
                          "sorted: requests grouped by signer (A/B of the comb's gather locality)")
     ap.add_argument("--key-sort", choices=["auto", "on", "off"], default="auto",
                     help="comb lanes in key-sorted order (edv_set_key_sort; auto = sub-batches >= 4096)")
+    ap.add_argument("--drain-n", type=int, default=40,
+                    help="drains of the end_to_end.node_drain leg (100 REQUESTs + 24 BATCHes of PROPAGATEs each; "
+                         "0 = skip)")
     ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--e2e-devices", type=int, default=1,
                     help="1: also run the end-to-end leg through MultiEngine over 1/2/4/8 of the visible devices "
@@ -310,6 +313,103 @@ def time_e2e(eng, reqs, idrs, vks):
                     "value = the median of 3 batches after the first full-size one (steady state); first_batch_* "
                     "= that first batch (buffers allocated). single_authenticate_us: authenticate() of one "
                     "request not in the verdict cache (300 calls after 30 warm-up)"}
+
+
+def time_node_drain(eng, reqs, idrs, vks, drains=40, per_drain=100, n_nodes=25, ref_drains=16):
+    """end_to_end.node_drain: the path a Plenum node actually runs
+    (plenum_amd/nodeloop.py restates it).  Per drain of an n = 25 pool: 100
+    client REQUESTs on the client stack and, on the node stack, 24 BATCH
+    messages (one per other node) each wrapping that node's PROPAGATEs of the
+    100 requests.  The stacks are the verify-ahead ones (batching.py
+    verify_ahead_stack): processReceived prefetches the drain's requests in one
+    GPU batch (native scan, one copy per distinct text) and hands the decoded
+    objects to the reference loop, which calls authenticate() once per REQUEST
+    and once per PROPAGATE (node.py:2294-2314, BATCH entries via
+    unpackNodeMsg, node.py:1333-1337): 2,500 calls per drain, each a
+    verdict-cache hit.  Beside it, the reference loop over the same drains on
+    one core (oracle/ref_authn_port.py --drain: json per message, the
+    reference authenticate() over libsodium), as a child process."""
+    import subprocess
+    import tempfile
+    from plenum_amd.batching import verify_ahead_stack
+    from plenum_amd.client_authn import GpuAuthNr
+    from plenum_amd.nodeloop import NodeCounters, Stack, drain_texts
+    a = GpuAuthNr(engine=eng)
+    for idr, vk in zip(idrs, vks):
+        a.addIdr(idr, vk)
+    a.keys_settle()
+    warm = 3
+    need = (drains + warm) * per_drain
+    assert len(reqs) >= need, (len(reqs), need)
+    texts = [drain_texts(reqs[d * per_drain:(d + 1) * per_drain], n_nodes) for d in range(drains + warm)]
+    nc = NodeCounters()
+    ns = verify_ahead_stack(Stack, a)(a, "node", nc)
+    cs = verify_ahead_stack(Stack, a)(a, "client", nc)
+    per = []
+    for d, (client, node) in enumerate(texts):
+        if d == warm:
+            nc.authenticated = nc.rejected = nc.messages = 0
+            st0 = dict(a.stats)
+            t0 = time.perf_counter()
+        td = time.perf_counter()
+        ns.rxMsgs.extend(node)
+        cs.rxMsgs.extend(client)
+        ns.processReceived(100)  # node stack first: its drain is the one that sees each request first
+        cs.processReceived(100)
+        if d >= warm:
+            per.append(time.perf_counter() - td)
+    el = time.perf_counter() - t0
+    st1 = dict(a.stats)
+    calls = nc.authenticated + nc.rejected
+    rx = drains * (n_nodes - 1 + per_drain)
+    # authenticate() alone on the node thread: a drain's PROPAGATE-shaped request dicts, prefetched
+    last = [json.loads(json.dumps(r)) for r in reqs[:per_drain]]
+    a.prefetch(last)
+    msgs = [json.loads(json.dumps(r)) for r in last] * (n_nodes - 1)
+    lat = []
+    for k in range(0, len(msgs), 100):
+        tk = time.perf_counter()
+        for m in msgs[k:k + 100]:
+            a.authenticate(m)
+        lat.append((time.perf_counter() - tk) / 100 * 1e6)
+    out = {"value": calls / el, "unit": "authenticate() calls/s (node thread, one process)",
+           "requests_per_s": drains * per_drain / el, "rx_entries_per_s": rx / el,
+           "drains": drains, "per_drain": {"requests": per_drain, "nodes": n_nodes, "rx_entries": n_nodes - 1 + per_drain,
+                                           "authenticate_calls": calls // drains},
+           "accepted": nc.authenticated, "rejected": nc.rejected,
+           "us_per_authenticate_in_loop": el / calls * 1e6,
+           "ms_per_drain": {"p50": float(np.percentile(per, 50)) * 1e3, "max": float(max(per)) * 1e3},
+           "node_thread_us_per_authenticate": {"p50": float(np.percentile(lat, 50)), "mean": float(np.mean(lat))},
+           "gpu_batches_per_drain": (st1["batches"] - st0["batches"]) / drains,
+           "single_verifies": st1["single_verifies"] - st0["single_verifies"],
+           "cache_hits": st1["cache_hits"] - st0["cache_hits"],
+           "prefetched": st1["prefetched"] - st0["prefetched"]}
+    # the reference loop over the same drains, one core
+    if ref_drains:
+        with tempfile.NamedTemporaryFile("w", suffix=".json", delete=False) as f:
+            json.dump({"drains": [{"client": [t for t, _ in c], "node": [t for t, _ in nd]}
+                                  for c, nd in texts[warm:warm + ref_drains]],
+                       "verkeys": dict(zip(idrs, vks))}, f)
+            path = f.name
+        try:
+            r = subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "ref_authn_port.py"), path, "--drain"],
+                               capture_output=True, text=True, timeout=900)
+            if r.returncode == 0:
+                ref = json.loads(r.stdout.strip().splitlines()[-1])
+                out["reference_loop_1_core"] = ref
+                out["vs_reference_per_core"] = out["value"] / ref["authenticate_per_s"]
+            else:
+                out["reference_loop_1_core"] = {"error": r.stderr[-500:]}
+        finally:
+            os.unlink(path)
+    out["note"] = ("configs[1] requests (1,000 signers' NYMs, ~200 B signed payload) in drains of %d REQUESTs + %d "
+                   "BATCHes of PROPAGATEs (n = %d); value = authenticate() calls per second of the whole loop (decode, "
+                   "prefetch incl. the GPU batch, the node's handlers, authenticate); the scan's helper threads "
+                   "join only for batches of 2k+ items (a drain's prefetch scans its ~100 distinct texts on the "
+                   "node thread). reference_loop_1_core = the same drains through the reference's loop and "
+                   "authenticate() chain over libsodium (oracle/ref_authn_port.py --drain)" % (per_drain, n_nodes - 1,
+                                                                                            n_nodes))
+    return out
 
 
 def time_e2e_devices(eng, reqs, idrs, vks, counts):
@@ -845,6 +945,8 @@ def main():
             reqs, idrs, vks = e2e_requests(eng, m, args.signers, args.alias_len, spec=nym_spec, sig=sig_all,
                                            pks=pks)
             e2e["configs1"] = time_e2e(eng, reqs, idrs, vks)
+            if args.drain_n > 0:
+                e2e["node_drain"] = time_node_drain(eng, reqs, idrs, vks, drains=args.drain_n)
             if args.e2e_devices:
                 ndev = torch.cuda.device_count()
                 counts = [k for k in (1, 2, 4, 8) if k <= ndev]

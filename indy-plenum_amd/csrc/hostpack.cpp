@@ -1886,6 +1886,162 @@ PyObject* py_gather_items(PyObject*, PyObject* args) {
                        (const char*)o.data(), (Py_ssize_t)(o.size() * 8));
 }
 
+// ------------------------------------------------------- the node's per-message path
+// Node.verifySignature calls authenticate(req) once per client REQUEST and once per PROPAGATE
+// (node.py:2294-2314), ~n times per request; with the verdicts already cached by the verify-ahead,
+// that call must cost a few microseconds.  authn_key does authenticate()'s host steps up to the
+// verkey lookup (client_authn.py:72-92) in one native call: the signature / identifier presence
+// checks, b58decode(signature) and the signing serialization, returned as crypto_sign_open's input
+// sm = sig || ser (nacl_wrappers.py:108) -- the verdict cache's key together with the verkey's
+// bytes.  None whenever the reference would raise (or the bytes need Python): the caller then
+// takes the per-message Python path, which raises the reference's exception.
+
+PyObject* g_key_sig = nullptr;  // interned "signature" / "identifier"
+PyObject* g_key_idr = nullptr;
+
+bool intern_keys() {
+  if (!g_key_sig) g_key_sig = PyUnicode_InternFromString("signature");
+  if (!g_key_idr) g_key_idr = PyUnicode_InternFromString("identifier");
+  return g_key_sig && g_key_idr;
+}
+
+// authn_key(msg, ignore) -> (identifier, sm) | None
+PyObject* py_authn_key(PyObject*, PyObject* args) {
+  PyObject *msg, *ignore;
+  if (!PyArg_ParseTuple(args, "OO", &msg, &ignore)) return nullptr;
+  if (!PyDict_CheckExact(msg)) Py_RETURN_NONE;
+  if (!intern_keys()) return nullptr;
+  PyObject* sv = PyDict_GetItemWithError(msg, g_key_sig);  // borrowed
+  PyObject* iv = sv ? PyDict_GetItemWithError(msg, g_key_idr) : nullptr;
+  if (!sv || !iv) {
+    PyErr_Clear();
+    Py_RETURN_NONE;  // missing (or a key compare raised): the Python path
+  }
+  if (!PyUnicode_CheckExact(sv) || !PyUnicode_IS_ASCII(sv) || PyUnicode_GET_LENGTH(sv) == 0 ||
+      !PyUnicode_CheckExact(iv) || PyUnicode_GET_LENGTH(iv) == 0)
+    Py_RETURN_NONE;
+  static std::vector<uint8_t> sig;  // the GIL serialises calls
+  if (!b58decode_raw(PyUnicode_1BYTE_DATA(sv), (size_t)PyUnicode_GET_LENGTH(sv), sig)) Py_RETURN_NONE;
+  PyObject* ign = nullptr;
+  if (ignore != Py_None) {
+    ign = PySequence_Fast(ignore, "ignore must be a sequence");
+    if (!ign) return nullptr;
+  }
+  static OutBuf ser;
+  ser.clear();
+  const bool ok = ser_obj(msg, 0, ign, ser);
+  Py_XDECREF(ign);
+  if (!ok) Py_RETURN_NONE;
+  PyObject* sm = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)(sig.size() + ser.size()));
+  if (!sm) return nullptr;
+  char* d = PyBytes_AS_STRING(sm);
+  if (!sig.empty()) memcpy(d, sig.data(), sig.size());
+  if (ser.size()) memcpy(d + sig.size(), ser.data(), ser.size());
+  PyObject* r = PyTuple_Pack(2, iv, sm);
+  Py_DECREF(sm);
+  return r;
+}
+
+inline uint64_t mix64(uint64_t h, uint64_t v) {
+  const unsigned __int128 p = (unsigned __int128)(h ^ v) * 0x9E3779B97F4A7C15ull;
+  return (uint64_t)p ^ (uint64_t)(p >> 64);
+}
+
+uint64_t hash_bytes(uint64_t h, const uint8_t* p, size_t n) {
+  size_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t v;
+    memcpy(&v, p + i, 8);
+    h = mix64(h, v);
+  }
+  uint64_t t = 0;
+  if (i < n) memcpy(&t, p + i, n - i);
+  return mix64(h, t ^ ((uint64_t)n << 56));
+}
+
+// distinct_sm(sig64, msgs, off, short, uidx, fast) -> ([item], [sm]): the items of a
+// scan_batch_u (slot 64) with a distinct (identifier, sm = sig64 || msgs[off[i]:off[i+1]]), in
+// order of first occurrence, and their sm bytes.  Items the scan left to Python (fast 0) and
+// items whose sm is shorter than 64 bytes (short 1: crypto_sign_open rejects them, no key or GPU
+// needed) are left out.  The verify-ahead batches a drain's n copies of each request with this:
+// one verify per distinct signed message.
+PyObject* py_distinct_sm(PyObject*, PyObject* args) {
+  Py_buffer bs, bm, bo, bsh, bu, bf;
+  if (!PyArg_ParseTuple(args, "y*y*y*y*y*y*", &bs, &bm, &bo, &bsh, &bu, &bf)) return nullptr;
+  struct Rel {
+    Py_buffer* b[6];
+    ~Rel() {
+      for (Py_buffer* x : b) PyBuffer_Release(x);
+    }
+  } rel{{&bs, &bm, &bo, &bsh, &bu, &bf}};
+  const Py_ssize_t n = bf.len;
+  if (bsh.len < n || bu.len < 4 * n || bo.len < 8 * (n + 1) || bs.len < 64 * n) {
+    PyErr_SetString(PyExc_ValueError, "buffer sizes do not match");
+    return nullptr;
+  }
+  const uint8_t* sig = (const uint8_t*)bs.buf;
+  const uint8_t* msg = (const uint8_t*)bm.buf;
+  const uint64_t* off = (const uint64_t*)bo.buf;
+  const uint8_t* shortv = (const uint8_t*)bsh.buf;
+  const uint32_t* uidx = (const uint32_t*)bu.buf;
+  const uint8_t* fast = (const uint8_t*)bf.buf;
+  if (n && off[n] > (uint64_t)bm.len) {
+    PyErr_SetString(PyExc_ValueError, "offsets outside the message buffer");
+    return nullptr;
+  }
+  size_t cap = 64;
+  while (cap < 2 * (size_t)n) cap <<= 1;
+  std::vector<int64_t> tab(cap, -1);
+  std::vector<uint64_t> hv;
+  std::vector<Py_ssize_t> pick;
+  hv.reserve(64);
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    if (!fast[i] || shortv[i]) continue;
+    const uint64_t m0 = off[i], ml = off[i + 1] - off[i];
+    const uint64_t h = hash_bytes(hash_bytes(0x51EDull ^ uidx[i], sig + 64 * i, 64), msg + m0, (size_t)ml);
+    size_t s = (size_t)h & (cap - 1);
+    for (;; s = (s + 1) & (cap - 1)) {
+      const int64_t j = tab[s];
+      if (j < 0) {
+        tab[s] = (int64_t)pick.size();
+        pick.push_back(i);
+        hv.push_back(h);
+        break;
+      }
+      const Py_ssize_t k = pick[(size_t)j];
+      if (hv[(size_t)j] == h && uidx[k] == uidx[i] && off[k + 1] - off[k] == ml &&
+          memcmp(sig + 64 * k, sig + 64 * i, 64) == 0 && memcmp(msg + off[k], msg + m0, (size_t)ml) == 0)
+        break;  // a copy of item k
+    }
+  }
+  PyObject* items = PyList_New((Py_ssize_t)pick.size());
+  PyObject* sms = items ? PyList_New((Py_ssize_t)pick.size()) : nullptr;
+  if (!sms) {
+    Py_XDECREF(items);
+    return nullptr;
+  }
+  for (size_t j = 0; j < pick.size(); ++j) {
+    const Py_ssize_t i = pick[j];
+    const uint64_t ml = off[i + 1] - off[i];
+    PyObject* b = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)(64 + ml));
+    PyObject* ix = b ? PyLong_FromSsize_t(i) : nullptr;
+    if (!ix) {
+      Py_XDECREF(b);
+      Py_DECREF(items);
+      Py_DECREF(sms);
+      return nullptr;
+    }
+    memcpy(PyBytes_AS_STRING(b), sig + 64 * i, 64);
+    if (ml) memcpy(PyBytes_AS_STRING(b) + 64, msg + off[i], (size_t)ml);
+    PyList_SET_ITEM(items, (Py_ssize_t)j, ix);
+    PyList_SET_ITEM(sms, (Py_ssize_t)j, b);
+  }
+  PyObject* r = PyTuple_Pack(2, items, sms);
+  Py_DECREF(items);
+  Py_DECREF(sms);
+  return r;
+}
+
 PyMethodDef kMethods[] = {
     {"scan_batch", py_scan_batch, METH_VARARGS,
      "scan_batch(msgs, ignore, threads=0, out=None) -> (fast, idrs, sig64, msgbuf, off, short): authenticate()'s "
@@ -1918,6 +2074,12 @@ PyMethodDef kMethods[] = {
     {"pack_split64", py_pack_split64, METH_VARARGS,
      "pack_split64(sigs, sers) -> (sig64, msgs, off_u64le, short): crypto_sign_open's split at byte 64"},
     {"pack_sm", py_pack_sm, METH_VARARGS, "pack_sm(sigs, sers, keys) -> (sm, off_u64le, pk32)"},
+    {"authn_key", py_authn_key, METH_VARARGS,
+     "authn_key(msg, ignore) -> (identifier, sm = b58decode(signature) || serialization) or None for the Python "
+     "path: authenticate()'s host steps before getVerkey (client_authn.py:72-92) in one call"},
+    {"distinct_sm", py_distinct_sm, METH_VARARGS,
+     "distinct_sm(sig64, msgs, off, short, uidx, fast) -> ([item], [sm]): scanned items with a distinct "
+     "(identifier, sig || ser), first occurrences, and their sm bytes"},
     {nullptr, nullptr, 0, nullptr}};
 
 PyModuleDef kModule = {PyModuleDef_HEAD_INIT, "_hostpack",

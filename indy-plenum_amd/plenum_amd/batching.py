@@ -20,6 +20,7 @@ one GPU batch (`prefetch`) covers client REQUESTs, bare PROPAGATEs and batched
 PROPAGATEs alike; the unchanged per-message authenticate() then hits the
 verdict cache."""
 import json
+from itertools import islice
 
 PROPAGATE = "PROPAGATE"
 BATCH = "BATCH"
@@ -33,7 +34,7 @@ def _decode(raw, deserialize):
         return None
 
 
-def _collect(m, deserialize, out, depth):
+def _collect(m, deserialize, out, depth, seen):
     if not isinstance(m, dict):
         return
     op = m.get("op")
@@ -41,7 +42,7 @@ def _collect(m, deserialize, out, depth):
         inner = m.get("messages")
         if depth < _MAX_BATCH_DEPTH and isinstance(inner, list):
             for raw in inner:
-                _collect(_decode(raw, deserialize), deserialize, out, depth + 1)
+                _visit(raw, deserialize, out, depth + 1, seen)
         return
     if op == PROPAGATE:
         m = m.get("request")
@@ -51,19 +52,36 @@ def _collect(m, deserialize, out, depth):
         out.append(m)
 
 
-def requests_in_drain(raw_msgs, deserialize=json.loads, limit=None):
+def _visit(raw, deserialize, out, depth, seen):
+    """Decode one entry (every entry: the node loop gets the object back from
+    the memo) and collect its requests -- once per distinct raw text: the
+    n - 1 PROPAGATEs of a request usually arrive as the same text from every
+    node, and one copy is all the prefetch needs (authenticate() recomputes
+    every message's own bytes anyway)."""
+    m = _decode(raw, deserialize)
+    if seen is not None and isinstance(raw, (str, bytes)):
+        if raw in seen:
+            return
+        seen.add(raw)
+    _collect(m, deserialize, out, depth, seen)
+
+
+def requests_in_drain(raw_msgs, deserialize=json.loads, limit=None, distinct=False):
     """Signed request dicts inside a list of raw rxMsgs entries
     ((text, ident) pairs or bare texts): client requests themselves, the
     `request` of PROPAGATE messages, and both of those inside BATCH messages.
     `limit` counts rxMsgs entries (a BATCH is one entry, as in
     processReceived).  Undecodable entries are skipped (the reference logs and
-    drops them, zstack.py:541-545)."""
+    drops them, zstack.py:541-545).  distinct=True: entries whose raw text
+    was already seen in this drain contribute nothing more (they are still
+    decoded)."""
     out = []
+    seen = set() if distinct else None
     for n, item in enumerate(raw_msgs):
         if limit is not None and n >= limit:
             break
         raw = item[0] if isinstance(item, tuple) else item
-        _collect(_decode(raw, deserialize), deserialize, out, 0)
+        _visit(raw, deserialize, out, 0, seen)
     return out
 
 
@@ -73,12 +91,47 @@ def prefetch_drain(authnr, raw_msgs, deserialize=json.loads, limit=None):
     return authnr.prefetch(requests_in_drain(raw_msgs, deserialize, limit))
 
 
+class _Memo:
+    """Decoded messages of one drain, by the identity of their raw text: the
+    verify-ahead decodes each rxMsgs entry (and each entry of a BATCH) once,
+    and the stack's deserializeMsg hands that object back when the reference
+    loop asks for the same raw object (zstack.py:538, node.py:1335) -- one
+    json decode per message instead of two.  An entry is used once; anything
+    not found (another object, a second copy) is decoded as before."""
+
+    __slots__ = ("d", "deserialize")
+
+    def __init__(self, deserialize):
+        self.d = {}
+        self.deserialize = deserialize
+
+    def __call__(self, raw):
+        obj = self.deserialize(raw)
+        self.d[id(raw)] = (raw, obj)  # raw kept alive, so its id is not reused while held
+        return obj
+
+    def take(self, raw):
+        e = self.d.pop(id(raw), None)
+        if e is not None and e[0] is raw:
+            return e[1]
+        return _NONE
+
+
+_NONE = object()
+
+
 class VerifyAheadMixin:
     """Mix in front of a ZStack subclass (e.g. plenum.common.stacks.ClientZStack
     / NodeZStack).  The authenticator is the class attribute `authnr`
-    (verify_ahead_stack binds it) or a constructor keyword `authnr=`."""
+    (verify_ahead_stack binds it) or a constructor keyword `authnr=`.
+
+    processReceived(limit) first decodes the next `limit` rxMsgs entries
+    (descending into BATCH entries) and prefetches their signed requests in one
+    GPU batch, then runs the reference loop; deserializeMsg returns the
+    objects decoded for the prefetch, so every message is decoded once."""
 
     authnr = None
+    _va_memo = None
 
     def __init__(self, *args, authnr=None, **kwargs):
         if authnr is not None:
@@ -86,9 +139,23 @@ class VerifyAheadMixin:
         super().__init__(*args, **kwargs)
 
     def processReceived(self, limit):
-        if self.authnr is not None and limit > 0:
-            prefetch_drain(self.authnr, list(self.rxMsgs), self.deserializeMsg, limit)
-        return super().processReceived(limit)
+        if self.authnr is None or limit <= 0:
+            return super().processReceived(limit)
+        memo = _Memo(super().deserializeMsg)
+        self.authnr.prefetch(requests_in_drain(islice(self.rxMsgs, limit), memo, limit, distinct=True))
+        self._va_memo = memo
+        try:
+            return super().processReceived(limit)
+        finally:
+            self._va_memo = None
+
+    def deserializeMsg(self, msg):
+        memo = self._va_memo
+        if memo is not None:
+            obj = memo.take(msg)
+            if obj is not _NONE:
+                return obj
+        return super().deserializeMsg(msg)
 
 
 _stack_classes = {}

@@ -68,6 +68,10 @@ try:
                             results_ok as _results_ok)
 except ImportError:  # pragma: no cover
     _pack_range = _repack_spans = _gather_u32 = _results_ok = None
+try:  # the node's per-message path: authenticate()'s host steps in one call; the verify-ahead's dedupe
+    from ._hostpack import authn_key as _authn_key, distinct_sm as _distinct_sm
+except ImportError:  # pragma: no cover
+    _authn_key = _distinct_sm = None
 
 try:  # native packing (csrc/hostpack.cpp)
     from ._hostpack import pack_sm as _pack_sm, pack_split64 as _pack_split64
@@ -115,6 +119,7 @@ _STAGE_MIN_BATCH = 1 << 16  # batches staged while scanned (edv_stage_put from t
 
 
 _MISSING = object()
+_IGNORE_SIG = (SIG,)
 
 
 class _Prepared:
@@ -192,8 +197,12 @@ class _GpuState:
         # streamed path (r05m/r05n: 29-31 M requests/s either way; the copies it hides are
         # not what bounds the batch -- the scan's workers are)
         self.stage = stage
+        # identifier -> (verkey as getVerkey returned it, key bytes): authenticate()'s per-message
+        # DidVerifier step without the VerkeyCache call while the verkey stays the same
+        self.fast_keys = {}
+        self.fast_keys_max = 1 << 16
         self.stats = {"batches": 0, "batch_items": 0, "cache_hits": 0, "single_verifies": 0, "keyed_items": 0,
-                      "keys_registered": 0}
+                      "keys_registered": 0, "prefetched": 0}
 
 
 class GpuAuthMixin:
@@ -250,6 +259,13 @@ class GpuAuthMixin:
 
     # -- the reference authenticate(), verify on the GPU ----------------------
     def authenticate(self, msg: Dict, identifier: str = None, signature: str = None) -> str:
+        if identifier is None and signature is None and _authn_key is not None:
+            # the node's call (node.py:2310): the host steps up to getVerkey natively, then the
+            # verdict cache the verify-ahead filled; anything unusual takes the path below
+            if self._native_host_steps():
+                k = _authn_key(msg, _IGNORE_SIG)
+                if k is not None:
+                    return self._authenticate_sm(k[0], k[1])
         try:
             p = self._prepare(msg, identifier, signature)
             if not self._verify_prepared(p):
@@ -259,6 +275,40 @@ class GpuAuthMixin:
         except Exception as ex:
             raise CouldNotAuthenticate from ex
         return p.identifier
+
+    def _authenticate_sm(self, identifier, sm):
+        """authenticate() after its host steps (client_authn.py:93-106):
+        sm = b58decode(signature) || serializeForSig(msg), as authn_key
+        returns them -- the same order of checks and exceptions as _prepare
+        from getVerkey on."""
+        g = self._g
+        try:
+            verkey = self.getVerkey(identifier)
+            if verkey is None:
+                raise CouldNotAuthenticate('Can not find verkey for DID {}'.format(identifier))
+            fk = g.fast_keys.get(identifier)
+            if fk is not None and (fk[0] is verkey or (verkey.__class__ is str and fk[0] == verkey)):
+                key = fk[1]
+            else:
+                key = self._resolve_key(verkey, identifier)
+                if verkey.__class__ is str and key.__class__ is bytes:
+                    if len(g.fast_keys) >= g.fast_keys_max:
+                        g.fast_keys.clear()
+                    g.fast_keys[identifier] = (verkey, key)
+            if not key:  # nacl_wrappers.py:237-238: no key -> False
+                raise InvalidSignature
+            hit = g.verdicts.get((key, sm))
+            if hit is None:
+                hit = self._verify_prepared(_Prepared(identifier, sm[:64], sm[64:], key))
+            else:
+                g.stats["cache_hits"] += 1
+            if not hit:
+                raise InvalidSignature
+        except SigningException as e:
+            raise e
+        except Exception as ex:
+            raise CouldNotAuthenticate from ex
+        return identifier
 
     def _prepare(self, msg, identifier=None, signature=None, ignore=(SIG,)):
         """Everything authenticate() does before the verify, reference order."""
@@ -436,11 +486,14 @@ class GpuAuthMixin:
     # -- verify-ahead cache ------------------------------------------------
     @staticmethod
     def _vkey(p):
-        return (p.key, p.sig, p.ser)
+        """Verdict-cache key: the verkey's bytes and crypto_sign_open's input
+        sm = sig || ser (nacl_wrappers.py:108) -- exact content, so a hit is
+        the verdict of exactly these bytes under exactly this key."""
+        return (p.key, p.sig + p.ser)
 
-    def _remember(self, p, ok):
+    def _remember(self, p, ok, vkey=None):
         g = self._g
-        g.verdicts[self._vkey(p)] = ok
+        g.verdicts[vkey if vkey is not None else self._vkey(p)] = ok
         if len(g.verdicts) > g.verdict_cache_size:
             g.verdicts.popitem(last=False)
 
@@ -448,13 +501,15 @@ class GpuAuthMixin:
         if not p.key:  # nacl_wrappers.py:237-238: no key -> False
             return False
         g = self._g
-        hit = g.verdicts.get(self._vkey(p))
+        vk = self._vkey(p)
+        hit = g.verdicts.get(vk)
         if hit is not None:
             g.stats["cache_hits"] += 1
             return hit
         g.stats["single_verifies"] += 1
-        ok = self._verify_many([p])[0]
-        self._remember(p, ok)
+        with _engine_lock(self._engine()):
+            ok = self._verify_many_locked([p])[0]
+            self._remember(p, ok, vk)
         return ok
 
     def _verify_many(self, prepared):
@@ -890,23 +945,67 @@ class GpuAuthMixin:
     def prefetch(self, msgs):
         """Verify-ahead: batch-verify every message that gets as far as the
         verify step, and cache the verdicts for authenticate().  Returns the
-        number of distinct signatures verified."""
+        number of distinct signatures verified.  The host steps run in the
+        native scan (as in authenticate_batch), the drain's copies of a
+        request are verified once (distinct (identifier, sig || ser)), and
+        the verdict cache is written under the engine lock."""
+        if _scan_batch is not None and _distinct_sm is not None and self._native_host_steps():
+            return self._prefetch_scanned(msgs)
         prepared = []
         for msg in msgs:
             try:
                 prepared.append(self._prepare(msg))
             except Exception:
                 continue  # authenticate() will raise it again
+        return self._prefetch_prepared(prepared)
+
+    def _prefetch_prepared(self, prepared):
         verdicts = self._g.verdicts
         uniq = OrderedDict()
         for p in prepared:
             k = self._vkey(p)
             if k not in verdicts and k not in uniq:
                 uniq[k] = p
-        items = list(uniq.values())
-        for p, ok in zip(items, self._verify_many(items)):
-            self._remember(p, ok)
+        items = list(uniq.items())
+        with _engine_lock(self._engine()):
+            oks = self._verify_many_locked([p for _, p in items])
+            for (k, p), ok in zip(items, oks):
+                self._remember(p, ok, k)
+        self._g.stats["prefetched"] += len(items)
         return len(items)
+
+    def _prefetch_scanned(self, msgs):
+        import numpy as np
+        g = self._g
+        eng = self._engine()
+        with _engine_lock(eng):
+            # slot 64: sig64 holds sm[:64], the message buffer sm[64:] (the split at byte 64)
+            fast_b, uidx_b, uniq, sig_o, msg_o, off, short = _scan_batch(msgs, [SIG], g.scan_threads, g.scan_out, 64)
+            n = len(msgs)
+            picks, sms = _distinct_sm(memoryview(sig_o)[:64 * n], msg_o, off, short, uidx_b, fast_b)
+        ukeys = {}
+        uidx = np.frombuffer(uidx_b, np.uint32)
+        verdicts = g.verdicts
+        prepared, seen = [], set()
+        for i, sm in zip(picks, sms):
+            u = int(uidx[i])
+            key = ukeys.get(u, _MISSING)
+            if key is _MISSING:
+                key = ukeys[u] = self._key_for(uniq[u])  # getVerkey + DidVerifier, once per identifier
+            if key.__class__ is not bytes or not key:
+                continue  # no key (False without a verify) or an exception: authenticate() raises it
+            vk = (key, sm)
+            if vk in verdicts or vk in seen:
+                continue
+            seen.add(vk)
+            prepared.append(_Prepared(uniq[u], sm[:64], sm[64:], key))
+        slow = [msgs[i] for i in np.flatnonzero(np.frombuffer(fast_b, np.uint8) == 0).tolist()]
+        for msg in slow:  # items the scan left to Python (odd types, non-ASCII, bad base58 ...)
+            try:
+                prepared.append(self._prepare(msg))
+            except Exception:
+                continue  # authenticate() will raise it again
+        return self._prefetch_prepared(prepared)
 
     def clear_verdicts(self):
         self._g.verdicts.clear()

@@ -20,6 +20,7 @@ same libsodium the reference reaches through libnacl:
 No product code (plenum_amd) is imported.  Usage (a child process of bench.py,
 so the GPU process never forks):
     python oracle/ref_authn_port.py INPUT.json [--procs K]
+    python oracle/ref_authn_port.py DRAINS.json --drain   (the node's receive loop, run_drains)
 INPUT.json: {"requests": [...], "verkeys": {identifier: verkey}}; prints one
 JSON line {"value": requests/s, "procs": K, "accepted": A, ...}.
 """
@@ -157,8 +158,69 @@ def run_slice(path, lo, hi, out_q=None):
     return {"n": len(reqs), "seconds": dt, "accepted": acc, "version": sodium.version}
 
 
+def run_drains(path):
+    """--drain: the node's receive loop over recorded drains, the reference way
+    (zstack.py:528-549 processReceived: json-decode each entry; node.py:1270-1337
+    handleOneNodeMsg: a PROPAGATE authenticates msg.request, a BATCH re-decodes
+    and re-enters for every entry; node.py:1399-1451 validateClientMsg: a
+    request authenticates SafeRequest(**msg).as_dict, request.py:27-39), every
+    authenticate() the reference chain above over libsodium.
+    INPUT.json: {"drains": [{"node": [text, ...], "client": [text, ...]}, ...],
+    "verkeys": {...}}; the node stack is drained first, as bench.py's leg does."""
+    spec = json.load(open(path))
+    verkeys = spec["verkeys"]
+    sodium = Sodium()
+    stats = {"authenticate": 0, "accepted": 0, "entries": 0}
+
+    def auth(req):
+        stats["authenticate"] += 1
+        r = authenticate(sodium, verkeys, req)
+        stats["accepted"] += r == req.get("identifier")
+
+    def node_msg(m):
+        if not isinstance(m, dict):
+            return
+        op = m.get("op")
+        if op == "PROPAGATE" and isinstance(m.get("request"), dict):
+            auth(m["request"])
+        elif op == "BATCH":
+            for t in m.get("messages") or ():
+                try:
+                    node_msg(json.loads(t))
+                except ValueError:
+                    continue
+
+    def client_msg(m):
+        if isinstance(m, dict) and all(k in m for k in ("operation", "identifier", "reqId")):
+            req = {"identifier": m["identifier"], "reqId": m["reqId"], "operation": m["operation"]}
+            if m.get("signature") is not None:
+                req["signature"] = m["signature"]
+            if m.get("protocolVersion") is not None:
+                req["protocolVersion"] = m["protocolVersion"]
+            auth(req)
+
+    t0 = time.perf_counter()
+    for d in spec["drains"]:
+        for handler, texts in ((node_msg, d["node"]), (client_msg, d["client"])):
+            for t in texts:
+                stats["entries"] += 1
+                try:
+                    m = json.loads(t)
+                except ValueError:
+                    continue
+                handler(m)
+    dt = time.perf_counter() - t0
+    return {"seconds": dt, "drains": len(spec["drains"]), "rx_entries": stats["entries"],
+            "authenticate_calls": stats["authenticate"], "accepted": stats["accepted"],
+            "authenticate_per_s": stats["authenticate"] / dt, "us_per_authenticate": dt / stats["authenticate"] * 1e6,
+            "procs": 1, "libsodium": sodium.version}
+
+
 def main():
     path = sys.argv[1]
+    if "--drain" in sys.argv:
+        print(json.dumps(run_drains(path)))
+        return
     procs = int(sys.argv[sys.argv.index("--procs") + 1]) if "--procs" in sys.argv else 1
     n = len(json.load(open(path))["requests"])
     if procs == 1:

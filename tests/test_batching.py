@@ -44,7 +44,7 @@ def test_verify_ahead_mixin_prefetches_then_processes():
     st = S([(json.dumps(req), 1)] * 3)
     st.authnr = _Auth()
     assert st.processReceived(2) == 2
-    assert st.authnr.batches == [[req, req]]
+    assert st.authnr.batches == [[req]]  # the two entries are the same text: one copy prefetched
     assert prefetch_drain(st.authnr, st.rxMsgs) == 3
 
 
@@ -92,7 +92,7 @@ def test_verify_ahead_stack_binds_authenticator():
     st = cls(msgs=[(_batch([{"op": "PROPAGATE", "request": req}] * 2), b"n")], stackParams={"name": "x"})
     assert st.kw == {"stackParams": {"name": "x"}}
     st.processReceived(100)
-    assert auth.batches == [[req, req]]
+    assert auth.batches == [[req]]  # identical PROPAGATE texts inside the BATCH: one copy
     other = _Auth()
     st2 = verify_ahead_stack(Base, auth)(msgs=[(json.dumps(req), 1)], authnr=other)
     st2.processReceived(1)

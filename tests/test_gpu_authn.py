@@ -171,6 +171,52 @@ def test_verify_ahead_batch_framed_drain_on_gpu(gpu_engine, oracle):
     assert eng.launches == 1 and a.stats["single_verifies"] == 0 and a.stats["cache_hits"] == 200
 
 
+def test_node_loop_drains_on_gpu(gpu_engine, oracle):
+    """bench.py's end_to_end.node_drain shape, checked: three drains of an
+    n = 25 pool through the verify-ahead stacks over the restated node loop
+    (plenum_amd/nodeloop.py): per drain 100 client REQUESTs + 24 BATCHes of
+    PROPAGATEs, every raw message decoded once, ONE engine launch per drain,
+    0 single verifies, and all 2,500 authenticate() outcomes per drain equal
+    to the oracle's verdict (forged payloads, a corrupted S, an unknown
+    identifier among them)."""
+    from plenum_amd.batching import verify_ahead_stack
+    from plenum_amd.nodeloop import NodeCounters, Stack, drain_texts
+    reqs, _rx, idrs, vks, pks, sers, sig = _drain(gpu_engine, n_req=300, n_nodes=1)
+    reqs[7]["signature"] = reqs[8]["signature"]            # another request's signature
+    reqs[150]["identifier"] = "UnknownIdentifier111111"   # getVerkey raises
+    eng = _Counting(gpu_engine)
+    a = GpuAuthNr(engine=eng)
+    for idr, vk in zip(idrs, vks):
+        a.addIdr(idr, vk)
+    a.keys_settle()
+    want = []
+    for i, r in enumerate(reqs):
+        if i == 150:
+            want.append("UnknownIdentifier")
+            continue
+        s = sig[8] if i == 7 else sig[i]
+        ser = sers[i]
+        ok = i % 10 != 3 and oracle.oracle_verify_detached(s.tobytes(), ser, len(ser), pks[i % 10].tobytes()) == 0
+        want.append(r["identifier"] if ok else "InvalidSignature")
+    assert want.count("InvalidSignature") == 31
+    nc = NodeCounters()
+    nc.record = True
+    ns = verify_ahead_stack(Stack, a)(a, "node", nc)
+    cs = verify_ahead_stack(Stack, a)(a, "client", nc)
+    for d in range(3):
+        part = reqs[d * 100:(d + 1) * 100]
+        client, node = drain_texts(part, 25)
+        ns.rxMsgs.extend(node)
+        cs.rxMsgs.extend(client)
+        l0, s0 = eng.launches, a.stats["single_verifies"]
+        nc.outcomes.clear()
+        assert ns.processReceived(100) == 24 and cs.processReceived(100) == 100
+        assert eng.launches - l0 == 1 and a.stats["single_verifies"] == s0
+        w = want[d * 100:(d + 1) * 100]
+        assert [o[1] for o in nc.outcomes] == w * 24 + w
+    assert a.stats["single_verifies"] == 0 and a.stats["cache_hits"] == 3 * 2500 - 25  # the unknown id never reaches it
+
+
 def test_multi_engine_one_device(gpu_engine):
     """The single-process multi-GPU path with the devices of this box (one
     here): MultiEngine through the authenticator == the plain engine."""
