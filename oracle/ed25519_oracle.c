@@ -407,6 +407,10 @@ static void init_consts(void) {
   consts_ready = 1;
 }
 
+/* Built when the library loads, so threads calling the verify concurrently
+   (cpu_baseline.c's workers) never see the constants half-written. */
+__attribute__((constructor)) static void init_consts_at_load(void) { init_consts(); }
+
 /* libsodium 1.0.18 ge25519_has_small_order: the 7-entry blacklist, first 31
  * bytes exact, last byte compared with the sign bit masked. */
 static const uint8_t SMALL_ORDER[7][32] = {

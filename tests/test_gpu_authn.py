@@ -448,3 +448,131 @@ def test_staged_batch_on_gpu(gpu_engine):
             else:
                 assert r == batch[i]["identifier"], (rep, i)
     assert a.stats["keyed_items"] - before == 2 * n
+
+
+def _oracle_verdicts(sig64, pk32, msgs, threads=16):
+    """The C oracle's crypto_sign_verify_detached over many items, on host
+    threads (oracle/cpu_baseline.c with use_sodium=0: the plain-C restatement)."""
+    import ctypes
+    import os
+    from conftest import ROOT
+    from plenum_amd import pack_messages
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "_build", "libcpu_baseline.so"))
+    buf, off = pack_messages(msgs)
+    buf = np.concatenate([buf, np.zeros(16, np.uint8)])
+    n = len(msgs)
+    ok = np.zeros(n, np.uint8)
+    secs = ctypes.c_double()
+    P = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    sig64, pk32 = np.ascontiguousarray(sig64), np.ascontiguousarray(pk32)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    assert lib.cpu_baseline_run(P(sig64), P(pk32), P(buf), P(off), ctypes.c_uint64(n), threads, 0, P(ok),
+                                ctypes.byref(secs)) == 0
+    return ok.astype(bool)
+
+
+_C3_SIGS = 100_000
+
+
+def test_configs3_multi_signature_shape_vs_oracle(gpu_engine):
+    """BASELINE configs[3] at its real shape through authenticate_multi_batch:
+    >= 100k signatures, 1-5 per request (distinct signers), signed payloads
+    log-uniform over 64 B - 4 KiB, ~6 % of the signatures corrupted (a bit of
+    R or S flipped, a signature moved to another signer, a payload changed
+    after signing).  Every per-signature verdict of the GPU path equals the C
+    oracle's, and every request's outcome (identifiers up to the threshold, or
+    InsufficientCorrectSignatures / InsufficientSignatures) is the one those
+    verdicts give.  Signers: 48 registered (key-table path) + 16 known only
+    through the state lookup (general path)."""
+    from plenum_amd import _hostpack, pack_messages, synth
+    from plenum_amd.base58 import b58encode
+    from plenum_amd.exceptions import InsufficientCorrectSignatures, InsufficientSignatures
+    from plenum_amd.serialization import serialize_msg_for_signing
+    rng = np.random.default_rng(33)
+    S = 64
+    pks, sks = gpu_engine.seed_keypair_batch(synth.signer_seeds(S + 77)[77:])
+    idrs = [b58encode(bytes(pk[:16])) for pk in pks]
+    vks = ["~" + b58encode(bytes(pk[16:])) for pk in pks]
+    state = {idrs[j]: {"verkey": vks[j]} for j in range(48, S)}
+    a = GpuAuthNr(engine=gpu_engine, nym_lookup=lambda st, idr: state.get(idr, {}))
+    for j in range(48):
+        a.addIdr(idrs[j], vks[j])
+    a.keys_settle()
+    reqs, signers, sers = [], [], []
+    total = 0
+    while total < _C3_SIGS:
+        k = int(rng.integers(1, 6))
+        who = rng.choice(S, size=k, replace=False)
+        target = int(np.exp(rng.uniform(np.log(64), np.log(4096))))
+        req = {"identifier": idrs[int(who[0])], "reqId": 1_700_000_000_000_000 + len(reqs),
+               "operation": {"type": "1", "raw": ""}, "protocolVersion": 1}
+        base = len(serialize_msg_for_signing(req, topLevelKeysToIgnore=["signature", "signatures"]))
+        req["operation"]["raw"] = "".join(map(chr, rng.integers(97, 123, size=max(0, target - base))))
+        ser = serialize_msg_for_signing(req, topLevelKeysToIgnore=["signature", "signatures"])
+        reqs.append(req)
+        signers.append([int(w) for w in who])
+        sers.append(ser)
+        total += k
+    lens = np.array([len(s) for s in sers])
+    assert lens.min() <= 100 and lens.max() >= 3500  # the 64 B - 4 KiB spread
+    item_req = np.repeat(np.arange(len(reqs)), [len(s) for s in signers])
+    item_key = np.concatenate([np.array(s) for s in signers]).astype(np.uint32)
+    buf, off = pack_messages(sers)
+    starts, ends = off[:-1][item_req], off[1:][item_req]
+    ibuf, ioff = pack_messages([bytes(buf[s:e]) for s, e in zip(starts, ends)])
+    sig = gpu_engine.sign_batch(sks, item_key, ibuf, ioff)
+    n = len(item_key)
+    bad = rng.random(n) < 0.05
+    for i in np.flatnonzero(bad):
+        kind = i % 3
+        if kind == 0:
+            sig[i, int(rng.integers(0, 32))] ^= 1 << int(rng.integers(0, 8))    # R
+        elif kind == 1:
+            sig[i, 32 + int(rng.integers(0, 31))] ^= 1 << int(rng.integers(0, 8))  # S
+        else:
+            sig[i] = sig[(i + 1) % n]                                            # someone else's
+    moved = rng.choice(len(reqs), size=len(reqs) // 100, replace=False)          # payload changed after signing
+    for r in moved:
+        reqs[r]["reqId"] += 1
+    texts = _hostpack.b58encode_rows(np.ascontiguousarray(sig).tobytes(), 64)
+    batch, pos = [], 0
+    thresholds = []
+    for r, req in enumerate(reqs):
+        k = len(signers[r])
+        sigs = {idrs[w]: texts[pos + j] for j, w in enumerate(signers[r])}
+        pos += k
+        thr = [None, 1, k, k + 1, int(rng.integers(1, k + 1))][r % 5]
+        thresholds.append(thr)
+        batch.append((req, sigs, thr))
+    # the oracle's verdict of every signature, over the bytes each request now serializes to
+    now = [serialize_msg_for_signing(q, topLevelKeysToIgnore=["signature", "signatures"]) for q in reqs]
+    want = _oracle_verdicts(sig, pks[item_key], [now[r] for r in item_req])
+    assert 0.85 < want.mean() < 0.97, want.mean()
+    # per-signature verdicts on the GPU path, through the same preparation authenticate_multi uses
+    items = []
+    for req, sigs, thr in batch:
+        _, steps = a._prepare_multi(req, sigs, None)
+        items += steps
+    assert len(items) == n
+    got = np.array(a._verify_many(items), bool)
+    bad_i = np.flatnonzero(got != want)[:10]
+    assert (got == want).all(), [(int(i), bool(got[i]), bool(want[i]), int(item_key[i]), bool(bad[i]), int(item_req[i]),
+                                  int(item_req[i]) in set(moved.tolist()), len(now[item_req[i]])) for i in bad_i]
+    assert a.stats["keyed_items"] > 0 and a.stats["batch_items"] > a.stats["keyed_items"]  # both paths ran
+    # every request's outcome
+    res = a.authenticate_multi_batch(batch)
+    pos = 0
+    for r, out in enumerate(res):
+        k = len(signers[r])
+        v = want[pos:pos + k]
+        ids = [idrs[w] for w in signers[r]]
+        pos += k
+        thr = thresholds[r] if thresholds[r] is not None else k
+        if k < thr:
+            assert isinstance(out, InsufficientSignatures), r
+            continue
+        good = [i for i, ok in zip(ids, v) if ok]
+        if len(good) >= thr:
+            assert out == good[:thr], r
+        else:
+            assert isinstance(out, InsufficientCorrectSignatures) and out.args == (len(good), thr), (r, out)
