@@ -286,15 +286,7 @@ class GpuAuthMixin:
             verkey = self.getVerkey(identifier)
             if verkey is None:
                 raise CouldNotAuthenticate('Can not find verkey for DID {}'.format(identifier))
-            fk = g.fast_keys.get(identifier)
-            if fk is not None and (fk[0] is verkey or (verkey.__class__ is str and fk[0] == verkey)):
-                key = fk[1]
-            else:
-                key = self._resolve_key(verkey, identifier)
-                if verkey.__class__ is str and key.__class__ is bytes:
-                    if len(g.fast_keys) >= g.fast_keys_max:
-                        g.fast_keys.clear()
-                    g.fast_keys[identifier] = (verkey, key)
+            key = self._key_of(identifier, verkey)
             if not key:  # nacl_wrappers.py:237-238: no key -> False
                 raise InvalidSignature
             hit = g.verdicts.get((key, sm))
@@ -340,6 +332,21 @@ class GpuAuthMixin:
     def serializeForSig(self, msg, topLevelKeysToIgnore=None):
         """The reference serializer's exact bytes (native, KAT-pinned)."""
         return serialize_msg_for_signing(msg, topLevelKeysToIgnore=topLevelKeysToIgnore)
+
+    def _key_of(self, identifier, verkey):
+        """DidVerifier(verkey, identifier).key (verifier.py:21-46), remembered
+        per identifier while getVerkey keeps returning the same verkey (the
+        node's steady state): one dict lookup instead of the VerkeyCache call."""
+        g = self._g
+        fk = g.fast_keys.get(identifier)
+        if fk is not None and (fk[0] is verkey or (verkey.__class__ is str and fk[0] == verkey)):
+            return fk[1]
+        key = self._resolve_key(verkey, identifier)
+        if verkey.__class__ is str and key.__class__ is bytes and identifier.__class__ is str:
+            if len(g.fast_keys) >= g.fast_keys_max:
+                g.fast_keys.clear()
+            g.fast_keys[identifier] = (verkey, key)
+        return key
 
     def _resolve_key(self, verkey, identifier):
         try:
@@ -564,7 +571,7 @@ class GpuAuthMixin:
             verkey = self.getVerkey(identifier)
             if verkey is None:
                 raise CouldNotAuthenticate('Can not find verkey for DID {}'.format(identifier))
-            return self._resolve_key(verkey, identifier)
+            return self._key_of(identifier, verkey)
         except SigningException as e:
             return e
         except Exception as ex:

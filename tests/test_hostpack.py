@@ -262,3 +262,33 @@ def test_results_ok():
         H.results_ok(bytes([1]), bytes([0]), struct.pack("<I", 5), ["a"])
     with pytest.raises(ValueError):
         H.results_ok(bytes([1, 1]), bytes([0]), struct.pack("<2I", 0, 0), ["a"])
+
+
+def test_results_ok_parallel_matches_serial_and_refcounts():
+    """results_ok fills the result list on the scan's worker threads and adds
+    the reference counts per identifier afterwards: same list as the serial
+    definition, failures in index order, and exact reference counts."""
+    import sys
+
+    import numpy as np
+    from plenum_amd import _hostpack
+    rng = np.random.default_rng(5)
+    n = 200_000
+    uniq = ["idr%d" % i + "x" * i for i in range(7)]
+    ok = (rng.random(n) < 0.9).astype(np.uint8)
+    short = (rng.random(n) < 0.01).astype(np.uint8)
+    uidx = rng.integers(0, len(uniq), n).astype(np.uint32)
+    before = [sys.getrefcount(u) for u in uniq]
+    none_before = sys.getrefcount(None)
+    res, failed = _hostpack.results_ok(ok.tobytes(), short.tobytes(), uidx.tobytes(), uniq)
+    want_pass = (ok == 1) & (short == 0)
+    assert failed == np.flatnonzero(~want_pass).tolist()
+    assert res == [uniq[u] if p else None for u, p in zip(uidx.tolist(), want_pass.tolist())]
+    per = np.bincount(uidx[want_pass], minlength=len(uniq))
+    after = [sys.getrefcount(u) for u in uniq]
+    assert [x - b for x, b in zip(after, before)] == per.tolist()
+    assert sys.getrefcount(None) - none_before >= int((~want_pass).sum()) - 10
+    del res
+    assert [sys.getrefcount(u) for u in uniq] == before
+    with pytest.raises(ValueError):
+        _hostpack.results_ok(b"\x01", b"\x00", np.array([9], np.uint32).tobytes(), uniq)
