@@ -6,6 +6,7 @@ stp_core/crypto/nacl_wrappers.py:232-242 (Verifier.verify) with one batched
 launch; verdicts are libsodium 1.0.18's (crypto_sign_verify_detached == 0).
 """
 import ctypes
+import threading
 
 import numpy as np
 
@@ -114,6 +115,7 @@ class EdVerifyEngine:
         self._lib = lib
         self._ctx = ctypes.c_void_p(ctx)
         self.device = device
+        self._one_args = threading.local()  # verify_one_keyed's reusable ctypes arguments
 
     # ------------------------------------------------------------- lifecycle
     def close(self):
@@ -485,11 +487,18 @@ class EdVerifyEngine:
         without the numpy packing around it."""
         if len(sig64) != 64:
             raise ValueError("sig64 must be 64 bytes")
-        # per-call argument objects (a couple of microseconds; safe from any thread)
-        kid, off, bits = ctypes.c_uint32(int(key_id)), (ctypes.c_uint64 * 2)(0, len(msg)), ctypes.c_uint8(0)
-        check(self._lib.edv_verify_batch_keyed(self._ctx, bytes(sig64), ctypes.byref(kid), bytes(msg) if msg else None,
-                                               off, 1, ctypes.byref(bits)))
-        return bool(bits.value & 1)
+        # argument objects of this thread, reused from call to call (building them costs microseconds)
+        tl = self._one_args.__dict__
+        if "kid" not in tl:
+            tl["kid"], tl["off"], tl["bits"] = ctypes.c_uint32(), (ctypes.c_uint64 * 2)(), ctypes.c_uint8()
+            tl["kid_p"], tl["bits_p"] = ctypes.byref(tl["kid"]), ctypes.byref(tl["bits"])
+        tl["kid"].value = int(key_id)
+        off = tl["off"]
+        off[1] = len(msg)
+        tl["bits"].value = 0
+        check(self._lib.edv_verify_batch_keyed(self._ctx, bytes(sig64), tl["kid_p"], bytes(msg) if msg else None,
+                                               off, 1, tl["bits_p"]))
+        return bool(tl["bits"].value & 1)
 
     def verify_batch_keyed_device(self, d_sig64, d_key_idx, d_msgs, d_msg_off, n, d_accept_words, stream=None):
         st = _stream_for(stream, d_sig64, d_accept_words)
