@@ -155,7 +155,7 @@ class _GpuState:
 
     def __init__(self, engine=None, device=0, devices=None, verdict_cache_size=1 << 20, key_window="auto",
                  max_keys=16384, hot_key_uses=2, key_store_bytes=KEY_STORE_BYTES, scan_threads=0,
-                 pipeline_part=0, async_key_builds=True, stream=True, stage=False):
+                 pipeline_part=0, async_key_builds=True, stream=True, stage=True):
         self.engine = engine
         self.device = device
         self.devices = devices
@@ -192,10 +192,10 @@ class _GpuState:
         # kernels overlapping the next chunk's pack (_authenticate_streamed)
         self.stream = stream
         self.last_breakdown = None  # the last streamed batch's phases (ms)
-        # stage=True: batches of 2^16 requests or more are staged while scanned
-        # (_authenticate_staged).  Off by default: on the box it measured level with the
-        # streamed path (r05m/r05n: 29-31 M requests/s either way; the copies it hides are
-        # not what bounds the batch -- the scan's workers are)
+        # stage=True (default): batches of 2^16 requests or more are staged while scanned
+        # (_authenticate_staged): 35-40 against 34-37 M requests/s streamed, alternating in one
+        # process on the box (profiles/r07c/e2e_ab.log) once its verdict list was built on the
+        # workers; stage=False: the streamed path
         self.stage = stage
         # identifier -> (verkey as getVerkey returned it, key bytes): authenticate()'s per-message
         # DidVerifier step without the VerkeyCache call while the verkey stays the same
@@ -655,7 +655,8 @@ class GpuAuthMixin:
         if not staged_ok:
             g.msg_bytes_per_item *= 1.5  # the next buffers are sized larger
             return None
-        g.msg_bytes_per_item = max(g.msg_bytes_per_item * 0.5, float((me - ms).sum()) / n)
+        # (the chunks' reservations are contiguous from 0: the largest end is the bytes staged)
+        g.msg_bytes_per_item = max(g.msg_bytes_per_item * 0.5, float(me.max()) / n if n else 0.0)
         ukeys = [self._key_for(idr) for idr in uniq]  # authenticate():93-99, once per identifier
         ids = None
         ks = self._key_store()

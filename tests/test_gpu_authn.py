@@ -576,3 +576,35 @@ def test_configs3_multi_signature_shape_vs_oracle(gpu_engine):
             assert out == good[:thr], r
         else:
             assert isinstance(out, InsufficientCorrectSignatures) and out.args == (len(good), thr), (r, out)
+
+
+def test_large_batch_staged_and_streamed_on_gpu(gpu_engine):
+    """The two large-batch paths on the device over one 300,000-request batch
+    (above 2^18, so the streamed path submits several chunks; staged by
+    default): every 10th request forged, a missing signature, an unknown
+    identifier -- both give the construction's outcome for every request."""
+    import copy
+    n = 300_000
+    reqs, rx, idrs, vks, pks, sers, sig = _drain(gpu_engine, n_req=n, n_nodes=1, n_signers=32)
+    batch = [copy.deepcopy(r) for r in reqs]
+    del batch[1234]["signature"]
+    batch[4321]["identifier"] = "UnknownIdentifier11111111"
+    want = []
+    for i, r in enumerate(batch):
+        want.append("MissingSignature" if i == 1234 else "UnknownIdentifier" if i == 4321 else
+                    "InvalidSignature" if i % 10 == 3 else r["identifier"])
+    outs = {}
+    for mode in ("stage", "stream"):
+        a = GpuAuthNr(engine=gpu_engine, stage=(mode == "stage"))
+        for idr, vk in zip(idrs, vks):
+            a.addIdr(idr, vk)
+        a.keys_settle()
+        clean = [copy.deepcopy(r) for i, r in enumerate(batch) if i not in (1234, 4321)]
+        a.authenticate_batch(clean)  # sizes the pinned buffers, then the steady-state batch
+        res = a.authenticate_batch(batch)
+        outs[mode] = [r if isinstance(r, str) else type(r).__name__ for r in res]
+        assert outs[mode] == want, mode
+        ok = a.authenticate_batch(clean)  # the steady state (every item scanned, every key built)
+        assert [r if isinstance(r, str) else type(r).__name__ for r in ok] == \
+               [w for i, w in enumerate(want) if i not in (1234, 4321)], mode
+        assert a._g.last_breakdown is not None, mode
