@@ -1872,29 +1872,45 @@ PyObject* py_results_ok(PyObject*, PyObject* args) {
 // array to intp first).  ValueError on an index past the table.
 PyObject* py_gather_u32(PyObject*, PyObject* args) {
   Py_buffer bt, bi;
-  if (!PyArg_ParseTuple(args, "y*y*", &bt, &bi)) return nullptr;
-  PyObject* ret = nullptr;
+  PyObject* out = Py_None;
+  if (!PyArg_ParseTuple(args, "y*y*|O", &bt, &bi, &out)) return nullptr;
+  struct Rel {
+    Py_buffer *a, *b;
+    ~Rel() {
+      PyBuffer_Release(a);
+      PyBuffer_Release(b);
+    }
+  } rel{&bt, &bi};
   const Py_ssize_t nt = bt.len / 4, n = bi.len / 4;
   if (bt.len % 4 || bi.len % 4) {
     PyErr_SetString(PyExc_ValueError, "gather_u32: buffers of uint32 expected");
-  } else if ((ret = PyByteArray_FromStringAndSize(nullptr, n * 4))) {
-    const uint32_t* t = (const uint32_t*)bt.buf;
-    const uint32_t* ix = (const uint32_t*)bi.buf;
-    uint32_t* o = (uint32_t*)PyByteArray_AS_STRING(ret);
-    uint32_t bad = 0;
-    for (Py_ssize_t i = 0; i < n; ++i) {
+    return nullptr;
+  }
+  // out: a bytearray reused from call to call (grown, never shrunk: a fresh 4 MB result per 1M
+  // requests costs its page faults every batch); else a new bytearray of exactly n ids
+  char* data = nullptr;
+  PyObject* ret = (out != Py_None && PyByteArray_CheckExact(out)) ? out_buffer(out, n * 4, &data)
+                                                                     : PyByteArray_FromStringAndSize(nullptr, n * 4);
+  if (!ret) return nullptr;
+  if (!data) data = PyByteArray_AS_STRING(ret);
+  const uint32_t* t = (const uint32_t*)bt.buf;
+  const uint32_t* ix = (const uint32_t*)bi.buf;
+  uint32_t* o = (uint32_t*)data;
+  std::atomic<uint32_t> bad{0};
+  run_chunks(n, n >= (1 << 18) ? scan_threads(n / 8, 0) : 1, [&](int, Py_ssize_t a, Py_ssize_t b) {
+    uint32_t bd = 0;
+    for (Py_ssize_t i = a; i < b; ++i) {
       const uint32_t k = ix[i];
-      bad |= (uint32_t)(k >= (uint32_t)nt);
+      bd |= (uint32_t)(k >= (uint32_t)nt);
       o[i] = k < (uint32_t)nt ? t[k] : 0u;
     }
-    if (bad) {
-      Py_DECREF(ret);
-      ret = nullptr;
-      PyErr_SetString(PyExc_ValueError, "gather_u32: index out of range");
-    }
+    if (bd) bad = 1;
+  }, 1 << 16);
+  if (bad) {
+    Py_DECREF(ret);
+    PyErr_SetString(PyExc_ValueError, "gather_u32: index out of range");
+    return nullptr;
   }
-  PyBuffer_Release(&bt);
-  PyBuffer_Release(&bi);
   return ret;
 }
 
@@ -2106,7 +2122,9 @@ PyMethodDef kMethods[] = {
      "an 8th element) into its output buffers"},
     {"repack_spans", py_repack_spans, METH_VARARGS,
      "repack_spans(buf, spans) -> (msgs, off): a staged scan's messages laid out contiguously with offsets"},
-    {"gather_u32", py_gather_u32, METH_VARARGS, "gather_u32(table, idx) -> bytearray: table[idx[i]] (uint32)"},
+    {"gather_u32", py_gather_u32, METH_VARARGS,
+     "gather_u32(table, idx, out=None) -> bytearray: table[idx[i]] (uint32); out: a bytearray to grow and reuse "
+     "(slice the result to len(idx) * 4 bytes)"},
     {"results_ok", py_results_ok, METH_VARARGS,
      "results_ok(ok, short, uidx, uniq) -> (results, failed indices) of a steady-state batch"},
     {"results_from", py_results_from, METH_VARARGS,

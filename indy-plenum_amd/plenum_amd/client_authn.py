@@ -201,6 +201,7 @@ class _GpuState:
         # DidVerifier step without the VerkeyCache call while the verkey stays the same
         self.fast_keys = {}
         self.fast_keys_max = 1 << 16
+        self.kid_out = bytearray()  # a batch's key id per request (gather_u32 output, reused)
         self.stats = {"batches": 0, "batch_items": 0, "cache_hits": 0, "single_verifies": 0, "keyed_items": 0,
                       "keys_registered": 0, "prefetched": 0}
 
@@ -591,6 +592,32 @@ class GpuAuthMixin:
             e.__cause__ = ex
             return e
 
+    def _keys_for(self, uniq):
+        """[_key_for(i) for i in uniq] (getVerkey once per identifier, reference
+        order of checks and exceptions), with the per-identifier key fast path
+        inlined: a batch's ~1,000 identifiers in well under a millisecond."""
+        fk = self._g.fast_keys
+        get_verkey = self.getVerkey
+        out = []
+        append = out.append
+        for idr in uniq:
+            try:
+                verkey = get_verkey(idr)
+                e = fk.get(idr)
+                if e is not None and e[0] is verkey:
+                    append(e[1])
+                    continue
+                if verkey is None:
+                    raise CouldNotAuthenticate('Can not find verkey for DID {}'.format(idr))
+                append(self._key_of(idr, verkey))
+            except SigningException as ex:
+                append(ex)
+            except Exception as ex:
+                c = CouldNotAuthenticate()
+                c.__cause__ = ex
+                append(c)
+        return out
+
     @staticmethod
     def _fresh(e):
         """A per-message copy of an exception (same class, args, __cause__)."""
@@ -657,20 +684,22 @@ class GpuAuthMixin:
             return None
         # (the chunks' reservations are contiguous from 0: the largest end is the bytes staged)
         g.msg_bytes_per_item = max(g.msg_bytes_per_item * 0.5, float(me.max()) / n if n else 0.0)
-        ukeys = [self._key_for(idr) for idr in uniq]  # authenticate():93-99, once per identifier
+        ukeys = self._keys_for(uniq)  # authenticate():93-99, once per identifier
         ids = None
         ks = self._key_store()
         if ks is not None and fast_b.count(0) == 0 and all(k.__class__ is bytes for k in ukeys):
-            self._register_waiting(ks, list(dict.fromkeys(ukeys)))
+            if g.hot or g.pending:
+                self._register_waiting(ks, list(dict.fromkeys(ukeys)))
             ids = ks.lookup(ukeys)
             if any(i is None for i in ids):
                 ids = None
         if ids is None:  # not the steady state: contiguous messages, the ordinary path
             msg_c, off_c = _repack_spans(msg_o, spans_b)
             return self._finish_scanned(msgs, (fast_b, uidx_b, uniq, sig_o, msg_c, off_c, short), slot, ukeys)
-        kid = np.frombuffer(_gather_u32(np.asarray(ids, np.uint32).tobytes(), uidx_b), np.uint32)
+        kid = np.frombuffer(_gather_u32(np.asarray(ids, np.uint32).tobytes(), uidx_b, g.kid_out), np.uint32, count=n)
         t2 = perf_counter()
         ok = np.asarray(eng.verify_staged(True, kid, slot_base, 0, ms, me), bool)
+        del kid
         t3 = perf_counter()
         g.stats["batches"] += 1
         g.stats["batch_items"] += n
@@ -703,18 +732,19 @@ class GpuAuthMixin:
         off_a = np.frombuffer(off, np.uint64)
         mlen = int(off_a[-1])
         g.msg_bytes_per_item = max(g.msg_bytes_per_item * 0.5, mlen / n)
-        ukeys = [self._key_for(idr) for idr in uniq]  # authenticate():93-99, once per identifier
+        ukeys = self._keys_for(uniq)  # authenticate():93-99, once per identifier
         ids = None
         ks = self._key_store()
         if ks is not None and fast_b.count(0) == 0 and all(k.__class__ is bytes for k in ukeys):
-            self._register_waiting(ks, list(dict.fromkeys(ukeys)))
+            if g.hot or g.pending:
+                self._register_waiting(ks, list(dict.fromkeys(ukeys)))
             ids = ks.lookup(ukeys)
             if any(i is None for i in ids):
                 ids = None
         if ids is None:  # not the steady state: the whole batch packed, the ordinary path
             _pack_range(handle, 0, n)
             return self._finish_scanned(msgs, scan[:7], slot, ukeys)
-        kid = np.frombuffer(_gather_u32(np.asarray(ids, np.uint32).tobytes(), uidx_b), np.uint32)
+        kid = np.frombuffer(_gather_u32(np.asarray(ids, np.uint32).tobytes(), uidx_b, g.kid_out), np.uint32, count=n)
         sig_a = np.frombuffer(sig_o, np.uint8, count=slot * n).reshape(-1, slot)
         msg_a = np.frombuffer(msg_o, np.uint8, count=mlen)
         t2 = perf_counter()
@@ -729,7 +759,7 @@ class GpuAuthMixin:
         oks += [np.asarray(eng.verify_collect(h), bool) for h in handles[len(oks):]]
         ok = np.concatenate(oks) if oks else np.zeros(0, bool)
         t4 = perf_counter()
-        del handles, oks, sig_a, msg_a
+        del handles, oks, sig_a, msg_a, kid
         g.stats["batches"] += 1
         g.stats["batch_items"] += n
         g.stats["keyed_items"] += n
@@ -851,7 +881,7 @@ class GpuAuthMixin:
         fast = np.frombuffer(fast_b, np.uint8).view(bool)
         uidx = np.frombuffer(uidx_b, np.uint32)
         if ukeys is None:
-            ukeys = [self._key_for(idr) for idr in uniq]  # authenticate():93-99, once per identifier
+            ukeys = self._keys_for(uniq)  # authenticate():93-99, once per identifier
         # per distinct identifier: 0 = key bytes, 1 = no key (the verify fails), 2 = exception
         ucls = np.fromiter((0 if k.__class__ is bytes else 1 if k is None else 2 for k in ukeys), np.uint8,
                            len(ukeys))
