@@ -151,6 +151,8 @@ def parse():
                     help="drains of the end_to_end.node_drain leg (100 REQUESTs + 24 BATCHes of PROPAGATEs each; "
                          "0 = skip)")
     ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--force-dist", action="store_true",
+                    help="run the N > 1 exchange path (process group, all-gather, all-reduce) even at N = 1")
     ap.add_argument("--e2e-devices", type=int, default=1,
                     help="1: also run the end-to-end leg through MultiEngine over 1/2/4/8 of the visible devices "
                          "(one node process; rank 0 at world 1)")
@@ -552,7 +554,16 @@ def main():
         local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    # the exchange path (process group, bitmask all-gather, ballot all-reduce): with N > 1 ranks, or
+    # at N = 1 with --force-dist (exercises the RCCL calls on a one-GPU box)
+    dist_on = world > 1 or args.force_dist
+    if dist_on and "WORLD_SIZE" not in os.environ:  # --force-dist at N = 1: a one-rank group
+        import socket
+        so = socket.socket()
+        so.bind(("127.0.0.1", 0))
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(so.getsockname()[1]), RANK="0", WORLD_SIZE="1")
+        so.close()
+    if dist_on:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -623,7 +634,7 @@ def main():
         d_msgs = torch.from_numpy(np.concatenate([buf_h, np.zeros(16, np.uint8)])).to(dev)
     nwords = (n + 63) // 64
     d_words = torch.zeros(nwords, dtype=torch.int64, device=dev)
-    gathered = [torch.zeros_like(d_words) for _ in range(world)] if world > 1 else None
+    gathered = [torch.zeros_like(d_words) for _ in range(world)] if dist_on else None
     stream = torch.cuda.current_stream(dev)
 
     # keyed path: register the signers' verkeys once (not per request)
@@ -645,12 +656,12 @@ def main():
 
     def step_general():
         eng.verify_spans_device(d_sig, d_pk, False, d_msgs, d_ms, d_me, n, d_words, stream=stream)
-        if world > 1:
+        if dist_on:
             dist.all_gather(gathered, d_words)
 
     def step_keyed():
         eng.verify_spans_device(d_sig, d_kreq, True, d_msgs, d_ms, d_me, n, d_words, stream=stream)
-        if world > 1:
+        if dist_on:
             dist.all_gather(gathered, d_words)
 
     step = step_keyed if args.path == "keyed" else step_general
@@ -688,7 +699,7 @@ def main():
             d_valid = bits * d_keep
             eng.tally_device(d_vkey, d_vvoter, d_vphase, d_valid, nv, n_keys, V, d_ballot, d_counts, d_quorum,
                              stream=stream, d_primary=d_primary)
-            if world > 1:
+            if dist_on:
                 dist.all_reduce(d_ballot, op=dist.ReduceOp.MAX)
             eng.tally_finish_device(d_ballot, n_keys, V, d_counts, d_quorum, stream=stream)
 
@@ -727,7 +738,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     phases = []
@@ -736,11 +747,11 @@ def main():
         step()
         phases.append(eng.last_phases_ms())  # waits for this step's events
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if dist_on:
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
@@ -751,7 +762,7 @@ def main():
     # verify): the bitmask all-gather (+ the ballot all-reduce MAX on configs[4])
     # on the same buffers, timed with events on the compute stream, max over ranks
     collective = None
-    if world > 1:
+    if dist_on:
         reps = 20
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         dist.barrier()
@@ -780,7 +791,7 @@ def main():
     mismatches = int((got != expect).sum())
     accepted, expected = int(got.sum()), int(expect.sum())
     gathered_accepted = None
-    if world > 1:  # every rank's parity, and the bitmask as the all-gather delivers it
+    if dist_on:  # every rank's parity, and the bitmask as the all-gather delivers it
         red = torch.tensor([mismatches, accepted, expected], dtype=torch.int64, device=dev)
         dist.all_reduce(red)
         mismatches, accepted, expected = (int(x) for x in red.tolist())
@@ -795,7 +806,7 @@ def main():
         ostep = step_general if args.path == "keyed" else step_keyed
         ostep()
         torch.cuda.synchronize()
-        if world > 1:
+        if dist_on:
             dist.barrier()
         o_ms = []
         t1 = time.perf_counter()
@@ -803,10 +814,10 @@ def main():
             ostep()
             o_ms.append(eng.last_phases_ms())
         torch.cuda.synchronize()
-        if world > 1:
+        if dist_on:
             dist.barrier()
         o_el = time.perf_counter() - t1
-        if world > 1:
+        if dist_on:
             e = torch.tensor([o_el], dtype=torch.float64, device=dev)
             dist.all_reduce(e, op=dist.ReduceOp.MAX)
             o_el = float(e.item())
@@ -1013,7 +1024,7 @@ def main():
             "collective": collective,
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist_on:
         dist.barrier()
         dist.destroy_process_group()
     eng.close()

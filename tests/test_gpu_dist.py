@@ -68,3 +68,21 @@ def test_bench_gpus_2_without_launcher():
     assert p["mismatches_vs_construction"] == 0 and p["accepted"] == p["expected"] == 2 * 131072
     assert p["accepted_in_gathered_bitmask"] == 2 * 131072
     assert d["collective"]["all_gather_bitmask_ms"] > 0
+
+
+def test_bench_rccl_path_one_rank():
+    """The RCCL exchange path of bench.py (nccl process group with device_id,
+    the bitmask all-gather, the ballot all-reduce MAX on configs[4], barriers,
+    the max-over-ranks timing) run as a one-rank group on this box's GPU
+    (--force-dist): the calls SCALE makes at N = 2..8, exercised on ROCm."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--force-dist", "--config", "c4", "--requests", "131072",
+           "--signers", "64", "--key-window", "10", "--steps", "2", "--warmup", "1", "--no-cpu",
+           "--general-steps", "0", "--dropin-steps", "0", "--e2e-n", "0", "--e2e-c0", "0"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="4")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=ROOT, env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-8000:])
+    d = json.loads([x for x in r.stdout.splitlines() if x.startswith('{"metric')][-1])
+    assert d["n_gpus"] == 1 and d["parity"]["accepted_in_gathered_bitmask"] == 131072
+    assert d["collective"]["all_gather_bitmask_ms"] > 0 and d["collective"]["all_reduce_max_ballots_ms"] > 0
+    assert d["tally"]["counts_match"] and d["tally"]["quorum_match"]
