@@ -46,6 +46,23 @@
 #else
 #define EDV_BN_FP2 EDV_BN_NI
 #endif
+// 3: the Fp6 products inline too; 4: also the Fp12 squarings / products and the sparse line
+// product; 5: also the Miller loop's doubling / addition steps and the twist point's arithmetic
+#if EDV_BN_INLINE_LEVEL >= 3
+#define EDV_BN_FP6 EDV_HD
+#else
+#define EDV_BN_FP6 EDV_BN_NI
+#endif
+#if EDV_BN_INLINE_LEVEL >= 4
+#define EDV_BN_FP12 EDV_HD
+#else
+#define EDV_BN_FP12 EDV_BN_NI
+#endif
+#if EDV_BN_INLINE_LEVEL >= 5
+#define EDV_BN_ML EDV_HD
+#else
+#define EDV_BN_ML EDV_BN_NI
+#endif
 
 namespace edv {
 namespace bn {
@@ -336,7 +353,7 @@ EDV_HD void fp6_neg(fp6& r, const fp6& x) {
   fp2_neg(r.c2, x.c2);
 }
 // Karatsuba over v^3 = xi: 6 Fp2 products
-EDV_BN_NI void fp6_mul(fp6& r, const fp6& x, const fp6& y) {
+EDV_BN_FP6 void fp6_mul(fp6& r, const fp6& x, const fp6& y) {
   fp2 t0, t1, t2, s, u, c0, c1, c2;
   fp2_mul(t0, x.c0, y.c0);
   fp2_mul(t1, x.c1, y.c1);
@@ -409,7 +426,7 @@ EDV_HD bool fp12_isone(const fp12& x) {
   return fp2_eq(x.c0.c0, one) && fp2_iszero(x.c0.c1) && fp2_iszero(x.c0.c2) && fp2_iszero(x.c1.c0) &&
          fp2_iszero(x.c1.c1) && fp2_iszero(x.c1.c2);
 }
-EDV_BN_NI void fp12_mul(fp12& r, const fp12& x, const fp12& y) {  // 3 Fp6 products
+EDV_BN_FP12 void fp12_mul(fp12& r, const fp12& x, const fp12& y) {  // 3 Fp6 products
   fp6 t0, t1, s, u;
   fp6_mul(t0, x.c0, y.c0);
   fp6_mul(t1, x.c1, y.c1);
@@ -421,7 +438,7 @@ EDV_BN_NI void fp12_mul(fp12& r, const fp12& x, const fp12& y) {  // 3 Fp6 produ
   fp6_mul_v(t1, t1);
   fp6_add(r.c0, t0, t1);
 }
-EDV_BN_NI void fp12_sqr(fp12& r, const fp12& x) {  // complex squaring: 2 Fp6 products
+EDV_BN_FP12 void fp12_sqr(fp12& r, const fp12& x) {  // complex squaring: 2 Fp6 products
   fp6 t, s, u, ab;
   fp6_mul(ab, x.c0, x.c1);
   fp6_add(s, x.c0, x.c1);
@@ -461,7 +478,7 @@ EDV_HD void fp2_3t_p2z(fp2& r, const fp2& t, const fp2& z) {  // 3 t + 2 z
   fp2_dbl(d, d);
   fp2_add(r, d, t);
 }
-EDV_BN_NI void fp12_cyclo_sqr(fp12& r, const fp12& x) {
+EDV_BN_FP12 void fp12_cyclo_sqr(fp12& r, const fp12& x) {
   fp2 t0, t1, t2, t3, t4, t5, xt5;
   fp4_sqr(t0, t1, x.c0.c0, x.c1.c1);  // (1, w^3)
   fp4_sqr(t2, t3, x.c1.c0, x.c0.c2);  // (w, w^4)
@@ -515,7 +532,7 @@ EDV_BN_NI void fp12_frob(fp12& r, const fp12& x) {
 
 // f * line, line = l0 + (l1 + l2 v) w, l0, l1, l2 in Fp2: the sparse
 // product (15 Fp2 products instead of the 18 of fp12_mul)
-EDV_BN_NI void fp6_mul_01(fp6& r, const fp6& a, const fp2& b0, const fp2& b1) {  // a * (b0 + b1 v)
+EDV_BN_FP6 void fp6_mul_01(fp6& r, const fp6& a, const fp2& b0, const fp2& b1) {  // a * (b0 + b1 v)
   fp2 t0, t1, u, w2, c0, c1, c2;
   fp2_mul(t0, a.c0, b0);
   fp2_mul(t1, a.c1, b1);
@@ -533,7 +550,7 @@ EDV_BN_NI void fp6_mul_01(fp6& r, const fp6& a, const fp2& b0, const fp2& b1) { 
   r.c1 = c1;
   r.c2 = c2;
 }
-EDV_BN_NI void fp12_mul_line(fp12& f, const fp2& l0, const fp2& l1, const fp2& l2) {
+EDV_BN_FP12 void fp12_mul_line(fp12& f, const fp2& l0, const fp2& l1, const fp2& l2) {
   fp6 aA, bB, s;
   fp2_mul(aA.c0, f.c0.c0, l0);  // a * (l0, 0, 0)
   fp2_mul(aA.c1, f.c0.c1, l0);
@@ -670,7 +687,7 @@ EDV_HD void g2_inf(g2& r) {
   fp2_zero(r.Z);
 }
 EDV_HD bool g2_isinf(const g2& p) { return fp2_iszero(p.Z); }
-EDV_BN_NI void g2_dbl(g2& r, const g2& p) {
+EDV_BN_ML void g2_dbl(g2& r, const g2& p) {
   if (g2_isinf(p)) {
     r = p;
     return;
@@ -698,7 +715,7 @@ EDV_BN_NI void g2_dbl(g2& r, const g2& p) {
   fp2_dbl(C, C);
   fp2_sub(r.Y, t, C);
 }
-EDV_BN_NI void g2_add(g2& r, const g2& p, const g2& q) {
+EDV_BN_ML void g2_add(g2& r, const g2& p, const g2& q) {
   if (g2_isinf(p)) {
     r = q;
     return;
@@ -901,29 +918,49 @@ struct LineDirect {
   EDV_HDM void sqr(fp12& g) const { fp12_sqr(g, g); }
   EDV_HDM void mul_line(fp12& f, const fp2& l0, const fp2& l1, const fp2& l2) const { fp12_mul_line(f, l0, l1, l2); }
 };
+// The tangent line at T and T <- 2T in one pass (a = 0 Jacobian doubling, dbl-2009-l, sharing
+// X^2, Y^2 and Y Z with the line): 6 squarings + 5 products + 2 Fp scalings, against 8 + 6 + 2
+// with the line and g2_dbl apart; the same values bit for bit.
 template <class SP = LineDirect>
-EDV_BN_NI void miller_dbl(fp12& f, g2& T, const fp& xP, const fp& yP, SP sp = SP()) {
-  fp2 XX, YY, ZZ, u, l0, l1, l2, t;
-  fp2_sqr(XX, T.X);
-  fp2_sqr(YY, T.Y);
+EDV_BN_ML void miller_dbl(fp12& f, g2& T, const fp& xP, const fp& yP, SP sp = SP()) {
+  fp2 A, B, ZZ, YZ, E, l0, l1, l2, t;
+  fp2_sqr(A, T.X);
+  fp2_sqr(B, T.Y);
   fp2_sqr(ZZ, T.Z);
-  fp2_mul(l0, T.Y, T.Z);  // 2 Y Z^3 yP
-  fp2_mul(l0, l0, ZZ);
+  fp2_mul(YZ, T.Y, T.Z);
+  fp2_mul(l0, YZ, ZZ);  // 2 Y Z^3 yP
   fp2_dbl(l0, l0);
   fp2_mul_fp(l0, l0, yP);
-  fp2_dbl(u, XX);  // 3 X^2
-  fp2_add(u, u, XX);
-  fp2_mul(l1, u, ZZ);  // -3 X^2 Z^2 xP
+  fp2_dbl(E, A);  // E = 3 X^2
+  fp2_add(E, E, A);
+  fp2_mul(l1, E, ZZ);  // -3 X^2 Z^2 xP
   fp2_mul_fp(l1, l1, xP);
   fp2_neg(l1, l1);
-  fp2_mul(l2, u, T.X);  // 3 X^3 - 2 Y^2
-  fp2_dbl(t, YY);
+  fp2_mul(l2, E, T.X);  // 3 X^3 - 2 Y^2
+  fp2_dbl(t, B);
   fp2_sub(l2, l2, t);
   sp.mul_line(f, l0, l1, l2);
-  g2_dbl(T, T);
+  if (g2_isinf(T)) return;  // g2_dbl's infinity case: T stays
+  fp2 C, D, F;
+  fp2_sqr(C, B);
+  fp2_add(t, T.X, B);
+  fp2_sqr(t, t);
+  fp2_sub(t, t, A);
+  fp2_sub(t, t, C);
+  fp2_dbl(D, t);
+  fp2_sqr(F, E);
+  fp2_dbl(T.Z, YZ);
+  fp2_sub(t, F, D);
+  fp2_sub(T.X, t, D);
+  fp2_sub(t, D, T.X);
+  fp2_mul(t, E, t);
+  fp2_dbl(C, C);
+  fp2_dbl(C, C);
+  fp2_dbl(C, C);
+  fp2_sub(T.Y, t, C);
 }
 template <class SP = LineDirect>
-EDV_BN_NI void miller_add(fp12& f, g2& T, const fp2& xQ, const fp2& yQ, const fp& xP, const fp& yP, SP sp = SP()) {
+EDV_BN_ML void miller_add(fp12& f, g2& T, const fp2& xQ, const fp2& yQ, const fp& xP, const fp& yP, SP sp = SP()) {
   fp2 ZZ, ZZZ, theta, eps, k, t, l0, l1, l2;
   fp2_sqr(ZZ, T.Z);
   fp2_mul(ZZZ, ZZ, T.Z);
@@ -1029,27 +1066,36 @@ EDV_BN_NI void final_exp(fp12& r, const fp12& f, SQ sq = SQ()) {
   fp12_pow_x(b, a, sq);  // t^(x^2)
   fp12_pow_x(c, b, sq);  // t^(x^3)
   fp12_pow_small(c36, c, 36, sq);
+  // the small powers of a and b share their chains: b^6, b^12, b^18, b^30 and a^6, a^12, a^18
+  // from 6 squarings and 5 products (11 and 4 more as separate powers); the same exponents
+  fp12 b6, b12, b18, a6, a12;
+  sq(b6, b);
+  fp12_mul(b6, b6, b);  // b^3
+  sq(b6, b6);           // b^6
+  sq(b12, b6);
+  fp12_mul(b18, b12, b6);
+  sq(a6, a);
+  fp12_mul(a6, a6, a);  // a^3
+  sq(a6, a6);           // a^6
+  sq(a12, a6);
   // t^l0 = conj(c^36 b^30 a^18 t^2)
-  fp12_pow_small(y, b, 30, sq);
+  fp12_mul(y, b18, b12);  // b^30
   fp12_mul(y, y, c36);
-  fp12_pow_small(z, a, 18, sq);
+  fp12_mul(z, a12, a6);   // a^18
   fp12_mul(y, y, z);
   sq(z, t);
   fp12_mul(y, y, z);
   fp12 res;
   fp12_conj(res, y);
   // (t^l1)^p, t^l1 = conj(c^36 b^18 a^12) t
-  fp12_pow_small(y, b, 18, sq);
-  fp12_mul(y, y, c36);
-  fp12_pow_small(z, a, 12, sq);
-  fp12_mul(y, y, z);
+  fp12_mul(y, b18, c36);
+  fp12_mul(y, y, a12);
   fp12_conj(y, y);
   fp12_mul(y, y, t);
   fp12_frob(y, y);
   fp12_mul(res, res, y);
   // (t^l2)^(p^2), t^l2 = b^6 t
-  fp12_pow_small(y, b, 6, sq);
-  fp12_mul(y, y, t);
+  fp12_mul(y, b6, t);
   fp12_frob(y, y);
   fp12_frob(y, y);
   fp12_mul(res, res, y);
