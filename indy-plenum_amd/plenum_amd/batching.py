@@ -120,6 +120,30 @@ class _Memo:
 _NONE = object()
 
 
+class _MemoDeserialize:
+    """VerifyAheadMixin.deserializeMsg: on an instance, the memo's object for a
+    raw message it decoded (else the base class's decode); on the class (the
+    reference calls ZStack.deserializeMsg(...) as a static method, e.g.
+    plenum/test/input_validation/test_message_serialization.py:15), the base
+    class's static method itself."""
+
+    def __set_name__(self, owner, name):
+        self.owner, self.name = owner, name
+
+    def __get__(self, obj, objtype=None):
+        base = getattr(super(self.owner, objtype if objtype is not None else type(obj)), self.name)
+        if obj is None:
+            return base
+        memo = obj._va_memo
+        if memo is None:
+            return base
+
+        def deserialize(msg):
+            o = memo.take(msg)
+            return base(msg) if o is _NONE else o
+        return deserialize
+
+
 class VerifyAheadMixin:
     """Mix in front of a ZStack subclass (e.g. plenum.common.stacks.ClientZStack
     / NodeZStack).  The authenticator is the class attribute `authnr`
@@ -149,13 +173,7 @@ class VerifyAheadMixin:
         finally:
             self._va_memo = None
 
-    def deserializeMsg(self, msg):
-        memo = self._va_memo
-        if memo is not None:
-            obj = memo.take(msg)
-            if obj is not _NONE:
-                return obj
-        return super().deserializeMsg(msg)
+    deserializeMsg = _MemoDeserialize()
 
 
 _stack_classes = {}

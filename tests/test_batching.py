@@ -97,3 +97,36 @@ def test_verify_ahead_stack_binds_authenticator():
     st2 = verify_ahead_stack(Base, auth)(msgs=[(json.dumps(req), 1)], authnr=other)
     st2.processReceived(1)
     assert other.batches == [[req]] and len(auth.batches) == 1
+
+
+def test_memo_decode_edge_cases():
+    """The verify-ahead's decode memo: the same raw object twice in rxMsgs (the
+    second is decoded afresh, never the same dict twice), ping / pong entries
+    (left to the reference loop), an undecodable entry, and deserializeMsg on
+    the class (a static call, as the reference's own tests make)."""
+    from plenum_amd.batching import verify_ahead_stack
+    from plenum_amd.nodeloop import PING, NodeCounters, Stack
+
+    class Auth:
+        def __init__(self):
+            self.seen = []
+
+        def prefetch(self, reqs):
+            return len(reqs)
+
+        def authenticate(self, req):
+            self.seen.append(req)
+            return req["identifier"]
+    a = Auth()
+    cls = verify_ahead_stack(Stack, a)
+    assert cls.deserializeMsg('{"a": 1}') == {"a": 1}  # class-level: the base's static method
+    nc = NodeCounters()
+    st = cls(a, "node", nc)
+    req = {"identifier": "i", "reqId": 1, "operation": {"type": "1"}, "signature": "s"}
+    prop = json.dumps({"op": "PROPAGATE", "request": req, "senderClient": "c"})
+    batch = json.dumps({"op": "BATCH", "messages": [prop, PING.decode(), prop], "signature": None})
+    st.rxMsgs.extend([(prop, "n1"), (prop, "n1"), (PING, "n2"), ("{not json", "n3"), (batch, "n4")])
+    assert st.processReceived(10) == 5
+    assert len(a.seen) == 4 and all(r == req for r in a.seen)
+    assert len({id(r) for r in a.seen}) == 4  # every authenticate() got its own dict
+    assert st._va_memo is None
