@@ -2522,12 +2522,26 @@ int edv_verify_staged(edv_ctx* ctx, int keyed, const uint8_t* keys, uint64_t slo
       (r = ensure(ctx->b_sig, 64 * n)) || (r = ensure(ctx->d_bits[0], 8 * nwords)) ||
       (r = ensure_pinned(ctx->h_bits[0], 8 * nwords)))
     return r;
-  memcpy(ctx->h_key[0].p, keys, key_bytes * n);
-  memcpy(ctx->h_off[0].p, msg_start, 8 * n);
-  memcpy((char*)ctx->h_off[0].p + 8 * n, msg_end, 8 * n);
+  // the key ids and the spans straight from the caller's memory when it is pinned (the
+  // authenticator gathers the ids and the scan writes the spans, starts then ends, into
+  // edv_host_alloc blocks); else through the pinned staging, copied by the pooled threads
+  const bool keys_direct = pinned_range(keys, key_bytes * n);
+  const bool spans_direct = msg_end == msg_start + n && pinned_range(msg_start, 16 * n);
+  const void* src_key = keys;
+  const void* src_spans = msg_start;
+  if (!keys_direct) {
+    stage_copy(ctx->h_key[0].p, keys, key_bytes * n);
+    src_key = ctx->h_key[0].p;
+  }
+  if (!spans_direct) {
+    stage_copy(ctx->h_off[0].p, msg_start, 8 * n);
+    stage_copy((char*)ctx->h_off[0].p + 8 * n, msg_end, 8 * n);
+    src_spans = ctx->h_off[0].p;
+  }
+  ctx->last_direct = (keys_direct ? 2 : 0) | (spans_direct ? 8 : 0);
   hipStream_t cs = ctx->stream_copy, st = ctx->stream;
-  HIP_TRY(hipMemcpyAsync(ctx->d_key[0].p, ctx->h_key[0].p, key_bytes * n, hipMemcpyHostToDevice, cs));
-  HIP_TRY(hipMemcpyAsync(ctx->d_spans.p, ctx->h_off[0].p, 16 * n, hipMemcpyHostToDevice, cs));
+  HIP_TRY(hipMemcpyAsync(ctx->d_key[0].p, src_key, key_bytes * n, hipMemcpyHostToDevice, cs));
+  HIP_TRY(hipMemcpyAsync(ctx->d_spans.p, src_spans, 16 * n, hipMemcpyHostToDevice, cs));
   HIP_TRY(hipEventRecord(ctx->ev_h2d[0], cs));  // after every put queued before this call
   HIP_TRY(hipStreamWaitEvent(st, ctx->ev_h2d[0], 0));
   const uint8_t* stage = (const uint8_t*)ctx->d_stage.p;

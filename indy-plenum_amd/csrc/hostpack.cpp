@@ -1169,14 +1169,16 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
     return nullptr;
   }
   const bool slots = sig_slot == kSigSlot;
-  PyObject *out_sig = nullptr, *out_msg = nullptr;
+  PyObject *out_sig = nullptr, *out_msg = nullptr, *out_spans = nullptr;
   if (out != Py_None) {
-    if (!PyList_CheckExact(out) || PyList_GET_SIZE(out) != 2) {
-      PyErr_SetString(PyExc_TypeError, "out must be a list of two writable buffers (bytearray, pinned memory)");
+    if (!PyList_CheckExact(out) || PyList_GET_SIZE(out) < 2 || PyList_GET_SIZE(out) > 3) {
+      PyErr_SetString(PyExc_TypeError,
+                      "out must be a list of two (or, staged, three) writable buffers (bytearray, pinned memory)");
       return nullptr;
     }
     out_sig = PyList_GET_ITEM(out, 0);
     out_msg = PyList_GET_ITEM(out, 1);
+    if (PyList_GET_SIZE(out) == 3) out_spans = PyList_GET_ITEM(out, 2);
   }
   PyObject* fm = refs.fm = PySequence_Fast(msgs, "msgs must be a sequence");
   if (!fm) return nullptr;
@@ -1230,6 +1232,7 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
   // by chunk (each chunk's bytes contiguous, chunks in completion order; item spans say where)
   char* smsg = nullptr;
   uint64_t smsg_cap = 0;
+  uint64_t* spans_p = nullptr;  // staged: starts [n] then ends [n]
   std::atomic<uint64_t> scursor{0};
   std::atomic<bool> staged_ok{true};
   StageCopier copier;
@@ -1243,7 +1246,21 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
     smsg = (char*)view.buf;
     smsg_cap = (uint64_t)view.len;
     PyBuffer_Release(&view);  // the caller keeps the owner alive
-    S.spans.resize(2 * (size_t)n);
+    // the item spans go straight into out[2] when it holds 16 n bytes (the engine's pinned memory:
+    // edv_verify_staged then DMAs them with no copy), else into the scratch and a bytes result
+    spans_p = nullptr;
+    if (out_spans && out_spans != Py_None) {
+      if (PyObject_GetBuffer(out_spans, &view, PyBUF_WRITABLE | PyBUF_C_CONTIGUOUS) == 0) {
+        if ((uint64_t)view.len >= 16 * (uint64_t)n) spans_p = (uint64_t*)view.buf;
+        PyBuffer_Release(&view);
+      } else {
+        PyErr_Clear();
+      }
+    }
+    if (!spans_p) {
+      S.spans.resize(2 * (size_t)n);
+      spans_p = S.spans.data();
+    }
   }
   std::vector<std::vector<uint8_t>> sigs((size_t)t);
   for (int w = 0; w < t; ++w) {  // no-ops once a batch of this size has been seen
@@ -1272,7 +1289,7 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
       return;
     }
     uint64_t at = pos;
-    uint64_t* st0 = S.spans.data();
+    uint64_t* st0 = spans_p;
     uint64_t* en0 = st0 + n;
     for (Py_ssize_t i = a; i < b; ++i) {
       const ScanItem& x = it[(size_t)i];
@@ -1552,6 +1569,10 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
       fprintf(stderr, "scan (staged): n=%zd threads=%d  workers %.0f us, merge %.0f us, bookkeeping %.0f us\n", n, t,
               us(t_start, t_p1), us(t_p1, t_p2), us(t_p3, now()));
     }
+    if (spans_p != S.spans.data())  // written in place: the caller's buffer is the result
+      return Py_BuildValue("(y#y#NOOOy#O)", fast.data(), (Py_ssize_t)n, (const char*)uidx.data(),
+                           (Py_ssize_t)(uidx.size() * 4), ul, o_sig, out_msg, out_spans, shortv.data(), (Py_ssize_t)n,
+                           staged_ok.load() ? Py_True : Py_False);
     return Py_BuildValue("(y#y#NOOy#y#O)", fast.data(), (Py_ssize_t)n, (const char*)uidx.data(),
                          (Py_ssize_t)(uidx.size() * 4), ul, o_sig, out_msg, (const char*)S.spans.data(),
                          (Py_ssize_t)(S.spans.size() * 8), shortv.data(), (Py_ssize_t)n,
@@ -1889,10 +1910,9 @@ PyObject* py_gather_u32(PyObject*, PyObject* args) {
   // out: a bytearray reused from call to call (grown, never shrunk: a fresh 4 MB result per 1M
   // requests costs its page faults every batch); else a new bytearray of exactly n ids
   char* data = nullptr;
-  PyObject* ret = (out != Py_None && PyByteArray_CheckExact(out)) ? out_buffer(out, n * 4, &data)
-                                                                     : PyByteArray_FromStringAndSize(nullptr, n * 4);
+  PyObject* ret = out != Py_None ? out_buffer(out, n * 4, &data) : PyByteArray_FromStringAndSize(nullptr, n * 4);
   if (!ret) return nullptr;
-  if (!data) data = PyByteArray_AS_STRING(ret);
+  if (!data) data = PyByteArray_Check(ret) ? PyByteArray_AS_STRING(ret) : PyBytes_AS_STRING(ret);
   const uint32_t* t = (const uint32_t*)bt.buf;
   const uint32_t* ix = (const uint32_t*)bi.buf;
   uint32_t* o = (uint32_t*)data;
@@ -2123,8 +2143,8 @@ PyMethodDef kMethods[] = {
     {"repack_spans", py_repack_spans, METH_VARARGS,
      "repack_spans(buf, spans) -> (msgs, off): a staged scan's messages laid out contiguously with offsets"},
     {"gather_u32", py_gather_u32, METH_VARARGS,
-     "gather_u32(table, idx, out=None) -> bytearray: table[idx[i]] (uint32); out: a bytearray to grow and reuse "
-     "(slice the result to len(idx) * 4 bytes)"},
+     "gather_u32(table, idx, out=None) -> buffer: table[idx[i]] (uint32); out: a bytearray to grow and reuse, or "
+     "any writable buffer of len(idx) * 4 bytes or more (e.g. pinned memory); slice the result to len(idx) * 4"},
     {"results_ok", py_results_ok, METH_VARARGS,
      "results_ok(ok, short, uidx, uniq) -> (results, failed indices) of a steady-state batch"},
     {"results_from", py_results_from, METH_VARARGS,

@@ -673,11 +673,15 @@ class GpuAuthMixin:
         msg_cap = len(bufs[1])
         slot_base = (msg_cap + 255) // 256 * 256
         eng.stage_reserve(slot_base + n * slot)
+        spans_buf = self._pinned(eng, "pinned_spans", 16 * n)  # the scan writes the item spans here
         t0 = perf_counter()
-        scan = _scan_batch(msgs, [SIG], g.scan_threads, bufs, slot, 2, eng.stager(), slot_base)
+        scan = _scan_batch(msgs, [SIG], g.scan_threads, [bufs[0], bufs[1], spans_buf], slot, 2, eng.stager(),
+                           slot_base)
         t1 = perf_counter()
         fast_b, uidx_b, uniq, sig_o, msg_o, spans_b, short, staged_ok = scan
-        spans = np.frombuffer(spans_b, np.uint64)
+        if spans_b is spans_buf:
+            spans_b = memoryview(spans_b).cast("B")[:16 * n]
+        spans = np.frombuffer(spans_b, np.uint64, count=2 * n)
         ms, me = spans[:n], spans[n:]
         if not staged_ok:
             g.msg_bytes_per_item *= 1.5  # the next buffers are sized larger
@@ -694,12 +698,15 @@ class GpuAuthMixin:
             if any(i is None for i in ids):
                 ids = None
         if ids is None:  # not the steady state: contiguous messages, the ordinary path
+            del spans, ms, me
             msg_c, off_c = _repack_spans(msg_o, spans_b)
             return self._finish_scanned(msgs, (fast_b, uidx_b, uniq, sig_o, msg_c, off_c, short), slot, ukeys)
-        kid = np.frombuffer(_gather_u32(np.asarray(ids, np.uint32).tobytes(), uidx_b, g.kid_out), np.uint32, count=n)
+        kid_buf = self._pinned(eng, "pinned_kid", 4 * n)  # key ids straight into pinned memory: no copy
+        kid = np.frombuffer(_gather_u32(np.asarray(ids, np.uint32).tobytes(), uidx_b,
+                                        kid_buf if kid_buf is not None else g.kid_out), np.uint32, count=n)
         t2 = perf_counter()
         ok = np.asarray(eng.verify_staged(True, kid, slot_base, 0, ms, me), bool)
-        del kid
+        del kid, spans, ms, me, spans_b
         t3 = perf_counter()
         g.stats["batches"] += 1
         g.stats["batch_items"] += n
@@ -836,6 +843,24 @@ class GpuAuthMixin:
                 payload = res
             results += payload
         return results
+
+    def _pinned(self, eng, name, nbytes):
+        """A pinned host buffer of at least nbytes kept on the state under `name`
+        (engine.host_alloc; grown by half again when short, never shrunk), or
+        None without pinned memory."""
+        g = self._g
+        buf = g.__dict__.get(name)
+        if buf is not None and len(buf) >= nbytes:
+            return buf
+        alloc = getattr(eng, "host_alloc", None)
+        if alloc is None:
+            return None
+        try:
+            buf = alloc(max(int(nbytes * 1.25) + 4096, int(len(buf) * 1.5) if buf is not None else 0))
+        except Exception:
+            return None
+        g.__dict__[name] = buf
+        return buf
 
     def _scan_buffers(self, eng, n, slot):
         """The scan's output buffers for an n-request batch: the engine's pinned
