@@ -63,6 +63,13 @@ def launch_ranks(n, argv, poll_s=0.2):
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL across the rank processes
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
     rcs = [None] * n
+
+    def forward(signum, frame):  # a launcher stopped from outside stops its ranks too
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+        raise SystemExit(128 + signum)
+    signal.signal(signal.SIGTERM, forward)
     try:
         while any(rc is None for rc in rcs):
             for i, p in enumerate(procs):

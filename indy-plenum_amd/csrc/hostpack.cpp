@@ -2070,6 +2070,11 @@ PyObject* py_distinct_sm(PyObject*, PyObject* args) {
   const uint8_t* shortv = (const uint8_t*)bsh.buf;
   const uint32_t* uidx = (const uint32_t*)bu.buf;
   const uint8_t* fast = (const uint8_t*)bf.buf;
+  for (Py_ssize_t i = 0; i < n; ++i)
+    if (off[i + 1] < off[i]) {
+      PyErr_SetString(PyExc_ValueError, "offsets decrease");
+      return nullptr;
+    }
   if (n && off[n] > (uint64_t)bm.len) {
     PyErr_SetString(PyExc_ValueError, "offsets outside the message buffer");
     return nullptr;

@@ -163,3 +163,14 @@ def test_verify_ahead_node_loop(oracle, monkeypatch, n_nodes):
     want = [r["identifier"] for r in reqs]
     want[5], want[6] = "InvalidSignature", "UnknownIdentifier"
     assert [o[1] for o in nc.outcomes] == want * (n_nodes - 1) + want
+
+
+def test_distinct_sm_rejects_bad_offsets():
+    import numpy as np
+    sig = bytes(64 * 2)
+    off = np.array([0, 10, 5], np.uint64).tobytes()
+    with pytest.raises(ValueError):
+        _hostpack.distinct_sm(sig, bytes(20), off, bytes(2), bytes(8), b"\x01\x01")
+    off = np.array([0, 10, 30], np.uint64).tobytes()
+    with pytest.raises(ValueError):
+        _hostpack.distinct_sm(sig, bytes(20), off, bytes(2), bytes(8), b"\x01\x01")
