@@ -234,6 +234,19 @@ int edv_stage_reserve(edv_ctx *ctx, uint64_t bytes);
 int edv_stage_put(edv_ctx *ctx, const void *src, uint64_t nbytes, uint64_t off);
 int edv_verify_staged(edv_ctx *ctx, int keyed, const uint8_t *keys, uint64_t slot_off, uint64_t msg_base,
                       const uint64_t *msg_start, const uint64_t *msg_end, uint64_t n, uint8_t *accept_bits);
+/* Two batches in flight (a pipeline of staged batches): edv_stage_select(ctx, set) makes
+ * staging set 0 or 1 current for the next edv_stage_reserve / edv_stage_put /
+ * edv_verify_staged_submit; each set has its own staging buffer and verdict buffers, so batch
+ * k + 1 is staged into one set while batch k's kernels still read the other.
+ * edv_verify_staged_submit queues the verify of the staged batch and returns a ticket at once;
+ * edv_verify_staged_collect(ctx, ticket, accept_bits) waits for it and writes the bits.
+ * A set holding an uncollected submission refuses reserve and submit (EDV_EINVAL).
+ * edv_verify_staged == submit + collect.  Replaces, like edv_verify_staged, libsodium's
+ * crypto_sign_open per request (nacl_wrappers.py:108). */
+int edv_stage_select(edv_ctx *ctx, int set);
+int edv_verify_staged_submit(edv_ctx *ctx, int keyed, const uint8_t *keys, uint64_t slot_off, uint64_t msg_base,
+                             const uint64_t *msg_start, const uint64_t *msg_end, uint64_t n, uint64_t *ticket);
+int edv_verify_staged_collect(edv_ctx *ctx, uint64_t ticket, uint8_t *accept_bits);
 
 /* Signature slots: the host-pointer verifies below take, instead of sig64,
  * n slots of EDV_SIG_SLOT96 bytes, so that the base58 decode of the request

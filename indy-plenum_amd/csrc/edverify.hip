@@ -1458,10 +1458,20 @@ struct edv_ctx {
   // Staged inputs (edv_stage_reserve / edv_stage_put / edv_verify_staged): a device buffer the
   // caller fills piece by piece from pinned memory while it still produces the rest; the puts
   // queue on stream_copy (any thread, under stage_mu) and edv_verify_staged orders after them
-  Buf d_stage;
+  // Two staging sets (edv_stage_select): batch k + 1 is staged into one set while batch k's
+  // kernels still read the other (edv_verify_staged_submit / _collect); each set has its
+  // own staging buffer, inputs, verdict buffers and completion event.
+  static constexpr int kSets = 2;
+  int cur_set = 0;
+  Buf d_stage_set[kSets];
   std::mutex stage_mu;
   int stage_err = 0;  // first failed put since the last reserve (reported by edv_verify_staged)
-  Buf d_spans;        // message starts and ends of a staged verify [2][n]
+  Buf d_spans[kSets];  // message starts and ends of a staged verify [2][n]
+  Buf s_sig[kSets], s_key[kSets], s_bits[kSets];  // device: decoded signatures, key ids, accept words
+  Buf sh_key[kSets], sh_off[kSets], sh_bits[kSets];  // pinned: staging of non-pinned inputs, verdicts
+  hipEvent_t ev_sh2d[kSets] = {}, ev_sdone[kSets] = {};
+  uint64_t set_ticket[kSets] = {}, set_n[kSets] = {};  // the uncollected submission holding each set
+  Buf& d_stage() { return d_stage_set[cur_set]; }
 };
 
 namespace {
@@ -2469,12 +2479,23 @@ int edv_stage_reserve(edv_ctx* ctx, uint64_t bytes) {
   int r = set_device(ctx);
   if (r) return r;
   std::lock_guard<std::mutex> lk(ctx->stage_mu);
+  if (ctx->set_ticket[ctx->cur_set])
+    return set_err(EDV_EINVAL, "staging set %d holds an uncollected submission", ctx->cur_set);
   ctx->stage_err = 0;
-  if (ctx->d_stage.cap < bytes) {
+  if (ctx->d_stage().cap < bytes) {
     HIP_TRY(hipStreamSynchronize(ctx->stream_copy));  // earlier puts may still write the old buffer
     HIP_TRY(hipStreamSynchronize(ctx->stream));       // ... and earlier verifies read it
-    if ((r = ensure(ctx->d_stage, bytes))) return r;
+    if ((r = ensure(ctx->d_stage(), bytes))) return r;
   }
+  return 0;
+}
+
+int edv_stage_select(edv_ctx* ctx, int set) {
+  int r = set_device(ctx);
+  if (r) return r;
+  if (set < 0 || set >= edv_ctx::kSets) return set_err(EDV_EINVAL, "staging set %d (0 or 1)", set);
+  std::lock_guard<std::mutex> lk(ctx->stage_mu);
+  ctx->cur_set = set;
   return 0;
 }
 
@@ -2483,84 +2504,117 @@ int edv_stage_put(edv_ctx* ctx, const void* src, uint64_t nbytes, uint64_t off) 
   std::lock_guard<std::mutex> lk(ctx->stage_mu);
   if (!nbytes) return 0;
   int r = 0;
-  if (!src || off > ctx->d_stage.cap || nbytes > ctx->d_stage.cap - off)
+  if (!src || off > ctx->d_stage().cap || nbytes > ctx->d_stage().cap - off)
     r = set_err(EDV_EINVAL, "stage_put [%llu, +%llu) outside the %llu-byte staging buffer", (unsigned long long)off,
-                (unsigned long long)nbytes, (unsigned long long)ctx->d_stage.cap);
+                (unsigned long long)nbytes, (unsigned long long)ctx->d_stage().cap);
   else if (!pinned_range(src, nbytes))
     r = set_err(EDV_EINVAL, "stage_put source is not edv_host_alloc memory");
   else if (hipSetDevice(ctx->device) != hipSuccess ||
-           hipMemcpyAsync((char*)ctx->d_stage.p + off, src, nbytes, hipMemcpyHostToDevice, ctx->stream_copy) !=
+           hipMemcpyAsync((char*)ctx->d_stage().p + off, src, nbytes, hipMemcpyHostToDevice, ctx->stream_copy) !=
                hipSuccess)
     r = set_err(EDV_EHIP, "stage_put copy failed");
   if (r && !ctx->stage_err) ctx->stage_err = r;
   return r;
 }
 
-int edv_verify_staged(edv_ctx* ctx, int keyed, const uint8_t* keys, uint64_t slot_off, uint64_t msg_base,
-                      const uint64_t* msg_start, const uint64_t* msg_end, uint64_t n, uint8_t* accept_bits) {
+int edv_verify_staged_submit(edv_ctx* ctx, int keyed, const uint8_t* keys, uint64_t slot_off, uint64_t msg_base,
+                             const uint64_t* msg_start, const uint64_t* msg_end, uint64_t n, uint64_t* ticket) {
   int r = set_device(ctx);
   if (r) return r;
-  if (n && (!keys || !msg_start || !msg_end || !accept_bits)) return set_err(EDV_EINVAL, "null pointer");
+  if (!ticket || (n && (!keys || !msg_start || !msg_end))) return set_err(EDV_EINVAL, "null pointer");
+  const int set = ctx->cur_set;
   {
     std::lock_guard<std::mutex> lk(ctx->stage_mu);
     if (ctx->stage_err) return set_err(ctx->stage_err, "an earlier stage_put failed");
+    if (ctx->set_ticket[set]) return set_err(EDV_EINVAL, "staging set %d holds an uncollected submission", set);
   }
-  if (!n) return 0;
-  if (keyed && ctx->key_count == 0) return set_err(EDV_EINVAL, "no registered keys");
-  const uint64_t cap = ctx->d_stage.cap;
-  if (slot_off > cap || n > (cap - slot_off) / EDV_SIG_SLOT96) return set_err(EDV_EINVAL, "slots outside staging");
-  for (uint64_t i = 0; i < n; ++i)  // the kernels read msg_base + [start, end): inside the staging buffer
-    if (msg_start[i] > msg_end[i] || msg_end[i] > cap - msg_base)
-      return set_err(EDV_EINVAL, "message span %llu outside staging", (unsigned long long)i);
+  if (keyed && n && ctx->key_count == 0) return set_err(EDV_EINVAL, "no registered keys");
+  const uint64_t cap = ctx->d_stage().cap;
+  if (n && (slot_off > cap || n > (cap - slot_off) / EDV_SIG_SLOT96)) return set_err(EDV_EINVAL, "slots outside staging");
+  uint64_t bad = 0;  // the kernels read msg_base + [start, end): inside the staging buffer
+  for (uint64_t i = 0; i < n; ++i) bad |= (uint64_t)(msg_start[i] > msg_end[i]) | (uint64_t)(msg_end[i] > cap - msg_base);
+  if (bad) return set_err(EDV_EINVAL, "a message span outside staging");
   const uint64_t key_bytes = keyed ? 4 : 32, nwords = div_up(n, 64);
-  // submissions still holding the slot-0 buffers finish (and hand over their verdicts) before the
-  // buffers below may be reallocated
-  for (int sl = 0; sl < edv_ctx::kSlots; ++sl)
-    if ((r = drain_slot(ctx, sl))) return r;
-  if ((r = ensure_pinned(ctx->h_key[0], key_bytes * n)) || (r = ensure_pinned(ctx->h_off[0], 16 * n)) ||
-      (r = ensure(ctx->d_key[0], key_bytes * n)) || (r = ensure(ctx->d_spans, 16 * n)) ||
-      (r = ensure(ctx->b_sig, 64 * n)) || (r = ensure(ctx->d_bits[0], 8 * nwords)) ||
-      (r = ensure_pinned(ctx->h_bits[0], 8 * nwords)))
+  if ((r = ensure_pinned(ctx->sh_bits[set], 8 * nwords + 8)) || (r = ensure(ctx->s_key[set], key_bytes * n)) ||
+      (r = ensure(ctx->d_spans[set], 16 * n)) || (r = ensure(ctx->s_sig[set], 64 * n)) ||
+      (r = ensure(ctx->s_bits[set], 8 * nwords)))
     return r;
-  // the key ids and the spans straight from the caller's memory when it is pinned (the
-  // authenticator gathers the ids and the scan writes the spans, starts then ends, into
-  // edv_host_alloc blocks); else through the pinned staging, copied by the pooled threads
-  const bool keys_direct = pinned_range(keys, key_bytes * n);
-  const bool spans_direct = msg_end == msg_start + n && pinned_range(msg_start, 16 * n);
-  const void* src_key = keys;
-  const void* src_spans = msg_start;
-  if (!keys_direct) {
-    stage_copy(ctx->h_key[0].p, keys, key_bytes * n);
-    src_key = ctx->h_key[0].p;
+  const uint64_t tk = ctx->next_ticket++;
+  if (n) {
+    // the key ids and the spans straight from the caller's memory when it is pinned (the
+    // authenticator gathers the ids and the scan writes the spans, starts then ends, into
+    // edv_host_alloc blocks); else through the set's pinned staging, copied by the pooled threads
+    const bool keys_direct = pinned_range(keys, key_bytes * n);
+    const bool spans_direct = msg_end == msg_start + n && pinned_range(msg_start, 16 * n);
+    const void* src_key = keys;
+    const void* src_spans = msg_start;
+    if (!keys_direct) {
+      if ((r = ensure_pinned(ctx->sh_key[set], key_bytes * n))) return r;
+      stage_copy(ctx->sh_key[set].p, keys, key_bytes * n);
+      src_key = ctx->sh_key[set].p;
+    }
+    if (!spans_direct) {
+      if ((r = ensure_pinned(ctx->sh_off[set], 16 * n))) return r;
+      stage_copy(ctx->sh_off[set].p, msg_start, 8 * n);
+      stage_copy((char*)ctx->sh_off[set].p + 8 * n, msg_end, 8 * n);
+      src_spans = ctx->sh_off[set].p;
+    }
+    ctx->last_direct = (keys_direct ? 2 : 0) | (spans_direct ? 8 : 0);
+    hipStream_t cs = ctx->stream_copy, st = ctx->stream;
+    HIP_TRY(hipMemcpyAsync(ctx->s_key[set].p, src_key, key_bytes * n, hipMemcpyHostToDevice, cs));
+    HIP_TRY(hipMemcpyAsync(ctx->d_spans[set].p, src_spans, 16 * n, hipMemcpyHostToDevice, cs));
+    HIP_TRY(hipEventRecord(ctx->ev_sh2d[set], cs));  // after every put queued before this call
+    HIP_TRY(hipStreamWaitEvent(st, ctx->ev_sh2d[set], 0));
+    const uint8_t* stage = (const uint8_t*)ctx->d_stage().p;
+    hipLaunchKernelGGL(edv_b58_sig_kernel, dim3((uint32_t)div_up(n, kBlock)), dim3(kBlock), 0, st, stage + slot_off,
+                       n, (uint8_t*)ctx->s_sig[set].p);
+    HIP_TRY(hipGetLastError());
+    const uint64_t* ms = (const uint64_t*)ctx->d_spans[set].p;
+    set_bucketing(ctx, false);
+    if (keyed && n <= ctx->small_max)
+      r = launch_small(ctx, ctx->s_sig[set].p, ctx->s_key[set].p, stage + msg_base, ms, ms + n, n,
+                       ctx->s_bits[set].p, st);
+    else
+      r = launch_pipeline(ctx, keyed != 0, ctx->s_sig[set].p, ctx->s_key[set].p, stage + msg_base, ms, ms + n, n,
+                          ctx->s_bits[set].p, st);
+    if (r) return r;
+    HIP_TRY(hipMemcpyAsync(ctx->sh_bits[set].p, ctx->s_bits[set].p, 8 * nwords, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipEventRecord(ctx->ev_sdone[set], st));
   }
-  if (!spans_direct) {
-    stage_copy(ctx->h_off[0].p, msg_start, 8 * n);
-    stage_copy((char*)ctx->h_off[0].p + 8 * n, msg_end, 8 * n);
-    src_spans = ctx->h_off[0].p;
-  }
-  ctx->last_direct = (keys_direct ? 2 : 0) | (spans_direct ? 8 : 0);
-  hipStream_t cs = ctx->stream_copy, st = ctx->stream;
-  HIP_TRY(hipMemcpyAsync(ctx->d_key[0].p, src_key, key_bytes * n, hipMemcpyHostToDevice, cs));
-  HIP_TRY(hipMemcpyAsync(ctx->d_spans.p, src_spans, 16 * n, hipMemcpyHostToDevice, cs));
-  HIP_TRY(hipEventRecord(ctx->ev_h2d[0], cs));  // after every put queued before this call
-  HIP_TRY(hipStreamWaitEvent(st, ctx->ev_h2d[0], 0));
-  const uint8_t* stage = (const uint8_t*)ctx->d_stage.p;
-  hipLaunchKernelGGL(edv_b58_sig_kernel, dim3((uint32_t)div_up(n, kBlock)), dim3(kBlock), 0, st, stage + slot_off, n,
-                     (uint8_t*)ctx->b_sig.p);
-  HIP_TRY(hipGetLastError());
-  const uint64_t* ms = (const uint64_t*)ctx->d_spans.p;
-  set_bucketing(ctx, false);
-  if (keyed && n <= ctx->small_max)
-    r = launch_small(ctx, ctx->b_sig.p, ctx->d_key[0].p, stage + msg_base, ms, ms + n, n, ctx->d_bits[0].p, st);
-  else
-    r = launch_pipeline(ctx, keyed != 0, ctx->b_sig.p, ctx->d_key[0].p, stage + msg_base, ms, ms + n, n,
-                        ctx->d_bits[0].p, st);
-  if (r) return r;
-  HIP_TRY(hipMemcpyAsync(ctx->h_bits[0].p, ctx->d_bits[0].p, 8 * nwords, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
-  memcpy(accept_bits, ctx->h_bits[0].p, (size_t)((n + 7) / 8));
-  if (n & 7) accept_bits[n / 8] &= (uint8_t)((1u << (n & 7)) - 1);
+  std::lock_guard<std::mutex> lk(ctx->stage_mu);
+  ctx->set_ticket[set] = tk;
+  ctx->set_n[set] = n;
+  *ticket = tk;
   return 0;
+}
+
+int edv_verify_staged_collect(edv_ctx* ctx, uint64_t ticket, uint8_t* accept_bits) {
+  int r = set_device(ctx);
+  if (r) return r;
+  int set = -1;
+  for (int k = 0; k < edv_ctx::kSets; ++k)
+    if (ticket && ctx->set_ticket[k] == ticket) set = k;
+  if (set < 0) return set_err(EDV_EINVAL, "no staged submission %llu", (unsigned long long)ticket);
+  const uint64_t n = ctx->set_n[set];
+  if (n && !accept_bits) return set_err(EDV_EINVAL, "null pointer");
+  if (n) {
+    HIP_TRY(hipEventSynchronize(ctx->ev_sdone[set]));
+    memcpy(accept_bits, ctx->sh_bits[set].p, (size_t)((n + 7) / 8));
+    if (n & 7) accept_bits[n / 8] &= (uint8_t)((1u << (n & 7)) - 1);
+  }
+  std::lock_guard<std::mutex> lk(ctx->stage_mu);
+  ctx->set_ticket[set] = 0;
+  ctx->set_n[set] = 0;
+  return 0;
+}
+
+int edv_verify_staged(edv_ctx* ctx, int keyed, const uint8_t* keys, uint64_t slot_off, uint64_t msg_base,
+                      const uint64_t* msg_start, const uint64_t* msg_end, uint64_t n, uint8_t* accept_bits) {
+  if (n && !accept_bits) return set_err(EDV_EINVAL, "null pointer");
+  uint64_t ticket = 0;
+  int r = edv_verify_staged_submit(ctx, keyed, keys, slot_off, msg_base, msg_start, msg_end, n, &ticket);
+  if (r) return r;
+  return edv_verify_staged_collect(ctx, ticket, accept_bits);
 }
 
 int edv_verify_submit(edv_ctx* ctx, int keyed, const uint8_t* sig, int sig_format, const uint8_t* keys,
@@ -2669,6 +2723,10 @@ edv_ctx* edv_create(int device) {
     if ((e = hipEventCreateWithFlags(&ctx->ev_kfork[sb], hipEventDisableTiming)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&ctx->ev_kjoin[sb], hipEventDisableTiming)) != hipSuccess)
       return fail("hipEventCreate", e);
+  for (int k = 0; k < edv_ctx::kSets; ++k)
+    if ((e = hipEventCreateWithFlags(&ctx->ev_sh2d[k], hipEventDisableTiming)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&ctx->ev_sdone[k], hipEventDisableTiming)) != hipSuccess)
+      return fail("hipEventCreate", e);
   for (int k = 0; k < edv_ctx::kSlots; ++k)
     if ((e = hipEventCreateWithFlags(&ctx->ev_h2d[k], hipEventDisableTiming)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&ctx->ev_done[k], hipEventDisableTiming)) != hipSuccess)
@@ -2744,9 +2802,15 @@ void edv_destroy(edv_ctx* ctx) {
   if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
   if (ctx->stream_key) (void)hipStreamSynchronize(ctx->stream_key);
   if (ctx->stream_build) (void)hipStreamSynchronize(ctx->stream_build);
-  for (edv_ctx::Buf* b : {&ctx->b_sig, &ctx->b_pk, &ctx->b_msg, &ctx->b_off, &ctx->b_bits, &ctx->b_aux, &ctx->b_build,
-                          &ctx->d_stage, &ctx->d_spans})
+  for (edv_ctx::Buf* b : {&ctx->b_sig, &ctx->b_pk, &ctx->b_msg, &ctx->b_off, &ctx->b_bits, &ctx->b_aux, &ctx->b_build})
     free_buf(*b);
+  for (int k = 0; k < edv_ctx::kSets; ++k) {
+    for (edv_ctx::Buf* b : {&ctx->d_stage_set[k], &ctx->d_spans[k], &ctx->s_sig[k], &ctx->s_key[k], &ctx->s_bits[k],
+                            &ctx->sh_key[k], &ctx->sh_off[k], &ctx->sh_bits[k]})
+      free_buf(*b);
+    if (ctx->ev_sh2d[k]) (void)hipEventDestroy(ctx->ev_sh2d[k]);
+    if (ctx->ev_sdone[k]) (void)hipEventDestroy(ctx->ev_sdone[k]);
+  }
   for (edv_ctx::BuildEv& b : ctx->builds) (void)hipEventDestroy(b.ev);
   for (hipEvent_t f : ctx->ev_fence)
     if (f) (void)hipEventDestroy(f);

@@ -653,7 +653,7 @@ class GpuAuthMixin:
                 return self._authenticate_streamed(msgs, eng, slot, bufs)
             return self._authenticate_batch_scanned_into(msgs, bufs, slot)
 
-    def _authenticate_staged(self, msgs, eng, slot, bufs):
+    def _authenticate_staged(self, msgs, eng, slot, bufs, staging_set=0, defer=False):
         """A large batch whose PCIe copy runs under its scan: the native scan's
         workers place each 4k-request chunk's messages at a bump cursor in the
         engine's pinned memory and queue that chunk's messages and signature
@@ -665,15 +665,21 @@ class GpuAuthMixin:
         repacks its messages contiguously and takes the ordinary path (same
         verdicts).  None when the scan could not stage (the pinned buffer
         was too small for this batch, or items needed the interpreter): the
-        caller scans again the ordinary way."""
+        caller scans again the ordinary way.  staging_set / defer: the
+        pipeline of authenticate_batches -- staged into that set of the
+        engine's (and this authenticator's) buffers, and in the steady state a
+        callable returning the results once the kernels are collected."""
         import numpy as np
         from time import perf_counter
         g = self._g
         n = len(msgs)
         msg_cap = len(bufs[1])
         slot_base = (msg_cap + 255) // 256 * 256
+        if hasattr(eng, "stage_select"):
+            eng.stage_select(staging_set)
         eng.stage_reserve(slot_base + n * slot)
-        spans_buf = self._pinned(eng, "pinned_spans", 16 * n)  # the scan writes the item spans here
+        sfx = "" if staging_set == 0 else str(staging_set)
+        spans_buf = self._pinned(eng, "pinned_spans" + sfx, 16 * n)  # the scan writes the item spans here
         t0 = perf_counter()
         scan = _scan_batch(msgs, [SIG], g.scan_threads, [bufs[0], bufs[1], spans_buf], slot, 2, eng.stager(),
                            slot_base)
@@ -701,23 +707,75 @@ class GpuAuthMixin:
             del spans, ms, me
             msg_c, off_c = _repack_spans(msg_o, spans_b)
             return self._finish_scanned(msgs, (fast_b, uidx_b, uniq, sig_o, msg_c, off_c, short), slot, ukeys)
-        kid_buf = self._pinned(eng, "pinned_kid", 4 * n)  # key ids straight into pinned memory: no copy
+        kid_buf = self._pinned(eng, "pinned_kid" + sfx, 4 * n)  # key ids straight into pinned memory: no copy
         kid = np.frombuffer(_gather_u32(np.asarray(ids, np.uint32).tobytes(), uidx_b,
                                         kid_buf if kid_buf is not None else g.kid_out), np.uint32, count=n)
         t2 = perf_counter()
-        ok = np.asarray(eng.verify_staged(True, kid, slot_base, 0, ms, me), bool)
-        del kid, spans, ms, me, spans_b
-        t3 = perf_counter()
         g.stats["batches"] += 1
         g.stats["batch_items"] += n
         g.stats["keyed_items"] += n
-        results, failed = _results_ok(ok, short, uidx_b, uniq)
-        for i in failed:
-            results[i] = InvalidSignature()
-        t4 = perf_counter()
-        g.last_breakdown = {"scan_and_copies": (t1 - t0) * 1e3, "keys_and_ids": (t2 - t1) * 1e3,
-                            "verify_wait": (t3 - t2) * 1e3, "verdicts": (t4 - t3) * 1e3}
-        return results
+
+        def verdicts(ok, t3):
+            results, failed = _results_ok(ok, short, uidx_b, uniq)
+            for i in failed:
+                results[i] = InvalidSignature()
+            t4 = perf_counter()
+            g.last_breakdown = {"scan_and_copies": (t1 - t0) * 1e3, "keys_and_ids": (t2 - t1) * 1e3,
+                                "verify_wait": (t3 - t2) * 1e3, "verdicts": (t4 - t3) * 1e3}
+            return results
+        if defer:  # the kernels run while the caller goes on (its next batch's scan)
+            handle = eng.verify_staged_submit(True, kid, slot_base, 0, ms, me)
+            t2 = perf_counter()
+            del kid, spans, ms, me, spans_b
+
+            def finish():
+                with _engine_lock(eng):
+                    ok = np.asarray(eng.verify_staged_collect(handle), bool)
+                return verdicts(ok, perf_counter())
+            return finish
+        ok = np.asarray(eng.verify_staged(True, kid, slot_base, 0, ms, me), bool)
+        del kid, spans, ms, me, spans_b
+        return verdicts(ok, perf_counter())
+
+    def authenticate_batches(self, batches):
+        """authenticate_batch over an iterable of batches, yielding each batch's
+        result list in order, with two batches in flight: batch k + 1's host
+        scan (and its PCIe copy, staged under it) runs while batch k's kernels
+        run on the GPU -- the engine's two staging sets (edv_stage_select,
+        edv_verify_staged_submit / _collect) and two sets of this
+        authenticator's pinned buffers alternate.  A node verifying drain after
+        drain ahead of handling them gets the same.  Batches outside the
+        staged steady state (small, or items the scan leaves to Python, or
+        keys not yet built) are finished synchronously, after the batch in
+        flight; every outcome equals authenticate_batch's.  Other calls on
+        this authenticator must not interleave with an unfinished iteration."""
+        eng = self._engine()
+        slot = _SIG_SLOT if getattr(eng, "supports_sig_slots", False) else 64
+        can = (self._g.stage and _scan_batch is not None and _repack_spans is not None and slot == _SIG_SLOT and
+               getattr(eng, "supports_staging", False) and hasattr(eng, "verify_staged_submit") and
+               self._native_host_steps())
+        pending = None
+        k = 0
+        for msgs in batches:
+            res = None
+            if can and len(msgs) >= _STAGE_MIN_BATCH:
+                with _engine_lock(eng):
+                    s = k % 2
+                    bufs = self._scan_buffers(eng, len(msgs), slot, s)
+                    if bufs is not self._g.scan_out:
+                        res = self._authenticate_staged(msgs, eng, slot, bufs, staging_set=s, defer=True)
+            if callable(res):
+                if pending is not None:
+                    yield pending()
+                pending = res
+                k += 1
+                continue
+            if pending is not None:  # the batch in flight first (its staging set is free after)
+                yield pending()
+                pending = None
+            yield res if res is not None else self.authenticate_batch(msgs)
+        if pending is not None:
+            yield pending()
 
     def _authenticate_streamed(self, msgs, eng, slot, bufs):
         """A large batch whose pack overlaps its DMA: one scan of the whole
@@ -862,16 +920,27 @@ class GpuAuthMixin:
         g.__dict__[name] = buf
         return buf
 
-    def _scan_buffers(self, eng, n, slot):
+    def _scan_buffers(self, eng, n, slot, staging_set=0):
         """The scan's output buffers for an n-request batch: the engine's pinned
         host memory (host_alloc) when it has some -- the GPU call then copies
         from them with no staging copy -- grown ahead of need (never shrunk),
-        else the reused bytearrays."""
+        else the reused bytearrays.  staging_set 1: the second set of the
+        pipeline (authenticate_batches)."""
         g = self._g
         alloc = getattr(eng, "host_alloc", None)
         if alloc is None or n < _PINNED_MIN_BATCH:
             return g.scan_out
         need = (n * slot, int(n * g.msg_bytes_per_item * 1.25) + (64 << 10))
+        if staging_set:
+            bufs = g.__dict__.get("pinned_out1")
+            if bufs is None or any(len(b) < k for b, k in zip(bufs, need)):
+                old = [len(b) for b in bufs] if bufs else [0, 0]
+                try:
+                    bufs = [alloc(max(k, int(o * 1.5))) for k, o in zip(need, old)]
+                except Exception:
+                    return g.scan_out
+                g.__dict__["pinned_out1"] = bufs
+            return bufs
         bufs = g.pinned_out
         if bufs is None or any(len(b) < k for b, k in zip(bufs, need)):
             old = [len(b) for b in bufs] if bufs else [0, 0]

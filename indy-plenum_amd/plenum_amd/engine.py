@@ -241,6 +241,32 @@ class EdVerifyEngine:
                                           _ptr(ms), _ptr(me), n, _ptr(bits) if n else ctypes.c_void_p(1)))
         return unpack_bits(bits, n)
 
+    def stage_select(self, staging_set):
+        """Make staging set 0 or 1 current (edv_stage_select): batch k + 1 is
+        staged into one set while batch k's kernels read the other."""
+        check(self._lib.edv_stage_select(self._ctx, int(staging_set)))
+
+    def verify_staged_submit(self, keyed, keys, slot_off, msg_base, msg_start, msg_end):
+        """edv_verify_staged without the wait: a handle for verify_staged_collect.
+        The inputs must stay untouched until the collect."""
+        keys = np.ascontiguousarray(keys, dtype=np.uint32) if keyed else _u8(keys, 32)
+        ms = np.ascontiguousarray(msg_start, dtype=np.uint64)
+        me = np.ascontiguousarray(msg_end, dtype=np.uint64)
+        n = ms.shape[0]
+        if keys.shape[0] != n or me.shape[0] != n:
+            raise ValueError("shape mismatch: keys %d, starts %d, ends %d" % (keys.shape[0], n, me.shape[0]))
+        ticket = ctypes.c_uint64()
+        check(self._lib.edv_verify_staged_submit(self._ctx, 1 if keyed else 0, _ptr(keys), int(slot_off),
+                                                 int(msg_base), _ptr(ms), _ptr(me), n, ctypes.byref(ticket)))
+        return (ticket.value, n, (keys, ms, me))
+
+    def verify_staged_collect(self, handle):
+        """The verdicts of a verify_staged_submit (edv_verify_staged_collect)."""
+        ticket, n, _keep = handle
+        bits = np.zeros((n + 7) // 8, dtype=np.uint8)
+        check(self._lib.edv_verify_staged_collect(self._ctx, ticket, _ptr(bits) if n else ctypes.c_void_p(1)))
+        return unpack_bits(bits, n)
+
     def host_alloc(self, nbytes):
         """nbytes of pinned host memory (edv_host_alloc) as a writable ctypes
         array; host-pointer verifies copy inputs inside it to the device with no

@@ -251,12 +251,37 @@ class StagingOracleEngine(OracleEngine):
     def __init__(self, lib=None):
         super().__init__(lib)
         self._put = ctypes.CDLL(os.path.join(ROOT, "oracle", "_build", "libstage_double.so")).stage_double_put
-        self.stage = (ctypes.c_ubyte * 0)()
+        self.sets = [(ctypes.c_ubyte * 0)(), (ctypes.c_ubyte * 0)()]  # edv_stage_select's two staging sets
+        self.cur = 0
+        self.held = [None, None]  # the uncollected submission of each set
         self.staged_calls = 0
+        self.submits_staged = 0
+
+    @property
+    def stage(self):
+        return self.sets[self.cur]
+
+    def stage_select(self, staging_set):
+        assert staging_set in (0, 1)
+        self.cur = staging_set
 
     def stage_reserve(self, nbytes):
+        assert self.held[self.cur] is None, "staging set %d holds an uncollected submission" % self.cur
         if len(self.stage) < nbytes:
-            self.stage = (ctypes.c_ubyte * int(nbytes))()
+            self.sets[self.cur] = (ctypes.c_ubyte * int(nbytes))()
+
+    def verify_staged_submit(self, keyed, keys, slot_off, msg_base, msg_start, msg_end):
+        assert self.held[self.cur] is None, "staging set %d holds an uncollected submission" % self.cur
+        self.submits_staged += 1
+        ok = self.verify_staged(keyed, keys, slot_off, msg_base, msg_start, msg_end)
+        self.held[self.cur] = ok
+        return (self.cur, ok)
+
+    def verify_staged_collect(self, handle):
+        s, ok = handle
+        assert self.held[s] is ok
+        self.held[s] = None
+        return ok
 
     def stager(self):
         return (ctypes.cast(self._put, ctypes.c_void_p).value, ctypes.addressof(self.stage))

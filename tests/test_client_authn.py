@@ -708,3 +708,34 @@ def test_streamed_batch_bounded_in_flight(oracle, monkeypatch):
     assert eng.max_in_flight <= 4
     assert [_outcome(r) for r in got] == [m["identifier"] if i != 4321 else ("InvalidSignature", (), None)
                                           for i, m in enumerate(msgs)]
+
+
+def test_authenticate_batches_pipeline(oracle, monkeypatch):
+    """authenticate_batches: two batches in flight over the engine's two
+    staging sets (the double refuses to reuse a set whose submission was not
+    collected), every outcome equal to authenticate_batch's, batch by batch,
+    with batches that leave the steady state (a forgery is steady; an unknown
+    identifier and a missing signature are not; a batch below the staging
+    threshold) finished synchronously in order."""
+    from engine_double import StagingOracleEngine
+    from plenum_amd import client_authn as CA
+    monkeypatch.setattr(CA, "_STAGE_MIN_BATCH", 1000)
+    monkeypatch.setattr(CA, "_PINNED_MIN_BATCH", 1000)
+    idrs, vks, msgs = _signed(3, 6000)
+    eng = StagingOracleEngine(oracle)
+    a = GpuAuthNr(engine=eng)
+    ref = GpuAuthNr(engine=OracleEngine(oracle), max_keys=0)
+    for i, v in zip(idrs, vks):
+        a.addIdr(i, v)
+        ref.addIdr(i, v)
+    a.keys_settle()
+    batches = [[dict(m) for m in msgs[k * 1200:(k + 1) * 1200]] for k in range(5)]
+    batches[1][7]["reqId"] += 1                           # forged: still the steady state
+    batches[2][3]["identifier"] = "UnknownIdentifier1111"  # leaves it: finished synchronously
+    del batches[3][5]["signature"]
+    batches.insert(4, [dict(m) for m in msgs[:50]])       # below the staging threshold
+    got = [[_outcome(r) for r in res] for res in a.authenticate_batches(iter(batches))]
+    want = [[_outcome(r) for r in ref.authenticate_batch(b)] for b in batches]
+    assert got == want
+    assert eng.submits_staged == 3 and eng.held == [None, None]  # batches 0, 1 and 5 were in flight
+    assert list(a.authenticate_batches([])) == []

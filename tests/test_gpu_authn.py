@@ -608,3 +608,25 @@ def test_large_batch_staged_and_streamed_on_gpu(gpu_engine):
         assert [r if isinstance(r, str) else type(r).__name__ for r in ok] == \
                [w for i, w in enumerate(want) if i not in (1234, 4321)], mode
         assert a._g.last_breakdown is not None, mode
+
+
+def test_authenticate_batches_pipeline_on_gpu(gpu_engine):
+    """authenticate_batches on the device: 3 batches of 70,000 requests (above
+    the staging threshold) in flight two at a time over the engine's staging
+    sets, plus a batch that leaves the steady state in the middle: every
+    outcome equals the synchronous authenticate_batch's."""
+    import copy
+    n = 70000
+    reqs, rx, idrs, vks, pks, sers, sig = _drain(gpu_engine, n_req=n, n_nodes=1, n_signers=16)
+    a = GpuAuthNr(engine=gpu_engine)
+    for idr, vk in zip(idrs, vks):
+        a.addIdr(idr, vk)
+    a.keys_settle()
+    odd = [copy.deepcopy(r) for r in reqs]
+    odd[99]["identifier"] = "UnknownIdentifier11111111"
+    batches = [reqs, reqs, odd, reqs]
+    want = [[r if isinstance(r, str) else type(r).__name__ for r in a.authenticate_batch(b)] for b in batches]
+    for rep in range(2):
+        got = [[r if isinstance(r, str) else type(r).__name__ for r in res] for res in a.authenticate_batches(batches)]
+        assert got == want, rep
+    assert want[0].count("InvalidSignature") == n // 10 and want[2][99] == "UnknownIdentifier"
