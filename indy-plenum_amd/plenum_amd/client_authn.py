@@ -756,26 +756,32 @@ class GpuAuthMixin:
                self._native_host_steps())
         pending = None
         k = 0
-        for msgs in batches:
-            res = None
-            if can and len(msgs) >= _STAGE_MIN_BATCH:
-                with _engine_lock(eng):
-                    s = k % 2
-                    bufs = self._scan_buffers(eng, len(msgs), slot, s)
-                    if bufs is not self._g.scan_out:
-                        res = self._authenticate_staged(msgs, eng, slot, bufs, staging_set=s, defer=True)
-            if callable(res):
-                if pending is not None:
-                    yield pending()
-                pending = res
-                k += 1
-                continue
-            if pending is not None:  # the batch in flight first (its staging set is free after)
-                yield pending()
-                pending = None
-            yield res if res is not None else self.authenticate_batch(msgs)
-        if pending is not None:
-            yield pending()
+        try:
+            for msgs in batches:
+                res = None
+                if can and len(msgs) >= _STAGE_MIN_BATCH:
+                    with _engine_lock(eng):
+                        s = k % 2
+                        bufs = self._scan_buffers(eng, len(msgs), slot, s)
+                        if bufs is not self._g.scan_out:
+                            res = self._authenticate_staged(msgs, eng, slot, bufs, staging_set=s, defer=True)
+                if callable(res):
+                    if pending is not None:
+                        done, pending = pending, None
+                        yield done()
+                    pending = res
+                    k += 1
+                    continue
+                if pending is not None:  # the batch in flight first (its staging set is free after)
+                    done, pending = pending, None
+                    yield done()
+                yield res if res is not None else self.authenticate_batch(msgs)
+            if pending is not None:
+                done, pending = pending, None
+                yield done()
+        finally:
+            if pending is not None:  # an iteration abandoned with a batch in flight: free its staging set
+                pending()
 
     def _authenticate_streamed(self, msgs, eng, slot, bufs):
         """A large batch whose pack overlaps its DMA: one scan of the whole

@@ -739,3 +739,25 @@ def test_authenticate_batches_pipeline(oracle, monkeypatch):
     assert got == want
     assert eng.submits_staged == 3 and eng.held == [None, None]  # batches 0, 1 and 5 were in flight
     assert list(a.authenticate_batches([])) == []
+
+
+def test_authenticate_batches_abandoned_frees_the_set(oracle, monkeypatch):
+    """An authenticate_batches iteration closed with a batch in flight collects
+    it, so the staging sets are free for the next call."""
+    from engine_double import StagingOracleEngine
+    from plenum_amd import client_authn as CA
+    monkeypatch.setattr(CA, "_STAGE_MIN_BATCH", 1000)
+    monkeypatch.setattr(CA, "_PINNED_MIN_BATCH", 1000)
+    idrs, vks, msgs = _signed(3, 2400)
+    eng = StagingOracleEngine(oracle)
+    a = GpuAuthNr(engine=eng)
+    for i, v in zip(idrs, vks):
+        a.addIdr(i, v)
+    a.keys_settle()
+    b = [dict(m) for m in msgs[:1200]]
+    it = a.authenticate_batches([b, b, b])
+    first = next(it)  # batch 0 returned; batch 1 in flight
+    it.close()
+    assert eng.held == [None, None]
+    assert first == [m["identifier"] for m in b]
+    assert a.authenticate_batch(b) == first
