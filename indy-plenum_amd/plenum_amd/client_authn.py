@@ -766,11 +766,10 @@ class GpuAuthMixin:
                         if bufs is not self._g.scan_out:
                             res = self._authenticate_staged(msgs, eng, slot, bufs, staging_set=s, defer=True)
                 if callable(res):
-                    if pending is not None:
-                        done, pending = pending, None
-                        yield done()
-                    pending = res
+                    prev, pending = pending, res  # (held first: a close() at the yield collects it)
                     k += 1
+                    if prev is not None:
+                        yield prev()
                     continue
                 if pending is not None:  # the batch in flight first (its staging set is free after)
                     done, pending = pending, None

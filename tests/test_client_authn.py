@@ -758,6 +758,6 @@ def test_authenticate_batches_abandoned_frees_the_set(oracle, monkeypatch):
     it = a.authenticate_batches([b, b, b])
     first = next(it)  # batch 0 returned; batch 1 in flight
     it.close()
-    assert eng.held == [None, None]
+    assert eng.held[0] is None and eng.held[1] is None
     assert first == [m["identifier"] for m in b]
     assert a.authenticate_batch(b) == first
