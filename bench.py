@@ -254,11 +254,11 @@ def time_e2e(eng, reqs, idrs, vks):
     pipe = []
     for _ in range(3):
         t0 = time.perf_counter()
-        acc = 0
-        for res in a.authenticate_batches([reqs] * 4):
-            acc += sum(1 for r, m in zip(res, reqs) if r == m["identifier"])
+        outs = list(a.authenticate_batches([reqs] * 4))
         pipe.append(time.perf_counter() - t0)
-        assert acc == 4 * ok, (acc, ok)
+        for res in outs:  # every batch's verdicts, checked after the clock
+            assert sum(1 for r, m in zip(res, reqs) if r == m["identifier"]) == ok
+        del outs
     pipe_s = sorted(pipe)[1]
     from plenum_amd import _hostpack
     from plenum_amd.client_authn import _SIG_SLOT
@@ -314,7 +314,7 @@ def time_e2e(eng, reqs, idrs, vks):
             "pipelined": {"value": 4 * n / pipe_s, "batches": 4, "seconds": pipe_s,
                           "note": "authenticate_batches over 4 batches of these requests: two in flight (the "
                                   "engine's two staging sets), batch k + 1's host scan and PCIe copy under batch "
-                                  "k's kernels; the verdict check of each batch is inside the timed loop"},
+                                  "k's kernels; median of 3 runs, every batch's verdicts checked after the clock"},
             "first_batch_seconds": first, "first_batch_value": n / first,
             "in_batch_ms": in_batch,
             "host_scan_ms": t_scan * 1e3, "host_scan_us_per_request": t_scan / n * 1e6,
