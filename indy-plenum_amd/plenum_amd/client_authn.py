@@ -151,7 +151,17 @@ def _engine_lock(eng):
 
 
 class _GpuState:
-    """Per-authenticator GPU state (created on first use)."""
+    """Per-authenticator GPU state (created on first use).
+
+    Threads: the engine, its key store and the scan / staging buffers are
+    used only under _engine_lock.  The bookkeeping dicts -- verdicts,
+    key_uses, hot, pending -- are also updated outside it (authenticate()'s
+    cache hit and miss, _count_verified).  Every single dict operation is
+    atomic under the GIL, so concurrent callers cannot corrupt them; a race
+    between two threads can at most lose a use count (a key earns its slot a
+    request later) or evict one extra verdict (a later re-verify).  The node
+    calls authenticate() from its one looper thread (looper.py:141-151), as
+    the reference does."""
 
     def __init__(self, engine=None, device=0, devices=None, verdict_cache_size=1 << 20, key_window="auto",
                  max_keys=16384, hot_key_uses=2, key_store_bytes=KEY_STORE_BYTES, scan_threads=0,
