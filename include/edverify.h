@@ -396,6 +396,15 @@ int edv_bls_keygen_batch(edv_ctx *ctx, const uint8_t *sk32, const uint8_t *gen12
  * then the final exponentiation's cyclotomic squarings spread over three.
  * 0: always one lane per check.  Same verdicts in every form.  Default 32768. */
 int edv_bls_set_pair_lanes(edv_ctx *ctx, uint64_t max_checks);
+/* Verify batches of at most max_checks run one wave per check: the whole
+ * pairing check (both Miller loops on one accumulator, the final
+ * exponentiation) as a straight-line program of Fp operations spread over
+ * the wave's 64 lanes (bls_program.h, tools/gen_bls_program.py), the latency
+ * form for a COMMIT round's ~25 checks.  A degenerate Miller step (only a
+ * verkey sum outside the order-r subgroup makes one) re-runs on the
+ * four-lane kernel, so the verdicts are every form's.  0: never.  Default
+ * 1024.  Replaces the same indy-crypto calls as edv_bls_verify_batch. */
+int edv_bls_set_wave_checks(edv_ctx *ctx, uint64_t max_checks);
 
 #ifdef __cplusplus
 }

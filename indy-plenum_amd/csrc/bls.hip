@@ -15,10 +15,13 @@
 #include <vector>
 
 #include "../../include/edverify.h"
+#include "bls_wave.h"
 #include "bn254.h"
 #include "edv_internal.h"
 
 using namespace edv::bn;
+namespace blsp = edv::blsp;
+using edv::sha256_msg;
 using edv_internal::set_err;
 
 #define BLS_TRY(expr)                                                                              \
@@ -305,6 +308,160 @@ __global__ __launch_bounds__(kBlsBlock) void edv_bls_verify_quad_kernel(const ui
   if ((threadIdx.x & 63) == 0 && (lane_g >> 2) < n) words16[lane_g >> 6] = (uint16_t)b;
 }
 
+// The wave form (batches of at most bls_wave_max checks -- a COMMIT round's ~25): one wave per
+// check running bls_program.h, the whole pairing check as a straight-line program of Fp
+// operations scheduled over the 64 lanes (tools/gen_bls_program.py).  Prologue (per-lane code,
+// as the other forms): H(m) with the try-and-increment's first 16 candidates on lanes 0-15 side
+// by side (the first candidate that is a point wins, as in g1_hash's loop), then the signature,
+// generator and verkey-sum decodes on lanes 16-18.  Per step each lane reads its operation
+// (prefetched kPre steps ahead), its two operand slots, and writes its result after a barrier.
+// verdict[i]: 1 accept, 0 reject, 2 redo on the four-lane kernel (a degenerate Miller step
+// flagged by the program, or no point among the 16 candidates: bn254.h's branches decide).
+constexpr int kHashTries = 16;
+constexpr int kPre = 4;
+__global__ __launch_bounds__(kBlsBlock) void edv_bls_verify_wave_kernel(const uint8_t* __restrict__ sig128,
+                                                                       const uint8_t* __restrict__ msgs,
+                                                                       const uint64_t* __restrict__ moff,
+                                                                       const uint8_t* __restrict__ vk128,
+                                                                       const uint64_t* __restrict__ vk_off,
+                                                                       const uint8_t* __restrict__ gen128, uint64_t n,
+                                                                       uint8_t* __restrict__ verdict) {
+  __shared__ fp S[blsp::kSlots];
+  __shared__ uint32_t bad[4];  // [0] reject (a point at infinity), [1] redo
+  const uint64_t i = blockIdx.x;
+  const int lane = (int)threadIdx.x;
+  if (i >= n) return;  // the whole block
+  for (int k = lane; k < blsp::kConsts; k += kBlsBlock) fp_load(S[blsp::kConstSlot[k]], blsp::kConstVal + 8 * k);
+  if (lane < 4) bad[lane] = 0;
+  // H(m): candidate h + lane on lanes 0..kHashTries-1
+  bool hit = false;
+  fp hx, hy;
+  if (lane < kHashTries) {
+    uint32_t d[8];
+    sha256_msg(d, msgs + moff[i], moff[i + 1] - moff[i]);
+    uint8_t hb[32];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      hb[4 * k] = (uint8_t)d[k];
+      hb[4 * k + 1] = (uint8_t)(d[k] >> 8);
+      hb[4 * k + 2] = (uint8_t)(d[k] >> 16);
+      hb[4 * k + 3] = (uint8_t)(d[k] >> 24);
+    }
+    uint32_t x[8];
+    words_from_be(x, hb);
+    uint64_t c = (uint64_t)lane;  // h + lane, wrapping at 2^256 like g1_hash's h += 1
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint64_t t = (uint64_t)x[k] + c;
+      x[k] = (uint32_t)t;
+      c = t >> 32;
+    }
+    while (fp_geq_p(x)) {  // mod p (h < 2^256 < 5p)
+      fp t;
+      fp_reduce_once(t, x);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) x[k] = t.v[k];
+    }
+    fp rhs, bb;
+    fp_from_plain(hx, x);
+    fp_sqr(rhs, hx);
+    fp_mul(rhs, rhs, hx);
+    fp_load(bb, kB1);
+    fp_add(rhs, rhs, bb);
+    hit = fp_sqrt(hy, rhs);
+  }
+  const unsigned long long hits = __ballot(hit);
+  __syncthreads();
+  if (hits == 0) {
+    if (lane == 0) bad[1] = 1;
+  } else if (lane == __ffsll((long long)hits) - 1) {
+    S[blsp::kIn_xP2] = hx;
+    S[blsp::kIn_yP2] = hy;
+  }
+  if (lane == kHashTries) {
+    g1 s;
+    g1_from_bytes(s, sig128 + 128 * i);  // affine (Z = 1) when finite
+    if (g1_isinf(s)) {
+      bad[0] = 1;
+    } else {
+      S[blsp::kIn_xP1] = s.X;
+      S[blsp::kIn_yP1] = s.Y;
+    }
+  } else if (lane == kHashTries + 1 || lane == kHashTries + 2) {
+    g2 q;
+    if (lane == kHashTries + 1) {
+      g2_from_bytes(q, gen128);
+    } else {
+      const uint64_t k0 = vk_off ? vk_off[i] : i, k1 = vk_off ? vk_off[i + 1] : i + 1;
+      g2_inf(q);
+      for (uint64_t k = k0; k < k1; ++k) {  // Bls.verify_multi_sig: the verkeys' sum
+        g2 t;
+        g2_from_bytes(t, vk128 + 128 * k);
+        g2_add(q, q, t);
+      }
+    }
+    if (g2_isinf(q)) {
+      bad[0] = 1;
+    } else if (lane == kHashTries + 1) {
+      S[blsp::kIn_Q1Xa] = q.X.a;
+      S[blsp::kIn_Q1Xb] = q.X.b;
+      S[blsp::kIn_Q1Ya] = q.Y.a;
+      S[blsp::kIn_Q1Yb] = q.Y.b;
+      S[blsp::kIn_Q1Za] = q.Z.a;
+      S[blsp::kIn_Q1Zb] = q.Z.b;
+    } else {
+      S[blsp::kIn_Q2Xa] = q.X.a;
+      S[blsp::kIn_Q2Xb] = q.X.b;
+      S[blsp::kIn_Q2Ya] = q.Y.a;
+      S[blsp::kIn_Q2Yb] = q.Y.b;
+      S[blsp::kIn_Q2Za] = q.Z.a;
+      S[blsp::kIn_Q2Zb] = q.Z.b;
+    }
+  }
+  __syncthreads();
+  if (bad[0] || bad[1]) {  // bls_check's rejections; or no H among the candidates: redo
+    if (lane == 0) verdict[i] = bad[0] ? 0 : 2;
+    return;
+  }
+  // the program: operations of step s+kPre are loaded while step s runs
+  uint32_t q0[kPre], q1[kPre];
+  uint32_t flag = 0;
+#pragma unroll
+  for (int j = 0; j < kPre; ++j) {
+    const uint32_t o = blsp::kStep[j] + (uint32_t)lane;
+    const bool live = j < blsp::kSteps && o < blsp::kStep[j + 1];
+    q0[j] = live ? blsp::kOp[2 * o] : 0u;
+    q1[j] = live ? blsp::kOp[2 * o + 1] : 0u;
+  }
+  for (int s0 = 0; s0 < blsp::kSteps; s0 += kPre) {
+#pragma unroll
+    for (int j = 0; j < kPre; ++j) {
+      const int s = s0 + j;
+      if (s < blsp::kSteps) {  // uniform
+        const uint32_t w0 = q0[j], w1 = q1[j];
+        const int sn = s + kPre;  // refill this ring entry with step s + kPre
+        const uint32_t o = (sn < blsp::kSteps ? blsp::kStep[sn] : 0u) + (uint32_t)lane;
+        const bool live = sn < blsp::kSteps && o < blsp::kStep[sn + 1];
+        q0[j] = live ? blsp::kOp[2 * o] : 0u;
+        q1[j] = live ? blsp::kOp[2 * o + 1] : 0u;
+        const uint32_t kind = w0 & 0xffu;
+        fp r;
+        bool wr = false;
+        if (kind != blsp::kNop) {
+          const fp x = S[w1 & 0xffffu];
+          const fp y = S[w1 >> 16];
+          wr = blsp_exec(kind, x, y, r, &flag);
+        }
+        __syncthreads();  // every operand read before any result is written
+        if (wr) S[w0 >> 8] = r;
+        __syncthreads();
+      }
+    }
+  }
+  const bool degenerate = __ballot(flag != 0) != 0;
+  if (lane == 0) verdict[i] = degenerate ? 2 : blsp_result_is_one(S) ? 1 : 0;
+}
+
 __global__ __launch_bounds__(kBlsBlock) void edv_bls_aggregate_kernel(const uint8_t* __restrict__ sig128,
                                                                      const uint64_t* __restrict__ off, uint64_t m,
                                                                      uint8_t* __restrict__ out128) {
@@ -421,7 +578,26 @@ int edv_bls_verify_batch(edv_ctx* ctx, const uint8_t* sig128, const uint8_t* msg
     for (uint64_t i = 0; i <= n; ++i) vo[i] = vk_off[i] - vk0;
     BLS_TRY(hipMemcpyAsync(d_vkoff, vo.data(), 8 * (n + 1), hipMemcpyHostToDevice, st));
   }
-  if (2 * n <= edv_internal::bls_pair_max(ctx))
+  std::vector<uint8_t> vb;
+  if (n <= edv_internal::bls_wave_max(ctx)) {
+    uint8_t* d_verdict;
+    if ((r = sc.alloc(&d_verdict, n))) return r;
+    hipLaunchKernelGGL(edv_bls_verify_wave_kernel, dim3((uint32_t)n), dim3(kBlsBlock), 0, st, d_sig, d_msgs, d_off,
+                       d_vk, d_vkoff, d_gen, n, d_verdict);
+    BLS_TRY(hipGetLastError());
+    vb.resize(n);
+    BLS_TRY(hipMemcpyAsync(vb.data(), d_verdict, n, hipMemcpyDeviceToHost, st));
+    BLS_TRY(hipStreamSynchronize(st));
+    bool redo = false;
+    for (uint64_t k = 0; k < n; ++k) redo = redo || vb[k] == 2;
+    if (!redo) {
+      for (uint64_t b = 0; b < (n + 7) / 8; ++b) accept_bits[b] = 0;
+      for (uint64_t k = 0; k < n; ++k) accept_bits[k / 8] |= (uint8_t)((vb[k] & 1u) << (k % 8));
+      return 0;
+    }
+    // a degenerate check (a verkey sum outside the order-r subgroup): the four-lane kernel's verdicts
+  }
+  if (!vb.empty() || 2 * n <= edv_internal::bls_pair_max(ctx))
     hipLaunchKernelGGL(edv_bls_verify_quad_kernel, dim3(grid_of(4 * n)), dim3(kBlsBlock), 0, st, d_sig, d_msgs, d_off,
                        d_vk, d_vkoff, d_gen, n, (uint16_t*)d_words);
   else if (n <= edv_internal::bls_pair_max(ctx))
@@ -436,6 +612,17 @@ int edv_bls_verify_batch(edv_ctx* ctx, const uint8_t* sig128, const uint8_t* msg
   BLS_TRY(hipStreamSynchronize(st));
   for (uint64_t b = 0; b < (n + 7) / 8; ++b) accept_bits[b] = (uint8_t)(w[b / 8] >> (8 * (b % 8)));
   if (n & 7) accept_bits[n / 8] &= (uint8_t)((1u << (n & 7)) - 1);
+  if (!vb.empty()) {  // the wave form's own verdicts where it had one
+    for (uint64_t k = 0; k < n; ++k)
+      if (vb[k] != 2)
+        accept_bits[k / 8] = (uint8_t)((accept_bits[k / 8] & ~(1u << (k % 8))) | ((vb[k] & 1u) << (k % 8)));
+  }
+  return 0;
+}
+
+int edv_bls_set_wave_checks(edv_ctx* ctx, uint64_t max_checks) {
+  if (!ctx) return set_err(EDV_EINVAL, "null context");
+  edv_internal::bls_wave_max(ctx) = max_checks;
   return 0;
 }
 

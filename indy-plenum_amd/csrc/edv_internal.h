@@ -12,4 +12,6 @@ int begin(edv_ctx* ctx, hipStream_t* stream);
 int set_err(int code, const char* fmt, ...);
 // BLS verify batches of at most this many checks take two lanes per check (edv_bls_set_pair_lanes).
 uint64_t& bls_pair_max(edv_ctx* ctx);
+// ... and batches of at most this many one wave per check (edv_bls_set_wave_checks).
+uint64_t& bls_wave_max(edv_ctx* ctx);
 }  // namespace edv_internal

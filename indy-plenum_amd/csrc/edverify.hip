@@ -1384,6 +1384,7 @@ struct edv_ctx {
   // per sub-batch: block offsets [kSortBlocks][bins], bin totals / bases [bins] x 2, scan scratch
   int key_sort = 2;
   uint64_t bls_pair_max = 32768;  // edv_bls_set_pair_lanes
+  uint64_t bls_wave_max = 1024;   // edv_bls_set_wave_checks
   // the small keyed path reads its packed inputs straight from pinned host memory (no H2D copy
   // before the kernel); A/B switch EDV_SMALL_ZC=1
   bool small_zero_copy = getenv("EDV_SMALL_ZC") != nullptr;
@@ -2250,6 +2251,7 @@ int begin(edv_ctx* ctx, hipStream_t* stream) {
   return 0;
 }
 uint64_t& bls_pair_max(edv_ctx* ctx) { return ctx->bls_pair_max; }
+uint64_t& bls_wave_max(edv_ctx* ctx) { return ctx->bls_wave_max; }
 int set_err(int code, const char* fmt, ...) {
   char buf[512];
   va_list ap;

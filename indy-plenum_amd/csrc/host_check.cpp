@@ -429,3 +429,54 @@ int edv_host_bls_verify(const uint8_t sig128[128], const uint8_t* msg, uint64_t 
 }
 
 }  // extern "C"
+
+// ---- the wave form's program (bls_wave.h) run step by step on the CPU, for tests/test_bls_program.py.
+#include "bls_wave.h"
+extern "C" {
+// Bls.verify over wire bytes through bls_program.h: 1 accept, 0 reject, 2 degenerate (the
+// kernel would redo the check on the four-lane form), -1 an input at infinity (rejected by
+// the prologue).  vk_n verkeys are summed (verify_multi_sig).
+int edv_host_bls_verify_program(const uint8_t sig128[128], const uint8_t* msg, uint64_t mlen, const uint8_t* vk128,
+                                uint64_t vk_n, const uint8_t gen128[128]) {
+  using namespace edv::bn;
+  static fp S[edv::blsp::kSlots];
+  for (int k = 0; k < edv::blsp::kConsts; ++k) fp_load(S[edv::blsp::kConstSlot[k]], edv::blsp::kConstVal + 8 * k);
+  g1 s, h;
+  g2 g, v;
+  g1_from_bytes(s, sig128);
+  g1_hash(h, msg, mlen);
+  g2_from_bytes(g, gen128);
+  g2_inf(v);
+  for (uint64_t k = 0; k < vk_n; ++k) {
+    g2 t;
+    g2_from_bytes(t, vk128 + 128 * k);
+    g2_add(v, v, t);
+  }
+  if (g1_isinf(s) || g2_isinf(g) || g2_isinf(v) || g1_isinf(h)) return -1;
+  namespace P = edv::blsp;
+  S[P::kIn_xP1] = s.X;
+  S[P::kIn_yP1] = s.Y;
+  S[P::kIn_xP2] = h.X;
+  S[P::kIn_yP2] = h.Y;
+  const fp* q[12] = {&g.X.a, &g.X.b, &g.Y.a, &g.Y.b, &g.Z.a, &g.Z.b, &v.X.a, &v.X.b, &v.Y.a, &v.Y.b, &v.Z.a, &v.Z.b};
+  const int qs[12] = {P::kIn_Q1Xa, P::kIn_Q1Xb, P::kIn_Q1Ya, P::kIn_Q1Yb, P::kIn_Q1Za, P::kIn_Q1Zb,
+                      P::kIn_Q2Xa, P::kIn_Q2Xb, P::kIn_Q2Ya, P::kIn_Q2Yb, P::kIn_Q2Za, P::kIn_Q2Zb};
+  for (int k = 0; k < 12; ++k) S[qs[k]] = *q[k];
+  uint32_t flag = 0;
+  static fp res[64];
+  bool wr[64];
+  uint32_t dst[64];
+  for (int st = 0; st < P::kSteps; ++st) {
+    const uint32_t o0 = P::kStep[st], o1 = P::kStep[st + 1];
+    for (uint32_t o = o0; o < o1; ++o) {  // every lane reads ...
+      const uint32_t w0 = P::kOp[2 * o], w1 = P::kOp[2 * o + 1];
+      wr[o - o0] = blsp_exec(w0 & 0xffu, S[w1 & 0xffffu], S[w1 >> 16], res[o - o0], &flag);
+      dst[o - o0] = w0 >> 8;
+    }
+    for (uint32_t o = o0; o < o1; ++o)  // ... then every lane writes
+      if (wr[o - o0]) S[dst[o - o0]] = res[o - o0];
+  }
+  if (flag) return 2;
+  return blsp_result_is_one(S) ? 1 : 0;
+}
+}  // extern "C"

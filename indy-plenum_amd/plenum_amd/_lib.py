@@ -79,6 +79,7 @@ SIGNATURES = {
     "edv_bls_sign_batch": (_I, [_P, _P, _P, _P, _U64, _P]),
     "edv_bls_keygen_batch": (_I, [_P, _P, _P, _U64, _P]),
     "edv_bls_set_pair_lanes": (_I, [_P, _U64]),
+    "edv_bls_set_wave_checks": (_I, [_P, _U64]),
 }
 
 

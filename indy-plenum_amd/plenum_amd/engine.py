@@ -389,6 +389,12 @@ class EdVerifyEngine:
         latency); 0 = one lane per check always (edv_bls_set_pair_lanes)."""
         check(self._lib.edv_bls_set_pair_lanes(self._ctx, int(max_checks)))
 
+    def bls_set_wave_checks(self, max_checks):
+        """Verify batches of at most max_checks run one wave per check (the
+        check as a straight-line program over the wave's lanes: the latency
+        form); 0 = never (edv_bls_set_wave_checks)."""
+        check(self._lib.edv_bls_set_wave_checks(self._ctx, int(max_checks)))
+
     def bls_aggregate(self, sig128, sig_off):
         """out[i] = sum of sig128[sig_off[i]:sig_off[i+1]] (create_multi_sig)."""
         sig128 = _u8(sig128, 128)

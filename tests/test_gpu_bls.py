@@ -14,13 +14,16 @@ pytestmark = pytest.mark.gpu
 V = json.load(open(os.path.join(GOLDEN, "bls_vectors.json")))
 
 
-@pytest.fixture(params=["quad", "pair", "one"])
+@pytest.fixture(params=["wave", "quad", "pair", "one"])
 def bls_mode(request, gpu_engine):
-    """Every verify form: four lanes per check (batches up to half the pair limit), two, one.
-    Returns set(n): selects that form for an n-check batch."""
+    """Every verify form: one wave per check (the straight-line program), four lanes per check
+    (batches up to half the pair limit), two, one.  Returns set(n): selects that form for an
+    n-check batch."""
     def set_for(n):
-        gpu_engine.bls_set_pair_lanes({"quad": 2 * n, "pair": n, "one": 0}[request.param])
+        gpu_engine.bls_set_wave_checks(n if request.param == "wave" else 0)
+        gpu_engine.bls_set_pair_lanes({"wave": 0, "quad": 2 * n, "pair": n, "one": 0}[request.param])
     yield set_for
+    gpu_engine.bls_set_wave_checks(1024)
     gpu_engine.bls_set_pair_lanes(32768)
 
 
