@@ -12,6 +12,8 @@
 //   edv_bls_sign_kernel / edv_bls_keygen_kernel  [sk]H(m), [sk]g (test data)
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "../../include/edverify.h"
@@ -314,19 +316,23 @@ __global__ __launch_bounds__(kBlsBlock) void edv_bls_verify_quad_kernel(const ui
 // as the other forms): H(m) with the try-and-increment's first 16 candidates on lanes 0-15 side
 // by side (the first candidate that is a point wins, as in g1_hash's loop), then the signature,
 // generator and verkey-sum decodes on lanes 16-18.  Per step each lane reads its operation
-// (prefetched kPre steps ahead), its two operand slots, and writes its result after a barrier.
+// (prefetched two steps ahead) and its operand slots, and writes its result after a barrier
+// (for a one-wave block the barrier is only the compiler's fence: LDS is in order per wave).
 // verdict[i]: 1 accept, 0 reject, 2 redo on the four-lane kernel (a degenerate Miller step
 // flagged by the program, or no point among the 16 candidates: bn254.h's branches decide).
 constexpr int kHashTries = 16;
-constexpr int kPre = 4;
 __global__ __launch_bounds__(kBlsBlock) void edv_bls_verify_wave_kernel(const uint8_t* __restrict__ sig128,
                                                                        const uint8_t* __restrict__ msgs,
                                                                        const uint64_t* __restrict__ moff,
                                                                        const uint8_t* __restrict__ vk128,
                                                                        const uint64_t* __restrict__ vk_off,
                                                                        const uint8_t* __restrict__ gen128, uint64_t n,
-                                                                       uint8_t* __restrict__ verdict) {
+                                                                       uint8_t* __restrict__ verdict,
+                                                                       unsigned long long* __restrict__ clk) {
   __shared__ fp S[blsp::kSlots];
+  // clk (EDV_BLS_WAVE_CLOCKS=1, block 0): shader clocks at the start, after the prologue, after
+  // the program, and the program's clocks in steps with a product / without one
+  const unsigned long long c_start = clock64();
   __shared__ uint32_t bad[4];  // [0] reject (a point at infinity), [1] redo
   const uint64_t i = blockIdx.x;
   const int lane = (int)threadIdx.x;
@@ -423,43 +429,66 @@ __global__ __launch_bounds__(kBlsBlock) void edv_bls_verify_wave_kernel(const ui
     if (lane == 0) verdict[i] = bad[0] ? 0 : 2;
     return;
   }
-  // the program: operations of step s+kPre are loaded while step s runs
-  uint32_t q0[kPre], q1[kPre];
-  uint32_t flag = 0;
+  struct OpW {
+    uint32_t w[blsp::kOpWords];
+  };
+  static_assert(blsp::kOpWords % 4 == 0, "operations load as 16-byte vectors");
+  auto load_op = [&](OpW& q, int sn) {
+    const uint32_t o = (sn < blsp::kSteps ? blsp::kStep[sn] : 0u) + (uint32_t)lane;
+    if (sn < blsp::kSteps && o < blsp::kStep[sn + 1]) {
+      const uint4* src = (const uint4*)(blsp::kOp + (size_t)blsp::kOpWords * o);
 #pragma unroll
-  for (int j = 0; j < kPre; ++j) {
-    const uint32_t o = blsp::kStep[j] + (uint32_t)lane;
-    const bool live = j < blsp::kSteps && o < blsp::kStep[j + 1];
-    q0[j] = live ? blsp::kOp[2 * o] : 0u;
-    q1[j] = live ? blsp::kOp[2 * o + 1] : 0u;
-  }
-  for (int s0 = 0; s0 < blsp::kSteps; s0 += kPre) {
-#pragma unroll
-    for (int j = 0; j < kPre; ++j) {
-      const int s = s0 + j;
-      if (s < blsp::kSteps) {  // uniform
-        const uint32_t w0 = q0[j], w1 = q1[j];
-        const int sn = s + kPre;  // refill this ring entry with step s + kPre
-        const uint32_t o = (sn < blsp::kSteps ? blsp::kStep[sn] : 0u) + (uint32_t)lane;
-        const bool live = sn < blsp::kSteps && o < blsp::kStep[sn + 1];
-        q0[j] = live ? blsp::kOp[2 * o] : 0u;
-        q1[j] = live ? blsp::kOp[2 * o + 1] : 0u;
-        const uint32_t kind = w0 & 0xffu;
-        fp r;
-        bool wr = false;
-        if (kind != blsp::kNop) {
-          const fp x = S[w1 & 0xffffu];
-          const fp y = S[w1 >> 16];
-          wr = blsp_exec(kind, x, y, r, &flag);
-        }
-        __syncthreads();  // every operand read before any result is written
-        if (wr) S[w0 >> 8] = r;
-        __syncthreads();
+      for (int v = 0; v < blsp::kOpWords / 4; ++v) {
+        const uint4 t = src[v];
+        q.w[4 * v] = t.x;
+        q.w[4 * v + 1] = t.y;
+        q.w[4 * v + 2] = t.z;
+        q.w[4 * v + 3] = t.w;
       }
+    } else {
+      q.w[0] = blsp::kNop;
     }
+  };
+  // two named prefetch registers, ping-pong (an array indexed by the step would live in scratch
+  // memory): step s runs while the operation of step s + 2 loads
+  OpW qa, qb;
+  uint32_t flag = 0;
+  const bool timing = clk != nullptr && blockIdx.x == 0;
+  const unsigned long long c_prologue = clock64();
+  unsigned long long c_prev = c_prologue, c_heavy = 0, c_light = 0;
+  auto run_step = [&](OpW& q, int s) __attribute__((always_inline)) {
+    const OpW cur = q;
+    load_op(q, s + 2);
+    fp r;
+    bool wr = false;
+    if ((cur.w[0] & 15u) != blsp::kNop) wr = blsp_exec(cur.w, S, r, &flag);
+    __syncthreads();  // every operand read before any result is written
+    if (wr) S[blsp_field(cur.w, 0)] = r;
+    __syncthreads();
+    if (timing) {
+      const unsigned long long c = clock64();
+      if (__ballot((cur.w[0] & 15u) == blsp::kMul || (cur.w[0] & 15u) == blsp::kInv))
+        c_heavy += c - c_prev;
+      else
+        c_light += c - c_prev;
+      c_prev = c;
+    }
+  };
+  load_op(qa, 0);
+  load_op(qb, 1);
+  for (int s = 0; s < blsp::kSteps; s += 2) {
+    run_step(qa, s);
+    if (s + 1 < blsp::kSteps) run_step(qb, s + 1);  // uniform
   }
   const bool degenerate = __ballot(flag != 0) != 0;
   if (lane == 0) verdict[i] = degenerate ? 2 : blsp_result_is_one(S) ? 1 : 0;
+  if (timing && lane == 0) {
+    clk[0] = c_start;
+    clk[1] = c_prologue;
+    clk[2] = clock64();
+    clk[3] = c_heavy;
+    clk[4] = c_light;
+  }
 }
 
 __global__ __launch_bounds__(kBlsBlock) void edv_bls_aggregate_kernel(const uint8_t* __restrict__ sig128,
@@ -582,9 +611,19 @@ int edv_bls_verify_batch(edv_ctx* ctx, const uint8_t* sig128, const uint8_t* msg
   if (n <= edv_internal::bls_wave_max(ctx)) {
     uint8_t* d_verdict;
     if ((r = sc.alloc(&d_verdict, n))) return r;
+    unsigned long long* d_clk = nullptr;
+    const bool clocks = getenv("EDV_BLS_WAVE_CLOCKS") != nullptr;
+    if (clocks && (r = sc.alloc(&d_clk, 8 * 8))) return r;
     hipLaunchKernelGGL(edv_bls_verify_wave_kernel, dim3((uint32_t)n), dim3(kBlsBlock), 0, st, d_sig, d_msgs, d_off,
-                       d_vk, d_vkoff, d_gen, n, d_verdict);
+                       d_vk, d_vkoff, d_gen, n, d_verdict, d_clk);
     BLS_TRY(hipGetLastError());
+    if (clocks) {  // diagnostics: where block 0's shader clocks went
+      unsigned long long c[8];
+      BLS_TRY(hipMemcpyAsync(c, d_clk, sizeof c, hipMemcpyDeviceToHost, st));
+      BLS_TRY(hipStreamSynchronize(st));
+      fprintf(stderr, "bls wave clocks: prologue %llu, program %llu (steps with a product %llu, without %llu)\n",
+              c[1] - c[0], c[2] - c[1], c[3], c[4]);
+    }
     vb.resize(n);
     BLS_TRY(hipMemcpyAsync(vb.data(), d_verdict, n, hipMemcpyDeviceToHost, st));
     BLS_TRY(hipStreamSynchronize(st));

@@ -469,9 +469,9 @@ int edv_host_bls_verify_program(const uint8_t sig128[128], const uint8_t* msg, u
   for (int st = 0; st < P::kSteps; ++st) {
     const uint32_t o0 = P::kStep[st], o1 = P::kStep[st + 1];
     for (uint32_t o = o0; o < o1; ++o) {  // every lane reads ...
-      const uint32_t w0 = P::kOp[2 * o], w1 = P::kOp[2 * o + 1];
-      wr[o - o0] = blsp_exec(w0 & 0xffu, S[w1 & 0xffffu], S[w1 >> 16], res[o - o0], &flag);
-      dst[o - o0] = w0 >> 8;
+      const uint32_t* w = P::kOp + (size_t)P::kOpWords * o;
+      wr[o - o0] = blsp_exec(w, S, res[o - o0], &flag);
+      dst[o - o0] = blsp_field(w, 0);
     }
     for (uint32_t o = o0; o < o1; ++o)  // ... then every lane writes
       if (wr[o - o0]) S[dst[o - o0]] = res[o - o0];

@@ -33,15 +33,19 @@ def test_program_equals_oracle_pairing_product():
 
 
 def test_program_structure():
-    g, outs, steps, slot, nslots, pinned = gp.compile_program()
+    g, ops, outs, steps, slot, nslots, pinned = gp.compile_program()
     written = {slot[x] for x in pinned}
-    for ops in steps:
-        assert 0 < len(ops) <= gp.LANES
-        dsts = {slot[x] for x in ops if g.kind[x] != gp.ZCHK}
-        srcs = {slot[a] for x in ops for a in g.args[x]}
+    for st in steps:
+        assert 0 < len(st) <= gp.LANES
+        dsts = {slot[x] for x in st if ops[x].kind != gp.ZCHK}
+        srcs = {slot[a] for x in st for a in ops[x].args()}
         assert not (dsts & srcs)
         assert srcs <= written
         written |= dsts
+        for x in st:
+            op = ops[x]
+            assert len(op.A) + len(op.B) <= gp.MAX_TERMS
+            assert op.kind != gp.MUL or (len(op.A) <= 2 and len(op.B) <= 2)
     assert all(slot[x] in written for x in outs)
     assert nslots * 32 <= 64 * 1024  # LDS per wave
 

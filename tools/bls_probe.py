@@ -1,6 +1,6 @@
 """Throughput probe of the GPU BLS verify (edv_bls_verify_batch): n signed
 items (distinct keys and messages), one call, wall time incl. H2D.
-usage: python tools/bls_probe.py [FORM [n,n,...]]  (FORM: wave / quad / pair / one)"""
+usage: python tools/bls_probe.py [FORM [n n ...]]  (FORM: wave / quad / pair / one)"""
 import os
 import sys
 import time
@@ -18,7 +18,7 @@ if os.environ.get("BLS_PAIR") is not None:  # batches up to this many checks: tw
 FORM = sys.argv[1] if len(sys.argv) > 1 else os.environ.get("BLS_FORM")  # wave / quad / pair / one: that verify form at every size
 gen = np.frombuffer(b58decode(GENERATOR), np.uint8)
 rng = np.random.default_rng(1)
-SIZES = sys.argv[2] if len(sys.argv) > 2 else os.environ.get("BLS_SIZES", "64,1024,16384,65536,262144")
+SIZES = ",".join(sys.argv[2:]) if len(sys.argv) > 2 else os.environ.get("BLS_SIZES", "64,1024,16384,65536,262144")
 for n in [int(x) for x in SIZES.split(",")]:
     sks = np.frombuffer(b"".join((int.from_bytes(rng.bytes(32), "big") % ORDER).to_bytes(32, "big")
                                  for _ in range(n)), np.uint8).reshape(n, 32)

@@ -494,37 +494,144 @@ def build(values=None):
     return G, outs
 
 
-# ---------------------------------------------------------------- schedule + slots
-def schedule(g, outs, weights=None):
-    """List scheduling into steps of <= LANES operations.  A step whose best
-    ready operation is a product (or inversion) is a heavy step and takes
-    every kind of ready operation; otherwise only light ones (sums,
-    differences, zero tests) -- a product costs ~6 light steps."""
-    w = weights or {MUL: 6, INV: 40, ADD: 1, SUB: 1, ZCHK: 1}
-    need = set()
-    stack = list(outs) + list(g.checks)
+# ---------------------------------------------------------------- fuse, schedule, slots
+LIN = 6        # signed sum of up to MAX_TERMS slots (device kind kLin)
+MAX_TERMS = 12  # terms per operation (signed sums; a product: two sums of at most 2)
+
+
+class Op:
+    """A device operation: MUL = (sum A) * (sum B); LIN = sum A; INV = A[0]^-1;
+    ZCHK = flag if A[0] == A[1] == 0.  A, B: lists of (node, negated)."""
+    __slots__ = ("kind", "A", "B")
+
+    def __init__(self, kind, A, B=()):
+        self.kind, self.A, self.B = kind, list(A), list(B)
+
+    def args(self):
+        return [t for t, _ in self.A] + [t for t, _ in self.B]
+
+
+def fuse(g, outs, mul_terms=2, dup=True):
+    """Collapse sums and differences into LIN operations of up to MAX_TERMS
+    signed terms: an operand that is itself a sum is expanded in place when
+    the terms fit (dup: even when other operations read it too -- the lanes
+    are mostly idle, the steps are not); one- or two-term sums are folded into
+    a product's operands (Karatsuba's pre-sums) when mul_terms >= 2.  Only
+    what the outputs and zero tests reach through the final terms is kept.
+    Returns (ops: node -> Op in topological order, outs with aliases resolved)."""
+    need, stack = set(), list(outs) + list(g.checks)
     while stack:
         x = stack.pop()
         if x in need or g.kind[x] in (IN, CONST):
             continue
         need.add(x)
         stack.extend(g.args[x])
-    order = sorted(need)  # node ids are topological (args precede)
-    users = {x: [] for x in order}
+    order = sorted(need)
+    fan = {}
     for x in order:
         for a in g.args[x]:
+            fan[a] = fan.get(a, 0) + 1
+    out_set = set(outs)
+    zero = g.consts.get(0)
+    expr, alias, sides = {}, {}, {}
+
+    def res(y):
+        while y in alias:
+            y = alias[y]
+        return y
+
+    def size(e):
+        return sum(abs(c) for c in e.values())
+
+    def operand(y, limit):
+        y = res(y)
+        if y in expr and (dup or fan.get(y, 0) == 1) and size(expr[y]) <= limit:
+            return dict(expr[y])
+        return {y: 1}
+
+    def combine(ea, eb, sign):
+        e = dict(ea)
+        for t, c in eb.items():
+            e[t] = e.get(t, 0) + sign * c
+        return {t: c for t, c in e.items() if c != 0 and t != zero}
+
+    for x in order:
+        k = g.kind[x]
+        if k in (ADD, SUB):
+            a, b = g.args[x]
+            sign = 1 if k == ADD else -1
+            e = None
+            for ta, tb in ((True, True), (True, False), (False, True), (False, False)):
+                ea = operand(a, MAX_TERMS) if ta else {res(a): 1}
+                eb = operand(b, MAX_TERMS) if tb else {res(b): 1}
+                e = combine(ea, eb, sign)
+                if size(e) <= MAX_TERMS:
+                    break
+            if not e:
+                alias[x] = zero if zero is not None else g.const(0)
+            elif len(e) == 1 and list(e.values())[0] == 1:
+                alias[x] = list(e)[0]
+            else:
+                expr[x] = e
+        elif k == MUL:
+            sides[x] = [operand(y, mul_terms) if mul_terms >= 2 else {res(y): 1} for y in g.args[x]]
+
+    def terms(e):
+        t = []
+        for n, c in sorted(e.items()):
+            t += [(n, c < 0)] * abs(c)
+        return t
+
+    def op_of(x):
+        if x in expr:
+            return Op(LIN, terms(expr[x]))
+        k = g.kind[x]
+        if k == MUL:
+            return Op(MUL, terms(sides[x][0]), terms(sides[x][1]))
+        if k == INV:
+            return Op(INV, [(res(g.args[x][0]), False)])
+        if k == ZCHK:
+            return Op(ZCHK, [(res(g.args[x][0]), False), (res(g.args[x][1]), False)])
+        raise AssertionError(k)
+    outs = [res(o) for o in outs]
+    keep, stack = {}, list(outs) + list(g.checks)
+    while stack:
+        x = stack.pop()
+        if x in keep or g.kind[x] in (IN, CONST):
+            continue
+        keep[x] = op_of(x)
+        stack.extend(keep[x].args())
+    return {x: keep[x] for x in sorted(keep)}, outs
+
+
+def _is_heavy(op):
+    return op.kind in HEAVY
+
+
+def schedule(ops, outs):
+    """List scheduling into steps of <= LANES operations.  A step whose best
+    ready operation is a product (or inversion) is a heavy step and takes
+    every kind of ready operation; otherwise only light ones (sums, zero
+    tests) -- a product costs ~6 light steps."""
+    w = {MUL: 6.0, INV: 40.0, LIN: 1.0, ZCHK: 1.0}
+    order = list(ops)  # topological
+    users = {x: [] for x in order}
+    for x in order:
+        for a in set(ops[x].args()):
             if a in users:
                 users[a].append(x)
     prio = {}
     for x in reversed(order):
-        prio[x] = w[g.kind[x]] + max((prio[u] for u in users[x]), default=0)
-    pending = {x: sum(1 for a in g.args[x] if a in users) for x in order}
-    ready = [x for x in order if pending[x] == 0]
-    steps = []
+        op = ops[x]
+        c = w[op.kind] + (0.05 * len(op.A) if op.kind == LIN else 0)
+        prio[x] = c + max((prio[u] for u in users[x]), default=0)
+    pending = {x: len([a for a in set(ops[x].args()) if a in users]) for x in order}
     import heapq
     heap_h, heap_l = [], []
-    for x in ready:
-        heapq.heappush(heap_h if g.kind[x] in HEAVY else heap_l, (-prio[x], x))
+    for x in order:
+        if pending[x] == 0:
+            heapq.heappush(heap_h if _is_heavy(ops[x]) else heap_l, (-prio[x], x))
+    steps = []
     while heap_h or heap_l:
         best_h = -heap_h[0][0] if heap_h else -1
         best_l = -heap_l[0][0] if heap_l else -1
@@ -539,71 +646,88 @@ def schedule(g, outs, weights=None):
             for u in users[x]:
                 pending[u] -= 1
                 if pending[u] == 0:
-                    heapq.heappush(heap_h if g.kind[u] in HEAVY else heap_l, (-prio[u], u))
+                    heapq.heappush(heap_h if _is_heavy(ops[u]) else heap_l, (-prio[u], u))
     return steps
 
 
-def allocate(g, outs, steps):
+def allocate(g, ops, outs, steps):
     """LDS slots: inputs and constants pinned; an operation's result lives from
     its step to its last reader's step, and its slot is reused from the step
     after that (never within a step)."""
-    step_of = {}
-    for s, ops in enumerate(steps):
-        for x in ops:
-            step_of[x] = s
     last = {}
-    for s, ops in enumerate(steps):
-        for x in ops:
-            for a in g.args[x]:
+    for s, st in enumerate(steps):
+        for x in st:
+            for a in ops[x].args():
                 last[a] = max(last.get(a, -1), s)
     for o in outs:
         last[o] = len(steps)
     slot = {}
     nxt = 0
-    pinned = [x for x in range(len(g.kind)) if g.kind[x] in (IN, CONST) and (x in last or x in g.inputs.values())]
+    pinned = [x for x in range(len(g.kind)) if g.kind[x] in (IN, CONST) and
+              (x in last or x in g.inputs.values() or x == ZERO_NODE)]
     for x in pinned:
         slot[x] = nxt
         nxt += 1
-    free = []
     import heapq
-    release_at = {}  # step -> slots freed after it
+    free = []
+    release_at = {}
     for x, s in last.items():
-        if x in step_of:
+        if x in ops:
             release_at.setdefault(s, []).append(x)
-    for s, ops in enumerate(steps):
-        for x in ops:
-            if g.kind[x] == ZCHK:
+    for s, st in enumerate(steps):
+        for x in st:
+            if ops[x].kind == ZCHK:
                 continue
-            if free:
-                slot[x] = heapq.heappop(free)
-            else:
-                slot[x] = nxt
+            slot[x] = heapq.heappop(free) if free else nxt
+            if slot[x] == nxt:
                 nxt += 1
         for x in release_at.get(s, ()):
             if x in slot:
                 heapq.heappush(free, slot[x])
-        # a result nobody reads (none expected) would leak its slot: free it
-        for x in ops:
-            if g.kind[x] != ZCHK and x not in last:
+        for x in st:
+            if ops[x].kind != ZCHK and x not in last:
                 heapq.heappush(free, slot[x])
     return slot, nxt, pinned
 
 
-def encode(g, steps, slot):
+def op_words():
+    """32-bit words per operation: the header, then 16-bit fields dst, t0 .. t(MAX_TERMS-1); a
+    multiple of 4 (16-byte loads)."""
+    return -(-(1 + (MAX_TERMS + 2) // 2) // 4) * 4
+
+
+def encode(ops, steps, slot):
+    """Per operation: kind | nA << 4 | nB << 8 | negated-term mask << 12 (terms A then B),
+    then dst and the term slots, two 16-bit fields a word."""
     words, starts = [], [0]
-    for ops in steps:
-        for x in ops:
-            k = g.kind[x]
-            a = g.args[x]
-            dst = slot.get(x, 0) if k != ZCHK else 0
-            sa = slot[a[0]]
-            sb = slot[a[1]] if len(a) > 1 else 0
-            words.append((k | (dst << 8), sa | (sb << 16)))
+    for st in steps:
+        for x in st:
+            op = ops[x]
+            # a product's two sums sit at fixed fields (terms 0-1 and 2-3), so the device reads every
+            # field at a compile-time position (a run-time index into the words would put them in
+            # scratch memory)
+            # unused term fields name the constant-zero slot: the device sums every field of a sum
+            # unconditionally (all operand loads issued at once, no branch per term)
+            if op.kind == MUL:
+                t = op.A + [(ZERO_NODE, False)] * (2 - len(op.A)) + op.B + [(ZERO_NODE, False)] * (2 - len(op.B))
+            elif op.kind == LIN:
+                t = op.A + [(ZERO_NODE, False)] * (MAX_TERMS - len(op.A))
+            else:
+                t = op.A + op.B
+            assert len(t) <= MAX_TERMS and len(op.A) < 16 and len(op.B) < 16
+            neg = 0
+            for i, (_, ng) in enumerate(t):
+                neg |= int(ng) << i
+            halves = [slot.get(x, 0) if op.kind != ZCHK else 0] + [slot[n] for n, _ in t]
+            halves += [0] * (2 * (op_words() - 1) - len(halves))
+            w = [op.kind | (len(op.A) << 4) | (len(op.B) << 8) | (neg << 12)]
+            w += [halves[2 * i] | (halves[2 * i + 1] << 16) for i in range(op_words() - 1)]
+            words.append(tuple(w))
         starts.append(len(words))
     return words, starts
 
 
-def simulate(g, steps, slot, nslots, values):
+def simulate(g, ops, steps, slot, nslots, values):
     """The allocated program on concrete values (plain integers mod p; the
     device's Montgomery form maps onto it exactly).  Returns (slots, flag)."""
     mem = [None] * nslots
@@ -612,34 +736,58 @@ def simulate(g, steps, slot, nslots, values):
     for v, x in g.consts.items():
         if x in slot:
             mem[slot[x]] = v
-    flag = False
-    for ops in steps:
-        reads = [[mem[slot[a]] for a in g.args[x]] for x in ops]
-        writes = []
-        for x, r in zip(ops, reads):
-            k = g.kind[x]
-            if any(v is None for v in r):
+
+    def lsum(terms):
+        acc = 0
+        for n, ng in terms:
+            v = mem[slot[n]]
+            if v is None:
                 raise AssertionError("read of an unwritten slot")
-            if k == MUL:
-                writes.append((slot[x], r[0] * r[1] % P))
-            elif k == ADD:
-                writes.append((slot[x], (r[0] + r[1]) % P))
-            elif k == SUB:
-                writes.append((slot[x], (r[0] - r[1]) % P))
-            elif k == INV:
-                writes.append((slot[x], pow(r[0], P - 2, P)))
-            elif k == ZCHK:
-                flag = flag or (r[0] == 0 and r[1] == 0)
-        for s, v in writes:
-            mem[s] = v
+            acc += -v if ng else v
+        return acc % P
+    flag = False
+    for st in steps:
+        writes = []
+        for x in st:
+            op = ops[x]
+            if op.kind == MUL:
+                writes.append((slot[x], lsum(op.A) * lsum(op.B) % P))
+            elif op.kind == LIN:
+                writes.append((slot[x], lsum(op.A)))
+            elif op.kind == INV:
+                writes.append((slot[x], pow(lsum(op.A), P - 2, P)))
+            elif op.kind == ZCHK:
+                flag = flag or (lsum(op.A[:1]) == 0 and lsum(op.A[1:]) == 0)
+        for s_, v in writes:
+            mem[s_] = v
     return mem, flag
 
 
-def compile_program():
+def estimate_us(ops, steps, clock_ghz=2.1):
+    """Rough device time: a heavy step ~2,900 cycles (+250 when a lane sums a
+    product's operands), a light one ~450 + 60 per term of its longest sum."""
+    cyc = 0
+    for st in steps:
+        if any(ops[x].kind == INV for x in st):
+            cyc += 150000
+        elif any(ops[x].kind == MUL for x in st):
+            cyc += 2900 + (250 if any(len(ops[x].A) + len(ops[x].B) > 2 for x in st if ops[x].kind == MUL) else 0)
+        else:
+            cyc += 450 + 60 * max(len(ops[x].A) for x in st)
+    return cyc / clock_ghz / 1e3
+
+
+ZERO_NODE = None
+
+
+def compile_program(mul_terms=2, dup=True):
+    global ZERO_NODE
     g, outs = build()
-    steps = schedule(g, outs)
-    slot, nslots, pinned = allocate(g, outs, steps)
-    return g, outs, steps, slot, nslots, pinned
+    ZERO_NODE = g.const(0)
+    ops, outs = fuse(g, outs, mul_terms, dup)
+    steps = schedule(ops, outs)
+    slot, nslots, pinned = allocate(g, ops, outs, steps)
+    return g, ops, outs, steps, slot, nslots, pinned
 
 
 # ---------------------------------------------------------------- emit
@@ -652,9 +800,9 @@ def mont(v):
 
 
 def emit(prog):
-    g, outs, steps, slot, nslots, pinned = prog
-    words, starts = encode(g, steps, slot)
-    heavy = sum(1 for ops in steps if any(g.kind[x] in HEAVY for x in ops))
+    g, ops, outs, steps, slot, nslots, pinned = prog
+    words, starts = encode(ops, steps, slot)
+    heavy = sum(1 for st in steps if any(_is_heavy(ops[x]) for x in st))
     n_ops = len(words)
     consts = [(slot[x], g.val[x]) for x in pinned if g.kind[x] == CONST]
     lines = ["// Generated by tools/gen_bls_program.py -- do not edit.",
@@ -665,8 +813,9 @@ def emit(prog):
              "#if defined(__HIPCC__)", "#define EDV_BLSP_CONST __device__ static const", "#else",
              "#define EDV_BLSP_CONST static const", "#endif",
              "namespace edv {", "namespace blsp {",
-             "enum : uint32_t { kNop = %d, kMul = %d, kAdd = %d, kSub = %d, kInv = %d, kZchk = %d };" % (
-                 NOP, MUL, ADD, SUB, INV, ZCHK),
+             "enum : uint32_t { kNop = %d, kMul = %d, kInv = %d, kZchk = %d, kLin = %d };" % (NOP, MUL, INV, ZCHK, LIN),
+             "constexpr int kMaxTerms = %d;" % MAX_TERMS,
+             "constexpr int kOpWords = %d;" % op_words(),
              "constexpr int kSteps = %d;" % len(steps),
              "constexpr int kOps = %d;" % n_ops,
              "constexpr int kSlots = %d;" % nslots,
@@ -674,6 +823,16 @@ def emit(prog):
     for name in INPUTS:
         lines.append("constexpr int kIn_%s = %d;" % (name, slot[g.inputs[name]]))
     lines.append("EDV_BLSP_CONST uint16_t kOut[12] = {%s};" % ", ".join(str(slot[o]) for o in outs))
+    lines.append("// 8p, 4p, 2p, p as 9 limbs: a signed sum's reduction (sums < 16p)")
+    pm = []
+    for k in (8, 4, 2, 1):
+        pm += [((k * P) >> (32 * j)) & 0xffffffff for j in range(9)]
+    lines.append("EDV_BLSP_CONST uint32_t kPMul[36] = {%s};" % ", ".join("0x%08xu" % w for w in pm))
+    kp = []
+    for k in range(MAX_TERMS + 1):
+        kp += [((k * (P + 1)) >> (32 * j)) & 0xffffffff for j in range(9)]
+    lines.append("// k (p + 1), k = 0 .. kMaxTerms, as 9 limbs: a signed sum's correction for its k negated terms")
+    lines.append("EDV_BLSP_CONST uint32_t kKP1[%d] = {%s};" % (len(kp), ", ".join("0x%08xu" % w for w in kp)))
     lines.append("// R^3 mod p (plain): Montgomery inverse = plain inverse * R^3 / R")
     lines.append("EDV_BLSP_CONST uint32_t kR3[8] = {%s};" % ", ".join("0x%08xu" % w for w in limbs(MONT ** 3 % P)))
     lines.append("EDV_BLSP_CONST uint16_t kConstSlot[%d] = {%s};" % (max(1, len(consts)),
@@ -690,11 +849,13 @@ def emit(prog):
     for i in range(0, len(starts), 16):
         lines.append("    " + ", ".join(str(v) for v in starts[i:i + 16]) + ",")
     lines.append("};")
-    lines.append("// per operation: kind | dst << 8, a | b << 16")
-    lines.append("EDV_BLSP_CONST uint32_t kOp[%d] = {" % (2 * n_ops))
+    lines.append("// per operation (kOpWords words): kind | nA << 4 | nB << 8 | negated-term mask << 12; then")
+    lines.append("// dst, t0, t1, ... two 16-bit fields a word -- LIN: the signed sum of terms 0..nA-1; MUL:")
+    lines.append("// (sum of terms 0..nA-1) * (sum of terms 2..2+nB-1); INV: t0^-1; ZCHK: flag if t0 == t1 == 0")
+    lines.append("EDV_BLSP_CONST uint32_t kOp[%d] __attribute__((aligned(16))) = {" % (op_words() * n_ops))
     flat = [w for pair in words for w in pair]
-    for i in range(0, len(flat), 12):
-        lines.append("    " + ",".join("0x%x" % v for v in flat[i:i + 12]) + ",")
+    for i in range(0, len(flat), 18):
+        lines.append("    " + ",".join("0x%x" % v for v in flat[i:i + 18]) + ",")
     lines.append("};")
     lines += ["}  // namespace blsp", "}  // namespace edv", ""]
     return "\n".join(lines)
@@ -711,7 +872,7 @@ def check(prog, trials=2, seed=1):
     """Simulate the allocated program on random inputs (Q2 a sum of two keys:
     Jacobian with Z != 1) and compare with the oracle's reduced pairings."""
     o = _oracle()
-    g, outs, steps, slot, nslots, pinned = prog
+    g, ops, outs, steps, slot, nslots, pinned = prog
     rng = random.Random(seed)
     gen = o.generator()
     for t in range(trials):
@@ -726,7 +887,7 @@ def check(prog, trials=2, seed=1):
             X, Y = _jac2(pt, zz)
             vals.update({"Q%dXa" % q: X[0], "Q%dXb" % q: X[1], "Q%dYa" % q: Y[0], "Q%dYb" % q: Y[1],
                          "Q%dZa" % q: zz[0], "Q%dZb" % q: zz[1]})
-        mem, flag = simulate(g, steps, slot, nslots, vals)
+        mem, flag = simulate(g, ops, steps, slot, nslots, vals)
         got = [mem[slot[x]] for x in outs]
         want = o.f12_to_tower(o.pairing(p1, q1) * o.pairing(o.g1_neg(p2), q2))
         assert not flag, "valid inputs flagged"
@@ -748,18 +909,20 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--check", type=int, default=0)
     ap.add_argument("--stats", action="store_true")
+    ap.add_argument("--mul-terms", type=int, default=2)
+    ap.add_argument("--max-terms", type=int, default=MAX_TERMS)
     a = ap.parse_args()
-    prog = compile_program()
-    g, outs, steps, slot, nslots, pinned = prog
+    globals()["MAX_TERMS"] = a.max_terms
+    prog = compile_program(a.mul_terms)
+    g, ops, outs, steps, slot, nslots, pinned = prog
     if a.stats or not a.out:
         kinds = {}
-        for ops in steps:
-            for x in ops:
-                kinds[g.kind[x]] = kinds.get(g.kind[x], 0) + 1
-        heavy = sum(1 for ops in steps if any(g.kind[x] in HEAVY for x in ops))
-        inv = sum(1 for ops in steps if any(g.kind[x] == INV for x in ops))
-        print("steps %d (heavy %d, inv %d, light %d), ops %s, slots %d" % (
-            len(steps), heavy, inv, len(steps) - heavy, kinds, nslots), file=sys.stderr)
+        for st in steps:
+            for x in st:
+                kinds[ops[x].kind] = kinds.get(ops[x].kind, 0) + 1
+        heavy = sum(1 for st in steps if any(_is_heavy(ops[x]) for x in st))
+        print("steps %d (heavy %d, light %d), ops %s, slots %d, estimate %.0f us" % (
+            len(steps), heavy, len(steps) - heavy, kinds, nslots, estimate_us(ops, steps)), file=sys.stderr)
     if a.check:
         check(prog, a.check)
         print("check: %d random pairings == oracle" % a.check, file=sys.stderr)
