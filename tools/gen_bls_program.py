@@ -608,11 +608,14 @@ def _is_heavy(op):
     return op.kind in HEAVY
 
 
+RIDERS = True  # heavy steps also take ready sums (--no-riders: products only)
+
+
 def schedule(ops, outs):
     """List scheduling into steps of <= LANES operations.  A step whose best
     ready operation is a product (or inversion) is a heavy step and takes
-    every kind of ready operation; otherwise only light ones (sums, zero
-    tests) -- a product costs ~6 light steps."""
+    every kind of ready operation (RIDERS) or only products; otherwise only
+    light ones (sums, zero tests) -- a product costs ~2 light steps."""
     w = {MUL: 6.0, INV: 40.0, LIN: 1.0, ZCHK: 1.0}
     order = list(ops)  # topological
     users = {x: [] for x in order}
@@ -636,11 +639,13 @@ def schedule(ops, outs):
         best_h = -heap_h[0][0] if heap_h else -1
         best_l = -heap_l[0][0] if heap_l else -1
         take = []
-        if best_h >= best_l:
+        heavy = best_h >= best_l
+        if heavy:
             while heap_h and len(take) < LANES:
                 take.append(heapq.heappop(heap_h)[1])
-        while heap_l and len(take) < LANES:
-            take.append(heapq.heappop(heap_l)[1])
+        if RIDERS or not heavy:
+            while heap_l and len(take) < LANES:
+                take.append(heapq.heappop(heap_l)[1])
         steps.append(take)
         for x in take:
             for u in users[x]:
@@ -911,8 +916,10 @@ def main():
     ap.add_argument("--stats", action="store_true")
     ap.add_argument("--mul-terms", type=int, default=2)
     ap.add_argument("--max-terms", type=int, default=MAX_TERMS)
+    ap.add_argument("--no-riders", action="store_true")
     a = ap.parse_args()
     globals()["MAX_TERMS"] = a.max_terms
+    globals()["RIDERS"] = not a.no_riders
     prog = compile_program(a.mul_terms)
     g, ops, outs, steps, slot, nslots, pinned = prog
     if a.stats or not a.out:
