@@ -23,7 +23,7 @@ def bls_mode(request, gpu_engine):
         gpu_engine.bls_set_wave_checks(n if request.param == "wave" else 0)
         gpu_engine.bls_set_pair_lanes({"wave": 0, "quad": 2 * n, "pair": n, "one": 0}[request.param])
     yield set_for
-    gpu_engine.bls_set_wave_checks(1024)
+    gpu_engine.bls_set_wave_checks(4096)
     gpu_engine.bls_set_pair_lanes(32768)
 
 
