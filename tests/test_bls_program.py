@@ -88,3 +88,15 @@ def test_host_program_random_checks(hostcheck):
         assert _verify_program(hostcheck, o.g1_to_bytes(sig), msg + b"!", vks, gen) == 0
         if len(vks) > 1:
             assert _verify_program(hostcheck, o.g1_to_bytes(sig), msg, vks[:-1], gen) == 0
+
+
+def test_redo_fixture_needs_more_than_16_hash_candidates():
+    """tests/test_gpu_bls.py's REDO_MSG: the wave form's 16 side-by-side candidates of H(m)'s
+    try-and-increment are all non-points, so the kernel must hand the check over."""
+    import hashlib
+    h = int.from_bytes(hashlib.sha256(b"wave-form redo 11075").digest(), "big")
+    for k in range(16):
+        x = (h + k) % o.P
+        assert not o._is_square((x ** 3 + o.B1) % o.P)
+    x, y = o.hash_to_g1(b"wave-form redo 11075")
+    assert (x - h % o.P) % o.P >= 16

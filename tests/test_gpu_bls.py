@@ -124,3 +124,30 @@ def test_dropin_reference_scenarios(gpu_engine):
     assert ver.verify_sig_batch(items) == [True, False, True, False]
     assert ver.verify_multi_sig_batch([(multi, msg, [pk1, pk2]), (multi, msg, [pk2])]) == [True, False]
     assert GpuBlsUtils.bls_from_str(multi) is not None
+
+
+REDO_MSG = b"wave-form redo 11075"  # H(m) needs more than 16 candidates (tests/test_bls_program.py)
+
+
+def test_wave_form_hands_over_what_it_cannot_decide(gpu_engine):
+    """The wave form tries 16 hash candidates side by side; for REDO_MSG the first point is
+    candidate 17 or later, so the check goes to the four-lane kernel (verdict 2 -> redo) --
+    in a batch with ordinary checks, every verdict as in the four-lane form."""
+    from plenum_amd import pack_messages
+    gen = np.frombuffer(bytes.fromhex(V["generator"]), np.uint8)
+    sks = np.frombuffer(b"".join(bytes.fromhex(k["sk"]) for k in V["keys"][:2]), np.uint8).reshape(-1, 32)
+    vks = gpu_engine.bls_keygen_batch(sks, gen)
+    msgs = [REDO_MSG, b"ordinary", REDO_MSG, REDO_MSG + b"!"]
+    buf, off = pack_messages(msgs)
+    rows = sks[[0, 1, 1, 0]]
+    sigs = gpu_engine.bls_sign_batch(rows, buf, off)
+    sigs[3] = sigs[0]  # REDO_MSG's signature on another message
+    vk_rows = vks[[0, 1, 0, 0]]  # check 2: signed by key 1, checked against key 0
+    want = np.array([True, True, False, False])
+    try:
+        for wave in (16, 0):
+            gpu_engine.bls_set_wave_checks(wave)
+            gpu_engine.bls_set_pair_lanes(32768)
+            assert (gpu_engine.bls_verify_batch(sigs, buf, off, vk_rows, gen) == want).all(), wave
+    finally:
+        gpu_engine.bls_set_wave_checks(4096)
