@@ -158,6 +158,9 @@ def parse():
                          "sorted: requests grouped by signer (A/B of the comb's gather locality)")
     ap.add_argument("--key-sort", choices=["auto", "on", "off"], default="auto",
                     help="comb lanes in key-sorted order (edv_set_key_sort; auto = sub-batches >= 4096)")
+    ap.add_argument("--bls-checks", type=int, default=25,
+                    help="checks of the end_to_end.bls_commit_round leg (a 3PC batch's COMMIT BLS signatures in one "
+                         "call; 0 = skip)")
     ap.add_argument("--drain-n", type=int, default=40,
                     help="drains of the end_to_end.node_drain leg (100 REQUESTs + 24 BATCHes of PROPAGATEs each; "
                          "0 = skip)")
@@ -341,6 +344,41 @@ def time_e2e(eng, reqs, idrs, vks):
                     "value = the median of 3 batches after the first full-size one (steady state); first_batch_* "
                     "= that first batch (buffers allocated). single_authenticate_us: authenticate() of one "
                     "request not in the verdict cache (300 calls after 30 warm-up)"}
+
+
+def time_bls_commit_round(eng, checks=25, reps=5):
+    """bls_commit_round: a 3PC batch's COMMIT BLS signatures (one per node, distinct keys, a
+    state-root-sized message each) verified in one edv_bls_verify_batch call -- the wave form
+    (one wave per check) and, for comparison, the four-lane form; median wall ms per call,
+    H2D of the inputs included, every verdict checked."""
+    from plenum_amd import pack_messages
+    from plenum_amd.base58 import b58decode
+    from plenum_amd.bls import GENERATOR, ORDER
+    rng = np.random.default_rng(29)
+    gen = np.frombuffer(b58decode(GENERATOR), np.uint8)
+    sks = np.frombuffer(b"".join((int.from_bytes(rng.bytes(32), "big") % ORDER).to_bytes(32, "big")
+                                 for _ in range(checks)), np.uint8).reshape(checks, 32)
+    vks = eng.bls_keygen_batch(sks, gen)
+    buf, off = pack_messages([rng.bytes(96) for _ in range(checks)])
+    sigs = eng.bls_sign_batch(sks, buf, off)
+    res = {"checks": checks}
+    for form, wave, pair in (("wave", 4096, 32768), ("four_lane", 0, 32768)):
+        eng.bls_set_wave_checks(wave)
+        eng.bls_set_pair_lanes(pair)
+        ok = eng.bls_verify_batch(sigs, buf, off, vks, gen)
+        times = []
+        for _ in range(reps if form == "wave" else 2):
+            t0 = time.perf_counter()
+            ok = eng.bls_verify_batch(sigs, buf, off, vks, gen)
+            times.append((time.perf_counter() - t0) * 1e3)
+            if not ok.all():
+                raise SystemExit("bls_commit_round: a valid signature rejected (%s form)" % form)
+        res[form + "_ms"] = float(np.median(times))
+    eng.bls_set_wave_checks(4096)
+    res["note"] = ("one edv_bls_verify_batch call over %d (signature, message, verkey) checks: wave = one wave per "
+                   "check running the pairing check as a straight-line program (default for <= 4096 checks), "
+                   "four_lane = the earlier latency form; median wall ms, inputs' H2D included" % checks)
+    return res
 
 
 def time_node_drain(eng, reqs, idrs, vks, drains=40, per_drain=100, n_nodes=25, ref_drains=16):
@@ -993,6 +1031,8 @@ def main():
                     "64-aligned request index across k devices (one host thread each), the native scan as in "
                     "configs1 (up to 16 host threads); %d device(s) visible" % (m, ndev))
             del reqs
+        if args.bls_checks > 0:
+            e2e["bls_commit_round"] = time_bls_commit_round(eng, args.bls_checks)
 
     if rank == 0:
         out = {

@@ -1,5 +1,5 @@
 """One-screen summary of a bench.py log (its last JSON line): headline, roofline,
-CPU baseline and the end-to-end / node-drain legs.  Usage: python tools/bench_summary.py LOG"""
+CPU baseline and the end-to-end / node-drain / BLS legs.  Usage: python tools/bench_summary.py LOG"""
 import json
 import sys
 
@@ -26,7 +26,7 @@ def main(path):
     for k, v in (d.get("end_to_end") or {}).items():
         if k == "by_devices":
             print(" ", k, {kk: r(vv["value"] / 1e6, 2) for kk, vv in v.items() if isinstance(vv, dict)})
-        elif k == "node_drain":
+        elif k in ("node_drain", "bls_commit_round"):
             print(" ", k, {kk: (r(vv, 2) if isinstance(vv, float) else vv) for kk, vv in v.items()
                            if not isinstance(vv, (dict, list, str))})
         else:
