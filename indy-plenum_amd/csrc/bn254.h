@@ -165,35 +165,51 @@ EDV_HD void fp_neg(fp& r, const fp& a) {
 }
 EDV_HD void fp_dbl(fp& r, const fp& a) { fp_add(r, a, a); }
 
-// Montgomery product a * b / 2^256 mod p (CIOS; inputs < p, output < p).
+// 32-bit add with carry: on the device one v_add_co_u32 / v_addc_co_u32 (a 64-bit intermediate
+// would take the slower 64-bit adds and the register moves they need).
+EDV_HD uint32_t bn_addc(uint32_t a, uint32_t b, unsigned& c) {
+#if defined(__clang__)
+  unsigned co;
+  const uint32_t r = __builtin_addc(a, b, c, &co);
+  c = co;
+  return r;
+#else
+  const uint64_t t = (uint64_t)a + b + c;
+  c = (unsigned)(t >> 32);
+  return (uint32_t)t;
+#endif
+}
+
+// Montgomery product a * b / 2^256 mod p (CIOS; inputs < p, output < p), shaped for a lone
+// wave: in each of the 8 rounds the 8 products a_j b_i + t_j (and then m p_j + t_j) are
+// independent v_mad_u64_u32 -- none waits for the one before it, as the carry-in of the
+// textbook inner loop makes it -- and their high words go into the next limb by one
+// add-with-carry chain afterwards (a_j b_i + t_j < 2^64).  The BLS wave form's A/B: 25 checks
+// 3.24-3.32 ms against 3.36-3.43 with the carry-in form (profiles/r07w).
 EDV_BN_FP void fp_mul(fp& r, const fp& a, const fp& b) {
   uint32_t t[10];
 #pragma unroll
   for (int k = 0; k < 10; ++k) t[k] = 0;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    uint64_t c = 0;
+    uint64_t p[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const uint64_t s = (uint64_t)a.v[j] * b.v[i] + t[j] + c;
-      t[j] = (uint32_t)s;
-      c = s >> 32;
-    }
-    uint64_t s = (uint64_t)t[8] + c;
-    t[8] = (uint32_t)s;
-    t[9] = (uint32_t)(s >> 32);
+    for (int j = 0; j < 8; ++j) p[j] = (uint64_t)a.v[j] * b.v[i] + t[j];
+    unsigned cy = 0;
+    t[0] = (uint32_t)p[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) t[j] = bn_addc((uint32_t)p[j], (uint32_t)(p[j - 1] >> 32), cy);
+    t[8] = bn_addc(t[8], (uint32_t)(p[7] >> 32), cy);
+    t[9] = cy;
     const uint32_t m = t[0] * kNP0;
-    s = (uint64_t)m * kP[0] + t[0];
-    c = s >> 32;
+    uint64_t q[8];
 #pragma unroll
-    for (int j = 1; j < 8; ++j) {
-      s = (uint64_t)m * kP[j] + t[j] + c;
-      t[j - 1] = (uint32_t)s;
-      c = s >> 32;
-    }
-    s = (uint64_t)t[8] + c;
-    t[7] = (uint32_t)s;
-    t[8] = t[9] + (uint32_t)(s >> 32);
+    for (int j = 0; j < 8; ++j) q[j] = (uint64_t)m * kP[j] + t[j];
+    cy = 0;  // q[0]'s low word is 0: m makes t_0 + m p_0 divisible by 2^32
+#pragma unroll
+    for (int j = 1; j < 8; ++j) t[j - 1] = bn_addc((uint32_t)q[j], (uint32_t)(q[j - 1] >> 32), cy);
+    t[7] = bn_addc(t[8], (uint32_t)(q[7] >> 32), cy);
+    t[8] = t[9] + cy;
   }
   fp_reduce_once(r, t);
 }
