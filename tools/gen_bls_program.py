@@ -609,6 +609,7 @@ def _is_heavy(op):
 
 
 RIDERS = True  # heavy steps also take ready sums (--no-riders: products only)
+MUL_WEIGHT = 6.0  # a product's cost in light steps, for the critical-path priorities (--mul-weight)
 
 
 def schedule(ops, outs):
@@ -616,7 +617,7 @@ def schedule(ops, outs):
     ready operation is a product (or inversion) is a heavy step and takes
     every kind of ready operation (RIDERS) or only products; otherwise only
     light ones (sums, zero tests) -- a product costs ~2 light steps."""
-    w = {MUL: 6.0, INV: 40.0, LIN: 1.0, ZCHK: 1.0}
+    w = {MUL: MUL_WEIGHT, INV: 40.0, LIN: 1.0, ZCHK: 1.0}
     order = list(ops)  # topological
     users = {x: [] for x in order}
     for x in order:
@@ -917,7 +918,9 @@ def main():
     ap.add_argument("--mul-terms", type=int, default=2)
     ap.add_argument("--max-terms", type=int, default=MAX_TERMS)
     ap.add_argument("--no-riders", action="store_true")
+    ap.add_argument("--mul-weight", type=float, default=MUL_WEIGHT)
     a = ap.parse_args()
+    globals()["MUL_WEIGHT"] = a.mul_weight
     globals()["MAX_TERMS"] = a.max_terms
     globals()["RIDERS"] = not a.no_riders
     prog = compile_program(a.mul_terms)
