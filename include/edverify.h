@@ -400,11 +400,11 @@ int edv_bls_set_pair_lanes(edv_ctx *ctx, uint64_t max_checks);
  * pairing check (both Miller loops on one accumulator, the final
  * exponentiation) as a straight-line program of Fp operations spread over
  * the wave's 64 lanes (bls_program.h, tools/gen_bls_program.py), the latency
- * form for a COMMIT round's ~25 checks (~3 ms; 4,096 checks ~11.5 ms, where
- * the four-lane form takes ~20 ms from one check).  A degenerate Miller step
+ * form for a COMMIT round's ~25 checks (~3 ms; 8,192 checks ~22 ms, where
+ * the two-lane form takes ~27 ms and the four-lane ~18 ms from one check).  A degenerate Miller step
  * (only a verkey sum outside the order-r subgroup makes one) re-runs on the
  * four-lane kernel, so the verdicts are every form's.  0: never.  Default
- * 4096.  Replaces the same indy-crypto calls as edv_bls_verify_batch. */
+ * 8192.  Replaces the same indy-crypto calls as edv_bls_verify_batch. */
 int edv_bls_set_wave_checks(edv_ctx *ctx, uint64_t max_checks);
 
 #ifdef __cplusplus

@@ -1384,7 +1384,7 @@ struct edv_ctx {
   // per sub-batch: block offsets [kSortBlocks][bins], bin totals / bases [bins] x 2, scan scratch
   int key_sort = 2;
   uint64_t bls_pair_max = 32768;  // edv_bls_set_pair_lanes
-  uint64_t bls_wave_max = 4096;   // edv_bls_set_wave_checks (4,096 checks 11.5 ms; the four-lane form ~20)
+  uint64_t bls_wave_max = 8192;   // edv_bls_set_wave_checks (8,192 checks 21.8 ms; the two-lane form 27.3)
   // the small keyed path reads its packed inputs straight from pinned host memory (no H2D copy
   // before the kernel); A/B switch EDV_SMALL_ZC=1
   bool small_zero_copy = getenv("EDV_SMALL_ZC") != nullptr;

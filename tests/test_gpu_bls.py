@@ -23,7 +23,7 @@ def bls_mode(request, gpu_engine):
         gpu_engine.bls_set_wave_checks(n if request.param == "wave" else 0)
         gpu_engine.bls_set_pair_lanes({"wave": 0, "quad": 2 * n, "pair": n, "one": 0}[request.param])
     yield set_for
-    gpu_engine.bls_set_wave_checks(4096)
+    gpu_engine.bls_set_wave_checks(8192)
     gpu_engine.bls_set_pair_lanes(32768)
 
 
@@ -150,4 +150,4 @@ def test_wave_form_hands_over_what_it_cannot_decide(gpu_engine):
             gpu_engine.bls_set_pair_lanes(32768)
             assert (gpu_engine.bls_verify_batch(sigs, buf, off, vk_rows, gen) == want).all(), wave
     finally:
-        gpu_engine.bls_set_wave_checks(4096)
+        gpu_engine.bls_set_wave_checks(8192)
