@@ -621,8 +621,8 @@ __global__ __launch_bounds__(kBlock) void edv_ok_pack_kernel(const uint8_t* __re
 // with LDS cursors.  Order within a key is arbitrary (verdicts are per
 // request).
 constexpr uint32_t kSortBlocks = 256, kSortThreads = 1024;
-constexpr uint64_t kCompactBytes = 256 << 10;
-constexpr size_t kMaxPending = 64;  // uncollected edv_verify_submit tickets per context  // host_submit: small chunks in one pinned block, one copy
+constexpr uint64_t kCompactBytes = 256 << 10;  // host_submit: small chunks in one pinned block, one copy
+constexpr size_t kMaxPending = 64;  // uncollected edv_verify_submit tickets per context
 constexpr uint32_t kSortMaxBins = 16384;  // 64 KiB of LDS per block
 __device__ __forceinline__ void sort_range(uint64_t n, uint64_t& lo, uint64_t& hi) {
   const uint64_t per = (n + gridDim.x - 1) / gridDim.x;

@@ -439,7 +439,7 @@ extern "C" {
 int edv_host_bls_verify_program(const uint8_t sig128[128], const uint8_t* msg, uint64_t mlen, const uint8_t* vk128,
                                 uint64_t vk_n, const uint8_t gen128[128]) {
   using namespace edv::bn;
-  static fp S[edv::blsp::kSlots];
+  thread_local fp S[edv::blsp::kSlots];  // per thread: concurrent callers (test workers) never share slots
   for (int k = 0; k < edv::blsp::kConsts; ++k) fp_load(S[edv::blsp::kConstSlot[k]], edv::blsp::kConstVal + 8 * k);
   g1 s, h;
   g2 g, v;
@@ -463,7 +463,7 @@ int edv_host_bls_verify_program(const uint8_t sig128[128], const uint8_t* msg, u
                       P::kIn_Q2Xa, P::kIn_Q2Xb, P::kIn_Q2Ya, P::kIn_Q2Yb, P::kIn_Q2Za, P::kIn_Q2Zb};
   for (int k = 0; k < 12; ++k) S[qs[k]] = *q[k];
   uint32_t flag = 0;
-  static fp res[64];
+  thread_local fp res[64];
   bool wr[64];
   uint32_t dst[64];
   for (int st = 0; st < P::kSteps; ++st) {

@@ -119,6 +119,7 @@ _STAGE_MIN_BATCH = 1 << 16  # batches staged while scanned (edv_stage_put from t
 
 
 _MISSING = object()
+_BUSY = object()  # _authenticate_staged: the staging set is held by a batch in flight
 _IGNORE_SIG = (SIG,)
 
 
@@ -130,6 +131,17 @@ class _Prepared:
 
 
 _LOCKS_LOCK = threading.Lock()
+
+
+def _collect_quietly(eng, handles):
+    """Collect (and so free) submitted verify tickets whose verdicts nobody will
+    read -- the clean-up of a batch path that raised between submit and
+    collect; their errors are not the caller's."""
+    for h in handles:
+        try:
+            eng.verify_collect(h)
+        except Exception:
+            pass
 
 
 def _engine_lock(eng):
@@ -655,6 +667,8 @@ class GpuAuthMixin:
             if (self._g.stage and _repack_spans is not None and len(msgs) >= _STAGE_MIN_BATCH
                     and getattr(eng, "supports_staging", False) and slot == _SIG_SLOT and bufs is not self._g.scan_out):
                 res = self._authenticate_staged(msgs, eng, slot, bufs)
+                if res is _BUSY:  # set 0's pinned buffers may still be feeding that batch's copies
+                    return self._authenticate_batch_scanned_into(msgs, self._g.scan_out, slot)
                 if res is not None:
                     return res
                 bufs = self._scan_buffers(eng, len(msgs), slot)  # regrown from the new size estimate
@@ -685,9 +699,16 @@ class GpuAuthMixin:
         n = len(msgs)
         msg_cap = len(bufs[1])
         slot_base = (msg_cap + 255) // 256 * 256
-        if hasattr(eng, "stage_select"):
-            eng.stage_select(staging_set)
-        eng.stage_reserve(slot_base + n * slot)
+        try:
+            if hasattr(eng, "stage_select"):
+                eng.stage_select(staging_set)
+            eng.stage_reserve(slot_base + n * slot)
+        except Exception:
+            # the set is busy (an unfinished authenticate_batches iteration holds its batch in
+            # flight there): nothing was scanned or staged, the caller takes the unstaged path
+            if defer:
+                raise
+            return _BUSY
         sfx = "" if staging_set == 0 else str(staging_set)
         spans_buf = self._pinned(eng, "pinned_spans" + sfx, 16 * n)  # the scan writes the item spans here
         t0 = perf_counter()
@@ -829,14 +850,18 @@ class GpuAuthMixin:
         msg_a = np.frombuffer(msg_o, np.uint8, count=mlen)
         t2 = perf_counter()
         handles, oks = [], []
-        for c0 in range(0, n, _STREAM_CHUNK):
-            c1 = min(n, c0 + _STREAM_CHUNK)
-            _pack_range(handle, c0, c1)
-            if len(handles) - len(oks) >= _STREAM_WINDOW:  # bounded in flight (the library holds 64 tickets)
+        try:
+            for c0 in range(0, n, _STREAM_CHUNK):
+                c1 = min(n, c0 + _STREAM_CHUNK)
+                _pack_range(handle, c0, c1)
+                if len(handles) - len(oks) >= _STREAM_WINDOW:  # bounded in flight (the library holds 64 tickets)
+                    oks.append(np.asarray(eng.verify_collect(handles[len(oks)]), bool))
+                handles.append(eng.verify_submit(sig_a[c0:c1], kid[c0:c1], msg_a, off_a[c0:c1 + 1], True, slot))
+            t3 = perf_counter()
+            while len(oks) < len(handles):
                 oks.append(np.asarray(eng.verify_collect(handles[len(oks)]), bool))
-            handles.append(eng.verify_submit(sig_a[c0:c1], kid[c0:c1], msg_a, off_a[c0:c1 + 1], True, slot))
-        t3 = perf_counter()
-        oks += [np.asarray(eng.verify_collect(h), bool) for h in handles[len(oks):]]
+        finally:
+            _collect_quietly(eng, handles[len(oks):])  # an exception between submit and collect: free the tickets
         ok = np.concatenate(oks) if oks else np.zeros(0, bool)
         t4 = perf_counter()
         del handles, oks, sig_a, msg_a, kid
@@ -861,7 +886,9 @@ class GpuAuthMixin:
         state (every item scanned, every identifier resolved to a registered
         key) is submitted asynchronously; any other part takes the ordinary
         path synchronously (same verdicts either way).  getVerkey is called
-        once per distinct identifier of the whole batch."""
+        once per distinct identifier of the whole batch.  At most
+        _STREAM_WINDOW parts are in flight (the library holds kMaxPending
+        tickets); a part that raises leaves no ticket behind."""
         import numpy as np
         g = self._g
         n = len(msgs)
@@ -871,49 +898,60 @@ class GpuAuthMixin:
         msg_mv = memoryview(bufs[1]).cast("B")
         mpos, mtotal = 0, 0
         parts = []
-        for lo in range(0, n, part):
-            hi = min(n, lo + part)
-            chunk = msgs[lo:hi]
-            out = [sig_mv[lo * slot:hi * slot], msg_mv[mpos:]]
-            scan = _scan_batch(chunk, [SIG], g.scan_threads, out, slot)
-            fast_b, uidx_b, uniq, sig_o, msg_o, off, short = scan
-            mlen = int(np.frombuffer(off, np.uint64)[-1])
-            mtotal += mlen
-            if msg_o is out[1]:
-                mpos += mlen
-            ukeys = []
-            for idr in uniq:
-                k = memo.get(idr, _MISSING)
-                if k is _MISSING:
-                    k = memo[idr] = self._key_for(idr)  # authenticate():93-99, once per identifier
-                ukeys.append(k)
-            ids = None
-            if ks is not None and fast_b.count(0) == 0 and all(k.__class__ is bytes for k in ukeys):
-                ids = ks.lookup(ukeys)
-                if any(i is None for i in ids):
-                    ids = None
-            if ids is None:  # not the steady state: this part the ordinary way
-                parts.append(("done", self._finish_scanned(chunk, scan, slot, ukeys)))
-                continue
-            kid = np.asarray(ids, np.uint32)[np.frombuffer(uidx_b, np.uint32)]
-            handle = eng.verify_submit(np.frombuffer(sig_o, np.uint8, count=slot * (hi - lo)).reshape(-1, slot),
-                                       kid, np.frombuffer(msg_o, np.uint8, count=mlen),
-                                       np.frombuffer(off, np.uint64), True, slot)
-            parts.append(("async", (handle, uidx_b, uniq, short)))
-            g.stats["batches"] += 1
-            g.stats["batch_items"] += hi - lo
-            g.stats["keyed_items"] += hi - lo
+        inflight = []  # indices into parts of the submitted, uncollected parts (oldest first)
+
+        def collect(j):
+            handle, uidx_b, uniq, short = parts[j][1]
+            ok = np.asarray(eng.verify_collect(handle), bool) & (np.frombuffer(short, np.uint8) == 0)
+            res = _results_from(ok.view(np.uint8).tobytes(), uidx_b, uniq)
+            for i in np.flatnonzero(~ok).tolist():
+                res[i] = InvalidSignature()
+            parts[j] = ("done", res)
+        try:
+            for lo in range(0, n, part):
+                hi = min(n, lo + part)
+                chunk = msgs[lo:hi]
+                out = [sig_mv[lo * slot:hi * slot], msg_mv[mpos:]]
+                scan = _scan_batch(chunk, [SIG], g.scan_threads, out, slot)
+                fast_b, uidx_b, uniq, sig_o, msg_o, off, short = scan
+                mlen = int(np.frombuffer(off, np.uint64)[-1])
+                mtotal += mlen
+                if msg_o is out[1]:
+                    mpos += mlen
+                ukeys = []
+                for idr in uniq:
+                    k = memo.get(idr, _MISSING)
+                    if k is _MISSING:
+                        k = memo[idr] = self._key_for(idr)  # authenticate():93-99, once per identifier
+                    ukeys.append(k)
+                ids = None
+                if ks is not None and fast_b.count(0) == 0 and all(k.__class__ is bytes for k in ukeys):
+                    ids = ks.lookup(ukeys)
+                    if any(i is None for i in ids):
+                        ids = None
+                if ids is None:  # not the steady state: this part the ordinary way
+                    parts.append(("done", self._finish_scanned(chunk, scan, slot, ukeys)))
+                    continue
+                if len(inflight) >= _STREAM_WINDOW:  # bounded in flight
+                    collect(inflight.pop(0))
+                kid = np.asarray(ids, np.uint32)[np.frombuffer(uidx_b, np.uint32)]
+                handle = eng.verify_submit(np.frombuffer(sig_o, np.uint8, count=slot * (hi - lo)).reshape(-1, slot),
+                                           kid, np.frombuffer(msg_o, np.uint8, count=mlen),
+                                           np.frombuffer(off, np.uint64), True, slot)
+                parts.append(("async", (handle, uidx_b, uniq, short)))
+                inflight.append(len(parts) - 1)
+                g.stats["batches"] += 1
+                g.stats["batch_items"] += hi - lo
+                g.stats["keyed_items"] += hi - lo
+            while inflight:
+                collect(inflight[0])
+                inflight.pop(0)
+        finally:
+            _collect_quietly(eng, [parts[j][1][0] for j in inflight])
         if n:
             g.msg_bytes_per_item = max(g.msg_bytes_per_item * 0.5, mtotal / n)
         results = []
-        for kind, payload in parts:
-            if kind == "async":
-                handle, uidx_b, uniq, short = payload
-                ok = np.asarray(eng.verify_collect(handle), bool) & (np.frombuffer(short, np.uint8) == 0)
-                res = _results_from(ok.view(np.uint8).tobytes(), uidx_b, uniq)
-                for i in np.flatnonzero(~ok).tolist():
-                    res[i] = InvalidSignature()
-                payload = res
+        for _, payload in parts:
             results += payload
         return results
 

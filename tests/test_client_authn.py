@@ -710,6 +710,60 @@ def test_streamed_batch_bounded_in_flight(oracle, monkeypatch):
                                           for i, m in enumerate(msgs)]
 
 
+def test_pipelined_parts_bounded_in_flight(oracle, monkeypatch):
+    """a pipelined batch of more parts than the library holds
+    tickets (kMaxPending = 64): the oldest parts are collected before new ones
+    go out, every verdict in request order."""
+    from plenum_amd import client_authn as CA
+    idrs, vks, msgs = _signed(3, 4480)
+    monkeypatch.setattr(CA, "_STREAM_WINDOW", 5)
+    eng = OracleEngine(oracle)
+    a = GpuAuthNr(engine=eng, pipeline_part=64)  # 70 parts
+    for i, v in zip(idrs, vks):
+        a.addIdr(i, v)
+    a.keys_settle()
+    batch = [dict(m) for m in msgs]
+    batch[4400]["reqId"] += 1
+    got = a.authenticate_batch(batch)
+    assert eng.submits >= 70 and eng.max_in_flight <= 5 and eng.in_flight == 0
+    assert [_outcome(r) for r in got] == [m["identifier"] if i != 4400 else ("InvalidSignature", (), None)
+                                          for i, m in enumerate(msgs)]
+
+
+@pytest.mark.parametrize("where", ["streamed", "pipelined"])
+def test_batch_raising_between_submit_and_collect_frees_tickets(oracle, monkeypatch, where):
+    """an exception after some chunks were submitted and before they
+    were collected (here in the pack, or in a later part's scan) leaves no
+    ticket outstanding, so the next batch on the same engine still runs."""
+    from plenum_amd import client_authn as CA
+    idrs, vks, msgs = _signed(3, 5000)
+    eng = OracleEngine(oracle)
+    if where == "streamed":
+        monkeypatch.setattr(CA, "_STREAM_CHUNK", 512)
+        a = GpuAuthNr(engine=eng)
+        real, name = CA._pack_range, "_pack_range"
+    else:
+        a = GpuAuthNr(engine=eng, pipeline_part=512)
+        real, name = CA._scan_batch, "_scan_batch"
+    for i, v in zip(idrs, vks):
+        a.addIdr(i, v)
+    a.keys_settle()
+    calls = []
+
+    def flaky(*args):
+        calls.append(1)
+        if len(calls) == 4:
+            raise MemoryError("injected")
+        return real(*args)
+    monkeypatch.setattr(CA, name, flaky)
+    with pytest.raises(MemoryError):
+        a.authenticate_batch([dict(m) for m in msgs])
+    assert eng.submits >= 2 and eng.in_flight == 0
+    monkeypatch.setattr(CA, name, real)
+    assert a.authenticate_batch(msgs) == [m["identifier"] for m in msgs]
+    assert eng.in_flight == 0
+
+
 def test_authenticate_batches_pipeline(oracle, monkeypatch):
     """authenticate_batches: two batches in flight over the engine's two
     staging sets (the double refuses to reuse a set whose submission was not
@@ -761,3 +815,33 @@ def test_authenticate_batches_abandoned_frees_the_set(oracle, monkeypatch):
     assert eng.held[0] is None and eng.held[1] is None
     assert first == [m["identifier"] for m in b]
     assert a.authenticate_batch(b) == first
+
+
+def test_authenticate_batch_while_an_iteration_holds_set_0(oracle, monkeypatch):
+    """an authenticate_batches generator left unfinished (still
+    referenced) with its batch in flight in staging set 0; a later
+    authenticate_batch does not raise out of the busy set: it takes the
+    unpinned path, with the same outcomes, and leaves the batch in flight
+    alone until the iteration is finished."""
+    from engine_double import StagingOracleEngine
+    from plenum_amd import client_authn as CA
+    monkeypatch.setattr(CA, "_STAGE_MIN_BATCH", 1000)
+    monkeypatch.setattr(CA, "_PINNED_MIN_BATCH", 1000)
+    idrs, vks, msgs = _signed(3, 2400)
+    eng = StagingOracleEngine(oracle)
+    a = GpuAuthNr(engine=eng)
+    for i, v in zip(idrs, vks):
+        a.addIdr(i, v)
+    a.keys_settle()
+    b = [dict(m) for m in msgs[:1200]]
+    want = [m["identifier"] for m in b]
+    it = a.authenticate_batches([b, b, b, b])
+    assert next(it) == want and next(it) == want  # batch 2 now in flight in set 0
+    assert eng.held[0] is not None
+    forged = [dict(m) for m in b]
+    forged[9]["reqId"] += 1
+    got = a.authenticate_batch(forged)
+    assert [_outcome(r) for r in got] == [m["identifier"] if i != 9 else ("InvalidSignature", (), None)
+                                          for i, m in enumerate(b)]
+    assert eng.held[0] is not None  # untouched
+    assert list(it) == [want, want] and eng.held == [None, None]
