@@ -189,6 +189,21 @@ def cpu_baseline(sig, pk, msgs, off, threads):
     return n / secs.value, ok.astype(bool), ("reference" if kind == 1 else "port"), ver
 
 
+def sodium_all_items(sig, pk, msgs, starts, ends, threads):
+    """libsodium 1.0.18's verdict on EVERY item of the batch (spans into msgs;
+    oracle/cpu_baseline.c, untimed, all of this job's CPUs): the full-batch
+    parity check beside the construction's.  None when libsodium is absent."""
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "_build", "libcpu_baseline.so"))
+    n = len(starts)
+    ok = np.zeros(n, np.uint8)
+    P = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    sig, pk, msgs = (np.ascontiguousarray(a, np.uint8) for a in (sig, pk, msgs))
+    starts, ends = (np.ascontiguousarray(a, np.uint64) for a in (starts, ends))
+    t0 = time.perf_counter()
+    r = lib.cpu_baseline_verdicts_spans(P(sig), P(pk), P(msgs), P(starts), P(ends), ctypes.c_uint64(n), threads, P(ok))
+    return (ok.astype(bool), time.perf_counter() - t0) if r == 1 else (None, 0.0)
+
+
 def host_cpus():
     """nproc / affinity / cgroup CPU quota of this host (the GPU box shows the
     whole machine in nproc; the quota is this job's share)."""
@@ -980,6 +995,7 @@ def main():
                                                                                           reg_pks.shape[0])}
 
     cpu = None
+    lib_mis = 0
     if rank == 0 and world == 1 and not args.no_cpu:
         s = min(args.cpu_sample if args.config != "c3" else args.cpu_sample // 4, n)
         sig_h = d_sig[:s].cpu().numpy()
@@ -1004,6 +1020,14 @@ def main():
                "by_threads": {str(t): r for t, (r, _) in runs.items()},
                "host": host,
                "agrees_with_gpu": bool(all((o == got[:s]).all() for _, o in runs.values()))}
+        # every item of the timed batch against libsodium (untimed): the step's bitmask == libsodium's
+        lib_ok, lib_s = sodium_all_items(d_sig.cpu().numpy(), d_pk.cpu().numpy(), buf, item_start, item_end,
+                                         min(16, host["affinity"]))
+        if lib_ok is not None:
+            lib_mis = int((lib_ok != got).sum())
+            cpu["agrees_with_gpu_all_items"] = lib_mis == 0
+            cpu["all_items_check"] = {"items": n, "mismatches": lib_mis, "accepted_by_libsodium": int(lib_ok.sum()),
+                                      "threads": min(16, host["affinity"]), "seconds": lib_s}
         if args.e2e_c0 > 0:
             cpu["reference_path_configs0"] = reference_path_baseline(eng, args.e2e_c0, host)
 
@@ -1085,6 +1109,7 @@ def main():
             "end_to_end": e2e,
             "cpu_baseline": cpu,
             "parity": {"mismatches_vs_construction": mismatches, "accepted": accepted, "expected": expected,
+                       "mismatches_vs_libsodium_all_items": (cpu or {}).get("all_items_check", {}).get("mismatches"),
                        "ranks": world, "accepted_in_gathered_bitmask": gathered_accepted},
             "tally": tally_result,
             "collective": collective,
@@ -1094,7 +1119,7 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     eng.close()
-    if mismatches:
+    if mismatches or lib_mis:
         sys.exit(3)
 
 

@@ -55,6 +55,7 @@ const char *cpu_baseline_sodium_version(void) {
 typedef struct {
   const uint8_t *sig, *pk, *msgs;
   const uint64_t *off;
+  const uint64_t *start, *end; /* spans form (off == NULL): item i's message is msgs[start[i], end[i]) */
   uint64_t lo, hi;
   int use_sodium;
   uint8_t *ok; /* one byte per item */
@@ -63,8 +64,9 @@ typedef struct {
 static void *worker(void *arg) {
   job_t *j = (job_t *)arg;
   for (uint64_t i = j->lo; i < j->hi; i++) {
-    const uint8_t *m = j->msgs + j->off[i];
-    uint64_t ml = j->off[i + 1] - j->off[i];
+    const uint64_t a = j->off ? j->off[i] : j->start[i], b = j->off ? j->off[i + 1] : j->end[i];
+    const uint8_t *m = j->msgs + a;
+    uint64_t ml = b - a;
     int r = j->use_sodium ? g_sodium_verify(j->sig + 64 * i, m, ml, j->pk + 32 * i)
                           : oracle_verify_detached(j->sig + 64 * i, m, ml, j->pk + 32 * i);
     j->ok[i] = (r == 0);
@@ -90,10 +92,29 @@ int cpu_baseline_run(const uint8_t *sig64, const uint8_t *pk32, const uint8_t *m
   job_t jobs[1024];
   double t0 = now_s();
   for (int t = 0; t < threads; t++) {
-    jobs[t] = (job_t){sig64, pk32, msgs, msg_off, n * t / threads, n * (t + 1) / threads, sodium, ok};
+    jobs[t] = (job_t){sig64, pk32, msgs, msg_off, NULL, NULL, n * t / threads, n * (t + 1) / threads, sodium, ok};
     if (pthread_create(&tid[t], NULL, worker, &jobs[t]) != 0) return -1;
   }
   for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);
   *seconds = now_s() - t0;
   return sodium;
+}
+
+/* Verdicts of n items whose messages are spans msgs[start[i], end[i]) (several
+ * items may share one message: configs[3]'s multi-signature requests), on
+ * `threads` threads -- the parity tests' full-batch check against libsodium.
+ * Returns 1 if libsodium gave the verdicts, 0 if it is absent (nothing
+ * written), -1 on error. */
+int cpu_baseline_verdicts_spans(const uint8_t *sig64, const uint8_t *pk32, const uint8_t *msgs, const uint64_t *start,
+                                const uint64_t *end, uint64_t n, int threads, uint8_t *ok) {
+  if (threads < 1 || threads > 1024) return -1;
+  if (!load_sodium()) return 0;
+  pthread_t tid[1024];
+  job_t jobs[1024];
+  for (int t = 0; t < threads; t++) {
+    jobs[t] = (job_t){sig64, pk32, msgs, NULL, start, end, n * t / threads, n * (t + 1) / threads, 1, ok};
+    if (pthread_create(&tid[t], NULL, worker, &jobs[t]) != 0) return -1;
+  }
+  for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);
+  return 1;
 }

@@ -85,3 +85,46 @@ def sodium():
         lib.sodium_version_string.restype = ctypes.c_char_p
         return lib
     return None
+
+
+def host_threads():
+    """CPUs this process may use: affinity capped by a cgroup v2 quota (the GPU
+    box shows 256 CPUs and grants 16)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, int(float(q) / float(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+@pytest.fixture(scope="session")
+def sodium_verdicts():
+    """verdicts(sig64[n,64], pk32[n,32], msgs, start[n], end[n]) -> bool[n]:
+    libsodium 1.0.18's crypto_sign_verify_detached on every item, on all of
+    this host's CPUs (oracle/cpu_baseline.c; test infrastructure) -- the
+    full-batch parity check (about 2 s per 1M items on 16 threads)."""
+    lib = ctypes.CDLL(_ensure_built(os.path.join(ROOT, "oracle", "_build", "libcpu_baseline.so"),
+                                    os.path.join(ROOT, "oracle")))
+    lib.cpu_baseline_sodium_version.restype = ctypes.c_char_p
+    P = ctypes.c_void_p
+
+    def verdicts(sig, pk, msgs, start, end):
+        sig = np.ascontiguousarray(sig, np.uint8)
+        pk = np.ascontiguousarray(pk, np.uint8)
+        msgs = np.ascontiguousarray(msgs, np.uint8)
+        start = np.ascontiguousarray(start, np.uint64)
+        end = np.ascontiguousarray(end, np.uint64)
+        n = len(start)
+        assert sig.shape == (n, 64) and pk.shape == (n, 32) and len(end) == n
+        assert n == 0 or int(end.max()) <= len(msgs)
+        ok = np.zeros(n, np.uint8)
+        r = lib.cpu_baseline_verdicts_spans(P(sig.ctypes.data), P(pk.ctypes.data), P(msgs.ctypes.data),
+                                            P(start.ctypes.data), P(end.ctypes.data), ctypes.c_uint64(n),
+                                            host_threads(), P(ok.ctypes.data))
+        assert r == 1, "libsodium not loadable (cpu_baseline_verdicts_spans -> %d)" % r
+        assert lib.cpu_baseline_sodium_version().decode() == "1.0.18"
+        return ok.astype(bool)
+    return verdicts

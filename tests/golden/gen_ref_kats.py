@@ -119,6 +119,23 @@ def authn_kats():
     run("explicit-signature-wrong", dict(base), abbr_vk, identifier=did_idr, signature=sign(dict(base, reqId=2)))
     run("float-field", dict(base, reqId=1.5, signature=sign(dict(base, reqId=1.5))), abbr_vk)
     run("tuple-field", dict(good, operation=(1, 2)), abbr_vk)
+    # A signed request the reference itself holds: the PROPAGATE payload of
+    # plenum/test/node_request/message_request/test_valid_message_request.py:60-64
+    # (data only).  Its identifier is a 32-byte cryptonym, so with an empty
+    # verkey on record DidVerifier uses the identifier as the key
+    # (plenum/common/verifier.py:26-28).
+    prop = {"identifier": "5rArie7XKukPCaEwq5XGQJnM9Fc5aZE3M9HAPVfMU2xC",
+            "signature": "ZbZG68WiaK67eU3CsgpVi85jpgCztW9Yqe7D5ezDUfWbKdiPPVbWq4Tb5m4Ur3jcR5wJ8zmBUZXZudjvMN63Aa9",
+            "operation": {"amount": 62, "type": "buy"},
+            "reqId": 1499782864169193}
+    psig = _b58decode(prop["signature"])
+    run("ref-propagate-cryptonym", prop, "")
+    run("ref-propagate-full-verkey", prop, prop["identifier"])
+    run("ref-propagate-tampered-reqId", dict(prop, reqId=prop["reqId"] + 1), "")
+    run("ref-propagate-tampered-amount", dict(prop, operation=dict(prop["operation"], amount=63)), "")
+    run("ref-propagate-tampered-S", dict(prop, signature=_b58encode(psig[:40] + bytes([psig[40] ^ 1]) + psig[41:])), "")
+    run("ref-propagate-sig-63-bytes", dict(prop, signature=_b58encode(psig[:63])), "")
+    run("ref-propagate-unregistered", prop, "", register=False)
     # DidVerifier KATs from plenum/test/common/test_verifier.py
     dv = DidVerifier("~8zH9ZSyZTFPGJ4ZPL5Rvxx", identifier="99BgFBg35BehzfSADV5nM4")
     return {"cases": cases, "did_expand": [{"verkey": "~8zH9ZSyZTFPGJ4ZPL5Rvxx", "identifier": "99BgFBg35BehzfSADV5nM4",

@@ -30,7 +30,7 @@ def test_mixin_over_reference_simpleauthnr():
 
 def test_committed_record():
     rec = json.load(open(os.path.join(GOLDEN, "dropin_ref_check.json")))
-    assert rec["ok"] and rec["matched"] == rec["cases"] == 50
+    assert rec["ok"] and rec["matched"] == rec["cases"] == 64
     assert rec["libsodium_crypto_sign_open_calls"] == 0
     assert rec["forged_propagate"].startswith("SuspiciousNode")
 

@@ -30,6 +30,35 @@ def test_batch_on_gpu(gpu_engine):
     assert a.stats["batches"] == 1
 
 
+def test_reference_propagate_vector_on_gpu(gpu_engine):
+    """The signed PROPAGATE the reference holds (test_valid_message_request.py:
+    60-64; cryptonym identifier, so the key is the identifier itself,
+    verifier.py:26-28) and its tampered variants, one batch of them repeated
+    across a 5,000-request authenticate_batch (the native scan, the GPU) and
+    each once through authenticate(), on the key-table and general paths:
+    every outcome the reference's own authenticate() gave (authn_kat.json)."""
+    cases = [c for c in T.kat()["cases"] if c["name"].startswith("ref-propagate-")]
+    assert len(cases) == 7
+    for max_keys in (16, 0):
+        a = GpuAuthNr(engine=gpu_engine, max_keys=max_keys)
+        idr = cases[0]["msg"]["identifier"]
+        a.addIdr(idr, "")  # on record with an empty verkey: the cryptonym resolves to the key
+        a.keys_settle()
+        pool = [c for c in cases if c["register"] and c["verkey"] == ""]
+        batch = [dict(pool[i % len(pool)]["msg"]) for i in range(5000)]
+        res = a.authenticate_batch(batch)
+        for i, r in enumerate(res):
+            c = pool[i % len(pool)]
+            if "result" in c:
+                assert r == c["result"], (max_keys, c["name"], r)
+            else:
+                assert type(r).__name__ == c["raises"], (max_keys, c["name"], r)
+        for c in cases:
+            T.check_result(c, T.run_single(T.make(gpu_engine, c), c))
+        if max_keys:
+            assert a.stats["keyed_items"] > 0
+
+
 def test_multi_on_gpu(gpu_engine):
     a, msg, sigs = T._multi_fixture(gpu_engine)
     assert a.authenticate_multi(msg, sigs) == list(sigs)
@@ -474,7 +503,7 @@ def _oracle_verdicts(sig64, pk32, msgs, threads=16):
 _C3_SIGS = 100_000
 
 
-def test_configs3_multi_signature_shape_vs_oracle(gpu_engine):
+def test_configs3_multi_signature_shape_vs_oracle(gpu_engine, sodium_verdicts):
     """BASELINE configs[3] at its real shape through authenticate_multi_batch:
     >= 100k signatures, 1-5 per request (distinct signers), signed payloads
     log-uniform over 64 B - 4 KiB, ~6 % of the signatures corrupted (a bit of
@@ -482,8 +511,9 @@ def test_configs3_multi_signature_shape_vs_oracle(gpu_engine):
     after signing).  Every per-signature verdict of the GPU path equals the C
     oracle's, and every request's outcome (identifiers up to the threshold, or
     InsufficientCorrectSignatures / InsufficientSignatures) is the one those
-    verdicts give.  Signers: 48 registered (key-table path) + 16 known only
-    through the state lookup (general path)."""
+    verdicts give; the verdicts are also libsodium 1.0.18's, every one.
+    Signers: 48 registered (key-table path) + 16 known only through the state
+    lookup (general path)."""
     from plenum_amd import _hostpack, pack_messages, synth
     from plenum_amd.base58 import b58encode
     from plenum_amd.exceptions import InsufficientCorrectSignatures, InsufficientSignatures
@@ -548,6 +578,10 @@ def test_configs3_multi_signature_shape_vs_oracle(gpu_engine):
     now = [serialize_msg_for_signing(q, topLevelKeysToIgnore=["signature", "signatures"]) for q in reqs]
     want = _oracle_verdicts(sig, pks[item_key], [now[r] for r in item_req])
     assert 0.85 < want.mean() < 0.97, want.mean()
+    # and libsodium 1.0.18 itself on every signature (the requests' messages shared through spans)
+    nbuf, noff = pack_messages(now)
+    lib = sodium_verdicts(sig, pks[item_key], nbuf, noff[:-1][item_req], noff[1:][item_req])
+    assert (lib == want).all(), np.flatnonzero(lib != want)[:10]
     # per-signature verdicts on the GPU path, through the same preparation authenticate_multi uses
     items = []
     for req, sigs, thr in batch:

@@ -91,3 +91,18 @@ def test_oracle_differential_vs_libsodium(oracle):
             sg = bytearray(rng.getrandbits(8) for _ in range(64))
         want = s.crypto_sign_verify_detached(bytes(sg), m, ctypes.c_ulonglong(len(m)), bytes(pkk))
         assert oracle.oracle_verify_detached(bytes(sg), m, len(m), bytes(pkk)) == want, t
+
+
+@pytest.mark.parametrize("name", ["ed25519_valid.npz", "ed25519_edge.npz"])
+def test_full_batch_sodium_harness_matches_golden(sodium_verdicts, name):
+    """The -m gpu tests' full-batch check (conftest.sodium_verdicts: libsodium on
+    every host CPU over message spans) gives the golden verdicts, with items
+    sharing one message copy too."""
+    import numpy as np
+    d = load_npz(name)
+    off = d["off"].astype(np.uint64)
+    got = sodium_verdicts(d["sig"], d["pk"], d["msgs"], off[:-1], off[1:])
+    assert (got == d["expect"].astype(bool)).all()
+    rev = np.arange(len(off) - 1)[::-1]  # the same messages through reordered spans
+    got = sodium_verdicts(d["sig"][rev], d["pk"][rev], d["msgs"], off[:-1][rev], off[1:][rev])
+    assert (got == d["expect"].astype(bool)[rev]).all()
