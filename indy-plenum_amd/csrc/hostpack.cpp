@@ -80,8 +80,38 @@ struct OutBuf {
   }
   void append(const char* src, size_t k) {
     if (n + k > cap) grow_to(n + k);
-    memcpy(d + n, src, k);
+    copy_small(d + n, src, k);
     n += k;
+  }
+  // memcpy for the short pieces of a serialization (keys and values, mostly 1-64 bytes) inlined:
+  // overlapping 16/8/4-byte moves, every load inside [src, src + k) and every store inside
+  // [dst, dst + k) (libc's memcpy was an out-of-line call per piece)
+  static inline void copy_small(char* dst, const char* src, size_t k) {
+    if (k >= 16) {
+      if (k > 64) {
+        memcpy(dst, src, k);
+        return;
+      }
+      for (size_t i = 0; i + 16 < k; i += 16)
+        _mm_storeu_si128((__m128i*)(dst + i), _mm_loadu_si128((const __m128i*)(src + i)));
+      _mm_storeu_si128((__m128i*)(dst + k - 16), _mm_loadu_si128((const __m128i*)(src + k - 16)));
+    } else if (k >= 8) {
+      uint64_t a, b;
+      memcpy(&a, src, 8);
+      memcpy(&b, src + k - 8, 8);
+      memcpy(dst, &a, 8);
+      memcpy(dst + k - 8, &b, 8);
+    } else if (k >= 4) {
+      uint32_t a, b;
+      memcpy(&a, src, 4);
+      memcpy(&b, src + k - 4, 4);
+      memcpy(dst, &a, 4);
+      memcpy(dst + k - 4, &b, 4);
+    } else if (k) {
+      dst[0] = src[0];
+      dst[k / 2] = src[k / 2];
+      dst[k - 1] = src[k - 1];
+    }
   }
   void append(const char* z) { append(z, strlen(z)); }
   void push_back(char c) {
@@ -286,6 +316,10 @@ inline const DkEntry* dk_entries(PyObject* o, Py_ssize_t& n) {
 #define EDV_HAVE_DK 1
 #endif
 bool g_scan_direct = true;  // EDV_SCAN_DIRECT=0: PyDict_Next instead (A/B); set per scan call
+inline bool g_scan_direct_env() {
+  const char* e = getenv("EDV_SCAN_DIRECT");
+  return !(e && e[0] == '0');
+}
 
 bool w_str_eq(PyObject* a, PyObject* b) {  // canonical kinds: equal strings have equal kinds
   const Py_ssize_t n = PyUnicode_GET_LENGTH(a);
@@ -446,6 +480,171 @@ WRes wser_obj(PyObject* o, int level, PyObject* ignore, OutBuf& out) {
   if (PyFloat_CheckExact(o)) return kDefer;  // Python's repr: str() under the GIL
   return kFail;
 }
+
+// ------------------------------------------------ shape-cached serialization
+// Requests from one client library have the same keys in the same insertion order, batch after
+// batch (a NYM: identifier, reqId, operation {type, dest, verkey, alias}, protocolVersion,
+// signature).  Each scan worker remembers, per nesting class and entry count, the last dict
+// "shape" it serialized generically: its key texts in insertion order, the order the serializer
+// emits them in (sorted, level-0 ignored keys dropped), the "|key:" prefixes, and where the
+// signature / identifier entries sit.  A dict whose keys match a remembered shape text for text
+// (exact compact-ASCII str keys, no deleted entries) is emitted from it: no per-key ignore or
+// top-key comparisons, no sort, one prefix copy per key.  Anything else takes wser_dict (which
+// then remembers the new shape).  The bytes are wser_dict's in every case (tests/
+// test_hostpack.py: shapes on / off / the Python restatement over a pool of near-miss shapes).
+#ifdef EDV_HAVE_DK
+constexpr int kShapeKeys = 12;     // dicts with more entries: wser_dict
+constexpr size_t kShapeKeyLen = 40;  // longer keys: wser_dict
+struct ShapeKey {
+  uint32_t len = 0;
+  uint64_t a = 0, b = 0;  // the text's first and last 8 (or 4) bytes (keys of up to 16 bytes)
+  const char* txt = nullptr;
+};
+inline uint64_t ld8(const char* p) {
+  uint64_t v;
+  memcpy(&v, p, 8);
+  return v;
+}
+inline uint32_t ld4(const char* p) {
+  uint32_t v;
+  memcpy(&v, p, 4);
+  return v;
+}
+inline void key_words(const char* p, size_t n, uint64_t& a, uint64_t& b) {
+  if (n >= 8) {
+    a = ld8(p), b = ld8(p + n - 8);
+  } else if (n >= 4) {
+    a = ld4(p), b = ld4(p + n - 4);
+  } else {
+    a = n ? (uint64_t)(unsigned char)p[0] | (uint64_t)(unsigned char)p[n / 2] << 8 |
+                (uint64_t)(unsigned char)p[n - 1] << 16
+          : 0;
+    b = 0;
+  }
+}
+// k is an exact, compact ASCII str whose text is sk's
+inline bool key_is(const ShapeKey& sk, PyObject* k) {
+  if (Py_TYPE(k) != &PyUnicode_Type) return false;
+  const PyASCIIObject* o = (const PyASCIIObject*)k;
+  if (!o->state.compact || !o->state.ascii || (uint32_t)o->length != sk.len) return false;
+  const char* p = (const char*)(o + 1);
+  if (sk.len > 16) return memcmp(p, sk.txt, sk.len) == 0;
+  uint64_t a, b;
+  key_words(p, sk.len, a, b);
+  return a == sk.a && b == sk.b;
+}
+struct Shape {
+  int ne = -1;  // entries; -1: empty
+  ShapeKey key[kShapeKeys];
+  uint8_t emit[kShapeKeys];  // entry index of each emitted key, in emit order
+  uint8_t pre_len[kShapeKeys];
+  uint16_t pre_at[kShapeKeys];
+  int nemit = 0;
+  int8_t sig_at = -1, idr_at = -1;  // level 0: the entries holding the signature / identifier
+  char text[kShapeKeys * (kShapeKeyLen + 2)];
+  char pre[kShapeKeys * (kShapeKeyLen + 2)];
+};
+struct ShapeCache {
+  Shape s[2][8];  // [level 0 / deeper][entries % 8]
+  Shape& at(int level, Py_ssize_t ne) { return s[level ? 1 : 0][ne & 7]; }
+};
+
+WRes shaped_dict(PyObject* d, int level, PyObject* ignore, OutBuf& out, PyObject* const* top, PyObject** found,
+                 ShapeCache& sc);
+
+inline WRes shaped_val(PyObject* v, int level, OutBuf& out, ShapeCache& sc) {
+  PyTypeObject* t = Py_TYPE(v);
+  if (t == &PyUnicode_Type) {
+    const PyASCIIObject* o = (const PyASCIIObject*)v;
+    if (o->state.compact && o->state.ascii) {
+      out.append((const char*)(o + 1), (size_t)o->length);
+      return kOk;
+    }
+    return w_append_str(v, out);
+  }
+  if (t == &PyDict_Type) return shaped_dict(v, level, nullptr, out, nullptr, nullptr, sc);
+  return wser_obj(v, level, nullptr, out);
+}
+
+// remember d's shape (after wser_dict serialized it with kOk): every key an exact compact ASCII
+// str of at most kShapeKeyLen bytes, at most kShapeKeys entries, none deleted
+void shape_learn(Shape& sh, const DkEntry* ent, Py_ssize_t ne, int level, PyObject* ignore, PyObject* const* top) {
+  sh.ne = -1;
+  if (ne > kShapeKeys) return;
+  size_t tat = 0;
+  int keep[kShapeKeys];
+  int nk = 0;
+  sh.sig_at = sh.idr_at = -1;
+  for (Py_ssize_t j = 0; j < ne; ++j) {
+    PyObject* k = ent[j].k;
+    if (!ent[j].v || Py_TYPE(k) != &PyUnicode_Type) return;
+    const PyASCIIObject* o = (const PyASCIIObject*)k;
+    if (!o->state.compact || !o->state.ascii || (size_t)o->length > kShapeKeyLen) return;
+    ShapeKey& sk = sh.key[j];
+    sk.len = (uint32_t)o->length;
+    memcpy(sh.text + tat, (const char*)(o + 1), sk.len);
+    sk.txt = sh.text + tat;
+    tat += sk.len;
+    key_words(sk.txt, sk.len, sk.a, sk.b);
+    if (top) {
+      if (k == top[0] || w_str_eq(k, top[0]))
+        sh.sig_at = (int8_t)j;
+      else if (k == top[1] || w_str_eq(k, top[1]))
+        sh.idr_at = (int8_t)j;
+    }
+    if (level == 0 && w_ignored(k, ignore)) continue;
+    keep[nk++] = (int)j;
+  }
+  for (int i = 1; i < nk; ++i) {  // wser_dict's order
+    const int x = keep[i];
+    int j = i;
+    while (j > 0 && w_less(ent[x].k, ent[keep[j - 1]].k)) {
+      keep[j] = keep[j - 1];
+      --j;
+    }
+    keep[j] = x;
+  }
+  size_t pat = 0;
+  for (int i = 0; i < nk; ++i) {
+    const ShapeKey& sk = sh.key[keep[i]];
+    sh.emit[i] = (uint8_t)keep[i];
+    sh.pre_at[i] = (uint16_t)pat;
+    if (i) sh.pre[pat++] = '|';
+    memcpy(sh.pre + pat, sk.txt, sk.len);
+    pat += sk.len;
+    sh.pre[pat++] = ':';
+    sh.pre_len[i] = (uint8_t)(pat - sh.pre_at[i]);
+  }
+  sh.nemit = nk;
+  sh.ne = (int)ne;
+}
+
+WRes shaped_dict(PyObject* d, int level, PyObject* ignore, OutBuf& out, PyObject* const* top, PyObject** found,
+                 ShapeCache& sc) {
+  if (level > kMaxDepth) return kFail;
+  Py_ssize_t ne = 0;
+  const DkEntry* ent = dk_entries(d, ne);
+  if (!ent || ne != ((PyDictObject*)d)->ma_used) return wser_dict(d, level, ignore, out, top, found);
+  Shape& sh = sc.at(level, ne);
+  bool hit = sh.ne == ne;
+  for (Py_ssize_t j = 0; hit && j < ne; ++j) hit = key_is(sh.key[j], ent[j].k);
+  if (!hit) {
+    const WRes r = wser_dict(d, level, ignore, out, top, found);
+    if (r == kOk) shape_learn(sh, ent, ne, level, ignore, top);
+    return r;
+  }
+  if (top) {
+    found[0] = sh.sig_at >= 0 ? ent[sh.sig_at].v : nullptr;
+    found[1] = sh.idr_at >= 0 ? ent[sh.idr_at].v : nullptr;
+  }
+  for (int i = 0; i < sh.nemit; ++i) {
+    out.append(sh.pre + sh.pre_at[i], sh.pre_len[i]);
+    const WRes r = shaped_val(ent[sh.emit[i]].v, level + 1, out, sc);
+    if (r != kOk) return r;
+  }
+  return kOk;
+}
+#endif
 
 // ------------------------------------------------------------------- base58
 
@@ -1220,9 +1419,20 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
     std::vector<PyObject*> obj;
     std::vector<Py_ssize_t> first;  // the item where the worker met it first
     size_t deferred = 0;            // items left for the GIL pass (3)
+#ifdef EDV_HAVE_DK
+    std::unique_ptr<ShapeCache> shapes;  // this call's remembered dict shapes (shaped_dict)
+#endif
   };
   std::vector<WorkerIdrs> tabs((size_t)t);
-  for (WorkerIdrs& w : tabs) w.slot.reset(1024);
+  // remembered dict shapes (shaped_dict); EDV_SCAN_SHAPES=0: wser_dict for every request (A/B)
+  const char* shape_env = getenv("EDV_SCAN_SHAPES");
+  const bool shapes = g_scan_direct_env() && !(shape_env && shape_env[0] == '0');
+  for (WorkerIdrs& w : tabs) {
+    w.slot.reset(1024);
+#ifdef EDV_HAVE_DK
+    if (shapes) w.shapes.reset(new ShapeCache);
+#endif
+  }
   // the signature output (n slots) is sized before the scan: in slot mode the workers write an
   // item's base58 text slot while its text is still in cache (phase 5 writes the rest)
   char* dsig = nullptr;
@@ -1364,7 +1574,12 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
       // the fast path) and the signature and identifier values
       PyObject* found[2] = {nullptr, nullptr};
       const size_t at = sb.ser.size();
+#ifdef EDV_HAVE_DK
+      const WRes r = shapes ? shaped_dict(m, 0, ign, sb.ser, top_keys, found, *tab.shapes)
+                            : wser_dict(m, 0, ign, sb.ser, top_keys, found);
+#else
       const WRes r = wser_dict(m, 0, ign, sb.ser, top_keys, found);
+#endif
       PyObject *sv = found[0], *iv = found[1];
       if (!(sv && iv && PyUnicode_CheckExact(sv) && PyUnicode_GET_LENGTH(sv) > 0 && PyUnicode_CheckExact(iv) &&
             PyUnicode_GET_LENGTH(iv) > 0 && PyUnicode_IS_ASCII(sv))) {

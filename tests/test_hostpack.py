@@ -292,3 +292,81 @@ def test_results_ok_parallel_matches_serial_and_refcounts():
     assert [sys.getrefcount(u) for u in uniq] == before
     with pytest.raises(ValueError):
         _hostpack.results_ok(b"\x01", b"\x00", np.array([9], np.uint32).tobytes(), uniq)
+
+
+def _shape_pool(r, n):
+    """Request dicts that mostly share one shape (the scan workers' remembered
+    dict shapes) with near misses: keys in another insertion order, a key of
+    the same length with other text, an extra or a missing key, a deleted
+    entry (a dict with a hole in its entry table), nested dicts of the same
+    shape holding other value types, non-ASCII and wider-kind text, long keys,
+    ints at the digit boundaries, str subclasses, floats."""
+    class S(str):
+        pass
+    msgs = []
+    for i in range(n):
+        op = {"type": "1", "dest": "Dest%05d" % (i % 97), "verkey": "~Vk%05d" % (i % 13), "alias": "a" * (i % 40)}
+        m = {"identifier": "idr%d" % (i % 9), "reqId": 1500000000000000 + i, "operation": op,
+             "protocolVersion": 1, "signature": b58encode(bytes(r.getrandbits(8) for _ in range(64)))}
+        k = r.randrange(40)
+        if k == 0:
+            m = dict(reversed(list(m.items())))
+        elif k == 1:
+            op["typf"] = op.pop("type")           # same length, other text
+        elif k == 2:
+            op["extra"] = [1, "x", None]
+        elif k == 3:
+            del op["alias"]
+        elif k == 4:
+            m["zz"] = 1
+            del m["zz"]                            # a deleted entry in the table
+        elif k == 5:
+            op["dest"] = {"type": 2, "dest": "x", "verkey": 3.5, "alias": True}   # same shape nested
+        elif k == 6:
+            op["alias"] = "é" * 3                   # non-ASCII value: deferred to the GIL
+        elif k == 7:
+            op["ключ"] = "v"                        # wider-kind key
+        elif k == 8:
+            op["k" * 50] = "long key"
+        elif k == 9:
+            m["reqId"] = r.choice(_EDGE_INTS)
+        elif k == 10:
+            op["dest"] = S("subclass")
+        elif k == 11:
+            m[S("identifier2")] = "x"
+        elif k == 12:
+            op["alias"] = 0.1
+        elif k == 13:
+            m["operation"] = {"type": "1", "dest": "D", "verkey": "V", "alias": "x", "a": 1, "b": 2, "c": 3,
+                              "d": 4, "e": 5, "f": 6, "g": 7, "h": 8, "i": 9}   # more keys than a shape holds
+        elif k == 14:
+            del m["signature"]
+        elif k == 15:
+            m["signature"] = 5
+        elif k == 16:
+            op["dest"] = [{"type": "1"}, {"type": 1}]
+        msgs.append(m)
+    return msgs
+
+
+@pytest.mark.parametrize("threads", [1, 4])
+def test_scan_shapes_equal_generic_and_python(monkeypatch, threads):
+    """shaped_dict (remembered dict shapes) gives byte for byte what wser_dict
+    gives (EDV_SCAN_SHAPES=0), and both the Python restatement's bytes."""
+    r = random.Random(5)
+    msgs = _shape_pool(r, 4000)
+    monkeypatch.setenv("EDV_SCAN_SHAPES", "1")
+    on = H.scan_batch_u(msgs, ["signature"], threads)
+    monkeypatch.setenv("EDV_SCAN_SHAPES", "0")
+    off = H.scan_batch_u(msgs, ["signature"], threads)
+    assert on == off
+    fast, uidx, uniq, sig64, mbuf, off_b, short = on
+    offs = struct.unpack("<%dQ" % (len(msgs) + 1), off_b)
+    nfast = 0
+    for i, m in enumerate(msgs):
+        if not fast[i]:
+            continue
+        nfast += 1
+        sm = b58decode_py(m["signature"]) + py_ser(m, ["signature"])
+        assert sig64[64 * i:64 * i + 64] == sm[:64] and mbuf[offs[i]:offs[i + 1]] == sm[64:], (i, m)
+    assert nfast > 3000

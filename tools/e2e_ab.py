@@ -2,6 +2,8 @@
 1M-request batches, each request json-decoded on its own, modes alternating):
   stream  the default (scan with the pack deferred, 2^17-request submits)
   stage   stage=True (the scan's workers queue each 4k chunk's DMA while scanning)
+  MODE:VAR=VAL   that mode with the environment variable set around each of its calls
+                 (e.g. stage:EDV_SCAN_SHAPES=0)
 usage: python tools/e2e_ab.py [n] [reps] [mode,mode,...]"""
 import os
 import sys
@@ -20,8 +22,25 @@ modes = (sys.argv[3] if len(sys.argv) > 3 else "stream,stage").split(",")
 eng = EdVerifyEngine(0)
 reqs, idrs, vks = bench.e2e_requests(eng, n, 1000, 43)
 auths = {}
+def env_of(m):
+    return dict(kv.split("=", 1) for kv in m.split(":")[1:])
+
+
+def with_env(m, f):
+    saved = {k: os.environ.get(k) for k in env_of(m)}
+    os.environ.update(env_of(m))
+    try:
+        return f()
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
 for m in modes:
-    a = GpuAuthNr(engine=eng, stage=(m == "stage"))
+    a = GpuAuthNr(engine=eng, stage=(m.split(":")[0] == "stage"))
     for idr, vk in zip(idrs, vks):
         a.addIdr(idr, vk)
     a.keys_settle()
@@ -33,10 +52,10 @@ for rep in range(reps):
         a = auths[m]
         a._g.last_breakdown = None
         t0 = time.perf_counter()
-        res = a.authenticate_batch(reqs)
+        res = with_env(m, lambda: a.authenticate_batch(reqs))
         el = time.perf_counter() - t0
         ok = sum(1 for r, q in zip(res, reqs) if r == q["identifier"])
         del res
-        print("%-6s %.2f ms = %.2f M requests/s  accepted %d  %s" % (
+        print("%-24s %.2f ms = %.2f M requests/s  accepted %d  %s" % (
             m, el * 1e3, n / el / 1e6, ok, {k: round(v, 2) for k, v in (a._g.last_breakdown or {}).items()}),
             flush=True)
