@@ -1058,6 +1058,20 @@ def main():
         if args.bls_checks > 0:
             e2e["bls_commit_round"] = time_bls_commit_round(eng, args.bls_checks)
 
+    # the metric's "whole node" reading: GpuAuthNr.authenticate_batch over json-decoded request dicts
+    # (host scan + PCIe + kernels + result list, one node process), beside the same run's libsodium
+    whole, whole_vs = None, None
+    c1 = (e2e or {}).get("configs1")
+    if c1:
+        whole = {"synchronous": c1["value"], "pipelined": c1["pipelined"]["value"], "unit": "requests/s",
+                 "requests_per_batch": c1["requests"], "in_batch_ms": c1.get("in_batch_ms"),
+                 "note": "end_to_end.configs1: authenticate_batch over 1M json-decoded configs[1] requests in one node "
+                         "process (synchronous: one batch at a time; pipelined: authenticate_batches, two in "
+                         "flight); every verdict checked after the clock"}
+        if cpu:
+            whole_vs = {"synchronous": c1["value"] / cpu["value"], "pipelined": c1["pipelined"]["value"] / cpu["value"],
+                        "cpu": "cpu_baseline.value: libsodium 1.0.18 crypto_sign_verify_detached on %d host threads"
+                               % cpu["cores"]}
     if rank == 0:
         out = {
             "metric": METRIC, "value": value, "unit": "verifies/s", "n_gpus": world, "steps": args.steps,
@@ -1106,6 +1120,8 @@ def main():
             "ref10_equivalent_frac": (n * RL.MAD_PER_VERIFY / (ms_per_step * 1e-3)) / RL.PEAK_MAD_PER_S,
             "other_path": other,
             "dropin_window": dropin,
+            "whole_node": whole,
+            "whole_node_vs_cpu": whole_vs,
             "end_to_end": e2e,
             "cpu_baseline": cpu,
             "parity": {"mismatches_vs_construction": mismatches, "accepted": accepted, "expected": expected,

@@ -22,7 +22,12 @@ def main(path):
     print("phases", {k: r(v, 3) for k, v in ph.items() if k != "note"})
     cpu = d.get("cpu_baseline")
     if cpu:
-        print("cpu %.1f k/s on %s cores (%s)" % (cpu["value"] / 1e3, cpu["cores"], cpu["kind"]))
+        print("cpu %.1f k/s on %s cores (%s)  all items vs libsodium: %s" % (
+            cpu["value"] / 1e3, cpu["cores"], cpu["kind"], (cpu.get("all_items_check") or {}).get("mismatches")))
+    w, wv = d.get("whole_node"), d.get("whole_node_vs_cpu") or {}
+    if w:
+        print("whole node: sync %.2f M/s (%sx cpu), pipelined %.2f M/s (%sx cpu)" % (
+            w["synchronous"] / 1e6, r(wv.get("synchronous")), w["pipelined"] / 1e6, r(wv.get("pipelined"))))
     for k, v in (d.get("end_to_end") or {}).items():
         if k == "by_devices":
             print(" ", k, {kk: r(vv["value"] / 1e6, 2) for kk, vv in v.items() if isinstance(vv, dict)})
@@ -31,7 +36,8 @@ def main(path):
                            if not isinstance(vv, (dict, list, str))})
         else:
             s = v.get("single_authenticate_us") or {}
-            print(" ", k, r(v["value"] / 1e6, 2), "M/s  single p50", r(s.get("p50")),
+            print(" ", k, r(v["value"] / 1e6, 2), "M/s  pipelined", r((v.get("pipelined") or {}).get("value", 0) / 1e6, 2),
+                  "single p50", r(s.get("p50")),
                   {kk: r(vv, 2) for kk, vv in (v.get("in_batch_ms") or {}).items()})
 
 
