@@ -247,6 +247,24 @@ int edv_stage_select(edv_ctx *ctx, int set);
 int edv_verify_staged_submit(edv_ctx *ctx, int keyed, const uint8_t *keys, uint64_t slot_off, uint64_t msg_base,
                              const uint64_t *msg_start, const uint64_t *msg_end, uint64_t n, uint64_t *ticket);
 int edv_verify_staged_collect(edv_ctx *ctx, uint64_t ticket, uint8_t *accept_bits);
+/* A staged batch verified in parts while it is still being produced (the authenticator's
+ * synchronous batch: its kernels run under its own scan, with key ids the scan takes from the
+ * previous batches' identifiers and the authenticator checks after it).
+ *   edv_verify_staged_begin(ctx, keyed, n, ticket): the current set for an n-item batch (its
+ *     buffers sized here), held until edv_verify_staged_collect(ctx, ticket, bits).
+ *   edv_verify_staged_part(ctx, keys, slot_off, msg_base, spans, n, lo, hi): items [lo, hi)
+ *     (lo a multiple of 64) -- keys (n uint32 ids, or n x 32-byte keys) and spans (starts[n]
+ *     then ends[n]) in edv_host_alloc memory, written for those items; their slots and
+ *     messages put -- are copied and verified (edv_verify_staged's kernels) after every put
+ *     queued before the call.  Any thread, one call at a time.
+ *   edv_verify_staged_end(ctx): the verdicts' copy after the last part; a failed part is
+ *     reported here (the set still needs its collect).
+ * Items no part covered are rejected.  Replaces, like edv_verify_staged, libsodium's
+ * crypto_sign_open per request (nacl_wrappers.py:108). */
+int edv_verify_staged_begin(edv_ctx *ctx, int keyed, uint64_t n, uint64_t *ticket);
+int edv_verify_staged_part(edv_ctx *ctx, const void *keys, uint64_t slot_off, uint64_t msg_base,
+                           const uint64_t *spans, uint64_t n, uint64_t lo, uint64_t hi);
+int edv_verify_staged_end(edv_ctx *ctx);
 
 /* Signature slots: the host-pointer verifies below take, instead of sig64,
  * n slots of EDV_SIG_SLOT96 bytes, so that the base58 decode of the request

@@ -1472,6 +1472,12 @@ struct edv_ctx {
   Buf sh_key[kSets], sh_off[kSets], sh_bits[kSets];  // pinned: staging of non-pinned inputs, verdicts
   hipEvent_t ev_sh2d[kSets] = {}, ev_sdone[kSets] = {};
   uint64_t set_ticket[kSets] = {}, set_n[kSets] = {};  // the uncollected submission holding each set
+  // parts of a staged batch launched while it is still being scanned (edv_verify_staged_begin /
+  // _part / _end): the set the batch holds, its keying, the first part error, parts launched
+  int part_set = -1;
+  bool part_keyed = true;
+  int part_err = 0;
+  uint64_t part_launched = 0;
   Buf& d_stage() { return d_stage_set[cur_set]; }
 };
 
@@ -2587,6 +2593,103 @@ int edv_verify_staged_submit(edv_ctx* ctx, int keyed, const uint8_t* keys, uint6
   ctx->set_ticket[set] = tk;
   ctx->set_n[set] = n;
   *ticket = tk;
+  return 0;
+}
+
+int edv_verify_staged_begin(edv_ctx* ctx, int keyed, uint64_t n, uint64_t* ticket) {
+  int r = set_device(ctx);
+  if (r) return r;
+  if (!ticket) return set_err(EDV_EINVAL, "null pointer");
+  const int set = ctx->cur_set;
+  {
+    std::lock_guard<std::mutex> lk(ctx->stage_mu);
+    if (ctx->set_ticket[set]) return set_err(EDV_EINVAL, "staging set %d holds an uncollected submission", set);
+    if (ctx->part_set >= 0) return set_err(EDV_EINVAL, "a batch of parts is open (set %d)", ctx->part_set);
+  }
+  if (keyed && n && ctx->key_count == 0) return set_err(EDV_EINVAL, "no registered keys");
+  const uint64_t key_bytes = keyed ? 4 : 32, nwords = div_up(n, 64);
+  // every buffer the parts use, sized here on the caller's thread (the parts only launch)
+  if ((r = ensure_pinned(ctx->sh_bits[set], 8 * nwords + 8)) || (r = ensure(ctx->s_key[set], key_bytes * n)) ||
+      (r = ensure(ctx->d_spans[set], 16 * n)) || (r = ensure(ctx->s_sig[set], 64 * n)) ||
+      (r = ensure(ctx->s_bits[set], 8 * nwords)))
+    return r;
+  if (n) HIP_TRY(hipMemsetAsync(ctx->s_bits[set].p, 0, 8 * nwords, ctx->stream));
+  set_bucketing(ctx, false);
+  std::lock_guard<std::mutex> lk(ctx->stage_mu);
+  const uint64_t tk = ctx->next_ticket++;
+  ctx->set_ticket[set] = tk;
+  ctx->set_n[set] = n;
+  ctx->part_set = set;
+  ctx->part_keyed = keyed != 0;
+  ctx->part_err = 0;
+  ctx->part_launched = 0;
+  *ticket = tk;
+  return 0;
+}
+
+int edv_verify_staged_part(edv_ctx* ctx, const void* keys, uint64_t slot_off, uint64_t msg_base,
+                           const uint64_t* spans, uint64_t n, uint64_t lo, uint64_t hi) {
+  if (!ctx) return set_err(EDV_EINVAL, "null context");
+  std::lock_guard<std::mutex> lk(ctx->stage_mu);  // one part at a time, ordered with the puts
+  const int set = ctx->part_set;
+  int r = 0;
+  auto fail = [&](int code) {
+    if (!ctx->part_err) ctx->part_err = code;
+    return code;
+  };
+  if (set < 0) return fail(set_err(EDV_EINVAL, "no batch of parts is open"));
+  if (ctx->part_err) return ctx->part_err;
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(set_err(EDV_EHIP, "hipSetDevice"));
+  if (n != ctx->set_n[set] || lo > hi || hi > n || (lo & 63) || !keys || !spans)
+    return fail(set_err(EDV_EINVAL, "part [%llu, %llu) of %llu", (unsigned long long)lo, (unsigned long long)hi,
+                        (unsigned long long)n));
+  if (lo == hi) return 0;
+  const uint64_t cap = ctx->d_stage_set[set].cap, m = hi - lo;
+  if (ctx->stage_err) return fail(ctx->stage_err);
+  if (slot_off > cap || hi > (cap - slot_off) / EDV_SIG_SLOT96) return fail(set_err(EDV_EINVAL, "slots outside staging"));
+  const uint64_t *ms_h = spans + lo, *me_h = spans + n + lo;
+  uint64_t bad = 0;  // the kernels read msg_base + [start, end): inside the staging buffer
+  for (uint64_t i = 0; i < m; ++i) bad |= (uint64_t)(ms_h[i] > me_h[i]) | (uint64_t)(me_h[i] > cap - msg_base);
+  if (bad) return fail(set_err(EDV_EINVAL, "a message span outside staging"));
+  const bool keyed = ctx->part_keyed;
+  const uint64_t key_bytes = keyed ? 4 : 32;
+  if (!pinned_range((const uint8_t*)keys + key_bytes * lo, key_bytes * m) || !pinned_range(ms_h, 8 * m) ||
+      !pinned_range(me_h, 8 * m))
+    return fail(set_err(EDV_EINVAL, "part inputs are not edv_host_alloc memory"));
+  hipStream_t cs = ctx->stream_copy, st = ctx->stream;
+  uint64_t* d_ms = (uint64_t*)ctx->d_spans[set].p;
+  uint8_t* d_key = (uint8_t*)ctx->s_key[set].p + key_bytes * lo;
+  if (hipMemcpyAsync(d_key, (const uint8_t*)keys + key_bytes * lo, key_bytes * m, hipMemcpyHostToDevice, cs) ||
+      hipMemcpyAsync(d_ms + lo, ms_h, 8 * m, hipMemcpyHostToDevice, cs) ||
+      hipMemcpyAsync(d_ms + n + lo, me_h, 8 * m, hipMemcpyHostToDevice, cs) ||
+      hipEventRecord(ctx->ev_sh2d[set], cs) ||  // after every put queued before this part
+      hipStreamWaitEvent(st, ctx->ev_sh2d[set], 0))
+    return fail(set_err(EDV_EHIP, "part copies"));
+  const uint8_t* stage = (const uint8_t*)ctx->d_stage_set[set].p;
+  uint8_t* sig = (uint8_t*)ctx->s_sig[set].p + 64 * lo;
+  hipLaunchKernelGGL(edv_b58_sig_kernel, dim3((uint32_t)div_up(m, kBlock)), dim3(kBlock), 0, st,
+                     stage + slot_off + EDV_SIG_SLOT96 * lo, m, sig);
+  if (hipGetLastError() != hipSuccess) return fail(set_err(EDV_EHIP, "part b58 launch"));
+  r = launch_pipeline(ctx, keyed, sig, d_key, stage + msg_base, d_ms + lo, d_ms + n + lo, m,
+                      (unsigned long long*)ctx->s_bits[set].p + lo / 64, st);
+  if (r) return fail(r);
+  ++ctx->part_launched;
+  return 0;
+}
+
+int edv_verify_staged_end(edv_ctx* ctx) {
+  int r = set_device(ctx);
+  if (r) return r;
+  std::lock_guard<std::mutex> lk(ctx->stage_mu);
+  const int set = ctx->part_set;
+  if (set < 0) return set_err(EDV_EINVAL, "no batch of parts is open");
+  ctx->part_set = -1;
+  const uint64_t nwords = div_up(ctx->set_n[set], 64);
+  if (nwords) {
+    HIP_TRY(hipMemcpyAsync(ctx->sh_bits[set].p, ctx->s_bits[set].p, 8 * nwords, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipEventRecord(ctx->ev_sdone[set], ctx->stream));
+  }
+  if (ctx->part_err) return set_err(ctx->part_err, "a part of this batch failed");
   return 0;
 }
 

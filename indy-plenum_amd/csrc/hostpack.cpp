@@ -1040,6 +1040,104 @@ struct IdrTable {
   }
 };
 
+// Identifier text -> key-store id, from the batches before (the authenticator's speculation
+// for a staged batch: the scan writes each request's key id while it scans, so the batch's
+// kernels can run under the scan; the authenticator checks every id against getVerkey and
+// the key store afterwards).  Owns copies of the texts.
+struct KidMap {
+  struct E {
+    uint64_t h = 0;
+    uint32_t off = 0, len = 0, kid = 0;
+    bool used = false;
+  };
+  std::vector<E> e;
+  std::string text;
+  size_t used = 0;
+  KidMap() { e.resize(1024); }
+  uint32_t get(const char* p, size_t n) const {
+    const size_t mask = e.size() - 1;
+    const uint64_t h = IdrTable::hash(p, n);
+    for (size_t s = h & mask;; s = (s + 1) & mask) {
+      const E& x = e[s];
+      if (!x.used) return 0xffffffffu;
+      if (x.h == h && x.len == n && memcmp(text.data() + x.off, p, n) == 0) return x.kid;
+    }
+  }
+  void put(const char* p, size_t n, uint32_t kid) {
+    if (2 * (used + 1) > e.size()) {
+      std::vector<E> old;
+      old.swap(e);
+      e.resize(old.size() * 2);
+      for (const E& x : old)
+        if (x.used)
+          for (size_t s = x.h & (e.size() - 1);; s = (s + 1) & (e.size() - 1))
+            if (!e[s].used) {
+              e[s] = x;
+              break;
+            }
+    }
+    const size_t mask = e.size() - 1;
+    const uint64_t h = IdrTable::hash(p, n);
+    for (size_t s = h & mask;; s = (s + 1) & mask) {
+      E& x = e[s];
+      if (!x.used) {
+        x.h = h, x.off = (uint32_t)text.size(), x.len = (uint32_t)n, x.kid = kid, x.used = true;
+        text.append(p, n);
+        ++used;
+        return;
+      }
+      if (x.h == h && x.len == n && memcmp(text.data() + x.off, p, n) == 0) {
+        x.kid = kid;  // (an id that is no longer right: ~0u, so the scan writes "unknown")
+        return;
+      }
+    }
+  }
+};
+void kid_map_free(PyObject* cap) { delete (KidMap*)PyCapsule_GetPointer(cap, "edv.kidmap"); }
+
+// kid_map(old, identifiers, ids) -> map: old (a kid_map or None) with identifiers[j] -> ids[j]
+// (uint32 bytes; 0xffffffff = no id) put; a new map when old is None.  ASCII identifiers only
+// (others are skipped: the scan defers their requests anyway).
+PyObject* py_kid_map(PyObject*, PyObject* args) {
+  PyObject *old, *idrs;
+  Py_buffer bk;
+  if (!PyArg_ParseTuple(args, "OOy*", &old, &idrs, &bk)) return nullptr;
+  struct Rel {
+    Py_buffer* b;
+    ~Rel() { PyBuffer_Release(b); }
+  } rel{&bk};
+  if (!PyList_CheckExact(idrs) || bk.len != PyList_GET_SIZE(idrs) * 4) {
+    PyErr_SetString(PyExc_ValueError, "kid_map: a list of identifiers and as many uint32 ids");
+    return nullptr;
+  }
+  KidMap* m = nullptr;
+  PyObject* ret = nullptr;
+  if (old == Py_None) {
+    m = new KidMap;
+    ret = PyCapsule_New(m, "edv.kidmap", kid_map_free);
+    if (!ret) {
+      delete m;
+      return nullptr;
+    }
+  } else {
+    m = (KidMap*)PyCapsule_GetPointer(old, "edv.kidmap");
+    if (!m) return nullptr;
+    Py_INCREF(old);
+    ret = old;
+  }
+  const uint32_t* k = (const uint32_t*)bk.buf;
+  for (Py_ssize_t j = 0; j < PyList_GET_SIZE(idrs); ++j) {
+    PyObject* o = PyList_GET_ITEM(idrs, j);
+    if (PyUnicode_CheckExact(o) && PyUnicode_IS_ASCII(o))
+      m->put((const char*)PyUnicode_1BYTE_DATA(o), (size_t)PyUnicode_GET_LENGTH(o), k[j]);
+  }
+  return ret;
+}
+PyObject* py_kid_map_size(PyObject*, PyObject* cap) {
+  KidMap* m = (KidMap*)PyCapsule_GetPointer(cap, "edv.kidmap");
+  return m ? PyLong_FromSize_t(m->used) : nullptr;
+}
+
 struct ScanItem {
   PyObject* m = nullptr;
   const unsigned char* sp = nullptr;
@@ -1182,6 +1280,8 @@ struct ScanScratch {
 
 // Staged mode (defer = 2): edverify.h edv_stage_put, called by the workers.
 using StageFn = int (*)(void*, const void*, uint64_t, uint64_t);
+// edverify.h edv_verify_staged_part, called by the staged scan's copier thread
+using PartFn = int (*)(void*, const void*, uint64_t, uint64_t, const uint64_t*, uint64_t, uint64_t, uint64_t);
 constexpr Py_ssize_t kStageChunk = 4096;  // items per staged chunk: ~0.8 MB of messages, 0.4 MB of slots
 
 // The copies of a staged scan, issued by one thread of their own so no worker ever waits on the
@@ -1204,9 +1304,47 @@ struct StageCopier {
   std::thread th;
   uint64_t msg_sent = 0, msg_ready = 0;
   size_t next_res = 0, next_chunk = 0, slot_sent_chunk = 0;
+  // parts (edv_verify_staged_part): every part_items items, once their chunks are written and
+  // copied, their key ids and spans copied and their kernels queued -- while the scan goes on
+  PartFn part_fn = nullptr;
+  void* part_ctx = nullptr;
+  const void* part_keys = nullptr;
+  const uint64_t* part_spans = nullptr;
+  uint64_t n_items = 0, part_items = 0, next_part = 0;
+  std::atomic<bool> part_failed{false};
+  std::unique_ptr<std::atomic<uint32_t>[]> chunk_seq;  // by chunk index: its message reservation number
 
   void put(const char* src, uint64_t nbytes, uint64_t off) {
     if (nbytes && fn(ctx, src, nbytes, off) != 0) failed = true;
+  }
+  void send_ready() {  // every ready message byte and slot, whatever the grain
+    if (msg_ready > msg_sent) {
+      put(smsg + msg_sent, msg_ready - msg_sent, msg_sent);
+      msg_sent = msg_ready;
+    }
+    const uint64_t s0 = slot_sent_chunk * slot_bytes_per_chunk;
+    const uint64_t s1 = std::min<uint64_t>(next_chunk * slot_bytes_per_chunk, slot_bytes_total);
+    if (s1 > s0) {
+      put(dsig + s0, s1 - s0, slot_base + s0);
+      slot_sent_chunk = next_chunk;
+    }
+  }
+  // the parts whose chunks are all written (slot_done) and whose messages are in the ready prefix
+  void launch_parts() {
+    if (!part_fn || part_failed) return;
+    while (next_part * part_items < n_items) {
+      const uint64_t lo = next_part * part_items, hi = std::min(n_items, lo + part_items);
+      const size_t c0 = (size_t)(lo / kStageChunk), c1 = (size_t)((hi + kStageChunk - 1) / kStageChunk);
+      if (c1 > next_chunk) return;  // (next_chunk: the contiguous prefix of written chunks)
+      for (size_t c = c0; c < c1; ++c)
+        if (chunk_seq[c].load(std::memory_order_acquire) >= next_res) return;
+      send_ready();
+      if (part_fn(part_ctx, part_keys, slot_base, 0, part_spans, n_items, lo, hi) != 0) {
+        part_failed = true;
+        return;
+      }
+      ++next_part;
+    }
   }
   // one pass over what became ready; `flush` sends every ready byte
   void pump(bool flush) {
@@ -1227,6 +1365,7 @@ struct StageCopier {
       put(dsig + s0, s1 - s0, slot_base + s0);
       slot_sent_chunk = next_chunk;
     }
+    launch_parts();
   }
   void start() {
     th = std::thread([this] {
@@ -1335,11 +1474,11 @@ struct PyRefs {
 };
 
 PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
-  PyObject *msgs, *ignore = Py_None, *out = Py_None, *stager = Py_None;
+  PyObject *msgs, *ignore = Py_None, *out = Py_None, *stager = Py_None, *spec = Py_None;
   int want_threads = 0, sig_slot = 64, defer = 0;
   unsigned long long slot_base = 0;
-  if (!PyArg_ParseTuple(args, "O|OiOiiOK", &msgs, &ignore, &want_threads, &out, &sig_slot, &defer, &stager,
-                        &slot_base))
+  if (!PyArg_ParseTuple(args, "O|OiOiiOKO", &msgs, &ignore, &want_threads, &out, &sig_slot, &defer, &stager,
+                        &slot_base, &spec))
     return nullptr;
   if (defer && !unique_form) {
     PyErr_SetString(PyExc_ValueError, "defer needs scan_batch_u");
@@ -1368,6 +1507,39 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
     return nullptr;
   }
   const bool slots = sig_slot == kSigSlot;
+  // staged mode with speculation: spec = (kid_map, key-id buffer (4 n bytes, the engine's pinned
+  // memory), (edv_verify_staged_part address, context address), items per part): each request's
+  // key id from the map by its identifier (0xffffffff: not in it) written while scanning, and each
+  // part's kernels queued by the copier as soon as the part is staged
+  const KidMap* kmap = nullptr;
+  uint32_t* kid_out = nullptr;
+  PartFn part_fn = nullptr;
+  void* part_ctx = nullptr;
+  unsigned long long part_items = 0;
+  if (spec != Py_None) {
+    PyObject *cap, *kbuf, *pf;
+    unsigned long long fa = 0, ca = 0;
+    if (!staged || !PyTuple_Check(spec) || !PyArg_ParseTuple(spec, "OOOK", &cap, &kbuf, &pf, &part_items) ||
+        !PyTuple_Check(pf) || !PyArg_ParseTuple(pf, "KK", &fa, &ca) || !fa || !ca || !part_items ||
+        part_items % kStageChunk) {
+      if (!PyErr_Occurred())
+        PyErr_SetString(PyExc_ValueError, "spec = (kid_map, pinned key ids, (part fn, ctx), items per part: k * 4096)");
+      return nullptr;
+    }
+    kmap = (const KidMap*)PyCapsule_GetPointer(cap, "edv.kidmap");
+    if (!kmap) return nullptr;
+    Py_buffer view;
+    if (PyObject_GetBuffer(kbuf, &view, PyBUF_WRITABLE | PyBUF_C_CONTIGUOUS) != 0) return nullptr;
+    const bool fits = (uint64_t)view.len >= 4 * (uint64_t)PySequence_Size(msgs);
+    kid_out = (uint32_t*)view.buf;
+    PyBuffer_Release(&view);  // the caller keeps the owner alive
+    if (!fits) {
+      PyErr_SetString(PyExc_ValueError, "spec: the key-id buffer holds fewer than 4 n bytes");
+      return nullptr;
+    }
+    part_fn = (PartFn)(uintptr_t)fa;
+    part_ctx = (void*)(uintptr_t)ca;
+  }
   PyObject *out_sig = nullptr, *out_msg = nullptr, *out_spans = nullptr;
   if (out != Py_None) {
     if (!PyList_CheckExact(out) || PyList_GET_SIZE(out) < 2 || PyList_GET_SIZE(out) > 3) {
@@ -1417,6 +1589,7 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
   struct alignas(64) WorkerIdrs {  // a cache line (or more) of its own per worker
     IdrTable slot;
     std::vector<PyObject*> obj;
+    std::vector<uint32_t> kid;      // speculation: the key id of each of its identifiers (kmap)
     std::vector<Py_ssize_t> first;  // the item where the worker met it first
     size_t deferred = 0;            // items left for the GIL pass (3)
 #ifdef EDV_HAVE_DK
@@ -1492,6 +1665,7 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
     const uint64_t got = scursor.fetch_add(total + (1ull << kSeqShift), std::memory_order_relaxed);
     const size_t seq = (size_t)(got >> kSeqShift);
     const uint64_t pos = got & ((1ull << kSeqShift) - 1);
+    if (copier.chunk_seq) copier.chunk_seq[(size_t)(a / kStageChunk)].store((uint32_t)seq, std::memory_order_relaxed);
     if (pos + total > smsg_cap) {
       staged_ok = false;  // the buffer was sized from earlier batches: the caller re-scans unstaged
       copier.res_end[seq].store(pos + 1, std::memory_order_release);  // (nothing of it is copied)
@@ -1546,6 +1720,15 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
     copier.nchunks = (size_t)((n + kStageChunk - 1) / kStageChunk);
     copier.res_end.reset(new std::atomic<uint64_t>[copier.nchunks]);
     copier.slot_done.reset(new std::atomic<uint8_t>[copier.nchunks]);
+    if (part_fn) {
+      copier.chunk_seq.reset(new std::atomic<uint32_t>[copier.nchunks]);
+      copier.part_fn = part_fn;
+      copier.part_ctx = part_ctx;
+      copier.part_keys = kid_out;
+      copier.part_spans = spans_p;
+      copier.n_items = (uint64_t)n;
+      copier.part_items = part_items;
+    }
     for (size_t c = 0; c < copier.nchunks; ++c) {
       copier.res_end[c].store(0, std::memory_order_relaxed);
       copier.slot_done[c].store(0, std::memory_order_relaxed);
@@ -1568,6 +1751,7 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
       ScanItem& x = it[(size_t)i];
       x = ScanItem{};
       idr_of[(size_t)i] = nullptr;
+      if (kid_out) kid_out[i] = 0xffffffffu;
       if (prefetch) prefetch_ahead(items, i, b);
       if (!PyDict_CheckExact(m)) continue;
       // one pass over the request's keys: its signing serialization (kept if the item stays on
@@ -1636,7 +1820,9 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
       if (fresh) {
         tab.obj.push_back(iv);
         tab.first.push_back(i);
+        if (kmap) tab.kid.push_back(kmap->get((const char*)PyUnicode_1BYTE_DATA(iv), (size_t)PyUnicode_GET_LENGTH(iv)));
       }
+      if (kid_out) kid_out[i] = tab.kid[x.uid];
     }
     if (staged) stage_chunk(w, a, b);
   }, staged ? kStageChunk : kScanChunk);
@@ -1649,6 +1835,7 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
   // first occurrence in the batch (the single-thread order, whichever worker
   // took which chunk)
   std::vector<PyObject*> uniq;
+  std::vector<uint32_t> spec_u;  // speculation: the key id the scan wrote for each distinct identifier
   IdrTable slot;
   slot.reset(tabs.empty() ? 64 : tabs[0].obj.size() + 64);
   std::vector<std::vector<uint32_t>> to_global((size_t)t);
@@ -1672,7 +1859,10 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
       bool fresh = false;
       const uint32_t g = slot.find_or_add((const char*)PyUnicode_1BYTE_DATA(o), (size_t)PyUnicode_GET_LENGTH(o),
                                           (uint32_t)uniq.size(), fresh);
-      if (fresh) uniq.push_back(o);
+      if (fresh) {
+        uniq.push_back(o);
+        if (kmap) spec_u.push_back(tabs[(size_t)c.w].kid[c.local]);
+      }
       to_global[(size_t)c.w][c.local] = g;
     }
   }
@@ -1784,14 +1974,24 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
       fprintf(stderr, "scan (staged): n=%zd threads=%d  workers %.0f us, merge %.0f us, bookkeeping %.0f us\n", n, t,
               us(t_start, t_p1), us(t_p1, t_p2), us(t_p3, now()));
     }
+    // speculation: the key id used per distinct identifier (uint32 bytes), or None; parts_ok: every
+    // part's kernels were queued
+    PyObject* su = kmap ? PyBytes_FromStringAndSize((const char*)spec_u.data(), (Py_ssize_t)(spec_u.size() * 4))
+                        : (Py_INCREF(Py_None), Py_None);
+    if (!su) {
+      Py_DECREF(ul);
+      return nullptr;
+    }
+    PyObject* parts_ok = part_fn && !copier.part_failed && copier.next_part * part_items >= (uint64_t)n ? Py_True
+                                                                                                      : Py_False;
     if (spans_p != S.spans.data())  // written in place: the caller's buffer is the result
-      return Py_BuildValue("(y#y#NOOOy#O)", fast.data(), (Py_ssize_t)n, (const char*)uidx.data(),
+      return Py_BuildValue("(y#y#NOOOy#ONO)", fast.data(), (Py_ssize_t)n, (const char*)uidx.data(),
                            (Py_ssize_t)(uidx.size() * 4), ul, o_sig, out_msg, out_spans, shortv.data(), (Py_ssize_t)n,
-                           staged_ok.load() ? Py_True : Py_False);
-    return Py_BuildValue("(y#y#NOOy#y#O)", fast.data(), (Py_ssize_t)n, (const char*)uidx.data(),
+                           staged_ok.load() ? Py_True : Py_False, su, parts_ok);
+    return Py_BuildValue("(y#y#NOOy#y#ONO)", fast.data(), (Py_ssize_t)n, (const char*)uidx.data(),
                          (Py_ssize_t)(uidx.size() * 4), ul, o_sig, out_msg, (const char*)S.spans.data(),
                          (Py_ssize_t)(S.spans.size() * 8), shortv.data(), (Py_ssize_t)n,
-                         staged_ok.load() ? Py_True : Py_False);
+                         staged_ok.load() ? Py_True : Py_False, su, parts_ok);
   }
   PyObject* o_msg = refs.o_msg = out_buffer(out_msg, (Py_ssize_t)off[(size_t)n], &dmsg);
   PyObject* ret = nullptr;
@@ -2352,6 +2552,10 @@ PyMethodDef kMethods[] = {
      "scan_batch(msgs, ignore, threads=0, out=None) -> (fast, idrs, sig64, msgbuf, off, short): authenticate()'s "
      "host steps for a batch.  out = [bytearray, bytearray]: sig64 / msgbuf are written into them (grown, never "
      "shrunk: slice to n * 64 and off[n] bytes) and returned"},
+    {"kid_map", py_kid_map, METH_VARARGS,
+     "kid_map(old, identifiers, ids_u32) -> map: identifier text -> key id (0xffffffff: none) for the staged "
+     "scan's speculation (old: a kid_map to update in place, or None)"},
+    {"kid_map_size", py_kid_map_size, METH_O, "kid_map_size(map) -> entries"},
     {"scan_batch_u", py_scan_batch_u, METH_VARARGS,
      "scan_batch_u(msgs, ignore, threads=0, out=None, slot=64) -> (fast, uidx_u32, uniq, sig, msgbuf, off, short): "
      "scan_batch with the identifiers as indices into the batch's distinct identifiers; slot=96: sig is n "

@@ -65,9 +65,9 @@ except ImportError:  # pragma: no cover - the per-message path below
     _scan_batch = _gather_items = _results_from = None
 try:
     from ._hostpack import (gather_u32 as _gather_u32, pack_range as _pack_range, repack_spans as _repack_spans,
-                            results_ok as _results_ok)
+                            results_ok as _results_ok, kid_map as _kid_map, kid_map_size as _kid_map_size)
 except ImportError:  # pragma: no cover
-    _pack_range = _repack_spans = _gather_u32 = _results_ok = None
+    _pack_range = _repack_spans = _gather_u32 = _results_ok = _kid_map = _kid_map_size = None
 try:  # the node's per-message path: authenticate()'s host steps in one call; the verify-ahead's dedupe
     from ._hostpack import authn_key as _authn_key, distinct_sm as _distinct_sm
 except ImportError:  # pragma: no cover
@@ -116,6 +116,7 @@ _PINNED_MIN_BATCH = 4096  # smaller batches keep the bytearrays (the library sta
 _STREAM_CHUNK = 1 << 17  # requests per streamed submit: 2^17 beat 2^18 and 2^16 by 2-3 % (profiles/r06c)
 _STREAM_WINDOW = 16  # streamed submits in flight before the oldest is collected (edverify.hip kMaxPending = 64)
 _STAGE_MIN_BATCH = 1 << 16  # batches staged while scanned (edv_stage_put from the scan's workers)
+_PART_ITEMS = 1 << 16  # a speculative staged batch's kernels go out per this many requests
 
 
 _MISSING = object()
@@ -177,7 +178,7 @@ class _GpuState:
 
     def __init__(self, engine=None, device=0, devices=None, verdict_cache_size=1 << 20, key_window="auto",
                  max_keys=16384, hot_key_uses=2, key_store_bytes=KEY_STORE_BYTES, scan_threads=0,
-                 pipeline_part=0, async_key_builds=True, stream=True, stage=True):
+                 pipeline_part=0, async_key_builds=True, stream=True, stage=True, speculate=True):
         self.engine = engine
         self.device = device
         self.devices = devices
@@ -224,6 +225,14 @@ class _GpuState:
         self.fast_keys = {}
         self.fast_keys_max = 1 << 16
         self.kid_out = bytearray()  # a batch's key id per request (gather_u32 output, reused)
+        # speculate=True (default): a synchronous staged batch runs its kernels under its own scan,
+        # part by part, with key ids the scan takes from kid_map (identifier -> key id of the batches
+        # before); after the scan every distinct identifier's id is checked against getVerkey and the
+        # key store (and the store's version), and any difference re-runs the verify the ordinary way
+        self.speculate = speculate
+        self.kid_map = None
+        self.kid_map_version = None
+        self.kid_map_max = 1 << 20
         self.stats = {"batches": 0, "batch_items": 0, "cache_hits": 0, "single_verifies": 0, "keyed_items": 0,
                       "keys_registered": 0, "prefetched": 0}
 
@@ -684,15 +693,23 @@ class GpuAuthMixin:
         slots to the device (edv_stage_put) as soon as they are written, so
         by the time the scan returns most of the batch is already in HBM;
         edv_verify_staged then waits for the rest and runs the kernels over
-        the item spans.  In the node's steady state (every item scanned,
-        every identifier resolved to a built key); a batch with other items
-        repacks its messages contiguously and takes the ordinary path (same
-        verdicts).  None when the scan could not stage (the pinned buffer
-        was too small for this batch, or items needed the interpreter): the
-        caller scans again the ordinary way.  staging_set / defer: the
-        pipeline of authenticate_batches -- staged into that set of the
-        engine's (and this authenticator's) buffers, and in the steady state a
-        callable returning the results once the kernels are collected."""
+        the item spans.  Synchronous batches (defer False) speculate: the scan
+        also writes each request's key id from kid_map (the ids of the batches
+        before) and its copier queues the kernels of every 2^16 staged
+        requests (edv_verify_staged_part), so the kernels run under the scan
+        too; after it, the ids of the batch's distinct identifiers (getVerkey,
+        the key store) must equal the ones used and the store must not have
+        moved a key (KeyStore.version), else the verify runs again the
+        ordinary way -- the verdicts are the ordinary path's either way.  In
+        the node's steady state (every item scanned, every identifier
+        resolved to a built key); a batch with other items repacks its
+        messages contiguously and takes the ordinary path (same verdicts).
+        None when the scan could not stage (the pinned buffer was too small
+        for this batch, or items needed the interpreter): the caller scans
+        again the ordinary way.  staging_set / defer: the pipeline of
+        authenticate_batches -- staged into that set of the engine's (and this
+        authenticator's) buffers, and in the steady state a callable returning
+        the results once the kernels are collected."""
         import numpy as np
         from time import perf_counter
         g = self._g
@@ -711,23 +728,51 @@ class GpuAuthMixin:
             return _BUSY
         sfx = "" if staging_set == 0 else str(staging_set)
         spans_buf = self._pinned(eng, "pinned_spans" + sfx, 16 * n)  # the scan writes the item spans here
+        kid_buf = self._pinned(eng, "pinned_kid" + sfx, 4 * n)  # key ids straight into pinned memory: no copy
+        ks = self._key_store()
+        spec, parts = None, None
+        if (not defer and g.speculate and g.kid_map is not None and ks is not None and _kid_map is not None
+                and spans_buf is not None and kid_buf is not None and getattr(eng, "supports_staged_parts", False)):
+            ks_version = ks.version
+            parts = eng.verify_staged_begin(True, n)
+            spec = (g.kid_map, kid_buf, eng.parter(), _PART_ITEMS)
         t0 = perf_counter()
-        scan = _scan_batch(msgs, [SIG], g.scan_threads, [bufs[0], bufs[1], spans_buf], slot, 2, eng.stager(),
-                           slot_base)
+        try:
+            scan = _scan_batch(msgs, [SIG], g.scan_threads, [bufs[0], bufs[1], spans_buf], slot, 2, eng.stager(),
+                               slot_base, spec)
+        except BaseException:
+            if parts is not None:  # free the set the parts held
+                for f in (eng.verify_staged_end, lambda: eng.verify_staged_collect(parts)):
+                    try:
+                        f()
+                    except Exception:
+                        pass
+            raise
+        fast_b, uidx_b, uniq, sig_o, msg_o, spans_b, short, staged_ok, spec_u, parts_ok = scan
+        if parts is not None:  # the parts' verdict copy queued after the last part
+            try:
+                eng.verify_staged_end()
+            except Exception:
+                parts_ok = False  # a part failed: the verdicts come from the ordinary verify
         t1 = perf_counter()
-        fast_b, uidx_b, uniq, sig_o, msg_o, spans_b, short, staged_ok = scan
+
+        def drop_parts():  # the speculative verdicts are not used: free the set
+            nonlocal parts
+            if parts is not None:
+                eng.verify_staged_collect(parts)
+                parts = None
         if spans_b is spans_buf:
             spans_b = memoryview(spans_b).cast("B")[:16 * n]
         spans = np.frombuffer(spans_b, np.uint64, count=2 * n)
         ms, me = spans[:n], spans[n:]
         if not staged_ok:
+            drop_parts()
             g.msg_bytes_per_item *= 1.5  # the next buffers are sized larger
             return None
         # (the chunks' reservations are contiguous from 0: the largest end is the bytes staged)
         g.msg_bytes_per_item = max(g.msg_bytes_per_item * 0.5, float(me.max()) / n if n else 0.0)
         ukeys = self._keys_for(uniq)  # authenticate():93-99, once per identifier
         ids = None
-        ks = self._key_store()
         if ks is not None and fast_b.count(0) == 0 and all(k.__class__ is bytes for k in ukeys):
             if g.hot or g.pending:
                 self._register_waiting(ks, list(dict.fromkeys(ukeys)))
@@ -735,16 +780,23 @@ class GpuAuthMixin:
             if any(i is None for i in ids):
                 ids = None
         if ids is None:  # not the steady state: contiguous messages, the ordinary path
+            drop_parts()
             del spans, ms, me
             msg_c, off_c = _repack_spans(msg_o, spans_b)
             return self._finish_scanned(msgs, (fast_b, uidx_b, uniq, sig_o, msg_c, off_c, short), slot, ukeys)
-        kid_buf = self._pinned(eng, "pinned_kid" + sfx, 4 * n)  # key ids straight into pinned memory: no copy
-        kid = np.frombuffer(_gather_u32(np.asarray(ids, np.uint32).tobytes(), uidx_b,
-                                        kid_buf if kid_buf is not None else g.kid_out), np.uint32, count=n)
+        ids_b = np.asarray(ids, np.uint32).tobytes()
+        spec_hit = parts is not None and parts_ok and spec_u == ids_b and ks.version == ks_version
+        if g.speculate and _kid_map is not None and (spec_u != ids_b or g.kid_map is None or
+                                                     g.kid_map_version != ks.version):
+            # remember this batch's ids for the next batch's scan (a fresh map when the store moved keys)
+            fresh = g.kid_map is None or g.kid_map_version != ks.version or _kid_map_size(g.kid_map) > g.kid_map_max
+            g.kid_map = _kid_map(None if fresh else g.kid_map, uniq, ids_b)
+            g.kid_map_version = ks.version
         t2 = perf_counter()
         g.stats["batches"] += 1
         g.stats["batch_items"] += n
         g.stats["keyed_items"] += n
+        g.stats["speculated"] = g.stats.get("speculated", 0) + (n if spec_hit else 0)
 
         def verdicts(ok, t3):
             results, failed = _results_ok(ok, short, uidx_b, uniq)
@@ -752,8 +804,17 @@ class GpuAuthMixin:
                 results[i] = InvalidSignature()
             t4 = perf_counter()
             g.last_breakdown = {"scan_and_copies": (t1 - t0) * 1e3, "keys_and_ids": (t2 - t1) * 1e3,
-                                "verify_wait": (t3 - t2) * 1e3, "verdicts": (t4 - t3) * 1e3}
+                                "verify_wait": (t3 - t2) * 1e3, "verdicts": (t4 - t3) * 1e3,
+                                "speculated": bool(spec_hit)}
             return results
+        if spec_hit:  # the kernels ran under the scan with exactly these ids
+            ok = np.asarray(eng.verify_staged_collect(parts), bool)
+            parts = None
+            del spans, ms, me, spans_b
+            return verdicts(ok, perf_counter())
+        drop_parts()
+        kid = np.frombuffer(_gather_u32(ids_b, uidx_b, kid_buf if kid_buf is not None else g.kid_out), np.uint32,
+                            count=n)
         if defer:  # the kernels run while the caller goes on (its next batch's scan)
             handle = eng.verify_staged_submit(True, kid, slot_base, 0, ms, me)
             t2 = perf_counter()

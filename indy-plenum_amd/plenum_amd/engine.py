@@ -267,6 +267,26 @@ class EdVerifyEngine:
         check(self._lib.edv_verify_staged_collect(self._ctx, ticket, _ptr(bits) if n else ctypes.c_void_p(1)))
         return unpack_bits(bits, n)
 
+    supports_staged_parts = True
+
+    def verify_staged_begin(self, keyed, n):
+        """Take the current staging set for an n-item batch verified in parts
+        (edv_verify_staged_begin): a handle for verify_staged_collect once
+        verify_staged_end has run."""
+        ticket = ctypes.c_uint64()
+        check(self._lib.edv_verify_staged_begin(self._ctx, 1 if keyed else 0, int(n), ctypes.byref(ticket)))
+        return (ticket.value, int(n), None)
+
+    def parter(self):
+        """(edv_verify_staged_part address, context address): what the native
+        scan's copier calls for each part of the batch it has staged."""
+        return (ctypes.cast(self._lib.edv_verify_staged_part, ctypes.c_void_p).value, self._ctx.value)
+
+    def verify_staged_end(self):
+        """Queue the verdicts' copy after the last part (edv_verify_staged_end);
+        raises if a part failed (collect the handle all the same)."""
+        check(self._lib.edv_verify_staged_end(self._ctx))
+
     def host_alloc(self, nbytes):
         """nbytes of pinned host memory (edv_host_alloc) as a writable ctypes
         array; host-pointer verifies copy inputs inside it to the device with no

@@ -60,6 +60,9 @@ class KeyStore:
         self._generation = None
         self._building = {}           # id -> ticket of its latest build (asynchronous registrations)
         self._tickets = OrderedDict()  # ticket -> ids, ascending (tickets complete in order)
+        # bumped whenever an id may stop meaning the key it meant (a reset, an eviction, a retired
+        # slot): what a speculative batch (key ids from earlier batches) checks it ran against
+        self.version = 0
 
     @classmethod
     def attach(cls, engine, window, capacity):
@@ -86,6 +89,7 @@ class KeyStore:
         self._building.clear()
         self._tickets.clear()
         self._generation = getattr(self.engine, "keys_generation", 0)
+        self.version += 1
 
     def _refresh(self):
         """Drop the ids whose builds have completed from the building set
@@ -178,6 +182,7 @@ class KeyStore:
             victims = [k for k in self._ids if k not in pinned][:len(over)]
             for k_new, k_old in zip(over, victims):
                 slot = self._ids.pop(k_old)
+                self.version += 1
                 try:
                     pk = np.frombuffer(k_new, np.uint8).reshape(1, 32)
                     if use_async and hasattr(self.engine, "keys_set_async"):

@@ -12,6 +12,19 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+_BASELINE = []
+
+
+def _baseline_lib():
+    if not _BASELINE:
+        _BASELINE.append(ctypes.CDLL(os.path.join(ROOT, "oracle", "_build", "libcpu_baseline.so")))
+    return _BASELINE[0]
+
+
+def _threads():
+    return max(1, min(16, len(os.sched_getaffinity(0))))
+
+
 def load_oracle():
     lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "_build", "libed25519_oracle.so"))
     lib.oracle_verify_detached.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p]
@@ -120,13 +133,24 @@ class OracleEngine:
         return self._verify(self._sig64(sig64, sig_slot), pk32, msgs, msg_off)
 
     def _verify(self, sig64, pk32, msgs, msg_off):
+        sig64 = np.ascontiguousarray(np.asarray(sig64, np.uint8).reshape(-1, 64))
+        pk32 = np.ascontiguousarray(np.asarray(pk32, np.uint8).reshape(-1, 32))
+        off = np.ascontiguousarray(np.asarray(msg_off, np.uint64))
+        n = len(off) - 1
+        if n >= 64:  # the same C oracle on every host CPU (oracle/cpu_baseline.c, use_sodium = 0)
+            buf = np.frombuffer(bytes(msgs) if not isinstance(msgs, np.ndarray) else msgs.tobytes(), np.uint8)
+            buf = np.concatenate([buf, np.zeros(16, np.uint8)])
+            ok = np.zeros(n, np.uint8)
+            secs = ctypes.c_double()
+            P = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+            assert _baseline_lib().cpu_baseline_run(P(sig64), P(pk32), P(buf), P(off), ctypes.c_uint64(n),
+                                                    _threads(), 0, P(ok), ctypes.byref(secs)) == 0
+            return ok.astype(bool)
         msgs = bytes(msgs) if not isinstance(msgs, np.ndarray) else msgs.tobytes()
-        sig64 = np.asarray(sig64, np.uint8).reshape(-1, 64)
-        pk32 = np.asarray(pk32, np.uint8).reshape(-1, 32)
-        off = [int(x) for x in msg_off]
-        return np.array([self.lib.oracle_verify_detached(sig64[i].tobytes(), msgs[off[i]:off[i + 1]],
-                                                         off[i + 1] - off[i], pk32[i].tobytes()) == 0
-                         for i in range(len(off) - 1)], dtype=bool)
+        o = [int(x) for x in off]
+        return np.array([self.lib.oracle_verify_detached(sig64[i].tobytes(), msgs[o[i]:o[i + 1]],
+                                                         o[i + 1] - o[i], pk32[i].tobytes()) == 0
+                         for i in range(n)], dtype=bool)
 
 
 class OracleBlsEngine:
@@ -278,10 +302,61 @@ class StagingOracleEngine(OracleEngine):
         return (self.cur, ok)
 
     def verify_staged_collect(self, handle):
+        if isinstance(handle, _Parts):
+            return self._collect_parts(handle)
         s, ok = handle
         assert self.held[s] is ok
         self.held[s] = None
         return ok
+
+    # -- edv_verify_staged_begin / _part / _end (stage_double_part snapshots each part)
+    supports_staged_parts = True
+    part_fail_at = 0  # make the k-th part call fail (tests)
+
+    def verify_staged_begin(self, keyed, n):
+        assert keyed and self.held[self.cur] is None, "staging set %d holds an uncollected submission" % self.cur
+        h = _Parts(self.cur, n, self.part_fail_at)
+        self.held[self.cur] = h
+        self.parts_begun = getattr(self, "parts_begun", 0) + 1
+        self._open = h
+        return h
+
+    def parter(self):
+        fn = ctypes.CDLL(os.path.join(ROOT, "oracle", "_build", "libstage_double.so")).stage_double_part
+        return (ctypes.cast(fn, ctypes.c_void_p).value, ctypes.addressof(self._open.c))
+
+    def verify_staged_end(self):
+        h, self._open = self._open, None
+        h.ended = True
+        if h.c.bad or (h.c.fail_at and h.c.calls >= h.c.fail_at):
+            raise RuntimeError("a part failed")
+
+    def _collect_parts(self, h):
+        assert self.held[h.set] is h and h.ended
+        self.held[h.set] = None
+        n, cov = h.n, int(h.c.covered)
+        ok = np.zeros(n, bool)
+        if cov:
+            st = np.frombuffer(self.sets[h.set], np.uint8)
+            keys = np.ctypeslib.as_array(h.keys)[:cov]
+            spans = np.ctypeslib.as_array(h.spans)
+            ok[:cov] = self._verify_span_items(st, keys, spans[:cov], spans[n:n + cov], h)
+        return ok
+
+    def _verify_span_items(self, st, keys, ms, me, h):
+        # the slots sit at the staging's slot offset; the scan reserved them after the messages
+        slot_off = self._slot_off_of(h)
+        n = len(ms)
+        slots = st[slot_off:slot_off + 96 * n].reshape(-1, 96)
+        parts = [st[int(a):int(b)].tobytes() for a, b in zip(ms, me)]
+        off = np.zeros(n + 1, np.uint64)
+        off[1:] = np.cumsum([len(p) for p in parts])
+        buf = np.frombuffer(b"".join(parts), np.uint8)
+        self.parts_verified = getattr(self, "parts_verified", 0) + n
+        return self.verify_batch_keyed(slots, keys, buf, off, sig_slot=96)
+
+    def _slot_off_of(self, h):
+        return int(h.c.slot_off)
 
     def stager(self):
         return (ctypes.cast(self._put, ctypes.c_void_p).value, ctypes.addressof(self.stage))
@@ -298,3 +373,20 @@ class StagingOracleEngine(OracleEngine):
         if keyed:
             return self.verify_batch_keyed(slots, keys, buf, off, sig_slot=96)
         return self.verify_batch(slots, keys, buf, off, sig_slot=96)
+
+
+class _PartC(ctypes.Structure):
+    _fields_ = [("keys", ctypes.c_void_p), ("spans", ctypes.c_void_p), ("n", ctypes.c_uint64),
+                ("covered", ctypes.c_uint64), ("calls", ctypes.c_uint64), ("fail_at", ctypes.c_uint64),
+                ("bad", ctypes.c_uint64), ("slot_off", ctypes.c_uint64)]
+
+
+class _Parts:
+    """A speculative staged batch of StagingOracleEngine (the double's edv_verify_staged_begin
+    handle): the part snapshots stage_double_part writes."""
+
+    def __init__(self, s, n, fail_at):
+        self.set, self.n, self.ended = s, n, False
+        self.keys = (ctypes.c_uint32 * max(n, 1))()
+        self.spans = (ctypes.c_uint64 * max(2 * n, 1))()
+        self.c = _PartC(ctypes.addressof(self.keys), ctypes.addressof(self.spans), n, 0, 0, fail_at, 0, 0)

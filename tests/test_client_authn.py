@@ -845,3 +845,88 @@ def test_authenticate_batch_while_an_iteration_holds_set_0(oracle, monkeypatch):
                                           for i, m in enumerate(b)]
     assert eng.held[0] is not None  # untouched
     assert list(it) == [want, want] and eng.held == [None, None]
+
+
+def _staged_pair(oracle, monkeypatch, n_msgs=5500, **kw):
+    from engine_double import StagingOracleEngine
+    from plenum_amd import client_authn as CA
+    monkeypatch.setattr(CA, "_STAGE_MIN_BATCH", 1000)
+    monkeypatch.setattr(CA, "_PINNED_MIN_BATCH", 1000)
+    monkeypatch.setattr(CA, "_PART_ITEMS", 4096)
+    idrs, vks, msgs = _signed(5, n_msgs)
+    eng = StagingOracleEngine(oracle)
+    a = GpuAuthNr(engine=eng, **kw)
+    ref = GpuAuthNr(engine=OracleEngine(oracle), max_keys=0)
+    for i, v in zip(idrs[:4], vks[:4]):
+        a.addIdr(i, v)
+    a.clients[idrs[4]] = {"verkey": vks[4], "role": None}  # known, not queued for a key slot
+    for i, v in zip(idrs, vks):
+        ref.addIdr(i, v)
+    a.keys_settle()
+    return eng, a, ref, idrs, vks, msgs
+
+
+def test_speculative_staged_batches(oracle, monkeypatch):
+    """A synchronous staged batch whose kernels run under its own scan (key ids
+    from kid_map, edv_verify_staged_part per staged part -- the double
+    snapshots each part as the library DMAs it): the first batch builds the
+    map, the next ones speculate; forgeries still reject; a new signer, an
+    identifier whose key moved (eviction: KeyStore.version) and a failing part
+    all fall back to the ordinary verify; every outcome equals the general
+    path's."""
+    eng, a, ref, idrs, vks, msgs = _staged_pair(oracle, monkeypatch, max_keys=4)
+    steady = [m for m in msgs if m["identifier"] in idrs[:4]]
+    b = [dict(m) for m in steady]
+    b[5]["reqId"] += 1
+    b[-1]["reqId"] += 1
+
+    def check(batch):
+        assert [_outcome(r) for r in a.authenticate_batch(batch)] == \
+            [_outcome(r) for r in ref.authenticate_batch(batch)]
+        assert eng.held == [None, None]
+    check(b)
+    assert getattr(eng, "parts_begun", 0) == 0 and a._g.kid_map is not None  # no map yet: ordinary
+    check(b)
+    assert eng.parts_begun == 1 and a.stats["speculated"] == len(b) and a._g.last_breakdown["speculated"]
+    assert eng.parts_verified == len(b)
+    # identifiers[4] is known to the state only: its key is not registered -> not the steady state
+    check([dict(m) for m in msgs])
+    # a new key registered (evicting one of the four): its requests' ids change -> fallback, then speculate
+    a.addIdr(idrs[4], vks[4])
+    a.keys_settle()
+    v0 = a._key_store().version
+    mixed = [dict(m) for m in msgs if m["identifier"] != idrs[0]]
+    check(mixed)
+    spec0 = a.stats["speculated"]
+    check(mixed)
+    check(mixed)
+    assert a._key_store().version >= v0 and a.stats["speculated"] > spec0
+    # a part that fails: the ordinary verify
+    eng.part_fail_at = 2
+    before = a.stats["speculated"]
+    check(mixed)
+    assert a.stats["speculated"] == before and not a._g.last_breakdown["speculated"]
+    eng.part_fail_at = 0
+    check(mixed)
+    assert a.stats["speculated"] > before
+
+
+def test_speculative_staged_batch_raising_scan_frees_the_set(oracle, monkeypatch):
+    """A scan that raises inside a speculative batch leaves neither staging
+    set held."""
+    from plenum_amd import client_authn as CA
+    eng, a, ref, idrs, vks, msgs = _staged_pair(oracle, monkeypatch)
+    steady = [dict(m) for m in msgs if m["identifier"] in idrs[:4]]
+    a.authenticate_batch(steady)
+    real = CA._scan_batch
+
+    def boom(*args):
+        if len(args) > 8 and args[8] is not None:
+            raise MemoryError("injected")
+        return real(*args)
+    monkeypatch.setattr(CA, "_scan_batch", boom)
+    with pytest.raises(MemoryError):
+        a.authenticate_batch(steady)
+    assert eng.held == [None, None]
+    monkeypatch.setattr(CA, "_scan_batch", real)
+    assert a.authenticate_batch(steady) == [m["identifier"] for m in steady]

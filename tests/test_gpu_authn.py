@@ -664,3 +664,42 @@ def test_authenticate_batches_pipeline_on_gpu(gpu_engine):
         got = [[r if isinstance(r, str) else type(r).__name__ for r in res] for res in a.authenticate_batches(batches)]
         assert got == want, rep
     assert want[0].count("InvalidSignature") == n // 10 and want[2][99] == "UnknownIdentifier"
+
+
+def test_speculative_staged_batches_on_gpu(gpu_engine):
+    """A synchronous staged batch's kernels under its own scan on the device
+    (edv_verify_staged_part from the scan's copier, key ids from kid_map): a
+    300,000-request batch (several 2^16-request parts, a ragged last one)
+    with every 7th request forged (and _drain's every 10th), three times -- the first builds the map,
+    the next two speculate -- then a batch in which one signer's key was
+    replaced in the store (the ids differ: the ordinary verify) and the
+    speculation after it; every outcome is the construction's."""
+    import copy
+    n = 300_001
+    reqs, rx, idrs, vks, pks, sers, sig = _drain(gpu_engine, n_req=n, n_nodes=1, n_signers=32)
+    batch = [copy.deepcopy(r) for r in reqs]
+    for i in range(0, n, 7):
+        batch[i]["reqId"] += 1
+    want = ["InvalidSignature" if i % 7 == 0 or i % 10 == 3 else r["identifier"] for i, r in enumerate(batch)]
+    a = GpuAuthNr(engine=gpu_engine, max_keys=32)
+    for idr, vk in zip(idrs, vks):
+        a.addIdr(idr, vk)
+    a.keys_settle()
+    spec = []
+    for rep in range(3):
+        res = a.authenticate_batch(batch)
+        assert [r if isinstance(r, str) else type(r).__name__ for r in res] == want, rep
+        spec.append(bool(a._g.last_breakdown.get("speculated")))
+    assert spec == [False, True, True], spec
+    # a signer whose key moves: the store evicts the LRU key for a new one (version bump)
+    ks = a._key_store()
+    v0 = ks.version
+    ks.register([bytes(range(32))])  # any valid-length key: takes a slot by evicting one
+    ks.settle()
+    assert ks.version > v0
+    res = a.authenticate_batch(batch)
+    assert not a._g.last_breakdown.get("speculated")
+    assert [r if isinstance(r, str) else type(r).__name__ for r in res] == want
+    a.keys_settle()
+    res = a.authenticate_batch(batch)
+    assert [r if isinstance(r, str) else type(r).__name__ for r in res] == want
