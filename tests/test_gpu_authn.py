@@ -39,6 +39,28 @@ def test_reference_propagate_vector_on_gpu(gpu_engine):
     every outcome the reference's own authenticate() gave (authn_kat.json)."""
     cases = [c for c in T.kat()["cases"] if c["name"].startswith("ref-propagate-")]
     assert len(cases) == 7
+    with _own_key_store(gpu_engine):
+        _propagate_cases(gpu_engine, cases)
+
+
+def _own_key_store(eng):
+    """A test whose authenticators size the engine's key store themselves (the
+    first authenticator on an engine fixes its capacity and window): a store
+    of their own for the test, and the default store again after it."""
+    import contextlib
+
+    @contextlib.contextmanager
+    def cm():
+        eng.__dict__.pop("_edv_key_store", None)
+        try:
+            yield
+        finally:
+            eng.__dict__.pop("_edv_key_store", None)
+            eng.keys_reset()
+    return cm()
+
+
+def _propagate_cases(gpu_engine, cases):
     for max_keys in (16, 0):
         a = GpuAuthNr(engine=gpu_engine, max_keys=max_keys)
         idr = cases[0]["msg"]["identifier"]
@@ -681,6 +703,11 @@ def test_speculative_staged_batches_on_gpu(gpu_engine):
     for i in range(0, n, 7):
         batch[i]["reqId"] += 1
     want = ["InvalidSignature" if i % 7 == 0 or i % 10 == 3 else r["identifier"] for i, r in enumerate(batch)]
+    with _own_key_store(gpu_engine):
+        _speculate_on_gpu(gpu_engine, batch, want, idrs, vks)
+
+
+def _speculate_on_gpu(gpu_engine, batch, want, idrs, vks):
     a = GpuAuthNr(engine=gpu_engine, max_keys=32)
     for idr, vk in zip(idrs, vks):
         a.addIdr(idr, vk)
