@@ -47,7 +47,8 @@ authenticators (names from BASELINE.json's north star).
 import copy
 import threading
 from abc import abstractmethod
-from collections import OrderedDict
+from collections import OrderedDict, deque
+from time import monotonic
 from copy import deepcopy
 from typing import Dict
 
@@ -120,6 +121,7 @@ _PART_ITEMS = 1 << 16  # a speculative staged batch's kernels go out per this ma
 
 
 _MISSING = object()
+_VERDICT_ENTRY_BYTES = 240  # a verdict-cache entry's objects beyond its key and sm bytes (tuple, 2 bytes, dict slot)
 _BUSY = object()  # _authenticate_staged: the staging set is held by a batch in flight
 _IGNORE_SIG = (SIG,)
 
@@ -176,15 +178,24 @@ class _GpuState:
     calls authenticate() from its one looper thread (looper.py:141-151), as
     the reference does."""
 
-    def __init__(self, engine=None, device=0, devices=None, verdict_cache_size=1 << 20, key_window="auto",
+    def __init__(self, engine=None, device=0, devices=None, verdict_cache_size=1 << 20,
+                 verdict_cache_bytes=256 << 20, verdict_max_age=300.0, key_window="auto",
                  max_keys=16384, hot_key_uses=2, key_store_bytes=KEY_STORE_BYTES, scan_threads=0,
                  pipeline_part=0, async_key_builds=True, stream=True, stage=True, speculate=True):
         self.engine = engine
         self.device = device
         self.devices = devices
         self.keys = VerkeyCache()
+        # the verify-ahead verdicts: (key bytes, sm) -> bool, oldest first, bounded by entries, by
+        # bytes (keys + sm + ~240 B of objects per entry) and by age (seconds since insertion; trimmed
+        # on insert, per one-second epoch).  A verdict never goes stale -- it is the verdict of
+        # exactly those bytes under exactly that key -- so the bounds only cap memory.
         self.verdicts = OrderedDict()
         self.verdict_cache_size = verdict_cache_size
+        self.verdict_cache_bytes = verdict_cache_bytes
+        self.verdict_max_age = verdict_max_age
+        self.verdict_bytes = 0
+        self.verdict_epochs = deque()  # [start time, entries inserted in that second], oldest first
         self.key_window = auto_window(max_keys, key_store_bytes) if key_window == "auto" else key_window
         self.max_keys = max_keys
         self.hot_key_uses = hot_key_uses
@@ -246,7 +257,10 @@ class GpuAuthMixin:
     def _gpu_init(self, engine=None, device=0, **options):
         """engine: an EdVerifyEngine / MultiEngine (default: one on `device`;
         devices=[...] or "all": a MultiEngine sharding every batch over them).
-        options (_GpuState): verdict_cache_size; key_window ('auto' = widest
+        options (_GpuState): verdict_cache_size / verdict_cache_bytes /
+        verdict_max_age (the verify-ahead cache's bounds: entries, bytes,
+        seconds); speculate (a synchronous staged batch's kernels under its
+        own scan, key ids from the batches before; default True); key_window ('auto' = widest
         comb whose max_keys tables fit key_store_bytes, e.g. 16,384 keys in
         32 GiB -> W=10, 1,000 keys -> W=14); max_keys; hot_key_uses;
         scan_threads (host threads of authenticate_batch's native scan, 0 =
@@ -532,9 +546,32 @@ class GpuAuthMixin:
 
     def _remember(self, p, ok, vkey=None):
         g = self._g
-        g.verdicts[vkey if vkey is not None else self._vkey(p)] = ok
-        if len(g.verdicts) > g.verdict_cache_size:
-            g.verdicts.popitem(last=False)
+        k = vkey if vkey is not None else self._vkey(p)
+        verdicts = g.verdicts
+        if k in verdicts:
+            verdicts[k] = ok
+            return
+        verdicts[k] = ok
+        g.verdict_bytes += len(k[0]) + len(k[1]) + _VERDICT_ENTRY_BYTES
+        now = monotonic()
+        epochs = g.verdict_epochs
+        if not epochs or now - epochs[-1][0] >= 1.0:
+            epochs.append([now, 0])
+        epochs[-1][1] += 1
+        while len(verdicts) > g.verdict_cache_size or g.verdict_bytes > g.verdict_cache_bytes:
+            self._forget_oldest_verdict()
+        while epochs and now - epochs[0][0] > g.verdict_max_age and verdicts:
+            self._forget_oldest_verdict()
+
+    def _forget_oldest_verdict(self):
+        g = self._g
+        k, _ = g.verdicts.popitem(last=False)
+        g.verdict_bytes -= len(k[0]) + len(k[1]) + _VERDICT_ENTRY_BYTES
+        epochs = g.verdict_epochs
+        if epochs:
+            epochs[0][1] -= 1
+            if epochs[0][1] <= 0:
+                epochs.popleft()
 
     def _verify_prepared(self, p):
         if not p.key:  # nacl_wrappers.py:237-238: no key -> False
@@ -1274,6 +1311,8 @@ class GpuAuthMixin:
 
     def clear_verdicts(self):
         self._g.verdicts.clear()
+        self._g.verdict_bytes = 0
+        self._g.verdict_epochs.clear()
 
     # -- multi-signature extension (parity unpinned) --------------------------
     def _prepare_multi(self, msg, signatures, threshold):

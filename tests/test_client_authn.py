@@ -930,3 +930,39 @@ def test_speculative_staged_batch_raising_scan_frees_the_set(oracle, monkeypatch
     assert eng.held == [None, None]
     monkeypatch.setattr(CA, "_scan_batch", real)
     assert a.authenticate_batch(steady) == [m["identifier"] for m in steady]
+
+
+def test_verdict_cache_bounded_by_entries_bytes_and_age(oracle, monkeypatch):
+    """The verify-ahead verdict cache (bounded by bytes, trimmed by
+    age): entries beyond verdict_cache_size, bytes beyond verdict_cache_bytes
+    and entries older than verdict_max_age go, oldest first; the byte count
+    stays exact; authenticate() answers the same with or without the entry."""
+    from plenum_amd import client_authn as CA
+    idrs, vks, msgs = _signed(2, 300)
+    clock = [1000.0]
+    monkeypatch.setattr(CA, "monotonic", lambda: clock[0])
+    a = GpuAuthNr(engine=OracleEngine(oracle), verdict_cache_size=250, verdict_cache_bytes=1 << 30,
+                  verdict_max_age=10.0)
+    for i, v in zip(idrs, vks):
+        a.addIdr(i, v)
+    g = a._g
+
+    def size_of():
+        return sum(len(k[0]) + len(k[1]) + CA._VERDICT_ENTRY_BYTES for k in g.verdicts)
+    a.prefetch(msgs[:200])
+    assert len(g.verdicts) == 200 and g.verdict_bytes == size_of()
+    clock[0] += 5
+    a.prefetch(msgs[200:])
+    assert len(g.verdicts) == 250 and g.verdict_bytes == size_of()  # entries bound: the oldest 50 went
+    assert (a._vkey(a._prepare(msgs[0])) not in g.verdicts) and (a._vkey(a._prepare(msgs[299])) in g.verdicts)
+    clock[0] += 6  # the first second's entries are now 11 s old
+    a.prefetch([msgs[0]])
+    assert len(g.verdicts) == 101 and g.verdict_bytes == size_of()  # only the 5-second-old ones and the new one
+    g.verdict_cache_bytes = 50 * (size_of() // len(g.verdicts))
+    a.prefetch([msgs[1]])
+    assert g.verdict_bytes <= g.verdict_cache_bytes and g.verdict_bytes == size_of()
+    hits = g.stats["cache_hits"]
+    assert [a.authenticate(m) for m in msgs] == [m["identifier"] for m in msgs]
+    assert g.stats["cache_hits"] > hits
+    a.clear_verdicts()
+    assert g.verdict_bytes == 0 and not g.verdict_epochs
