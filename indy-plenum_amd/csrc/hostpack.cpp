@@ -1180,9 +1180,11 @@ int cpu_budget() {
 constexpr int kMaxScanThreads = 48;
 int scan_threads(Py_ssize_t n, int want) {
   if (want > 0) return std::min(want, 64);
+  const char* env = getenv("EDV_SCAN_THREADS");  // at most this many workers (A/B)
+  const int env_max = env ? atoi(env) : 0;
   const Py_ssize_t by_size = n / 2048 + 1;
-  return (int)std::max<Py_ssize_t>(
-      1, std::min<Py_ssize_t>({(Py_ssize_t)cpu_budget(), (Py_ssize_t)kMaxScanThreads, by_size}));
+  const Py_ssize_t cap = env_max > 0 ? (Py_ssize_t)env_max : (Py_ssize_t)kMaxScanThreads;
+  return (int)std::max<Py_ssize_t>(1, std::min<Py_ssize_t>({(Py_ssize_t)cpu_budget(), cap, by_size}));
 }
 
 // Host workers of the scan and the pack: the calling thread (worker 0, left

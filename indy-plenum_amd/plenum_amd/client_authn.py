@@ -46,6 +46,7 @@ authenticators (names from BASELINE.json's north star).
 """
 import copy
 import threading
+import os
 from abc import abstractmethod
 from collections import OrderedDict, deque
 from time import monotonic
@@ -772,7 +773,7 @@ class GpuAuthMixin:
                 and spans_buf is not None and kid_buf is not None and getattr(eng, "supports_staged_parts", False)):
             ks_version = ks.version
             parts = eng.verify_staged_begin(True, n)
-            spec = (g.kid_map, kid_buf, eng.parter(), _PART_ITEMS)
+            spec = (g.kid_map, kid_buf, eng.parter(), int(os.environ.get("EDV_PART_ITEMS", _PART_ITEMS)))
         t0 = perf_counter()
         try:
             scan = _scan_batch(msgs, [SIG], g.scan_threads, [bufs[0], bufs[1], spans_buf], slot, 2, eng.stager(),
