@@ -1138,6 +1138,29 @@ PyObject* py_kid_map_size(PyObject*, PyObject* cap) {
   return m ? PyLong_FromSize_t(m->used) : nullptr;
 }
 
+// Writes into the engine's pinned memory that only the DMA reads back: non-temporal stores
+// (no read-for-ownership of the destination lines, nothing evicted from the worker's cache).
+// The caller fences (_mm_sfence) before publishing what it wrote to another thread.
+bool g_scan_nt = true;  // EDV_SCAN_NT=0: ordinary stores (A/B); set per scan call
+inline void nt_slot96(char* dst, const unsigned char* text, size_t n) {  // dst 16-byte aligned, n <= 95
+  alignas(16) char b[96];
+  memcpy(b, text, n);
+  memset(b + n, 0, 95 - n);
+  b[95] = (char)n;
+  for (int k = 0; k < 6; ++k) _mm_stream_si128((__m128i*)(dst + 16 * k), _mm_load_si128((const __m128i*)(b + 16 * k)));
+}
+inline void nt_copy(char* dst, const char* src, size_t n) {
+  const size_t head = (size_t)((16 - ((uintptr_t)dst & 15)) & 15);
+  if (n < head + 32) {
+    memcpy(dst, src, n);
+    return;
+  }
+  memcpy(dst, src, head);
+  dst += head, src += head, n -= head;
+  for (; n >= 16; dst += 16, src += 16, n -= 16) _mm_stream_si128((__m128i*)dst, _mm_loadu_si128((const __m128i*)src));
+  memcpy(dst, src, n);
+}
+
 struct ScanItem {
   PyObject* m = nullptr;
   const unsigned char* sp = nullptr;
@@ -1669,6 +1692,7 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
     const uint64_t pos = got & ((1ull << kSeqShift) - 1);
     if (copier.chunk_seq) copier.chunk_seq[(size_t)(a / kStageChunk)].store((uint32_t)seq, std::memory_order_relaxed);
     if (pos + total > smsg_cap) {
+      if (g_scan_nt) _mm_sfence();
       staged_ok = false;  // the buffer was sized from earlier batches: the caller re-scans unstaged
       copier.res_end[seq].store(pos + 1, std::memory_order_release);  // (nothing of it is copied)
       copier.slot_done[(size_t)(a / kStageChunk)].store(1, std::memory_order_release);
@@ -1682,7 +1706,10 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
       char* ds = dsig + (size_t)i * sig_slot;
       st0[i] = en0[i] = at;
       if (x.state == 1 && x.text) {  // the slot was written in the item loop
-        memcpy(smsg + at, sb.ser.data() + x.ser_at, x.ser_len);
+        if (g_scan_nt)
+          nt_copy(smsg + at, sb.ser.data() + x.ser_at, x.ser_len);
+        else
+          memcpy(smsg + at, sb.ser.data() + x.ser_at, x.ser_len);
         at += x.ser_len;
         en0[i] = at;
         continue;
@@ -1708,6 +1735,7 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
       at += ls + lm - 64;
       en0[i] = at;
     }
+    if (g_scan_nt) _mm_sfence();  // the chunk's non-temporal stores before the copier sees the chunk
     copier.res_end[seq].store(pos + total + 1, std::memory_order_release);
     copier.slot_done[(size_t)(a / kStageChunk)].store(1, std::memory_order_release);
   };
@@ -1744,6 +1772,10 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
   const bool prefetch = !(pf_env && pf_env[0] == '0');
   const char* dir_env = getenv("EDV_SCAN_DIRECT");
   g_scan_direct = !(dir_env && dir_env[0] == '0');
+  // non-temporal stores for what only the DMA reads: the staged scan's slots and messages
+  const char* nt_env = getenv("EDV_SCAN_NT");
+  g_scan_nt = staged && !(nt_env && nt_env[0] == '0');
+  const bool nt_slots = g_scan_nt;
   run_chunks(n, t, [&](int w, Py_ssize_t a, Py_ssize_t b) {
     ScanBuf& sb = bufs[(size_t)w];
     WorkerIdrs& tab = tabs[(size_t)w];
@@ -1807,9 +1839,13 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
         x.text = 1;
         x.sig_len = 64;
         char* ds = dsig + (size_t)i * sig_slot;  // slot: the text, zero padding, its length in the last byte
-        memcpy(ds, x.sp, (size_t)x.ns);
-        memset(ds + x.ns, 0, (size_t)sig_slot - 1 - (size_t)x.ns);
-        ds[sig_slot - 1] = (char)x.ns;
+        if (nt_slots && ((uintptr_t)ds & 15) == 0) {
+          nt_slot96(ds, x.sp, (size_t)x.ns);
+        } else {
+          memcpy(ds, x.sp, (size_t)x.ns);
+          memset(ds + x.ns, 0, (size_t)sig_slot - 1 - (size_t)x.ns);
+          ds[sig_slot - 1] = (char)x.ns;
+        }
       } else {
         x.sig_at = sb.sig.size();
         x.sig_len = (uint32_t)sig.size();

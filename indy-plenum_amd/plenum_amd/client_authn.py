@@ -770,6 +770,7 @@ class GpuAuthMixin:
         ks = self._key_store()
         spec, parts = None, None
         if (not defer and g.speculate and g.kid_map is not None and ks is not None and _kid_map is not None
+                and os.environ.get("EDV_SPECULATE", "1") != "0"
                 and spans_buf is not None and kid_buf is not None and getattr(eng, "supports_staged_parts", False)):
             ks_version = ks.version
             parts = eng.verify_staged_begin(True, n)

@@ -18,7 +18,7 @@ from plenum_amd.client_authn import GpuAuthNr  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 4
-modes = (sys.argv[3] if len(sys.argv) > 3 else "stream,stage").split(",")
+modes = (sys.argv[3] if len(sys.argv) > 3 else "stream,stage").replace("+", ",").split(",")
 eng = EdVerifyEngine(0)
 reqs, idrs, vks = bench.e2e_requests(eng, n, 1000, 43)
 auths = {}
