@@ -1009,8 +1009,10 @@ struct IdrTable {
   }
   // the id of text (p, n), or `next` (fresh = true) when it is new
   uint32_t find_or_add(const char* p, size_t n, uint32_t next, bool& fresh) {
+    return find_or_add_h(hash(p, n), p, n, next, fresh);
+  }
+  uint32_t find_or_add_h(uint64_t h, const char* p, size_t n, uint32_t next, bool& fresh) {  // h = hash(p, n)
     if (2 * (used + 1) > e.size()) grow();
-    const uint64_t h = hash(p, n);
     for (size_t s = h & mask;; s = (s + 1) & mask) {
       E& x = e[s];
       if (!x.p) {
@@ -1616,6 +1618,7 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
     std::vector<PyObject*> obj;
     std::vector<uint32_t> kid;      // speculation: the key id of each of its identifiers (kmap)
     std::vector<Py_ssize_t> first;  // the item where the worker met it first
+    std::vector<uint64_t> hash;     // IdrTable::hash of each of its identifiers (the merge's partitions)
     size_t deferred = 0;            // items left for the GIL pass (3)
 #ifdef EDV_HAVE_DK
     std::unique_ptr<ShapeCache> shapes;  // this call's remembered dict shapes (shaped_dict)
@@ -1858,6 +1861,7 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
       if (fresh) {
         tab.obj.push_back(iv);
         tab.first.push_back(i);
+        tab.hash.push_back(IdrTable::hash((const char*)PyUnicode_1BYTE_DATA(iv), (size_t)PyUnicode_GET_LENGTH(iv)));
         if (kmap) tab.kid.push_back(kmap->get((const char*)PyUnicode_1BYTE_DATA(iv), (size_t)PyUnicode_GET_LENGTH(iv)));
       }
       if (kid_out) kid_out[i] = tab.kid[x.uid];
@@ -1880,28 +1884,75 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
   size_t deferred = 0;
   for (const WorkerIdrs& w : tabs) deferred += w.deferred;
   {
+    // partitioned by identifier hash, one partition per worker, merged side by side: each
+    // partition keeps its identifiers' earliest first occurrence (every worker's table holds most
+    // of a batch's identifiers, so a serial merge compared ~t x distinct texts on one thread); then
+    // the distinct identifiers are numbered in order of first occurrence
+    const int P = t;
+    struct Part {
+      IdrTable tab;
+      std::vector<PyObject*> obj;
+      std::vector<Py_ssize_t> first;
+      std::vector<uint32_t> kid;
+      std::vector<uint32_t> gid;
+    };
+    std::vector<Part> parts((size_t)P);
+    for (int w = 0; w < t; ++w) to_global[(size_t)w].resize(tabs[(size_t)w].obj.size());
+    run_chunks(P, P, [&](int, Py_ssize_t a, Py_ssize_t b) {
+      for (Py_ssize_t p = a; p < b; ++p) {
+        Part& pt = parts[(size_t)p];
+        pt.tab.reset(tabs.empty() ? 64 : tabs[0].obj.size() / (size_t)P + 64);
+        for (int w = 0; w < t; ++w) {
+          const WorkerIdrs& tb = tabs[(size_t)w];
+          for (size_t u = 0; u < tb.obj.size(); ++u) {
+            const uint64_t h = tb.hash[u];
+            if ((Py_ssize_t)(h % (uint64_t)P) != p) continue;
+            PyObject* o = tb.obj[u];
+            bool fresh = false;
+            const uint32_t l = pt.tab.find_or_add_h(h, (const char*)PyUnicode_1BYTE_DATA(o),
+                                                     (size_t)PyUnicode_GET_LENGTH(o), (uint32_t)pt.obj.size(), fresh);
+            if (fresh) {
+              pt.obj.push_back(o);
+              pt.first.push_back(tb.first[u]);
+              if (kmap) pt.kid.push_back(tb.kid[u]);  // (the map's id for this text: the same in every worker)
+            } else if (tb.first[u] < pt.first[l]) {
+              pt.first[l] = tb.first[u];
+              pt.obj[l] = o;  // the object of its first occurrence, as a serial scan returns it
+            }
+            to_global[(size_t)w][u] = l;  // partition-local for now
+          }
+        }
+      }
+    }, 1);
     struct Cand {
       Py_ssize_t first;
-      int w;
+      int p;
       uint32_t local;
     };
     std::vector<Cand> cand;
-    for (int w = 0; w < t; ++w) {
-      const WorkerIdrs& tb = tabs[(size_t)w];
-      to_global[(size_t)w].resize(tb.obj.size());
-      for (size_t u = 0; u < tb.obj.size(); ++u) cand.push_back(Cand{tb.first[u], w, (uint32_t)u});
+    for (int p = 0; p < P; ++p) {
+      Part& pt = parts[(size_t)p];
+      pt.gid.resize(pt.obj.size());
+      for (size_t l = 0; l < pt.obj.size(); ++l) cand.push_back(Cand{pt.first[l], p, (uint32_t)l});
     }
     std::sort(cand.begin(), cand.end(), [](const Cand& a, const Cand& b) { return a.first < b.first; });
+    uniq.reserve(cand.size());
     for (const Cand& c : cand) {
-      PyObject* o = tabs[(size_t)c.w].obj[c.local];
+      Part& pt = parts[(size_t)c.p];
+      pt.gid[c.local] = (uint32_t)uniq.size();
+      uniq.push_back(pt.obj[c.local]);
+      if (kmap) spec_u.push_back(pt.kid[c.local]);
+    }
+    for (int w = 0; w < t; ++w) {
+      const WorkerIdrs& tb = tabs[(size_t)w];
+      std::vector<uint32_t>& tg = to_global[(size_t)w];
+      for (size_t u = 0; u < tg.size(); ++u) tg[u] = parts[(size_t)(tb.hash[u] % (uint64_t)P)].gid[tg[u]];
+    }
+    // the GIL pass (3) below adds the deferred items' identifiers to this table
+    for (size_t g = 0; deferred && g < uniq.size(); ++g) {
       bool fresh = false;
-      const uint32_t g = slot.find_or_add((const char*)PyUnicode_1BYTE_DATA(o), (size_t)PyUnicode_GET_LENGTH(o),
-                                          (uint32_t)uniq.size(), fresh);
-      if (fresh) {
-        uniq.push_back(o);
-        if (kmap) spec_u.push_back(tabs[(size_t)c.w].kid[c.local]);
-      }
-      to_global[(size_t)c.w][c.local] = g;
+      slot.find_or_add((const char*)PyUnicode_1BYTE_DATA(uniq[g]), (size_t)PyUnicode_GET_LENGTH(uniq[g]),
+                       (uint32_t)g, fresh);
     }
   }
   // (the items' worker-local ids are mapped in (4), on the workers)
