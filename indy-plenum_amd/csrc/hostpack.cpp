@@ -2073,14 +2073,16 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
     }
     PyObject* parts_ok = part_fn && !copier.part_failed && copier.next_part * part_items >= (uint64_t)n ? Py_True
                                                                                                       : Py_False;
+    // staged_bytes: the message bytes the chunks reserved (the largest span end; sizes the next buffer)
+    const unsigned long long staged_bytes = scursor.load() & ((1ull << kSeqShift) - 1);
     if (spans_p != S.spans.data())  // written in place: the caller's buffer is the result
-      return Py_BuildValue("(y#y#NOOOy#ONO)", fast.data(), (Py_ssize_t)n, (const char*)uidx.data(),
+      return Py_BuildValue("(y#y#NOOOy#ONOK)", fast.data(), (Py_ssize_t)n, (const char*)uidx.data(),
                            (Py_ssize_t)(uidx.size() * 4), ul, o_sig, out_msg, out_spans, shortv.data(), (Py_ssize_t)n,
-                           staged_ok.load() ? Py_True : Py_False, su, parts_ok);
-    return Py_BuildValue("(y#y#NOOy#y#ONO)", fast.data(), (Py_ssize_t)n, (const char*)uidx.data(),
+                           staged_ok.load() ? Py_True : Py_False, su, parts_ok, staged_bytes);
+    return Py_BuildValue("(y#y#NOOy#y#ONOK)", fast.data(), (Py_ssize_t)n, (const char*)uidx.data(),
                          (Py_ssize_t)(uidx.size() * 4), ul, o_sig, out_msg, (const char*)S.spans.data(),
                          (Py_ssize_t)(S.spans.size() * 8), shortv.data(), (Py_ssize_t)n,
-                         staged_ok.load() ? Py_True : Py_False, su, parts_ok);
+                         staged_ok.load() ? Py_True : Py_False, su, parts_ok, staged_bytes);
   }
   PyObject* o_msg = refs.o_msg = out_buffer(out_msg, (Py_ssize_t)off[(size_t)n], &dmsg);
   PyObject* ret = nullptr;

@@ -787,7 +787,7 @@ class GpuAuthMixin:
                     except Exception:
                         pass
             raise
-        fast_b, uidx_b, uniq, sig_o, msg_o, spans_b, short, staged_ok, spec_u, parts_ok = scan
+        fast_b, uidx_b, uniq, sig_o, msg_o, spans_b, short, staged_ok, spec_u, parts_ok, staged_bytes = scan
         if parts is not None:  # the parts' verdict copy queued after the last part
             try:
                 eng.verify_staged_end()
@@ -808,8 +808,8 @@ class GpuAuthMixin:
             drop_parts()
             g.msg_bytes_per_item *= 1.5  # the next buffers are sized larger
             return None
-        # (the chunks' reservations are contiguous from 0: the largest end is the bytes staged)
-        g.msg_bytes_per_item = max(g.msg_bytes_per_item * 0.5, float(me.max()) / n if n else 0.0)
+        # (the chunks' reservations are contiguous from 0: their total is the largest span end)
+        g.msg_bytes_per_item = max(g.msg_bytes_per_item * 0.5, float(staged_bytes) / n if n else 0.0)
         ukeys = self._keys_for(uniq)  # authenticate():93-99, once per identifier
         ids = None
         if ks is not None and fast_b.count(0) == 0 and all(k.__class__ is bytes for k in ukeys):
