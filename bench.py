@@ -164,6 +164,10 @@ def parse():
     ap.add_argument("--drain-n", type=int, default=40,
                     help="drains of the end_to_end.node_drain leg (100 REQUESTs + 24 BATCHes of PROPAGATEs each; "
                          "0 = skip)")
+    ap.add_argument("--churn-signers", type=int, default=100_000,
+                    help="signers of the end_to_end.key_churn leg (all registered with addIdr; 0 = skip)")
+    ap.add_argument("--churn-requests", type=int, default=1_000_000,
+                    help="requests of the key_churn leg (4 batches, Zipf-distributed signers)")
     ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--force-dist", action="store_true",
                     help="run the N > 1 exchange path (process group, all-gather, all-reduce) even at N = 1")
@@ -491,6 +495,78 @@ def time_node_drain(eng, reqs, idrs, vks, drains=40, per_drain=100, n_nodes=25, 
                    "authenticate() chain over libsodium (oracle/ref_authn_port.py --drain)" % (per_drain, n_nodes - 1,
                                                                                             n_nodes))
     return out
+
+
+def time_key_churn(eng, signers=100_000, n=1_000_000, batches=4, zipf=1.1, seed_offset=1 << 20):
+    """end_to_end.key_churn: a domain ledger's signer population through
+    GpuAuthNr -- `signers` NYM owners all registered with addIdr
+    (node.py:2476-2494), far more than the key store's max_keys slots, and
+    requests whose signers follow a Zipf(zipf) law (synth.zipf_signers), in
+    `batches` batches of n / batches json-decoded requests (0.5 % forged).
+    Keys that verified hot_key_uses requests on the general path earn a slot
+    and evict the least-recently-used (asynchronous table builds), so each
+    batch reports its rate, its keyed / general shares and the registrations
+    it triggered.  Every outcome is checked after the clock."""
+    from plenum_amd import _hostpack
+    from plenum_amd.base58 import b58encode
+    from plenum_amd.client_authn import GpuAuthNr
+    pks, sks = eng.seed_keypair_batch(synth.signer_seeds(seed_offset + signers)[seed_offset:])
+    idrs = [b58encode(bytes(pk[:16])) for pk in pks]
+    vks = ["~" + b58encode(bytes(pk[16:])) for pk in pks]
+    kidx = synth.zipf_signers(n, signers, zipf)
+    msgs, spec = synth.churn_messages(kidx, idrs, alias_len=43, req_id_base=synth.REQ_ID_BASE + (1 << 40))
+    buf, off = pack_messages(msgs)
+    del msgs
+    sig = eng.sign_batch(sks, kidx, buf, off)
+    sig_b58 = _hostpack.b58encode_rows(np.ascontiguousarray(sig).tobytes(), 64)
+    del sig, buf, off
+    dumps, loads = json.dumps, json.loads
+    reqs = []
+    for i in range(n):
+        r = synth.churn_request_dict(spec, i)
+        if i % 200 == 7:
+            r["reqId"] += 1  # forged after signing
+        r["signature"] = sig_b58[i]
+        reqs.append(loads(dumps(r)))
+    del sig_b58
+    a = GpuAuthNr(engine=eng)
+    t0 = time.perf_counter()
+    for idr, vk in zip(idrs, vks):
+        a.addIdr(idr, vk)
+    a.keys_settle()  # genesis: the free slots take addIdr keys
+    genesis_s = time.perf_counter() - t0
+    per = n // batches
+    out_b = []
+    total = 0.0
+    bad = 0
+    for b in range(batches):
+        chunk = reqs[b * per:(b + 1) * per]
+        st0 = dict(a.stats)
+        t0 = time.perf_counter()
+        res = a.authenticate_batch(chunk)
+        el = time.perf_counter() - t0
+        total += el
+        st1 = dict(a.stats)
+        for j, (r, m) in enumerate(zip(res, chunk)):
+            forged = (b * per + j) % 200 == 7
+            bad += (type(r).__name__ != "InvalidSignature") if forged else (r != m["identifier"])
+        del res
+        items = st1["batch_items"] - st0["batch_items"]
+        keyed = st1["keyed_items"] - st0["keyed_items"]
+        out_b.append({"requests": per, "value": per / el, "ms": el * 1e3,
+                      "distinct_signers": int(len(np.unique(kidx[b * per:(b + 1) * per]))),
+                      "keyed_share": keyed / max(1, items), "general_share": 1 - keyed / max(1, items),
+                      "registrations": st1["keys_registered"] - st0["keys_registered"],
+                      "speculated": bool((a._g.last_breakdown or {}).get("speculated"))})
+    ks = a._key_store()
+    return {"signers": signers, "zipf_s": zipf, "requests": per * batches, "batches": out_b,
+            "value": per * batches / total, "mismatches": int(bad), "key_slots": ks.capacity if ks else 0,
+            "key_window": a._g.key_window, "genesis_addidr_and_builds_s": genesis_s,
+            "note": "%d signers registered with addIdr (more than the %d key slots), requests' signers Zipf(%.1f), "
+                    "%d batches of %d json-decoded requests, 0.5%% forged; keys earn slots by verified use "
+                    "(hot_key_uses) and evict the least-recently-used, tables built asynchronously; value = "
+                    "requests / summed batch seconds; mismatches = outcomes != the construction's (checked after "
+                    "the clock)" % (signers, ks.capacity if ks else 0, zipf, batches, per)}
 
 
 def time_e2e_devices(eng, reqs, idrs, vks, counts):
@@ -1057,6 +1133,10 @@ def main():
             del reqs
         if args.bls_checks > 0:
             e2e["bls_commit_round"] = time_bls_commit_round(eng, args.bls_checks)
+        if args.churn_signers > 0:
+            e2e["key_churn"] = time_key_churn(eng, args.churn_signers, args.churn_requests)
+            if e2e["key_churn"]["mismatches"]:
+                lib_mis += e2e["key_churn"]["mismatches"]
 
     # the metric's "whole node" reading: GpuAuthNr.authenticate_batch over json-decoded request dicts
     # (host scan + PCIe + kernels + result list, one node process), beside the same run's libsodium

@@ -61,6 +61,38 @@ def nym_messages(n, signer_pks, alias_len=0, seed=1, req_id_base=REQ_ID_BASE, po
     return msgs, key_idx, spec
 
 
+def zipf_signers(n, n_signers, s=1.1, seed=17):
+    """The signer of each of n requests under a Zipf(s) popularity law over
+    n_signers (the signer of rank r drawn with weight r^-s; ranks assigned
+    to signers in a random order): a domain ledger's long tail of NYM
+    owners, a few of them very active."""
+    rng = np.random.default_rng(seed)
+    w = np.arange(1, n_signers + 1, dtype=np.float64) ** -s
+    ranks = rng.choice(n_signers, size=n, p=w / w.sum())
+    return rng.permutation(n_signers).astype(np.uint32)[ranks]
+
+
+def churn_messages(key_idx, idrs, alias_len=43, seed=1, req_id_base=REQ_ID_BASE, pool=4096):
+    """NYM requests signed by signers key_idx[i] (identifiers idrs[k]): the
+    signing bytes of each (nym_messages' format) and a spec for its dict
+    (churn_request_dict)."""
+    rng = np.random.default_rng(seed)
+    dests = _pool(rng, pool, 16)
+    vks = ["~" + v for v in _pool(rng, pool, 16)]
+    alias = "".join(rng.choice(list("abcdefghijklmnopqrstuvwxyz0123456789"), size=alias_len)) if alias_len else None
+    op_prefix = "operation:alias:%s|" % alias if alias is not None else "operation:"
+    msgs = [("identifier:%s|%sdest:%s|type:1|verkey:%s|protocolVersion:1|reqId:%d" % (
+        idrs[k], op_prefix, dests[i % pool], vks[(i * 7) % pool], req_id_base + i)).encode()
+        for i, k in enumerate(key_idx.tolist())]
+    spec = dict(idrs=idrs, key_idx=key_idx, dests=dests, vks=vks, alias=alias, pool=pool, req_id_base=req_id_base)
+    return msgs, spec
+
+
+def churn_request_dict(spec, i):
+    return nym_request(spec["idrs"][int(spec["key_idx"][i])], spec["req_id_base"] + i,
+                       spec["dests"][i % spec["pool"]], spec["vks"][(i * 7) % spec["pool"]], spec["alias"])
+
+
 def nym_request_dict(spec, i, n_signers):
     return nym_request(spec["idrs"][i % n_signers], spec["req_id_base"] + i, spec["dests"][i % spec["pool"]],
                        spec["vks"][(i * 7) % spec["pool"]], spec["alias"])

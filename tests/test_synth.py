@@ -52,3 +52,18 @@ def test_lengths_mixed_rule():
     lens[0] = blk3
     off = np.concatenate([[0], np.cumsum(lens)])
     assert lengths_mixed(off[:-1], off[1:])  # 64*3 = 192 > 1.25 * 129
+
+
+def test_churn_messages_are_the_serialized_dicts():
+    """synth.churn_messages' signing bytes == serialize_msg_for_signing of the
+    dict churn_request_dict rebuilds; Zipf signers: a long tail and a head."""
+    from plenum_amd import synth
+    from plenum_amd.serialization import serialize_msg_for_signing
+    kidx = synth.zipf_signers(5000, 2000, 1.1, seed=3)
+    counts = np.bincount(kidx, minlength=2000)
+    assert counts.max() > 200 and (counts == 0).sum() > 500  # a few hot signers, many never seen
+    idrs = ["Idr%05d" % k for k in range(2000)]
+    msgs, spec = synth.churn_messages(kidx, idrs, alias_len=43)
+    for i in range(0, 5000, 97):
+        assert serialize_msg_for_signing(synth.churn_request_dict(spec, i), topLevelKeysToIgnore=["signature"]) == \
+            msgs[i]
