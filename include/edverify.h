@@ -194,6 +194,11 @@ int edv_keys_set(edv_ctx *ctx, uint64_t first_id, const uint8_t *pk32, uint64_t 
  * addIdr path (SimpleAuthNr keeps its dict; the tables are this library's). */
 int edv_keys_add_async(edv_ctx *ctx, const uint8_t *pk32, uint64_t nkeys, uint64_t *first_id, uint64_t *ticket);
 int edv_keys_set_async(edv_ctx *ctx, uint64_t first_id, const uint8_t *pk32, uint64_t nkeys, uint64_t *ticket);
+/* edv_keys_set_async for scattered slots: key ids[k] (distinct, registered) becomes pk32[k], all
+ * nkeys in one upload (through the library's pinned staging: the host returns without waiting for
+ * the builds already queued) and one build launch -- the key store's evictions of a batch. */
+int edv_keys_set_many_async(edv_ctx *ctx, const uint32_t *ids, const uint8_t *pk32, uint64_t nkeys,
+                            uint64_t *ticket);
 /* 1 when every build up to `ticket` has finished, 0 while one still runs, < 0 on error. */
 int edv_keys_ready(edv_ctx *ctx, uint64_t ticket);
 /* Wait for every queued build. */

@@ -676,16 +676,26 @@ constexpr int kRowWords = 40;
 
 // One lane per key: decode -A, libsodium's key checks, the row bases.
 template <int W>
+// ids (edv_keys_set_many_async): key k of the launch is store slot ids[k]; its encoding is
+// pk32[k] and is also copied to store_pk[ids[k]] (valid and store_pk indexed by slot); null ids:
+// slots are consecutive and pk32 / valid already point at the first
 __global__ __launch_bounds__(kBlock) void edv_key_rows_kernel(const uint8_t* __restrict__ pk32, uint64_t nkeys,
                                                              uint32_t* __restrict__ rows,
-                                                             uint8_t* __restrict__ valid) {
+                                                             uint8_t* __restrict__ valid,
+                                                             const uint32_t* __restrict__ ids = nullptr,
+                                                             uint8_t* __restrict__ store_pk = nullptr) {
   const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= nkeys) return;
   uint32_t pk[8];
   load_words(pk, pk32 + 32 * k, 8);
+  const uint64_t slot = ids ? ids[k] : k;
+  if (ids) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ((uint32_t*)(store_pk + 32 * slot))[j] = pk[j];
+  }
   ge_p3 P;
   const bool dec = ge_frombytes(P, pk, true);
-  valid[k] = (dec && is_canonical_point(pk) && !has_small_order(pk)) ? 1 : 0;
+  valid[slot] = (dec && is_canonical_point(pk) && !has_small_order(pk)) ? 1 : 0;
   comb_rows<W>(rows + k * Window<W>::kRows * kRowWords, P);
 }
 
@@ -703,14 +713,16 @@ struct FillShape {
 template <int W>
 __global__ __launch_bounds__(kBlock) void edv_comb_fill_kernel(const uint32_t* __restrict__ rows, uint64_t nrows,
                                                               uint32_t* __restrict__ tab, uint32_t* __restrict__ pre,
-                                                              uint64_t key0, uint64_t cap) {
+                                                              uint64_t key0, uint64_t cap,
+                                                              const uint32_t* __restrict__ ids = nullptr) {
   using F = FillShape<W>;
   const uint64_t nl = nrows * F::NCH;
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= nl) return;
   const uint64_t r = g / F::NCH;
   const int c = (int)(g % F::NCH);
-  const uint64_t row = r % Window<W>::kRows, k = key0 + r / Window<W>::kRows;
+  const uint64_t row = r % Window<W>::kRows,
+                 k = ids ? (uint64_t)ids[key0 + r / Window<W>::kRows] : key0 + r / Window<W>::kRows;
   comb_fill_strided(tab + (row * cap + k) * F::E * kEntryWords, pre + g * 10, nl * 10, rows + r * kRowWords, c,
                     F::NCH, F::CH);
 }
@@ -1449,6 +1461,12 @@ struct edv_ctx {
   // stream_build with scratch of their own; build k records builds[k].ev; tickets complete in order
   hipStream_t stream_build = nullptr;
   Buf b_build;
+  // edv_keys_set_many_async: ids + encodings through pinned staging (a ring of kManyRing, each reused
+  // after its copy's event) into device buffers the builds read (one per ring entry)
+  static constexpr int kManyRing = 4;
+  Buf h_many[kManyRing], d_many[kManyRing];
+  hipEvent_t ev_many[kManyRing] = {};
+  int many_next = 0;
   struct BuildEv {
     uint64_t ticket;
     hipEvent_t ev;
@@ -1969,6 +1987,33 @@ static int keys_build_w(edv_ctx* ctx, uint64_t first, uint64_t nkeys, hipStream_
   return 0;
 }
 
+// Tables for keys d_pk[0 .. nkeys) (device) into store slots d_ids[0 .. nkeys) (device, distinct), their
+// encodings copied into the store too: edv_keys_set_many_async.
+template <int W>
+static int keys_build_ids_w(edv_ctx* ctx, const uint8_t* d_pk, const uint32_t* d_ids, uint64_t nkeys, hipStream_t st,
+                            edv_ctx::Buf& aux) {
+  constexpr int R = Window<W>::kRows, E = Window<W>::kEntries;
+  constexpr uint64_t per_key = (uint64_t)R * kRowWords * 4 + (uint64_t)R * E * 10 * 4;
+  const uint64_t max_slice = kKeyBuildScratch / per_key > 0 ? kKeyBuildScratch / per_key : 1;
+  const uint64_t slice = nkeys < max_slice ? nkeys : max_slice;
+  const size_t need = slice * R * kRowWords * 4 + slice * R * E * 10 * 4;
+  if (aux.cap < need) HIP_TRY(hipStreamSynchronize(st));
+  int r;
+  if ((r = ensure(aux, need))) return r;
+  uint32_t* rows = (uint32_t*)aux.p;
+  uint32_t* pre = rows + slice * R * kRowWords;
+  for (uint64_t k0 = 0; k0 < nkeys; k0 += slice) {
+    const uint64_t kn = nkeys - k0 < slice ? nkeys - k0 : slice;
+    hipLaunchKernelGGL(edv_key_rows_kernel<W>, dim3((uint32_t)div_up(kn, kBlock)), dim3(kBlock), 0, st, d_pk + 32 * k0,
+                       kn, rows, ctx->d_key_valid, d_ids + k0, ctx->d_key_pk);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(edv_comb_fill_kernel<W>, dim3((uint32_t)div_up(kn * R * FillShape<W>::NCH, kBlock)),
+                       dim3(kBlock), 0, st, rows, kn * R, ctx->d_key_tab, pre, (uint64_t)0, ctx->key_cap, d_ids + k0);
+    HIP_TRY(hipGetLastError());
+  }
+  return 0;
+}
+
 static int keys_build(edv_ctx* ctx, uint64_t first, uint64_t nkeys, hipStream_t st) {
   if (!nkeys) return 0;
   edv_ctx::Buf& aux = st == ctx->stream_build ? ctx->b_build : ctx->b_aux;
@@ -2374,6 +2419,61 @@ int edv_keys_set_async(edv_ctx* ctx, uint64_t first_id, const uint8_t* pk32, uin
     HIP_TRY(hipMemcpyAsync(ctx->d_key_pk + 32 * first_id, pk32, 32 * nkeys, hipMemcpyHostToDevice,
                            ctx->stream_build));
     if ((r = keys_build(ctx, first_id, nkeys, ctx->stream_build))) return r;
+  }
+  return build_ticket(ctx, ticket);
+}
+
+int edv_keys_set_many_async(edv_ctx* ctx, const uint32_t* ids, const uint8_t* pk32, uint64_t nkeys,
+                            uint64_t* ticket) {
+  int r = set_device(ctx);
+  if (r) return r;
+  if (nkeys && (!ids || !pk32)) return set_err(EDV_EINVAL, "null pointer");
+  for (uint64_t k = 0; k < nkeys; ++k)
+    if (ids[k] >= ctx->key_count)
+      return set_err(EDV_EINVAL, "key id %u outside the %llu registered", ids[k], (unsigned long long)ctx->key_count);
+  {  // distinct ids: two builds of one slot in one launch would race
+    std::vector<uint32_t> sorted(ids, ids + nkeys);
+    std::sort(sorted.begin(), sorted.end());
+    for (uint64_t k = 1; k < nkeys; ++k)
+      if (sorted[k] == sorted[k - 1]) return set_err(EDV_EINVAL, "key id %u twice", sorted[k]);
+  }
+  if (nkeys) {
+    const int slot = ctx->many_next;
+    ctx->many_next = (slot + 1) % edv_ctx::kManyRing;
+    edv_ctx::Buf &hb = ctx->h_many[slot], &db = ctx->d_many[slot];
+    const uint64_t bytes = 36 * nkeys;  // encodings, then ids
+    if (ctx->ev_many[slot]) HIP_TRY(hipEventSynchronize(ctx->ev_many[slot]));  // its last copy has read hb
+    else HIP_TRY(hipEventCreateWithFlags(&ctx->ev_many[slot], hipEventDisableTiming));
+    if ((r = ensure_pinned(hb, bytes))) return r;
+    if (db.cap < bytes) {  // a build queued earlier may still read the old device buffer
+      HIP_TRY(hipStreamSynchronize(ctx->stream_build));
+      if ((r = ensure(db, bytes))) return r;
+    }
+    memcpy(hb.p, pk32, 32 * nkeys);
+    memcpy((uint8_t*)hb.p + 32 * nkeys, ids, 4 * nkeys);
+    // the rebuild starts after the work already queued on the context's streams (verifies that may
+    // still read these slots' old tables); the host does not wait
+    hipStream_t qs[4] = {ctx->stream, ctx->stream2, ctx->stream_copy, ctx->stream_key};
+    for (int k = 0; k < 4; ++k) {
+      HIP_TRY(hipEventRecord(ctx->ev_fence[k], qs[k]));
+      HIP_TRY(hipStreamWaitEvent(ctx->stream_build, ctx->ev_fence[k], 0));
+    }
+    HIP_TRY(hipMemcpyAsync(db.p, hb.p, bytes, hipMemcpyHostToDevice, ctx->stream_build));
+    HIP_TRY(hipEventRecord(ctx->ev_many[slot], ctx->stream_build));
+    const uint8_t* d_pk = (const uint8_t*)db.p;
+    const uint32_t* d_ids = (const uint32_t*)(d_pk + 32 * nkeys);
+    edv_ctx::Buf& aux = ctx->b_build;
+#define EDV_MANY_CASE(W)                                                                  \
+  case W:                                                                                 \
+    r = keys_build_ids_w<W>(ctx, d_pk, d_ids, nkeys, ctx->stream_build, aux);            \
+    break;
+    switch (ctx->key_w) {
+      EDV_KEY_WINDOWS(EDV_MANY_CASE)
+      default:
+        return set_err(EDV_EINVAL, "key window %d", ctx->key_w);
+    }
+#undef EDV_MANY_CASE
+    if (r) return r;
   }
   return build_ticket(ctx, ticket);
 }
@@ -2917,6 +3017,11 @@ void edv_destroy(edv_ctx* ctx) {
     if (ctx->ev_sdone[k]) (void)hipEventDestroy(ctx->ev_sdone[k]);
   }
   for (edv_ctx::BuildEv& b : ctx->builds) (void)hipEventDestroy(b.ev);
+  for (int k = 0; k < edv_ctx::kManyRing; ++k) {
+    free_buf(ctx->h_many[k]);
+    free_buf(ctx->d_many[k]);
+    if (ctx->ev_many[k]) (void)hipEventDestroy(ctx->ev_many[k]);
+  }
   for (hipEvent_t f : ctx->ev_fence)
     if (f) (void)hipEventDestroy(f);
   for (int k = 0; k < edv_ctx::kSlots; ++k) {

@@ -52,6 +52,7 @@ SIGNATURES = {
     "edv_keys_set": (_I, [_P, _U64, _P, _U64]),
     "edv_keys_add_async": (_I, [_P, _P, _U64, _P, _P]),
     "edv_keys_set_async": (_I, [_P, _U64, _P, _U64, _P]),
+    "edv_keys_set_many_async": (_I, [_P, _P, _P, _U64, _P]),
     "edv_keys_ready": (_I, [_P, _U64]),
     "edv_keys_sync": (_I, [_P]),
     "edv_keys_count": (_U64, [_P]),

@@ -182,7 +182,8 @@ class _GpuState:
     def __init__(self, engine=None, device=0, devices=None, verdict_cache_size=1 << 20,
                  verdict_cache_bytes=256 << 20, verdict_max_age=300.0, key_window="auto",
                  max_keys=16384, hot_key_uses=2, key_store_bytes=KEY_STORE_BYTES, scan_threads=0,
-                 pipeline_part=0, async_key_builds=True, stream=True, stage=True, speculate=True):
+                 pipeline_part=0, async_key_builds=True, stream=True, stage=True, speculate=True,
+                 max_promotions=1024):
         self.engine = engine
         self.device = device
         self.devices = devices
@@ -200,8 +201,9 @@ class _GpuState:
         self.key_window = auto_window(max_keys, key_store_bytes) if key_window == "auto" else key_window
         self.max_keys = max_keys
         self.hot_key_uses = hot_key_uses
-        self.key_uses = OrderedDict()   # key -> successful general-path verifies (bounded LRU)
+        self.key_uses = OrderedDict()   # key -> (decayed successful general-path verifies, epoch) (bounded LRU)
         self.key_uses_max = 1 << 16
+        self.max_promotions = max_promotions  # keys that earned a slot, registered per batch at most
         self.pending = OrderedDict()    # addIdr keys waiting for a free slot
         self.hot = OrderedDict()        # keys that earned a slot (hot_key_uses verified requests)
         self.scan_threads = scan_threads  # host threads of the native batch scan (0 = auto)
@@ -430,8 +432,9 @@ class GpuAuthMixin:
         this batch) and addIdr keys (free slots only), registered before the
         batch routes its items (asynchronous builds by default)."""
         g = self._g
-        if g.hot:
-            got = ks.register(list(g.hot), pinned=batch_keys, evict=True, asynchronous=g.async_key_builds)
+        if g.hot:  # at most max_promotions per batch (each a table build on the device)
+            got = ks.register(list(g.hot)[:g.max_promotions], pinned=batch_keys, evict=True,
+                              asynchronous=g.async_key_builds)
             g.stats["keys_registered"] += len(got)
             g.hot.clear()
         if g.pending:
@@ -469,7 +472,8 @@ class GpuAuthMixin:
             return [], [], todo
         batch_keys = [p.key for p in todo]
         if g.hot:  # earned a slot: may evict least-recently-used keys not in this batch
-            got = ks.register(list(g.hot), pinned=batch_keys, evict=True, asynchronous=g.async_key_builds)
+            got = ks.register(list(g.hot)[:g.max_promotions], pinned=batch_keys, evict=True,
+                              asynchronous=g.async_key_builds)
             g.stats["keys_registered"] += len(got)
             g.hot.clear()
         if g.pending:  # addIdr keys: free slots only
@@ -484,40 +488,40 @@ class GpuAuthMixin:
         general = [p for p, i in zip(todo, ids) if i is None]
         return [p for p, _ in keyed], [i for _, i in keyed], general
 
+    def _use_epoch(self):
+        """The verified-use counts' clock: one tick per 2^18 requests this
+        authenticator has verified in batches or alone; a key's count halves
+        per tick (so only keys in sustained use earn a slot, and a long tail of
+        signers seen now and then does not churn the store)."""
+        st = self._g.stats
+        return (st["batch_items"] + st["single_verifies"]) >> 18
+
     def _count_verified(self, items, oks):
         """A general-path key earns a slot after hot_key_uses requests that
-        VERIFIED (bad signatures cannot push keys into the store)."""
-        g = self._g
-        if g.max_keys <= 0:
-            return
-        uses = g.key_uses
+        VERIFIED (bad signatures cannot push keys into the store), counted
+        with decay (_use_epoch)."""
+        counts = {}
         for p, ok in zip(items, oks):
-            if not ok:
-                continue
-            u = uses.pop(p.key, 0) + 1
-            if u >= g.hot_key_uses:
-                g.hot[p.key] = None
-            else:
-                uses[p.key] = u
-        while len(uses) > g.key_uses_max:
-            uses.popitem(last=False)
+            if ok:
+                counts[p.key] = counts.get(p.key, 0) + 1
+        self._count_verified_keys(list(counts), list(counts.values()))
 
     def _count_verified_keys(self, keys, counts):
-        """_count_verified for c[j] verified requests of key j at once (the
-        same final state as counting them one by one)."""
+        """_count_verified for c[j] verified requests of key j at once."""
         g = self._g
         if g.max_keys <= 0:
             return
-        uses, h = g.key_uses, g.hot_key_uses
+        uses, h, now = g.key_uses, g.hot_key_uses, self._use_epoch()
         for key, c in zip(keys, counts):
             if not c:
                 continue
-            u = uses.pop(key, 0) + int(c)
+            u, e = uses.pop(key, (0, now))
+            u = (u >> min(62, now - e)) + int(c)
             if u >= h:
                 g.hot[key] = None
-                u %= h
+                u = 0
             if u:
-                uses[key] = u
+                uses[key] = (u, now)
         while len(uses) > g.key_uses_max:
             uses.popitem(last=False)
 

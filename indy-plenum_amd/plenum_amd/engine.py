@@ -488,6 +488,17 @@ class EdVerifyEngine:
                                            ctypes.byref(ticket)))
         return first.value, ticket.value
 
+    def keys_set_many_async(self, ids, pk32):
+        """Rebuild slots ids[k] (distinct) with keys pk32[k], all in one call,
+        without waiting (edv_keys_set_many_async); returns the ticket."""
+        pk32 = _u8(pk32, 32)
+        ids = np.ascontiguousarray(ids, dtype=np.uint32)
+        if ids.shape[0] != pk32.shape[0]:
+            raise ValueError("shape mismatch: %d ids, %d keys" % (ids.shape[0], pk32.shape[0]))
+        ticket = ctypes.c_uint64()
+        check(self._lib.edv_keys_set_many_async(self._ctx, _ptr(ids), _ptr(pk32), ids.shape[0], ctypes.byref(ticket)))
+        return ticket.value
+
     def keys_set_async(self, first_id, pk32):
         """Rebuild slots first_id.. with new keys without waiting; returns the ticket."""
         pk32 = _u8(pk32, 32)

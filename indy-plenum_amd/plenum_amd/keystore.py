@@ -180,6 +180,25 @@ class KeyStore:
         if over and evict and hasattr(self.engine, "keys_set"):
             pinned = set(pinned)
             victims = [k for k in self._ids if k not in pinned][:len(over)]
+            if use_async and hasattr(self.engine, "keys_set_many_async") and victims:
+                # every eviction of this call in one upload and one build launch
+                pairs = list(zip(over, victims))
+                slots = [self._ids.pop(k_old) for _, k_old in pairs]
+                self.version += 1
+                pk = np.frombuffer(b"".join(k for k, _ in pairs), np.uint8).reshape(-1, 32)
+                try:
+                    ticket = self.engine.keys_set_many_async(np.asarray(slots, np.uint32), pk)
+                except Exception:
+                    for sl in slots:  # the slots' old tables may be half rewritten: retire them
+                        self._slot_key[sl] = None
+                    self._fail([k for k, _ in pairs])
+                    return done
+                self._mark_building(slots, ticket)
+                for (k_new, _), sl in zip(pairs, slots):
+                    self._slot_key[sl] = k_new
+                    self._ids[k_new] = sl
+                    done.append(k_new)
+                return done
             for k_new, k_old in zip(over, victims):
                 slot = self._ids.pop(k_old)
                 self.version += 1

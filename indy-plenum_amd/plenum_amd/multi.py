@@ -159,6 +159,10 @@ class MultiEngine:
             raise RuntimeError("key stores of the devices diverged (first ids %s)" % sorted(firsts))
         return firsts.pop(), tuple(t for _, t in res)
 
+    def keys_set_many_async(self, ids, pk32):
+        pk32 = _u8(pk32, 32)
+        return tuple(self._each(lambda e: e.keys_set_many_async(ids, pk32)))
+
     def keys_set_async(self, first_id, pk32):
         pk32 = _u8(pk32, 32)
         return tuple(self._each(lambda e: e.keys_set_async(first_id, pk32)))

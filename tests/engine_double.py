@@ -244,6 +244,18 @@ class AsyncOracleEngine(OracleEngine):
             self.building[i] = self.issued
         return self.issued
 
+    def keys_set_many_async(self, ids, pk32):
+        pk32 = np.asarray(pk32, np.uint8).reshape(-1, 32)
+        ids = [int(i) for i in ids]
+        assert len(set(ids)) == len(ids) == pk32.shape[0]
+        for i, k in zip(ids, pk32):
+            OracleEngine.keys_set(self, i, k.reshape(1, 32))
+        self.issued += 1
+        self.many_calls = getattr(self, "many_calls", 0) + 1
+        for i in ids:
+            self.building[i] = self.issued
+        return self.issued
+
     def keys_ready(self, ticket):
         return ticket <= self.done
 

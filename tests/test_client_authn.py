@@ -966,3 +966,41 @@ def test_verdict_cache_bounded_by_entries_bytes_and_age(oracle, monkeypatch):
     assert g.stats["cache_hits"] > hits
     a.clear_verdicts()
     assert g.verdict_bytes == 0 and not g.verdict_epochs
+
+
+def test_promotions_decay_cap_and_one_build_call(oracle):
+    """Keys earn slots by verified use counted with decay (a count halves per
+    2^18 requests: _use_epoch), at most max_promotions per batch, and a batch's
+    evictions go to the engine as one keys_set_many_async call."""
+    from engine_double import AsyncOracleEngine
+    eng = AsyncOracleEngine(oracle)
+    idrs, vks, msgs = _signed(6, 60)
+    table = dict(zip(idrs, vks))
+    a = GpuAuthNr(engine=eng, nym_lookup=lambda st, idr: {"verkey": table[idr]}, max_keys=2, hot_key_uses=2,
+                  max_promotions=3)
+    g = a._g
+    key_of = {i: a._key_for(i) for i in idrs}
+    # fill the two slots
+    a._count_verified_keys([key_of[idrs[0]], key_of[idrs[1]]], [5, 5])
+    a._register_waiting(a._key_store(), [])
+    eng.finish_builds()
+    assert len(a._key_store()) == 2 and not g.hot
+    # four keys earn a slot at once; the two slots go to the first of them (the batch's cap is 3), both
+    # evictions in one call
+    a._count_verified_keys([key_of[i] for i in idrs[2:6]], [3, 3, 3, 3])
+    assert len(g.hot) == 4
+    calls = getattr(eng, "many_calls", 0)
+    got = a._key_store().register(list(g.hot)[:g.max_promotions], evict=True, asynchronous=True)
+    assert len(got) == 2 and eng.many_calls == calls + 1  # two slots to evict: one set-many call
+    # decay: one verified use per 2^18 requests never reaches 2
+    g.hot.clear()
+    k = key_of[idrs[5]]
+    g.key_uses.pop(k, None)
+    for _ in range(6):
+        a._count_verified_keys([k], [1])
+        g.stats["batch_items"] += 1 << 18
+    assert k not in g.hot
+    a._count_verified_keys([k], [1])
+    assert k not in g.hot
+    a._count_verified_keys([k], [1])  # a second use in the same epoch: it earns a slot
+    assert k in g.hot
