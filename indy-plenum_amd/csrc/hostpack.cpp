@@ -2443,6 +2443,43 @@ PyObject* py_gather_u32(PyObject*, PyObject* args) {
 // gather_items(sig, msgbuf, off, idx, stride=64) -> (sig', msgbuf', off'): the
 // items idx (uint32 LE) of a split batch, repacked contiguously; stride is the
 // signature record size (64 = R || S, 96 = edverify.h signature slots).
+// gather_spans(sig, msgbuf, spans, idx_u32, stride=96) -> (sig_k, msg_k, off_k): gather_items over a
+// staged batch, whose item i's message is msgbuf[starts[i], ends[i]) (spans = starts[n] then ends[n],
+// uint64): the items of a staged batch that take another path.
+PyObject* py_gather_spans(PyObject*, PyObject* args) {
+  Py_buffer bs, bm, bp, bi;
+  Py_ssize_t stride = 64;
+  if (!PyArg_ParseTuple(args, "y*y*y*y*|n", &bs, &bm, &bp, &bi, &stride)) return nullptr;
+  const uint64_t* st = (const uint64_t*)bp.buf;
+  const uint32_t* idx = (const uint32_t*)bi.buf;
+  const Py_ssize_t n = bp.len / 16, k = bi.len / 4;
+  const uint64_t* en = st + n;
+  bool ok = (stride == 64 || stride == kSigSlot) && bp.len % 16 == 0 && bs.len >= n * stride;
+  std::string sig, msg;
+  std::vector<uint64_t> o((size_t)k + 1, 0);
+  if (ok) sig.assign((size_t)k * (size_t)stride, '\0');
+  for (Py_ssize_t j = 0; j < k && ok; ++j) {
+    const uint32_t i = idx[j];
+    if ((Py_ssize_t)i >= n || en[i] < st[i] || en[i] > (uint64_t)bm.len) {
+      ok = false;
+      break;
+    }
+    memcpy(&sig[(size_t)j * stride], (const char*)bs.buf + (size_t)i * stride, (size_t)stride);
+    msg.append((const char*)bm.buf + st[i], en[i] - st[i]);
+    o[(size_t)j + 1] = msg.size();
+  }
+  PyBuffer_Release(&bs);
+  PyBuffer_Release(&bm);
+  PyBuffer_Release(&bp);
+  PyBuffer_Release(&bi);
+  if (!ok) {
+    PyErr_SetString(PyExc_ValueError, "gather_spans: stride, index or spans out of range");
+    return nullptr;
+  }
+  return Py_BuildValue("(y#y#y#)", sig.data(), (Py_ssize_t)sig.size(), msg.data(), (Py_ssize_t)msg.size(),
+                       (const char*)o.data(), (Py_ssize_t)(o.size() * 8));
+}
+
 PyObject* py_gather_items(PyObject*, PyObject* args) {
   Py_buffer bs, bm, bo, bi;
   Py_ssize_t stride = 64;
@@ -2643,6 +2680,9 @@ PyMethodDef kMethods[] = {
      "scan_batch(msgs, ignore, threads=0, out=None) -> (fast, idrs, sig64, msgbuf, off, short): authenticate()'s "
      "host steps for a batch.  out = [bytearray, bytearray]: sig64 / msgbuf are written into them (grown, never "
      "shrunk: slice to n * 64 and off[n] bytes) and returned"},
+    {"gather_spans", py_gather_spans, METH_VARARGS,
+     "gather_spans(sig, msgbuf, spans_u64, idx_u32, stride=64) -> (sig_k, msg_k, off_k): gather_items for a staged "
+     "batch's item spans (starts[n] then ends[n])"},
     {"kid_map", py_kid_map, METH_VARARGS,
      "kid_map(old, identifiers, ids_u32) -> map: identifier text -> key id (0xffffffff: none) for the staged "
      "scan's speculation (old: a kid_map to update in place, or None)"},

@@ -63,8 +63,9 @@ from .verifier import DidVerifier, VerkeyCache
 
 try:  # native batch scan (csrc/hostpack.cpp): authenticate()'s host steps for a whole batch
     from ._hostpack import gather_items as _gather_items, results_from as _results_from, scan_batch_u as _scan_batch
+    from ._hostpack import gather_spans as _gather_spans
 except ImportError:  # pragma: no cover - the per-message path below
-    _scan_batch = _gather_items = _results_from = None
+    _scan_batch = _gather_items = _results_from = _gather_spans = None
 try:
     from ._hostpack import (gather_u32 as _gather_u32, pack_range as _pack_range, repack_spans as _repack_spans,
                             results_ok as _results_ok, kid_map as _kid_map, kid_map_size as _kid_map_size)
@@ -816,17 +817,23 @@ class GpuAuthMixin:
         g.msg_bytes_per_item = max(g.msg_bytes_per_item * 0.5, float(staged_bytes) / n if n else 0.0)
         ukeys = self._keys_for(uniq)  # authenticate():93-99, once per identifier
         ids = None
-        if ks is not None and fast_b.count(0) == 0 and all(k.__class__ is bytes for k in ukeys):
+        general_u = None  # distinct identifiers whose key has no built table: the general path
+        if ks is not None and fast_b.count(0) == 0 and all(k.__class__ is bytes and k for k in ukeys):
             if g.hot or g.pending:
                 self._register_waiting(ks, list(dict.fromkeys(ukeys)))
             ids = ks.lookup(ukeys)
             if any(i is None for i in ids):
-                ids = None
+                general_u = [u for u, i in enumerate(ids) if i is None]
+                ids = [0xffffffff if i is None else i for i in ids]  # (an id the kernels reject)
         if ids is None:  # not the steady state: contiguous messages, the ordinary path
             drop_parts()
             del spans, ms, me
             msg_c, off_c = _repack_spans(msg_o, spans_b)
             return self._finish_scanned(msgs, (fast_b, uidx_b, uniq, sig_o, msg_c, off_c, short), slot, ukeys)
+        if general_u is not None:  # a mixed batch (key churn): the keyed verify, then the rest
+            drop_parts()
+            return self._staged_mixed(msgs, eng, slot, slot_base, ks, ukeys, ids, general_u, scan, spans_buf,
+                                      kid_buf, t0, t1)
         ids_b = np.asarray(ids, np.uint32).tobytes()
         spec_hit = parts is not None and parts_ok and spec_u == ids_b and ks.version == ks_version
         if g.speculate and _kid_map is not None and (spec_u != ids_b or g.kid_map is None or
@@ -871,6 +878,55 @@ class GpuAuthMixin:
         ok = np.asarray(eng.verify_staged(True, kid, slot_base, 0, ms, me), bool)
         del kid, spans, ms, me, spans_b
         return verdicts(ok, perf_counter())
+
+    def _staged_mixed(self, msgs, eng, slot, slot_base, ks, ukeys, ids, general_u, scan, spans_buf, kid_buf, t0, t1):
+        """A staged batch whose identifiers' keys are partly without a built
+        table (a signer population larger than the key store): one keyed
+        verify of the whole staged batch over the store's ids (the others get
+        an id the kernels reject), then the general path (the key bytes) for
+        the items of the other identifiers only, gathered from the pinned
+        buffers -- the same verdicts as per message."""
+        import numpy as np
+        from time import perf_counter
+        g = self._g
+        fast_b, uidx_b, uniq, sig_o, msg_o, spans_b, short = scan[:7]
+        n = len(msgs)
+        if spans_b is spans_buf:
+            spans_b = memoryview(spans_b).cast("B")[:16 * n]
+        spans = np.frombuffer(spans_b, np.uint64, count=2 * n)
+        kid = np.frombuffer(_gather_u32(np.asarray(ids, np.uint32).tobytes(), uidx_b,
+                                        kid_buf if kid_buf is not None else g.kid_out), np.uint32, count=n)
+        t2 = perf_counter()
+        ok = np.array(eng.verify_staged(True, kid, slot_base, 0, spans[:n], spans[n:]), bool)
+        uidx = np.frombuffer(uidx_b, np.uint32)
+        is_gen = np.zeros(len(ukeys), bool)
+        is_gen[general_u] = True
+        gen = np.flatnonzero(is_gen[uidx])
+        if len(gen):
+            s_sig, s_msg, s_off = _gather_spans(memoryview(sig_o).cast("B")[:slot * n], msg_o, spans_b,
+                                                gen.astype(np.uint32).tobytes(), slot)
+            ukey_arr = np.zeros((len(ukeys), 32), np.uint8)
+            ukey_arr[general_u] = np.frombuffer(b"".join(ukeys[u] for u in general_u), np.uint8).reshape(-1, 32)
+            okg = np.asarray(eng.verify_batch(np.frombuffer(s_sig, np.uint8).reshape(-1, slot), ukey_arr[uidx[gen]],
+                                              np.frombuffer(s_msg, np.uint8), np.frombuffer(s_off, np.uint64),
+                                              **({"sig_slot": slot} if slot != 64 else {})), bool)
+            ok[gen] = okg
+            # general-path keys earn a slot by verified requests (short items never verify)
+            good = gen[okg & (np.frombuffer(short, np.uint8)[gen] == 0)]
+            per_u = np.bincount(uidx[good], minlength=len(ukeys))
+            hot_u = np.flatnonzero(per_u).tolist()
+            self._count_verified_keys([ukeys[u] for u in hot_u], [int(per_u[u]) for u in hot_u])
+        t3 = perf_counter()
+        g.stats["batches"] += 1
+        g.stats["batch_items"] += n
+        g.stats["keyed_items"] += n - len(gen)
+        results, failed = _results_ok(ok, short, uidx_b, uniq)
+        for i in failed:
+            results[i] = InvalidSignature()
+        g.last_breakdown = {"scan_and_copies": (t1 - t0) * 1e3, "keys_and_ids": (t2 - t1) * 1e3,
+                            "verify_wait": (t3 - t2) * 1e3, "verdicts": (perf_counter() - t3) * 1e3,
+                            "speculated": False, "general_items": int(len(gen))}
+        return results
 
     def authenticate_batches(self, batches):
         """authenticate_batch over an iterable of batches, yielding each batch's

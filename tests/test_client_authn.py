@@ -1004,3 +1004,35 @@ def test_promotions_decay_cap_and_one_build_call(oracle):
     assert k not in g.hot
     a._count_verified_keys([k], [1])  # a second use in the same epoch: it earns a slot
     assert k in g.hot
+
+
+def test_staged_mixed_batch_keyed_and_general(oracle, monkeypatch):
+    """A staged batch whose signers outnumber the key store (identifiers known,
+    only some keys built): one keyed verify of the staged batch plus the
+    general path for the other identifiers' items (gathered from the pinned
+    spans), forgeries and a short signature among both; every outcome equals
+    the general path's, and the general items count towards promotion."""
+    from engine_double import StagingOracleEngine
+    from plenum_amd import client_authn as CA
+    monkeypatch.setattr(CA, "_STAGE_MIN_BATCH", 1000)
+    monkeypatch.setattr(CA, "_PINNED_MIN_BATCH", 1000)
+    idrs, vks, msgs = _signed(5, 5000)
+    table = dict(zip(idrs, vks))
+    eng = StagingOracleEngine(oracle)
+    a = GpuAuthNr(engine=eng, nym_lookup=lambda st, idr: {"verkey": table[idr]}, max_keys=2, hot_key_uses=10 ** 9)
+    for i, v in zip(idrs[:2], vks[:2]):
+        a.addIdr(i, v)
+    a.keys_settle()
+    ref = GpuAuthNr(engine=OracleEngine(oracle), max_keys=0)
+    for i, v in zip(idrs, vks):
+        ref.addIdr(i, v)
+    batch = [dict(m) for m in msgs]
+    batch[10]["reqId"] += 1
+    batch[11]["reqId"] += 1
+    batch[12]["signature"] = batch[12]["signature"][:-3]
+    got = [_outcome(r) for r in a.authenticate_batch(batch)]
+    assert got == [_outcome(r) for r in ref.authenticate_batch(batch)]
+    bd = a._g.last_breakdown
+    assert bd and bd["general_items"] > 0 and eng.staged_calls == 1
+    assert 0 < a.stats["keyed_items"] < len(batch)
+    assert a._g.key_uses  # general-path keys counted
