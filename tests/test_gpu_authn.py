@@ -93,8 +93,9 @@ def test_default_engine_is_gpu():
 
 
 def test_keyed_and_general_paths_agree_on_gpu(gpu_engine):
-    with_keys, n_keyed = T._outcomes(gpu_engine, 16)
-    without, n_general = T._outcomes(gpu_engine, 0)
+    with _own_key_store(gpu_engine):
+        with_keys, n_keyed = T._outcomes(gpu_engine, 16)
+        without, n_general = T._outcomes(gpu_engine, 0)
     assert with_keys == without
     assert n_keyed > 0 and n_general == 0
     for c, r in zip(T.kat()["cases"], with_keys):
