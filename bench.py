@@ -557,7 +557,9 @@ def time_key_churn(eng, signers=100_000, n=1_000_000, batches=4, zipf=1.1, seed_
                       "distinct_signers": int(len(np.unique(kidx[b * per:(b + 1) * per]))),
                       "keyed_share": keyed / max(1, items), "general_share": 1 - keyed / max(1, items),
                       "registrations": st1["keys_registered"] - st0["keys_registered"],
-                      "speculated": bool((a._g.last_breakdown or {}).get("speculated"))})
+                      "in_batch_ms": {k: (round(v, 3) if isinstance(v, float) else v)
+                                      for k, v in (a._g.last_breakdown or {}).items()}})
+        a._g.last_breakdown = None
     ks = a._key_store()
     return {"signers": signers, "zipf_s": zipf, "requests": per * batches, "batches": out_b,
             "value": per * batches / total, "mismatches": int(bad), "key_slots": ks.capacity if ks else 0,
