@@ -1888,7 +1888,9 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
     // partition keeps its identifiers' earliest first occurrence (every worker's table holds most
     // of a batch's identifiers, so a serial merge compared ~t x distinct texts on one thread); then
     // the distinct identifiers are numbered in order of first occurrence
-    const int P = t;
+    size_t ncand = 0;
+    for (const WorkerIdrs& w : tabs) ncand += w.obj.size();
+    const int P = ncand >= 8192 ? t : 1;  // (a small batch merges on this thread: no helper wake-ups)
     struct Part {
       IdrTable tab;
       std::vector<PyObject*> obj;
@@ -1900,7 +1902,7 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
     for (int w = 0; w < t; ++w) to_global[(size_t)w].resize(tabs[(size_t)w].obj.size());
     run_chunks(P, P, [&](int, Py_ssize_t a, Py_ssize_t b) {
       for (Py_ssize_t p = a; p < b; ++p) {
-        Part& pt = parts[(size_t)p];
+        Part& pt = parts[(size_t)p];  // (P = 1: the one partition, serially)
         pt.tab.reset(tabs.empty() ? 64 : tabs[0].obj.size() / (size_t)P + 64);
         for (int w = 0; w < t; ++w) {
           const WorkerIdrs& tb = tabs[(size_t)w];
