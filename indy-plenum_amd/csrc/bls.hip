@@ -11,6 +11,7 @@
 //   edv_bls_aggregate_kernel  create_multi_sig: the sum of G1 points
 //   edv_bls_sign_kernel / edv_bls_keygen_kernel  [sk]H(m), [sk]g (test data)
 #include <hip/hip_runtime.h>
+#include <string.h>
 
 #include <cstdio>
 #include <cstdlib>
@@ -313,14 +314,18 @@ __global__ __launch_bounds__(kBlsBlock) void edv_bls_verify_quad_kernel(const ui
 // The wave form (batches of at most bls_wave_max checks -- a COMMIT round's ~25): one wave per
 // check running bls_program.h, the whole pairing check as a straight-line program of Fp
 // operations scheduled over the 64 lanes (tools/gen_bls_program.py).  Prologue (per-lane code,
-// as the other forms): H(m) with the try-and-increment's first 16 candidates on lanes 0-15 side
-// by side (the first candidate that is a point wins, as in g1_hash's loop), then the signature,
-// generator and verkey-sum decodes on lanes 16-18.  Per step each lane reads its operation
+// as the other forms): H(m) with the try-and-increment's first 61 candidates side by side on every
+// lane but 16-18 (candidate c on lane c for c < 16, on lane c + 3 after; the first candidate that is
+// a point wins, as in g1_hash's loop), the signature, generator and verkey-sum decodes on lanes
+// 16-18.  Per step each lane reads its operation
 // (prefetched two steps ahead) and its operand slots, and writes its result after a barrier
 // (for a one-wave block the barrier is only the compiler's fence: LDS is in order per wave).
 // verdict[i]: 1 accept, 0 reject, 2 redo on the four-lane kernel (a degenerate Miller step
-// flagged by the program, or no point among the 16 candidates: bn254.h's branches decide).
-constexpr int kHashTries = 16;
+// flagged by the program, or no point among the 61 candidates -- about 2^-61 of messages, so no
+// message can be searched for that costs its round the four-lane kernel: bn254.h's branches decide).
+constexpr int kHashTries = 16;  // candidates on lanes 0..15; lanes kHashTries..+2 decode; 45 more after
+__device__ __forceinline__ bool hash_lane(int lane) { return lane < kHashTries || lane >= kHashTries + 3; }
+__device__ __forceinline__ int hash_candidate(int lane) { return lane < kHashTries ? lane : lane - 3; }
 __global__ __launch_bounds__(kBlsBlock) void edv_bls_verify_wave_kernel(const uint8_t* __restrict__ sig128,
                                                                        const uint8_t* __restrict__ msgs,
                                                                        const uint64_t* __restrict__ moff,
@@ -328,7 +333,8 @@ __global__ __launch_bounds__(kBlsBlock) void edv_bls_verify_wave_kernel(const ui
                                                                        const uint64_t* __restrict__ vk_off,
                                                                        const uint8_t* __restrict__ gen128, uint64_t n,
                                                                        uint8_t* __restrict__ verdict,
-                                                                       unsigned long long* __restrict__ clk) {
+                                                                       unsigned long long* __restrict__ clk,
+                                                                       int tries) {
   __shared__ fp S[blsp::kSlots];
   // clk (EDV_BLS_WAVE_CLOCKS=1, block 0): shader clocks at the start, after the prologue, after
   // the program, and the program's clocks in steps with a product / without one
@@ -339,10 +345,10 @@ __global__ __launch_bounds__(kBlsBlock) void edv_bls_verify_wave_kernel(const ui
   if (i >= n) return;  // the whole block
   for (int k = lane; k < blsp::kConsts; k += kBlsBlock) fp_load(S[blsp::kConstSlot[k]], blsp::kConstVal + 8 * k);
   if (lane < 4) bad[lane] = 0;
-  // H(m): candidate h + lane on lanes 0..kHashTries-1
+  // H(m): candidate h + hash_candidate(lane) on the hash lanes
   bool hit = false;
   fp hx, hy;
-  if (lane < kHashTries) {
+  if (hash_lane(lane) && hash_candidate(lane) < tries) {
     uint32_t d[8];
     sha256_msg(d, msgs + moff[i], moff[i + 1] - moff[i]);
     uint8_t hb[32];
@@ -355,7 +361,7 @@ __global__ __launch_bounds__(kBlsBlock) void edv_bls_verify_wave_kernel(const ui
     }
     uint32_t x[8];
     words_from_be(x, hb);
-    uint64_t c = (uint64_t)lane;  // h + lane, wrapping at 2^256 like g1_hash's h += 1
+    uint64_t c = (uint64_t)hash_candidate(lane);  // h + c, wrapping at 2^256 like g1_hash's h += 1
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const uint64_t t = (uint64_t)x[k] + c;
@@ -378,9 +384,13 @@ __global__ __launch_bounds__(kBlsBlock) void edv_bls_verify_wave_kernel(const ui
   }
   const unsigned long long hits = __ballot(hit);
   __syncthreads();
+  // the winner: the lowest candidate that is a point (lanes 0..15 hold candidates 0..15, lanes 19..
+  // hold 16..)
+  const unsigned long long lo = hits & ((1ull << kHashTries) - 1);
+  const int win = lo ? __ffsll((long long)lo) - 1 : (hits ? __ffsll((long long)hits) - 1 : -1);
   if (hits == 0) {
     if (lane == 0) bad[1] = 1;
-  } else if (lane == __ffsll((long long)hits) - 1) {
+  } else if (lane == win) {
     S[blsp::kIn_xP2] = hx;
     S[blsp::kIn_yP2] = hy;
   }
@@ -578,9 +588,19 @@ uint32_t grid_of(uint64_t n) { return (uint32_t)((n + kBlsBlock - 1) / kBlsBlock
 
 extern "C" {
 
+static int bls_verify(edv_ctx* ctx, const uint8_t* sig128, const uint8_t* msgs, const uint64_t* msg_off,
+                      const uint8_t* vk128, const uint64_t* vk_off, const uint8_t* gen128, uint64_t n,
+                      uint8_t* accept_bits, bool allow_wave);
+
 int edv_bls_verify_batch(edv_ctx* ctx, const uint8_t* sig128, const uint8_t* msgs, const uint64_t* msg_off,
                          const uint8_t* vk128, const uint64_t* vk_off, const uint8_t* gen128, uint64_t n,
                          uint8_t* accept_bits) {
+  return bls_verify(ctx, sig128, msgs, msg_off, vk128, vk_off, gen128, n, accept_bits, true);
+}
+
+static int bls_verify(edv_ctx* ctx, const uint8_t* sig128, const uint8_t* msgs, const uint64_t* msg_off,
+                      const uint8_t* vk128, const uint64_t* vk_off, const uint8_t* gen128, uint64_t n,
+                      uint8_t* accept_bits, bool allow_wave) {
   hipStream_t st;
   int r = edv_internal::begin(ctx, &st);
   if (r) return r;
@@ -608,14 +628,17 @@ int edv_bls_verify_batch(edv_ctx* ctx, const uint8_t* sig128, const uint8_t* msg
     BLS_TRY(hipMemcpyAsync(d_vkoff, vo.data(), 8 * (n + 1), hipMemcpyHostToDevice, st));
   }
   std::vector<uint8_t> vb;
-  if (n <= edv_internal::bls_wave_max(ctx)) {
+  if (allow_wave && n <= edv_internal::bls_wave_max(ctx)) {
     uint8_t* d_verdict;
     if ((r = sc.alloc(&d_verdict, n))) return r;
     unsigned long long* d_clk = nullptr;
     const bool clocks = getenv("EDV_BLS_WAVE_CLOCKS") != nullptr;
     if (clocks && (r = sc.alloc(&d_clk, 8 * 8))) return r;
+    // EDV_BLS_HASH_TRIES (tests): fewer side-by-side H(m) candidates than the 61 the wave has lanes for
+    const char* te = getenv("EDV_BLS_HASH_TRIES");
+    const int tries = te && atoi(te) > 0 && atoi(te) < 61 ? atoi(te) : 61;
     hipLaunchKernelGGL(edv_bls_verify_wave_kernel, dim3((uint32_t)n), dim3(kBlsBlock), 0, st, d_sig, d_msgs, d_off,
-                       d_vk, d_vkoff, d_gen, n, d_verdict, d_clk);
+                       d_vk, d_vkoff, d_gen, n, d_verdict, d_clk, tries);
     BLS_TRY(hipGetLastError());
     if (clocks) {  // diagnostics: where block 0's shader clocks went
       unsigned long long c[8];
@@ -627,14 +650,39 @@ int edv_bls_verify_batch(edv_ctx* ctx, const uint8_t* sig128, const uint8_t* msg
     vb.resize(n);
     BLS_TRY(hipMemcpyAsync(vb.data(), d_verdict, n, hipMemcpyDeviceToHost, st));
     BLS_TRY(hipStreamSynchronize(st));
-    bool redo = false;
-    for (uint64_t k = 0; k < n; ++k) redo = redo || vb[k] == 2;
-    if (!redo) {
-      for (uint64_t b = 0; b < (n + 7) / 8; ++b) accept_bits[b] = 0;
-      for (uint64_t k = 0; k < n; ++k) accept_bits[k / 8] |= (uint8_t)((vb[k] & 1u) << (k % 8));
-      return 0;
+    for (uint64_t b = 0; b < (n + 7) / 8; ++b) accept_bits[b] = 0;
+    std::vector<uint64_t> redo;
+    for (uint64_t k = 0; k < n; ++k) {
+      accept_bits[k / 8] |= (uint8_t)((vb[k] & 1u) << (k % 8));
+      if (vb[k] == 2) redo.push_back(k);
     }
-    // a degenerate check (a verkey sum outside the order-r subgroup): the four-lane kernel's verdicts
+    if (redo.empty()) return 0;
+    // the checks the wave form could not decide (no point among H(m)'s first candidates -- a message
+    // can be searched for that --, a degenerate Miller step): only they, compacted, on the four-lane
+    // kernel (one crafted message no longer re-runs its whole COMMIT round)
+    const uint64_t m = redo.size();
+    std::vector<uint8_t> rs(128 * m), rmsg, rvk;
+    std::vector<uint64_t> roff(m + 1, 0), rvoff;
+    if (vk_off) rvoff.assign(m + 1, 0);
+    for (uint64_t j = 0; j < m; ++j) {
+      const uint64_t k = redo[j];
+      memcpy(&rs[128 * j], sig128 + 128 * k, 128);
+      rmsg.insert(rmsg.end(), msgs + msg_off[k], msgs + msg_off[k + 1]);
+      roff[j + 1] = rmsg.size();
+      const uint64_t v0 = vk_off ? vk_off[k] : k, v1 = vk_off ? vk_off[k + 1] : k + 1;
+      rvk.insert(rvk.end(), vk128 + 128 * v0, vk128 + 128 * v1);
+      if (vk_off) rvoff[j + 1] = rvk.size() / 128;
+    }
+    std::vector<uint8_t> rbits((m + 7) / 8, 0);
+    if ((r = bls_verify(ctx, rs.data(), rmsg.empty() ? nullptr : rmsg.data(), roff.data(), rvk.data(),
+                        vk_off ? rvoff.data() : nullptr, gen128, m, rbits.data(), false)))
+      return r;
+    for (uint64_t j = 0; j < m; ++j) {
+      const uint64_t k = redo[j];
+      const uint8_t bit = (rbits[j / 8] >> (j % 8)) & 1u;
+      accept_bits[k / 8] = (uint8_t)((accept_bits[k / 8] & ~(1u << (k % 8))) | (bit << (k % 8)));
+    }
+    return 0;
   }
   if (!vb.empty() || 2 * n <= edv_internal::bls_pair_max(ctx))
     hipLaunchKernelGGL(edv_bls_verify_quad_kernel, dim3(grid_of(4 * n)), dim3(kBlsBlock), 0, st, d_sig, d_msgs, d_off,
@@ -651,11 +699,6 @@ int edv_bls_verify_batch(edv_ctx* ctx, const uint8_t* sig128, const uint8_t* msg
   BLS_TRY(hipStreamSynchronize(st));
   for (uint64_t b = 0; b < (n + 7) / 8; ++b) accept_bits[b] = (uint8_t)(w[b / 8] >> (8 * (b % 8)));
   if (n & 7) accept_bits[n / 8] &= (uint8_t)((1u << (n & 7)) - 1);
-  if (!vb.empty()) {  // the wave form's own verdicts where it had one
-    for (uint64_t k = 0; k < n; ++k)
-      if (vb[k] != 2)
-        accept_bits[k / 8] = (uint8_t)((accept_bits[k / 8] & ~(1u << (k % 8))) | ((vb[k] & 1u) << (k % 8)));
-  }
   return 0;
 }
 

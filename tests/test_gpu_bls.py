@@ -129,10 +129,14 @@ def test_dropin_reference_scenarios(gpu_engine):
 REDO_MSG = b"wave-form redo 11075"  # H(m) needs more than 16 candidates (tests/test_bls_program.py)
 
 
-def test_wave_form_hands_over_what_it_cannot_decide(gpu_engine):
-    """The wave form tries 16 hash candidates side by side; for REDO_MSG the first point is
-    candidate 17 or later, so the check goes to the four-lane kernel (verdict 2 -> redo) --
-    in a batch with ordinary checks, every verdict as in the four-lane form."""
+@pytest.mark.parametrize("tries", ["16", "61"])
+def test_wave_form_hands_over_what_it_cannot_decide(gpu_engine, monkeypatch, tries):
+    """The wave form tries H(m)'s candidates side by side (61 by default; EDV_BLS_HASH_TRIES=16
+    here to force the hand-over): for REDO_MSG the first point is candidate 17 or later, so with
+    16 tries those checks -- and only they, compacted -- go to the four-lane kernel (verdict 2 ->
+    redo); with 61 the wave form decides them.  Either way, in a batch with ordinary checks,
+    every verdict is the four-lane form's."""
+    monkeypatch.setenv("EDV_BLS_HASH_TRIES", tries)
     from plenum_amd import pack_messages
     gen = np.frombuffer(bytes.fromhex(V["generator"]), np.uint8)
     sks = np.frombuffer(b"".join(bytes.fromhex(k["sk"]) for k in V["keys"][:2]), np.uint8).reshape(-1, 32)
