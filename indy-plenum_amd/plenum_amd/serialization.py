@@ -13,38 +13,37 @@ from collections.abc import Iterable
 acceptableTypes = (str, int, float, list, dict, type(None))
 
 
-def _error(msg):
-    raise Exception(msg)
+def _text(obj, top, path, ignore):
+    """The signing text of obj.  top: obj is the message itself (only there are
+    the ignored keys dropped); path: the dotted key path of obj, used in the
+    error text and -- as the reference's does -- joined with each dict key, so a
+    non-str key below the top level raises TypeError just as the reference's
+    join does."""
+    if not isinstance(obj, acceptableTypes):
+        raise Exception("invalid type found {}: {}".format(path, obj))
+    if isinstance(obj, str):
+        return obj
+    if isinstance(obj, dict):
+        names = [k for k in obj.keys() if not top or k not in ignore]
+        names.sort()
+        fields = []
+        for name in names:
+            sub = ".".join([path, name]) if path else name
+            head = str(name) + ":"
+            fields.append(head + _text(obj[name], False, sub, ()))
+        return "|".join(fields)
+    if isinstance(obj, Iterable):  # a list: its items' texts, comma-separated, same path
+        return ",".join([_text(item, False, path, ()) for item in obj])
+    return "" if obj is None else str(obj)
 
 
 class SigningSerializer:
+    """The reference's serializer interface (serialize(obj, level, objname,
+    topLevelKeysToIgnore, toBytes)) over _text."""
+
     def serialize(self, obj, level=0, objname=None, topLevelKeysToIgnore=None, toBytes=True):
-        res = None
-        if not isinstance(obj, acceptableTypes):
-            _error("invalid type found {}: {}".format(objname, obj))
-        elif isinstance(obj, str):
-            res = obj
-        elif isinstance(obj, dict):
-            if level > 0:
-                keys = list(obj.keys())
-            else:
-                topLevelKeysToIgnore = topLevelKeysToIgnore or []
-                keys = [k for k in obj.keys() if k not in topLevelKeysToIgnore]
-            keys.sort()
-            strs = []
-            for k in keys:
-                onm = ".".join([objname, k]) if objname else k
-                strs.append(str(k) + ":" + self.serialize(obj[k], level + 1, onm, toBytes=False))
-            res = "|".join(strs)
-        elif isinstance(obj, Iterable):
-            res = ",".join(self.serialize(o, level + 1, objname, toBytes=False) for o in obj)
-        elif obj is None:
-            res = ""
-        else:
-            res = str(obj)
-        if not toBytes:
-            return res
-        return res.encode("utf-8")
+        text = _text(obj, level == 0, objname, topLevelKeysToIgnore or [])
+        return text.encode("utf-8") if toBytes else text
 
 
 signing_serializer = SigningSerializer()

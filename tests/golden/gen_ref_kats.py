@@ -45,6 +45,7 @@ def serializer_kats():
          "protocolVersion": 1, "signature": "x"},
         {"myMsg": "42 (forty-two) is the natural number that succeeds 41 and precedes 43."},
         {"1": "a", "2": "b", "3": [1, {"2": "k"}]},
+        {"": {"k": "v"}}, {"a": {"": {"q": 1}}}, {"l": [[1, [2]], None, True, 1.5e300, -0.0]},
     ]
     out = []
     for c in cases:
@@ -52,7 +53,8 @@ def serializer_kats():
             out.append({"msg": c, "ignore": ignore,
                         "bytes_hex": serialize_msg_for_signing(c, topLevelKeysToIgnore=ignore).hex()})
     # non-acceptable types raise
-    for bad in ({"t": (1, 2)}, {"b": b"x"}, {"s": {1, 2}}):
+    for bad in ({"t": (1, 2)}, {"b": b"x"}, {"s": {1, 2}},
+                {"a": {1: "x"}}, {"a": [{"b": {2: 1}}]}):  # a non-str key below the top: the key-path join raises
         try:
             serialize_msg_for_signing(bad)
             res = "ok"

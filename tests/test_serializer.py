@@ -35,6 +35,19 @@ def test_serializer_rejects_non_primitive_types(bad):
         serialize_msg_for_signing(bad)
 
 
+def test_serializer_raises_what_the_reference_raised():
+    """Every failing case of the reference-run KATs raises the same exception
+    class here (a non-str key below the top level: the reference's key-path
+    join raises TypeError; non-primitive values: Exception)."""
+    import ast
+    raising = [c for c in kats() if "raises" in c]
+    assert {c["raises"] for c in raising} == {"Exception", "TypeError"}
+    for c in raising:
+        with pytest.raises(Exception) as ei:
+            serialize_msg_for_signing(ast.literal_eval(c["msg_repr"]))
+        assert type(ei.value).__name__ == c["raises"], c
+
+
 def test_base58_reference_kats():
     cryptonym = 'BPtrqHo3WyjmTNpVchEhWxp3qfDdssdFUNoM8kmKoEWw'
     did_id, did_verkey = 'L5AD5g65TDQr1PPHHRoiGf', 'Bf9Z1tKWpcJAvKJVhZhvVZ'
