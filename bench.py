@@ -208,6 +208,19 @@ def sodium_all_items(sig, pk, msgs, starts, ends, threads):
     return (ok.astype(bool), time.perf_counter() - t0) if r == 1 else (None, 0.0)
 
 
+def build_stamp(eng):
+    """Which binaries this line was measured with: the library's version string and the
+    sha256 (16 hex) of the loaded libplenum_edverify.so and _hostpack extension."""
+    import hashlib
+    from plenum_amd import _hostpack
+    out = {"edv_version": eng._lib.edv_version().decode()}
+    for key, path in (("lib", getattr(eng._lib, "_name", None)), ("hostpack", getattr(_hostpack, "__file__", None))):
+        if path and os.path.exists(path):
+            out[key] = os.path.relpath(path, ROOT)
+            out[key + "_sha16"] = hashlib.sha256(open(path, "rb").read()).hexdigest()[:16]
+    return out
+
+
 def host_cpus():
     """nproc / affinity / cgroup CPU quota of this host (the GPU box shows the
     whole machine in nproc; the quota is this job's share)."""
@@ -1202,6 +1215,7 @@ def main():
             "ref10_equivalent_frac": (n * RL.MAD_PER_VERIFY / (ms_per_step * 1e-3)) / RL.PEAK_MAD_PER_S,
             "other_path": other,
             "dropin_window": dropin,
+            "build": build_stamp(eng),
             "whole_node": whole,
             "whole_node_vs_cpu": whole_vs,
             "end_to_end": e2e,
