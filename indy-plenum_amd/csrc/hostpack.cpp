@@ -114,6 +114,11 @@ struct OutBuf {
     }
   }
   void append(const char* z) { append(z, strlen(z)); }
+  void append_short(const char* src, size_t k) {  // k <= 24 (a number's decimal text)
+    if (n + k > cap) grow_to(n + k);
+    memcpy(d + n, src, k < 24 ? k : 24);
+    n += k;
+  }
   void push_back(char c) {
     if (n + 1 > cap) grow_to(n + 1);
     d[n++] = c;
@@ -122,6 +127,9 @@ struct OutBuf {
 
 template <class Out>
 bool ser_obj(PyObject* o, int level, PyObject* ignore, Out& out);
+
+inline void append_num(OutBuf& out, const char* b, size_t k) { out.append_short(b, k); }
+inline void append_num(std::string& out, const char* b, size_t k) { out.append(b, k); }
 
 template <class Out>
 bool append_str(PyObject* s, Out& out) {
@@ -250,7 +258,7 @@ bool ser_obj(PyObject* o, int level, PyObject* ignore, Out& out) {
     }
     char b[24];
     const auto r = std::to_chars(b, b + sizeof b, x);  // str(int) for 64-bit values
-    out.append(b, (size_t)(r.ptr - b));
+    append_num(out, b, (size_t)(r.ptr - b));
     return true;
   }
   if (PyFloat_CheckExact(o)) return append_text_of(o, out);
@@ -474,7 +482,7 @@ WRes wser_obj(PyObject* o, int level, PyObject* ignore, OutBuf& out) {
     }
     char b[24];
     const auto r = std::to_chars(b, b + sizeof b, x);
-    out.append(b, (size_t)(r.ptr - b));
+    out.append_short(b, (size_t)(r.ptr - b));
     return kOk;
   }
   if (PyFloat_CheckExact(o)) return kDefer;  // Python's repr: str() under the GIL
