@@ -736,7 +736,7 @@ class GpuAuthMixin:
         slots to the device (edv_stage_put) as soon as they are written, so
         by the time the scan returns most of the batch is already in HBM;
         edv_verify_staged then waits for the rest and runs the kernels over
-        the item spans.  Synchronous batches (defer False) speculate: the scan
+        the item spans.  Batches speculate: the scan
         also writes each request's key id from kid_map (the ids of the batches
         before) and its copier queues the kernels of every 2^16 staged
         requests (edv_verify_staged_part), so the kernels run under the scan
@@ -774,7 +774,7 @@ class GpuAuthMixin:
         kid_buf = self._pinned(eng, "pinned_kid" + sfx, 4 * n)  # key ids straight into pinned memory: no copy
         ks = self._key_store()
         spec, parts = None, None
-        if (not defer and g.speculate and g.kid_map is not None and ks is not None and _kid_map is not None
+        if (g.speculate and g.kid_map is not None and ks is not None and _kid_map is not None
                 and os.environ.get("EDV_SPECULATE", "1") != "0"
                 and spans_buf is not None and kid_buf is not None and getattr(eng, "supports_staged_parts", False)):
             ks_version = ks.version
@@ -858,9 +858,15 @@ class GpuAuthMixin:
                                 "speculated": bool(spec_hit)}
             return results
         if spec_hit:  # the kernels ran under the scan with exactly these ids
-            ok = np.asarray(eng.verify_staged_collect(parts), bool)
-            parts = None
+            ticket, parts = parts, None
             del spans, ms, me, spans_b
+            if defer:  # (they may still run: collected when the caller asks for the results)
+                def finish_spec():
+                    with _engine_lock(eng):
+                        ok = np.asarray(eng.verify_staged_collect(ticket), bool)
+                    return verdicts(ok, perf_counter())
+                return finish_spec
+            ok = np.asarray(eng.verify_staged_collect(ticket), bool)
             return verdicts(ok, perf_counter())
         drop_parts()
         kid = np.frombuffer(_gather_u32(ids_b, uidx_b, kid_buf if kid_buf is not None else g.kid_out), np.uint32,

@@ -791,8 +791,39 @@ def test_authenticate_batches_pipeline(oracle, monkeypatch):
     got = [[_outcome(r) for r in res] for res in a.authenticate_batches(iter(batches))]
     want = [[_outcome(r) for r in ref.authenticate_batch(b)] for b in batches]
     assert got == want
-    assert eng.submits_staged == 3 and eng.held == [None, None]  # batches 0, 1 and 5 were in flight
+    # batches 0, 1 and 5 were in flight: 0 submitted, 1 and 5 speculated (their kernels queued
+    # under their scans with the ids of the batches before)
+    assert eng.submits_staged == 1 and a._g.stats["speculated"] == 2 * 1200 and eng.held == [None, None]
     assert list(a.authenticate_batches([])) == []
+
+
+def test_authenticate_batches_speculation_hits_and_misses(oracle, monkeypatch):
+    """authenticate_batches speculates too: a batch whose identifiers all
+    resolved in the batches before runs its kernels under its own scan (and
+    is collected when the caller asks for it); a batch bringing an identifier
+    the kid map does not hold drops its parts and takes the ordinary submit;
+    every outcome equals authenticate_batch's."""
+    from engine_double import StagingOracleEngine
+    from plenum_amd import client_authn as CA
+    monkeypatch.setattr(CA, "_STAGE_MIN_BATCH", 1000)
+    monkeypatch.setattr(CA, "_PINNED_MIN_BATCH", 1000)
+    idrs, vks, msgs = _signed(4, 7200)
+    eng = StagingOracleEngine(oracle)
+    a = GpuAuthNr(engine=eng)
+    ref = GpuAuthNr(engine=OracleEngine(oracle), max_keys=0)
+    for i, v in zip(idrs, vks):
+        a.addIdr(i, v)
+        ref.addIdr(i, v)
+    a.keys_settle()
+    three = [dict(m) for m in msgs if m["identifier"] != idrs[3]]
+    batches = [three[k * 1200:(k + 1) * 1200] for k in range(3)]  # signers 0-2 only
+    batches.insert(2, [dict(m) for m in msgs[:1200]])             # signer 3 appears: a miss
+    batches[1][11]["signature"] = batches[1][12]["signature"]      # a forgery in a speculated batch
+    got = [[_outcome(r) for r in res] for res in a.authenticate_batches(iter(batches))]
+    want = [[_outcome(r) for r in ref.authenticate_batch(b)] for b in batches]
+    assert got == want
+    # batch 0: no kid map yet; batch 2: the miss -- both submitted; batches 1 and 3 speculated
+    assert eng.submits_staged == 2 and a._g.stats["speculated"] == 2 * 1200 and eng.held == [None, None]
 
 
 def test_authenticate_batches_abandoned_frees_the_set(oracle, monkeypatch):
