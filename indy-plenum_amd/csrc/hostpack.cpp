@@ -1350,6 +1350,9 @@ struct StageCopier {
   std::unique_ptr<std::atomic<uint32_t>[]> chunk_seq;  // by chunk index: its message reservation number
 
   void put(const char* src, uint64_t nbytes, uint64_t off) {
+#ifdef EDV_STAGE_NODMA  // diagnostic builds only (tools/: the scan's cost without the copies under it)
+    return;
+#endif
     if (nbytes && fn(ctx, src, nbytes, off) != 0) failed = true;
   }
   void send_ready() {  // every ready message byte and slot, whatever the grain
@@ -2022,8 +2025,10 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
   std::vector<uint32_t>& uidx = S.uidx;
   fast.resize((size_t)n);
   shortv.resize((size_t)n);
-  off.resize((size_t)n + 1);
-  off[0] = 0;
+  if (!staged) {  // (a staged batch's messages are placed already: its spans say where)
+    off.resize((size_t)n + 1);
+    off[0] = 0;
+  }
   if (unique_form) uidx.resize((size_t)n);
   std::vector<uint64_t> csum((size_t)((n + kScanChunk - 1) / kScanChunk) + 1, 0);
   run_chunks(n, t, [&](int, Py_ssize_t a, Py_ssize_t b) {
@@ -2045,16 +2050,18 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
       fast[(size_t)i] = f;
       shortv[(size_t)i] = sh;
       if (unique_form) uidx[(size_t)i] = u;
-      off[(size_t)i + 1] = len;
+      if (!staged) off[(size_t)i + 1] = len;
       sum += len;
     }
     csum[(size_t)(a / kScanChunk) + 1] = sum;  // (one call over [0, n) when not chunked: csum[1])
   });
-  for (size_t c = 1; c < csum.size(); ++c) csum[c] += csum[c - 1];
-  run_chunks(n, t, [&](int, Py_ssize_t a, Py_ssize_t b) {
-    uint64_t at = csum[(size_t)(a / kScanChunk)];
-    for (Py_ssize_t i = a; i < b; ++i) off[(size_t)i + 1] = at += off[(size_t)i + 1];
-  });
+  if (!staged) {
+    for (size_t c = 1; c < csum.size(); ++c) csum[c] += csum[c - 1];
+    run_chunks(n, t, [&](int, Py_ssize_t a, Py_ssize_t b) {
+      uint64_t at = csum[(size_t)(a / kScanChunk)];
+      for (Py_ssize_t i = a; i < b; ++i) off[(size_t)i + 1] = at += off[(size_t)i + 1];
+    });
+  }
   // (5) sig64 and the messages, written by the workers into the result objects (a deferred
   // scan leaves this to pack_range, stretch by stretch, so the caller can queue each stretch's
   // DMA while the next one packs)
