@@ -963,6 +963,33 @@ def test_speculative_staged_batch_raising_scan_frees_the_set(oracle, monkeypatch
     assert a.authenticate_batch(steady) == [m["identifier"] for m in steady]
 
 
+def test_pipelined_speculative_batch_raising_scan_frees_the_sets(oracle, monkeypatch):
+    """authenticate_batches: a scan that raises while batch k's kernels are in
+    flight and batch k + 1 speculates propagates, and neither staging set
+    stays held (the open parts are ended and collected, the batch in flight
+    is collected by the generator's close)."""
+    from plenum_amd import client_authn as CA
+    eng, a, ref, idrs, vks, msgs = _staged_pair(oracle, monkeypatch)
+    steady = [dict(m) for m in msgs if m["identifier"] in idrs[:4]]
+    a.authenticate_batch(steady)  # the kid map
+    real = CA._scan_batch
+    calls = [0]
+
+    def boom(*args):
+        calls[0] += 1
+        if calls[0] == 2 and len(args) > 8 and args[8] is not None:
+            raise MemoryError("injected")
+        return real(*args)
+    monkeypatch.setattr(CA, "_scan_batch", boom)
+    it = a.authenticate_batches([steady, steady, steady])
+    with pytest.raises(MemoryError):
+        list(it)
+    assert eng.held == [None, None]
+    monkeypatch.setattr(CA, "_scan_batch", real)
+    want = [m["identifier"] for m in steady]
+    assert list(a.authenticate_batches([steady, steady])) == [want, want]
+
+
 def test_verdict_cache_bounded_by_entries_bytes_and_age(oracle, monkeypatch):
     """The verify-ahead verdict cache (bounded by bytes, trimmed by
     age): entries beyond verdict_cache_size, bytes beyond verdict_cache_bytes
