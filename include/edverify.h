@@ -270,6 +270,16 @@ int edv_verify_staged_begin(edv_ctx *ctx, int keyed, uint64_t n, uint64_t *ticke
 int edv_verify_staged_part(edv_ctx *ctx, const void *keys, uint64_t slot_off, uint64_t msg_base,
                            const uint64_t *spans, uint64_t n, uint64_t lo, uint64_t hi);
 int edv_verify_staged_end(edv_ctx *ctx);
+/* Items of the last staged batch again, on the general path: after edv_verify_staged (or a
+ * collected edv_verify_staged_submit) of the current set, verify its items idx[j] (< that
+ * batch's n) with the key bytes pk32[j] (32 each), accept bit j of accept_bits[(m + 7) / 8].
+ * The batch's decoded signatures, spans and messages are still in HBM, so only the indices and
+ * keys cross PCIe -- the authenticator's mixed batches (signers whose keys have no table: a
+ * keyed verify of the whole batch, then these items by their key bytes).  Refused once the set
+ * is reserved or begun again.  Replaces, like edv_verify_staged, libsodium's crypto_sign_open per
+ * request (nacl_wrappers.py:108). */
+int edv_verify_staged_subset(edv_ctx *ctx, const uint32_t *idx, const uint8_t *pk32, uint64_t m,
+                             uint8_t *accept_bits);
 
 /* Signature slots: the host-pointer verifies below take, instead of sig64,
  * n slots of EDV_SIG_SLOT96 bytes, so that the base58 decode of the request

@@ -607,6 +607,24 @@ __global__ __launch_bounds__(kBlock) void edv_ok_pack_kernel(const uint8_t* __re
   if ((i & 63) == 0) words[i >> 6] = bits;
 }
 
+// edv_verify_staged_subset: item idx[j] of the last staged batch (its decoded signature and its
+// message span, starts [n] then ends [n]) into position j of the subset's contiguous inputs.
+__global__ __launch_bounds__(kBlock) void edv_subset_gather_kernel(const uint32_t* __restrict__ idx, uint64_t m,
+                                                                  uint64_t n, const uint8_t* __restrict__ sig,
+                                                                  const uint64_t* __restrict__ spans,
+                                                                  uint8_t* __restrict__ sig_out,
+                                                                  uint64_t* __restrict__ spans_out) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  const uint64_t i = idx[j] < n ? idx[j] : 0;  // (checked on the host)
+  const uint4* s = (const uint4*)(sig + 64 * i);
+  uint4* o = (uint4*)(sig_out + 64 * j);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) o[k] = s[k];
+  spans_out[j] = spans[i];
+  spans_out[m + j] = spans[n + i];
+}
+
 // ---- key order of the comb (edv_set_key_sort) ------------------------------
 // A counting sort of a sub-batch's key ids: requests of one key become
 // neighbours, so a wave's 64 comb lanes gather from one key's rows (a few
@@ -1496,6 +1514,12 @@ struct edv_ctx {
   bool part_keyed = true;
   int part_err = 0;
   uint64_t part_launched = 0;
+  // edv_verify_staged_subset: each set's last submitted staged batch (its item count and message
+  // base, kept after the collect while its decoded signatures, spans and messages stay in HBM;
+  // cleared by the next reserve or begin of the set) and the subset's own buffers
+  uint64_t last_n[kSets] = {}, last_msg_base[kSets] = {};
+  bool last_ok[kSets] = {};
+  Buf sub_h, sub_d_in, sub_d_sig, sub_d_spans, sub_d_words, sub_h_bits;
   Buf& d_stage() { return d_stage_set[cur_set]; }
 };
 
@@ -2590,6 +2614,7 @@ int edv_stage_reserve(edv_ctx* ctx, uint64_t bytes) {
   if (ctx->set_ticket[ctx->cur_set])
     return set_err(EDV_EINVAL, "staging set %d holds an uncollected submission", ctx->cur_set);
   ctx->stage_err = 0;
+  ctx->last_ok[ctx->cur_set] = false;  // the puts that follow overwrite the last batch's messages
   if (ctx->d_stage().cap < bytes) {
     HIP_TRY(hipStreamSynchronize(ctx->stream_copy));  // earlier puts may still write the old buffer
     HIP_TRY(hipStreamSynchronize(ctx->stream));       // ... and earlier verifies read it
@@ -2692,6 +2717,9 @@ int edv_verify_staged_submit(edv_ctx* ctx, int keyed, const uint8_t* keys, uint6
   std::lock_guard<std::mutex> lk(ctx->stage_mu);
   ctx->set_ticket[set] = tk;
   ctx->set_n[set] = n;
+  ctx->last_n[set] = n;
+  ctx->last_msg_base[set] = msg_base;
+  ctx->last_ok[set] = n > 0;
   *ticket = tk;
   return 0;
 }
@@ -2719,6 +2747,7 @@ int edv_verify_staged_begin(edv_ctx* ctx, int keyed, uint64_t n, uint64_t* ticke
   const uint64_t tk = ctx->next_ticket++;
   ctx->set_ticket[set] = tk;
   ctx->set_n[set] = n;
+  ctx->last_ok[set] = false;  // (a speculative batch's parts may not cover it: no subsets of it)
   ctx->part_set = set;
   ctx->part_keyed = keyed != 0;
   ctx->part_err = 0;
@@ -2820,6 +2849,52 @@ int edv_verify_staged(edv_ctx* ctx, int keyed, const uint8_t* keys, uint64_t slo
   int r = edv_verify_staged_submit(ctx, keyed, keys, slot_off, msg_base, msg_start, msg_end, n, &ticket);
   if (r) return r;
   return edv_verify_staged_collect(ctx, ticket, accept_bits);
+}
+
+int edv_verify_staged_subset(edv_ctx* ctx, const uint32_t* idx, const uint8_t* pk32, uint64_t m,
+                             uint8_t* accept_bits) {
+  int r = set_device(ctx);
+  if (r) return r;
+  if (m == 0) return 0;
+  if (!idx || !pk32 || !accept_bits) return set_err(EDV_EINVAL, "null pointer");
+  const int set = ctx->cur_set;
+  uint64_t n = 0, base = 0;
+  {
+    std::lock_guard<std::mutex> lk(ctx->stage_mu);
+    if (ctx->set_ticket[set]) return set_err(EDV_EINVAL, "staging set %d holds an uncollected submission", set);
+    if (!ctx->last_ok[set]) return set_err(EDV_EINVAL, "staging set %d holds no submitted staged batch", set);
+    n = ctx->last_n[set];
+    base = ctx->last_msg_base[set];
+  }
+  uint64_t bad = 0;
+  for (uint64_t j = 0; j < m; ++j) bad |= (uint64_t)(idx[j] >= n);
+  if (bad) return set_err(EDV_EINVAL, "a subset index outside the staged batch of %llu", (unsigned long long)n);
+  const uint64_t nwords = div_up(m, 64);
+  // the keys first (16-byte aligned for the general path's loads), then the indices
+  if ((r = ensure_pinned(ctx->sub_h, 36 * m)) || (r = ensure(ctx->sub_d_in, 36 * m)) ||
+      (r = ensure(ctx->sub_d_sig, 64 * m)) || (r = ensure(ctx->sub_d_spans, 16 * m)) ||
+      (r = ensure(ctx->sub_d_words, 8 * nwords)) || (r = ensure_pinned(ctx->sub_h_bits, 8 * nwords)))
+    return r;
+  stage_copy(ctx->sub_h.p, pk32, 32 * m);
+  stage_copy((uint8_t*)ctx->sub_h.p + 32 * m, idx, 4 * m);
+  hipStream_t st = ctx->stream;
+  HIP_TRY(hipMemcpyAsync(ctx->sub_d_in.p, ctx->sub_h.p, 36 * m, hipMemcpyHostToDevice, st));
+  const uint8_t* d_pk = (const uint8_t*)ctx->sub_d_in.p;
+  const uint32_t* d_idx = (const uint32_t*)(d_pk + 32 * m);
+  uint64_t* d_sp = (uint64_t*)ctx->sub_d_spans.p;
+  hipLaunchKernelGGL(edv_subset_gather_kernel, dim3((uint32_t)div_up(m, kBlock)), dim3(kBlock), 0, st, d_idx, m, n,
+                     (const uint8_t*)ctx->s_sig[set].p, (const uint64_t*)ctx->d_spans[set].p,
+                     (uint8_t*)ctx->sub_d_sig.p, d_sp);
+  HIP_TRY(hipGetLastError());
+  set_bucketing(ctx, false);
+  r = launch_pipeline(ctx, false, ctx->sub_d_sig.p, d_pk, (const uint8_t*)ctx->d_stage_set[set].p + base, d_sp,
+                      d_sp + m, m, ctx->sub_d_words.p, st);
+  if (r) return r;
+  HIP_TRY(hipMemcpyAsync(ctx->sub_h_bits.p, ctx->sub_d_words.p, 8 * nwords, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  memcpy(accept_bits, ctx->sub_h_bits.p, (size_t)((m + 7) / 8));
+  if (m & 7) accept_bits[m / 8] &= (uint8_t)((1u << (m & 7)) - 1);
+  return 0;
 }
 
 int edv_verify_submit(edv_ctx* ctx, int keyed, const uint8_t* sig, int sig_format, const uint8_t* keys,
@@ -3007,7 +3082,9 @@ void edv_destroy(edv_ctx* ctx) {
   if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
   if (ctx->stream_key) (void)hipStreamSynchronize(ctx->stream_key);
   if (ctx->stream_build) (void)hipStreamSynchronize(ctx->stream_build);
-  for (edv_ctx::Buf* b : {&ctx->b_sig, &ctx->b_pk, &ctx->b_msg, &ctx->b_off, &ctx->b_bits, &ctx->b_aux, &ctx->b_build})
+  for (edv_ctx::Buf* b : {&ctx->b_sig, &ctx->b_pk, &ctx->b_msg, &ctx->b_off, &ctx->b_bits, &ctx->b_aux, &ctx->b_build,
+                          &ctx->sub_h, &ctx->sub_d_in, &ctx->sub_d_sig, &ctx->sub_d_spans, &ctx->sub_d_words,
+                          &ctx->sub_h_bits})
     free_buf(*b);
   for (int k = 0; k < edv_ctx::kSets; ++k) {
     for (edv_ctx::Buf* b : {&ctx->d_stage_set[k], &ctx->d_spans[k], &ctx->s_sig[k], &ctx->s_key[k], &ctx->s_bits[k],

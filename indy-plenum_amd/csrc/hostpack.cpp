@@ -2497,6 +2497,65 @@ PyObject* py_gather_spans(PyObject*, PyObject* args) {
                        (const char*)o.data(), (Py_ssize_t)(o.size() * 8));
 }
 
+// keys_known(clients, fast_keys, identifiers, field) -> (keys, holes): the authenticator's
+// per-identifier key resolution (SimpleAuthNr.getVerkey, client_authn.py:142-154, then the
+// remembered DidVerifier key) for the identifiers whose answer needs no Python: clients[idr] an
+// exact non-empty dict, its `field` entry the very verkey object fast_keys[idr] = (verkey, key)
+// remembers.  keys[j] = that key bytes, else None; holes = the j of the Nones (the caller's Python
+// path: getVerkey's state lookup, its exceptions, a changed verkey).  Only for an exact-dict
+// `clients` read by the known getVerkey (the caller checks); nothing here has side effects.
+PyObject* py_keys_known(PyObject*, PyObject* args) {
+  PyObject *clients, *fk, *idrs, *field;
+  if (!PyArg_ParseTuple(args, "O!O!O!O", &PyDict_Type, &clients, &PyDict_Type, &fk, &PyList_Type, &idrs, &field))
+    return nullptr;
+  if (!PyDict_CheckExact(clients) || !PyDict_CheckExact(fk) || !PyList_CheckExact(idrs)) {
+    PyErr_SetString(PyExc_TypeError, "keys_known: exact dicts and a list");
+    return nullptr;
+  }
+  const Py_ssize_t n = PyList_GET_SIZE(idrs);
+  PyObject* keys = PyList_New(n);
+  PyObject* holes = keys ? PyList_New(0) : nullptr;
+  if (!holes) {
+    Py_XDECREF(keys);
+    return nullptr;
+  }
+  for (Py_ssize_t j = 0; j < n; ++j) {
+    PyObject* idr = PyList_GET_ITEM(idrs, j);
+    PyObject* key = nullptr;
+    if (PyUnicode_CheckExact(idr)) {
+      PyObject* nym = PyDict_GetItemWithError(clients, idr);  // borrowed
+      if (nym && PyDict_CheckExact(nym) && PyDict_GET_SIZE(nym) > 0) {
+        PyObject* vk = PyDict_GetItemWithError(nym, field);
+        PyObject* e = vk ? PyDict_GetItemWithError(fk, idr) : nullptr;
+        if (e && PyTuple_CheckExact(e) && PyTuple_GET_SIZE(e) == 2 && PyTuple_GET_ITEM(e, 0) == vk &&
+            PyBytes_CheckExact(PyTuple_GET_ITEM(e, 1)))
+          key = PyTuple_GET_ITEM(e, 1);
+      }
+      if (PyErr_Occurred()) {
+        Py_DECREF(keys);
+        Py_DECREF(holes);
+        return nullptr;
+      }
+    }
+    if (key) {
+      Py_INCREF(key);
+      PyList_SET_ITEM(keys, j, key);
+    } else {
+      Py_INCREF(Py_None);
+      PyList_SET_ITEM(keys, j, Py_None);
+      PyObject* jj = PyLong_FromSsize_t(j);
+      if (!jj || PyList_Append(holes, jj) != 0) {
+        Py_XDECREF(jj);
+        Py_DECREF(keys);
+        Py_DECREF(holes);
+        return nullptr;
+      }
+      Py_DECREF(jj);
+    }
+  }
+  return Py_BuildValue("(NN)", keys, holes);
+}
+
 PyObject* py_gather_items(PyObject*, PyObject* args) {
   Py_buffer bs, bm, bo, bi;
   Py_ssize_t stride = 64;
@@ -2697,6 +2756,9 @@ PyMethodDef kMethods[] = {
      "scan_batch(msgs, ignore, threads=0, out=None) -> (fast, idrs, sig64, msgbuf, off, short): authenticate()'s "
      "host steps for a batch.  out = [bytearray, bytearray]: sig64 / msgbuf are written into them (grown, never "
      "shrunk: slice to n * 64 and off[n] bytes) and returned"},
+    {"keys_known", py_keys_known, METH_VARARGS,
+     "keys_known(clients, fast_keys, identifiers, field) -> (keys, holes): the remembered key of each identifier "
+     "whose clients entry still holds the remembered verkey, else None (holes: their positions)"},
     {"gather_spans", py_gather_spans, METH_VARARGS,
      "gather_spans(sig, msgbuf, spans_u64, idx_u32, stride=64) -> (sig_k, msg_k, off_k): gather_items for a staged "
      "batch's item spans (starts[n] then ends[n])"},

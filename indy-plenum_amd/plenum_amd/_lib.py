@@ -44,6 +44,7 @@ SIGNATURES = {
     "edv_verify_staged_begin": (_I, [_P, _I, _U64, _P]),
     "edv_verify_staged_part": (_I, [_P, _P, _U64, _U64, _P, _U64, _U64, _U64]),
     "edv_verify_staged_end": (_I, [_P]),
+    "edv_verify_staged_subset": (_I, [_P, _P, _P, _U64, _P]),
     "edv_set_unit_arena": (_I, [_P, _U64]),
     "edv_last_phase_ms": (_I, [_P, _P, _P, _P]),
     "edv_last_kernel_ms": (_c.c_double, [_P]),

@@ -49,6 +49,7 @@ import threading
 import os
 from abc import abstractmethod
 from collections import OrderedDict, deque
+from itertools import islice
 from time import monotonic
 from copy import deepcopy
 from typing import Dict
@@ -71,6 +72,10 @@ try:
                             results_ok as _results_ok, kid_map as _kid_map, kid_map_size as _kid_map_size)
 except ImportError:  # pragma: no cover
     _pack_range = _repack_spans = _gather_u32 = _results_ok = _kid_map = _kid_map_size = None
+try:  # the batch's per-identifier keys for the known getVerkey (SimpleAuthNr's dict lookup) in one call
+    from ._hostpack import keys_known as _keys_known
+except ImportError:  # pragma: no cover
+    _keys_known = None
 try:  # the node's per-message path: authenticate()'s host steps in one call; the verify-ahead's dedupe
     from ._hostpack import authn_key as _authn_key, distinct_sm as _distinct_sm
 except ImportError:  # pragma: no cover
@@ -111,6 +116,14 @@ SIGS = 'signatures'
 IDENTIFIER = 'identifier'
 REQ_ID = 'reqId'
 VERKEY = 'verkey'
+
+
+def _known_getverkey(cls):
+    """cls.getVerkey is SimpleAuthNr's -- this module's restatement or the reference's own
+    (client_authn.py:142-154): clients.get(identifier), the state only when that is empty."""
+    f = getattr(cls, "getVerkey", None)
+    return f is SimpleAuthNr.getVerkey or (getattr(f, "__qualname__", "") == "SimpleAuthNr.getVerkey" and
+                                            getattr(f, "__module__", "") == "plenum.server.client_authn")
 ROLE = 'role'
 
 KEY_STORE_BYTES = 32 << 30  # HBM for key tables: the window is the widest that fits max_keys
@@ -238,7 +251,7 @@ class _GpuState:
         # identifier -> (verkey as getVerkey returned it, key bytes): authenticate()'s per-message
         # DidVerifier step without the VerkeyCache call while the verkey stays the same
         self.fast_keys = {}
-        self.fast_keys_max = 1 << 16
+        self.fast_keys_max = 1 << 18  # (identifier -> (verkey, key): ~200 B each)
         self.kid_out = bytearray()  # a batch's key id per request (gather_u32 output, reused)
         # speculate=True (default): a synchronous staged batch runs its kernels under its own scan,
         # part by part, with key ids the scan takes from kid_map (identifier -> key id of the batches
@@ -392,11 +405,18 @@ class GpuAuthMixin:
         if fk is not None and (fk[0] is verkey or (verkey.__class__ is str and fk[0] == verkey)):
             return fk[1]
         key = self._resolve_key(verkey, identifier)
-        if verkey.__class__ is str and key.__class__ is bytes and identifier.__class__ is str:
-            if len(g.fast_keys) >= g.fast_keys_max:
-                g.fast_keys.clear()
-            g.fast_keys[identifier] = (verkey, key)
+        self._remember_key(identifier, verkey, key)
         return key
+
+    def _remember_key(self, identifier, verkey, key):
+        """fast_keys[identifier] = (verkey, key): valid while getVerkey(identifier) returns this
+        very verkey object.  Full: the oldest eighth goes (insertion order)."""
+        if verkey.__class__ is str and key.__class__ is bytes and identifier.__class__ is str:
+            fk = self._g.fast_keys
+            if len(fk) >= self._g.fast_keys_max and identifier not in fk:
+                for old in list(islice(fk, max(1, len(fk) // 8))):
+                    del fk[old]
+            fk[identifier] = (verkey, key)
 
     def _resolve_key(self, verkey, identifier):
         try:
@@ -416,6 +436,9 @@ class GpuAuthMixin:
             key = self._resolve_key(verkey, identifier)
         except Exception:
             return  # authenticate() raises the reference's error for this key later
+        # the batch path's per-identifier key lookup hits from the first batch on (the key is
+        # resolved here anyway); valid while clients[identifier] holds this verkey object
+        self._remember_key(identifier, verkey, key)
         if key and len(key) == 32:
             g = self._g
             g.pending[key] = None
@@ -671,6 +694,21 @@ class GpuAuthMixin:
         order of checks and exceptions), with the per-identifier key fast path
         inlined: a batch's ~1,000 identifiers in well under a millisecond."""
         fk = self._g.fast_keys
+        if (_keys_known is not None and type(getattr(self, "clients", None)) is dict and type(fk) is dict
+                and uniq.__class__ is list and _known_getverkey(type(self))):
+            # getVerkey is SimpleAuthNr's (a clients lookup, the state only for a miss, no side
+            # effects): the identifiers whose clients entry is the verkey fast_keys remembers need
+            # no Python; the rest (state lookups, exceptions, changed verkeys) take _keys_for_py
+            out, holes = _keys_known(self.clients, fk, uniq, VERKEY)
+            if holes:
+                for j, k in zip(holes, self._keys_for_py([uniq[j] for j in holes])):
+                    out[j] = k
+            return out
+        return self._keys_for_py(uniq)
+
+    def _keys_for_py(self, uniq):
+        """_keys_for in Python: any getVerkey, in the identifiers' order."""
+        fk = self._g.fast_keys
         get_verkey = self.getVerkey
         out = []
         append = out.append
@@ -890,8 +928,10 @@ class GpuAuthMixin:
         table (a signer population larger than the key store): one keyed
         verify of the whole staged batch over the store's ids (the others get
         an id the kernels reject), then the general path (the key bytes) for
-        the items of the other identifiers only, gathered from the pinned
-        buffers -- the same verdicts as per message."""
+        the items of the other identifiers only -- on the engine's copy of the
+        staged batch (edv_verify_staged_subset: indices and keys cross PCIe),
+        or gathered from the pinned buffers -- the same verdicts as per
+        message."""
         import numpy as np
         from time import perf_counter
         g = self._g
@@ -909,13 +949,18 @@ class GpuAuthMixin:
         is_gen[general_u] = True
         gen = np.flatnonzero(is_gen[uidx])
         if len(gen):
-            s_sig, s_msg, s_off = _gather_spans(memoryview(sig_o).cast("B")[:slot * n], msg_o, spans_b,
-                                                gen.astype(np.uint32).tobytes(), slot)
             ukey_arr = np.zeros((len(ukeys), 32), np.uint8)
             ukey_arr[general_u] = np.frombuffer(b"".join(ukeys[u] for u in general_u), np.uint8).reshape(-1, 32)
-            okg = np.asarray(eng.verify_batch(np.frombuffer(s_sig, np.uint8).reshape(-1, slot), ukey_arr[uidx[gen]],
-                                              np.frombuffer(s_msg, np.uint8), np.frombuffer(s_off, np.uint64),
-                                              **({"sig_slot": slot} if slot != 64 else {})), bool)
+            if getattr(eng, "supports_staged_subset", False):
+                # the staged batch is still in HBM: only the items' indices and key bytes go over
+                okg = np.asarray(eng.verify_staged_subset(gen.astype(np.uint32), ukey_arr[uidx[gen]]), bool)
+            else:
+                s_sig, s_msg, s_off = _gather_spans(memoryview(sig_o).cast("B")[:slot * n], msg_o, spans_b,
+                                                    gen.astype(np.uint32).tobytes(), slot)
+                okg = np.asarray(eng.verify_batch(np.frombuffer(s_sig, np.uint8).reshape(-1, slot),
+                                                  ukey_arr[uidx[gen]], np.frombuffer(s_msg, np.uint8),
+                                                  np.frombuffer(s_off, np.uint64),
+                                                  **({"sig_slot": slot} if slot != 64 else {})), bool)
             ok[gen] = okg
             # general-path keys earn a slot by verified requests (short items never verify)
             good = gen[okg & (np.frombuffer(short, np.uint8)[gen] == 0)]

@@ -287,6 +287,22 @@ class EdVerifyEngine:
         raises if a part failed (collect the handle all the same)."""
         check(self._lib.edv_verify_staged_end(self._ctx))
 
+    supports_staged_subset = True
+
+    def verify_staged_subset(self, idx, pk32):
+        """Verdicts of items idx of the last staged batch of the current set
+        again, on the general path with their own key bytes pk32 (m x 32)
+        (edv_verify_staged_subset): only idx and the keys cross PCIe."""
+        idx = np.ascontiguousarray(idx, dtype=np.uint32)
+        pk32 = _u8(pk32, 32)
+        m = idx.shape[0]
+        if pk32.shape[0] != m:
+            raise ValueError("shape mismatch: idx %d, keys %d" % (m, pk32.shape[0]))
+        bits = np.zeros((m + 7) // 8, dtype=np.uint8)
+        if m:
+            check(self._lib.edv_verify_staged_subset(self._ctx, _ptr(idx), _ptr(pk32), m, _ptr(bits)))
+        return unpack_bits(bits, m)
+
     def host_alloc(self, nbytes):
         """nbytes of pinned host memory (edv_host_alloc) as a writable ctypes
         array; host-pointer verifies copy inputs inside it to the device with no

@@ -292,6 +292,8 @@ class StagingOracleEngine(OracleEngine):
         self.held = [None, None]  # the uncollected submission of each set
         self.staged_calls = 0
         self.submits_staged = 0
+        self._last = [None, None]  # each set's last staged batch: (slot_off, msg_base, starts, ends)
+        self.subset_calls = 0
 
     @property
     def stage(self):
@@ -303,6 +305,7 @@ class StagingOracleEngine(OracleEngine):
 
     def stage_reserve(self, nbytes):
         assert self.held[self.cur] is None, "staging set %d holds an uncollected submission" % self.cur
+        self._last[self.cur] = None  # (edv_verify_staged_subset refuses the set from here)
         if len(self.stage) < nbytes:
             self.sets[self.cur] = (ctypes.c_ubyte * int(nbytes))()
 
@@ -329,6 +332,7 @@ class StagingOracleEngine(OracleEngine):
         assert keyed and self.held[self.cur] is None, "staging set %d holds an uncollected submission" % self.cur
         h = _Parts(self.cur, n, self.part_fail_at)
         self.held[self.cur] = h
+        self._last[self.cur] = None
         self.parts_begun = getattr(self, "parts_begun", 0) + 1
         self._open = h
         return h
@@ -373,8 +377,28 @@ class StagingOracleEngine(OracleEngine):
     def stager(self):
         return (ctypes.cast(self._put, ctypes.c_void_p).value, ctypes.addressof(self.stage))
 
+    supports_staged_subset = True
+
+    def verify_staged_subset(self, idx, pk32):
+        """edv_verify_staged_subset: items idx of the set's last staged batch, general path."""
+        last = self._last[self.cur]
+        assert last is not None and self.held[self.cur] is None, "no staged batch to take a subset of"
+        slot_off, msg_base, ms, me = last
+        idx = np.asarray(idx, np.int64)
+        assert idx.size == 0 or int(idx.max()) < len(ms)
+        self.subset_calls += 1
+        st = np.frombuffer(self.stage, np.uint8)
+        slots = st[slot_off:slot_off + 96 * len(ms)].reshape(-1, 96)[idx]
+        parts = [st[msg_base + int(ms[i]):msg_base + int(me[i])].tobytes() for i in idx]
+        off = np.zeros(len(idx) + 1, np.uint64)
+        off[1:] = np.cumsum([len(p) for p in parts])
+        return self.verify_batch(slots, np.asarray(pk32, np.uint8).reshape(-1, 32),
+                                 np.frombuffer(b"".join(parts), np.uint8), off, sig_slot=96)
+
     def verify_staged(self, keyed, keys, slot_off, msg_base, msg_start, msg_end):
         self.staged_calls += 1
+        self._last[self.cur] = (int(slot_off), int(msg_base), np.array(msg_start, np.uint64),
+                                np.array(msg_end, np.uint64))
         st = np.frombuffer(self.stage, np.uint8)
         n = len(msg_start)
         slots = st[slot_off:slot_off + 96 * n].reshape(-1, 96)

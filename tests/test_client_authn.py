@@ -990,6 +990,39 @@ def test_pipelined_speculative_batch_raising_scan_frees_the_sets(oracle, monkeyp
     assert list(a.authenticate_batches([steady, steady])) == [want, want]
 
 
+def test_keys_known_matches_getverkey_path(oracle):
+    """The batch's per-identifier keys from the native lookup (_hostpack.keys_known, for
+    SimpleAuthNr's getVerkey) equal the per-message path's outcomes: a verkey replaced by
+    addIdr after the first batch (old signatures now fail), an identifier known only to the
+    state lookup, an unknown one, a clients entry without a verkey, an empty clients entry."""
+    from plenum_amd import _hostpack
+    idrs, vks, msgs = _signed(6, 600)
+    state = {idrs[2]: {"verkey": vks[2]}, idrs[5]: {"verkey": vks[5]}}
+    a = GpuAuthNr(engine=OracleEngine(oracle), nym_lookup=lambda st, idr: state.get(idr, {}), max_keys=0)
+    for i, v in zip(idrs[:2], vks[:2]):
+        a.addIdr(i, v)
+    a.clients[idrs[3]] = {"verkey": None}
+    a.clients[idrs[5]] = {}  # empty: getVerkey asks the state
+    batch = [dict(m) for m in msgs if m["identifier"] != idrs[4]] + [dict(msgs[4], identifier="Unknown111111")]
+    first = [_outcome(r) for r in a.authenticate_batch(batch)]
+    assert first == [_outcome(_single(a, m)) for m in batch]
+    a.addIdr(idrs[1], vks[0])  # idrs[1]'s key replaced: its requests no longer verify
+    again = [_outcome(r) for r in a.authenticate_batch(batch)]
+    assert again == [_outcome(_single(a, m)) for m in batch]
+    assert again != first and ("InvalidSignature", (), None) in again
+    uniq = list(dict.fromkeys(m["identifier"] for m in batch))
+    keys, holes = _hostpack.keys_known(a.clients, a._g.fast_keys, uniq, "verkey")
+    assert [uniq[j] for j in holes] == [i for i in uniq if i not in (idrs[0], idrs[1])]
+    assert keys[uniq.index(idrs[0])] == a._g.fast_keys[idrs[0]][1]
+
+
+def _single(a, m):
+    try:
+        return a.authenticate(dict(m))
+    except Exception as ex:
+        return ex
+
+
 def test_verdict_cache_bounded_by_entries_bytes_and_age(oracle, monkeypatch):
     """The verify-ahead verdict cache (bounded by bytes, trimmed by
     age): entries beyond verdict_cache_size, bytes beyond verdict_cache_bytes
@@ -1064,10 +1097,12 @@ def test_promotions_decay_cap_and_one_build_call(oracle):
     assert k in g.hot
 
 
-def test_staged_mixed_batch_keyed_and_general(oracle, monkeypatch):
+@pytest.mark.parametrize("subset", [True, False])
+def test_staged_mixed_batch_keyed_and_general(oracle, monkeypatch, subset):
     """A staged batch whose signers outnumber the key store (identifiers known,
     only some keys built): one keyed verify of the staged batch plus the
-    general path for the other identifiers' items (gathered from the pinned
+    general path for the other identifiers' items (on the engine's copy of
+    the staged batch, edv_verify_staged_subset, or gathered from the pinned
     spans), forgeries and a short signature among both; every outcome equals
     the general path's, and the general items count towards promotion."""
     from engine_double import StagingOracleEngine
@@ -1077,6 +1112,7 @@ def test_staged_mixed_batch_keyed_and_general(oracle, monkeypatch):
     idrs, vks, msgs = _signed(5, 5000)
     table = dict(zip(idrs, vks))
     eng = StagingOracleEngine(oracle)
+    eng.supports_staged_subset = subset
     a = GpuAuthNr(engine=eng, nym_lookup=lambda st, idr: {"verkey": table[idr]}, max_keys=2, hot_key_uses=10 ** 9)
     for i, v in zip(idrs[:2], vks[:2]):
         a.addIdr(i, v)
@@ -1091,6 +1127,6 @@ def test_staged_mixed_batch_keyed_and_general(oracle, monkeypatch):
     got = [_outcome(r) for r in a.authenticate_batch(batch)]
     assert got == [_outcome(r) for r in ref.authenticate_batch(batch)]
     bd = a._g.last_breakdown
-    assert bd and bd["general_items"] > 0 and eng.staged_calls == 1
+    assert bd and bd["general_items"] > 0 and eng.staged_calls == 1 and eng.subset_calls == (1 if subset else 0)
     assert 0 < a.stats["keyed_items"] < len(batch)
     assert a._g.key_uses  # general-path keys counted
