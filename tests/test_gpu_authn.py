@@ -734,6 +734,50 @@ def _speculate_on_gpu(gpu_engine, batch, want, idrs, vks):
     assert [r if isinstance(r, str) else type(r).__name__ for r in res] == want
 
 
+def test_staged_subset_on_gpu(gpu_engine, sodium_verdicts):
+    """edv_verify_staged_subset: after a staged batch of 70,000 requests, a subset of its items
+    (every 7th, in a scrambled order, some twice) verified again by its own key bytes -- the
+    true keys, then a wrong key for every 3rd -- equals libsodium's verdicts on the same bytes;
+    refused once the set is reserved again, and for an index outside the batch."""
+    import copy
+    from plenum_amd import pack_messages
+    from plenum_amd._lib import EdVerifyError
+    from plenum_amd.base58 import b58decode
+    from plenum_amd.serialization import serialize_msg_for_signing
+    n = 70000
+    reqs, rx, idrs, vks, pks, sers, sig = _drain(gpu_engine, n_req=n, n_nodes=1)
+    with _own_key_store(gpu_engine):
+        a = GpuAuthNr(engine=gpu_engine, stage=True)
+        for idr, vk in zip(idrs, vks):
+            a.addIdr(idr, vk)
+        a.keys_settle()
+        batch = [copy.deepcopy(r) for r in reqs]
+        a.authenticate_batch(batch)  # the staged batch (set 0)
+        rng = np.random.default_rng(5)
+        idx = rng.permutation(np.arange(0, n, 7))
+        idx = np.concatenate([idx, idx[:100]]).astype(np.uint32)
+        key_of = {i: a._key_for(i) for i in set(r["identifier"] for r in batch)}
+        pk = np.stack([np.frombuffer(key_of[batch[i]["identifier"]], np.uint8) for i in idx])
+        sm = [b58decode(batch[i]["signature"]) + serialize_msg_for_signing(batch[i], topLevelKeysToIgnore=["signature"])
+              for i in idx]
+        sig64 = np.stack([np.frombuffer(x[:64], np.uint8) for x in sm])
+        buf, off = pack_messages([x[64:] for x in sm])
+        for wrong in (False, True):
+            k = pk.copy()
+            if wrong:
+                k[::3] = np.roll(pk, 1, axis=0)[::3]  # another request's key (mostly another signer)
+            got = np.asarray(gpu_engine.verify_staged_subset(idx, k), bool)
+            want = sodium_verdicts(sig64, k, buf, off[:-1], off[1:])
+            assert (got == want).all(), wrong
+            assert want.any() and (not wrong or not want.all())
+        with pytest.raises(EdVerifyError):
+            gpu_engine.verify_staged_subset(np.array([n], np.uint32), pk[:1])
+        gpu_engine.stage_select(0)
+        gpu_engine.stage_reserve(1 << 20)
+        with pytest.raises(EdVerifyError):
+            gpu_engine.verify_staged_subset(idx[:1], pk[:1])
+
+
 def test_key_churn_zipf_on_gpu(gpu_engine, sodium_verdicts):
     """VERDICT r4 'measure key churn': 100,000 signers registered with addIdr
     (more than the store's 16,384 slots), 300,000 json-decoded requests whose
