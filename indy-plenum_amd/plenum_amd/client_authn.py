@@ -843,69 +843,77 @@ class GpuAuthMixin:
             if parts is not None:
                 eng.verify_staged_collect(parts)
                 parts = None
-        if spans_b is spans_buf:
-            spans_b = memoryview(spans_b).cast("B")[:16 * n]
-        spans = np.frombuffer(spans_b, np.uint64, count=2 * n)
-        ms, me = spans[:n], spans[n:]
-        if not staged_ok:
-            drop_parts()
-            g.msg_bytes_per_item *= 1.5  # the next buffers are sized larger
-            return None
-        # (the chunks' reservations are contiguous from 0: their total is the largest span end)
-        g.msg_bytes_per_item = max(g.msg_bytes_per_item * 0.5, float(staged_bytes) / n if n else 0.0)
-        ukeys = self._keys_for(uniq)  # authenticate():93-99, once per identifier
-        ids = None
-        general_u = None  # distinct identifiers whose key has no built table: the general path
-        if ks is not None and fast_b.count(0) == 0 and all(k.__class__ is bytes and k for k in ukeys):
-            if g.hot or g.pending:
-                self._register_waiting(ks, list(dict.fromkeys(ukeys)))
-            ids = ks.lookup(ukeys)
-            if any(i is None for i in ids):
-                general_u = [u for u, i in enumerate(ids) if i is None]
-                ids = [0xffffffff if i is None else i for i in ids]  # (an id the kernels reject)
-        if ids is None:  # not the steady state: contiguous messages, the ordinary path
-            drop_parts()
-            del spans, ms, me
-            msg_c, off_c = _repack_spans(msg_o, spans_b)
-            return self._finish_scanned(msgs, (fast_b, uidx_b, uniq, sig_o, msg_c, off_c, short), slot, ukeys)
-        if general_u is not None:  # a mixed batch (key churn): the keyed verify, then the rest
-            drop_parts()
-            return self._staged_mixed(msgs, eng, slot, slot_base, ks, ukeys, ids, general_u, scan, spans_buf,
-                                      kid_buf, t0, t1)
-        ids_b = np.asarray(ids, np.uint32).tobytes()
-        spec_hit = parts is not None and parts_ok and spec_u == ids_b and ks.version == ks_version
-        if g.speculate and _kid_map is not None and (spec_u != ids_b or g.kid_map is None or
-                                                     g.kid_map_version != ks.version):
-            # remember this batch's ids for the next batch's scan (a fresh map when the store moved keys)
-            fresh = g.kid_map is None or g.kid_map_version != ks.version or _kid_map_size(g.kid_map) > g.kid_map_max
-            g.kid_map = _kid_map(None if fresh else g.kid_map, uniq, ids_b)
-            g.kid_map_version = ks.version
-        t2 = perf_counter()
-        g.stats["batches"] += 1
-        g.stats["batch_items"] += n
-        g.stats["keyed_items"] += n
-        g.stats["speculated"] = g.stats.get("speculated", 0) + (n if spec_hit else 0)
+        try:  # (anything raised before the parts are collected or dropped frees their set)
+            if spans_b is spans_buf:
+                spans_b = memoryview(spans_b).cast("B")[:16 * n]
+            spans = np.frombuffer(spans_b, np.uint64, count=2 * n)
+            ms, me = spans[:n], spans[n:]
+            if not staged_ok:
+                drop_parts()
+                g.msg_bytes_per_item *= 1.5  # the next buffers are sized larger
+                return None
+            # (the chunks' reservations are contiguous from 0: their total is the largest span end)
+            g.msg_bytes_per_item = max(g.msg_bytes_per_item * 0.5, float(staged_bytes) / n if n else 0.0)
+            ukeys = self._keys_for(uniq)  # authenticate():93-99, once per identifier
+            ids = None
+            general_u = None  # distinct identifiers whose key has no built table: the general path
+            if ks is not None and fast_b.count(0) == 0 and all(k.__class__ is bytes and k for k in ukeys):
+                if g.hot or g.pending:
+                    self._register_waiting(ks, list(dict.fromkeys(ukeys)))
+                ids = ks.lookup(ukeys)
+                if any(i is None for i in ids):
+                    general_u = [u for u, i in enumerate(ids) if i is None]
+                    ids = [0xffffffff if i is None else i for i in ids]  # (an id the kernels reject)
+            if ids is None:  # not the steady state: contiguous messages, the ordinary path
+                drop_parts()
+                del spans, ms, me
+                msg_c, off_c = _repack_spans(msg_o, spans_b)
+                return self._finish_scanned(msgs, (fast_b, uidx_b, uniq, sig_o, msg_c, off_c, short), slot, ukeys)
+            if general_u is not None:  # a mixed batch (key churn): the keyed verify, then the rest
+                drop_parts()
+                return self._staged_mixed(msgs, eng, slot, slot_base, ks, ukeys, ids, general_u, scan, spans_buf,
+                                          kid_buf, t0, t1)
+            ids_b = np.asarray(ids, np.uint32).tobytes()
+            spec_hit = parts is not None and parts_ok and spec_u == ids_b and ks.version == ks_version
+            if g.speculate and _kid_map is not None and (spec_u != ids_b or g.kid_map is None or
+                                                         g.kid_map_version != ks.version):
+                # remember this batch's ids for the next batch's scan (a fresh map when the store moved keys)
+                fresh = g.kid_map is None or g.kid_map_version != ks.version or _kid_map_size(g.kid_map) > g.kid_map_max
+                g.kid_map = _kid_map(None if fresh else g.kid_map, uniq, ids_b)
+                g.kid_map_version = ks.version
+            t2 = perf_counter()
+            g.stats["batches"] += 1
+            g.stats["batch_items"] += n
+            g.stats["keyed_items"] += n
+            g.stats["speculated"] = g.stats.get("speculated", 0) + (n if spec_hit else 0)
 
-        def verdicts(ok, t3):
-            results, failed = _results_ok(ok, short, uidx_b, uniq)
-            for i in failed:
-                results[i] = InvalidSignature()
-            t4 = perf_counter()
-            g.last_breakdown = {"scan_and_copies": (t1 - t0) * 1e3, "keys_and_ids": (t2 - t1) * 1e3,
-                                "verify_wait": (t3 - t2) * 1e3, "verdicts": (t4 - t3) * 1e3,
-                                "speculated": bool(spec_hit)}
-            return results
-        if spec_hit:  # the kernels ran under the scan with exactly these ids
-            ticket, parts = parts, None
-            del spans, ms, me, spans_b
-            if defer:  # (they may still run: collected when the caller asks for the results)
-                def finish_spec():
-                    with _engine_lock(eng):
-                        ok = np.asarray(eng.verify_staged_collect(ticket), bool)
-                    return verdicts(ok, perf_counter())
-                return finish_spec
-            ok = np.asarray(eng.verify_staged_collect(ticket), bool)
-            return verdicts(ok, perf_counter())
+            def verdicts(ok, t3):
+                results, failed = _results_ok(ok, short, uidx_b, uniq)
+                for i in failed:
+                    results[i] = InvalidSignature()
+                t4 = perf_counter()
+                g.last_breakdown = {"scan_and_copies": (t1 - t0) * 1e3, "keys_and_ids": (t2 - t1) * 1e3,
+                                    "verify_wait": (t3 - t2) * 1e3, "verdicts": (t4 - t3) * 1e3,
+                                    "speculated": bool(spec_hit)}
+                return results
+            if spec_hit:  # the kernels ran under the scan with exactly these ids
+                ticket, parts = parts, None
+                del spans, ms, me, spans_b
+                if defer:  # (they may still run: collected when the caller asks for the results)
+                    def finish_spec():
+                        with _engine_lock(eng):
+                            ok = np.asarray(eng.verify_staged_collect(ticket), bool)
+                        return verdicts(ok, perf_counter())
+                    return finish_spec
+                ok = np.asarray(eng.verify_staged_collect(ticket), bool)
+                return verdicts(ok, perf_counter())
+        except BaseException:
+            if parts is not None:
+                try:
+                    eng.verify_staged_collect(parts)
+                except Exception:
+                    pass
+            raise
         drop_parts()
         kid = np.frombuffer(_gather_u32(ids_b, uidx_b, kid_buf if kid_buf is not None else g.kid_out), np.uint32,
                             count=n)

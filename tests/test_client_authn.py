@@ -963,6 +963,27 @@ def test_speculative_staged_batch_raising_scan_frees_the_set(oracle, monkeypatch
     assert a.authenticate_batch(steady) == [m["identifier"] for m in steady]
 
 
+def test_speculative_batch_raising_after_the_scan_frees_the_set(oracle, monkeypatch):
+    """Something raising between the scan and the parts' collect (here the key store's lookup)
+    propagates and leaves neither staging set held; the next batch speculates again."""
+    from plenum_amd import keystore as KS
+    eng, a, ref, idrs, vks, msgs = _staged_pair(oracle, monkeypatch)
+    steady = [dict(m) for m in msgs if m["identifier"] in idrs[:4]]
+    a.authenticate_batch(steady)  # the kid map
+    real = KS.KeyStore.lookup
+
+    def boom(self, keys):
+        raise MemoryError("injected")
+    monkeypatch.setattr(KS.KeyStore, "lookup", boom)
+    with pytest.raises(MemoryError):
+        a.authenticate_batch(steady)
+    assert eng.held == [None, None]
+    monkeypatch.setattr(KS.KeyStore, "lookup", real)
+    before = a._g.stats.get("speculated", 0)
+    assert a.authenticate_batch(steady) == [m["identifier"] for m in steady]
+    assert a._g.stats["speculated"] == before + len(steady) and eng.held == [None, None]
+
+
 def test_pipelined_speculative_batch_raising_scan_frees_the_sets(oracle, monkeypatch):
     """authenticate_batches: a scan that raises while batch k's kernels are in
     flight and batch k + 1 speculates propagates, and neither staging set
