@@ -11,7 +11,10 @@ leaving stale ids.
 
 Capacity is bounded (max_keys tables at the chosen comb window); once full,
 least-recently-used keys are evicted in place (edv_keys_set rebuilds a slot),
-never a key the current batch is using.  Which keys get in is the caller's
+never a key the current batch is using.  Recency is a per-slot tick (the
+lookup call that last returned the slot's id; registration counts as a use),
+so a batch's lookups mark its keys with one vectorized store and an eviction
+picks the slots with the oldest ticks (ties: lowest slot).  Which keys get in is the caller's
 policy (client_authn.GpuAuthMixin): keys given to addIdr while there is free
 room, and keys that verified successfully hot_key_uses times.  A key whose
 registration fails (allocation, HIP error) is remembered as unregistrable and
@@ -54,8 +57,10 @@ class KeyStore:
         self.engine = engine
         self.window = window
         self.capacity = capacity
-        self._ids = OrderedDict()     # key bytes -> id, LRU order (oldest first)
-        self._slot_key = []           # id -> key bytes
+        self._ids = {}                # key bytes -> id
+        self._slot_key = []           # id -> key bytes (None: a retired slot)
+        self._used = np.zeros(max(int(capacity), 1), np.int64)  # id -> tick of its last use
+        self._tick = 1
         self._failed = OrderedDict()  # keys that could not be registered
         self._generation = None
         self._building = {}           # id -> ticket of its latest build (asynchronous registrations)
@@ -86,6 +91,7 @@ class KeyStore:
             self.engine.keys_set_window(self.window)
         self._ids.clear()
         self._slot_key = []
+        self._used[:] = 0
         self._building.clear()
         self._tickets.clear()
         self._generation = getattr(self.engine, "keys_generation", 0)
@@ -136,15 +142,38 @@ class KeyStore:
         if self._building:
             self._refresh()
         building = self._building
-        out = []
-        for k in keys:
+        get = self._ids.get
+        out = [get(k) for k in keys]
+        hit = [i for i in out if i is not None]
+        if hit:
+            self._used[hit] = self._tick  # (one tick per call: its keys are equally recent)
+            self._tick += 1
+        if building:
+            out = [None if i is not None and i in building else i for i in out]
+        return out
+
+    def _touch(self, ids):
+        if len(ids):
+            self._used[np.asarray(ids, np.int64)] = self._tick
+            self._tick += 1
+
+    def _victims(self, count, pinned):
+        """Up to count least-recently-used keys outside `pinned` (oldest tick first, then lowest slot)."""
+        n = len(self._slot_key)
+        if count <= 0 or n == 0:
+            return []
+        live = np.array([k is not None for k in self._slot_key], bool)
+        for k in pinned:
             i = self._ids.get(k)
             if i is not None:
-                self._ids.move_to_end(k)
-                if building and i in building:
-                    i = None
-            out.append(i)
-        return out
+                live[i] = False
+        cand = np.flatnonzero(live)
+        if len(cand) > count:
+            used = self._used[cand]
+            sel = np.argpartition(used, count - 1)[:count]
+            cand = cand[sel]
+        cand = cand[np.lexsort((cand, self._used[cand]))]
+        return [self._slot_key[i] for i in cand[:count]]
 
     def register(self, keys, pinned=(), evict=True, asynchronous=False):
         """Register keys not yet in the store: into free slots, then (evict)
@@ -174,12 +203,13 @@ class KeyStore:
             for j, k in enumerate(new):
                 self._ids[k] = first + j
                 self._slot_key.append(k)
+            if new:
+                self._touch(range(first, first + len(new)))
             if ticket is not None and new:
                 self._mark_building(range(first, first + len(new)), ticket)
             done += new
         if over and evict and hasattr(self.engine, "keys_set"):
-            pinned = set(pinned)
-            victims = [k for k in self._ids if k not in pinned][:len(over)]
+            victims = self._victims(len(over), pinned)
             if use_async and hasattr(self.engine, "keys_set_many_async") and victims:
                 # every eviction of this call in one upload and one build launch
                 pairs = list(zip(over, victims))
@@ -198,6 +228,7 @@ class KeyStore:
                     self._slot_key[sl] = k_new
                     self._ids[k_new] = sl
                     done.append(k_new)
+                self._touch(slots)
                 return done
             for k_new, k_old in zip(over, victims):
                 slot = self._ids.pop(k_old)
@@ -215,6 +246,7 @@ class KeyStore:
                     continue
                 self._slot_key[slot] = k_new
                 self._ids[k_new] = slot
+                self._touch([slot])
                 done.append(k_new)
         return done
 
