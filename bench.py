@@ -1195,6 +1195,10 @@ def main():
                          "valu_busy": (utilisation or {}).get(key, {}).get("valu_busy"),
                          "hbm_GBps": (utilisation or {}).get(key, {}).get("hbm_GBps"),
                          "clock_GHz": (utilisation or {}).get(key, {}).get("clock_GHz"),
+                         # the same achieved rate against the MAD peak at the clock the chip held under
+                         # this kernel (GRBM_GUI_ACTIVE): what the instruction mix and issue leave
+                         "frac_at_held_clock": (achieved / (peak * (utilisation or {}).get(key, {})["clock_GHz"] / 2.4)
+                                                if (utilisation or {}).get(key, {}).get("clock_GHz") else None),
                          "utilisation": utilisation,
                          "frac_survey": (n * RL.MAD_PER_VERIFY / (ms_per_step * 1e-3)) / RL.PEAK_MAD_PER_S,
                          "frac_survey_note": "SURVEY 8(d)'s a-priori 305,000 MAD per verify (ref10: decode A + 253 "
