@@ -4,7 +4,7 @@
 # takes 3, WRITE_SIZE 2 -- SQ 8, GRBM 2); --pmc is never combined with tracing
 # domains.  Summaries: python tools/pmc_summary.py gpurun_out/pmc
 export TMPDIR=/tmp
-ARGS="--steps 2 --warmup 1 --no-cpu --general-steps 1 --pipeline 1 --e2e-n 0 --e2e-c0 0 --dropin-steps 0"
+ARGS="--steps 2 --warmup 1 --no-cpu --general-steps 1 --pipeline 1 --e2e-n 0 --e2e-c0 0 --dropin-steps 0 --churn-signers 0 --drain-n 0 --bls-checks 0"
 OUT=gpurun_out/pmc
 mkdir -p $OUT
 timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 bench.py $ARGS > $OUT/fetch.log 2>&1 &&
