@@ -597,9 +597,10 @@ def time_e2e_devices(eng, reqs, idrs, vks, counts):
     out = {}
     n = len(reqs)
     for k in counts:
-        extra = [EdVerifyEngine(d) for d in range(1, k)]
-        me = MultiEngine(engines=[eng] + extra)
+        extra, me = [], None
         try:
+            extra = [EdVerifyEngine(d) for d in range(1, k)]
+            me = MultiEngine(engines=[eng] + extra)
             a = GpuAuthNr(engine=me)
             for idr, vk in zip(idrs, vks):
                 a.addIdr(idr, vk)
@@ -619,10 +620,12 @@ def time_e2e_devices(eng, reqs, idrs, vks, counts):
             out[str(k)] = {"engines": k, "value": n / t, "seconds": t, "accepted": ok,
                            "keyed_items_share": a.stats["keyed_items"] / max(1, a.stats["batch_items"]),
                            "keys_build_s_all_devices": keys_s}
+        except Exception as ex:  # (reported in the line; the headline and the other legs stand)
+            out[str(k)] = {"engines": k, "error": "%s: %s" % (type(ex).__name__, ex)}
         finally:
             for e in extra:
                 e.close()
-            if me._pool:
+            if me is not None and me._pool:
                 me._pool.shutdown()
         if eng.keys_count():
             eng.keys_reset()

@@ -30,7 +30,8 @@ def main(path):
             w["synchronous"] / 1e6, r(wv.get("synchronous")), w["pipelined"] / 1e6, r(wv.get("pipelined"))))
     for k, v in (d.get("end_to_end") or {}).items():
         if k == "by_devices":
-            print(" ", k, {kk: r(vv["value"] / 1e6, 2) for kk, vv in v.items() if isinstance(vv, dict)})
+            print(" ", k, {kk: (r(vv["value"] / 1e6, 2) if "value" in vv else vv.get("error"))
+                           for kk, vv in v.items() if isinstance(vv, dict)})
         elif k in ("node_drain", "bls_commit_round"):
             print(" ", k, {kk: (r(vv, 2) if isinstance(vv, float) else vv) for kk, vv in v.items()
                            if not isinstance(vv, (dict, list, str))})
