@@ -63,3 +63,17 @@ def test_authenticator_over_multi_engine(oracle):
     got = [r if isinstance(r, str) else type(r).__name__ for r in a.authenticate_batch(forged)]
     assert got == exp and a.stats["keyed_items"] == 300
     assert all(e.keys == me.engines[0].keys for e in me.engines)  # replicated store
+
+
+def test_bench_devices_leg_reports_a_failing_device(oracle, monkeypatch):
+    """bench.time_e2e_devices (end_to_end.by_devices): a device count whose engines cannot be
+    created is reported in its entry; the counts before it are measured, the run goes on."""
+    import bench
+    idrs, vks, msgs = T._signed(3, 300)
+
+    def no_device(d):
+        raise RuntimeError("no HIP device %d" % d)
+    monkeypatch.setattr(bench, "EdVerifyEngine", no_device)
+    out = bench.time_e2e_devices(OracleEngine(oracle), [dict(m) for m in msgs], idrs, vks, [1, 2])
+    assert out["1"]["accepted"] == 300 and out["1"]["engines"] == 1
+    assert out["2"] == {"engines": 2, "error": "RuntimeError: no HIP device 1"}
