@@ -914,16 +914,21 @@ def main():
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
-    phases = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
-        phases.append(eng.last_phases_ms())  # waits for this step's events
+        step()  # (queued back to back: nothing in the loop waits on the device)
     torch.cuda.synchronize()
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    # kernel phases (HIP events on the launch streams; every step is the same work): the last timed
+    # step's and three more, each read after its step (untimed, so the timed loop never waits)
+    phases = [eng.last_phases_ms()]
+    for _ in range(3):
+        step()
+        phases.append(eng.last_phases_ms())
+    torch.cuda.synchronize()
     if dist_on:
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
