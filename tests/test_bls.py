@@ -9,7 +9,6 @@ import os
 import random
 import sys
 
-import pytest
 
 from conftest import GOLDEN, ROOT
 

@@ -1,7 +1,6 @@
 """Parity of the HIP path (libplenum_edverify.so on the MI355X) with libsodium
 1.0.18 (golden vectors) and with the oracle (fresh random/adversarial
 batches).  Bit-exact: every accept bit must equal libsodium's verdict."""
-import ctypes
 import hashlib
 
 import numpy as np

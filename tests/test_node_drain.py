@@ -10,7 +10,6 @@
   one prefetch per drain, one decode per message (the reference loop gets the
   prefetch's objects back), one engine launch for the drain's distinct
   requests, and authenticate() outcomes identical to the bare loop's."""
-import json
 
 import pytest
 from engine_double import OracleEngine

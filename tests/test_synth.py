@@ -22,7 +22,7 @@ def test_signer_seeds_match_config_c0():
 
 
 def test_add_torsion_changes_R():
-    import sys, os
+    import sys
     from conftest import GOLDEN
     sys.path.insert(0, GOLDEN)
     import edwards as E
