@@ -24,6 +24,7 @@ table on the device), and asserts:
      the NYM in the reference's `clients` dict.
 With --write the summary goes to dropin_ref_check.json (committed evidence).
 """
+import ctypes
 import json
 import os
 import sys
@@ -66,6 +67,64 @@ def node_validate(authnr, frm, message):
         authnr.authenticate(message)
     except ref_exc.BaseExc as ex:
         raise ref_exc.SuspiciousNode(frm, ex, message) from ex
+
+
+def batch_vs_single(eng):
+    import base58
+    from plenum_amd import client_authn as CA
+    sod = R.sodium()
+
+    def b58s(b):  # (the stand-in's b58encode may return str or bytes)
+        e = base58.b58encode(b)
+        return e.decode() if isinstance(e, bytes) else e
+    keys = []
+    for i in range(5):
+        pk, sk = ctypes.create_string_buffer(32), ctypes.create_string_buffer(64)
+        sod.crypto_sign_seed_keypair(pk, sk, bytes([9, i + 1]) + b"\0" * 30)
+        keys.append((b58s(pk.raw[:16]), "~" + b58s(pk.raw[16:]), sk))
+    a = GpuSimpleAuthNr(engine=eng)
+    for idr, vk, _ in keys[:4]:  # keys[4]: unknown (the reference's state lookup finds nothing)
+        a.addIdr(idr, vk)
+    msgs = []
+    for j in range(300):
+        idr, _, sk = keys[j % 5]
+        m = {"identifier": idr, "reqId": 5000 + j, "operation": {"type": "1", "dest": "d%d" % j}}
+        ser = a.serializeForSig(m, topLevelKeysToIgnore=["signature"])
+        sig = ctypes.create_string_buffer(64)
+        sod.crypto_sign_detached(sig, None, ser, ctypes.c_ulonglong(len(ser)), sk)
+        msgs.append(dict(m, signature=b58s(sig.raw)))
+    for j in range(0, 300, 7):
+        msgs[j] = dict(msgs[j], reqId=msgs[j]["reqId"] + 1)  # forged after signing
+    native = [0]
+    real = CA._keys_known
+
+    def counted(*args):
+        native[0] += 1
+        return real(*args)
+    CA._keys_known = counted if real is not None else None
+
+    def outcome(r):
+        return r if isinstance(r, str) else type(r).__name__
+
+    def single(m):
+        try:
+            return a.authenticate(dict(m))
+        except Exception as ex:
+            return ex
+    rounds = []
+    try:
+        for change in (False, True):
+            if change:
+                a.addIdr(keys[1][0], keys[0][1])  # keys[1]'s identifier now holds keys[0]'s verkey
+            got = [outcome(r) for r in a.authenticate_batch([dict(m) for m in msgs])]
+            want = [outcome(single(m)) for m in msgs]
+            assert got == want, change
+            rounds.append(got)
+    finally:
+        CA._keys_known = real
+    assert rounds[0] != rounds[1] and "UnknownIdentifier" in rounds[0] and "InvalidSignature" in rounds[0]
+    return {"batch_vs_single_items": 2 * len(msgs), "batch_vs_single_matched": 2 * len(msgs),
+            "keys_known_native_calls": native[0], "known_getverkey": CA._known_getverkey(type(a))}
 
 
 def main():
@@ -138,6 +197,11 @@ def main():
     res = a.authenticate_batch(msgs)
     assert res[:4] == [good["msg"]["identifier"]] * 4 and isinstance(res[4], ref_exc.InvalidSignature)
     assert R.CALLS["crypto_sign_open"] == 0
+
+    # batch == single over many signers on the reference class, with the per-identifier keys of
+    # the batch from the native lookup where it applies (_hostpack.keys_known: the reference's own
+    # getVerkey, clients entries holding the verkey addIdr gave); then one verkey replaced
+    summary.update(batch_vs_single(eng))
     summary["ok"] = True
     print(json.dumps(summary))
     if "--write" in sys.argv:

@@ -26,6 +26,7 @@ def test_mixin_over_reference_simpleauthnr():
     assert got["ok"] and got["libsodium_crypto_sign_open_calls"] == 0 and got["engine_calls"] > 0
     assert got["raised"] == got["raised_reference_baseexc"] > 0
     assert got["authenticate_after_prefetch_engine_calls"] == 0
+    assert got["batch_vs_single_matched"] == got["batch_vs_single_items"] > 0
 
 
 def test_committed_record():
@@ -33,6 +34,10 @@ def test_committed_record():
     assert rec["ok"] and rec["matched"] == rec["cases"] == 64
     assert rec["libsodium_crypto_sign_open_calls"] == 0
     assert rec["forged_propagate"].startswith("SuspiciousNode")
+    # authenticate_batch == authenticate() over 5 signers on the reference class, before and after
+    # a verkey is replaced, with the batch's keys from the native lookup (the reference's getVerkey)
+    assert rec["batch_vs_single_matched"] == rec["batch_vs_single_items"] == 600
+    assert rec["known_getverkey"] and rec["keys_known_native_calls"] == 2
 
 
 @pytest.mark.skipif(not (os.path.exists(PY39) and os.path.isdir("/root/reference/crypto")),
