@@ -58,7 +58,7 @@ from .base58 import b58decode
 from .exceptions import (CouldNotAuthenticate, EmptyIdentifier, EmptySignature, InsufficientCorrectSignatures,
                          InsufficientSignatures, InvalidSignature, InvalidSignatureFormat, MissingIdentifier,
                          MissingSignature, SigningException, UnknownIdentifier)
-from .keystore import KeyStore, auto_window
+from .keystore import KeyStore, UseCounts, auto_window
 from .serialization import serialize_msg_for_signing
 from .verifier import DidVerifier, VerkeyCache
 
@@ -184,12 +184,12 @@ class _GpuState:
     """Per-authenticator GPU state (created on first use).
 
     Threads: the engine, its key store and the scan / staging buffers are
-    used only under _engine_lock.  The bookkeeping dicts -- verdicts,
-    key_uses, hot, pending -- are also updated outside it (authenticate()'s
-    cache hit and miss, _count_verified).  Every single dict operation is
-    atomic under the GIL, so concurrent callers cannot corrupt them; a race
-    between two threads can at most lose a use count (a key earns its slot a
-    request later) or evict one extra verdict (a later re-verify).  The node
+    used only under _engine_lock.  The bookkeeping dicts -- verdicts, hot,
+    pending -- are also updated outside it (authenticate()'s cache hit and
+    miss, _count_verified).  Every single dict operation is atomic under the
+    GIL, so concurrent callers cannot corrupt them; a race between two
+    threads can at most evict one extra verdict (a later re-verify).  The
+    use counts (key_uses, keystore.UseCounts) take their own lock.  The node
     calls authenticate() from its one looper thread (looper.py:141-151), as
     the reference does."""
 
@@ -215,8 +215,8 @@ class _GpuState:
         self.key_window = auto_window(max_keys, key_store_bytes) if key_window == "auto" else key_window
         self.max_keys = max_keys
         self.hot_key_uses = hot_key_uses
-        self.key_uses = OrderedDict()   # key -> (decayed successful general-path verifies, epoch) (bounded LRU)
         self.key_uses_max = 1 << 16
+        self.key_uses = UseCounts(self.key_uses_max)  # key -> decayed successful general-path verifies (bounded)
         self.max_promotions = max_promotions  # keys that earned a slot, registered per batch at most
         self.pending = OrderedDict()    # addIdr keys waiting for a free slot
         self.hot = OrderedDict()        # keys that earned a slot (hot_key_uses verified requests)
@@ -535,19 +535,8 @@ class GpuAuthMixin:
         g = self._g
         if g.max_keys <= 0:
             return
-        uses, h, now = g.key_uses, g.hot_key_uses, self._use_epoch()
-        for key, c in zip(keys, counts):
-            if not c:
-                continue
-            u, e = uses.pop(key, (0, now))
-            u = (u >> min(62, now - e)) + int(c)
-            if u >= h:
-                g.hot[key] = None
-                u = 0
-            if u:
-                uses[key] = (u, now)
-        while len(uses) > g.key_uses_max:
-            uses.popitem(last=False)
+        for key in g.key_uses.add(keys, counts, self._use_epoch(), g.hot_key_uses):
+            g.hot[key] = None
 
     def _verify_keyed(self, items, ids):
         """crypto_sign_open(sig || ser) against registered keys: the split at
@@ -974,7 +963,7 @@ class GpuAuthMixin:
             good = gen[okg & (np.frombuffer(short, np.uint8)[gen] == 0)]
             per_u = np.bincount(uidx[good], minlength=len(ukeys))
             hot_u = np.flatnonzero(per_u).tolist()
-            self._count_verified_keys([ukeys[u] for u in hot_u], [int(per_u[u]) for u in hot_u])
+            self._count_verified_keys([ukeys[u] for u in hot_u], per_u[hot_u])
         t3 = perf_counter()
         g.stats["batches"] += 1
         g.stats["batch_items"] += n

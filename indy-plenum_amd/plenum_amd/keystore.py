@@ -255,3 +255,122 @@ class KeyStore:
             self._failed[k] = None
         while len(self._failed) > 65536:
             self._failed.popitem(last=False)
+
+
+class UseCounts:
+    """Decayed verified-use counts of general-path keys, the state of the
+    promotion policy (client_authn.GpuAuthMixin._count_verified_keys): key ->
+    a row of three arrays (count, the epoch it was last counted at, the call
+    that last counted it).  Rows are dense (0 .. len-1; a released row is
+    filled from the end), so add() maps a batch's keys to rows with one
+    dict.setdefault per key and does the rest -- decay (a count halves per
+    epoch since it was last counted), summing, promotion -- as array
+    operations.  Bounded at cap keys: past it, the least recently counted are
+    dropped (down to 7/8 of cap, so a churning batch stream trims every few
+    batches, not every batch).  pop / len / in behave as on a dict of
+    (count, epoch)."""
+
+    def __init__(self, cap):
+        import threading
+        self.cap = cap
+        self._row = {}                        # key -> row
+        self._keys = np.empty(1024, object)   # row -> key
+        self._u = np.zeros(1024, np.int64)
+        self._e = np.zeros(1024, np.int64)
+        self._t = np.zeros(1024, np.int64)    # the add() call that last counted the row
+        self._tick = 0
+        self._lock = threading.Lock()         # add() is several steps, not one dict op
+
+    def __len__(self):
+        return len(self._row)
+
+    def __contains__(self, key):
+        return key in self._row
+
+    def pop(self, key, default=None):
+        with self._lock:
+            r = self._row.pop(key, None)
+            if r is None:
+                return default
+            out = (int(self._u[r]), int(self._e[r]))
+            self._compact(np.array([r]), len(self._row) + 1)
+            return out
+
+    def _compact(self, gone, n):
+        """Rows `gone` (sorted, already out of the dict) of the n in use are
+        freed: the rows past the new end that stay move into the holes."""
+        m = n - len(gone)
+        keep = np.ones(n - m, bool)
+        keep[gone[gone >= m] - m] = False
+        movers = m + np.flatnonzero(keep)
+        holes = gone[gone < m]
+        if len(holes):
+            for a in (self._keys, self._u, self._e, self._t):
+                a[holes] = a[movers]
+            self._row.update(zip(self._keys[holes].tolist(), holes.tolist()))
+        self._keys[m:n] = None
+
+    def add(self, keys, counts, now, hot_at):
+        """Counts counts[j] verified requests of keys[j] at epoch now.  Returns,
+        in input order, the keys whose count reached hot_at; their rows are
+        dropped (they earned a slot; a later count starts from zero).  A key may
+        appear more than once (two identifiers sharing a verkey): its counts
+        are summed."""
+        c = np.asarray(counts, np.int64).reshape(-1)
+        if not c.all():
+            j = np.flatnonzero(c)
+            keys, c = [keys[i] for i in j.tolist()], c[j]
+        if not len(c):
+            return []
+        with self._lock:
+            row = self._row
+            n0 = len(row)
+            if n0 + len(c) > len(self._u):
+                grow = max(n0 + len(c), 2 * len(self._u)) - len(self._u)
+                self._keys = np.concatenate([self._keys, np.empty(grow, object)])
+                self._u = np.concatenate([self._u, np.zeros(grow, np.int64)])
+                self._e = np.concatenate([self._e, np.zeros(grow, np.int64)])
+                self._t = np.concatenate([self._t, np.zeros(grow, np.int64)])
+            sd, ln = row.setdefault, row.__len__
+            R = np.fromiter([sd(k, ln()) for k in keys], np.int64, len(c))
+            n = len(row)
+            if n > n0:  # new keys: rows n0 .. n-1, first occurrences in input order
+                new = np.flatnonzero(R >= n0)
+                if len(new) != n - n0:
+                    _, fi = np.unique(R[new], return_index=True)
+                    new = new[fi]
+                karr = np.empty(len(c), object)
+                karr[:] = keys
+                self._keys[R[new]] = karr[new]
+                self._u[n0:n] = 0
+                self._e[n0:n] = now
+            cu = np.bincount(R, weights=c, minlength=n).astype(np.int64)
+            ur = np.flatnonzero(cu)
+            shift = np.clip(now - self._e[ur], 0, 62)
+            u = (self._u[ur] >> shift) + cu[ur]
+            self._u[ur] = u
+            self._e[ur] = now
+            self._t[ur] = self._tick
+            self._tick += 1
+            hot = u >= hot_at
+            out = []
+            if hot.any():
+                hot_rows = ur[hot]
+                is_hot = np.zeros(n, bool)
+                is_hot[hot_rows] = True
+                pos = np.flatnonzero(is_hot[R])
+                if len(pos) != len(hot_rows):
+                    _, fi = np.unique(R[pos], return_index=True)
+                    pos = np.sort(pos[fi])
+                out = self._keys[R[pos]].tolist()
+                for k in out:
+                    del row[k]
+                self._compact(hot_rows, n)
+                n -= len(hot_rows)
+            if n > self.cap:
+                drop = n - self.cap + self.cap // 8
+                v = np.sort(np.argpartition(self._t[:n], drop - 1)[:drop]) if drop < n else np.arange(n)
+                for k in self._keys[v].tolist():
+                    del row[k]
+                self._compact(v, n)
+            return out

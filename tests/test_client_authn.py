@@ -1151,3 +1151,70 @@ def test_staged_mixed_batch_keyed_and_general(oracle, monkeypatch, subset):
     assert bd and bd["general_items"] > 0 and eng.staged_calls == 1 and eng.subset_calls == (1 if subset else 0)
     assert 0 < a.stats["keyed_items"] < len(batch)
     assert a._g.key_uses  # general-path keys counted
+
+
+def _use_counts_dict(uses, keys, counts, now, h, cap):
+    """The promotion policy's counts as first written: an LRU OrderedDict of
+    key -> (decayed count, epoch), one key at a time (the checker for
+    keystore.UseCounts)."""
+    hot = []
+    for key, c in zip(keys, counts):
+        if not c:
+            continue
+        u, e = uses.pop(key, (0, now))
+        u = (u >> min(62, now - e)) + int(c)
+        if u >= h:
+            hot.append(key)
+            u = 0
+        if u:
+            uses[key] = (u, now)
+    while len(uses) > cap:
+        uses.popitem(last=False)
+    return hot
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_use_counts_match_the_dict_policy(seed):
+    """keystore.UseCounts (vectorized, one pass per batch) gives the same hot
+    keys, in the same order, and the same (count, epoch) per key as the
+    one-key-at-a-time dict, over random batches with decay epochs, zero
+    counts and promotions; with a bound, the kept keys are the most recently
+    counted ones."""
+    from collections import OrderedDict
+    from plenum_amd.keystore import UseCounts
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    universe = [bytes([i % 256, i // 256]) * 16 for i in range(3000)]
+    uc, ref = UseCounts(10 ** 6), OrderedDict()
+    now = 0
+    for step in range(60):
+        now += int(rng.integers(0, 2))
+        idx = rng.choice(len(universe), int(rng.integers(1, 400)), replace=False)
+        keys = [universe[i] for i in idx]
+        counts = rng.integers(0, 4, len(keys))
+        h = int(rng.integers(2, 9))
+        assert uc.add(keys, counts, now, h) == _use_counts_dict(ref, keys, counts, now, h, 10 ** 6)
+        assert len(uc) == len(ref)
+    for k in list(ref)[:200]:
+        assert uc.pop(k, None) == ref.pop(k)
+        assert k not in uc
+    assert uc.pop(universe[0] + b"x", "none") == "none"
+    # bounded: keys counted in later calls outlive earlier ones
+    uc = UseCounts(100)
+    for b in range(10):
+        uc.add(universe[b * 50:(b + 1) * 50], [1] * 50, 0, 10)
+        assert len(uc) <= 100
+    assert all(k in uc for k in universe[450:500])
+    assert not any(k in uc for k in universe[:300])
+
+
+def test_use_counts_sum_a_repeated_key():
+    """Two identifiers sharing a verkey bring it twice in one call: the counts
+    add up, and the key is reported hot once."""
+    from plenum_amd.keystore import UseCounts
+    uc = UseCounts(16)
+    k1, k2 = b"a" * 32, b"b" * 32
+    assert uc.add([k1, k2, k1], [1, 1, 1], 0, 2) == [k1]
+    assert k1 not in uc and uc.pop(k2) == (1, 0)
+    assert uc.add([k2, k2], [1, 1], 3, 3) == []
+    assert uc.pop(k2) == (2, 3)
