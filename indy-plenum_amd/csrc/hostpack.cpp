@@ -2519,9 +2519,87 @@ PyObject* py_keys_known(PyObject*, PyObject* args) {
     Py_XDECREF(keys);
     return nullptr;
   }
+#ifdef EDV_HAVE_DK
+  // A churning batch brings ~30k identifiers whose clients / fast_keys entries (100k-entry dicts)
+  // and nym dicts are cold: each lookup below is a chain of dependent cache misses.  The
+  // identifiers D, 2D, 3D ahead walk the same chains one link per iteration (hash -> index slot ->
+  // entry -> key, value and the nym dict's keys), with prefetches only, so the lookups find them
+  // cached.  Reads stay in bounds (slot < size, entry < nentries); a stale guess only wastes a
+  // prefetch.
+  constexpr Py_ssize_t kD = 8;
+  static const bool prefetch = !(getenv("EDV_KEYS_PREFETCH") && getenv("EDV_KEYS_PREFETCH")[0] == '0');  // A/B
+  const auto slot_of = [](PyObject* d, Py_hash_t h, const DkEntry*& ent, Py_ssize_t& ne) -> Py_ssize_t {
+    const DkHead* k = (const DkHead*)((const PyDictObject*)d)->ma_keys;
+    ent = dk_entries(d, ne);
+    if (!ent) return -1;
+    const Py_ssize_t sz = k->size, s = (Py_ssize_t)((size_t)h & (size_t)(sz - 1));
+    const Py_ssize_t ix = sz <= 0xff ? ((const int8_t*)k->idx)[s]
+                          : sz <= 0xffff ? ((const int16_t*)k->idx)[s]
+                          : sz <= 0xffffffffLL ? ((const int32_t*)k->idx)[s] : ((const int64_t*)k->idx)[s];
+    return ix >= 0 && ix < ne ? ix : -1;
+  };
+  const auto pf_slot = [](PyObject* d, Py_hash_t h) {
+    if (((const PyDictObject*)d)->ma_values) return;
+    const DkHead* k = (const DkHead*)((const PyDictObject*)d)->ma_keys;
+    const Py_ssize_t sz = k->size, w = sz <= 0xff ? 1 : sz <= 0xffff ? 2 : sz <= 0xffffffffLL ? 4 : 8;
+    __builtin_prefetch(k->idx + ((size_t)h & (size_t)(sz - 1)) * w);
+  };
+  const auto hash_of = [](PyObject* s) -> Py_hash_t {  // cached after the first call; -1: not an exact str
+    if (!PyUnicode_CheckExact(s)) return -1;
+    Py_hash_t h = ((PyASCIIObject*)s)->hash;
+    if (h == -1) {
+      h = PyObject_Hash(s);
+      if (h == -1) PyErr_Clear();
+    }
+    return h;
+  };
+#endif
   for (Py_ssize_t j = 0; j < n; ++j) {
     PyObject* idr = PyList_GET_ITEM(idrs, j);
     PyObject* key = nullptr;
+#ifdef EDV_HAVE_DK
+    const auto hash_at = [&](Py_ssize_t i) -> Py_hash_t {
+      PyObject* s = PyList_GET_ITEM(idrs, i);
+      return PyUnicode_CheckExact(s) ? ((PyASCIIObject*)s)->hash : -1;
+    };
+    const DkEntry* ent;
+    Py_ssize_t ne, ix;
+    if (prefetch && j + 4 * kD < n) {  // link 1: the index slots
+      const Py_hash_t h = hash_of(PyList_GET_ITEM(idrs, j + 4 * kD));
+      if (h != -1) {
+        pf_slot(clients, h);
+        pf_slot(fk, h);
+      }
+    }
+    if (prefetch && j + 3 * kD < n) {  // link 2: the entries
+      const Py_hash_t h = hash_at(j + 3 * kD);
+      if (h != -1) {
+        if ((ix = slot_of(clients, h, ent, ne)) >= 0) __builtin_prefetch(&ent[ix]);
+        if ((ix = slot_of(fk, h, ent, ne)) >= 0) __builtin_prefetch(&ent[ix]);
+      }
+    }
+    if (prefetch && j + 2 * kD < n) {  // link 3: the keys, the nym dicts and the (verkey, key) tuples
+      const Py_hash_t h = hash_at(j + 2 * kD);
+      if (h != -1) {
+        if ((ix = slot_of(clients, h, ent, ne)) >= 0 && ent[ix].h == h) {
+          __builtin_prefetch(ent[ix].k);
+          __builtin_prefetch(ent[ix].v);
+        }
+        if ((ix = slot_of(fk, h, ent, ne)) >= 0 && ent[ix].h == h) __builtin_prefetch(ent[ix].v);
+      }
+    }
+    if (prefetch && j + kD < n) {  // link 4: the nym dicts' key tables and the tuples' key bytes
+      const Py_hash_t h = hash_at(j + kD);
+      if (h != -1) {
+        if ((ix = slot_of(clients, h, ent, ne)) >= 0 && ent[ix].h == h && ent[ix].v &&
+            Py_TYPE(ent[ix].v) == &PyDict_Type)
+          __builtin_prefetch(((const PyDictObject*)ent[ix].v)->ma_keys);
+        if ((ix = slot_of(fk, h, ent, ne)) >= 0 && ent[ix].h == h && ent[ix].v && PyTuple_CheckExact(ent[ix].v) &&
+            PyTuple_GET_SIZE(ent[ix].v) == 2)
+          __builtin_prefetch(PyTuple_GET_ITEM(ent[ix].v, 1));
+      }
+    }
+#endif
     if (PyUnicode_CheckExact(idr)) {
       PyObject* nym = PyDict_GetItemWithError(clients, idr);  // borrowed
       if (nym && PyDict_CheckExact(nym) && PyDict_GET_SIZE(nym) > 0) {

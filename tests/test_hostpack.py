@@ -370,3 +370,62 @@ def test_scan_shapes_equal_generic_and_python(monkeypatch, threads):
         sm = b58decode_py(m["signature"]) + py_ser(m, ["signature"])
         assert sig64[64 * i:64 * i + 64] == sm[:64] and mbuf[offs[i]:offs[i + 1]] == sm[64:], (i, m)
     assert nfast > 3000
+
+
+def _keys_known_py(clients, fk, idrs, field):
+    """keys_known restated: the key bytes when clients[idr] is an exact non-empty dict whose
+    `field` entry is the very object fast_keys[idr] = (verkey, key bytes) remembers."""
+    missing = object()
+    keys, holes = [], []
+    for j, idr in enumerate(idrs):
+        key = None
+        if type(idr) is str:
+            nym = clients.get(idr)
+            if type(nym) is dict and nym:
+                vk = nym.get(field, missing)
+                e = fk.get(idr) if vk is not missing else None
+                if type(e) is tuple and len(e) == 2 and e[0] is vk and type(e[1]) is bytes:
+                    key = e[1]
+        keys.append(key)
+        if key is None:
+            holes.append(j)
+    return keys, holes
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_keys_known_many_identifiers(seed):
+    """keys_known over thousands of identifiers (its prefetch chain runs 8-32 identifiers
+    ahead) equals the restatement, with deleted dict entries, non-str and str-subclass
+    identifiers, non-ASCII text, nym values that are not exact dicts or are empty, a changed
+    verkey object, malformed fast-key entries, and duplicates."""
+    rng = random.Random(seed)
+
+    class S(str):
+        pass
+
+    class D(dict):
+        pass
+
+    clients, fk, idrs = {}, {}, []
+    for i in range(3000):
+        idr = "%022x" % rng.getrandbits(88) if i % 97 else "idé%d" % i
+        vk = "~vk%d" % i
+        kind = rng.randrange(12)
+        clients[idr] = ({"verkey": vk, "role": None} if kind < 7 else {} if kind == 7 else
+                        D(verkey=vk) if kind == 8 else [vk] if kind == 9 else {"role": None})
+        fk[idr] = ((vk, os.urandom(32)) if kind != 10 else (vk, "not bytes") if i % 2 else (vk,))
+        if kind == 11:
+            clients[idr] = {"verkey": "~vk%d" % i}  # an equal verkey, another object
+        idrs.append(idr)
+    for idr in rng.sample(idrs, 300):  # dummy slots in both dicts
+        del clients[idr]
+        if rng.random() < 0.5:
+            del fk[idr]
+    q = [(i + ".")[:-1] for i in rng.sample(idrs, 2500)]  # fresh str objects, as from a scan
+    q += [q[5], 12345, None, S(idrs[0]), "unknown", b"bytes"] + [(i + ".")[:-1] for i in rng.sample(idrs, 200)]
+    rng.shuffle(q)
+    got = H.keys_known(clients, fk, q, "verkey")
+    want = _keys_known_py(clients, fk, q, "verkey")
+    assert got[1] == want[1]
+    assert all(a is b for a, b in zip(got[0], want[0]))
+    assert 0 < len(got[1]) < len(q)
