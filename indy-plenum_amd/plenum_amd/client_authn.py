@@ -848,11 +848,12 @@ class GpuAuthMixin:
             general_u = None  # distinct identifiers whose key has no built table: the general path
             if ks is not None and fast_b.count(0) == 0 and all(k.__class__ is bytes and k for k in ukeys):
                 if g.hot or g.pending:
-                    self._register_waiting(ks, list(dict.fromkeys(ukeys)))
-                ids = ks.lookup(ukeys)
-                if any(i is None for i in ids):
-                    general_u = [u for u, i in enumerate(ids) if i is None]
-                    ids = [0xffffffff if i is None else i for i in ids]  # (an id the kernels reject)
+                    self._register_waiting(ks, ukeys)
+                ids = ks.lookup_array(ukeys)
+                if (ids < 0).any():
+                    general_u = np.flatnonzero(ids < 0)
+                    ids[general_u] = 0xffffffff  # (an id the kernels reject)
+                ids = ids.astype(np.uint32)
             if ids is None:  # not the steady state: contiguous messages, the ordinary path
                 drop_parts()
                 del spans, ms, me

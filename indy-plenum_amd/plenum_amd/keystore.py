@@ -152,6 +152,22 @@ class KeyStore:
             out = [None if i is not None and i in building else i for i in out]
         return out
 
+    def lookup_array(self, keys):
+        """lookup() as an int64 array, -1 where lookup() answers None (one
+        pass over the keys; the hits' ticks and the building filter vectorized)."""
+        self._sync()
+        if self._building:
+            self._refresh()
+        get = self._ids.get
+        ids = np.fromiter((get(k, -1) for k in keys), np.int64, len(keys))
+        hit = ids[ids >= 0]
+        if len(hit):
+            self._used[hit] = self._tick
+            self._tick += 1
+        if self._building:
+            ids[np.isin(ids, np.fromiter(self._building, np.int64, len(self._building)))] = -1
+        return ids
+
     def _touch(self, ids):
         if len(ids):
             self._used[np.asarray(ids, np.int64)] = self._tick
@@ -162,11 +178,10 @@ class KeyStore:
         n = len(self._slot_key)
         if count <= 0 or n == 0:
             return []
-        live = np.array([k is not None for k in self._slot_key], bool)
-        for k in pinned:
-            i = self._ids.get(k)
-            if i is not None:
-                live[i] = False
+        live = np.fromiter((k is not None for k in self._slot_key), bool, n)
+        get = self._ids.get
+        pid = np.fromiter((get(k, -1) for k in pinned), np.int64)
+        live[pid[pid >= 0]] = False
         cand = np.flatnonzero(live)
         if len(cand) > count:
             used = self._used[cand]

@@ -970,15 +970,15 @@ def test_speculative_batch_raising_after_the_scan_frees_the_set(oracle, monkeypa
     eng, a, ref, idrs, vks, msgs = _staged_pair(oracle, monkeypatch)
     steady = [dict(m) for m in msgs if m["identifier"] in idrs[:4]]
     a.authenticate_batch(steady)  # the kid map
-    real = KS.KeyStore.lookup
+    real = KS.KeyStore.lookup_array
 
     def boom(self, keys):
         raise MemoryError("injected")
-    monkeypatch.setattr(KS.KeyStore, "lookup", boom)
+    monkeypatch.setattr(KS.KeyStore, "lookup_array", boom)
     with pytest.raises(MemoryError):
         a.authenticate_batch(steady)
     assert eng.held == [None, None]
-    monkeypatch.setattr(KS.KeyStore, "lookup", real)
+    monkeypatch.setattr(KS.KeyStore, "lookup_array", real)
     before = a._g.stats.get("speculated", 0)
     assert a.authenticate_batch(steady) == [m["identifier"] for m in steady]
     assert a._g.stats["speculated"] == before + len(steady) and eng.held == [None, None]
@@ -1218,3 +1218,27 @@ def test_use_counts_sum_a_repeated_key():
     assert k1 not in uc and uc.pop(k2) == (1, 0)
     assert uc.add([k2, k2], [1, 1], 3, 3) == []
     assert uc.pop(k2) == (2, 3)
+
+
+def test_keystore_lookup_array_matches_lookup(oracle):
+    """KeyStore.lookup_array is lookup() as an array (-1 for None): unregistered keys, keys
+    whose asynchronous builds are still queued, repeated keys; both mark the hits used."""
+    import numpy as np
+    from engine_double import AsyncOracleEngine
+    from plenum_amd.keystore import KeyStore
+    eng = AsyncOracleEngine(oracle)
+    ks = KeyStore(eng, 10, 8)
+    keys = [bytes([i]) * 32 for i in range(12)]
+    ks.register(keys[:3], asynchronous=True)
+    eng.finish_builds()
+    ks.register(keys[3:6], asynchronous=True)  # building until finish_builds
+    q = keys + keys[:4]
+    want = [-1 if i is None else i for i in ks.lookup(q)]
+    t = ks._tick
+    assert ks.lookup_array(q).tolist() == want and ks._tick == t + 1
+    assert want[3:6] == [-1, -1, -1] and want[:3] == [0, 1, 2]
+    eng.finish_builds()
+    got = ks.lookup_array(q)
+    assert got.tolist() == [-1 if i is None else i for i in ks.lookup(q)] and (got[:6] >= 0).all()
+    assert (ks._used[got[got >= 0]] == ks._tick - 1).all()
+    assert ks.lookup_array([]).dtype == np.int64
