@@ -347,7 +347,12 @@ class UseCounts:
                 self._e = np.concatenate([self._e, np.zeros(grow, np.int64)])
                 self._t = np.concatenate([self._t, np.zeros(grow, np.int64)])
             sd, ln = row.setdefault, row.__len__
-            R = np.fromiter([sd(k, ln()) for k in keys], np.int64, len(c))
+            try:
+                R = np.fromiter([sd(k, ln()) for k in keys], np.int64, len(c))
+            except BaseException:  # (an unhashable key): drop the rows this call began
+                for k in [k for k, r in row.items() if r >= n0]:
+                    del row[k]
+                raise
             n = len(row)
             if n > n0:  # new keys: rows n0 .. n-1, first occurrences in input order
                 new = np.flatnonzero(R >= n0)

@@ -1218,6 +1218,9 @@ def test_use_counts_sum_a_repeated_key():
     assert k1 not in uc and uc.pop(k2) == (1, 0)
     assert uc.add([k2, k2], [1, 1], 3, 3) == []
     assert uc.pop(k2) == (2, 3)
+    with pytest.raises(TypeError):  # an unhashable key: nothing of that call stays
+        uc.add([k1, [1]], [1, 1], 3, 3)
+    assert len(uc) == 0 and uc.add([k1], [1], 3, 3) == [] and uc.pop(k1) == (1, 3)
 
 
 def test_keystore_lookup_array_matches_lookup(oracle):
