@@ -41,6 +41,7 @@
 #include "host_pool.h"
 #include "batch_encode.h"
 #include "comb.h"
+#include "fe_lanes.h"
 #include "sha256.h"
 #include "verify_core.h"
 
@@ -1037,6 +1038,92 @@ __device__ bool r_decode_part2(fe& x, RDecode& d, const uint32_t s[8]) {
   return true;
 }
 
+// The same decode with fe_pow22523's chain spread over wave 2's lanes (fe_lanes.h): lane 0 runs
+// the few products before and after it, every lane of the wave the chain.  EDV_SMALL_LANES=0: the
+// one-lane chain above (A/B).
+#ifndef EDV_SMALL_LANES
+#define EDV_SMALL_LANES 1
+#endif
+struct RDecodeL {
+  fe y, u, v, v3;           // lane 0
+  uint32_t t0, t1, t2;      // distributed (limb k in lane k)
+};
+__device__ void r_decode_part1_lanes(RDecodeL& d, const uint32_t s[8], uint32_t lane) {
+  fe z;
+  fe_0(z);
+  if (lane == 0) {
+    fe one, x;
+    fe_1(one);
+    fe_frombytes(d.y, s);
+    fe_sq_o<kSO>(d.u, d.y);
+    fe_mul_o<kSO>(d.v, d.u, fe_const_d());
+    fe_sub(d.u, d.u, one);
+    fe_carry(d.u);
+    fe_add(d.v, d.v, one);
+    fe_sq_o<kSO>(d.v3, d.v);
+    fe_mul_o<kSO>(d.v3, d.v3, d.v);
+    fe_sq_o<kSO>(x, d.v3);
+    fe_mul_o<kSO>(x, x, d.v);
+    fe_mul_o<kSO>(z, x, d.u);  // u v^7
+  }
+  const uint32_t k = lane & 15;
+  const LaneTerms sq = c_lane_sq.t[lane], mu = c_lane_mul.t[lane];
+  const uint32_t zd = dist_from_lane0(z, lane);
+  uint32_t t0 = dist_sq(zd, sq, k);
+  uint32_t t1 = dist_sqn(t0, 2, sq, k);
+  t1 = dist_mul(zd, t1, mu, k);
+  t0 = dist_mul(t0, t1, mu, k);
+  t0 = dist_sq(t0, sq, k);
+  t0 = dist_mul(t1, t0, mu, k);
+  t1 = dist_sqn(t0, 5, sq, k);
+  t0 = dist_mul(t1, t0, mu, k);
+  t1 = dist_sqn(t0, 10, sq, k);
+  t1 = dist_mul(t1, t0, mu, k);
+  uint32_t t2 = dist_sqn(t1, 20, sq, k);
+  t1 = dist_mul(t2, t1, mu, k);
+  t1 = dist_sqn(t1, 10, sq, k);
+  t0 = dist_mul(t1, t0, mu, k);
+  t1 = dist_sqn(t0, 50, sq, k);
+  t1 = dist_mul(t1, t0, mu, k);
+  d.t2 = dist_sqn(t1, 30, sq, k);
+  d.t0 = t0;
+  d.t1 = t1;
+}
+// every lane of the wave calls; lane 0's x and result are r_decode_part2's
+__device__ bool r_decode_part2_lanes(fe& x, RDecodeL& d, const uint32_t s[8], uint32_t lane) {
+  const uint32_t k = lane & 15;
+  const LaneTerms sq = c_lane_sq.t[lane], mu = c_lane_mul.t[lane];
+  uint32_t t2 = dist_sqn(d.t2, 70, sq, k);
+  uint32_t t1 = dist_mul(t2, d.t1, mu, k);
+  t1 = dist_sqn(t1, 50, sq, k);
+  uint32_t t0 = dist_mul(t1, d.t0, mu, k);
+  t0 = dist_sqn(t0, 2, sq, k);
+  fe pw;
+  dist_to_fe(pw, t0);  // (u v^7)^((p-5)/8), class C, in every lane
+  if (lane != 0) return false;
+  fe z;
+  fe_sq_o<kSO>(x, d.v3);
+  fe_mul_o<kSO>(x, x, d.v);
+  fe_mul_o<kSO>(z, x, d.u);
+  fe_mul_o<kSO>(x, pw, z);
+  fe_mul_o<kSO>(x, x, d.v3);
+  fe_mul_o<kSO>(x, x, d.u);   // u v^3 (u v^7)^((p-5)/8)
+  fe vxx, chk;
+  fe_sq_o<kSO>(vxx, x);
+  fe_mul_o<kSO>(vxx, vxx, d.v);
+  fe_sub(chk, vxx, d.u);
+  if (!fe_iszero(chk)) {
+    fe_add(chk, vxx, d.u);
+    if (!fe_iszero(chk)) return false;
+    fe_mul_o<kSO>(x, x, fe_const_sqrtm1());
+  }
+  if (fe_isnegative(x) != (s[7] >> 31)) {
+    fe_neg(x, x);
+    fe_carry(x);
+  }
+  return true;
+}
+
 constexpr int kSmallThreads = 192;
 // EDV_SMALL_PROFILE=1 (probe builds only, tools/small_probe.py): the wall clock (100 MHz) at the
 // phase boundaries of request 0, read back with edv_small_profile.
@@ -1074,7 +1161,11 @@ __global__ __launch_bounds__(kSmallThreads) void edv_verify_small_kernel(
   const uint64_t i = blockIdx.x;
   if (i >= n) return;  // block-uniform
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#if EDV_SMALL_LANES
+  RDecodeL rd;  // wave 2: R's decode, across the first barrier
+#else
   RDecode rd;  // wave 2, lane 0: R's decode, across the first barrier
+#endif
   const uint32_t key0 = key_idx[i];
   const bool in_range = key0 < key_count;
   const uint64_t key = in_range ? key0 : 0;
@@ -1112,15 +1203,24 @@ __global__ __launch_bounds__(kSmallThreads) void edv_verify_small_kernel(
       store_fe(sh.base + 30, P.T);
     }
     EDV_SP(2);
-  } else if (lane == 0) {
-    r_decode_part1(rd, sig);
+  } else {
+#if EDV_SMALL_LANES
+    r_decode_part1_lanes(rd, sig, (uint32_t)lane);
+#else
+    if (lane == 0) r_decode_part1(rd, sig);
+#endif
     EDV_SP(3);
   }
   __syncthreads();
   if (wave == 2) {
+    fe x;
+#if EDV_SMALL_LANES
+    const bool dec = r_decode_part2_lanes(x, rd, sig, (uint32_t)lane);  // false: no root (lane 0)
+#endif
     if (lane == 0) {
-      fe x;
+#if !EDV_SMALL_LANES
       const bool dec = r_decode_part2(x, rd, sig);  // false: y^2 - 1 / (d y^2 + 1) has no root
+#endif
       const bool zero_signed = (sig[7] >> 31) && fe_iszero(x);
       store_fe(sh.xr, x);
       store_fe(sh.yr, rd.y);

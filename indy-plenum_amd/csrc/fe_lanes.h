@@ -1,0 +1,111 @@
+// GF(2^255 - 19) squarings and products spread over one wave's lanes, for the one dependent chain
+// of a single request (edv_verify_small_kernel's R decode: fe_pow22523's 250 squarings and 11
+// products).  On one lane that chain issues its 55-100 v_mad_u64_u32 one after another; here the
+// element sits in lanes 0..9 (limb k, radix 2^25.5 as fe25519.h) and lane 16r + k forms terms
+// 2r, 2r + 1 (a square) or 3r .. 3r + 2 (a product) of column k -- operands fetched with
+// ds_bpermute, the x2 (odd x odd, and i != j in a square) and x19 (past 2^255) factors from a
+// per-lane table --, the four rows of 16 are summed with permlane32 / permlane16 swaps, and two
+// carry rounds pass each limb's carry one lane up (lane 0 takes 19 x lane 9's).  252 dependent
+// squarings: 99k shader cycles against 135-170k on one lane (tools/microbench/ubench_lanesq.hip,
+// profiles/r09h).
+//
+// Bounds: inputs with even limbs <= 2^26 + 2^20 and odd limbs <= 2^25 + 2^18 (class C, or a
+// dist_* output); a term <= 2^28.1 x 2^30.3, a column of <= 10 terms < 2^61; the first carry round
+// leaves <= 2^40.3, the second limbs <= 2^26 + 2^19.6 (limb 0) / 2^26 + 2^15.3 -- inside the input
+// bounds.  dist_to_fe's fe_carry brings a result back to class C for the one-lane code.
+#pragma once
+#include "fe25519.h"
+
+namespace edv {
+
+struct LaneTerms {
+  uint32_t ia[3], ib[3], ma[3], mb[3];  // factor 0: an empty slot
+};
+struct LaneTab {
+  LaneTerms t[64];
+};
+constexpr LaneTab make_lane_tab(bool square) {
+  LaneTab tab{};
+  for (int k = 0; k < 10; ++k) {
+    int q = 0;
+    for (int i = 0; i < 10; ++i)
+      for (int j = square ? i : 0; j < 10; ++j) {
+        if ((i + j) % 10 != k) continue;
+        const int per = square ? 2 : 3, lane = (q / per) * 16 + k, s = q % per;
+        const bool odd2 = (i & 1) && (j & 1);
+        tab.t[lane].ia[s] = (uint32_t)i;
+        tab.t[lane].ib[s] = (uint32_t)j;
+        tab.t[lane].ma[s] = (square && i != j ? 2u : 1u) * (odd2 ? 2u : 1u);
+        tab.t[lane].mb[s] = i + j >= 10 ? 19u : 1u;
+        ++q;
+      }
+  }
+  return tab;
+}
+__constant__ LaneTab c_lane_sq = make_lane_tab(true);
+__constant__ LaneTab c_lane_mul = make_lane_tab(false);
+
+__device__ __forceinline__ uint32_t lane_bperm(uint32_t src_lane, uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane << 2), (int)v);
+}
+
+// the column sums of lanes 16r + k summed into lane k, then carried: limb k in lane k
+__device__ __forceinline__ uint32_t lane_cols_carry(uint64_t p, uint32_t k) {
+  uint32_t lo = (uint32_t)p, hi = (uint32_t)(p >> 32);
+  auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);  // [1]: lanes 0-31 <- lanes 32-63
+  auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  p += ((uint64_t)rh[1] << 32) | rl[1];
+  lo = (uint32_t)p, hi = (uint32_t)(p >> 32);
+  auto sl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);  // [1]: row 0 <- row 1
+  auto sh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  p += ((uint64_t)sh[1] << 32) | sl[1];
+  const uint32_t w = (k & 1) ? 25 : 26, mask = (1u << w) - 1, src = k == 0 ? 9 : k - 1, m = k == 0 ? 19 : 1;
+  const uint64_t c = p >> w;
+  const uint32_t cl = lane_bperm(src, (uint32_t)c), ch = lane_bperm(src, (uint32_t)(c >> 32));
+  const uint64_t s = ((uint64_t)ch << 32 | cl) * m + ((uint32_t)p & mask);
+  const uint32_t c2 = lane_bperm(src, (uint32_t)(s >> w));
+  return ((uint32_t)s & mask) + c2 * m;
+}
+
+// f^2; every lane of the wave takes part (t = c_lane_sq.t[lane], k = lane & 15)
+__device__ __forceinline__ uint32_t dist_sq(uint32_t f, const LaneTerms& t, uint32_t k) {
+  const uint32_t a0 = lane_bperm(t.ia[0], f), b0 = lane_bperm(t.ib[0], f);
+  const uint32_t a1 = lane_bperm(t.ia[1], f), b1 = lane_bperm(t.ib[1], f);
+  uint64_t p = (uint64_t)(a0 * t.ma[0]) * (b0 * t.mb[0]);
+  p += (uint64_t)(a1 * t.ma[1]) * (b1 * t.mb[1]);
+  return lane_cols_carry(p, k);
+}
+__device__ __forceinline__ uint32_t dist_sqn(uint32_t f, int n, const LaneTerms& t, uint32_t k) {
+#pragma unroll 1
+  for (int i = 0; i < n; ++i) f = dist_sq(f, t, k);
+  return f;
+}
+// f g (t = c_lane_mul.t[lane])
+__device__ __forceinline__ uint32_t dist_mul(uint32_t f, uint32_t g, const LaneTerms& t, uint32_t k) {
+  uint64_t p = 0;
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    const uint32_t a = lane_bperm(t.ia[s], f), b = lane_bperm(t.ib[s], g);
+    p += (uint64_t)(a * t.ma[s]) * (b * t.mb[s]);
+  }
+  return lane_cols_carry(p, k);
+}
+
+// lane 0's f as the distributed form (every lane calls; other lanes' f is ignored)
+__device__ __forceinline__ uint32_t dist_from_lane0(const fe& f, uint32_t lane) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+    const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)f.v[k], 0);
+    r = lane == (uint32_t)k ? v : r;
+  }
+  return r;
+}
+// the distributed d as an fe (class C) in every lane
+__device__ __forceinline__ void dist_to_fe(fe& f, uint32_t d) {
+#pragma unroll
+  for (int k = 0; k < 10; ++k) f.v[k] = (uint32_t)__builtin_amdgcn_readlane((int)d, k);
+  fe_carry(f);
+}
+
+}  // namespace edv
