@@ -1124,6 +1124,116 @@ __device__ bool r_decode_part2_lanes(fe& x, RDecodeL& d, const uint32_t s[8], ui
   return true;
 }
 
+// verify_phase_hash for the single-request kernel: SHA-512(R || A || M) with the blocks' message
+// schedules on wave 0's lanes (lane j: block p0 + j of a pass of kHashPass blocks, its 80 words
+// into LDS) and only the rounds on lane 0 -- the schedule is ~35 % of a round's instructions, and
+// on one lane every instruction is on the critical path.  Every lane of the wave calls; lane 0's
+// h and result are verify_phase_hash's.  EDV_SMALL_HASH_LANES=0: verify_phase_hash on lane 0 (A/B).
+#ifndef EDV_SMALL_HASH_LANES
+#define EDV_SMALL_HASH_LANES 1
+#endif
+constexpr int kHashPass = 8;
+constexpr int kHashRow = 81;  // u64 per block row (odd: the lanes' rows start in different banks)
+__device__ __forceinline__ void sha512_schedule_lds(uint64_t* out, uint64_t w[16]) {
+#pragma unroll
+  for (int t = 0; t < 16; ++t) out[t] = w[t];
+#pragma unroll 1
+  for (int r = 16; r < 80; r += 16) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const uint64_t w15 = w[(i + 1) & 15], w2 = w[(i + 14) & 15];
+      const uint64_t s0 = xor3_64(rotr64(w15, 1), rotr64(w15, 8), shr64(w15, 7));
+      const uint64_t s1 = xor3_64(rotr64(w2, 19), rotr64(w2, 61), shr64(w2, 6));
+      w[i] += s0 + w[(i + 9) & 15] + s1;
+      out[r + i] = w[i];
+    }
+  }
+}
+__device__ __forceinline__ void sha512_rounds_lds(uint64_t st[8], const uint64_t* w) {
+  uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll 1
+  for (int r = 0; r < 80; r += 16) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const uint64_t S1 = xor3_64(rotr64(e, 14), rotr64(e, 18), rotr64(e, 41));
+      const uint64_t ch = bitop3_64<0xca>(e, f, g);
+      const uint64_t t1 = h + S1 + ch + SHA512_K[r + i] + w[r + i];
+      const uint64_t S0 = xor3_64(rotr64(a, 28), rotr64(a, 34), rotr64(a, 39));
+      const uint64_t mj = bitop3_64<0xe8>(a, b, c);
+      h = g;
+      g = f;
+      f = e;
+      e = d + t1;
+      d = c;
+      c = b;
+      b = a;
+      a = t1 + S0 + mj;
+    }
+  }
+  st[0] += a;
+  st[1] += b;
+  st[2] += c;
+  st[3] += d;
+  st[4] += e;
+  st[5] += f;
+  st[6] += g;
+  st[7] += h;
+}
+__device__ bool verify_phase_hash_lanes(uint32_t hout[8], const uint32_t sig[16], const uint32_t pk[8],
+                                        const uint8_t* msg, uint64_t mlen, uint32_t lane, uint64_t* sw) {
+  constexpr int NP = 16;
+  uint32_t prefix[16];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    prefix[k] = sig[k];
+    prefix[8 + k] = pk[k];
+  }
+  const uint64_t total = 4 * NP + mlen, nblocks = (total + 16) / 128 + 1, bitlen = total * 8;
+  const uint32_t d16 = (uint32_t)((uintptr_t)msg & 15);
+  const Chunk16* c16 = (const Chunk16*)(msg - d16);
+  const uint64_t nq = (d16 + mlen + 15) / 16;
+  uint64_t st[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL, 0xa54ff53a5f1d36f1ULL,
+                    0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL, 0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
+#pragma unroll 1
+  for (uint64_t p0 = 0; p0 < nblocks; p0 += kHashPass) {
+    const uint64_t b = p0 + lane;
+    if (lane < (uint32_t)kHashPass && b < nblocks) {
+      uint64_t w[16];
+      if (b == 0)
+        sha512_block_words<NP, true>(w, 0, prefix, c16, nq, d16, mlen);
+      else
+        sha512_block_words<NP, false>(w, b, prefix, c16, nq, d16, mlen);
+      if (b == nblocks - 1) {
+        w[14] = 0;
+        w[15] = bitlen;
+      }
+      sha512_schedule_lds(sw + lane * kHashRow, w);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane == 0) {
+      const uint64_t nb = nblocks - p0 < (uint64_t)kHashPass ? nblocks - p0 : (uint64_t)kHashPass;
+#pragma unroll 1
+      for (uint64_t j = 0; j < nb; ++j) sha512_rounds_lds(st, sw + j * kHashRow);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the next pass overwrites sw
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  if (lane != 0) return false;
+  uint32_t digest[16];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    digest[2 * j] = bswap32((uint32_t)(st[j] >> 32));
+    digest[2 * j + 1] = bswap32((uint32_t)st[j]);
+  }
+  const uint32_t* S = sig + 8;
+  const bool ok = sc_is_canonical(S) && !has_small_order(sig) && is_canonical_point(pk) && !has_small_order(pk);
+  sc_reduce(hout, digest);
+  return ok;
+}
+
 constexpr int kSmallThreads = 192;
 // EDV_SMALL_PROFILE=1 (probe builds only, tools/small_probe.py): the wall clock (100 MHz) at the
 // phase boundaries of request 0, read back with edv_small_profile.
@@ -1142,6 +1252,7 @@ __device__ unsigned long long g_small_prof[10];  // [8], [9]: the shader clock a
   } while (0)
 #endif
 struct SmallShared {
+  uint64_t sw[kHashPass * kHashRow];  // wave 0's message schedules (verify_phase_hash_lanes)
   uint32_t h[8];
   uint32_t xr[10], yr[10];  // R decoded (wave 2)
   uint32_t base[40];        // [S]B (wave 1): X, Y, Z, T
@@ -1176,10 +1287,18 @@ __global__ __launch_bounds__(kSmallThreads) void edv_verify_small_kernel(
 #endif
   load_words(sig, sig64 + 64 * i, 16);
   if (wave == 0) {
+#if EDV_SMALL_HASH_LANES
+    uint32_t pk[8], h[8];
+    load_words(pk, key_pk + 32 * key, 8);
+    const bool hok = verify_phase_hash_lanes(h, sig, pk, msgs + ms[i], me[i] - ms[i], (uint32_t)lane, sh.sw);
+    if (lane == 0) {
+      const bool ok = hok && in_range && key_valid[key];
+#else
     if (lane == 0) {
       uint32_t pk[8], h[8];
       load_words(pk, key_pk + 32 * key, 8);
       const bool ok = verify_phase_hash(h, sig, pk, msgs + ms[i], me[i] - ms[i]) && in_range && key_valid[key];
+#endif
 #pragma unroll
       for (int k = 0; k < 8; ++k) sh.h[k] = h[k];
       sh.ok_hash = ok ? 1 : 0;
