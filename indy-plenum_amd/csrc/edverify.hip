@@ -1045,7 +1045,7 @@ __device__ bool r_decode_part2(fe& x, RDecode& d, const uint32_t s[8]) {
 #define EDV_SMALL_LANES 1
 #endif
 struct RDecodeL {
-  fe y, u, v, v3;           // lane 0
+  fe y, u, v, v3, uv7;      // lane 0
   uint32_t t0, t1, t2;      // distributed (limb k in lane k)
 };
 __device__ void r_decode_part1_lanes(RDecodeL& d, const uint32_t s[8], uint32_t lane) {
@@ -1065,6 +1065,7 @@ __device__ void r_decode_part1_lanes(RDecodeL& d, const uint32_t s[8], uint32_t 
     fe_sq_o<kSO>(x, d.v3);
     fe_mul_o<kSO>(x, x, d.v);
     fe_mul_o<kSO>(z, x, d.u);  // u v^7
+    d.uv7 = z;                 // (part 2 needs it again)
   }
   const uint32_t k = lane & 15;
   const LaneTerms sq = c_lane_sq.t[lane], mu = c_lane_mul.t[lane];
@@ -1101,11 +1102,7 @@ __device__ bool r_decode_part2_lanes(fe& x, RDecodeL& d, const uint32_t s[8], ui
   fe pw;
   dist_to_fe(pw, t0);  // (u v^7)^((p-5)/8), class C, in every lane
   if (lane != 0) return false;
-  fe z;
-  fe_sq_o<kSO>(x, d.v3);
-  fe_mul_o<kSO>(x, x, d.v);
-  fe_mul_o<kSO>(z, x, d.u);
-  fe_mul_o<kSO>(x, pw, z);
+  fe_mul_o<kSO>(x, pw, d.uv7);
   fe_mul_o<kSO>(x, x, d.v3);
   fe_mul_o<kSO>(x, x, d.u);   // u v^3 (u v^7)^((p-5)/8)
   fe vxx, chk;
