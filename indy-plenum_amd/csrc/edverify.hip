@@ -1362,19 +1362,21 @@ __global__ __launch_bounds__(kSmallThreads) void edv_verify_small_kernel(
     lane_tree_sum(P, lane, WK);
     EDV_SP(6);
   }
+  ge_p2 Q;
+  if (wave == 0 && lane == 0) {  // R' while wave 2 still decodes R ([S]B is in LDS since the first barrier)
+    ge_p3 B;
+    load_fe(B.X, sh.base);
+    load_fe(B.Y, sh.base + 10);
+    load_fe(B.Z, sh.base + 20);
+    load_fe(B.T, sh.base + 30);
+    ge_cached c;
+    ge_p1p1 t;
+    ge_p3_to_cached<kSO>(c, B);
+    ge_add<kSO>(t, P, c);
+    ge_p1p1_to_p2_addlike<kSO>(Q, t);  // R' = [h](-A) + [S]B, classes C
+  }
   __syncthreads();  // R's decode (wave 2) done
   if (wave != 0 || lane != 0) return;
-  ge_p3 B;
-  load_fe(B.X, sh.base);
-  load_fe(B.Y, sh.base + 10);
-  load_fe(B.Z, sh.base + 20);
-  load_fe(B.T, sh.base + 30);
-  ge_cached c;
-  ge_p1p1 t;
-  ge_p2 Q;
-  ge_p3_to_cached<kSO>(c, B);
-  ge_add<kSO>(t, P, c);
-  ge_p1p1_to_p2_addlike<kSO>(Q, t);  // R' = [h](-A) + [S]B, classes C
   fe xr, yr, u, d;
   load_fe(xr, sh.xr);
   load_fe(yr, sh.yr);
