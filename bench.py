@@ -150,6 +150,12 @@ def parse():
                     help="also time the general path for this many steps (0 = skip)")
     ap.add_argument("--dropin-steps", type=int, default=10,
                     help="also time the keyed path at the drop-in authenticator's key window (0 = skip)")
+    ap.add_argument("--whole-node-n", type=int, default=1_000_000,
+                    help="requests per batch of the headline whole-node leg (configs[1] json-decoded request dicts "
+                         "through GpuAuthNr.authenticate_batches, K = --steps batches timed; 0 = skip, value = the "
+                         "device-resident step)")
+    ap.add_argument("--device-steps", type=int, default=20,
+                    help="timed steps of the device-resident kernel leg (device_resident; its roofline)")
     ap.add_argument("--e2e-n", type=int, default=1_000_000,
                     help="requests of the end-to-end authenticate_batch leg over configs[1] (0 = skip)")
     ap.add_argument("--e2e-c0", type=int, default=10_000, help="configs[0] end-to-end requests (0 = skip)")
@@ -218,6 +224,21 @@ def build_stamp(eng):
         if path and os.path.exists(path):
             out[key] = os.path.relpath(path, ROOT)
             out[key + "_sha16"] = hashlib.sha256(open(path, "rb").read()).hexdigest()[:16]
+    # provenance: the stamp __graft_entry__.build() wrote after its make, against the binaries loaded
+    # here and the sources in this tree (recomputed now)
+    try:
+        import __graft_entry__ as GE
+        src = GE.source_sha16()
+        stamp = json.load(open(GE.STAMP)) if os.path.exists(GE.STAMP) else None
+        prov = {"source_sha16": src, "stamp": stamp}
+        if stamp:
+            bins = stamp.get("binaries", {})
+            prov["lib_matches_stamp"] = bins.get(out.get("lib")) == out.get("lib_sha16")
+            prov["hostpack_matches_stamp"] = bins.get(out.get("hostpack")) == out.get("hostpack_sha16")
+            prov["sources_match_stamp"] = stamp.get("source_sha16") == src
+        out["provenance"] = prov
+    except Exception as ex:  # (reported, never fatal to the measurement)
+        out["provenance"] = {"error": "%s: %s" % (type(ex).__name__, ex)}
     return out
 
 
@@ -376,6 +397,118 @@ def time_e2e(eng, reqs, idrs, vks):
                     "value = the median of 3 batches after the first full-size one (steady state); first_batch_* "
                     "= that first batch (buffers allocated). single_authenticate_us: authenticate() of one "
                     "request not in the verdict cache (300 calls after 30 warm-up)"}
+
+
+def whole_node_sets(eng, n, pks, sks, alias_len, rank, sets=2):
+    """`sets` distinct batches of n configs[1] NYM request dicts for this rank
+    (distinct reqIds per set and rank, request i signed by signer i % signers),
+    each json-encoded and decoded on its own as the node gets it off the wire;
+    signed on the GPU (the library's libsodium-exact signer)."""
+    out = []
+    for s in range(sets):
+        base = synth.REQ_ID_BASE + (1 << 44) + (rank * sets + s) * n
+        msgs, kidx, spec = synth.nym_messages(n, pks, alias_len=alias_len, seed=101 + 7 * rank + s, req_id_base=base)
+        b, o = pack_messages(msgs)
+        del msgs
+        sig = eng.sign_batch(sks, kidx, b, o)
+        del b, o
+        reqs, idrs, vks = e2e_requests(eng, n, len(pks), alias_len, spec=spec, sig=sig, pks=pks)
+        out.append(reqs)
+    return out, idrs, vks
+
+
+def time_whole_node(eng, args, sets, idrs, vks, dist_on, dev, scan_threads):
+    """The headline: BASELINE's "verifies/sec (whole node)" -- the drop-in
+    authenticator (GpuAuthNr over this rank's engine, the signers' NYMs
+    registered with addIdr as Node.addGenesisNyms does) verifying batches of
+    json-decoded configs[1] request dicts: the native scan (checks, base58,
+    signing serialization on the host's CPUs) with its PCIe copy and kernels
+    under it, getVerkey per identifier, the GPU verdicts and the result list
+    -- what replaces plenum/server/client_authn.py:67-107 per request.  A step
+    is one batch of n requests.  Pipelined (value): K batches through
+    authenticate_batches (two in flight); synchronous beside it: K batches
+    one authenticate_batch at a time.  The K batches alternate between the
+    distinct request sets; the batch path keeps no verdicts (every step scans,
+    serializes, copies and verifies all n).  Each timed region is bracketed by
+    a barrier and torch.cuda.synchronize() and takes the max over ranks; every
+    outcome is checked after the clock."""
+    from plenum_amd.client_authn import GpuAuthNr
+    K, W = args.steps, args.warmup
+    n = len(sets[0])
+    want = [[m["identifier"] for m in reqs] for reqs in sets]
+    a = GpuAuthNr(engine=eng, scan_threads=scan_threads)
+    t0 = time.perf_counter()
+    for idr, vk in zip(idrs, vks):
+        a.addIdr(idr, vk)
+    a.keys_settle()  # genesis NYMs' key tables built before traffic
+    genesis_s = time.perf_counter() - t0
+    order = [sets[k % len(sets)] for k in range(K)]
+    wants = [want[k % len(sets)] for k in range(K)]
+    for k in range(max(1, W)):  # scan buffers grown, kid_map built, both staging sets touched
+        a.authenticate_batch(sets[k % len(sets)])
+    for _ in a.authenticate_batches([sets[k % len(sets)] for k in range(2)]):
+        pass
+
+    def clocked(fn):
+        torch.cuda.synchronize()
+        if dist_on:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        out = fn()
+        torch.cuda.synchronize()
+        if dist_on:
+            dist.barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t
+        if dist_on:
+            e = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            el = float(e.item())
+        return el, out
+
+    def check(outs):
+        bad = 0
+        for res, w in zip(outs, wants):
+            if res != w:
+                bad += sum(1 for r, x in zip(res, w) if r != x)
+        return bad
+
+    st0 = dict(a.stats)
+    el_pipe, outs = clocked(lambda: list(a.authenticate_batches(order)))
+    st1 = dict(a.stats)
+    bad_pipe = check(outs)
+    del outs
+    per, parts = [], []
+
+    def sync_run():
+        res = []
+        for batch in order:
+            tb = time.perf_counter()
+            res.append(a.authenticate_batch(batch))
+            per.append(time.perf_counter() - tb)
+            parts.append(a._g.last_breakdown)
+        return res
+    el_sync, outs = clocked(sync_run)
+    st2 = dict(a.stats)
+    bad_sync = check(outs)
+    del outs
+    med = sorted(range(K), key=lambda k: per[k])[K // 2]
+    out = {"pipelined": {"value": n * K / el_pipe, "ms_per_batch": el_pipe / K * 1e3, "seconds": el_pipe,
+                         "speculated_share": (st1.get("speculated", 0) - st0.get("speculated", 0)) / (n * K),
+                         "mismatches": bad_pipe},
+           "synchronous": {"value": n * K / el_sync, "ms_per_batch": el_sync / K * 1e3, "seconds": el_sync,
+                           "batch_ms": {"p50": float(np.median(per)) * 1e3, "min": min(per) * 1e3,
+                                        "max": max(per) * 1e3},
+                           "speculated_share": (st2.get("speculated", 0) - st1.get("speculated", 0)) / (n * K),
+                           "in_batch_ms": {k: (round(v, 3) if isinstance(v, float) else v)
+                                           for k, v in (parts[med] or {}).items()},
+                           "mismatches": bad_sync},
+           "requests_per_batch": n, "batches": K, "distinct_request_sets": len(sets), "signers": len(idrs),
+           "scan_threads": scan_threads or "auto", "key_window": a._g.key_window,
+           "keyed_items_share": a.stats["keyed_items"] / max(1, a.stats["batch_items"]),
+           "genesis_addidr_and_builds_s": genesis_s}
+    return out, a
 
 
 def time_bls_commit_round(eng, checks=25, reps=5):
@@ -915,7 +1048,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(args.device_steps):
         step()  # (queued back to back: nothing in the loop waits on the device)
     torch.cuda.synchronize()
     if dist_on:
@@ -1011,9 +1144,9 @@ def main():
             if args.config == "c1" and rank == 0:
                 other["distinct_keys"] = time_general_distinct(eng, args, n, d_msgs, d_ms, d_me, stream)
 
-    total = n * world * args.steps
+    total = n * world * args.device_steps
     value = total / elapsed
-    ms_per_step = elapsed / args.steps * 1e3
+    ms_per_step = elapsed / args.device_steps * 1e3
     ph = np.mean(np.array(phases), axis=0)  # per step: per-phase sums over the sub-batch launches
     launches = eng.last_launch_count()
     n_chunk = eng.last_chunk_items()  # the phase times cover the last 2^20-request chunk
@@ -1093,8 +1226,37 @@ def main():
                           "in 32 GiB of key tables (the headline uses %d: %d keys)" % (args.key_window,
                                                                                           reg_pks.shape[0])}
 
+    # ---- the headline: the whole node (GpuAuthNr over json-decoded request dicts), every rank
+    whole, wn_sets, wn_idrs, wn_vks = None, None, None, None
+    if args.whole_node_n > 0 and args.config == "c1" and args.path == "keyed":
+        host0 = host_cpus()
+        budget = host0["affinity"]
+        if host0["cgroup_cpu_quota"]:
+            budget = min(budget, int(host0["cgroup_cpu_quota"]))
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+        # one node process per GPU: the host's CPU share divided between the ranks (0 = the scan's own rule:
+        # up to 16, one per 2k requests, within the affinity and the cgroup quota)
+        scan_threads = 0 if local_world == 1 else max(1, min(16, budget // local_world))
+        tw = time.perf_counter()
+        wn_sets, wn_idrs, wn_vks = whole_node_sets(eng, args.whole_node_n, pks, sks, args.alias_len, rank)
+        build_s = time.perf_counter() - tw
+        whole, _wa = time_whole_node(eng, args, wn_sets, wn_idrs, wn_vks, dist_on, dev, scan_threads)
+        del _wa
+        whole["requests_built_s"] = build_s
+        whole["host_cpus"] = host0
+        if dist_on:
+            bad = torch.tensor([whole["pipelined"]["mismatches"] + whole["synchronous"]["mismatches"]],
+                               dtype=torch.int64, device=dev)
+            dist.all_reduce(bad)
+            whole["mismatches_all_ranks"] = int(bad.item())
+        else:
+            whole["mismatches_all_ranks"] = whole["pipelined"]["mismatches"] + whole["synchronous"]["mismatches"]
+        for k in ("pipelined", "synchronous"):  # whole job: every rank's batches over the slowest rank's time
+            whole[k]["value_per_rank"] = whole[k]["value"]
+            whole[k]["value"] = whole[k]["value"] * world
+
     cpu = None
-    lib_mis = 0
+    lib_mis = 0 if whole is None else whole["mismatches_all_ranks"]
     if rank == 0 and world == 1 and not args.no_cpu:
         s = min(args.cpu_sample if args.config != "c3" else args.cpu_sample // 4, n)
         sig_h = d_sig[:s].cpu().numpy()
@@ -1139,9 +1301,12 @@ def main():
             del reqs
         if args.e2e_n > 0:
             m = min(args.e2e_n, n)
-            sig_all = d_sig[:m].cpu().numpy()
-            reqs, idrs, vks = e2e_requests(eng, m, args.signers, args.alias_len, spec=nym_spec, sig=sig_all,
-                                           pks=pks)
+            if wn_sets is not None and len(wn_sets[0]) == m:  # the headline's first request set
+                reqs, idrs, vks = wn_sets[0], wn_idrs, wn_vks
+            else:
+                sig_all = d_sig[:m].cpu().numpy()
+                reqs, idrs, vks = e2e_requests(eng, m, args.signers, args.alias_len, spec=nym_spec, sig=sig_all,
+                                               pks=pks)
             e2e["configs1"] = time_e2e(eng, reqs, idrs, vks)
             if args.drain_n > 0:
                 e2e["node_drain"] = time_node_drain(eng, reqs, idrs, vks, drains=args.drain_n)
@@ -1161,40 +1326,70 @@ def main():
             if e2e["key_churn"]["mismatches"]:
                 lib_mis += e2e["key_churn"]["mismatches"]
 
-    # the metric's "whole node" reading: GpuAuthNr.authenticate_batch over json-decoded request dicts
-    # (host scan + PCIe + kernels + result list, one node process), beside the same run's libsodium
-    whole, whole_vs = None, None
-    c1 = (e2e or {}).get("configs1")
-    if c1:
-        whole = {"synchronous": c1["value"], "pipelined": c1["pipelined"]["value"], "unit": "requests/s",
-                 "requests_per_batch": c1["requests"], "in_batch_ms": c1.get("in_batch_ms"),
-                 "note": "end_to_end.configs1: authenticate_batch over 1M json-decoded configs[1] requests in one node "
-                         "process (synchronous: one batch at a time; pipelined: authenticate_batches, two in "
-                         "flight); every verdict checked after the clock"}
-        if cpu:
-            whole_vs = {"synchronous": c1["value"] / cpu["value"], "pipelined": c1["pipelined"]["value"] / cpu["value"],
-                        "cpu": "cpu_baseline.value: libsodium 1.0.18 crypto_sign_verify_detached on %d host threads"
-                               % cpu["cores"]}
+    # the metric's "whole node" reading is the headline (time_whole_node); beside it the same run's libsodium
+    whole_vs = None
+    if whole is not None and cpu:
+        whole_vs = {"pipelined": whole["pipelined"]["value"] / cpu["value"],
+                    "synchronous": whole["synchronous"]["value"] / cpu["value"],
+                    "cpu": "cpu_baseline.value: libsodium %s crypto_sign_verify_detached on %d host threads" % (
+                        cpu.get("sample", "").split("libsodium ")[-1].split(" ")[0] or "1.0.18", cpu["cores"])}
+    device_resident = {
+        "value": value, "unit": "verifies/s", "steps": args.device_steps, "warmup": args.warmup,
+        "ms_per_step": ms_per_step, "path": args.path,
+        "note": "one step = the verify kernels over this rank's %d requests already resident in HBM (hash -> comb "
+                "-> encode on the keyed path), %d steps queued back to back; the roofline is this leg's dominant "
+                "kernel" % (n, args.device_steps),
+        "phase_ms": {"hash": float(ph[0]), "table": float(ph[1]),
+                     ("comb" if args.path == "keyed" else "dsm"): dsm_sum, "encode": float(ph[3]),
+                     "note": "per-phase sums over the %d sub-batch launches of the last %d-request chunk" % (
+                         launches, n_chunk)},
+        "length_buckets": "packed" if args.length_buckets == "packed" else bool(buckets),
+        "key_window": args.key_window, "key_table_build_ms": key_build_ms, "keys": int(reg_pks.shape[0]),
+        "base_window": RL.BASE_W, "engine_create_s": create_s,
+        "value_incl_key_build_one_step": (n * world / (ms_per_step * 1e-3 + key_build_ms * 1e-3)
+                                          if args.path == "keyed" else None),
+        "ref10_equivalent_frac": (n * RL.MAD_PER_VERIFY / (ms_per_step * 1e-3)) / RL.PEAK_MAD_PER_S,
+        "other_path": other, "dropin_window": dropin}
     if rank == 0:
+        if whole is not None:
+            head_value, head_ms, head_steps = whole["pipelined"]["value"], whole["pipelined"]["ms_per_batch"], args.steps
+            workload = ("configs[1]: %d single-signature NYM requests per GPU per step, each a request dict json-decoded "
+                        "on its own as the node receives it, %.0f B mean signed payload, %d signers (addIdr), all "
+                        "valid; step = one batch through GpuAuthNr.authenticate_batches (two batches in flight): "
+                        "native scan + serialization on the host CPUs, PCIe copy and kernels under it, getVerkey per "
+                        "identifier, result list -- the drop-in for client_authn.py:67-107; synchronous "
+                        "authenticate_batch beside it (whole_node)" % (whole["requests_per_batch"], mlen_mean,
+                                                                        args.signers))
+        else:
+            head_value, head_ms, head_steps = value, ms_per_step, args.device_steps
+            workload = "configs[%d]: %d %s per GPU, %.0f B mean signed payload, %d signers%s%s; step = the verify " \
+                       "kernels over HBM-resident inputs" % (
+                           int(args.config[1]), n,
+                           "signature verifications" if args.config == "c3" else "single-signature requests",
+                           mlen_mean, args.signers,
+                           ", 10% corrupted/non-canonical/small-order" if args.config == "c2" else ", all valid",
+                           req_desc + (" + PREPARE/COMMIT tally of %d keys x 25 validators in the step (RCCL "
+                                       "all-reduce MAX of the ballots)" % (-(-(n // 2) * world // 50))
+                                       if args.config == "c4" else ""))
         out = {
-            "metric": METRIC, "value": value, "unit": "verifies/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
+            "metric": METRIC, "value": head_value, "unit": "verifies/s", "n_gpus": world, "steps": head_steps,
+            "warmup": args.warmup, "ms_per_step": head_ms, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u32 (radix-2^25.5 GF(2^255-19), 64-bit MAD accumulators)",
-            "data": "synthetic NYM requests signed on-GPU (deterministic Ed25519, libsodium-exact)",
-            "config": {"workload": "configs[%d]: %d %s per GPU, %.0f B mean signed payload, %d signers%s%s" % (
-                int(args.config[1]), n, "signature verifications" if args.config == "c3" else "single-signature requests",
-                mlen_mean, args.signers,
-                ", 10% corrupted/non-canonical/small-order" if args.config == "c2" else ", all valid",
-                req_desc + (" + PREPARE/COMMIT tally of %d keys x 25 validators in the step (RCCL all-reduce MAX "
-                            "of the ballots)" % (-(-(n // 2) * world // 50)) if args.config == "c4" else "")),
-                       "requests_per_gpu": n, "signers": args.signers, "parallelism": "dp%d (request-index shards)" % world,
-                       "path": ("keyed: the signers' verkeys registered once (comb tables of key window %d, base "
-                                "window %d), inputs HBM-resident; the drop-in's own window and its end-to-end rate "
-                                "are the dropin_window / end_to_end fields" % (args.key_window, RL.BASE_W)
+            "data": ("synthetic NYM requests signed on-GPU (deterministic Ed25519, libsodium-exact)"
+                     + (", json-encoded and decoded one by one" if whole is not None else "")),
+            "config": {"workload": workload, "requests_per_gpu": (whole or {}).get("requests_per_batch", n),
+                       "signers": args.signers, "parallelism": "dp%d (one node process per GPU; request-index shards)"
+                                                               % world,
+                       "path": ("keyed: the signers' verkeys registered once (comb tables; drop-in window %s for the "
+                                "whole node, %d on the device-resident leg; base window %d)" % (
+                                    (whole or {}).get("key_window"), args.key_window, RL.BASE_W)
                                 if args.path == "keyed" else
                                 "general: every request carries its key bytes, inputs HBM-resident")},
+            "end_to_end": e2e,
+            "device_resident": device_resident,
             "roofline": {"bound": "valu", "kernel": kernel_name, "achieved": achieved, "peak": peak,
                          "unit": "TMAD/s", "frac": achieved / peak, "traffic": traffic,
+                         "leg": "device_resident (the whole node is host-bound; this is its dominant GPU kernel)",
                          "algorithmic": "%d MAD per verify (%s), %d launches per chunk of %d requests (n=%d each; "
                                         "%d requests per step), avg launch %.3f ms (HIP events on the launch streams)" % (
                              kernel_mad, RL.kernel_work(kernel_name, args.key_window), launches, n_chunk,
@@ -1210,33 +1405,21 @@ def main():
                          "utilisation": utilisation,
                          "frac_survey": (n * RL.MAD_PER_VERIFY / (ms_per_step * 1e-3)) / RL.PEAK_MAD_PER_S,
                          "frac_survey_note": "SURVEY 8(d)'s a-priori 305,000 MAD per verify (ref10: decode A + 253 "
-                                             "doublings + ~86 additions + inversion) x requests / step time / peak; "
-                                             "> 1 on the keyed path because per-key comb tables built once at "
+                                             "doublings + ~86 additions + inversion) x requests / device step time / "
+                                             "peak; > 1 on the keyed path because per-key comb tables built once at "
                                              "registration replace A's decode and every doubling (%d MAD per "
                                              "request in the step's dominant kernel)" % kernel_mad},
-            "path": args.path,
-            "phase_ms": {"hash": float(ph[0]), "table": float(ph[1]),
-                         ("comb" if args.path == "keyed" else "dsm"): dsm_sum, "encode": float(ph[3]),
-                         "note": "per-phase sums over the %d overlapped sub-batch launches of the last "
-                                 "%d-request chunk" % (launches, n_chunk)},
-            "length_buckets": "packed" if args.length_buckets == "packed" else bool(buckets),
-            "key_window": args.key_window, "key_table_build_ms": key_build_ms, "keys": int(reg_pks.shape[0]),
-            "base_window": RL.BASE_W, "engine_create_s": create_s,
-            "value_incl_key_build_one_step": (n * world / (ms_per_step * 1e-3 + key_build_ms * 1e-3)
-                                              if args.path == "keyed" else None),
-            "ref10_equivalent_frac": (n * RL.MAD_PER_VERIFY / (ms_per_step * 1e-3)) / RL.PEAK_MAD_PER_S,
-            "other_path": other,
-            "dropin_window": dropin,
             "build": build_stamp(eng),
-            "whole_node": whole,
-            "whole_node_vs_cpu": whole_vs,
-            "end_to_end": e2e,
             "cpu_baseline": cpu,
             "parity": {"mismatches_vs_construction": mismatches, "accepted": accepted, "expected": expected,
                        "mismatches_vs_libsodium_all_items": (cpu or {}).get("all_items_check", {}).get("mismatches"),
+                       "whole_node_mismatches": (whole or {}).get("mismatches_all_ranks"),
                        "ranks": world, "accepted_in_gathered_bitmask": gathered_accepted},
             "tally": tally_result,
             "collective": collective,
+            # last, so the driver's tail of the line keeps them: the headline's two forms and their ratio
+            "whole_node": whole,
+            "whole_node_vs_cpu": whole_vs,
         }
         print(json.dumps(out), flush=True)
     if dist_on:

@@ -47,6 +47,7 @@ extern "C" {
 #define EDV_EHIP -2     /* HIP runtime error (message has the hipError string) */
 #define EDV_ENOMEM -3   /* device or host allocation failed */
 #define EDV_ENODEV -4   /* no gfx950 device / device index out of range */
+#define EDV_EBUSY -5    /* the staging set holds an uncollected submission (collect it, or use the other set) */
 
 typedef struct edv_ctx edv_ctx;
 
@@ -245,7 +246,7 @@ int edv_verify_staged(edv_ctx *ctx, int keyed, const uint8_t *keys, uint64_t slo
  * k + 1 is staged into one set while batch k's kernels still read the other.
  * edv_verify_staged_submit queues the verify of the staged batch and returns a ticket at once;
  * edv_verify_staged_collect(ctx, ticket, accept_bits) waits for it and writes the bits.
- * A set holding an uncollected submission refuses reserve and submit (EDV_EINVAL).
+ * A set holding an uncollected submission refuses reserve and submit (EDV_EBUSY).
  * edv_verify_staged == submit + collect.  Replaces, like edv_verify_staged, libsodium's
  * crypto_sign_open per request (nacl_wrappers.py:108). */
 int edv_stage_select(edv_ctx *ctx, int set);

@@ -1731,6 +1731,7 @@ struct edv_ctx {
   int part_set = -1;
   bool part_keyed = true;
   int part_err = 0;
+  std::string part_msg;  // the first failed part's message (the part ran on the scan's copier thread)
   uint64_t part_launched = 0;
   // edv_verify_staged_subset: each set's last submitted staged batch (its item count and message
   // base, kept after the collect while its decoded signatures, spans and messages stay in HBM;
@@ -2830,7 +2831,7 @@ int edv_stage_reserve(edv_ctx* ctx, uint64_t bytes) {
   if (r) return r;
   std::lock_guard<std::mutex> lk(ctx->stage_mu);
   if (ctx->set_ticket[ctx->cur_set])
-    return set_err(EDV_EINVAL, "staging set %d holds an uncollected submission", ctx->cur_set);
+    return set_err(EDV_EBUSY, "staging set %d holds an uncollected submission", ctx->cur_set);
   ctx->stage_err = 0;
   ctx->last_ok[ctx->cur_set] = false;  // the puts that follow overwrite the last batch's messages
   if (ctx->d_stage().cap < bytes) {
@@ -2877,7 +2878,7 @@ int edv_verify_staged_submit(edv_ctx* ctx, int keyed, const uint8_t* keys, uint6
   {
     std::lock_guard<std::mutex> lk(ctx->stage_mu);
     if (ctx->stage_err) return set_err(ctx->stage_err, "an earlier stage_put failed");
-    if (ctx->set_ticket[set]) return set_err(EDV_EINVAL, "staging set %d holds an uncollected submission", set);
+    if (ctx->set_ticket[set]) return set_err(EDV_EBUSY, "staging set %d holds an uncollected submission", set);
   }
   if (keyed && n && ctx->key_count == 0) return set_err(EDV_EINVAL, "no registered keys");
   const uint64_t cap = ctx->d_stage().cap;
@@ -2949,7 +2950,7 @@ int edv_verify_staged_begin(edv_ctx* ctx, int keyed, uint64_t n, uint64_t* ticke
   const int set = ctx->cur_set;
   {
     std::lock_guard<std::mutex> lk(ctx->stage_mu);
-    if (ctx->set_ticket[set]) return set_err(EDV_EINVAL, "staging set %d holds an uncollected submission", set);
+    if (ctx->set_ticket[set]) return set_err(EDV_EBUSY, "staging set %d holds an uncollected submission", set);
     if (ctx->part_set >= 0) return set_err(EDV_EINVAL, "a batch of parts is open (set %d)", ctx->part_set);
   }
   if (keyed && n && ctx->key_count == 0) return set_err(EDV_EINVAL, "no registered keys");
@@ -2969,6 +2970,7 @@ int edv_verify_staged_begin(edv_ctx* ctx, int keyed, uint64_t n, uint64_t* ticke
   ctx->part_set = set;
   ctx->part_keyed = keyed != 0;
   ctx->part_err = 0;
+  ctx->part_msg.clear();
   ctx->part_launched = 0;
   *ticket = tk;
   return 0;
@@ -2981,7 +2983,10 @@ int edv_verify_staged_part(edv_ctx* ctx, const void* keys, uint64_t slot_off, ui
   const int set = ctx->part_set;
   int r = 0;
   auto fail = [&](int code) {
-    if (!ctx->part_err) ctx->part_err = code;
+    if (!ctx->part_err) {
+      ctx->part_err = code;
+      ctx->part_msg = g_err;  // (g_err is this thread's; edv_verify_staged_end reports it on the caller's)
+    }
     return code;
   };
   if (set < 0) return fail(set_err(EDV_EINVAL, "no batch of parts is open"));
@@ -3036,7 +3041,7 @@ int edv_verify_staged_end(edv_ctx* ctx) {
     HIP_TRY(hipMemcpyAsync(ctx->sh_bits[set].p, ctx->s_bits[set].p, 8 * nwords, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipEventRecord(ctx->ev_sdone[set], ctx->stream));
   }
-  if (ctx->part_err) return set_err(ctx->part_err, "a part of this batch failed");
+  if (ctx->part_err) return set_err(ctx->part_err, "a part of this batch failed: %s", ctx->part_msg.c_str());
   return 0;
 }
 
@@ -3079,7 +3084,7 @@ int edv_verify_staged_subset(edv_ctx* ctx, const uint32_t* idx, const uint8_t* p
   uint64_t n = 0, base = 0;
   {
     std::lock_guard<std::mutex> lk(ctx->stage_mu);
-    if (ctx->set_ticket[set]) return set_err(EDV_EINVAL, "staging set %d holds an uncollected submission", set);
+    if (ctx->set_ticket[set]) return set_err(EDV_EBUSY, "staging set %d holds an uncollected submission", set);
     if (!ctx->last_ok[set]) return set_err(EDV_EINVAL, "staging set %d holds no submitted staged batch", set);
     n = ctx->last_n[set];
     base = ctx->last_msg_base[set];

@@ -100,6 +100,14 @@ class EdVerifyError(RuntimeError):
         self.code = code
 
 
+EDV_EBUSY = -5  # include/edverify.h: the staging set holds an uncollected submission
+
+
+class EdVerifyBusy(EdVerifyError):
+    """EDV_EBUSY: the staging set holds an uncollected submission (not a fault:
+    the caller collects it first or takes another path)."""
+
+
 _lib = None
 
 
@@ -136,4 +144,5 @@ def load():
 
 def check(code):
     if code != 0:
-        raise EdVerifyError(code, load().edv_last_error().decode(errors="replace"))
+        cls = EdVerifyBusy if code == EDV_EBUSY else EdVerifyError
+        raise cls(code, load().edv_last_error().decode(errors="replace"))

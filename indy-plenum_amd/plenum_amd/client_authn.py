@@ -138,6 +138,7 @@ _PART_ITEMS = 1 << 16  # a speculative staged batch's kernels go out per this ma
 _MISSING = object()
 _VERDICT_ENTRY_BYTES = 240  # a verdict-cache entry's objects beyond its key and sm bytes (tuple, 2 bytes, dict slot)
 _BUSY = object()  # _authenticate_staged: the staging set is held by a batch in flight
+_EDV_EBUSY = -5  # include/edverify.h EDV_EBUSY (plenum_amd._lib.EdVerifyBusy.code)
 _IGNORE_SIG = (SIG,)
 
 
@@ -790,10 +791,11 @@ class GpuAuthMixin:
             if hasattr(eng, "stage_select"):
                 eng.stage_select(staging_set)
             eng.stage_reserve(slot_base + n * slot)
-        except Exception:
-            # the set is busy (an unfinished authenticate_batches iteration holds its batch in
-            # flight there): nothing was scanned or staged, the caller takes the unstaged path
-            if defer:
+        except Exception as ex:
+            # the set is busy (EDV_EBUSY: an unfinished authenticate_batches iteration holds its batch
+            # in flight there): nothing was scanned or staged, the caller takes the unstaged path.
+            # Any other failure (allocation, HIP) is a fault and is raised, not read as busy.
+            if defer or getattr(ex, "code", None) != _EDV_EBUSY:
                 raise
             return _BUSY
         sfx = "" if staging_set == 0 else str(staging_set)
@@ -804,9 +806,22 @@ class GpuAuthMixin:
         if (g.speculate and g.kid_map is not None and ks is not None and _kid_map is not None
                 and os.environ.get("EDV_SPECULATE", "1") != "0"
                 and spans_buf is not None and kid_buf is not None and getattr(eng, "supports_staged_parts", False)):
-            ks_version = ks.version
-            parts = eng.verify_staged_begin(True, n)
-            spec = (g.kid_map, kid_buf, eng.parter(), int(os.environ.get("EDV_PART_ITEMS", _PART_ITEMS)))
+            # kid_map's ids are usable only while no slot has been reused since it was made: an
+            # eviction, a retired slot or a reset (by anyone sharing the engine: _sync sees it)
+            # bumps ks.version, and a slot rebuilt for another key may still be building, so the
+            # kernels would read its old or half-written tables.  New keys in free slots do not
+            # touch kid_map's slots.
+            ks._sync()
+            if g.kid_map_version == ks.version:
+                ks_version = ks.version
+                try:
+                    parts = eng.verify_staged_begin(True, n)
+                except Exception as ex:  # no speculation for this batch; the ordinary verify follows
+                    parts = None
+                    g.stats["part_failures"] = g.stats.get("part_failures", 0) + 1
+                    g.last_part_error = str(ex)
+                if parts is not None:
+                    spec = (g.kid_map, kid_buf, eng.parter(), int(os.environ.get("EDV_PART_ITEMS", _PART_ITEMS)))
         t0 = perf_counter()
         try:
             scan = _scan_batch(msgs, [SIG], g.scan_threads, [bufs[0], bufs[1], spans_buf], slot, 2, eng.stager(),
@@ -823,8 +838,10 @@ class GpuAuthMixin:
         if parts is not None:  # the parts' verdict copy queued after the last part
             try:
                 eng.verify_staged_end()
-            except Exception:
+            except Exception as ex:
                 parts_ok = False  # a part failed: the verdicts come from the ordinary verify
+                g.stats["part_failures"] = g.stats.get("part_failures", 0) + 1
+                g.last_part_error = str(ex)  # (the library's message names the part's own failure)
         t1 = perf_counter()
 
         def drop_parts():  # the speculative verdicts are not used: free the set

@@ -15,6 +15,17 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 _BASELINE = []
 
 
+class StagingSetBusy(RuntimeError):
+    """What the library's EDV_EBUSY raises (plenum_amd._lib.EdVerifyBusy): the
+    staging set holds an uncollected submission."""
+    code = -5
+
+
+def _not_held(held, s):
+    if held[s] is not None:
+        raise StagingSetBusy("staging set %d holds an uncollected submission" % s)
+
+
 def _baseline_lib():
     if not _BASELINE:
         _BASELINE.append(ctypes.CDLL(os.path.join(ROOT, "oracle", "_build", "libcpu_baseline.so")))
@@ -304,13 +315,13 @@ class StagingOracleEngine(OracleEngine):
         self.cur = staging_set
 
     def stage_reserve(self, nbytes):
-        assert self.held[self.cur] is None, "staging set %d holds an uncollected submission" % self.cur
+        _not_held(self.held, self.cur)
         self._last[self.cur] = None  # (edv_verify_staged_subset refuses the set from here)
         if len(self.stage) < nbytes:
             self.sets[self.cur] = (ctypes.c_ubyte * int(nbytes))()
 
     def verify_staged_submit(self, keyed, keys, slot_off, msg_base, msg_start, msg_end):
-        assert self.held[self.cur] is None, "staging set %d holds an uncollected submission" % self.cur
+        _not_held(self.held, self.cur)
         self.submits_staged += 1
         ok = self.verify_staged(keyed, keys, slot_off, msg_base, msg_start, msg_end)
         self.held[self.cur] = ok
@@ -329,7 +340,10 @@ class StagingOracleEngine(OracleEngine):
     part_fail_at = 0  # make the k-th part call fail (tests)
 
     def verify_staged_begin(self, keyed, n):
-        assert keyed and self.held[self.cur] is None, "staging set %d holds an uncollected submission" % self.cur
+        assert keyed
+        _not_held(self.held, self.cur)
+        if n and not self.keys:  # edv_verify_staged_begin: EDV_EINVAL "no registered keys"
+            raise RuntimeError("edverify error -1: no registered keys")
         h = _Parts(self.cur, n, self.part_fail_at)
         self.held[self.cur] = h
         self._last[self.cur] = None

@@ -1245,3 +1245,83 @@ def test_keystore_lookup_array_matches_lookup(oracle):
     assert got.tolist() == [-1 if i is None else i for i in ks.lookup(q)] and (got[:6] >= 0).all()
     assert (ks._used[got[got >= 0]] == ks._tick - 1).all()
     assert ks.lookup_array([]).dtype == np.int64
+
+
+def test_no_speculation_over_a_reused_slot(oracle, monkeypatch):
+    """an eviction moves a slot to another key whose table build is
+    still in flight; the next all-keyed batch must not queue kernels under its
+    scan with the ids of the batches before it (kid_map), which would read that
+    slot's old or half-written tables.  The key store's version, bumped by the
+    eviction, gates the speculation (the double fails any keyed verify of an id
+    still building), and the batches after it speculate again once the map is
+    rebuilt."""
+    from engine_double import AsyncOracleEngine, StagingOracleEngine
+    from plenum_amd import client_authn as CA
+
+    class Eng(StagingOracleEngine, AsyncOracleEngine):
+        pass
+    monkeypatch.setattr(CA, "_STAGE_MIN_BATCH", 1000)
+    monkeypatch.setattr(CA, "_PINNED_MIN_BATCH", 1000)
+    monkeypatch.setattr(CA, "_PART_ITEMS", 4096)
+    idrs, vks, msgs = _signed(5, 6000)
+    eng = Eng(oracle)
+    a = GpuAuthNr(engine=eng, max_keys=4, hot_key_uses=1)
+    ref = GpuAuthNr(engine=OracleEngine(oracle), max_keys=0)
+    for i, v in zip(idrs, vks):
+        ref.addIdr(i, v)
+    for i, v in zip(idrs[:4], vks[:4]):
+        a.addIdr(i, v)
+    a.keys_settle()
+    a.clients[idrs[4]] = {"verkey": vks[4], "role": None}  # known, no slot: earns one by verified use
+
+    def check(batch):
+        assert [_outcome(r) for r in a.authenticate_batch(batch)] == \
+            [_outcome(r) for r in ref.authenticate_batch(batch)]
+        assert eng.held == [None, None]
+    old4 = [dict(m) for m in msgs if m["identifier"] in idrs[:4]]
+    check(old4)
+    check(old4)
+    assert eng.parts_begun == 1  # the steady state speculates
+    new4 = [dict(m) for m in msgs if m["identifier"] != idrs[0]]
+    check(new4)  # idrs[4] verifies on the general path: it earns a slot ...
+    check(new4)  # ... taken here, evicting idrs[0] (the least recently used) with an asynchronous build
+    assert eng.building, "the rebuilt slot's table is still in flight"
+    begun = eng.parts_begun
+    check(old4)  # idrs[0]'s id in kid_map now names a slot being rebuilt for idrs[4]
+    assert eng.parts_begun == begun  # no kernels under the scan with the stale map
+    eng.finish_builds()
+    for _ in range(3):
+        check(new4)
+    assert eng.parts_begun > begun  # speculating again on the rebuilt map
+
+
+def test_speculation_after_another_authenticator_reset_the_store(oracle, monkeypatch):
+    """the engine's key store reset by someone else sharing it
+    (keys_reset bumps keys_generation) while this authenticator's kid_map is
+    still set: authenticate_batch neither raises ('no registered keys' from
+    edv_verify_staged_begin) nor leaves a staging set held, and the outcomes
+    are the general path's."""
+    eng, a, ref, idrs, vks, msgs = _staged_pair(oracle, monkeypatch)
+    steady = [dict(m) for m in msgs if m["identifier"] in idrs[:4]]
+    a.authenticate_batch(steady)
+    a.authenticate_batch(steady)
+    begun = eng.parts_begun
+    eng.keys_reset()
+    got = a.authenticate_batch(steady)
+    assert [_outcome(r) for r in got] == [_outcome(r) for r in ref.authenticate_batch(steady)]
+    assert eng.parts_begun == begun and eng.held == [None, None]
+
+
+def test_staging_reserve_fault_is_raised_not_read_as_busy(oracle, monkeypatch):
+    """only EDV_EBUSY (the set holds an uncollected submission)
+    sends a batch to the unstaged path; any other stage_reserve failure (an
+    allocation or HIP error) is raised."""
+    eng, a, ref, idrs, vks, msgs = _staged_pair(oracle, monkeypatch)
+    steady = [dict(m) for m in msgs if m["identifier"] in idrs[:4]]
+
+    def fault(nbytes):
+        raise RuntimeError("edverify error -3: hipMalloc failed (test)")
+    monkeypatch.setattr(eng, "stage_reserve", fault)
+    with pytest.raises(RuntimeError, match="hipMalloc"):
+        a.authenticate_batch(steady)
+    assert eng.held == [None, None]

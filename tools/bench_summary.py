@@ -15,10 +15,12 @@ def main(path):
         return
     d = json.loads(lines[-1])
     rl = d["roofline"]
-    print("value %.1f M/s  %.3f ms/step  frac %.3f  busy %s  GB/s %s  clk %s  n_gpus %d" % (
-        d["value"] / 1e6, d["ms_per_step"], rl["frac"], r(rl.get("valu_busy"), 3), r(rl.get("hbm_GBps"), 0),
-        r(rl.get("clock_GHz"), 3), d["n_gpus"]))
-    ph = d.get("phase_ms") or {}
+    dr = d.get("device_resident") or d
+    print("value %.2f M/s  %.3f ms/step  n_gpus %d | device-resident %.1f M/s  %.3f ms/step  frac %.3f  busy %s  "
+          "GB/s %s  clk %s" % (d["value"] / 1e6, d["ms_per_step"], d["n_gpus"], dr["value"] / 1e6, dr["ms_per_step"],
+                               rl["frac"], r(rl.get("valu_busy"), 3), r(rl.get("hbm_GBps"), 0),
+                               r(rl.get("clock_GHz"), 3)))
+    ph = dr.get("phase_ms") or {}
     print("phases", {k: r(v, 3) for k, v in ph.items() if k != "note"})
     cpu = d.get("cpu_baseline")
     if cpu:
@@ -26,8 +28,11 @@ def main(path):
             cpu["value"] / 1e3, cpu["cores"], cpu["kind"], (cpu.get("all_items_check") or {}).get("mismatches")))
     w, wv = d.get("whole_node"), d.get("whole_node_vs_cpu") or {}
     if w:
-        print("whole node: sync %.2f M/s (%sx cpu), pipelined %.2f M/s (%sx cpu)" % (
-            w["synchronous"] / 1e6, r(wv.get("synchronous")), w["pipelined"] / 1e6, r(wv.get("pipelined"))))
+        print("whole node: sync %.2f M/s (%sx cpu), pipelined %.2f M/s (%sx cpu), mismatches %s" % (
+            w["synchronous"]["value"] / 1e6, r(wv.get("synchronous")), w["pipelined"]["value"] / 1e6,
+            r(wv.get("pipelined")), w.get("mismatches_all_ranks")))
+        print("   sync batch ms", {k: r(v, 2) for k, v in w["synchronous"]["batch_ms"].items()},
+              {k: r(v, 2) for k, v in (w["synchronous"].get("in_batch_ms") or {}).items()})
     for k, v in (d.get("end_to_end") or {}).items():
         if k == "by_devices":
             print(" ", k, {kk: (r(vv["value"] / 1e6, 2) if "value" in vv else vv.get("error"))
