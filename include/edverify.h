@@ -31,6 +31,17 @@
  *     little-endian 64-bit words of wave ballots.  1 = libsodium returns 0.
  *   - Threading: one context per GPU; calls on one context are serialised by
  *     the caller (Plenum's node is single-threaded asyncio).
+ *
+ * Stability.  STABLE: the drop-in's contract, what plenum_amd's authenticator
+ * binds -- context, verify (host-pointer, keyed, one-request, staged, submit /
+ * collect), the key store, pinned host memory, request digests, the tally and
+ * BLS.  Every tuning knob is one edv_options struct read and written whole
+ * (edv_set_options checks every field before applying any; the authenticator
+ * never changes them); measurements are one edv_stats struct.  DIAGNOSTIC
+ * (benches and tests, not the drop-in): edv_get_stats, the *_device forms,
+ * the synthetic-load signer (edv_seed_keypair_batch, edv_sign_*), and
+ * edv_bls_sign_batch / edv_bls_keygen_batch.  tests/test_abi.py fails on any
+ * exported edv_* symbol this header does not declare.
  */
 #ifndef PLENUM_EDVERIFY_H
 #define PLENUM_EDVERIFY_H
@@ -67,6 +78,72 @@ void edv_destroy(edv_ctx *ctx);
 /* Block until all work queued on the context stream has finished. */
 int edv_synchronize(edv_ctx *ctx);
 
+/* ------------------------------------------------------------ options (STABLE)
+ * Every tuning knob of a context.  edv_default_options fills what a fresh
+ * context has; edv_set_options validates every field before applying any (a
+ * refused call changes nothing). */
+typedef struct edv_options {
+  /* sub-batches per 2^20-request chunk, 1..4 (default 1: each kernel alone on the GPU; 2-4 alternate
+   * two streams so a sub-batch's encode overlaps the next one's hash -- within 1 % at 1M) */
+  int32_t pipeline;
+  /* hash lanes in SHA-512 block-count order (a stable descending radix sort of the block counts, one
+   * 6-bit rocPRIM pass, ~50 us per 1M): 0 off, 1 on, 2 auto (default: host-offset calls sort when
+   * unsorted waves would run > 1.25x the batch's blocks; device-pointer calls cannot see the lengths
+   * and treat auto as off), 3 sorted + packed (north_star (1): each 64-lane group's messages written
+   * as padded big-endian SHA-512 stream words, lane-interleaved, into the unit arena; groups that do
+   * not fit are read in place).  configs[3]: hash 4.72 -> 1.50 ms per 1M with sorting. */
+  int32_t length_buckets;
+  /* key order of the comb on the key-table path: 0 off, 1 on, 2 auto (default: sub-batches of 4,096+
+   * requests at key windows >= 15 with < 16,384 keys).  A counting sort makes one key's requests
+   * neighbours, so a wave gathers from one key's rows (W = 16, random key order: comb 1.70 -> 1.02 ms
+   * per 1M); the accept bits do not change. */
+  int32_t key_sort;
+  /* edv_verify_one's resident kernel: 1 on (default; 0 when EDV_RESIDENT=0 at edv_create), 0 off
+   * (every single request launches edv_verify_small_kernel) */
+  int32_t resident;
+  /* keyed host-pointer batches of at most this many requests run one workgroup of three waves per
+   * request (hash | base comb rows | R decode side by side) for latency (default 256, at most 65536;
+   * 0 = never) */
+  uint64_t small_batch;
+  /* the unit arena of length_buckets = 3, in bytes (default 1.25 GiB = 1,280 B per lane of a chunk) */
+  uint64_t unit_arena_bytes;
+  /* BLS: verify batches of at most this many checks take two lanes per check (each Miller loop on
+   * its own lane), of at most half of it four lanes (default 32768; 0 = always one lane) */
+  uint64_t bls_pair_lanes;
+  /* BLS: verify batches of at most this many checks run one wave per check (the check as a
+   * straight-line program over the wave's lanes, bls_program.h: ~3 ms for a COMMIT round's ~25;
+   * checks it cannot decide re-run on the four-lane kernel) (default 8192; 0 = never) */
+  uint64_t bls_wave_checks;
+} edv_options;
+void edv_default_options(edv_options *out);
+int edv_get_options(edv_ctx *ctx, edv_options *out);
+int edv_set_options(edv_ctx *ctx, const edv_options *opt);
+
+/* ------------------------------------------------------- statistics (DIAGNOSTIC)
+ * The roofline's kernel times and the last host-pointer call, in one read.
+ * The verify pipeline is four kernels: hash (prechecks + SHA-512 + mod L),
+ * table (decode -A, [1..8](-A); empty on the key-table path), dsm or comb
+ * ([h](-A) + [S]B), encode (batched inversion, encode, compare with R,
+ * ballot); a call over more than 2^20 requests runs in chunks and the phase
+ * times cover the last one.  Waits for the last timed launch's events. */
+typedef struct edv_stats {
+  double phase_ms[4];        /* hash, table, dsm/comb, encode: per phase the SUM over the last chunk's
+                                sub-batch launches, HIP events on the launch streams (a small-kernel
+                                launch counts as the comb phase) */
+  int32_t launch_count;      /* sub-batches (launches per phase) of that chunk */
+  int32_t phases_valid;      /* 1 once a timed verify has run on the context */
+  uint64_t chunk_items;      /* requests in that chunk */
+  double host_call_ms;       /* the last host-pointer verify: wall time of the call */
+  double host_stage_ms;      /*   CPU copies into pinned staging (0 when every input was pinned) */
+  uint64_t host_h2d_bytes;   /*   bytes copied host -> device */
+  uint32_t host_direct;      /*   inputs DMA'd straight from pinned memory: bit 0 signatures, 1 keys,
+                                  2 messages, 3 offsets */
+  uint32_t reserved;
+  uint64_t resident_launches; /* edv_verify_one: resident kernels launched, requests they served */
+  uint64_t resident_served;
+} edv_stats;
+int edv_get_stats(edv_ctx *ctx, edv_stats *out);
+
 /* ---------------------------------------------------------------- verify */
 
 /* libsodium crypto_sign_verify_detached over a batch.
@@ -93,70 +170,6 @@ int edv_sign_open_batch(edv_ctx *ctx, const uint8_t *sm, const uint64_t *sm_off,
 int edv_verify_batch_device(edv_ctx *ctx, const void *d_sig64, const void *d_pk32, const void *d_msgs,
                             const void *d_msg_off, uint64_t n, void *d_accept_words, void *stream);
 
-/* Kernel timing hooks for the roofline, measured with HIP events on the
- * streams the kernels ran on.  The verify pipeline is four kernels: hash
- * (prechecks + SHA-512 + mod L), table (decode -A, [1..8](-A); empty on the
- * key-table path), dsm or comb ([h](-A) + [S]B), and encode (batched
- * inversion, encode, compare with R, ballot).  Each chunk of up to 2^20 items
- * is cut into up to 4 sub-batches whose kernels alternate between two
- * streams (one sub-batch's encode and tail overlap the next one's work);
- * edv_last_launch_count() is the number of sub-batches (kernel launches per
- * phase) of the last chunk.  edv_last_phases_ms fills out4[0..3] = hash,
- * table, dsm/comb, encode, each the SUM of that phase's launch durations in
- * the last chunk (average launch = sum / count); edv_last_phase_ms the first
- * three; edv_last_kernel_ms returns the dsm/comb sum (the dominant kernel)
- * or < 0. */
-int edv_last_phases_ms(edv_ctx *ctx, double *out4);
-int edv_last_launch_count(edv_ctx *ctx);
-/* Requests in the last chunk of the last verify call (a call over more than
- * 2^20 requests runs in chunks; the phase times cover the last one). */
-uint64_t edv_last_chunk_items(edv_ctx *ctx);
-/* Sub-batches per chunk (1..4, default 1); 1 = no overlap (each kernel runs
- * alone on the GPU, e.g. to time one kernel in isolation). */
-int edv_set_pipeline(edv_ctx *ctx, int sub_batches);
-/* Hash lanes in SHA-512 block-count order: without it every lane of a wave
- * runs as many SHA-512 blocks as the longest message of its wave.  The order
- * is a stable descending radix sort of the block counts (rocPRIM, one 6-bit
- * pass, ~50 us per 1M requests), so a batch of one block count keeps the
- * identity order.  mode 0 off, 1 on, 2 auto (default): calls with host
- * offsets (edv_verify_batch, edv_verify_batch_keyed, edv_sign_open_batch)
- * sort when unsorted waves would run > 1.25x the batch's blocks; device-
- * pointer calls cannot see the lengths without a sync and treat auto as off.
- * Measured (profiles/r01g_*): configs[3] (64 B - 4 KiB log-uniform) hash
- * 4.72 -> 1.50 ms per 1M signatures, whole step 154M -> 297M/s; configs[1]
- * (all 2 blocks) -8% if forced on (the sort's launches), hence auto.
- * mode 3 = sorted + packed (north_star (1)): each 64-lane group of sorted
- * hash lanes gets a region of the context's unit arena where
- * edv_pack_units_kernel writes its messages as padded big-endian SHA-512
- * stream words, lane-interleaved, so the hash kernels' message loads are
- * coalesced 1 KiB wave accesses with no byte shuffling (one sub-batch per
- * chunk).  Groups that do not fit the arena are read in place.  The accept
- * bits do not depend on the mode. */
-int edv_set_length_buckets(edv_ctx *ctx, int mode);
-/* Key order of the comb (key-table path): mode 0 off, 1 on, 2 auto (default:
- * sub-batches of 4,096 requests or more at key windows of 15 and up).  A
- * counting sort of the sub-batch's key ids (the keyed path's "table" phase)
- * makes the requests of one key neighbours, so a wave's 64 comb lanes gather
- * from one key's rows instead of 64 keys' rows spread over the key store;
- * the encode reads the permutation back and the accept bits are unchanged.
- * Applies when the registered key count is below 16,384 (LDS cursors).
- * Measured (profiles/r05e): key window 16 with key ids in a random order
- * (configs[2]) comb 1.70 -> 1.02 ms per 1M; at window 14 no gain. */
-int edv_set_key_sort(edv_ctx *ctx, int mode);
-/* Small keyed batches (a message that missed the verify-ahead cache): host-
- * pointer keyed verifies of at most max_requests requests (default 256; 0 =
- * never) run one workgroup of three waves per request -- the hash, the two
- * combs' rows on separate lanes summed as trees, and R decoded beside them
- * instead of inverting R' afterwards (encode(R') == R iff X' = x_R Z',
- * Y' = y_R Z' with R canonical and decodable) -- for latency; same verdicts
- * as the batch kernels. */
-int edv_set_small_batch(edv_ctx *ctx, uint64_t max_requests);
-/* Size of the unit arena of mode 3 in bytes (default 1.25 GiB = 1,280 B per
- * lane of a 2^20-request chunk; allocated on first use; 0 = none).  Takes
- * effect at the next mode-3 launch. */
-int edv_set_unit_arena(edv_ctx *ctx, uint64_t bytes);
-int edv_last_phase_ms(edv_ctx *ctx, double *hash_ms, double *table_ms, double *dsm_ms);
-double edv_last_kernel_ms(edv_ctx *ctx);
 
 /* ------------------------------------------------------ key-table path */
 
@@ -219,6 +232,17 @@ int edv_verify_batch_keyed(edv_ctx *ctx, const uint8_t *sig64, const uint32_t *k
                            const uint64_t *msg_off, uint64_t n, uint8_t *accept_bits);
 int edv_verify_batch_keyed_device(edv_ctx *ctx, const void *d_sig64, const void *d_key_idx, const void *d_msgs,
                                   const void *d_msg_off, uint64_t n, void *d_accept_words, void *stream);
+/* One request against registered key key_id (*accept = 1 iff libsodium accepts; an id >=
+ * edv_keys_count() rejects): the per-message authenticate() that missed the verify-ahead cache
+ * (plenum/server/client_authn.py:99-100 -> nacl_wrappers.py:232-242 Verifier.verify for one
+ * message).  Latency form: a workgroup of edv_resident_kernel stays resident and takes the request
+ * from a mailbox in pinned host memory -- no launch, copy or completion event on the path -- and
+ * leaves after 200 us without a request or as soon as any other call on the context queues GPU
+ * work (it is relaunched by the next edv_verify_one).  Messages over 4 KiB, or a context with the
+ * resident path off (EDV_RESIDENT=0), take one launch of edv_verify_small_kernel.  Same verdicts as
+ * edv_verify_batch_keyed. */
+int edv_verify_one(edv_ctx *ctx, const uint8_t *sig64, uint32_t key_id, const uint8_t *msg, uint64_t mlen,
+                   uint8_t *accept);
 
 /* Staged inputs: the caller DMAs its inputs piece by piece while it is still
  * producing the rest (the authenticator's batch scan queues each 4k-request
@@ -317,10 +341,6 @@ int edv_verify_collect(edv_ctx *ctx, uint64_t ticket, uint8_t *accept_bits);
  * edv_host_free only after the verifies reading the block have returned. */
 int edv_host_alloc(edv_ctx *ctx, uint64_t bytes, void **out);
 int edv_host_free(void *p);
-/* The last host-pointer verify on ctx: out4 = {call ms, CPU staging-copy ms,
- * bytes copied host -> device, direct mask (bit 0 signatures, 1 keys,
- * 2 messages, 3 offsets copied straight from pinned memory)}. */
-int edv_last_host_stats(edv_ctx *ctx, double *out4);
 
 /* Either path with message spans instead of contiguous offsets: item i's
  * message is d_msgs[d_msg_start[i] .. d_msg_end[i]) (uint64 each), so the k
@@ -401,7 +421,7 @@ int edv_tally(edv_ctx *ctx, const uint32_t *key, const uint8_t *voter, const uin
  * verkeys) 128 bytes x.a | x.b | y.a | y.b; 32-byte big-endian coordinates.
  * A G1/G2 encoding that is off the curve decodes to the point at infinity.
  * One GPU lane per check, or two / four for small batches
- * (edv_bls_set_pair_lanes; a COMMIT round's ~25 see the latency, not the
+ * (edv_options.bls_pair_lanes; a COMMIT round's ~25 see the latency, not the
  * throughput); host-pointer calls, synchronous. */
 
 /* BlsCryptoVerifierIndyCrypto.verify_sig (:59-70) over a batch: item i
@@ -422,24 +442,6 @@ int edv_bls_aggregate(edv_ctx *ctx, const uint8_t *sig128, const uint64_t *sig_o
 int edv_bls_sign_batch(edv_ctx *ctx, const uint8_t *sk32, const uint8_t *msgs, const uint64_t *msg_off, uint64_t n,
                        uint8_t *sig128);
 int edv_bls_keygen_batch(edv_ctx *ctx, const uint8_t *sk32, const uint8_t *gen128, uint64_t n, uint8_t *vk128);
-/* Verify batches of at most max_checks take two lanes per check: one Miller
- * loop each (signature / generator on one lane, H(m) / verkey on its
- * neighbour), the product and final exponentiation on both -- about half the
- * serial work of the one-lane form, at half the checks per wave.  Batches of
- * at most max_checks / 2 take four: each Miller loop split over two lanes,
- * then the final exponentiation's cyclotomic squarings spread over three.
- * 0: always one lane per check.  Same verdicts in every form.  Default 32768. */
-int edv_bls_set_pair_lanes(edv_ctx *ctx, uint64_t max_checks);
-/* Verify batches of at most max_checks run one wave per check: the whole
- * pairing check (both Miller loops on one accumulator, the final
- * exponentiation) as a straight-line program of Fp operations spread over
- * the wave's 64 lanes (bls_program.h, tools/gen_bls_program.py), the latency
- * form for a COMMIT round's ~25 checks (~3 ms; 8,192 checks ~22 ms, where
- * the two-lane form takes ~27 ms and the four-lane ~18 ms from one check).  A degenerate Miller step
- * (only a verkey sum outside the order-r subgroup makes one) re-runs on the
- * four-lane kernel, so the verdicts are every form's.  0: never.  Default
- * 8192.  Replaces the same indy-crypto calls as edv_bls_verify_batch. */
-int edv_bls_set_wave_checks(edv_ctx *ctx, uint64_t max_checks);
 
 #ifdef __cplusplus
 }

@@ -702,18 +702,6 @@ static int bls_verify(edv_ctx* ctx, const uint8_t* sig128, const uint8_t* msgs, 
   return 0;
 }
 
-int edv_bls_set_wave_checks(edv_ctx* ctx, uint64_t max_checks) {
-  if (!ctx) return set_err(EDV_EINVAL, "null context");
-  edv_internal::bls_wave_max(ctx) = max_checks;
-  return 0;
-}
-
-int edv_bls_set_pair_lanes(edv_ctx* ctx, uint64_t max_checks) {
-  if (!ctx) return set_err(EDV_EINVAL, "null context");
-  edv_internal::bls_pair_max(ctx) = max_checks;
-  return 0;
-}
-
 int edv_bls_aggregate(edv_ctx* ctx, const uint8_t* sig128, const uint64_t* sig_off, uint64_t m, uint8_t* out128) {
   hipStream_t st;
   int r = edv_internal::begin(ctx, &st);

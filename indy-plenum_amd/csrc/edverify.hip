@@ -246,7 +246,7 @@ __global__ __launch_bounds__(kBlock) void edv_len_key_kernel(const uint64_t* __r
   key[i] = (uint8_t)(blocks < cap ? blocks : cap);
 }
 
-// ---- Packed (SoA) message layout, edv_set_length_buckets mode 3 (north_star
+// ---- Packed (SoA) message layout, edv_options.length_buckets = 3 (north_star
 // (1)): after the block-count sort, each 64-lane group of sorted hash lanes
 // owns a region of the context's unit arena, units(longest message of the
 // group) x 64 lanes x 16 B, unit p of lane l at region + p * 64 + l
@@ -626,7 +626,7 @@ __global__ __launch_bounds__(kBlock) void edv_subset_gather_kernel(const uint32_
   spans_out[m + j] = spans[n + i];
 }
 
-// ---- key order of the comb (edv_set_key_sort) ------------------------------
+// ---- key order of the comb (edv_options.key_sort) ------------------------------
 // A counting sort of a sub-batch's key ids: requests of one key become
 // neighbours, so a wave's 64 comb lanes gather from one key's rows (a few
 // pages) instead of 64 keys' rows spread over the key store -- what lets the
@@ -877,7 +877,7 @@ __global__ __launch_bounds__(kBlock, EDV_COMB_MIN_WAVES) void edv_comb_kernel(co
                                                          const uint32_t* __restrict__ ident,
                                                          uint32_t* __restrict__ pt, uint64_t stride,
                                                          const uint32_t* __restrict__ kperm) {
-  // lane t runs request i = kperm[t] (key-sorted order, edv_set_key_sort) and
+  // lane t runs request i = kperm[t] (key-sorted order, edv_options.key_sort) and
   // leaves R' in slot t for the encode, which reads kperm back
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
@@ -908,7 +908,7 @@ __global__ __launch_bounds__(kBlock, EDV_COMB_MIN_WAVES) void edv_comb_kernel(co
   if (sink == 0x9e3779b9u && key0 == 0xffffffffu && key_count == 0) pt[t] = sink;  // keeps the prefetches live
 }
 
-// ---- low-latency keyed verify for small batches (edv_set_small_batch) -------
+// ---- low-latency keyed verify for small batches (edv_options.small_batch) -------
 // A batch of a few requests (authenticate() of a message the verify-ahead did
 // not cover) is latency-bound: the three-kernel path runs each request's 29
 // mixed additions and its own ~265-product inversion as serial chains on one
@@ -1255,46 +1255,41 @@ struct SmallShared {
   uint32_t base[40];        // [S]B (wave 1): X, Y, Z, T
   int ok_hash, ok_r;
 };
+// One request's verify on a 192-thread workgroup (every thread calls, with the request's signature
+// words loaded): wave 0 hashes, then sums the key comb's rows on its lanes; wave 1 sums the base
+// comb's rows; wave 2 decodes R; the verdict is returned on thread 0 (false elsewhere).  The body
+// of edv_verify_small_kernel (one workgroup per request) and of edv_resident_kernel (one
+// workgroup serving request after request).
 template <int W>
-__global__ __launch_bounds__(kSmallThreads) void edv_verify_small_kernel(
-    const uint8_t* __restrict__ sig64, const uint32_t* __restrict__ key_idx, uint32_t key_count,
-    const uint8_t* __restrict__ key_pk, const uint8_t* __restrict__ key_valid, const uint8_t* __restrict__ msgs,
-    const uint64_t* __restrict__ ms, const uint64_t* __restrict__ me, uint64_t n,
-    const uint32_t* __restrict__ key_tab, uint64_t key_cap, const uint32_t* __restrict__ btab,
-    const uint32_t* __restrict__ ident, uint8_t* __restrict__ ok8) {
+__device__ __forceinline__ bool small_verify(SmallShared& sh, const uint32_t sig[16], uint32_t key0, uint32_t key_count,
+                                             const uint8_t* __restrict__ key_pk, const uint8_t* __restrict__ key_valid,
+                                             const uint8_t* msg, uint64_t mlen, const uint32_t* __restrict__ key_tab,
+                                             uint64_t key_cap, const uint32_t* __restrict__ btab,
+                                             const uint32_t* __restrict__ ident) {
   constexpr int RK = Window<W>::kRows, RB = Window<kBaseW>::kRows;
   static_assert(RK <= 64 && RB <= 64, "one lane per row");
   constexpr int WK = RK <= 16 ? 16 : RK <= 32 ? 32 : 64, WB = RB <= 16 ? 16 : RB <= 32 ? 32 : 64;
-  __shared__ SmallShared sh;
-  const uint64_t i = blockIdx.x;
-  if (i >= n) return;  // block-uniform
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #if EDV_SMALL_LANES
   RDecodeL rd;  // wave 2: R's decode, across the first barrier
 #else
   RDecode rd;  // wave 2, lane 0: R's decode, across the first barrier
 #endif
-  const uint32_t key0 = key_idx[i];
   const bool in_range = key0 < key_count;
   const uint64_t key = in_range ? key0 : 0;
-  uint32_t sig[16];
   if (wave == 0) EDV_SP(0);
-#if EDV_SMALL_PROFILE
-  if (blockIdx.x == 0 && threadIdx.x == 0) g_small_prof[8] = __builtin_amdgcn_s_memtime();
-#endif
-  load_words(sig, sig64 + 64 * i, 16);
   if (wave == 0) {
 #if EDV_SMALL_HASH_LANES
     uint32_t pk[8], h[8];
     load_words(pk, key_pk + 32 * key, 8);
-    const bool hok = verify_phase_hash_lanes(h, sig, pk, msgs + ms[i], me[i] - ms[i], (uint32_t)lane, sh.sw);
+    const bool hok = verify_phase_hash_lanes(h, sig, pk, msg, mlen, (uint32_t)lane, sh.sw);
     if (lane == 0) {
       const bool ok = hok && in_range && key_valid[key];
 #else
     if (lane == 0) {
       uint32_t pk[8], h[8];
       load_words(pk, key_pk + 32 * key, 8);
-      const bool ok = verify_phase_hash(h, sig, pk, msgs + ms[i], me[i] - ms[i]) && in_range && key_valid[key];
+      const bool ok = verify_phase_hash(h, sig, pk, msg, mlen) && in_range && key_valid[key];
 #endif
 #pragma unroll
       for (int k = 0; k < 8; ++k) sh.h[k] = h[k];
@@ -1376,7 +1371,7 @@ __global__ __launch_bounds__(kSmallThreads) void edv_verify_small_kernel(
     ge_p1p1_to_p2_addlike<kSO>(Q, t);  // R' = [h](-A) + [S]B, classes C
   }
   __syncthreads();  // R's decode (wave 2) done
-  if (wave != 0 || lane != 0) return;
+  if (wave != 0 || lane != 0) return false;
   fe xr, yr, u, d;
   load_fe(xr, sh.xr);
   load_fe(yr, sh.yr);
@@ -1386,11 +1381,143 @@ __global__ __launch_bounds__(kSmallThreads) void edv_verify_small_kernel(
   fe_mul_o<kSO>(u, yr, Q.Z);
   fe_sub(d, Q.Y, u);
   ok = ok && fe_iszero(d);
-  ok8[i] = ok ? 1 : 0;
   EDV_SP(7);
 #if EDV_SMALL_PROFILE
   if (blockIdx.x == 0) g_small_prof[9] = __builtin_amdgcn_s_memtime();
 #endif
+  return ok;
+}
+
+
+template <int W>
+__global__ __launch_bounds__(kSmallThreads) void edv_verify_small_kernel(
+    const uint8_t* __restrict__ sig64, const uint32_t* __restrict__ key_idx, uint32_t key_count,
+    const uint8_t* __restrict__ key_pk, const uint8_t* __restrict__ key_valid, const uint8_t* __restrict__ msgs,
+    const uint64_t* __restrict__ ms, const uint64_t* __restrict__ me, uint64_t n,
+    const uint32_t* __restrict__ key_tab, uint64_t key_cap, const uint32_t* __restrict__ btab,
+    const uint32_t* __restrict__ ident, uint8_t* __restrict__ ok8) {
+  __shared__ SmallShared sh;
+  const uint64_t i = blockIdx.x;
+  if (i >= n) return;  // block-uniform
+#if EDV_SMALL_PROFILE
+  if (blockIdx.x == 0 && threadIdx.x == 0) g_small_prof[8] = __builtin_amdgcn_s_memtime();
+#endif
+  uint32_t sig[16];
+  load_words(sig, sig64 + 64 * i, 16);
+  const bool ok = small_verify<W>(sh, sig, key_idx[i], key_count, key_pk, key_valid, msgs + ms[i], me[i] - ms[i],
+                                  key_tab, key_cap, btab, ident);
+  if (threadIdx.x == 0) ok8[i] = ok ? 1 : 0;
+}
+
+// ---------------------------------------------------------------- resident single-request kernel
+// edv_verify_one: one authenticate() that missed the verify-ahead cache.  Launching a kernel, copying
+// its inputs and waiting for its completion cost ~16 us around a ~52 us edv_verify_small_kernel; here
+// one workgroup stays resident and takes requests from a mailbox in fine-grained pinned host memory:
+// the host writes the request and then its number (req_seq); thread 0 polls req_seq with
+// system-scope loads, the workgroup copies the request into LDS, runs small_verify, and thread 0
+// writes the verdict and then done_seq with system-scope stores the host spins on.  It exits when
+// the host sets `stop` (every other library call that queues GPU work does: the stream it runs on may
+// share a hardware queue with theirs) or after idle_ticks of the 100 MHz wall clock without a
+// request, and clears `running` as it leaves -- so the grid always drains, whatever the host does.
+constexpr uint64_t kResMsgMax = 4096;  // longer messages take the launch path
+struct ResBox {
+  uint64_t req_seq;   // host: the request's number, stored after its fields
+  uint64_t stop;      // host: 1 = exit at the next poll
+  uint64_t done_seq;  // kernel: the last request verified, stored after its verdict
+  uint32_t verdict;   // kernel
+  uint32_t running;   // host: 1 at launch; kernel: 0 as it exits
+  uint64_t mlen;
+  uint32_t key_id, key_count;
+  const uint32_t* key_tab;
+  const uint8_t* key_pk;
+  const uint8_t* key_valid;
+  uint64_t key_cap;
+  uint64_t pad[6];
+  uint8_t sig[64];
+  uint8_t msg[kResMsgMax];
+};
+static_assert(offsetof(ResBox, sig) % 64 == 0, "sig 64-byte aligned");
+struct ResShared {
+  uint64_t seq, mlen, key_cap;
+  const uint32_t* key_tab;
+  const uint8_t* key_pk;
+  const uint8_t* key_valid;
+  uint32_t cmd, key_id, key_count, pad;
+  uint32_t sig[16];
+  uint64_t msg[kResMsgMax / 8 + 2];
+};
+__device__ __forceinline__ uint64_t sys_load64_relaxed(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+template <int W>
+__global__ __launch_bounds__(kSmallThreads) void edv_resident_kernel(ResBox* box, const uint32_t* __restrict__ btab,
+                                                                     const uint32_t* __restrict__ ident,
+                                                                     uint64_t idle_ticks) {
+  __shared__ SmallShared sh;
+  __shared__ ResShared rs;
+  const uint32_t t = threadIdx.x;
+  uint64_t last = 0;
+  if (t == 0) last = sys_load64_relaxed(&box->done_seq);
+  for (;;) {
+    if (t == 0) {
+      const uint64_t t0 = wall_clock64();
+      uint32_t cmd = 0;
+      uint64_t seq = last;
+      for (;;) {
+        // relaxed: an acquire here would invalidate this XCD's L2 on every poll, under whatever
+        // kernels share it; the one acquire follows the change
+        seq = sys_load64_relaxed(&box->req_seq);
+        if (seq != last) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: the request's fields after its number
+          cmd = 1;
+          break;
+        }
+        if (sys_load64_relaxed(&box->stop) || wall_clock64() - t0 > idle_ticks) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      rs.cmd = cmd;
+      if (cmd) {
+        rs.seq = seq;
+        rs.mlen = sys_load64_relaxed(&box->mlen);
+        const uint64_t ids = sys_load64_relaxed((const uint64_t*)&box->key_id);
+        rs.key_id = (uint32_t)ids;
+        rs.key_count = (uint32_t)(ids >> 32);
+        rs.key_tab = (const uint32_t*)sys_load64_relaxed((const uint64_t*)&box->key_tab);
+        rs.key_pk = (const uint8_t*)sys_load64_relaxed((const uint64_t*)&box->key_pk);
+        rs.key_valid = (const uint8_t*)sys_load64_relaxed((const uint64_t*)&box->key_valid);
+        rs.key_cap = sys_load64_relaxed(&box->key_cap);
+      }
+    }
+    __syncthreads();
+    if (!rs.cmd) break;  // workgroup-uniform
+    // the request into LDS: 8-byte system-scope loads, all in flight at once (the message is read
+    // over PCIe once; the hash's 16-byte chunk loads then read LDS)
+    const uint64_t mlen = rs.mlen < kResMsgMax ? rs.mlen : kResMsgMax;  // (the host never sends more)
+    const uint64_t nw = (mlen + 7) / 8;
+    for (uint64_t w = t; w < nw; w += kSmallThreads) rs.msg[w] = sys_load64_relaxed((const uint64_t*)box->msg + w);
+    if (t < 8) {
+      const uint64_t v = sys_load64_relaxed((const uint64_t*)box->sig + t);
+      rs.sig[2 * t] = (uint32_t)v;
+      rs.sig[2 * t + 1] = (uint32_t)(v >> 32);
+    }
+    if (t < 2) rs.msg[nw + t] = 0;  // (the hash's last chunk load reads past the message)
+    // key tables rebuilt since the last request (an eviction's build, finished before the host sent
+    // this request) must not be read from this CU's or this XCD's stale cache lines
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    __syncthreads();
+    uint32_t sig[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) sig[k] = rs.sig[k];
+    const bool ok = small_verify<W>(sh, sig, rs.key_id, rs.key_count, rs.key_pk, rs.key_valid,
+                                    (const uint8_t*)rs.msg, mlen, rs.key_tab, rs.key_cap, btab, ident);
+    if (t == 0) {
+      __hip_atomic_store(&box->verdict, ok ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&box->done_seq, rs.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      last = rs.seq;
+    }
+    __syncthreads();  // rs and sh are the next request's
+  }
+  if (t == 0) __hip_atomic_store(&box->running, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Fixed-base comb: [x]B with x < 2^253, 64 madds over BASE_COMB (global).
@@ -1553,7 +1680,7 @@ __global__ void edv_tally_count_kernel(const uint8_t* __restrict__ ballot, uint3
 
 uint64_t div_up(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 
-// Auto length buckets (edv_set_length_buckets mode 2) for calls whose offsets
+// Auto length buckets (edv_options.length_buckets = 2) for calls whose offsets
 // are on the host: sort the hash lanes when unsorted waves would run more than
 // 1.25x the batch's SHA-512 blocks (each wave runs its longest message's
 // block count on all 64 lanes).  Uniform batches (configs[1]: 147-149 B, all
@@ -1597,7 +1724,7 @@ struct edv_ctx {
   uint32_t* d_ucount = nullptr;
   void* d_sort_tmp = nullptr;     // radix-sort temporary storage, one slot per sub-batch
   size_t sort_tmp_bytes = 0;      // per slot (sized for kMaxLanes)
-  int bucket_mode = 2;            // edv_set_length_buckets: 0 off, 1 on, 2 auto, 3 on + packed units
+  int bucket_mode = 2;            // edv_options.length_buckets: 0 off, 1 on, 2 auto, 3 on + packed units
   bool bucket_now = false;        // this launch sorts its hash lanes
   bool pack_now = false;          // ... and packs the messages into the unit arena (mode 3)
   // packed message layout (mode 3): per-group units and offsets
@@ -1608,7 +1735,7 @@ struct edv_ctx {
   size_t scan_tmp_bytes = 0;
   Chunk16* d_arena = nullptr;
   uint64_t arena_units = 0;                  // allocated
-  uint64_t arena_want = kMaxLanes * 80ull;   // edv_set_unit_arena (1.25 GiB: 1,280 B per lane)
+  uint64_t arena_want = kMaxLanes * 80ull;   // edv_options.unit_arena_bytes (1.25 GiB: 1,280 B per lane)
   uint64_t scratch_lanes = 0;
   // Pipelined launches: each chunk of up to kMaxLanes requests is cut into
   // kSub sub-batches whose kernels alternate between `stream` (or the
@@ -1626,21 +1753,31 @@ struct edv_ctx {
   hipEvent_t ev_sub[kSub][kEv] = {};
   hipEvent_t ev_join[2] = {};
   int last_nsub = 0;
-  uint64_t last_chunk_n = 0;  // requests in the last chunk (what edv_last_phases_ms covers)
-  int max_sub = 1;  // edv_set_pipeline (1, 2 and 4 sub-batches measure within 1% at 1M: profiles/r02b)
-  // key-sorted comb order (edv_set_key_sort): the permutation and the verdict bytes [kMaxLanes];
+  uint64_t last_chunk_n = 0;  // requests in the last chunk (what edv_stats.phase_ms covers)
+  int max_sub = 1;  // edv_options.pipeline (1, 2 and 4 sub-batches measure within 1% at 1M: profiles/r02b)
+  // key-sorted comb order (edv_options.key_sort): the permutation and the verdict bytes [kMaxLanes];
   // per sub-batch: block offsets [kSortBlocks][bins], bin totals / bases [bins] x 2, scan scratch
   int key_sort = 2;
-  uint64_t bls_pair_max = 32768;  // edv_bls_set_pair_lanes
-  uint64_t bls_wave_max = 8192;   // edv_bls_set_wave_checks (8,192 checks 21.8 ms; the two-lane form 27.3)
+  uint64_t bls_pair_max = 32768;  // edv_options.bls_pair_lanes
+  uint64_t bls_wave_max = 8192;   // edv_options.bls_wave_checks (8,192 checks 21.8 ms; the two-lane form 27.3)
   // the small keyed path reads its packed inputs straight from pinned host memory (no H2D copy
   // before the kernel); A/B switch EDV_SMALL_ZC=1
   bool small_zero_copy = getenv("EDV_SMALL_ZC") != nullptr;
-  // phase events around a single request's small kernel (edv_last_phases_ms): off unless
+  // phase events around a single request's small kernel (edv_stats.phase_ms): off unless
   // EDV_SMALL_EVENTS=1 -- the two timestamps cost ~8 us of the round trip (119-126 against
   // 128-134 us per engine call, profiles/r05y)
   bool small_events = getenv("EDV_SMALL_EVENTS") != nullptr;
-  uint64_t small_max = 256;  // edv_set_small_batch: keyed host-pointer chunks of at most this many requests take
+  // edv_verify_one's resident kernel (edv_resident_kernel): its mailbox, stream, request counter,
+  // whether one was launched (it may have left since: box->running), the key window it serves, and
+  // whether the path is on (EDV_RESIDENT=0: every single request launches edv_verify_small_kernel)
+  ResBox* res_box = nullptr;
+  hipStream_t stream_res = nullptr;
+  uint64_t res_seq = 0;
+  bool res_launched = false, res_stopping = false;
+  int res_w = 0;
+  bool res_on = !(getenv("EDV_RESIDENT") && getenv("EDV_RESIDENT")[0] == '0');
+  uint64_t res_launches = 0, res_served = 0;
+  uint64_t small_max = 256;  // edv_options.small_batch: keyed host-pointer chunks of at most this many requests take
                              // edv_verify_small_kernel (0 = never)
   uint32_t* d_kperm = nullptr;
   uint8_t* d_ok8 = nullptr;
@@ -1781,8 +1918,19 @@ void free_buf(edv_ctx::Buf& b) {
   b.cap = 0;
 }
 
+// The resident kernel leaves at its next poll: any call that queues GPU work asks it to, since its
+// stream may share a hardware queue with the call's streams (GPU_MAX_HW_QUEUES), where it would
+// hold the call's kernels back until its idle timeout.
+void resident_yield(edv_ctx* ctx) {
+  if (ctx->res_launched && !ctx->res_stopping) {
+    __atomic_store_n(&ctx->res_box->stop, (uint64_t)1, __ATOMIC_RELEASE);
+    ctx->res_stopping = true;
+  }
+}
+
 int set_device(edv_ctx* ctx) {
   if (!ctx) return set_err(EDV_EINVAL, "null context");
+  resident_yield(ctx);
   HIP_TRY(hipSetDevice(ctx->device));
   return 0;
 }
@@ -2109,7 +2257,7 @@ int launch_pipeline(edv_ctx* ctx, bool keyed, const void* d_sig, const void* d_k
 }
 
 // A small keyed batch through edv_verify_small_kernel (one workgroup per request) and the
-// verdict-byte pack; its duration lands in the comb phase of edv_last_phases_ms.
+// verdict-byte pack; its duration lands in the comb phase of edv_stats.phase_ms.
 // host_ok8 (pinned host memory, n bytes): the kernel stores the verdict bytes there itself and
 // no pack kernel or D2H copy follows (d_words unused) -- two fewer GPU commands on the latency
 // path of one authenticate().
@@ -2722,8 +2870,8 @@ int edv_keys_set_many_async(edv_ctx* ctx, const uint32_t* ids, const uint8_t* pk
 }
 
 int edv_keys_ready(edv_ctx* ctx, uint64_t ticket) {
-  int r = set_device(ctx);
-  if (r) return r;
+  if (!ctx) return set_err(EDV_EINVAL, "null context");  // (a query: the resident kernel stays)
+  HIP_TRY(hipSetDevice(ctx->device));
   while (ticket > ctx->build_done && !ctx->builds.empty()) {
     const hipError_t e = hipEventQuery(ctx->builds.front().ev);
     if (e == hipErrorNotReady) return 0;
@@ -2806,6 +2954,121 @@ int edv_verify_batch_keyed(edv_ctx* ctx, const uint8_t* sig64, const uint32_t* k
   if (n == 0) return 0;
   if (!sig64 || !key_idx || !msg_off || !accept_bits) return set_err(EDV_EINVAL, "null pointer");
   return host_verify(ctx, true, sig64, 64, (const uint8_t*)key_idx, msgs, msg_off, n, accept_bits);
+}
+
+inline void cpu_relax() { __builtin_ia32_pause(); }
+
+// edv_verify_one through the resident kernel: 0 with *accept set, 1 when this request must take the
+// launch path instead (message too long, resident path off or broken), or an EDV_E* error.
+int verify_one_resident(edv_ctx* ctx, const uint8_t* sig64, uint32_t key_id, const uint8_t* msg, uint64_t mlen,
+                        uint8_t* accept) {
+  if (!ctx->res_on || mlen > kResMsgMax || ctx->key_count == 0) return 1;
+  using rclk = std::chrono::steady_clock;
+  HIP_TRY(hipSetDevice(ctx->device));
+  if (!ctx->res_box) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, sizeof(ResBox), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
+      ctx->res_on = false;
+      return 1;
+    }
+    memset(p, 0, sizeof(ResBox));
+    ctx->res_box = (ResBox*)p;
+  }
+  ResBox* b = ctx->res_box;
+  auto wait_gone = [&]() -> int {  // a kernel asked to leave: until it has (bounded: it polls every ~us)
+    const auto t0 = rclk::now();
+    while (__atomic_load_n(&b->running, __ATOMIC_ACQUIRE) != 0) {
+      if (rclk::now() - t0 > std::chrono::seconds(2)) {
+        HIP_TRY(hipStreamSynchronize(ctx->stream_res));
+        break;
+      }
+      cpu_relax();
+    }
+    ctx->res_launched = ctx->res_stopping = false;
+    return 0;
+  };
+  int r;
+  if (ctx->res_launched && ctx->res_w != ctx->key_w && !ctx->res_stopping) {  // another window: another kernel
+    __atomic_store_n(&b->stop, (uint64_t)1, __ATOMIC_RELEASE);
+    ctx->res_stopping = true;
+  }
+  if (ctx->res_launched && ctx->res_stopping && (r = wait_gone())) return r;
+  auto launch = [&](uint64_t answered) -> int {  // answered: the last request the host has its verdict of
+    __atomic_store_n(&b->stop, (uint64_t)0, __ATOMIC_RELAXED);
+    __atomic_store_n(&b->done_seq, answered, __ATOMIC_RELAXED);
+    __atomic_store_n(&b->running, 1u, __ATOMIC_RELEASE);
+    // idle exit after 200 us without a request (100 MHz wall clock): a burst of cache misses keeps it,
+    // and anything queued behind it on a shared hardware queue waits at most that long
+    const uint64_t idle = 20000;
+#define EDV_RES_CASE(W)                                                                                   \
+  case W:                                                                                                 \
+    hipLaunchKernelGGL(edv_resident_kernel<W>, dim3(1), dim3(kSmallThreads), 0, ctx->stream_res, b,      \
+                       ctx->d_btab_comb32, ctx->d_ident, idle);                                           \
+    break;
+    switch (ctx->key_w) {
+      EDV_KEY_WINDOWS(EDV_RES_CASE)
+      default:
+        __atomic_store_n(&b->running, 0u, __ATOMIC_RELEASE);
+        return set_err(EDV_EINVAL, "key window %d", ctx->key_w);
+    }
+#undef EDV_RES_CASE
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      __atomic_store_n(&b->running, 0u, __ATOMIC_RELEASE);
+      return set_err(EDV_EHIP, "resident kernel launch: %s", hipGetErrorString(e));
+    }
+    ctx->res_launched = true;
+    ctx->res_stopping = false;
+    ctx->res_w = ctx->key_w;
+    ++ctx->res_launches;
+    return 0;
+  };
+  if (ctx->res_launched && __atomic_load_n(&b->running, __ATOMIC_ACQUIRE) == 0) ctx->res_launched = false;  // idled out
+  if (!ctx->res_launched && (r = launch(ctx->res_seq))) return r;
+  // the request, then its number
+  b->mlen = mlen;
+  b->key_id = key_id;
+  b->key_count = (uint32_t)ctx->key_count;
+  b->key_tab = ctx->d_key_tab;
+  b->key_pk = ctx->d_key_pk;
+  b->key_valid = ctx->d_key_valid;
+  b->key_cap = ctx->key_cap;
+  memcpy(b->sig, sig64, 64);
+  if (mlen) memcpy(b->msg, msg, (size_t)mlen);
+  const uint64_t seq = ++ctx->res_seq;
+  __atomic_store_n(&b->req_seq, seq, __ATOMIC_RELEASE);
+  const auto t0 = rclk::now();
+  uint32_t spins = 0;
+  while (__atomic_load_n(&b->done_seq, __ATOMIC_ACQUIRE) != seq) {
+    cpu_relax();
+    if ((++spins & 255) != 0) continue;
+    if (__atomic_load_n(&b->running, __ATOMIC_ACQUIRE) == 0 &&
+        __atomic_load_n(&b->done_seq, __ATOMIC_ACQUIRE) != seq) {
+      // it idled out just before the request arrived: a fresh kernel picks the request up
+      ctx->res_launched = false;
+      if ((r = launch(seq - 1))) return r;
+    }
+    if (rclk::now() - t0 > std::chrono::seconds(5)) {  // never expected: stop using it on this context
+      resident_yield(ctx);
+      ctx->res_on = false;
+      return set_err(EDV_EHIP, "resident kernel did not answer request %llu within 5 s", (unsigned long long)seq);
+    }
+  }
+  *accept = __atomic_load_n(&b->verdict, __ATOMIC_ACQUIRE) ? 1 : 0;
+  ++ctx->res_served;
+  return 0;
+}
+
+int edv_verify_one(edv_ctx* ctx, const uint8_t* sig64, uint32_t key_id, const uint8_t* msg, uint64_t mlen,
+                   uint8_t* accept) {
+  if (!ctx) return set_err(EDV_EINVAL, "null context");
+  if (!sig64 || !accept || (mlen && !msg)) return set_err(EDV_EINVAL, "null pointer");
+  const int r = verify_one_resident(ctx, sig64, key_id, msg, mlen, accept);
+  if (r <= 0) return r;
+  // the launch path: one request through edv_verify_small_kernel
+  uint64_t off[2] = {0, mlen};
+  *accept = 0;
+  return edv_verify_batch_keyed(ctx, sig64, &key_id, msg, off, 1, accept);
 }
 
 int edv_verify_batch_keyed_slots(edv_ctx* ctx, const uint8_t* sig_slots, const uint32_t* key_idx, const uint8_t* msgs,
@@ -3166,14 +3429,6 @@ int edv_host_free(void* p) {
   return 0;
 }
 
-int edv_last_host_stats(edv_ctx* ctx, double* out4) {
-  if (!ctx || !out4) return set_err(EDV_EINVAL, "null argument");
-  out4[0] = ctx->last_call_ms;
-  out4[1] = ctx->last_stage_ms;
-  out4[2] = (double)ctx->last_h2d_bytes;
-  out4[3] = (double)ctx->last_direct;
-  return 0;
-}
 
 }  // extern "C"
 
@@ -3219,6 +3474,8 @@ edv_ctx* edv_create(int device) {
   if ((e = hipStreamCreateWithFlags(&ctx->stream_key, hipStreamNonBlocking)) != hipSuccess)
     return fail("hipStreamCreate", e);
   if ((e = hipStreamCreateWithFlags(&ctx->stream_build, hipStreamNonBlocking)) != hipSuccess)
+    return fail("hipStreamCreate", e);
+  if ((e = hipStreamCreateWithFlags(&ctx->stream_res, hipStreamNonBlocking)) != hipSuccess)
     return fail("hipStreamCreate", e);
   for (hipEvent_t& f : ctx->ev_fence)
     if ((e = hipEventCreateWithFlags(&f, hipEventDisableTiming)) != hipSuccess) return fail("hipEventCreate", e);
@@ -3300,6 +3557,10 @@ edv_ctx* edv_create(int device) {
 void edv_destroy(edv_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
+  resident_yield(ctx);  // the resident kernel leaves at its next poll; its stream is drained first
+  if (ctx->stream_res) (void)hipStreamSynchronize(ctx->stream_res);
+  if (ctx->stream_res) (void)hipStreamDestroy(ctx->stream_res);
+  if (ctx->res_box) (void)hipHostFree(ctx->res_box);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->stream_copy) (void)hipStreamSynchronize(ctx->stream_copy);
   if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
@@ -3390,10 +3651,10 @@ int edv_verify_batch_device(edv_ctx* ctx, const void* d_sig64, const void* d_pk3
   return launch_verify(ctx, d_sig64, d_pk32, d_msgs, d_msg_off, n, d_accept_words, pick_stream(ctx, stream));
 }
 
-int edv_last_phases_ms(edv_ctx* ctx, double* out4) {
-  if (!ctx || !ctx->timed) return set_err(EDV_EINVAL, "no timed verify launch yet");
-  if (!out4) return set_err(EDV_EINVAL, "null output");
-  for (int k = 0; k < edv_ctx::kEv - 1; ++k) out4[k] = 0.0;
+// Options and statistics (include/edverify.h: edv_options, edv_stats).
+namespace {
+int phases_into(edv_ctx* ctx, double* out4) {  // the last timed launch's phase sums (waits for its events)
+  for (int k = 0; k < 4; ++k) out4[k] = 0.0;
   if (ctx->small_timed) {  // launch_small: the one kernel is the comb phase
     float t = 0.f;
     HIP_TRY(hipEventSynchronize(ctx->ev_sub[0][3]));
@@ -3411,21 +3672,74 @@ int edv_last_phases_ms(edv_ctx* ctx, double* out4) {
   }
   return 0;
 }
+}  // namespace
 
-int edv_last_launch_count(edv_ctx* ctx) { return ctx ? ctx->last_nsub : 0; }
-uint64_t edv_last_chunk_items(edv_ctx* ctx) { return ctx ? ctx->last_chunk_n : 0; }
+void edv_default_options(edv_options* out) {
+  if (!out) return;
+  memset(out, 0, sizeof *out);
+  out->pipeline = 1;
+  out->length_buckets = 2;
+  out->key_sort = 2;
+  out->resident = 1;
+  out->small_batch = 256;
+  out->unit_arena_bytes = kMaxLanes * 80ull * sizeof(Chunk16);
+  out->bls_pair_lanes = 32768;
+  out->bls_wave_checks = 8192;
+}
 
-int edv_set_length_buckets(edv_ctx* ctx, int mode) {
-  if (!ctx) return set_err(EDV_EINVAL, "null context");
-  if (mode < 0 || mode > 3)
-    return set_err(EDV_EINVAL, "length-bucket mode %d (0 off, 1 on, 2 auto, 3 on + packed units)", mode);
-  ctx->bucket_mode = mode;
+int edv_get_options(edv_ctx* ctx, edv_options* out) {
+  if (!ctx || !out) return set_err(EDV_EINVAL, "null argument");
+  memset(out, 0, sizeof *out);
+  out->pipeline = ctx->max_sub;
+  out->length_buckets = ctx->bucket_mode;
+  out->key_sort = ctx->key_sort;
+  out->resident = ctx->res_on ? 1 : 0;
+  out->small_batch = ctx->small_max;
+  out->unit_arena_bytes = ctx->arena_want * sizeof(Chunk16);
+  out->bls_pair_lanes = ctx->bls_pair_max;
+  out->bls_wave_checks = ctx->bls_wave_max;
   return 0;
 }
 
-int edv_set_unit_arena(edv_ctx* ctx, uint64_t bytes) {
-  if (!ctx) return set_err(EDV_EINVAL, "null context");
-  ctx->arena_want = bytes / sizeof(Chunk16);
+int edv_set_options(edv_ctx* ctx, const edv_options* o) {
+  if (!ctx || !o) return set_err(EDV_EINVAL, "null argument");
+  // every field checked before any is applied: a refused call leaves the context as it was
+  if (o->pipeline < 1 || o->pipeline > edv_ctx::kSub)
+    return set_err(EDV_EINVAL, "pipeline %d (1..%d sub-batches)", o->pipeline, edv_ctx::kSub);
+  if (o->length_buckets < 0 || o->length_buckets > 3)
+    return set_err(EDV_EINVAL, "length_buckets %d (0 off, 1 on, 2 auto, 3 on + packed units)", o->length_buckets);
+  if (o->key_sort < 0 || o->key_sort > 2) return set_err(EDV_EINVAL, "key_sort %d (0 off, 1 on, 2 auto)", o->key_sort);
+  if (o->resident < 0 || o->resident > 1) return set_err(EDV_EINVAL, "resident %d (0 off, 1 on)", o->resident);
+  if (o->small_batch > 65536)
+    return set_err(EDV_EINVAL, "small_batch %llu (at most 65536)", (unsigned long long)o->small_batch);
+  if (!o->resident) resident_yield(ctx);
+  ctx->max_sub = o->pipeline;
+  ctx->bucket_mode = o->length_buckets;
+  ctx->key_sort = o->key_sort;
+  ctx->res_on = o->resident != 0;
+  ctx->small_max = o->small_batch;
+  ctx->arena_want = o->unit_arena_bytes / sizeof(Chunk16);
+  ctx->bls_pair_max = o->bls_pair_lanes;
+  ctx->bls_wave_max = o->bls_wave_checks;
+  return 0;
+}
+
+int edv_get_stats(edv_ctx* ctx, edv_stats* out) {
+  if (!ctx || !out) return set_err(EDV_EINVAL, "null argument");
+  memset(out, 0, sizeof *out);
+  if (ctx->timed) {
+    int r = phases_into(ctx, out->phase_ms);
+    if (r) return r;
+    out->phases_valid = 1;
+  }
+  out->launch_count = ctx->last_nsub;
+  out->chunk_items = ctx->last_chunk_n;
+  out->host_call_ms = ctx->last_call_ms;
+  out->host_stage_ms = ctx->last_stage_ms;
+  out->host_h2d_bytes = ctx->last_h2d_bytes;
+  out->host_direct = (uint32_t)ctx->last_direct;
+  out->resident_launches = ctx->res_launches;
+  out->resident_served = ctx->res_served;
   return 0;
 }
 
@@ -3435,44 +3749,6 @@ int edv_small_profile(uint64_t* out10) {  // probe builds only (not in include/e
   return 0;
 }
 #endif
-int edv_set_small_batch(edv_ctx* ctx, uint64_t max_requests) {
-  if (!ctx) return set_err(EDV_EINVAL, "null context");
-  if (max_requests > 65536) return set_err(EDV_EINVAL, "small-batch limit %llu (at most 65536)",
-                                            (unsigned long long)max_requests);
-  ctx->small_max = max_requests;
-  return 0;
-}
-
-int edv_set_key_sort(edv_ctx* ctx, int mode) {
-  if (!ctx) return set_err(EDV_EINVAL, "null context");
-  if (mode < 0 || mode > 2) return set_err(EDV_EINVAL, "key-sort mode %d (0 off, 1 on, 2 auto)", mode);
-  ctx->key_sort = mode;
-  return 0;
-}
-
-int edv_set_pipeline(edv_ctx* ctx, int sub_batches) {
-  if (!ctx) return set_err(EDV_EINVAL, "null context");
-  if (sub_batches < 1 || sub_batches > edv_ctx::kSub)
-    return set_err(EDV_EINVAL, "sub_batches %d (1..%d)", sub_batches, edv_ctx::kSub);
-  ctx->max_sub = sub_batches;
-  return 0;
-}
-
-int edv_last_phase_ms(edv_ctx* ctx, double* hash_ms, double* table_ms, double* dsm_ms) {
-  double t[4];
-  int r = edv_last_phases_ms(ctx, t);
-  if (r) return r;
-  if (hash_ms) *hash_ms = t[0];
-  if (table_ms) *table_ms = t[1];
-  if (dsm_ms) *dsm_ms = t[2];
-  return 0;
-}
-
-double edv_last_kernel_ms(edv_ctx* ctx) {
-  double d = -1.0;
-  if (edv_last_phase_ms(ctx, nullptr, nullptr, &d) != 0) return -1.0;
-  return d;
-}
 
 int edv_verify_batch(edv_ctx* ctx, const uint8_t* sig64, const uint8_t* pk32, const uint8_t* msgs,
                      const uint64_t* msg_off, uint64_t n, uint8_t* accept_bits) {

@@ -25,16 +25,13 @@ SIGNATURES = {
     "edv_create": (_P, [_I]),
     "edv_destroy": (None, [_P]),
     "edv_synchronize": (_I, [_P]),
+    "edv_default_options": (None, [_P]),
+    "edv_get_options": (_I, [_P, _P]),
+    "edv_set_options": (_I, [_P, _P]),
+    "edv_get_stats": (_I, [_P, _P]),
     "edv_verify_batch": (_I, [_P, _P, _P, _P, _P, _U64, _P]),
     "edv_sign_open_batch": (_I, [_P, _P, _P, _P, _U64, _P]),
     "edv_verify_batch_device": (_I, [_P, _P, _P, _P, _P, _U64, _P, _P]),
-    "edv_last_phases_ms": (_I, [_P, _P]),
-    "edv_last_launch_count": (_I, [_P]),
-    "edv_last_chunk_items": (_U64, [_P]),
-    "edv_set_pipeline": (_I, [_P, _I]),
-    "edv_set_length_buckets": (_I, [_P, _I]),
-    "edv_set_key_sort": (_I, [_P, _I]),
-    "edv_set_small_batch": (_I, [_P, _U64]),
     "edv_stage_reserve": (_I, [_P, _U64]),
     "edv_stage_put": (_I, [_P, _P, _U64, _U64]),
     "edv_verify_staged": (_I, [_P, _I, _P, _U64, _U64, _P, _P, _U64, _P]),
@@ -45,9 +42,6 @@ SIGNATURES = {
     "edv_verify_staged_part": (_I, [_P, _P, _U64, _U64, _P, _U64, _U64, _U64]),
     "edv_verify_staged_end": (_I, [_P]),
     "edv_verify_staged_subset": (_I, [_P, _P, _P, _U64, _P]),
-    "edv_set_unit_arena": (_I, [_P, _U64]),
-    "edv_last_phase_ms": (_I, [_P, _P, _P, _P]),
-    "edv_last_kernel_ms": (_c.c_double, [_P]),
     "edv_keys_add": (_I, [_P, _P, _U64, _P]),
     "edv_keys_add_device": (_I, [_P, _P, _U64, _P, _P]),
     "edv_keys_set": (_I, [_P, _U64, _P, _U64]),
@@ -62,6 +56,7 @@ SIGNATURES = {
     "edv_keys_window": (_I, [_P]),
     "edv_verify_batch_keyed": (_I, [_P, _P, _P, _P, _P, _U64, _P]),
     "edv_verify_batch_keyed_device": (_I, [_P, _P, _P, _P, _P, _U64, _P, _P]),
+    "edv_verify_one": (_I, [_P, _P, _U32, _P, _U64, _P]),
     "edv_verify_spans_device": (_I, [_P, _P, _P, _I, _P, _P, _P, _U64, _P, _P]),
     "edv_verify_batch_slots": (_I, [_P, _P, _P, _P, _P, _U64, _P]),
     "edv_verify_batch_keyed_slots": (_I, [_P, _P, _P, _P, _P, _U64, _P]),
@@ -69,7 +64,6 @@ SIGNATURES = {
     "edv_verify_collect": (_I, [_P, _U64, _P]),
     "edv_host_alloc": (_I, [_P, _U64, _P]),
     "edv_host_free": (_I, [_P]),
-    "edv_last_host_stats": (_I, [_P, _P]),
     "edv_seed_keypair_batch": (_I, [_P, _P, _U64, _P, _P]),
     "edv_sign_batch_device": (_I, [_P, _P, _P, _P, _P, _U64, _P, _P]),
     "edv_sign_spans_device": (_I, [_P, _P, _P, _P, _P, _P, _U64, _P, _P]),
@@ -83,8 +77,6 @@ SIGNATURES = {
     "edv_bls_aggregate": (_I, [_P, _P, _P, _U64, _P]),
     "edv_bls_sign_batch": (_I, [_P, _P, _P, _P, _U64, _P]),
     "edv_bls_keygen_batch": (_I, [_P, _P, _P, _U64, _P]),
-    "edv_bls_set_pair_lanes": (_I, [_P, _U64]),
-    "edv_bls_set_wave_checks": (_I, [_P, _U64]),
 }
 
 
@@ -98,6 +90,21 @@ class EdVerifyError(RuntimeError):
     def __init__(self, code, msg):
         super().__init__("edverify error %d: %s" % (code, msg))
         self.code = code
+
+
+class EdvOptions(ctypes.Structure):
+    """include/edverify.h edv_options."""
+    _fields_ = [("pipeline", ctypes.c_int32), ("length_buckets", ctypes.c_int32), ("key_sort", ctypes.c_int32),
+                ("resident", ctypes.c_int32), ("small_batch", ctypes.c_uint64), ("unit_arena_bytes", ctypes.c_uint64),
+                ("bls_pair_lanes", ctypes.c_uint64), ("bls_wave_checks", ctypes.c_uint64)]
+
+
+class EdvStats(ctypes.Structure):
+    """include/edverify.h edv_stats."""
+    _fields_ = [("phase_ms", ctypes.c_double * 4), ("launch_count", ctypes.c_int32), ("phases_valid", ctypes.c_int32),
+                ("chunk_items", ctypes.c_uint64), ("host_call_ms", ctypes.c_double), ("host_stage_ms", ctypes.c_double),
+                ("host_h2d_bytes", ctypes.c_uint64), ("host_direct", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+                ("resident_launches", ctypes.c_uint64), ("resident_served", ctypes.c_uint64)]
 
 
 EDV_EBUSY = -5  # include/edverify.h: the staging set holds an uncollected submission

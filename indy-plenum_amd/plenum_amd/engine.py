@@ -5,13 +5,14 @@ entry points replace per-request calls of
 stp_core/crypto/nacl_wrappers.py:232-242 (Verifier.verify) with one batched
 launch; verdicts are libsodium 1.0.18's (crypto_sign_verify_detached == 0).
 """
+import contextlib
 import ctypes
 import threading
 
 import numpy as np
 
 from . import _lib
-from ._lib import EdVerifyUnavailable, check
+from ._lib import EdVerifyError, EdVerifyUnavailable, check
 
 
 def _ptr(a):
@@ -317,10 +318,9 @@ class EdVerifyEngine:
         """The last host-pointer verify: dict(call_ms, stage_ms, h2d_bytes,
         direct) -- stage_ms is the CPU copy into pinned staging (0 when every
         input came from host_alloc memory)."""
-        out = (ctypes.c_double * 4)()
-        check(self._lib.edv_last_host_stats(self._ctx, out))
-        d = int(out[3])
-        return {"call_ms": out[0], "stage_ms": out[1], "h2d_bytes": int(out[2]),
+        st = self.stats()
+        d = int(st["host_direct"])
+        return {"call_ms": st["host_call_ms"], "stage_ms": st["host_stage_ms"], "h2d_bytes": int(st["host_h2d_bytes"]),
                 "direct": {"sig": bool(d & 1), "keys": bool(d & 2), "msgs": bool(d & 4), "offsets": bool(d & 8)}}
 
     def sign_open_batch(self, sm, sm_off, pk32):
@@ -344,54 +344,98 @@ class EdVerifyEngine:
         check(self._lib.edv_verify_batch_device(self._ctx, _dev(d_sig64), _dev(d_pk32), _dev(d_msgs),
                                                 _dev(d_msg_off), n, _dev(d_accept_words), st))
 
-    def last_phase_ms(self):
-        """(hash, table, dsm) milliseconds of the last verify launch (HIP events)."""
-        h, t, d = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
-        check(self._lib.edv_last_phase_ms(self._ctx, ctypes.byref(h), ctypes.byref(t), ctypes.byref(d)))
-        return h.value, t.value, d.value
+    # ------------------------------------------------------- options / stats
+    # edverify.h edv_options: every knob in one struct, read and written whole (edv_set_options checks
+    # every field before applying any); options(**kw) sets some for a with-block and puts the previous
+    # values back however the block ends.
+    _OPTION_NAMES = ("pipeline", "length_buckets", "key_sort", "resident", "small_batch", "unit_arena_bytes",
+                     "bls_pair_lanes", "bls_wave_checks")
+    _MODES = {"length_buckets": {"auto": 2, "on": 1, "off": 0, "packed": 3}, "key_sort": {"auto": 2, "on": 1, "off": 0}}
+
+    def get_options(self):
+        o = _lib.EdvOptions()
+        check(self._lib.edv_get_options(self._ctx, ctypes.byref(o)))
+        return {k: getattr(o, k) for k in self._OPTION_NAMES}
+
+    def set_options(self, **kw):
+        """Change some options (names of edv_options; modes also as "auto" / "on" / "off" / "packed",
+        booleans as 1 / 0); an invalid value raises and changes nothing."""
+        unknown = set(kw) - set(self._OPTION_NAMES)
+        if unknown:
+            raise ValueError("unknown options: %s" % sorted(unknown))
+        cur = self.get_options()
+        for k, v in kw.items():
+            cur[k] = int(self._MODES.get(k, {}).get(v, v))
+        check(self._lib.edv_set_options(self._ctx, ctypes.byref(_lib.EdvOptions(**cur))))
+
+    @contextlib.contextmanager
+    def options(self, **kw):
+        before = self.get_options()
+        self.set_options(**kw)
+        try:
+            yield self
+        finally:
+            check(self._lib.edv_set_options(self._ctx, ctypes.byref(_lib.EdvOptions(**before))))
+
+    @staticmethod
+    def default_options():
+        o = _lib.EdvOptions()
+        _lib.load().edv_default_options(ctypes.byref(o))
+        return {k: getattr(o, k) for k in EdVerifyEngine._OPTION_NAMES}
+
+    def stats(self):
+        """edv_get_stats as a dict (waits for the last timed launch's events)."""
+        st = _lib.EdvStats()
+        check(self._lib.edv_get_stats(self._ctx, ctypes.byref(st)))
+        out = {k: getattr(st, k) for k, _ in _lib.EdvStats._fields_ if k not in ("phase_ms", "reserved")}
+        out["phase_ms"] = tuple(st.phase_ms)
+        return out
 
     def last_phases_ms(self):
         """(hash, table, dsm-or-comb, encode) milliseconds of the last verify
         launch, from HIP events on the launch streams: per phase the sum over
         the last chunk's sub-batch launches (see last_launch_count)."""
-        out = (ctypes.c_double * 4)()
-        check(self._lib.edv_last_phases_ms(self._ctx, out))
-        return tuple(out)
+        st = self.stats()
+        if not st["phases_valid"]:
+            raise EdVerifyError(-1, "no timed verify launch yet")
+        return st["phase_ms"]
+
+    def last_phase_ms(self):
+        """(hash, table, dsm) milliseconds of the last verify launch (HIP events)."""
+        return self.last_phases_ms()[:3]
 
     def last_launch_count(self):
         """Kernel launches per phase (sub-batches) in the last verify chunk."""
-        return int(self._lib.edv_last_launch_count(self._ctx))
+        return int(self.stats()["launch_count"])
 
     def last_chunk_items(self):
         """Requests in the last verify chunk (what last_phases_ms covers)."""
-        return int(self._lib.edv_last_chunk_items(self._ctx))
+        return int(self.stats()["chunk_items"])
 
     def set_pipeline(self, sub_batches):
         """Sub-batches per chunk (1..4; 1 = kernels run one at a time)."""
-        check(self._lib.edv_set_pipeline(self._ctx, int(sub_batches)))
+        self.set_options(pipeline=sub_batches)
 
     def set_small_batch(self, max_requests):
         """Keyed host-pointer verifies of at most max_requests requests take the
-        low-latency kernel (edv_set_small_batch; default 256, 0 = never)."""
-        check(self._lib.edv_set_small_batch(self._ctx, int(max_requests)))
+        low-latency kernel (default 256, 0 = never)."""
+        self.set_options(small_batch=max_requests)
 
     def set_key_sort(self, mode):
         """Key-sorted comb order on the key-table path: False/0 off, True/1
         on, "auto"/2 (the default: sub-batches of 4,096 requests or more)."""
-        m = {"auto": 2, "on": 1, "off": 0}.get(mode, mode)
-        check(self._lib.edv_set_key_sort(self._ctx, int(m)))
+        self.set_options(key_sort=mode)
 
     def set_length_buckets(self, mode):
         """Hash lanes sorted by SHA-512 block count: False/0 off, True/1 on,
         "auto"/2 (the default; host-offset calls decide per batch, edverify.h),
         "packed"/3 sorted and packed into the length-bucketed SoA unit layout."""
-        m = {"auto": 2, "on": 1, "off": 0, "packed": 3}.get(mode, mode)
-        check(self._lib.edv_set_length_buckets(self._ctx, int(m)))
+        self.set_options(length_buckets=mode)
 
     def set_unit_arena(self, nbytes):
         """Unit-arena size of the packed mode in bytes (groups beyond it are
         hashed in place)."""
-        check(self._lib.edv_set_unit_arena(self._ctx, int(nbytes)))
+        self.set_options(unit_arena_bytes=nbytes)
 
     # ------------------------------------------------------------------ BLS
     # BN254 BLS (indy-crypto's Bls, bls_crypto_indy_crypto.py:59-90); G1 / G2
@@ -422,14 +466,14 @@ class EdVerifyEngine:
 
     def bls_set_pair_lanes(self, max_checks):
         """Verify batches of at most max_checks use two lanes per check (lower
-        latency); 0 = one lane per check always (edv_bls_set_pair_lanes)."""
-        check(self._lib.edv_bls_set_pair_lanes(self._ctx, int(max_checks)))
+        latency); 0 = one lane per check always (edv_options.bls_pair_lanes)."""
+        self.set_options(bls_pair_lanes=max_checks)
 
     def bls_set_wave_checks(self, max_checks):
         """Verify batches of at most max_checks run one wave per check (the
         check as a straight-line program over the wave's lanes: the latency
-        form); 0 = never (edv_bls_set_wave_checks)."""
-        check(self._lib.edv_bls_set_wave_checks(self._ctx, int(max_checks)))
+        form); 0 = never (edv_options.bls_wave_checks)."""
+        self.set_options(bls_wave_checks=max_checks)
 
     def bls_aggregate(self, sig128, sig_off):
         """out[i] = sum of sig128[sig_off[i]:sig_off[i+1]] (create_multi_sig)."""
@@ -566,18 +610,16 @@ class EdVerifyEngine:
         without the numpy packing around it."""
         if len(sig64) != 64:
             raise ValueError("sig64 must be 64 bytes")
+        # (edv_verify_one: the resident kernel's mailbox, or one launch of the small kernel)
         # argument objects of this thread, reused from call to call (building them costs microseconds)
         tl = self._one_args.__dict__
-        if "kid" not in tl:
-            tl["kid"], tl["off"], tl["bits"] = ctypes.c_uint32(), (ctypes.c_uint64 * 2)(), ctypes.c_uint8()
-            tl["kid_p"], tl["bits_p"] = ctypes.byref(tl["kid"]), ctypes.byref(tl["bits"])
-        tl["kid"].value = int(key_id)
-        off = tl["off"]
-        off[1] = len(msg)
-        tl["bits"].value = 0
-        check(self._lib.edv_verify_batch_keyed(self._ctx, bytes(sig64), tl["kid_p"], bytes(msg) if msg else None,
-                                               off, 1, tl["bits_p"]))
-        return bool(tl["bits"].value & 1)
+        if "ok" not in tl:
+            tl["ok"] = ctypes.c_uint8()
+            tl["ok_p"] = ctypes.byref(tl["ok"])
+        tl["ok"].value = 0
+        check(self._lib.edv_verify_one(self._ctx, bytes(sig64), int(key_id), bytes(msg) if msg else None, len(msg),
+                                       tl["ok_p"]))
+        return bool(tl["ok"].value & 1)
 
     def verify_batch_keyed_device(self, d_sig64, d_key_idx, d_msgs, d_msg_off, n, d_accept_words, stream=None):
         st = _stream_for(stream, d_sig64, d_accept_words)

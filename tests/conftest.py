@@ -73,6 +73,17 @@ def gpu_engine():
     eng.close()
 
 
+@pytest.fixture(autouse=True)
+def _gpu_engine_options_restored(request):
+    """Every test that uses the session's GPU engine leaves it with the default options
+    (edv_options), however it ends: the next test starts from a fresh context's modes."""
+    yield
+    if "gpu_engine" in request.fixturenames:
+        eng = request.getfixturevalue("gpu_engine")
+        from plenum_amd import EdVerifyEngine
+        eng.set_options(**EdVerifyEngine.default_options())
+
+
 def sodium():
     """libsodium 1.0.18 via ctypes if present (this container and the GPU
     box image have it); None otherwise."""

@@ -34,3 +34,41 @@ def test_library_is_gfx950_code_object():
     data = open(os.path.join(PKG, "libplenum_edverify.so"), "rb").read()
     assert b"gfx950" in data
     assert b"edv_dsm_kernel" in data
+
+
+def exported_symbols():
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only", os.path.join(PKG, "libplenum_edverify.so")],
+                         capture_output=True, text=True, check=True).stdout
+    return sorted({line.split()[-1] for line in out.splitlines() if line.split()[-1].startswith("edv_")})
+
+
+def test_library_exports_nothing_undeclared():
+    """The boundary is exactly the header: an edv_* symbol the library exports but
+    include/edverify.h does not declare fails (probe builds' edv_small_profile is
+    compiled only under EDV_SMALL_PROFILE)."""
+    extra = sorted(set(exported_symbols()) - set(declared_symbols()))
+    assert not extra, extra
+
+
+def test_default_options_struct():
+    """edv_options as ctypes sees it: the defaults a fresh context has (no GPU needed)."""
+    from plenum_amd.engine import EdVerifyEngine
+    d = EdVerifyEngine.default_options()
+    assert d == {"pipeline": 1, "length_buckets": 2, "key_sort": 2, "resident": 1, "small_batch": 256,
+                 "unit_arena_bytes": (1 << 20) * 1280, "bls_pair_lanes": 32768, "bls_wave_checks": 8192}
+
+
+def test_drop_in_never_changes_context_options():
+    """The authenticator's modules never call an options setter: a context is left in the
+    mode its owner chose whatever the drop-in does (or raises).  Only the key window
+    (KeyStore, with the key store it sizes) is set by the product."""
+    import glob
+    import re
+    pat = re.compile(r"\.(set_options|options|set_pipeline|set_small_batch|set_key_sort|set_length_buckets|"
+                     r"set_unit_arena|bls_set_pair_lanes|bls_set_wave_checks)\(")
+    for f in glob.glob(os.path.join(PKG, "plenum_amd", "*.py")):
+        if f.endswith("engine.py"):
+            continue
+        src = open(f).read()
+        assert not pat.search(src), (f, pat.search(src).group(0))

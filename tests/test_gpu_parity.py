@@ -103,11 +103,9 @@ def test_general_distinct_keys(gpu_engine, oracle):
     sig = gpu_engine.sign_batch(sk, np.arange(n, dtype=np.uint32), buf, off)
     bad = rng.choice(n, 250, replace=False)
     sig[bad, 5] ^= 0x20
-    try:
-        gpu_engine.set_pipeline(4)
+    with gpu_engine.options(pipeline=4):  # (the previous options come back however the block ends)
         got = gpu_engine.verify_batch(sig, pk, buf, off)
-    finally:
-        gpu_engine.set_pipeline(1)
+    assert gpu_engine.get_options()["pipeline"] == 1
     want = np.ones(n, bool)
     want[bad] = False
     assert (got == want).all(), np.nonzero(got != want)
@@ -650,3 +648,86 @@ def test_verify_one_keyed_matches_batch(gpu_engine):
     finally:
         gpu_engine.keys_reset()
         gpu_engine.keys_set_window(10)
+
+
+def test_resident_single_request_path(gpu_engine, oracle):
+    """edv_verify_one's resident kernel (one workgroup taking requests from a pinned mailbox):
+    the same verdicts as the oracle through everything that makes it leave and come back --
+    back-to-back requests, a batch call between two (the yield), an idle gap longer than its
+    200 us timeout, a message over its 4 KiB mailbox (the launch path), a key window change
+    (a kernel of the new window), and a key slot rebuilt for another key between two requests
+    (the verdict follows the new key: no stale table lines read from the kernel's caches)."""
+    import time
+    rng = np.random.default_rng(41)
+    pk, sk = gpu_engine.seed_keypair_batch(rng.integers(0, 256, (6, 32), dtype=np.uint8))
+    lens = [0, 1, 63, 64, 200, 255, 1000, 4095, 4096, 4097, 6000] + [int(x) for x in rng.integers(0, 400, 60)]
+    msgs = [bytes(rng.integers(0, 256, m, dtype=np.uint8)) for m in lens]
+    kidx = (np.arange(len(msgs)) % 4).astype(np.uint32)
+    buf, off = pack_messages(msgs)
+    sig = gpu_engine.sign_batch(sk, kidx, buf, off)
+    sig[3::7, 5] ^= 4  # forged R
+    sig[4::9, 40] ^= 1  # forged S
+
+    def want(i, key):
+        return oracle.oracle_verify_detached(sig[i].tobytes(), msgs[i], len(msgs[i]), pk[key].tobytes()) == 0
+    try:
+        for w in (10, 14):
+            gpu_engine.keys_reset()
+            gpu_engine.keys_set_window(w)
+            assert gpu_engine.keys_add(pk[:4]) == 0
+            for i in range(len(msgs)):
+                assert gpu_engine.verify_one_keyed(bytes(sig[i]), int(kidx[i]), msgs[i]) == want(i, kidx[i]), (w, i)
+                if i % 10 == 3:  # a batch call between two single requests
+                    got = gpu_engine.verify_batch_keyed(sig[:8], kidx[:8], buf, off[:9])
+                    assert list(got) == [want(j, kidx[j]) for j in range(8)]
+                if i % 10 == 6:
+                    time.sleep(0.002)  # longer than the idle timeout: the kernel has left
+            # an unregistered id rejects
+            assert not gpu_engine.verify_one_keyed(bytes(sig[0]), 4 + 9, msgs[0])
+        # slot 0 rebuilt for key 4 (an eviction): requests of key 0 now reject, key 4's accept
+        i0 = int(np.flatnonzero((kidx == 0) & (np.array(lens) < 300))[0])
+        assert gpu_engine.verify_one_keyed(bytes(sig[i0]), 0, msgs[i0]) == want(i0, 0)
+        gpu_engine.keys_set(0, pk[4:5])
+        assert gpu_engine.verify_one_keyed(bytes(sig[i0]), 0, msgs[i0]) == want(i0, 4)
+        m4 = b"key four"
+        b4, o4 = pack_messages([m4])
+        s4 = gpu_engine.sign_batch(sk[4:5], np.zeros(1, np.uint32), b4, o4)
+        assert gpu_engine.verify_one_keyed(bytes(s4[0]), 0, m4)
+    finally:
+        gpu_engine.keys_reset()
+        gpu_engine.keys_set_window(10)
+
+
+def test_resident_single_request_is_faster_than_a_launch(gpu_engine):
+    """The reason for the resident kernel: one request's engine call (p50 of 300 back to back)
+    is shorter than with a kernel launch per request (a context created with EDV_RESIDENT=0)."""
+    import os
+    import time
+    from plenum_amd import EdVerifyEngine
+    rng = np.random.default_rng(43)
+    pk, sk = gpu_engine.seed_keypair_batch(rng.integers(0, 256, (2, 32), dtype=np.uint8))
+    msg = bytes(rng.integers(0, 256, 200, dtype=np.uint8))
+    b, o = pack_messages([msg])
+    sig = bytes(gpu_engine.sign_batch(sk, np.zeros(1, np.uint32), b, o)[0])
+    os.environ["EDV_RESIDENT"] = "0"
+    try:
+        launch_eng = EdVerifyEngine(0)
+    finally:
+        del os.environ["EDV_RESIDENT"]
+    try:
+        p50 = {}
+        for name, eng in (("resident", gpu_engine), ("launch", launch_eng)):
+            eng.keys_reset()
+            eng.keys_set_window(10)
+            eng.keys_add(pk)
+            lat = []
+            for _ in range(330):
+                t = time.perf_counter()
+                assert eng.verify_one_keyed(sig, 0, msg)
+                lat.append(time.perf_counter() - t)
+            p50[name] = float(np.median(lat[30:])) * 1e6
+        print("engine call p50 us:", p50)
+        assert p50["resident"] < p50["launch"], p50
+    finally:
+        launch_eng.close()
+        gpu_engine.keys_reset()
