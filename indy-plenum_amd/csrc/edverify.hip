@@ -1437,12 +1437,13 @@ struct ResBox {
   uint8_t msg[kResMsgMax];
 };
 static_assert(offsetof(ResBox, sig) % 64 == 0, "sig 64-byte aligned");
-struct ResShared {
-  uint64_t seq, mlen, key_cap;
-  const uint32_t* key_tab;
-  const uint8_t* key_pk;
-  const uint8_t* key_valid;
-  uint32_t cmd, key_id, key_count, pad;
+static_assert(offsetof(ResBox, key_id) == offsetof(ResBox, mlen) + 8 && offsetof(ResBox, key_tab) == offsetof(ResBox, mlen) + 16 &&
+                  offsetof(ResBox, key_cap) == offsetof(ResBox, mlen) + 40,
+              "the kernel loads mlen .. key_cap as six consecutive words");
+struct alignas(16) ResShared {
+  uint64_t seq;
+  uint64_t field[6];  // ResBox's mlen .. key_cap, as loaded
+  uint32_t cmd, pad;
   uint32_t sig[16];
   uint64_t msg[kResMsgMax / 8 + 2];
 };
@@ -1476,30 +1477,29 @@ __global__ __launch_bounds__(kSmallThreads) void edv_resident_kernel(ResBox* box
         __builtin_amdgcn_s_sleep(1);
       }
       rs.cmd = cmd;
-      if (cmd) {
-        rs.seq = seq;
-        rs.mlen = sys_load64_relaxed(&box->mlen);
-        const uint64_t ids = sys_load64_relaxed((const uint64_t*)&box->key_id);
-        rs.key_id = (uint32_t)ids;
-        rs.key_count = (uint32_t)(ids >> 32);
-        rs.key_tab = (const uint32_t*)sys_load64_relaxed((const uint64_t*)&box->key_tab);
-        rs.key_pk = (const uint8_t*)sys_load64_relaxed((const uint64_t*)&box->key_pk);
-        rs.key_valid = (const uint8_t*)sys_load64_relaxed((const uint64_t*)&box->key_valid);
-        rs.key_cap = sys_load64_relaxed(&box->key_cap);
-      }
+      rs.seq = seq;
     }
     __syncthreads();
     if (!rs.cmd) break;  // workgroup-uniform
-    // the request into LDS: 8-byte system-scope loads, all in flight at once (the message is read
-    // over PCIe once; the hash's 16-byte chunk loads then read LDS)
-    const uint64_t mlen = rs.mlen < kResMsgMax ? rs.mlen : kResMsgMax;  // (the host never sends more)
-    const uint64_t nw = (mlen + 7) / 8;
-    for (uint64_t w = t; w < nw; w += kSmallThreads) rs.msg[w] = sys_load64_relaxed((const uint64_t*)box->msg + w);
-    if (t < 8) {
-      const uint64_t v = sys_load64_relaxed((const uint64_t*)box->sig + t);
-      rs.sig[2 * t] = (uint32_t)v;
-      rs.sig[2 * t + 1] = (uint32_t)(v >> 32);
+    // the request into LDS in one PCIe round trip: its fields (threads 0-5), signature (8-15) and the
+    // first kResHead message words (16 ..) are loaded side by side, each an 8-byte system-scope load
+    // (serially, thread 0's six field loads alone took ~10 us); a longer message's rest follows
+    constexpr uint32_t kResHead = kSmallThreads - 16;
+    if (t < 6) {
+      const uint64_t* f = (const uint64_t*)&box->mlen;  // mlen, key_id | key_count, key_tab, key_pk, key_valid, key_cap
+      rs.field[t] = sys_load64_relaxed(f + t);
+    } else if (t >= 8 && t < 16) {
+      const uint64_t v = sys_load64_relaxed((const uint64_t*)box->sig + (t - 8));
+      rs.sig[2 * (t - 8)] = (uint32_t)v;
+      rs.sig[2 * (t - 8) + 1] = (uint32_t)(v >> 32);
+    } else if (t >= 16) {
+      rs.msg[t - 16] = sys_load64_relaxed((const uint64_t*)box->msg + (t - 16));
     }
+    __syncthreads();
+    const uint64_t mlen = rs.field[0] < kResMsgMax ? rs.field[0] : kResMsgMax;  // (the host never sends more)
+    const uint64_t nw = (mlen + 7) / 8;
+    for (uint64_t w = kResHead + t; w < nw; w += kSmallThreads)
+      rs.msg[w] = sys_load64_relaxed((const uint64_t*)box->msg + w);
     if (t < 2) rs.msg[nw + t] = 0;  // (the hash's last chunk load reads past the message)
     // key tables rebuilt since the last request (an eviction's build, finished before the host sent
     // this request) must not be read from this CU's or this XCD's stale cache lines
@@ -1508,8 +1508,9 @@ __global__ __launch_bounds__(kSmallThreads) void edv_resident_kernel(ResBox* box
     uint32_t sig[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) sig[k] = rs.sig[k];
-    const bool ok = small_verify<W>(sh, sig, rs.key_id, rs.key_count, rs.key_pk, rs.key_valid,
-                                    (const uint8_t*)rs.msg, mlen, rs.key_tab, rs.key_cap, btab, ident);
+    const bool ok = small_verify<W>(sh, sig, (uint32_t)rs.field[1], (uint32_t)(rs.field[1] >> 32),
+                                    (const uint8_t*)rs.field[3], (const uint8_t*)rs.field[4], (const uint8_t*)rs.msg,
+                                    mlen, (const uint32_t*)rs.field[2], rs.field[5], btab, ident);
     if (t == 0) {
       __hip_atomic_store(&box->verdict, ok ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(&box->done_seq, rs.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);

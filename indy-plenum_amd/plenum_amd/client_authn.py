@@ -76,6 +76,10 @@ try:  # the batch's per-identifier keys for the known getVerkey (SimpleAuthNr's 
     from ._hostpack import keys_known as _keys_known
 except ImportError:  # pragma: no cover
     _keys_known = None
+try:  # ... on the scan's worker pool, with the keys as one buffer (key store lookup, general-path keys)
+    from ._hostpack import keys_known_flat as _keys_known_flat
+except ImportError:  # pragma: no cover
+    _keys_known_flat = None
 try:  # the node's per-message path: authenticate()'s host steps in one call; the verify-ahead's dedupe
     from ._hostpack import authn_key as _authn_key, distinct_sm as _distinct_sm
 except ImportError:  # pragma: no cover
@@ -127,6 +131,14 @@ def _known_getverkey(cls):
 ROLE = 'role'
 
 KEY_STORE_BYTES = 32 << 30  # HBM for key tables: the window is the widest that fits max_keys
+# Promotion priced by expected use: a key earns a table when its decayed count of verified requests
+# reaches HOT_KEY_USES.  A table build costs ~BUILD_US of GPU time at the drop-in's window (W = 10)
+# and a keyed verify saves ~SAVE_NS against the general path for a key of its own, so a build
+# repays after BUILD_US / SAVE_NS requests; with counts halving per 2^18 requests verified, a key
+# needs about that many per epoch to get there ("Key churn").  Keys with fewer
+# than 1/16 of it in a batch are not counted (they cannot reach it before the decay).
+HOT_KEY_USES = 64
+HOT_COUNT_FLOOR = 16
 _SIG_SLOT = 96  # edverify.h EDV_SIG_SLOT96: signatures as base58 text, decoded on the GPU
 _PINNED_MIN_BATCH = 4096  # smaller batches keep the bytearrays (the library stages them cheaply)
 _STREAM_CHUNK = 1 << 17  # requests per streamed submit: 2^17 beat 2^18 and 2^16 by 2-3 % (profiles/r06c)
@@ -196,7 +208,7 @@ class _GpuState:
 
     def __init__(self, engine=None, device=0, devices=None, verdict_cache_size=1 << 20,
                  verdict_cache_bytes=256 << 20, verdict_max_age=300.0, key_window="auto",
-                 max_keys=16384, hot_key_uses=2, key_store_bytes=KEY_STORE_BYTES, scan_threads=0,
+                 max_keys=16384, hot_key_uses=HOT_KEY_USES, key_store_bytes=KEY_STORE_BYTES, scan_threads=0,
                  pipeline_part=0, async_key_builds=True, stream=True, stage=True, speculate=True,
                  max_promotions=1024):
         self.engine = engine
@@ -608,7 +620,7 @@ class GpuAuthMixin:
             if len(p.sig) == 64 and not g.hot and not g.pending and hasattr(eng, "verify_one_keyed"):
                 # the steady state's miss: a registered, built key -- straight to the one-request launch
                 ks = self._key_store()
-                kid = ks.lookup([p.key])[0] if ks is not None else None
+                kid = ks.lookup_one(p.key) if ks is not None else None
                 if kid is not None:
                     ok = bool(eng.verify_one_keyed(p.sig, kid, p.ser))
                     g.stats["batches"] += 1
@@ -695,6 +707,32 @@ class GpuAuthMixin:
                     out[j] = k
             return out
         return self._keys_for_py(uniq)
+
+    def _keys_for_flat(self, uniq):
+        """_keys_for(uniq) plus the keys as one buffer of 32 bytes each (zeros
+        where a key is not 32 bytes), the positions of those (`odd`), and
+        whether every identifier resolved to a key (bytes, non-empty): the
+        per-identifier resolution on the scan's worker pool (keys_known_flat),
+        the holes (state lookups, exceptions, changed verkeys) in Python."""
+        fk = self._g.fast_keys
+        if (_keys_known_flat is not None and type(getattr(self, "clients", None)) is dict and type(fk) is dict
+                and uniq.__class__ is list and _known_getverkey(type(self))):
+            out, holes, flat = _keys_known_flat(self.clients, fk, uniq, VERKEY)
+            odd = []
+            if holes:
+                flat = bytearray(flat)
+                for j, k in zip(holes, self._keys_for_py([uniq[j] for j in holes])):
+                    out[j] = k
+                    if k.__class__ is bytes and len(k) == 32:
+                        flat[32 * j:32 * j + 32] = k
+                    else:
+                        odd.append(j)
+            all_keys = not odd or all(out[j].__class__ is bytes and out[j] for j in odd)
+            return out, bytes(flat), odd, all_keys
+        out = self._keys_for(uniq)
+        odd = [j for j, k in enumerate(out) if k.__class__ is not bytes or len(k) != 32]
+        flat = b"".join(k if k.__class__ is bytes and len(k) == 32 else bytes(32) for k in out)
+        return out, flat, odd, all(out[j].__class__ is bytes and out[j] for j in odd)
 
     def _keys_for_py(self, uniq):
         """_keys_for in Python: any getVerkey, in the identifiers' order."""
@@ -860,13 +898,14 @@ class GpuAuthMixin:
                 return None
             # (the chunks' reservations are contiguous from 0: their total is the largest span end)
             g.msg_bytes_per_item = max(g.msg_bytes_per_item * 0.5, float(staged_bytes) / n if n else 0.0)
-            ukeys = self._keys_for(uniq)  # authenticate():93-99, once per identifier
+            # authenticate():93-99, once per identifier (on the worker pool; the keys also as one buffer)
+            ukeys, uflat, uodd, all_keys = self._keys_for_flat(uniq)
             ids = None
             general_u = None  # distinct identifiers whose key has no built table: the general path
-            if ks is not None and fast_b.count(0) == 0 and all(k.__class__ is bytes and k for k in ukeys):
+            if ks is not None and fast_b.count(0) == 0 and all_keys:
                 if g.hot or g.pending:
                     self._register_waiting(ks, ukeys)
-                ids = ks.lookup_array(ukeys)
+                ids = ks.lookup_array(ukeys, uflat, uodd)
                 if (ids < 0).any():
                     general_u = np.flatnonzero(ids < 0)
                     ids[general_u] = 0xffffffff  # (an id the kernels reject)
@@ -879,7 +918,7 @@ class GpuAuthMixin:
             if general_u is not None:  # a mixed batch (key churn): the keyed verify, then the rest
                 drop_parts()
                 return self._staged_mixed(msgs, eng, slot, slot_base, ks, ukeys, ids, general_u, scan, spans_buf,
-                                          kid_buf, t0, t1)
+                                          kid_buf, t0, t1, None if uodd else uflat)
             ids_b = np.asarray(ids, np.uint32).tobytes()
             spec_hit = parts is not None and parts_ok and spec_u == ids_b and ks.version == ks_version
             if g.speculate and _kid_map is not None and (spec_u != ids_b or g.kid_map is None or
@@ -938,7 +977,8 @@ class GpuAuthMixin:
         del kid, spans, ms, me, spans_b
         return verdicts(ok, perf_counter())
 
-    def _staged_mixed(self, msgs, eng, slot, slot_base, ks, ukeys, ids, general_u, scan, spans_buf, kid_buf, t0, t1):
+    def _staged_mixed(self, msgs, eng, slot, slot_base, ks, ukeys, ids, general_u, scan, spans_buf, kid_buf, t0, t1,
+                      uflat=None):
         """A staged batch whose identifiers' keys are partly without a built
         table (a signer population larger than the key store): one keyed
         verify of the whole staged batch over the store's ids (the others get
@@ -964,8 +1004,11 @@ class GpuAuthMixin:
         is_gen[general_u] = True
         gen = np.flatnonzero(is_gen[uidx])
         if len(gen):
-            ukey_arr = np.zeros((len(ukeys), 32), np.uint8)
-            ukey_arr[general_u] = np.frombuffer(b"".join(ukeys[u] for u in general_u), np.uint8).reshape(-1, 32)
+            if uflat is not None and len(uflat) == 32 * len(ukeys):
+                ukey_arr = np.frombuffer(uflat, np.uint8).reshape(-1, 32)  # (the general identifiers' keys are 32 B)
+            else:
+                ukey_arr = np.zeros((len(ukeys), 32), np.uint8)
+                ukey_arr[general_u] = np.frombuffer(b"".join(ukeys[u] for u in general_u), np.uint8).reshape(-1, 32)
             if getattr(eng, "supports_staged_subset", False):
                 # the staged batch is still in HBM: only the items' indices and key bytes go over
                 okg = np.asarray(eng.verify_staged_subset(gen.astype(np.uint32), ukey_arr[uidx[gen]]), bool)
@@ -980,7 +1023,9 @@ class GpuAuthMixin:
             # general-path keys earn a slot by verified requests (short items never verify)
             good = gen[okg & (np.frombuffer(short, np.uint8)[gen] == 0)]
             per_u = np.bincount(uidx[good], minlength=len(ukeys))
-            hot_u = np.flatnonzero(per_u).tolist()
+            # (keys with fewer verified requests in this batch than 1/HOT_COUNT_FLOOR of the threshold
+            # cannot reach it through the decay: not counted -- the long tail of a churning batch)
+            hot_u = np.flatnonzero(per_u >= max(1, g.hot_key_uses // HOT_COUNT_FLOOR)).tolist()
             self._count_verified_keys([ukeys[u] for u in hot_u], per_u[hot_u])
         t3 = perf_counter()
         g.stats["batches"] += 1

@@ -30,6 +30,12 @@ from collections import OrderedDict
 
 import numpy as np
 
+try:  # the native mirror of the key -> id map (csrc/hostpack.cpp KeyIndex)
+    from ._hostpack import key_index as _key_index, key_index_set as _ki_set, key_index_del as _ki_del, \
+        key_index_clear as _ki_clear, key_index_get as _ki_get
+except ImportError:  # pragma: no cover
+    _key_index = None
+
 # comb windows the library builds (edverify.h edv_keys_set_window)
 WINDOWS = (4, 6, 8, 10, 12, 13, 14, 16)
 
@@ -58,6 +64,8 @@ class KeyStore:
         self.window = window
         self.capacity = capacity
         self._ids = {}                # key bytes -> id
+        # the same map for 32-byte keys, natively (lookup_array over a batch's flat key buffer)
+        self._index = _key_index() if _key_index is not None else None
         self._slot_key = []           # id -> key bytes (None: a retired slot)
         self._used = np.zeros(max(int(capacity), 1), np.int64)  # id -> tick of its last use
         self._tick = 1
@@ -90,12 +98,25 @@ class KeyStore:
         if hasattr(self.engine, "keys_set_window"):
             self.engine.keys_set_window(self.window)
         self._ids.clear()
+        if self._index is not None:
+            _ki_clear(self._index)
         self._slot_key = []
         self._used[:] = 0
         self._building.clear()
         self._tickets.clear()
         self._generation = getattr(self.engine, "keys_generation", 0)
         self.version += 1
+
+    def _id_set(self, key, i):
+        self._ids[key] = i
+        if self._index is not None and len(key) == 32:
+            _ki_set(self._index, key, int(i).to_bytes(8, "little", signed=True))
+
+    def _id_pop(self, key):
+        i = self._ids.pop(key)
+        if self._index is not None and len(key) == 32:
+            _ki_del(self._index, key)
+        return i
 
     def _refresh(self):
         """Drop the ids whose builds have completed from the building set
@@ -152,14 +173,36 @@ class KeyStore:
             out = [None if i is not None and i in building else i for i in out]
         return out
 
-    def lookup_array(self, keys):
-        """lookup() as an int64 array, -1 where lookup() answers None (one
-        pass over the keys; the hits' ticks and the building filter vectorized)."""
+    def lookup_one(self, key):
+        """lookup([key])[0] without the list and array operations: the id of
+        one key (None if unregistered or still building), marked recently used
+        (the per-message authenticate() path)."""
         self._sync()
         if self._building:
             self._refresh()
-        get = self._ids.get
-        ids = np.fromiter((get(k, -1) for k in keys), np.int64, len(keys))
+        i = self._ids.get(key)
+        if i is None:
+            return None
+        self._used[i] = self._tick
+        self._tick += 1
+        return None if i in self._building else i
+
+    def lookup_array(self, keys, flat=None, odd=()):
+        """lookup() as an int64 array, -1 where lookup() answers None (one
+        pass over the keys; the hits' ticks and the building filter vectorized).
+        flat: the same keys as one buffer of 32 bytes each (keys_known_flat),
+        looked up in the native index in one call; odd: the positions of keys
+        that are not 32 bytes (zeros in flat), looked up in the dict.""" 
+        self._sync()
+        if self._building:
+            self._refresh()
+        if flat is not None and self._index is not None and len(flat) == 32 * len(keys):
+            ids = np.frombuffer(_ki_get(self._index, flat), np.int64).copy()
+            for j in odd:  # (keys that are not 32 bytes: zeros in flat)
+                ids[j] = self._ids.get(keys[j], -1) if keys[j].__class__ is bytes else -1
+        else:
+            get = self._ids.get
+            ids = np.fromiter((get(k, -1) for k in keys), np.int64, len(keys))
         hit = ids[ids >= 0]
         if len(hit):
             self._used[hit] = self._tick
@@ -216,7 +259,7 @@ class KeyStore:
                 self._fail(new)
                 new = []
             for j, k in enumerate(new):
-                self._ids[k] = first + j
+                self._id_set(k, first + j)
                 self._slot_key.append(k)
             if new:
                 self._touch(range(first, first + len(new)))
@@ -228,7 +271,7 @@ class KeyStore:
             if use_async and hasattr(self.engine, "keys_set_many_async") and victims:
                 # every eviction of this call in one upload and one build launch
                 pairs = list(zip(over, victims))
-                slots = [self._ids.pop(k_old) for _, k_old in pairs]
+                slots = [self._id_pop(k_old) for _, k_old in pairs]
                 self.version += 1
                 pk = np.frombuffer(b"".join(k for k, _ in pairs), np.uint8).reshape(-1, 32)
                 try:
@@ -241,12 +284,12 @@ class KeyStore:
                 self._mark_building(slots, ticket)
                 for (k_new, _), sl in zip(pairs, slots):
                     self._slot_key[sl] = k_new
-                    self._ids[k_new] = sl
+                    self._id_set(k_new, sl)
                     done.append(k_new)
                 self._touch(slots)
                 return done
             for k_new, k_old in zip(over, victims):
-                slot = self._ids.pop(k_old)
+                slot = self._id_pop(k_old)
                 self.version += 1
                 try:
                     pk = np.frombuffer(k_new, np.uint8).reshape(1, 32)
@@ -260,7 +303,7 @@ class KeyStore:
                     self._fail([k_new])
                     continue
                 self._slot_key[slot] = k_new
-                self._ids[k_new] = slot
+                self._id_set(k_new, slot)
                 self._touch([slot])
                 done.append(k_new)
         return done

@@ -237,7 +237,7 @@ def _signed(n_signers, n_msgs, seed=1):
 
 def test_hot_keys_get_registered_after_verifying(oracle_engine):
     idrs, vks, msgs = _signed(1, 8)
-    a = GpuAuthNr(engine=oracle_engine, nym_lookup=lambda st, idr: {"verkey": vks[0]})
+    a = GpuAuthNr(engine=oracle_engine, nym_lookup=lambda st, idr: {"verkey": vks[0]}, hot_key_uses=2)
     assert a.authenticate_batch(msgs[:4]) == [idrs[0]] * 4      # general path, 4 verified uses
     assert len(a._g.hot) == 1 and a.stats["keyed_items"] == 0   # earned a slot
     assert a.authenticate_batch(msgs[4:]) == [idrs[0]] * 4      # registered, now keyed
@@ -246,7 +246,7 @@ def test_hot_keys_get_registered_after_verifying(oracle_engine):
 
 def test_bad_signatures_do_not_promote_keys(oracle_engine):
     idrs, vks, msgs = _signed(1, 6)
-    a = GpuAuthNr(engine=oracle_engine, nym_lookup=lambda st, idr: {"verkey": vks[0]})
+    a = GpuAuthNr(engine=oracle_engine, nym_lookup=lambda st, idr: {"verkey": vks[0]}, hot_key_uses=2)
     forged = [dict(m, reqId=m["reqId"] + 1) for m in msgs]
     for _ in range(3):
         assert all(isinstance(r, X.InvalidSignature) for r in a.authenticate_batch(forged))
@@ -972,7 +972,7 @@ def test_speculative_batch_raising_after_the_scan_frees_the_set(oracle, monkeypa
     a.authenticate_batch(steady)  # the kid map
     real = KS.KeyStore.lookup_array
 
-    def boom(self, keys):
+    def boom(self, keys, *rest):
         raise MemoryError("injected")
     monkeypatch.setattr(KS.KeyStore, "lookup_array", boom)
     with pytest.raises(MemoryError):
@@ -1134,7 +1134,7 @@ def test_staged_mixed_batch_keyed_and_general(oracle, monkeypatch, subset):
     table = dict(zip(idrs, vks))
     eng = StagingOracleEngine(oracle)
     eng.supports_staged_subset = subset
-    a = GpuAuthNr(engine=eng, nym_lookup=lambda st, idr: {"verkey": table[idr]}, max_keys=2, hot_key_uses=10 ** 9)
+    a = GpuAuthNr(engine=eng, nym_lookup=lambda st, idr: {"verkey": table[idr]}, max_keys=2, hot_key_uses=10 ** 4)
     for i, v in zip(idrs[:2], vks[:2]):
         a.addIdr(i, v)
     a.keys_settle()

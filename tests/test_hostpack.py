@@ -429,3 +429,90 @@ def test_keys_known_many_identifiers(seed):
     assert got[1] == want[1]
     assert all(a is b for a, b in zip(got[0], want[0]))
     assert 0 < len(got[1]) < len(q)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_keys_known_flat_matches_keys_known(seed):
+    """keys_known_flat (the same lookups on the scan's worker pool, CPython 3.10's dict probe
+    restated) answers what keys_known does on every identifier of the adversarial pool above --
+    deleted entries, non-str and str-subclass identifiers, non-ASCII text, odd nym values,
+    changed verkey objects, malformed fast-key entries, duplicates -- except that keys which are
+    not 32 bytes are holes too (the Python path); flat holds each key's bytes, zeros at holes;
+    the key objects' reference counts are the serial path's."""
+    import sys
+    rng = random.Random(seed)
+
+    class S(str):
+        pass
+    clients, fk, idrs = {}, {}, []
+    for i in range(6000):
+        idr = "%022x" % rng.getrandbits(88) if i % 97 else "idé%d" % i
+        vk = "~vk%d" % i
+        kind = rng.randrange(13)
+        clients[idr] = ({"verkey": vk, "role": None} if kind < 7 else {} if kind == 7 else
+                        [vk] if kind == 9 else {"role": None})
+        fk[idr] = ((vk, os.urandom(32)) if kind not in (10, 12) else (vk, os.urandom(31)) if kind == 12 else
+                   (vk, "not bytes") if i % 2 else (vk,))
+        if kind == 11:
+            clients[idr] = {"verkey": "~vk%d" % i}
+        idrs.append(idr)
+    for idr in rng.sample(idrs, 600):
+        del clients[idr]
+        if rng.random() < 0.5:
+            del fk[idr]
+    q = [(i + ".")[:-1] for i in rng.sample(idrs, 5000)]  # fresh str objects: hashes not cached yet
+    q += [q[5], 12345, None, S(idrs[0]), "unknown", b"bytes"] + [(i + ".")[:-1] for i in rng.sample(idrs, 400)]
+    rng.shuffle(q)
+    want_keys, _ = H.keys_known(clients, fk, q, "verkey")
+    want_holes = [j for j, k in enumerate(want_keys) if not (type(k) is bytes and len(k) == 32)]
+    distinct = list({id(k): k for k in want_keys if k is not None}.values())
+
+    def refs():
+        out = []
+        for k in distinct:
+            out.append(sys.getrefcount(k))
+        return out
+    before = refs()
+    keys, holes, flat = H.keys_known_flat(clients, fk, q, "verkey")
+    assert holes == want_holes
+    assert all((k is w) if j not in set(holes) else k is None for j, (k, w) in enumerate(zip(keys, want_keys)))
+    assert len(flat) == 32 * len(q)
+    for j in range(len(q)):
+        k = keys[j]
+        assert flat[32 * j:32 * j + 32] == (k if k is not None else bytes(32))
+    del k
+    after = refs()
+    assert sum(after) - sum(before) == sum(1 for k in keys if k is not None)  # one reference per entry of keys
+    del keys
+    assert refs() == before
+
+
+def test_key_index_matches_a_dict():
+    """The key store's native index (KeyIndex: 32-byte keys -> int64, tombstones, growth) answers
+    as a dict does over thousands of sets, overwrites, deletes and clears."""
+    rng = random.Random(5)
+    ki, ref = H.key_index(), {}
+    pool = [os.urandom(32) for _ in range(5000)]
+    for step in range(40000):
+        k = rng.choice(pool)
+        r = rng.random()
+        if r < 0.5:
+            v = rng.randrange(-5, 1 << 40)
+            H.key_index_set(ki, k, struct.pack("<q", v))
+            ref[k] = v
+        elif r < 0.8:
+            H.key_index_del(ki, k)
+            ref.pop(k, None)
+        elif r < 0.8005:
+            H.key_index_clear(ki)
+            ref.clear()
+        if step % 4000 == 0 or step == 39999:
+            got = struct.unpack("<%dq" % len(pool), H.key_index_get(ki, b"".join(pool)))
+            assert list(got) == [ref.get(k, -1) for k in pool]
+            assert H.key_index_len(ki) == len(ref)
+    # many keys at once
+    ks = [os.urandom(32) for _ in range(3000)]
+    H.key_index_set(ki, b"".join(ks), struct.pack("<3000q", *range(3000)))
+    assert list(struct.unpack("<3000q", H.key_index_get(ki, b"".join(ks)))) == list(range(3000))
+    with pytest.raises(ValueError):
+        H.key_index_get(ki, b"x" * 33)
