@@ -425,9 +425,11 @@ def time_whole_node(eng, args, sets, idrs, vks, dist_on, dev, scan_threads):
     signing serialization on the host's CPUs) with its PCIe copy and kernels
     under it, getVerkey per identifier, the GPU verdicts and the result list
     -- what replaces plenum/server/client_authn.py:67-107 per request.  A step
-    is one batch of n requests.  Pipelined (value): K batches through
-    authenticate_batches (two in flight); synchronous beside it: K batches
-    one authenticate_batch at a time.  The K batches alternate between the
+    is one batch of n requests.  Synchronous (the headline, value): K batches
+    one authenticate_batch at a time; pipelined beside it: K batches through
+    authenticate_batches (two in flight -- on a host-bound path the node
+    thread scans one batch while the GPU finishes the other, so it measures
+    level with synchronous).  The K batches alternate between the
     distinct request sets; the batch path keeps no verdicts (every step scans,
     serializes, copies and verifies all n).  Each timed region is bracketed by
     a barrier and torch.cuda.synchronize() and takes the max over ranks; every
@@ -1352,14 +1354,15 @@ def main():
         "other_path": other, "dropin_window": dropin}
     if rank == 0:
         if whole is not None:
-            head_value, head_ms, head_steps = whole["pipelined"]["value"], whole["pipelined"]["ms_per_batch"], args.steps
+            head_value = whole["synchronous"]["value"]
+            head_ms, head_steps = whole["synchronous"]["ms_per_batch"], args.steps
             workload = ("configs[1]: %d single-signature NYM requests per GPU per step, each a request dict json-decoded "
                         "on its own as the node receives it, %.0f B mean signed payload, %d signers (addIdr), all "
-                        "valid; step = one batch through GpuAuthNr.authenticate_batches (two batches in flight): "
-                        "native scan + serialization on the host CPUs, PCIe copy and kernels under it, getVerkey per "
-                        "identifier, result list -- the drop-in for client_authn.py:67-107; synchronous "
-                        "authenticate_batch beside it (whole_node)" % (whole["requests_per_batch"], mlen_mean,
-                                                                        args.signers))
+                        "valid; step = one GpuAuthNr.authenticate_batch of them, one batch at a time (synchronous): "
+                        "native scan + serialization on the host CPUs with the PCIe copy and kernels under it, "
+                        "getVerkey per identifier, result list -- the drop-in for client_authn.py:67-107, batch by "
+                        "batch; authenticate_batches (two batches in flight) beside it (whole_node.pipelined)" % (
+                            whole["requests_per_batch"], mlen_mean, args.signers))
         else:
             head_value, head_ms, head_steps = value, ms_per_step, args.device_steps
             workload = "configs[%d]: %d %s per GPU, %.0f B mean signed payload, %d signers%s%s; step = the verify " \

@@ -2320,10 +2320,14 @@ PyObject* py_results_from(PyObject*, PyObject* args) {
 // one pass -- results[i] = uniq[uidx[i]] when ok[i] and not short[i], else None, with the
 // indices of those failures (the caller puts InvalidSignature there).  ok / short: one byte
 // per request (0 / nonzero).
+// fails (optional): the objects to put at the failures instead of None, one per failure in index
+// order (the caller's InvalidSignature instances, made BEFORE this list exists: allocating them
+// after it would let the collector's young-generation passes walk the fresh list's items).
 PyObject* py_results_ok(PyObject*, PyObject* args) {
   Py_buffer bo, bs, bu;
   PyObject* uniq;
-  if (!PyArg_ParseTuple(args, "y*y*y*O", &bo, &bs, &bu, &uniq)) return nullptr;
+  PyObject* fails = nullptr;
+  if (!PyArg_ParseTuple(args, "y*y*y*O|O", &bo, &bs, &bu, &uniq, &fails)) return nullptr;
   struct Rel {
     Py_buffer *a, *b, *c;
     ~Rel() {
@@ -2396,6 +2400,14 @@ PyObject* py_results_ok(PyObject*, PyObject* args) {
   std::vector<Py_ssize_t> all;
   for (const std::vector<Py_ssize_t>& f : bad) all.insert(all.end(), f.begin(), f.end());
   std::sort(all.begin(), all.end());
+  if (fails && fails != Py_None && PyList_CheckExact(fails) && PyList_GET_SIZE(fails) == (Py_ssize_t)all.size()) {
+    for (size_t j = 0; j < all.size(); ++j) {  // (items[i] holds Py_None: its reference moves to the count below)
+      PyObject* o = PyList_GET_ITEM(fails, (Py_ssize_t)j);
+      Py_INCREF(o);
+      items[all[j]] = o;
+    }
+    Py_SET_REFCNT(Py_None, Py_REFCNT(Py_None) - (Py_ssize_t)all.size());
+  }
   PyObject* failed = PyList_New((Py_ssize_t)all.size());
   if (!failed) {
     Py_DECREF(res);

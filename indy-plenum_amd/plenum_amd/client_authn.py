@@ -122,6 +122,21 @@ REQ_ID = 'reqId'
 VERKEY = 'verkey'
 
 
+def _results_failing(ok, short, uidx_b, uniq):
+    """_results_ok with a fresh InvalidSignature at every failing item (verdict False or a short
+    signature), the exceptions made BEFORE the result list exists (hostpack.cpp results_ok: made
+    after it, their allocations let the collector's young-generation passes walk the fresh list)."""
+    import numpy as np
+    okb = np.frombuffer(ok, np.uint8) if not isinstance(ok, np.ndarray) else ok.view(np.uint8)
+    nf = int(np.count_nonzero((okb == 0) | (np.frombuffer(short, np.uint8) != 0)))
+    fails = [InvalidSignature() for _ in range(nf)]
+    results, failed = _results_ok(ok, short, uidx_b, uniq, fails)
+    if len(failed) != nf:  # (never expected: the native pass left None at its failures)
+        for i in failed:
+            results[i] = InvalidSignature()
+    return results, failed
+
+
 def _known_getverkey(cls):
     """cls.getVerkey is SimpleAuthNr's -- this module's restatement or the reference's own
     (client_authn.py:142-154): clients.get(identifier), the state only when that is empty."""
@@ -464,14 +479,15 @@ class GpuAuthMixin:
             return None
         return KeyStore.attach(self._engine(), g.key_window, g.max_keys)
 
-    def _register_waiting(self, ks, batch_keys):
+    def _register_waiting(self, ks, batch_keys, pinned_ids=None):
         """Keys that earned a slot (may evict least-recently-used keys not in
-        this batch) and addIdr keys (free slots only), registered before the
-        batch routes its items (asynchronous builds by default)."""
+        this batch: batch_keys, or their ids pinned_ids) and addIdr keys (free
+        slots only), registered before the batch routes its items (asynchronous
+        builds by default)."""
         g = self._g
         if g.hot:  # at most max_promotions per batch (each a table build on the device)
             got = ks.register(list(g.hot)[:g.max_promotions], pinned=batch_keys, evict=True,
-                              asynchronous=g.async_key_builds)
+                              asynchronous=g.async_key_builds, pinned_ids=pinned_ids)
             g.stats["keys_registered"] += len(got)
             g.hot.clear()
         if g.pending:
@@ -903,8 +919,8 @@ class GpuAuthMixin:
             ids = None
             general_u = None  # distinct identifiers whose key has no built table: the general path
             if ks is not None and fast_b.count(0) == 0 and all_keys:
-                if g.hot or g.pending:
-                    self._register_waiting(ks, ukeys)
+                if g.hot or g.pending:  # (the batch's keys pinned by id: one native lookup)
+                    self._register_waiting(ks, ukeys, ks.ids_of(uflat, uodd, ukeys) if g.hot else None)
                 ids = ks.lookup_array(ukeys, uflat, uodd)
                 if (ids < 0).any():
                     general_u = np.flatnonzero(ids < 0)
@@ -934,9 +950,7 @@ class GpuAuthMixin:
             g.stats["speculated"] = g.stats.get("speculated", 0) + (n if spec_hit else 0)
 
             def verdicts(ok, t3):
-                results, failed = _results_ok(ok, short, uidx_b, uniq)
-                for i in failed:
-                    results[i] = InvalidSignature()
+                results, failed = _results_failing(ok, short, uidx_b, uniq)
                 t4 = perf_counter()
                 g.last_breakdown = {"scan_and_copies": (t1 - t0) * 1e3, "keys_and_ids": (t2 - t1) * 1e3,
                                     "verify_wait": (t3 - t2) * 1e3, "verdicts": (t4 - t3) * 1e3,
@@ -1031,9 +1045,7 @@ class GpuAuthMixin:
         g.stats["batches"] += 1
         g.stats["batch_items"] += n
         g.stats["keyed_items"] += n - len(gen)
-        results, failed = _results_ok(ok, short, uidx_b, uniq)
-        for i in failed:
-            results[i] = InvalidSignature()
+        results, failed = _results_failing(ok, short, uidx_b, uniq)
         g.last_breakdown = {"scan_and_copies": (t1 - t0) * 1e3, "keys_and_ids": (t2 - t1) * 1e3,
                             "verify_wait": (t3 - t2) * 1e3, "verdicts": (perf_counter() - t3) * 1e3,
                             "speculated": False, "general_items": int(len(gen))}
@@ -1139,9 +1151,7 @@ class GpuAuthMixin:
         g.stats["batches"] += 1
         g.stats["batch_items"] += n
         g.stats["keyed_items"] += n
-        results, failed = _results_ok(ok, short, uidx_b, uniq)
-        for i in failed:
-            results[i] = InvalidSignature()
+        results, failed = _results_failing(ok, short, uidx_b, uniq)
         t5 = perf_counter()
         # where this batch's time went (bench.py end_to_end.in_batch_ms)
         g.last_breakdown = {"scan": (t1 - t0) * 1e3, "keys_and_ids": (t2 - t1) * 1e3,

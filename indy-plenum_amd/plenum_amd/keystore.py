@@ -67,6 +67,7 @@ class KeyStore:
         # the same map for 32-byte keys, natively (lookup_array over a batch's flat key buffer)
         self._index = _key_index() if _key_index is not None else None
         self._slot_key = []           # id -> key bytes (None: a retired slot)
+        self._retired = np.zeros(max(int(capacity), 1), bool)  # id -> retired (the eviction candidates' mask)
         self._used = np.zeros(max(int(capacity), 1), np.int64)  # id -> tick of its last use
         self._tick = 1
         self._failed = OrderedDict()  # keys that could not be registered
@@ -101,6 +102,7 @@ class KeyStore:
         if self._index is not None:
             _ki_clear(self._index)
         self._slot_key = []
+        self._retired[:] = False
         self._used[:] = 0
         self._building.clear()
         self._tickets.clear()
@@ -216,15 +218,31 @@ class KeyStore:
             self._used[np.asarray(ids, np.int64)] = self._tick
             self._tick += 1
 
-    def _victims(self, count, pinned):
-        """Up to count least-recently-used keys outside `pinned` (oldest tick first, then lowest slot)."""
+    def ids_of(self, flat, odd=(), keys=None):
+        """The ids of 32-byte keys given as one buffer (-1: not registered), from the native index,
+        without marking them used; odd: positions of keys not 32 bytes (looked up in `keys`)."""
+        self._sync()
+        if self._index is not None:
+            ids = np.frombuffer(_ki_get(self._index, flat), np.int64).copy()
+        else:
+            get = self._ids.get
+            ids = np.fromiter((get(bytes(flat[32 * j:32 * j + 32]), -1) for j in range(len(flat) // 32)), np.int64)
+        for j in odd:
+            ids[j] = self._ids.get(keys[j], -1) if keys is not None and keys[j].__class__ is bytes else -1
+        return ids
+
+    def _victims(self, count, pinned, pinned_ids=None):
+        """Up to count least-recently-used keys outside `pinned` (or the ids pinned_ids) (oldest
+        tick first, then lowest slot)."""
         n = len(self._slot_key)
         if count <= 0 or n == 0:
             return []
-        live = np.fromiter((k is not None for k in self._slot_key), bool, n)
-        get = self._ids.get
-        pid = np.fromiter((get(k, -1) for k in pinned), np.int64)
-        live[pid[pid >= 0]] = False
+        live = ~self._retired[:n]
+        if pinned_ids is None:
+            get = self._ids.get
+            pinned_ids = np.fromiter((get(k, -1) for k in pinned), np.int64)
+        pid = np.asarray(pinned_ids, np.int64)
+        live[pid[(pid >= 0) & (pid < n)]] = False
         cand = np.flatnonzero(live)
         if len(cand) > count:
             used = self._used[cand]
@@ -233,7 +251,7 @@ class KeyStore:
         cand = cand[np.lexsort((cand, self._used[cand]))]
         return [self._slot_key[i] for i in cand[:count]]
 
-    def register(self, keys, pinned=(), evict=True, asynchronous=False):
+    def register(self, keys, pinned=(), evict=True, asynchronous=False, pinned_ids=None):
         """Register keys not yet in the store: into free slots, then (evict)
         over least-recently-used keys outside `pinned`.  Returns the keys
         registered.  asynchronous: queue the table builds and return at once
@@ -267,7 +285,7 @@ class KeyStore:
                 self._mark_building(range(first, first + len(new)), ticket)
             done += new
         if over and evict and hasattr(self.engine, "keys_set"):
-            victims = self._victims(len(over), pinned)
+            victims = self._victims(len(over), pinned, pinned_ids)
             if use_async and hasattr(self.engine, "keys_set_many_async") and victims:
                 # every eviction of this call in one upload and one build launch
                 pairs = list(zip(over, victims))
@@ -279,6 +297,7 @@ class KeyStore:
                 except Exception:
                     for sl in slots:  # the slots' old tables may be half rewritten: retire them
                         self._slot_key[sl] = None
+                        self._retired[sl] = True
                     self._fail([k for k, _ in pairs])
                     return done
                 self._mark_building(slots, ticket)
@@ -300,6 +319,7 @@ class KeyStore:
                 except Exception:
                     # the slot's old table may be half rewritten: retire the slot
                     self._slot_key[slot] = None
+                    self._retired[slot] = True
                     self._fail([k_new])
                     continue
                 self._slot_key[slot] = k_new

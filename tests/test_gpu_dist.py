@@ -74,8 +74,8 @@ def test_bench_gpus_2_without_launcher():
     assert d["collective"]["all_gather_bitmask_ms"] > 0
     w = d["whole_node"]
     assert w["mismatches_all_ranks"] == 0 and p["whole_node_mismatches"] == 0
-    assert w["pipelined"]["value"] == d["value"] and w["pipelined"]["value_per_rank"] * 2 == d["value"]
-    assert w["synchronous"]["value"] > 0 and w["scan_threads"] != "auto"
+    assert w["synchronous"]["value"] == d["value"] and w["synchronous"]["value_per_rank"] * 2 == d["value"]
+    assert w["pipelined"]["value"] > 0 and w["scan_threads"] != "auto"
     assert d["device_resident"]["value"] > 0
 
 
