@@ -9,10 +9,10 @@
 // squarings: 99k shader cycles against 135-170k on one lane (tools/microbench/ubench_lanesq.hip,
 // profiles/r09h).
 //
-// Bounds: inputs with even limbs <= 2^26 + 2^20 and odd limbs <= 2^25 + 2^18 (class C, or a
-// dist_* output); a term <= 2^28.1 x 2^30.3, a column of <= 10 terms < 2^61; the first carry round
-// leaves <= 2^40.3, the second limbs <= 2^26 + 2^19.6 (limb 0) / 2^26 + 2^15.3 -- inside the input
-// bounds.  dist_to_fe's fe_carry brings a result back to class C for the one-lane code.
+// Bounds: inputs with limbs < 2^27 + 2^16 (class C, or a dist_* output: lane_cols_carry); a
+// term's operands after the x2 / x4 and x19 scalings < 2^29.1 and < 2^31.3, a column of 10 terms
+// < 2^62.6; the carry brings it back inside the input bounds.  dist_to_fe's fe_carry brings a
+// result back to class C for the one-lane code.
 #pragma once
 #include "fe25519.h"
 
@@ -49,7 +49,20 @@ __device__ __forceinline__ uint32_t lane_bperm(uint32_t src_lane, uint32_t v) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane << 2), (int)v);
 }
 
-// the column sums of lanes 16r + k summed into lane k, then carried: limb k in lane k
+// the column sums of lanes 16r + k summed into lane k, then carried: limb k in lane k.
+// EDV_LANE_CARRY 1 (default): ONE exchange -- each column sum p_k (< 2^62.6) is split at the limb
+// widths into a_k (w_k bits), b_k (the next limb's width) and d_k (the rest, < 2^11.6), and limb k
+// becomes a_k + b_{k-1} + d_{k-2} (x19 where the source wraps past 2^255: b_9 into limb 0, d_8 into
+// limb 0, d_9 into limb 1), both fetched by one pair of ds_bpermute; limb 0's excess (< 2^30.4 in
+// all) then moves into limb 1 through v_readlane, not another LDS round trip.  Outputs: limb 0 <
+// 2^26, limb 1 < 2^26 + 2^16, other even limbs < 2^27 + 2^12, odd limbs < 2^26 + 2^12 -- inputs
+// whose products keep a column of 10 terms below 2^62.6 (x2 and x19 factors included) and whose
+// x19 / x4 operand scalings stay below 2^32 (tests/test_fe_lanes_model.py runs this carry on the
+// CPU against exact arithmetic at those bounds).  EDV_LANE_CARRY 0: the two carry rounds of three
+// ds_bpermute (A/B).
+#ifndef EDV_LANE_CARRY
+#define EDV_LANE_CARRY 1
+#endif
 __device__ __forceinline__ uint32_t lane_cols_carry(uint64_t p, uint32_t k) {
   uint32_t lo = (uint32_t)p, hi = (uint32_t)(p >> 32);
   auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);  // [1]: lanes 0-31 <- lanes 32-63
@@ -59,12 +72,25 @@ __device__ __forceinline__ uint32_t lane_cols_carry(uint64_t p, uint32_t k) {
   auto sl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);  // [1]: row 0 <- row 1
   auto sh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
   p += ((uint64_t)sh[1] << 32) | sl[1];
+#if EDV_LANE_CARRY
+  const uint32_t w = (k & 1) ? 25 : 26, wn = 51 - w;  // widths of limb k and limb k + 1
+  const uint32_t a = (uint32_t)p & ((1u << w) - 1);
+  const uint32_t b = (uint32_t)(p >> w) & ((1u << wn) - 1);
+  const uint32_t d = (uint32_t)(p >> 51);
+  const uint32_t src1 = k == 0 ? 9 : k - 1, src2 = k >= 2 ? k - 2 : k + 8;
+  const uint32_t m1 = k == 0 ? 19 : 1, m2 = k <= 1 ? 19 : 1;
+  const uint32_t bb = lane_bperm(src1, b), dd = lane_bperm(src2, d);
+  const uint32_t r = a + bb * m1 + dd * m2;
+  const uint32_t c0 = (uint32_t)__builtin_amdgcn_readlane((int)(r >> 26), 0);
+  return k == 0 ? (r & ((1u << 26) - 1)) : k == 1 ? r + c0 : r;
+#else
   const uint32_t w = (k & 1) ? 25 : 26, mask = (1u << w) - 1, src = k == 0 ? 9 : k - 1, m = k == 0 ? 19 : 1;
   const uint64_t c = p >> w;
   const uint32_t cl = lane_bperm(src, (uint32_t)c), ch = lane_bperm(src, (uint32_t)(c >> 32));
   const uint64_t s = ((uint64_t)ch << 32 | cl) * m + ((uint32_t)p & mask);
   const uint32_t c2 = lane_bperm(src, (uint32_t)(s >> w));
   return ((uint32_t)s & mask) + c2 * m;
+#endif
 }
 
 // f^2; every lane of the wave takes part (t = c_lane_sq.t[lane], k = lane & 15)
