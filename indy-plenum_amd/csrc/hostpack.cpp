@@ -986,11 +986,15 @@ constexpr int kSigSlot = 96;  // edverify.h EDV_SIG_SLOT96
 // A node-based std::unordered_map<std::string_view> here allocated a node per
 // emplace and cost ~30 % of a worker's time per request.
 struct IdrTable {
-  struct E {
+  // an identifier of up to kInl bytes is compared against a copy in its entry (one cache line),
+  // not against the first object's data, which a churning batch's ~30k identifiers leave cold
+  static constexpr size_t kInl = 32;
+  struct alignas(64) E {
     uint64_t h;
     const char* p;  // the identifier's bytes (the str object's data; owned by the batch's dicts)
     size_t n;
     uint32_t id;
+    char inl[kInl];  // (n <= kInl) a copy of them
   };
   std::vector<E> e;
   size_t mask = 0, used = 0;
@@ -1011,7 +1015,7 @@ struct IdrTable {
   void reset(size_t expect) {
     size_t cap = 64;
     while (cap < 2 * expect) cap <<= 1;
-    e.assign(cap, E{0, nullptr, 0, 0});
+    e.assign(cap, E{});
     mask = cap - 1;
     used = 0;
   }
@@ -1024,12 +1028,13 @@ struct IdrTable {
     for (size_t s = h & mask;; s = (s + 1) & mask) {
       E& x = e[s];
       if (!x.p) {
-        x = E{h, p, n, next};
+        x.h = h, x.p = p, x.n = n, x.id = next;
+        if (n <= kInl) memcpy(x.inl, p, n);
         ++used;
         fresh = true;
         return next;
       }
-      if (x.h == h && x.n == n && (x.p == p || memcmp(x.p, p, n) == 0)) {
+      if (x.h == h && x.n == n && (x.p == p || memcmp(n <= kInl ? x.inl : x.p, p, n) == 0)) {
         fresh = false;
         return x.id;
       }
@@ -1038,7 +1043,7 @@ struct IdrTable {
   void grow() {
     std::vector<E> old;
     old.swap(e);
-    e.assign(old.empty() ? 64 : old.size() * 2, E{0, nullptr, 0, 0});
+    e.assign(old.empty() ? 64 : old.size() * 2, E{});
     mask = e.size() - 1;
     for (const E& x : old)
       if (x.p)
@@ -1630,6 +1635,8 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
     std::vector<uint32_t> kid;      // speculation: the key id of each of its identifiers (kmap)
     std::vector<Py_ssize_t> first;  // the item where the worker met it first
     std::vector<uint64_t> hash;     // IdrTable::hash of each of its identifiers (the merge's partitions)
+    std::vector<char> txt;          // the first IdrTable::kInl bytes of each (the merge compares these)
+    std::vector<uint32_t> tlen;     // and its length
     size_t deferred = 0;            // items left for the GIL pass (3)
 #ifdef EDV_HAVE_DK
     std::unique_ptr<ShapeCache> shapes;  // this call's remembered dict shapes (shaped_dict)
@@ -1873,6 +1880,12 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
         tab.obj.push_back(iv);
         tab.first.push_back(i);
         tab.hash.push_back(IdrTable::hash((const char*)PyUnicode_1BYTE_DATA(iv), (size_t)PyUnicode_GET_LENGTH(iv)));
+        {
+          const size_t tn = (size_t)PyUnicode_GET_LENGTH(iv), at = tab.txt.size();
+          tab.txt.resize(at + IdrTable::kInl);
+          memcpy(tab.txt.data() + at, PyUnicode_1BYTE_DATA(iv), tn < IdrTable::kInl ? tn : IdrTable::kInl);
+          tab.tlen.push_back((uint32_t)tn);
+        }
         if (kmap) tab.kid.push_back(kmap->get((const char*)PyUnicode_1BYTE_DATA(iv), (size_t)PyUnicode_GET_LENGTH(iv)));
       }
       if (kid_out) kid_out[i] = tab.kid[x.uid];
@@ -1922,8 +1935,13 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
             if ((Py_ssize_t)(h % (uint64_t)P) != p) continue;
             PyObject* o = tb.obj[u];
             bool fresh = false;
-            const uint32_t l = pt.tab.find_or_add_h(h, (const char*)PyUnicode_1BYTE_DATA(o),
-                                                     (size_t)PyUnicode_GET_LENGTH(o), (uint32_t)pt.obj.size(), fresh);
+            // the worker's copy of the text when it is short (no cache miss on the object), else its data
+            const bool copied = tb.tlen.size() > u;
+            const size_t on = copied ? (size_t)tb.tlen[u] : (size_t)PyUnicode_GET_LENGTH(o);
+            const char* op = copied && on <= IdrTable::kInl
+                                 ? tb.txt.data() + u * IdrTable::kInl
+                                 : (const char*)PyUnicode_1BYTE_DATA(o);
+            const uint32_t l = pt.tab.find_or_add_h(h, op, on, (uint32_t)pt.obj.size(), fresh);
             if (fresh) {
               pt.obj.push_back(o);
               pt.first.push_back(tb.first[u]);
@@ -1948,7 +1966,20 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
       pt.gid.resize(pt.obj.size());
       for (size_t l = 0; l < pt.obj.size(); ++l) cand.push_back(Cand{pt.first[l], p, (uint32_t)l});
     }
-    std::sort(cand.begin(), cand.end(), [](const Cand& a, const Cand& b) { return a.first < b.first; });
+    if (cand.size() > 4096 && (Py_ssize_t)cand.size() * 16 > n) {
+      // many distinct identifiers (a churning batch: ~30k of 250k items): their first occurrences
+      // are distinct positions of the batch, so a scatter into a position table and one pass over
+      // it orders them in O(n) -- the comparison sort took ~1.5 ms
+      std::vector<uint32_t> at((size_t)n, 0xffffffffu);
+      for (uint32_t c = 0; c < (uint32_t)cand.size(); ++c) at[(size_t)cand[c].first] = c;
+      std::vector<Cand> sorted;
+      sorted.reserve(cand.size());
+      for (Py_ssize_t i = 0; i < n; ++i)
+        if (at[(size_t)i] != 0xffffffffu) sorted.push_back(cand[at[(size_t)i]]);
+      cand.swap(sorted);
+    } else {
+      std::sort(cand.begin(), cand.end(), [](const Cand& a, const Cand& b) { return a.first < b.first; });
+    }
     uniq.reserve(cand.size());
     for (const Cand& c : cand) {
       Part& pt = parts[(size_t)c.p];
@@ -1956,11 +1987,13 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
       uniq.push_back(pt.obj[c.local]);
       if (kmap) spec_u.push_back(pt.kid[c.local]);
     }
-    for (int w = 0; w < t; ++w) {
-      const WorkerIdrs& tb = tabs[(size_t)w];
-      std::vector<uint32_t>& tg = to_global[(size_t)w];
-      for (size_t u = 0; u < tg.size(); ++u) tg[u] = parts[(size_t)(tb.hash[u] % (uint64_t)P)].gid[tg[u]];
-    }
+    run_chunks(t, P > 1 ? t : 1, [&](int, Py_ssize_t a, Py_ssize_t b) {  // each worker's table, side by side
+      for (Py_ssize_t w = a; w < b; ++w) {
+        const WorkerIdrs& tb = tabs[(size_t)w];
+        std::vector<uint32_t>& tg = to_global[(size_t)w];
+        for (size_t u = 0; u < tg.size(); ++u) tg[u] = parts[(size_t)(tb.hash[u] % (uint64_t)P)].gid[tg[u]];
+      }
+    }, 1);
     // the GIL pass (3) below adds the deferred items' identifiers to this table
     for (size_t g = 0; deferred && g < uniq.size(); ++g) {
       bool fresh = false;
