@@ -477,7 +477,19 @@ def time_whole_node(eng, args, sets, idrs, vks, dist_on, dev, scan_threads):
         return bad
 
     st0 = dict(a.stats)
-    el_pipe, outs = clocked(lambda: list(a.authenticate_batches(order)))
+    pipe_per, pipe_parts = [], []
+
+    def pipe_run():
+        res = []
+        tb = time.perf_counter()
+        for r in a.authenticate_batches(order):
+            res.append(r)
+            tn = time.perf_counter()
+            pipe_per.append(tn - tb)
+            pipe_parts.append(a._g.last_breakdown)
+            tb = tn
+        return res
+    el_pipe, outs = clocked(pipe_run)
     st1 = dict(a.stats)
     bad_pipe = check(outs)
     del outs
@@ -496,8 +508,13 @@ def time_whole_node(eng, args, sets, idrs, vks, dist_on, dev, scan_threads):
     bad_sync = check(outs)
     del outs
     med = sorted(range(K), key=lambda k: per[k])[K // 2]
+    pmed = sorted(range(len(pipe_per)), key=lambda k: pipe_per[k])[len(pipe_per) // 2] if pipe_per else None
     out = {"pipelined": {"value": n * K / el_pipe, "ms_per_batch": el_pipe / K * 1e3, "seconds": el_pipe,
                          "speculated_share": (st1.get("speculated", 0) - st0.get("speculated", 0)) / (n * K),
+                         "yield_ms": {"p50": float(np.median(pipe_per)) * 1e3, "min": min(pipe_per) * 1e3,
+                                      "max": max(pipe_per) * 1e3} if pipe_per else None,
+                         "in_batch_ms": {k: (round(v, 3) if isinstance(v, float) else v)
+                                         for k, v in ((pipe_parts[pmed] if pmed is not None else None) or {}).items()},
                          "mismatches": bad_pipe},
            "synchronous": {"value": n * K / el_sync, "ms_per_batch": el_sync / K * 1e3, "seconds": el_sync,
                            "batch_ms": {"p50": float(np.median(per)) * 1e3, "min": min(per) * 1e3,

@@ -2965,8 +2965,8 @@ int verify_one_resident(edv_ctx* ctx, const uint8_t* sig64, uint32_t key_id, con
                         uint8_t* accept) {
   if (!ctx->res_on || mlen > kResMsgMax || ctx->key_count == 0) return 1;
   using rclk = std::chrono::steady_clock;
-  HIP_TRY(hipSetDevice(ctx->device));
   if (!ctx->res_box) {
+    HIP_TRY(hipSetDevice(ctx->device));
     void* p = nullptr;
     if (hipHostMalloc(&p, sizeof(ResBox), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
       ctx->res_on = false;
@@ -2995,6 +2995,7 @@ int verify_one_resident(edv_ctx* ctx, const uint8_t* sig64, uint32_t key_id, con
   }
   if (ctx->res_launched && ctx->res_stopping && (r = wait_gone())) return r;
   auto launch = [&](uint64_t answered) -> int {  // answered: the last request the host has its verdict of
+    HIP_TRY(hipSetDevice(ctx->device));  // (only here: a request to a running kernel makes no HIP call)
     __atomic_store_n(&b->stop, (uint64_t)0, __ATOMIC_RELAXED);
     __atomic_store_n(&b->done_seq, answered, __ATOMIC_RELAXED);
     __atomic_store_n(&b->running, 1u, __ATOMIC_RELEASE);

@@ -44,7 +44,9 @@ message from Node.verifySignature, node.py:2294-2318):
 `CoreAuthNr` is an alias of GpuAuthNr; `ReqAuthenticator` aggregates
 authenticators (names from BASELINE.json's north star).
 """
+import contextlib
 import copy
+import gc
 import threading
 import os
 from abc import abstractmethod
@@ -135,6 +137,24 @@ def _results_failing(ok, short, uidx_b, uniq):
         for i in failed:
             results[i] = InvalidSignature()
     return results, failed
+
+
+@contextlib.contextmanager
+def _gc_paused():
+    """The cyclic collector paused for one batch call (reference counting still frees everything):
+    a batch makes a few large temporary containers (the distinct identifiers, their keys: ~30k
+    entries each under key churn), and every young-generation collection the call's own
+    allocations set off would walk all of them -- 5-10 ms of a 250k-request batch went there.
+    Collections due meanwhile run at the next allocation after the call, once the temporaries are
+    gone.  The previous state is restored however the call ends."""
+    was = gc.isenabled()
+    if was:
+        gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
 
 
 def _known_getverkey(cls):
@@ -680,9 +700,10 @@ class GpuAuthMixin:
     def authenticate_batch(self, msgs, identifiers=None, signatures=None):
         """Per message: the identifier authenticate() would return, or the
         exception instance it would raise (same class, args and __cause__)."""
-        if _scan_batch is not None and not identifiers and not signatures and self._native_host_steps():
-            return self._authenticate_batch_scanned(msgs)
-        return self._authenticate_batch_each(msgs, identifiers, signatures)
+        with _gc_paused():
+            if _scan_batch is not None and not identifiers and not signatures and self._native_host_steps():
+                return self._authenticate_batch_scanned(msgs)
+            return self._authenticate_batch_each(msgs, identifiers, signatures)
 
     def _native_host_steps(self):
         """The native scan restates GpuAuthMixin._prepare / serializeForSig;
@@ -1074,7 +1095,7 @@ class GpuAuthMixin:
             for msgs in batches:
                 res = None
                 if can and len(msgs) >= _STAGE_MIN_BATCH:
-                    with _engine_lock(eng):
+                    with _engine_lock(eng), _gc_paused():
                         s = k % 2
                         bufs = self._scan_buffers(eng, len(msgs), slot, s)
                         if bufs is not self._g.scan_out:
@@ -1083,15 +1104,21 @@ class GpuAuthMixin:
                     prev, pending = pending, res  # (held first: a close() at the yield collects it)
                     k += 1
                     if prev is not None:
-                        yield prev()
+                        with _gc_paused():
+                            out = prev()
+                        yield out
                     continue
                 if pending is not None:  # the batch in flight first (its staging set is free after)
                     done, pending = pending, None
-                    yield done()
+                    with _gc_paused():
+                        out = done()
+                    yield out
                 yield res if res is not None else self.authenticate_batch(msgs)
             if pending is not None:
                 done, pending = pending, None
-                yield done()
+                with _gc_paused():
+                    out = done()
+                yield out
         finally:
             if pending is not None:  # an iteration abandoned with a batch in flight: free its staging set
                 pending()

@@ -1325,3 +1325,38 @@ def test_staging_reserve_fault_is_raised_not_read_as_busy(oracle, monkeypatch):
     with pytest.raises(RuntimeError, match="hipMalloc"):
         a.authenticate_batch(steady)
     assert eng.held == [None, None]
+
+
+def test_batch_calls_pause_and_restore_the_collector(oracle, monkeypatch):
+    """authenticate_batch pauses the cyclic collector for its own duration only: enabled again
+    after the call, after a call that raises, and left disabled if the caller had disabled it."""
+    import gc
+    from plenum_amd import client_authn as CA
+    idrs, vks, msgs = _signed(2, 40)
+    a = GpuAuthNr(engine=OracleEngine(oracle))
+    for i, v in zip(idrs, vks):
+        a.addIdr(i, v)
+    seen = []
+    real = a._authenticate_batch_scanned
+
+    def spy(m):
+        seen.append(gc.isenabled())
+        return real(m)
+    monkeypatch.setattr(a, "_authenticate_batch_scanned", spy)
+    assert gc.isenabled()
+    assert a.authenticate_batch(msgs) == [m["identifier"] for m in msgs]
+    assert seen == [False] and gc.isenabled()
+
+    def boom(m):
+        raise MemoryError("injected")
+    monkeypatch.setattr(a, "_authenticate_batch_scanned", boom)
+    with pytest.raises(MemoryError):
+        a.authenticate_batch(msgs)
+    assert gc.isenabled()
+    gc.disable()
+    try:
+        monkeypatch.setattr(a, "_authenticate_batch_scanned", spy)
+        a.authenticate_batch(msgs)
+        assert not gc.isenabled()
+    finally:
+        gc.enable()
