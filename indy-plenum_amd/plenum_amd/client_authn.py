@@ -47,6 +47,7 @@ authenticators (names from BASELINE.json's north star).
 import contextlib
 import copy
 import gc
+from time import perf_counter as _perf_counter
 import threading
 import os
 from abc import abstractmethod
@@ -812,6 +813,8 @@ class GpuAuthMixin:
         natively.  Messages the scan leaves to Python (odd types, missing
         fields, bad base58 ...) go through _prepare, which raises the
         reference's exception."""
+        from time import perf_counter
+        self._g.t_enter = perf_counter()  # (the breakdown's before_scan: buffers, staging reserve)
         eng = self._engine()
         with _engine_lock(eng):
             slot = _SIG_SLOT if getattr(eng, "supports_sig_slots", False) else 64
@@ -973,7 +976,8 @@ class GpuAuthMixin:
             def verdicts(ok, t3):
                 results, failed = _results_failing(ok, short, uidx_b, uniq)
                 t4 = perf_counter()
-                g.last_breakdown = {"scan_and_copies": (t1 - t0) * 1e3, "keys_and_ids": (t2 - t1) * 1e3,
+                g.last_breakdown = {"before_scan": (t0 - getattr(g, "t_enter", t0)) * 1e3,
+                                    "scan_and_copies": (t1 - t0) * 1e3, "keys_and_ids": (t2 - t1) * 1e3,
                                     "verify_wait": (t3 - t2) * 1e3, "verdicts": (t4 - t3) * 1e3,
                                     "speculated": bool(spec_hit)}
                 return results
@@ -1067,10 +1071,25 @@ class GpuAuthMixin:
         g.stats["batch_items"] += n
         g.stats["keyed_items"] += n - len(gen)
         results, failed = _results_failing(ok, short, uidx_b, uniq)
-        g.last_breakdown = {"scan_and_copies": (t1 - t0) * 1e3, "keys_and_ids": (t2 - t1) * 1e3,
+        g.last_breakdown = {"before_scan": (t0 - getattr(g, "t_enter", t0)) * 1e3,
+                            "scan_and_copies": (t1 - t0) * 1e3, "keys_and_ids": (t2 - t1) * 1e3,
                             "verify_wait": (t3 - t2) * 1e3, "verdicts": (perf_counter() - t3) * 1e3,
                             "speculated": False, "general_items": int(len(gen))}
         return results
+
+    def _speculation_ready(self):
+        """The next staged batch would speculate: a key-id map from the batches before that no key
+        store change has invalidated (_authenticate_staged's condition)."""
+        g = self._g
+        if not (g.speculate and g.kid_map is not None and _kid_map is not None
+                and os.environ.get("EDV_SPECULATE", "1") != "0"
+                and getattr(self._engine(), "supports_staged_parts", False)):
+            return False
+        ks = self._key_store()
+        if ks is None:
+            return False
+        ks._sync()
+        return g.kid_map_version == ks.version
 
     def authenticate_batches(self, batches):
         """authenticate_batch over an iterable of batches, yielding each batch's
@@ -1094,8 +1113,15 @@ class GpuAuthMixin:
         try:
             for msgs in batches:
                 res = None
+                if can and len(msgs) >= _STAGE_MIN_BATCH and pending is None and self._speculation_ready():
+                    # the steady state: this batch's kernels run under its own scan (speculation), so
+                    # there is no GPU work left to overlap with the next batch -- one staging set, the
+                    # synchronous batch (two sets in flight measured slower there: profiles/r10f, r10h)
+                    yield self.authenticate_batch(msgs)
+                    continue
                 if can and len(msgs) >= _STAGE_MIN_BATCH:
                     with _engine_lock(eng), _gc_paused():
+                        self._g.t_enter = _perf_counter()
                         s = k % 2
                         bufs = self._scan_buffers(eng, len(msgs), slot, s)
                         if bufs is not self._g.scan_out:
