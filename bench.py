@@ -448,7 +448,7 @@ def time_whole_node(eng, args, sets, idrs, vks, dist_on, dev, scan_threads):
     wants = [want[k % len(sets)] for k in range(K)]
     for k in range(max(1, W)):  # scan buffers grown, kid_map built, both staging sets touched
         a.authenticate_batch(sets[k % len(sets)])
-    for _ in a.authenticate_batches([sets[k % len(sets)] for k in range(2)]):
+    for _ in a.authenticate_batches([sets[k % len(sets)] for k in range(max(2, W))]):
         pass
 
     def clocked(fn):
@@ -704,8 +704,9 @@ def time_key_churn(eng, signers=100_000, n=1_000_000, batches=4, zipf=1.1, seed_
     out_b = []
     total = 0.0
     bad = 0
+    chunks = [reqs[b * per:(b + 1) * per] for b in range(batches)]  # (the batch lists, made before the clock)
     for b in range(batches):
-        chunk = reqs[b * per:(b + 1) * per]
+        chunk = chunks[b]
         st0 = dict(a.stats)
         t0 = time.perf_counter()
         res = a.authenticate_batch(chunk)

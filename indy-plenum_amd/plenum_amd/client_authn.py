@@ -701,10 +701,17 @@ class GpuAuthMixin:
     def authenticate_batch(self, msgs, identifiers=None, signatures=None):
         """Per message: the identifier authenticate() would return, or the
         exception instance it would raise (same class, args and __cause__)."""
-        with _gc_paused():
+        # (_gc_paused's work inline: entering a context manager allocates, and that allocation could
+        # set off the very collection -- over the caller's fresh batch list -- the pause is for)
+        was = gc.isenabled()
+        gc.disable()
+        try:
             if _scan_batch is not None and not identifiers and not signatures and self._native_host_steps():
                 return self._authenticate_batch_scanned(msgs)
             return self._authenticate_batch_each(msgs, identifiers, signatures)
+        finally:
+            if was:
+                gc.enable()
 
     def _native_host_steps(self):
         """The native scan restates GpuAuthMixin._prepare / serializeForSig;
