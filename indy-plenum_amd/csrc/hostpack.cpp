@@ -1148,6 +1148,37 @@ PyObject* py_kid_map(PyObject*, PyObject* args) {
   }
   return ret;
 }
+// verify_one(fn, ctx, sig64, key_id, msg) -> bool: edverify.h edv_verify_one through its address
+// (EdVerifyEngine.verify_one_keyed's call without the ctypes argument conversions: the per-message
+// authenticate() that missed the verify-ahead cache), the GIL released while the GPU answers.
+// Raises RuntimeError(code) when the library returns an error (the caller reads edv_last_error).
+using VerifyOneFn = int (*)(void*, const uint8_t*, uint32_t, const uint8_t*, uint64_t, uint8_t*);
+PyObject* py_verify_one(PyObject*, PyObject* args) {
+  unsigned long long fn, ctx;
+  Py_buffer sig, msg;
+  unsigned int kid;
+  if (!PyArg_ParseTuple(args, "KKy*Iy*", &fn, &ctx, &sig, &kid, &msg)) return nullptr;
+  int r = -1;
+  uint8_t ok = 0;
+  if (sig.len != 64 || !fn || !ctx) {
+    PyBuffer_Release(&sig);
+    PyBuffer_Release(&msg);
+    PyErr_SetString(PyExc_ValueError, "verify_one: a 64-byte signature and the library's addresses");
+    return nullptr;
+  }
+  Py_BEGIN_ALLOW_THREADS
+  r = ((VerifyOneFn)(uintptr_t)fn)((void*)(uintptr_t)ctx, (const uint8_t*)sig.buf, (uint32_t)kid,
+                                   msg.len ? (const uint8_t*)msg.buf : nullptr, (uint64_t)msg.len, &ok);
+  Py_END_ALLOW_THREADS
+  PyBuffer_Release(&sig);
+  PyBuffer_Release(&msg);
+  if (r != 0) {
+    PyErr_Format(PyExc_RuntimeError, "edv_verify_one %d", r);
+    return nullptr;
+  }
+  return PyBool_FromLong(ok & 1);
+}
+
 PyObject* py_kid_map_size(PyObject*, PyObject* cap) {
   KidMap* m = (KidMap*)PyCapsule_GetPointer(cap, "edv.kidmap");
   return m ? PyLong_FromSize_t(m->used) : nullptr;
@@ -3194,6 +3225,8 @@ PyMethodDef kMethods[] = {
      "scan_batch(msgs, ignore, threads=0, out=None) -> (fast, idrs, sig64, msgbuf, off, short): authenticate()'s "
      "host steps for a batch.  out = [bytearray, bytearray]: sig64 / msgbuf are written into them (grown, never "
      "shrunk: slice to n * 64 and off[n] bytes) and returned"},
+    {"verify_one", py_verify_one, METH_VARARGS,
+     "verify_one(fn, ctx, sig64, key_id, msg) -> bool: edv_verify_one at address fn on context ctx"},
     {"keys_known_flat", py_keys_known_flat, METH_VARARGS,
      "keys_known_flat(clients, fast_keys, identifiers, field) -> (keys, holes, flat): keys_known on the "
      "worker pool, plus the 32-byte keys in one buffer"},

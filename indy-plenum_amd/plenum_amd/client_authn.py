@@ -506,10 +506,12 @@ class GpuAuthMixin:
         slots only), registered before the batch routes its items (asynchronous
         builds by default)."""
         g = self._g
+        n_reg = 0
         if g.hot:  # at most max_promotions per batch (each a table build on the device)
             got = ks.register(list(g.hot)[:g.max_promotions], pinned=batch_keys, evict=True,
                               asynchronous=g.async_key_builds, pinned_ids=pinned_ids)
             g.stats["keys_registered"] += len(got)
+            n_reg += len(got)
             g.hot.clear()
         if g.pending:
             room = ks.free_slots()
@@ -517,7 +519,9 @@ class GpuAuthMixin:
                 got = ks.register([k for k in g.pending if k not in ks][:room], evict=False,
                                   asynchronous=g.async_key_builds)
                 g.stats["keys_registered"] += len(got)
+                n_reg += len(got)
             g.pending.clear()
+        return n_reg
 
     def keys_settle(self):
         """Register the addIdr keys waiting for a slot and wait until every
@@ -950,9 +954,14 @@ class GpuAuthMixin:
             ids = None
             general_u = None  # distinct identifiers whose key has no built table: the general path
             if ks is not None and fast_b.count(0) == 0 and all_keys:
+                pre = None
                 if g.hot or g.pending:  # (the batch's keys pinned by id: one native lookup)
-                    self._register_waiting(ks, ukeys, ks.ids_of(uflat, uodd, ukeys) if g.hot else None)
-                ids = ks.lookup_array(ukeys, uflat, uodd)
+                    pre = ks.ids_of(uflat, uodd, ukeys) if g.hot else None
+                    v0 = ks.version
+                    got = self._register_waiting(ks, ukeys, pre)
+                    if got or ks.version != v0:
+                        pre = None  # (a key of this batch may have been registered: look up again)
+                ids = ks.lookup_array(ukeys, uflat, uodd, pre)
                 if (ids < 0).any():
                     general_u = np.flatnonzero(ids < 0)
                     ids[general_u] = 0xffffffff  # (an id the kernels reject)
@@ -1044,25 +1053,40 @@ class GpuAuthMixin:
         kid = np.frombuffer(_gather_u32(np.asarray(ids, np.uint32).tobytes(), uidx_b,
                                         kid_buf if kid_buf is not None else g.kid_out), np.uint32, count=n)
         t2 = perf_counter()
-        ok = np.array(eng.verify_staged(True, kid, slot_base, 0, spans[:n], spans[n:]), bool)
-        uidx = np.frombuffer(uidx_b, np.uint32)
-        is_gen = np.zeros(len(ukeys), bool)
-        is_gen[general_u] = True
-        gen = np.flatnonzero(is_gen[uidx])
+        # the keyed verify queued first; the general items' indices and keys are gathered while it runs
+        handle = eng.verify_staged_submit(True, kid, slot_base, 0, spans[:n], spans[n:]) \
+            if hasattr(eng, "verify_staged_submit") else None
+        ok = None if handle is not None else np.array(eng.verify_staged(True, kid, slot_base, 0, spans[:n],
+                                                                        spans[n:]), bool)
+        try:
+            uidx = np.frombuffer(uidx_b, np.uint32)
+            is_gen = np.zeros(len(ukeys), bool)
+            is_gen[general_u] = True
+            gen = np.flatnonzero(is_gen[uidx])
+            gen_keys = None
+            if len(gen):
+                if uflat is not None and len(uflat) == 32 * len(ukeys):
+                    ukey_arr = np.frombuffer(uflat, np.uint8).reshape(-1, 32)  # (the general keys are 32 B)
+                else:
+                    ukey_arr = np.zeros((len(ukeys), 32), np.uint8)
+                    ukey_arr[general_u] = np.frombuffer(b"".join(ukeys[u] for u in general_u),
+                                                        np.uint8).reshape(-1, 32)
+                gen_keys = ukey_arr[uidx[gen]]
+        except BaseException:
+            if handle is not None:  # (the set is freed before the error propagates)
+                eng.verify_staged_collect(handle)
+            raise
+        if handle is not None:
+            ok = np.array(eng.verify_staged_collect(handle), bool)
         if len(gen):
-            if uflat is not None and len(uflat) == 32 * len(ukeys):
-                ukey_arr = np.frombuffer(uflat, np.uint8).reshape(-1, 32)  # (the general identifiers' keys are 32 B)
-            else:
-                ukey_arr = np.zeros((len(ukeys), 32), np.uint8)
-                ukey_arr[general_u] = np.frombuffer(b"".join(ukeys[u] for u in general_u), np.uint8).reshape(-1, 32)
             if getattr(eng, "supports_staged_subset", False):
                 # the staged batch is still in HBM: only the items' indices and key bytes go over
-                okg = np.asarray(eng.verify_staged_subset(gen.astype(np.uint32), ukey_arr[uidx[gen]]), bool)
+                okg = np.asarray(eng.verify_staged_subset(gen.astype(np.uint32), gen_keys), bool)
             else:
                 s_sig, s_msg, s_off = _gather_spans(memoryview(sig_o).cast("B")[:slot * n], msg_o, spans_b,
                                                     gen.astype(np.uint32).tobytes(), slot)
                 okg = np.asarray(eng.verify_batch(np.frombuffer(s_sig, np.uint8).reshape(-1, slot),
-                                                  ukey_arr[uidx[gen]], np.frombuffer(s_msg, np.uint8),
+                                                  gen_keys, np.frombuffer(s_msg, np.uint8),
                                                   np.frombuffer(s_off, np.uint64),
                                                   **({"sig_slot": slot} if slot != 64 else {})), bool)
             ok[gen] = okg

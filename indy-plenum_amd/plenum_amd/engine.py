@@ -117,9 +117,16 @@ class EdVerifyEngine:
         self._ctx = ctypes.c_void_p(ctx)
         self.device = device
         self._one_args = threading.local()  # verify_one_keyed's reusable ctypes arguments
+        try:  # verify_one_keyed through the host extension: (function, edv_verify_one address, context)
+            from ._hostpack import verify_one as _native_one
+            self._one_native = (_native_one, ctypes.cast(self._lib.edv_verify_one, ctypes.c_void_p).value,
+                                self._ctx.value)
+        except (ImportError, AttributeError):
+            self._one_native = None
 
     # ------------------------------------------------------------- lifecycle
     def close(self):
+        self._one_native = None  # (it holds the context's address)
         if getattr(self, "_ctx", None):
             self._lib.edv_destroy(self._ctx)
             self._ctx = None
@@ -611,6 +618,13 @@ class EdVerifyEngine:
         if len(sig64) != 64:
             raise ValueError("sig64 must be 64 bytes")
         # (edv_verify_one: the resident kernel's mailbox, or one launch of the small kernel)
+        one = self._one_native
+        if one is not None:  # the native call (csrc/hostpack.cpp verify_one): no ctypes conversions
+            try:
+                return one[0](one[1], one[2], sig64, int(key_id), msg)
+            except RuntimeError as ex:
+                code = int(str(ex).split()[-1]) if str(ex).split()[-1].lstrip("-").isdigit() else -1
+                raise EdVerifyError(code, self._lib.edv_last_error().decode(errors="replace")) from None
         # argument objects of this thread, reused from call to call (building them costs microseconds)
         tl = self._one_args.__dict__
         if "ok" not in tl:

@@ -189,16 +189,19 @@ class KeyStore:
         self._tick += 1
         return None if i in self._building else i
 
-    def lookup_array(self, keys, flat=None, odd=()):
+    def lookup_array(self, keys, flat=None, odd=(), ids=None):
         """lookup() as an int64 array, -1 where lookup() answers None (one
         pass over the keys; the hits' ticks and the building filter vectorized).
         flat: the same keys as one buffer of 32 bytes each (keys_known_flat),
         looked up in the native index in one call; odd: the positions of keys
-        that are not 32 bytes (zeros in flat), looked up in the dict.""" 
+        that are not 32 bytes (zeros in flat), looked up in the dict; ids: the
+        same keys' ids_of() answer when nothing was registered since.""" 
         self._sync()
         if self._building:
             self._refresh()
-        if flat is not None and self._index is not None and len(flat) == 32 * len(keys):
+        if ids is not None and len(ids) == len(keys):  # (ids_of's answer, no registration since)
+            ids = np.array(ids, np.int64)
+        elif flat is not None and self._index is not None and len(flat) == 32 * len(keys):
             ids = np.frombuffer(_ki_get(self._index, flat), np.int64).copy()
             for j in odd:  # (keys that are not 32 bytes: zeros in flat)
                 ids[j] = self._ids.get(keys[j], -1) if keys[j].__class__ is bytes else -1
