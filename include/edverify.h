@@ -141,6 +141,8 @@ typedef struct edv_stats {
   uint32_t reserved;
   uint64_t resident_launches; /* edv_verify_one: resident kernels launched, requests they served */
   uint64_t resident_served;
+  double resident_service_us;  /* the last request's time in the resident kernel, from seeing it to its
+                                  verdict (100 MHz wall clock); the engine call's rest is PCIe and host */
 } edv_stats;
 int edv_get_stats(edv_ctx *ctx, edv_stats *out);
 

@@ -1432,7 +1432,8 @@ struct ResBox {
   const uint8_t* key_pk;
   const uint8_t* key_valid;
   uint64_t key_cap;
-  uint64_t pad[6];
+  uint64_t service_ticks;  // kernel: 100 MHz wall-clock ticks from seeing the request to its verdict (diagnostic)
+  uint64_t pad[5];
   uint8_t sig[64];
   uint8_t msg[kResMsgMax];
 };
@@ -1441,7 +1442,7 @@ static_assert(offsetof(ResBox, key_id) == offsetof(ResBox, mlen) + 8 && offsetof
                   offsetof(ResBox, key_cap) == offsetof(ResBox, mlen) + 40,
               "the kernel loads mlen .. key_cap as six consecutive words");
 struct alignas(16) ResShared {
-  uint64_t seq;
+  uint64_t seq, t_seen;
   uint64_t field[6];  // ResBox's mlen .. key_cap, as loaded
   uint32_t cmd, pad;
   uint32_t sig[16];
@@ -1478,6 +1479,7 @@ __global__ __launch_bounds__(kSmallThreads) void edv_resident_kernel(ResBox* box
       }
       rs.cmd = cmd;
       rs.seq = seq;
+      rs.t_seen = wall_clock64();
     }
     __syncthreads();
     if (!rs.cmd) break;  // workgroup-uniform
@@ -1512,6 +1514,7 @@ __global__ __launch_bounds__(kSmallThreads) void edv_resident_kernel(ResBox* box
                                     (const uint8_t*)rs.field[3], (const uint8_t*)rs.field[4], (const uint8_t*)rs.msg,
                                     mlen, (const uint32_t*)rs.field[2], rs.field[5], btab, ident);
     if (t == 0) {
+      __hip_atomic_store(&box->service_ticks, wall_clock64() - rs.t_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(&box->verdict, ok ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(&box->done_seq, rs.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       last = rs.seq;
@@ -3742,6 +3745,8 @@ int edv_get_stats(edv_ctx* ctx, edv_stats* out) {
   out->host_direct = (uint32_t)ctx->last_direct;
   out->resident_launches = ctx->res_launches;
   out->resident_served = ctx->res_served;
+  out->resident_service_us = ctx->res_box ? (double)__atomic_load_n(&ctx->res_box->service_ticks, __ATOMIC_ACQUIRE) / 100.0
+                                          : 0.0;
   return 0;
 }
 

@@ -104,7 +104,8 @@ class EdvStats(ctypes.Structure):
     _fields_ = [("phase_ms", ctypes.c_double * 4), ("launch_count", ctypes.c_int32), ("phases_valid", ctypes.c_int32),
                 ("chunk_items", ctypes.c_uint64), ("host_call_ms", ctypes.c_double), ("host_stage_ms", ctypes.c_double),
                 ("host_h2d_bytes", ctypes.c_uint64), ("host_direct", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
-                ("resident_launches", ctypes.c_uint64), ("resident_served", ctypes.c_uint64)]
+                ("resident_launches", ctypes.c_uint64), ("resident_served", ctypes.c_uint64),
+                ("resident_service_us", ctypes.c_double)]
 
 
 EDV_EBUSY = -5  # include/edverify.h: the staging set holds an uncollected submission
