@@ -2765,6 +2765,72 @@ int w_dict_get_str(PyObject* d, PyObject* key, PyObject** v) {
 }
 #endif
 
+#ifdef EDV_HAVE_DK
+// keys_known_flat's prefetch pipeline for identifier j of a worker's range [.., b): the link of
+// the identifiers 4d, 3d, 2d and d ahead (index slots; entries; the entries' key texts and values;
+// the nym dicts' tables and the tuples' key bytes).  Only the hash computation writes (into the
+// identifier's own cached hash, as the lookup would: the worker's own item).
+inline void keys_prefetch_links(PyObject* clients, PyObject* fk, PyObject** items, Py_ssize_t j, Py_ssize_t b,
+                                Py_ssize_t d) {
+  const auto idx_of = [](PyObject* dct, Py_hash_t h, const DkEntry*& ent) -> Py_ssize_t {
+    if (((const PyDictObject*)dct)->ma_values) return -1;
+    Py_ssize_t ne = 0;
+    ent = dk_entries(dct, ne);
+    if (!ent) return -1;
+    const DkHead* k = (const DkHead*)((const PyDictObject*)dct)->ma_keys;
+    const Py_ssize_t sz = k->size, s = (Py_ssize_t)((size_t)h & (size_t)(sz - 1));
+    const Py_ssize_t ix = sz <= 0xff ? ((const int8_t*)k->idx)[s]
+                          : sz <= 0xffff ? ((const int16_t*)k->idx)[s]
+                          : sz <= 0xffffffffLL ? ((const int32_t*)k->idx)[s] : ((const int64_t*)k->idx)[s];
+    return ix >= 0 && ix < ne ? ix : -1;
+  };
+  const auto cached_hash = [&](Py_ssize_t i) -> Py_hash_t {
+    PyObject* s = items[i];
+    return PyUnicode_CheckExact(s) ? ((PyASCIIObject*)s)->hash : -1;
+  };
+  const DkEntry* ent;
+  Py_ssize_t ix;
+  if (j + 4 * d < b) {  // link 1: the index slots (the hash computed now when not cached)
+    PyObject* s = items[j + 4 * d];
+    if (PyUnicode_CheckExact(s)) {
+      Py_hash_t h = ((PyASCIIObject*)s)->hash;
+      if (h == -1) h = PyObject_Hash(s);
+      for (PyObject* dct : {clients, fk}) {
+        if (h == -1 || ((const PyDictObject*)dct)->ma_values) continue;
+        const DkHead* k = (const DkHead*)((const PyDictObject*)dct)->ma_keys;
+        const Py_ssize_t sz = k->size, w = sz <= 0xff ? 1 : sz <= 0xffff ? 2 : sz <= 0xffffffffLL ? 4 : 8;
+        __builtin_prefetch(k->idx + ((size_t)h & (size_t)(sz - 1)) * w);
+      }
+    }
+  }
+  if (j + 3 * d < b) {  // link 2: the entries
+    const Py_hash_t h = cached_hash(j + 3 * d);
+    if (h != -1)
+      for (PyObject* dct : {clients, fk})
+        if ((ix = idx_of(dct, h, ent)) >= 0) __builtin_prefetch(&ent[ix]);
+  }
+  if (j + 2 * d < b) {  // link 3: the entries' key texts (compared) and values (nym dict, tuple)
+    const Py_hash_t h = cached_hash(j + 2 * d);
+    if (h != -1)
+      for (PyObject* dct : {clients, fk})
+        if ((ix = idx_of(dct, h, ent)) >= 0 && ent[ix].h == h) {
+          if (ent[ix].k != items[j + 2 * d]) __builtin_prefetch(ent[ix].k);
+          __builtin_prefetch(ent[ix].v);
+        }
+  }
+  if (j + d < b) {  // link 4: the nym dict's table, the tuple's key bytes
+    const Py_hash_t h = cached_hash(j + d);
+    if (h != -1) {
+      if ((ix = idx_of(clients, h, ent)) >= 0 && ent[ix].h == h && ent[ix].v && Py_TYPE(ent[ix].v) == &PyDict_Type)
+        __builtin_prefetch(((const PyDictObject*)ent[ix].v)->ma_keys);
+      if ((ix = idx_of(fk, h, ent)) >= 0 && ent[ix].h == h && ent[ix].v && PyTuple_CheckExact(ent[ix].v) &&
+          PyTuple_GET_SIZE(ent[ix].v) == 2)
+        __builtin_prefetch(PyTuple_GET_ITEM(ent[ix].v, 1));
+    }
+  }
+}
+#endif
+
 // keys_known_flat(clients, fast_keys, identifiers, field) -> (keys, holes, flat): keys_known on the
 // scan's worker pool, plus the keys' bytes in one buffer (flat[32 j .. 32 j + 32) = keys[j]; zeros
 // at the holes, which include any key that is not 32 bytes) so the key store lookup and the general path's key array need no
@@ -2791,9 +2857,15 @@ PyObject* py_keys_known_flat(PyObject* self, PyObject* args) {
     std::vector<PyObject*> got((size_t)n, nullptr);
     std::vector<uint8_t> undecided((size_t)n, 0);
     PyObject** items = ((PyListObject*)idrs)->ob_item;
+    static const bool prefetch = !(getenv("EDV_KEYS_PREFETCH") && getenv("EDV_KEYS_PREFETCH")[0] == '0');  // A/B
     run_chunks(n, scan_threads(n, 0), [&](int, Py_ssize_t a, Py_ssize_t b) {
+      // each lookup is a chain of ~10 dependent cache misses (index slot, entry, key text, nym
+      // dict, its table, tuple, key bytes): the identifiers 1-4 x kPD ahead walk the same chains
+      // one link per iteration with prefetches only (reads in bounds; a stale guess wastes a
+      // prefetch), so the lookups below find their lines cached -- keys_known's pipeline, per worker
+      constexpr Py_ssize_t kPD = 6;
       for (Py_ssize_t j = a; j < b; ++j) {
-        if (j + 8 < b) __builtin_prefetch(items[j + 8]);
+        if (prefetch) keys_prefetch_links(clients, fk, items, j, b, kPD);
         PyObject* idr = items[j];
         PyObject *nym = nullptr, *vk = nullptr, *e = nullptr, *key = nullptr;
         int r = w_dict_get_str(clients, idr, &nym);
@@ -3012,11 +3084,22 @@ PyObject* py_key_index_get(PyObject*, PyObject* args) {
     out = PyBytes_FromStringAndSize(nullptr, 8 * m);
     if (out) {
       int64_t* o = (int64_t*)PyBytes_AS_STRING(out);
-      for (Py_ssize_t j = 0; j < m; ++j) {
-        uint64_t w[4];
-        memcpy(w, (const char*)bk.buf + 32 * j, 32);
-        o[j] = ki->get(w);
-      }
+      const char* kb = (const char*)bk.buf;
+      const KeyIndex& kx = *ki;
+      // read-only probes: a churning batch's ~30k keys on the worker pool, each probe's slot
+      // prefetched 8 keys ahead (the table is ~1.5 MB for 16k keys: a miss per key otherwise)
+      run_chunks(m, m >= 8192 ? scan_threads(m, 0) : 1, [&](int, Py_ssize_t a, Py_ssize_t b) {
+        const size_t mask = kx.e.size() - 1;
+        for (Py_ssize_t j = a; j < b; ++j) {
+          uint64_t w[4];
+          if (j + 8 < b) {
+            memcpy(w, kb + 32 * (j + 8), 32);
+            __builtin_prefetch(&kx.e[KeyIndex::hash(w) & mask]);
+          }
+          memcpy(w, kb + 32 * j, 32);
+          o[j] = kx.get(w);
+        }
+      });
     }
   } else if (ki) {
     PyErr_SetString(PyExc_ValueError, "key_index_get: 32-byte keys");

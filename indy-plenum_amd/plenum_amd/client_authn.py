@@ -951,8 +951,10 @@ class GpuAuthMixin:
             g.msg_bytes_per_item = max(g.msg_bytes_per_item * 0.5, float(staged_bytes) / n if n else 0.0)
             # authenticate():93-99, once per identifier (on the worker pool; the keys also as one buffer)
             ukeys, uflat, uodd, all_keys = self._keys_for_flat(uniq)
+            tk = perf_counter()
             ids = None
             general_u = None  # distinct identifiers whose key has no built table: the general path
+            tr = tk
             if ks is not None and fast_b.count(0) == 0 and all_keys:
                 pre = None
                 if g.hot or g.pending:  # (the batch's keys pinned by id: one native lookup)
@@ -961,6 +963,7 @@ class GpuAuthMixin:
                     got = self._register_waiting(ks, ukeys, pre)
                     if got or ks.version != v0:
                         pre = None  # (a key of this batch may have been registered: look up again)
+                tr = perf_counter()
                 ids = ks.lookup_array(ukeys, uflat, uodd, pre)
                 if (ids < 0).any():
                     general_u = np.flatnonzero(ids < 0)
@@ -974,7 +977,7 @@ class GpuAuthMixin:
             if general_u is not None:  # a mixed batch (key churn): the keyed verify, then the rest
                 drop_parts()
                 return self._staged_mixed(msgs, eng, slot, slot_base, ks, ukeys, ids, general_u, scan, spans_buf,
-                                          kid_buf, t0, t1, None if uodd else uflat)
+                                          kid_buf, t0, t1, None if uodd else uflat, (tk, tr))
             ids_b = np.asarray(ids, np.uint32).tobytes()
             spec_hit = parts is not None and parts_ok and spec_u == ids_b and ks.version == ks_version
             if g.speculate and _kid_map is not None and (spec_u != ids_b or g.kid_map is None or
@@ -1033,7 +1036,7 @@ class GpuAuthMixin:
         return verdicts(ok, perf_counter())
 
     def _staged_mixed(self, msgs, eng, slot, slot_base, ks, ukeys, ids, general_u, scan, spans_buf, kid_buf, t0, t1,
-                      uflat=None):
+                      uflat=None, t_keys=None):
         """A staged batch whose identifiers' keys are partly without a built
         table (a signer population larger than the key store): one keyed
         verify of the whole staged batch over the store's ids (the others get
@@ -1076,8 +1079,10 @@ class GpuAuthMixin:
             if handle is not None:  # (the set is freed before the error propagates)
                 eng.verify_staged_collect(handle)
             raise
+        tg = perf_counter()
         if handle is not None:
             ok = np.array(eng.verify_staged_collect(handle), bool)
+        tw = perf_counter()
         if len(gen):
             if getattr(eng, "supports_staged_subset", False):
                 # the staged batch is still in HBM: only the items' indices and key bytes go over
@@ -1090,6 +1095,7 @@ class GpuAuthMixin:
                                                   np.frombuffer(s_off, np.uint64),
                                                   **({"sig_slot": slot} if slot != 64 else {})), bool)
             ok[gen] = okg
+            tv = perf_counter()
             # general-path keys earn a slot by verified requests (short items never verify)
             good = gen[okg & (np.frombuffer(short, np.uint8)[gen] == 0)]
             per_u = np.bincount(uidx[good], minlength=len(ukeys))
@@ -1097,6 +1103,8 @@ class GpuAuthMixin:
             # cannot reach it through the decay: not counted -- the long tail of a churning batch)
             hot_u = np.flatnonzero(per_u >= max(1, g.hot_key_uses // HOT_COUNT_FLOOR)).tolist()
             self._count_verified_keys([ukeys[u] for u in hot_u], per_u[hot_u])
+        else:
+            tv = tw
         t3 = perf_counter()
         g.stats["batches"] += 1
         g.stats["batch_items"] += n
@@ -1105,7 +1113,16 @@ class GpuAuthMixin:
         g.last_breakdown = {"before_scan": (t0 - getattr(g, "t_enter", t0)) * 1e3,
                             "scan_and_copies": (t1 - t0) * 1e3, "keys_and_ids": (t2 - t1) * 1e3,
                             "verify_wait": (t3 - t2) * 1e3, "verdicts": (perf_counter() - t3) * 1e3,
-                            "speculated": False, "general_items": int(len(gen))}
+                            "speculated": False, "general_items": int(len(gen)),
+                            # keys_and_ids' parts: the batch's keys resolved, slots registered, ids
+                            # looked up (and the kid gather); verify_wait's: the general items'
+                            # keys gathered under the keyed verify, its wait, the general
+                            # verify, the verified-use counts
+                            "parts_ms": {k: round(v * 1e3, 3) for k, v in (
+                                (("keys", t_keys[0] - t1), ("register", t_keys[1] - t_keys[0]),
+                                 ("ids", t2 - t_keys[1])) if t_keys else ()) + (
+                                ("gather", tg - t2), ("keyed_wait", tw - tg), ("general", tv - tw),
+                                ("count", t3 - tv))}}
         return results
 
     def _speculation_ready(self):

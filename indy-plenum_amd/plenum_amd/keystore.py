@@ -212,8 +212,11 @@ class KeyStore:
         if len(hit):
             self._used[hit] = self._tick
             self._tick += 1
-        if self._building:
-            ids[np.isin(ids, np.fromiter(self._building, np.int64, len(self._building)))] = -1
+        if self._building:  # (a mask over the slots: np.isin sorted the batch's ~30k ids)
+            building = np.zeros(max(len(self._slot_key), self.capacity, 1), bool)
+            building[np.fromiter(self._building, np.int64, len(self._building))] = True
+            live = ids >= 0
+            ids[live & building[np.where(live, ids, 0)]] = -1
         return ids
 
     def _touch(self, ids):
