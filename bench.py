@@ -662,7 +662,7 @@ def time_node_drain(eng, reqs, idrs, vks, drains=40, per_drain=100, n_nodes=25, 
     return out
 
 
-def time_key_churn(eng, signers=100_000, n=1_000_000, batches=4, zipf=1.1, seed_offset=1 << 20):
+def time_key_churn(eng, signers=100_000, n=1_000_000, batches=4, zipf=1.1, seed_offset=1 << 20, warm=2):
     """end_to_end.key_churn: a domain ledger's signer population through
     GpuAuthNr -- `signers` NYM owners all registered with addIdr
     (node.py:2476-2494), far more than the key store's max_keys slots, and
@@ -671,13 +671,18 @@ def time_key_churn(eng, signers=100_000, n=1_000_000, batches=4, zipf=1.1, seed_
     Keys that verified hot_key_uses requests on the general path earn a slot
     and evict the least-recently-used (asynchronous table builds), so each
     batch reports its rate, its keyed / general shares and the registrations
-    it triggered.  Every outcome is checked after the clock."""
+    it triggered.  `warm` batches of the same stream run first, untimed (the
+    node's steady state: its buffers sized and its hot signers' keys earned;
+    reported as cold_start), then the `batches` timed ones.  Every outcome is
+    checked after the clock."""
     from plenum_amd import _hostpack
     from plenum_amd.base58 import b58encode
     from plenum_amd.client_authn import GpuAuthNr
     pks, sks = eng.seed_keypair_batch(synth.signer_seeds(seed_offset + signers)[seed_offset:])
     idrs = [b58encode(bytes(pk[:16])) for pk in pks]
     vks = ["~" + b58encode(bytes(pk[16:])) for pk in pks]
+    per = n // batches
+    n = per * (batches + warm)  # (the warm-up batches first, then the timed ones: one request stream)
     kidx = synth.zipf_signers(n, signers, zipf)
     msgs, spec = synth.churn_messages(kidx, idrs, alias_len=43, req_id_base=synth.REQ_ID_BASE + (1 << 40))
     buf, off = pack_messages(msgs)
@@ -700,18 +705,20 @@ def time_key_churn(eng, signers=100_000, n=1_000_000, batches=4, zipf=1.1, seed_
         a.addIdr(idr, vk)
     a.keys_settle()  # genesis: the free slots take addIdr keys
     genesis_s = time.perf_counter() - t0
-    per = n // batches
     out_b = []
-    total = 0.0
+    total = cold = 0.0
     bad = 0
-    chunks = [reqs[b * per:(b + 1) * per] for b in range(batches)]  # (the batch lists, made before the clock)
-    for b in range(batches):
+    chunks = [reqs[b * per:(b + 1) * per] for b in range(batches + warm)]  # (the batch lists, made before the clock)
+    for b in range(batches + warm):
         chunk = chunks[b]
         st0 = dict(a.stats)
         t0 = time.perf_counter()
         res = a.authenticate_batch(chunk)
         el = time.perf_counter() - t0
-        total += el
+        if b >= warm:
+            total += el
+        else:
+            cold += el
         st1 = dict(a.stats)
         for j, (r, m) in enumerate(zip(res, chunk)):
             forged = (b * per + j) % 200 == 7
@@ -719,7 +726,7 @@ def time_key_churn(eng, signers=100_000, n=1_000_000, batches=4, zipf=1.1, seed_
         del res
         items = st1["batch_items"] - st0["batch_items"]
         keyed = st1["keyed_items"] - st0["keyed_items"]
-        out_b.append({"requests": per, "value": per / el, "ms": el * 1e3,
+        out_b.append({"requests": per, "value": per / el, "ms": el * 1e3, "timed": b >= warm,
                       "distinct_signers": int(len(np.unique(kidx[b * per:(b + 1) * per]))),
                       "keyed_share": keyed / max(1, items), "general_share": 1 - keyed / max(1, items),
                       "registrations": st1["keys_registered"] - st0["keys_registered"],
@@ -727,14 +734,17 @@ def time_key_churn(eng, signers=100_000, n=1_000_000, batches=4, zipf=1.1, seed_
                                       for k, v in (a._g.last_breakdown or {}).items()}})
         a._g.last_breakdown = None
     ks = a._key_store()
-    return {"signers": signers, "zipf_s": zipf, "requests": per * batches, "batches": out_b,
+    return {"signers": signers, "zipf_s": zipf, "requests": per * batches, "batches": out_b[warm:],
             "value": per * batches / total, "mismatches": int(bad), "key_slots": ks.capacity if ks else 0,
+            "cold_start": {"batches": out_b[:warm], "value": per * warm / cold if warm else None},
             "key_window": a._g.key_window, "genesis_addidr_and_builds_s": genesis_s,
             "note": "%d signers registered with addIdr (more than the %d key slots), requests' signers Zipf(%.1f), "
-                    "%d batches of %d json-decoded requests, 0.5%% forged; keys earn slots by verified use "
-                    "(hot_key_uses) and evict the least-recently-used, tables built asynchronously; value = "
-                    "requests / summed batch seconds; mismatches = outcomes != the construction's (checked after "
-                    "the clock)" % (signers, ks.capacity if ks else 0, zipf, batches, per)}
+                    "%d timed batches of %d json-decoded requests after %d untimed ones of the same stream "
+                    "(cold_start: the authenticator's first batches -- buffers sized, hot keys not yet earned), "
+                    "0.5%% forged; keys earn slots by verified use (hot_key_uses) and evict the "
+                    "least-recently-used, tables built asynchronously; value = timed requests / summed batch "
+                    "seconds; mismatches = outcomes != the construction's, every batch (checked after the clock)"
+                    % (signers, ks.capacity if ks else 0, zipf, batches, per, warm)}
 
 
 def time_e2e_devices(eng, reqs, idrs, vks, counts):

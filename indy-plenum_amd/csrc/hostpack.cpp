@@ -34,6 +34,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <condition_variable>
 #include <functional>
@@ -3108,6 +3109,253 @@ PyObject* py_key_index_get(PyObject*, PyObject* args) {
   return out;
 }
 
+// The promotion policy's decayed verified-use counts (keystore.UseCounts) for 32-byte keys: key ->
+// row (a KeyIndex) and per row the count, the epoch it was last counted at and the add() call that
+// last counted it.  Rows are dense (a freed row is filled from the end).  A churning batch counts
+// ~4k keys: the Python form spent ~2 ms on their dict probes and lists; here one pass over the
+// batch's flat key buffer.
+struct UseTable {
+  KeyIndex idx;
+  std::vector<std::array<uint64_t, 4>> key;
+  std::vector<int64_t> u, e, t;
+  std::vector<uint64_t> mark;  // scratch per row: the call that touched it, its sum, first position
+  std::vector<int64_t> acc;
+  std::vector<Py_ssize_t> first;
+  int64_t tick = 0;
+  uint64_t calls = 0;
+  size_t cap;
+  explicit UseTable(size_t c) : cap(c) {}
+  size_t size() const { return u.size(); }
+  // rows `gone` (distinct) are freed: the live rows past the new end move into the holes, both
+  // in ascending order (the array form's _compact: the two forms keep the same row layout)
+  void remove(std::vector<int64_t>& gone) {
+    std::sort(gone.begin(), gone.end());
+    for (int64_t r : gone) idx.del(key[(size_t)r].data());
+    size_t n = size();
+    std::vector<char> dead(n, 0);
+    for (int64_t r : gone) dead[(size_t)r] = 1;
+    size_t m = n - gone.size();
+    size_t src = m;
+    for (int64_t r : gone) {
+      if ((size_t)r >= m) break;
+      while (dead[src]) ++src;  // the next live row past the new end
+      key[(size_t)r] = key[src];
+      u[(size_t)r] = u[src];
+      e[(size_t)r] = e[src];
+      t[(size_t)r] = t[src];
+      idx.set(key[(size_t)r].data(), r);
+      ++src;
+    }
+    key.resize(m);
+    u.resize(m);
+    e.resize(m);
+    t.resize(m);
+  }
+  // counts[j] verified uses of key j (counts below `floor` are not counted); returns the positions
+  // j whose count reached hot_at, in input order (a key given twice: summed, reported once)
+  std::vector<Py_ssize_t> add(const char* flat, const int64_t* counts, Py_ssize_t m, int64_t floor, int64_t now,
+                              int64_t hot_at) {
+    ++calls;
+    std::vector<int64_t> rows((size_t)m, -1);
+    for (Py_ssize_t j = 0; j < m; ++j) {
+      const int64_t c = counts[j];
+      if (c <= 0 || c < floor) continue;
+      uint64_t w[4];
+      memcpy(w, flat + 32 * j, 32);
+      int64_t r = idx.get(w);
+      if (r < 0) {
+        r = (int64_t)size();
+        idx.set(w, r);
+        key.push_back({w[0], w[1], w[2], w[3]});
+        u.push_back(0);
+        e.push_back(now);
+        t.push_back(0);
+      }
+      if (mark.size() <= (size_t)r) {
+        mark.resize(size() * 2, 0);
+        acc.resize(mark.size());
+        first.resize(mark.size());
+      }
+      if (mark[(size_t)r] != calls) {
+        mark[(size_t)r] = calls;
+        acc[(size_t)r] = 0;
+        first[(size_t)r] = j;
+      }
+      acc[(size_t)r] += c;
+      rows[(size_t)j] = r;
+    }
+    std::vector<Py_ssize_t> out;
+    std::vector<int64_t> hot;
+    for (Py_ssize_t j = 0; j < m; ++j) {
+      const int64_t r = rows[(size_t)j];
+      if (r < 0 || first[(size_t)r] != j) continue;
+      const int64_t sh = std::min<int64_t>(std::max<int64_t>(now - e[(size_t)r], 0), 62);
+      const int64_t v = (u[(size_t)r] >> sh) + acc[(size_t)r];
+      u[(size_t)r] = v;
+      e[(size_t)r] = now;
+      t[(size_t)r] = tick;
+      if (v >= hot_at) {
+        out.push_back(j);
+        hot.push_back(r);
+      }
+    }
+    ++tick;
+    if (!hot.empty()) remove(hot);
+    if (size() > cap) {  // the least recently counted, down to 7/8 of cap
+      const size_t n = size(), drop = std::min(n, n - cap + cap / 8);
+      std::vector<int64_t> order(n);
+      for (size_t r = 0; r < n; ++r) order[r] = (int64_t)r;
+      if (drop < n)  // (ties: the lower row first, as the array form's stable sort)
+        std::nth_element(order.begin(), order.begin() + (Py_ssize_t)drop, order.end(), [&](int64_t a, int64_t b) {
+          return t[(size_t)a] < t[(size_t)b] || (t[(size_t)a] == t[(size_t)b] && a < b);
+        });
+      order.resize(drop);
+      remove(order);
+    }
+    return out;
+  }
+};
+void use_table_free(PyObject* cap) { delete (UseTable*)PyCapsule_GetPointer(cap, "edv.usetable"); }
+UseTable* use_table_of(PyObject* cap) { return (UseTable*)PyCapsule_GetPointer(cap, "edv.usetable"); }
+
+PyObject* py_use_table(PyObject*, PyObject* args) {
+  Py_ssize_t cap;
+  if (!PyArg_ParseTuple(args, "n", &cap)) return nullptr;
+  return PyCapsule_New(new UseTable((size_t)std::max<Py_ssize_t>(cap, 1)), "edv.usetable", use_table_free);
+}
+
+// use_table_add(table, flat, counts, floor, now, hot_at) -> bytes of int64 positions (UseTable::add);
+// flat: 32 m bytes, counts: m int64
+PyObject* py_use_table_add(PyObject*, PyObject* args) {
+  PyObject* cap;
+  Py_buffer bk, bc;
+  long long floor_, now, hot_at;
+  if (!PyArg_ParseTuple(args, "Oy*y*LLL", &cap, &bk, &bc, &floor_, &now, &hot_at)) return nullptr;
+  UseTable* ut = use_table_of(cap);
+  PyObject* ret = nullptr;
+  if (ut && bk.len % 32 == 0 && bc.len == bk.len / 4) {
+    const std::vector<Py_ssize_t> out =
+        ut->add((const char*)bk.buf, (const int64_t*)bc.buf, bk.len / 32, floor_, now, hot_at);
+    std::vector<int64_t> o(out.begin(), out.end());
+    ret = PyBytes_FromStringAndSize((const char*)o.data(), (Py_ssize_t)(8 * o.size()));
+  } else if (ut) {
+    PyErr_SetString(PyExc_ValueError, "use_table_add: 32-byte keys and one int64 count each");
+  }
+  PyBuffer_Release(&bk);
+  PyBuffer_Release(&bc);
+  return ret;
+}
+
+// use_table_pop(table, key32) -> (count, epoch) or None (the key's row freed)
+PyObject* py_use_table_pop(PyObject*, PyObject* args) {
+  PyObject* cap;
+  Py_buffer bk;
+  if (!PyArg_ParseTuple(args, "Oy*", &cap, &bk)) return nullptr;
+  UseTable* ut = use_table_of(cap);
+  PyObject* ret = nullptr;
+  if (ut && bk.len == 32) {
+    uint64_t w[4];
+    memcpy(w, bk.buf, 32);
+    const int64_t r = ut->idx.get(w);
+    if (r < 0) {
+      ret = Py_None;
+      Py_INCREF(ret);
+    } else {
+      ret = Py_BuildValue("(LL)", (long long)ut->u[(size_t)r], (long long)ut->e[(size_t)r]);
+      std::vector<int64_t> gone{r};
+      ut->remove(gone);
+    }
+  } else if (ut) {
+    PyErr_SetString(PyExc_ValueError, "use_table_pop: a 32-byte key");
+  }
+  PyBuffer_Release(&bk);
+  return ret;
+}
+
+PyObject* py_use_table_has(PyObject*, PyObject* args) {
+  PyObject* cap;
+  Py_buffer bk;
+  if (!PyArg_ParseTuple(args, "Oy*", &cap, &bk)) return nullptr;
+  UseTable* ut = use_table_of(cap);
+  PyObject* ret = nullptr;
+  if (ut) {
+    uint64_t w[4] = {0, 0, 0, 0};
+    if (bk.len == 32) memcpy(w, bk.buf, 32);
+    ret = PyBool_FromLong(bk.len == 32 && ut->idx.get(w) >= 0);
+  }
+  PyBuffer_Release(&bk);
+  return ret;
+}
+
+PyObject* py_use_table_len(PyObject*, PyObject* cap) {
+  UseTable* ut = use_table_of(cap);
+  if (!ut) return nullptr;
+  return PyLong_FromSize_t(ut->size());
+}
+
+// general_items(uidx, is_gen, flat) -> (gen, keys): a mixed batch's general-path items -- gen = the
+// positions i (uint32, ascending) whose distinct identifier uidx[i] has is_gen[uidx[i]] != 0, keys
+// = flat's 32-byte key of each, in that order -- on the worker pool (numpy's mask, flatnonzero and
+// row gather took ~1.2 ms for 60k of 250k items)
+PyObject* py_general_items(PyObject*, PyObject* args) {
+  Py_buffer bu, bg, bf;
+  if (!PyArg_ParseTuple(args, "y*y*y*", &bu, &bg, &bf)) return nullptr;
+  PyObject* ret = nullptr;
+  const Py_ssize_t n = bu.len / 4, nu = bg.len;
+  if (bu.len % 4 || bf.len != 32 * nu) {
+    PyErr_SetString(PyExc_ValueError, "general_items: uint32 ids, one flag and one 32-byte key per identifier");
+  } else {
+    const uint32_t* ui = (const uint32_t*)bu.buf;
+    const uint8_t* isg = (const uint8_t*)bg.buf;
+    const char* flat = (const char*)bf.buf;
+    const Py_ssize_t nc = (n + kScanChunk - 1) / kScanChunk;
+    std::vector<Py_ssize_t> cnt((size_t)nc + 1, 0);
+    std::atomic<bool> bad{false};
+    const int t = n >= 32768 ? scan_threads(n, 0) : 1;
+    run_chunks(n, t, [&](int, Py_ssize_t a, Py_ssize_t b) {
+      Py_ssize_t c = 0;
+      for (Py_ssize_t i = a; i < b; ++i) {
+        const uint32_t u = ui[i];
+        if (u >= (uint32_t)nu) {
+          bad.store(true, std::memory_order_relaxed);
+          continue;
+        }
+        c += isg[u] != 0;
+      }
+      cnt[(size_t)(a / kScanChunk) + 1] = c;
+    });
+    if (bad.load()) {
+      PyErr_SetString(PyExc_ValueError, "general_items: an identifier id out of range");
+    } else {
+      for (size_t c = 1; c < cnt.size(); ++c) cnt[c] += cnt[c - 1];
+      const Py_ssize_t m = cnt.back();
+      PyObject* gen = PyBytes_FromStringAndSize(nullptr, 4 * m);
+      PyObject* keys = gen ? PyBytes_FromStringAndSize(nullptr, 32 * m) : nullptr;
+      if (keys) {
+        uint32_t* go = (uint32_t*)PyBytes_AS_STRING(gen);
+        char* ko = PyBytes_AS_STRING(keys);
+        run_chunks(n, t, [&](int, Py_ssize_t a, Py_ssize_t b) {
+          Py_ssize_t at = cnt[(size_t)(a / kScanChunk)];
+          for (Py_ssize_t i = a; i < b; ++i) {
+            const uint32_t u = ui[i];
+            if (!isg[u]) continue;
+            go[at] = (uint32_t)i;
+            memcpy(ko + 32 * at, flat + 32 * (size_t)u, 32);
+            ++at;
+          }
+        });
+        ret = Py_BuildValue("(NN)", gen, keys);
+      } else {
+        Py_XDECREF(gen);
+      }
+    }
+  }
+  PyBuffer_Release(&bu);
+  PyBuffer_Release(&bg);
+  PyBuffer_Release(&bf);
+  return ret;
+}
+
 PyObject* py_gather_items(PyObject*, PyObject* args) {
   Py_buffer bs, bm, bo, bi;
   Py_ssize_t stride = 64;
@@ -3319,6 +3567,14 @@ PyMethodDef kMethods[] = {
     {"key_index_clear", py_key_index_clear, METH_O, "key_index_clear(index)"},
     {"key_index_len", py_key_index_len, METH_O, "key_index_len(index)"},
     {"key_index_get", py_key_index_get, METH_VARARGS, "key_index_get(index, flat) -> int64 ids, -1 absent"},
+    {"use_table", py_use_table, METH_VARARGS, "use_table(cap) -> native decayed use counts of 32-byte keys"},
+    {"general_items", py_general_items, METH_VARARGS,
+     "general_items(uidx_u32, is_gen_u8, flat_keys) -> (positions u32, their 32-byte keys)"},
+    {"use_table_add", py_use_table_add, METH_VARARGS,
+     "use_table_add(table, flat, counts_int64, floor, now, hot_at) -> int64 positions that reached hot_at"},
+    {"use_table_pop", py_use_table_pop, METH_VARARGS, "use_table_pop(table, key32) -> (count, epoch) or None"},
+    {"use_table_has", py_use_table_has, METH_VARARGS, "use_table_has(table, key32) -> bool"},
+    {"use_table_len", py_use_table_len, METH_O, "use_table_len(table)"},
     {"keys_known", py_keys_known, METH_VARARGS,
      "keys_known(clients, fast_keys, identifiers, field) -> (keys, holes): the remembered key of each identifier "
      "whose clients entry still holds the remembered verkey, else None (holes: their positions)"},

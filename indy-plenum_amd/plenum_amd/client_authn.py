@@ -83,6 +83,10 @@ try:  # ... on the scan's worker pool, with the keys as one buffer (key store lo
     from ._hostpack import keys_known_flat as _keys_known_flat
 except ImportError:  # pragma: no cover
     _keys_known_flat = None
+try:  # a mixed batch's general-path items and their keys, on the worker pool
+    from ._hostpack import general_items as _general_items
+except ImportError:  # pragma: no cover
+    _general_items = None
 try:  # the node's per-message path: authenticate()'s host steps in one call; the verify-ahead's dedupe
     from ._hostpack import authn_key as _authn_key, distinct_sm as _distinct_sm
 except ImportError:  # pragma: no cover
@@ -1062,19 +1066,23 @@ class GpuAuthMixin:
         ok = None if handle is not None else np.array(eng.verify_staged(True, kid, slot_base, 0, spans[:n],
                                                                         spans[n:]), bool)
         try:
-            uidx = np.frombuffer(uidx_b, np.uint32)
-            is_gen = np.zeros(len(ukeys), bool)
-            is_gen[general_u] = True
-            gen = np.flatnonzero(is_gen[uidx])
-            gen_keys = None
-            if len(gen):
-                if uflat is not None and len(uflat) == 32 * len(ukeys):
-                    ukey_arr = np.frombuffer(uflat, np.uint8).reshape(-1, 32)  # (the general keys are 32 B)
-                else:
-                    ukey_arr = np.zeros((len(ukeys), 32), np.uint8)
-                    ukey_arr[general_u] = np.frombuffer(b"".join(ukeys[u] for u in general_u),
-                                                        np.uint8).reshape(-1, 32)
-                gen_keys = ukey_arr[uidx[gen]]
+            uidx = np.frombuffer(uidx_b, np.uint32, count=n)
+            is_gen = np.zeros(len(ukeys), np.uint8)
+            is_gen[general_u] = 1
+            if uflat is not None and len(uflat) == 32 * len(ukeys):
+                ukey_flat = uflat  # (the general keys are 32 B)
+            else:
+                ukey_arr = np.zeros((len(ukeys), 32), np.uint8)
+                ukey_arr[general_u] = np.frombuffer(b"".join(ukeys[u] for u in general_u), np.uint8).reshape(-1, 32)
+                ukey_flat = ukey_arr.tobytes()
+            if _general_items is not None:  # (positions and their keys in one parallel pass)
+                gen_b, keys_b = _general_items(uidx, is_gen, ukey_flat)
+                gen = np.frombuffer(gen_b, np.uint32)
+                gen_keys = np.frombuffer(keys_b, np.uint8).reshape(-1, 32)
+            else:
+                gen = np.flatnonzero(is_gen[uidx]).astype(np.uint32)
+                gen_keys = np.frombuffer(ukey_flat, np.uint64).reshape(-1, 4).take(uidx[gen], axis=0).view(
+                    np.uint8).reshape(-1, 32)
         except BaseException:
             if handle is not None:  # (the set is freed before the error propagates)
                 eng.verify_staged_collect(handle)
@@ -1086,7 +1094,7 @@ class GpuAuthMixin:
         if len(gen):
             if getattr(eng, "supports_staged_subset", False):
                 # the staged batch is still in HBM: only the items' indices and key bytes go over
-                okg = np.asarray(eng.verify_staged_subset(gen.astype(np.uint32), gen_keys), bool)
+                okg = np.asarray(eng.verify_staged_subset(gen, gen_keys), bool)
             else:
                 s_sig, s_msg, s_off = _gather_spans(memoryview(sig_o).cast("B")[:slot * n], msg_o, spans_b,
                                                     gen.astype(np.uint32).tobytes(), slot)
@@ -1101,8 +1109,14 @@ class GpuAuthMixin:
             per_u = np.bincount(uidx[good], minlength=len(ukeys))
             # (keys with fewer verified requests in this batch than 1/HOT_COUNT_FLOOR of the threshold
             # cannot reach it through the decay: not counted -- the long tail of a churning batch)
-            hot_u = np.flatnonzero(per_u >= max(1, g.hot_key_uses // HOT_COUNT_FLOOR)).tolist()
-            self._count_verified_keys([ukeys[u] for u in hot_u], per_u[hot_u])
+            floor = max(1, g.hot_key_uses // HOT_COUNT_FLOOR)
+            if uflat is not None and len(uflat) == 32 * len(ukeys) and g.key_uses.native:
+                if g.max_keys > 0:  # the batch's flat key buffer counted natively: no per-key Python
+                    for j in g.key_uses.add_flat(uflat, per_u, self._use_epoch(), g.hot_key_uses, floor).tolist():
+                        g.hot[ukeys[j]] = None
+            else:
+                hot_u = np.flatnonzero(per_u >= floor).tolist()
+                self._count_verified_keys([ukeys[u] for u in hot_u], per_u[hot_u])
         else:
             tv = tw
         t3 = perf_counter()

@@ -35,6 +35,11 @@ try:  # the native mirror of the key -> id map (csrc/hostpack.cpp KeyIndex)
         key_index_clear as _ki_clear, key_index_get as _ki_get
 except ImportError:  # pragma: no cover
     _key_index = None
+try:  # the promotion policy's use counts for 32-byte keys (csrc/hostpack.cpp UseTable)
+    from ._hostpack import use_table as _use_table, use_table_add as _ut_add, use_table_pop as _ut_pop, \
+        use_table_has as _ut_has, use_table_len as _ut_len
+except ImportError:  # pragma: no cover
+    _use_table = None
 
 # comb windows the library builds (edverify.h edv_keys_set_window)
 WINDOWS = (4, 6, 8, 10, 12, 13, 14, 16)
@@ -343,7 +348,82 @@ class KeyStore:
 
 class UseCounts:
     """Decayed verified-use counts of general-path keys, the state of the
-    promotion policy (client_authn.GpuAuthMixin._count_verified_keys): key ->
+    promotion policy (client_authn.GpuAuthMixin._count_verified_keys): a
+    key's count halves per epoch since it was last counted; add() reports the
+    keys whose count reached hot_at (and drops them: they earned a slot);
+    bounded at cap keys, past which the least recently counted are dropped
+    (down to 7/8 of cap).  32-byte keys -- every key a verify can count --
+    live in the native table (csrc/hostpack.cpp UseTable: a batch's ~4k keys
+    counted in one pass over its flat key buffer, add_flat), any other key
+    in the array form (_ArrayUseCounts, the same policy).  pop / len / in
+    behave as on a dict of (count, epoch)."""
+
+    def __init__(self, cap):
+        import threading
+        self.cap = cap
+        self._nat = _use_table(cap) if _use_table is not None else None
+        self._py = _ArrayUseCounts(cap)
+        self._lock = threading.Lock()
+
+    @property
+    def native(self):
+        return self._nat is not None
+
+    def _is_nat(self, key):
+        return self._nat is not None and key.__class__ is bytes and len(key) == 32
+
+    def __len__(self):
+        return (_ut_len(self._nat) if self._nat is not None else 0) + len(self._py)
+
+    def __contains__(self, key):
+        if self._is_nat(key):
+            return _ut_has(self._nat, key)
+        return key in self._py
+
+    def pop(self, key, default=None):
+        if self._is_nat(key):
+            with self._lock:
+                r = _ut_pop(self._nat, key)
+            return default if r is None else r
+        return self._py.pop(key, default)
+
+    def add_flat(self, flat, counts, now, hot_at, floor=1):
+        """add() over 32-byte keys given as one buffer (flat[32 j:32 j + 32]
+        = key j), counts[j] below floor not counted: the positions j of the
+        keys that reached hot_at, in input order (int64 array)."""
+        c = np.ascontiguousarray(counts, np.int64)
+        with self._lock:
+            return np.frombuffer(_ut_add(self._nat, flat, c, int(floor), int(now), int(hot_at)), np.int64)
+
+    def add(self, keys, counts, now, hot_at):
+        """Counts counts[j] verified requests of keys[j] at epoch now.  Returns,
+        in input order, the keys whose count reached hot_at; their counts are
+        dropped (they earned a slot; a later count starts from zero).  A key may
+        appear more than once (two identifiers sharing a verkey): its counts
+        are summed."""
+        if self._nat is None:
+            return self._py.add(keys, counts, now, hot_at)
+        keys = list(keys)
+        counts = np.asarray(counts, np.int64).reshape(-1)
+        nat = [j for j, k in enumerate(keys) if self._is_nat(k)]
+        if len(nat) == len(keys):
+            return [keys[j] for j in self.add_flat(b"".join(keys), counts, now, hot_at).tolist()]
+        # the other keys first: an unhashable one raises before anything of this call is counted
+        oth = [j for j, k in enumerate(keys) if not self._is_nat(k)]
+        hot_o = self._py.add([keys[j] for j in oth], counts[oth], now, hot_at)
+        first = {}
+        for j in oth:
+            first.setdefault(keys[j], j)
+        out = [(first[k], k) for k in hot_o]
+        if nat:
+            pos = self.add_flat(b"".join(keys[j] for j in nat), counts[nat], now, hot_at).tolist()
+            out += [(nat[p], keys[nat[p]]) for p in pos]
+        return [k for _, k in sorted(out, key=lambda x: x[0])]
+
+
+class _ArrayUseCounts:
+    """UseCounts' policy for keys the native table does not take (and its
+    whole form without the native module): key ->
     a row of three arrays (count, the epoch it was last counted at, the call
     that last counted it).  Rows are dense (0 .. len-1; a released row is
     filled from the end), so add() maps a batch's keys to rows with one
@@ -458,7 +538,8 @@ class UseCounts:
                 n -= len(hot_rows)
             if n > self.cap:
                 drop = n - self.cap + self.cap // 8
-                v = np.sort(np.argpartition(self._t[:n], drop - 1)[:drop]) if drop < n else np.arange(n)
+                # (ties: the lower row first -- the native table drops the same rows)
+                v = np.sort(np.argsort(self._t[:n], kind="stable")[:drop]) if drop < n else np.arange(n)
                 for k in self._keys[v].tolist():
                     del row[k]
                 self._compact(v, n)

@@ -1223,6 +1223,39 @@ def test_use_counts_sum_a_repeated_key():
     assert len(uc) == 0 and uc.add([k1], [1], 3, 3) == [] and uc.pop(k1) == (1, 3)
 
 
+def test_use_counts_native_and_array_forms_agree():
+    """UseCounts keeps 32-byte keys in the native table (add_flat over one
+    buffer) and other keys in the array form: a call mixing both reports its
+    hot keys in input order, counts floor-filtered by add_flat, and both forms
+    decay and promote alike."""
+    from plenum_amd.keystore import UseCounts, _ArrayUseCounts
+    import numpy as np
+    uc = UseCounts(1000)
+    if not uc.native:
+        pytest.skip("native module not built")
+    a32, b32, c16 = b"a" * 32, b"b" * 32, b"c" * 16
+    assert uc.add([c16, a32, b32], [3, 3, 1], 0, 3) == [c16, a32]
+    assert len(uc) == 1 and b32 in uc and uc.pop(b32) == (1, 0)
+    # floor: counts below it are not counted at all
+    flat = a32 + b32
+    assert uc.add_flat(flat, np.array([1, 2]), 1, 10, floor=2).tolist() == []
+    assert a32 not in uc and uc.pop(b32) == (2, 1)
+    # random sequences: the native table against the array form
+    rng = np.random.default_rng(5)
+    universe = [bytes(rng.integers(0, 256, 32, dtype=np.uint8)) for _ in range(500)]
+    nat, arr = UseCounts(300), _ArrayUseCounts(300)
+    for step in range(40):
+        now = step // 3
+        idx = rng.choice(len(universe), int(rng.integers(1, 120)))  # (repeats: summed)
+        keys = [universe[i] for i in idx]
+        counts = rng.integers(0, 5, len(keys))
+        h = int(rng.integers(3, 12))
+        assert nat.add(keys, counts, now, h) == arr.add(keys, counts, now, h)
+        assert len(nat) == len(arr)
+    for k in universe:
+        assert nat.pop(k, None) == arr.pop(k, None)
+
+
 def test_keystore_lookup_array_matches_lookup(oracle):
     """KeyStore.lookup_array is lookup() as an array (-1 for None): unregistered keys, keys
     whose asynchronous builds are still queued, repeated keys; both mark the hits used."""

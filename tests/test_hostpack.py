@@ -516,3 +516,24 @@ def test_key_index_matches_a_dict():
     assert list(struct.unpack("<3000q", H.key_index_get(ki, b"".join(ks)))) == list(range(3000))
     with pytest.raises(ValueError):
         H.key_index_get(ki, b"x" * 33)
+
+
+def test_general_items_matches_numpy():
+    """general_items: the positions whose identifier is flagged general, ascending, and each one's
+    32-byte key -- numpy's mask / flatnonzero / row gather, on the worker pool; ids out of range
+    raise."""
+    import numpy as np
+    from plenum_amd._hostpack import general_items
+    rng = np.random.default_rng(3)
+    for n, nu in ((0, 4), (7, 3), (5000, 200), (120000, 9000)):
+        uidx = rng.integers(0, nu, n).astype(np.uint32)
+        isg = (rng.random(nu) < 0.3).astype(np.uint8)
+        flat = rng.integers(0, 256, 32 * nu, dtype=np.uint8).tobytes()
+        g, k = general_items(uidx, isg, flat)
+        gen = np.flatnonzero(isg[uidx])
+        assert np.array_equal(np.frombuffer(g, np.uint32), gen)
+        assert k == np.frombuffer(flat, np.uint8).reshape(-1, 32)[uidx[gen]].tobytes()
+    with pytest.raises(ValueError):
+        general_items(np.array([5], np.uint32), np.zeros(3, np.uint8), bytes(96))
+    with pytest.raises(ValueError):
+        general_items(np.array([0], np.uint32), np.zeros(3, np.uint8), bytes(95))
