@@ -513,12 +513,14 @@ def time_whole_node(eng, args, sets, idrs, vks, dist_on, dev, scan_threads):
                          "speculated_share": (st2.get("speculated", 0) - st1.get("speculated", 0)) / (n * K),
                          "yield_ms": {"p50": float(np.median(pipe_per)) * 1e3, "min": min(pipe_per) * 1e3,
                                       "max": max(pipe_per) * 1e3} if pipe_per else None,
+                         "each_ms": [round(x * 1e3, 2) for x in pipe_per],
                          "in_batch_ms": {k: (round(v, 3) if isinstance(v, float) else v)
                                          for k, v in ((pipe_parts[pmed] if pmed is not None else None) or {}).items()},
                          "mismatches": bad_pipe},
            "synchronous": {"value": n * K / el_sync, "ms_per_batch": el_sync / K * 1e3, "seconds": el_sync,
                            "batch_ms": {"p50": float(np.median(per)) * 1e3, "min": min(per) * 1e3,
                                         "max": max(per) * 1e3},
+                           "each_ms": [round(x * 1e3, 2) for x in per],
                            "speculated_share": (st1.get("speculated", 0) - st0.get("speculated", 0)) / (n * K),
                            "in_batch_ms": {k: (round(v, 3) if isinstance(v, float) else v)
                                            for k, v in (parts[med] or {}).items()},
