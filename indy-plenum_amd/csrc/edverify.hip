@@ -1044,13 +1044,44 @@ __device__ bool r_decode_part2(fe& x, RDecode& d, const uint32_t s[8]) {
 #ifndef EDV_SMALL_LANES
 #define EDV_SMALL_LANES 1
 #endif
+// EDV_SMALL_DIST_EDGES 1 (default): the products before the chain (u, v, v^3, u v^7) and after it
+// (x, v x^2) distributed too -- ~0.17 us each on the wave against ~0.37 us on lane 0 -- with u - 1
+// formed as u + 2p - 1 and carried back into the dist_* input bounds; 0: on lane 0 (A/B).
+#ifndef EDV_SMALL_DIST_EDGES
+#define EDV_SMALL_DIST_EDGES 1
+#endif
 struct RDecodeL {
-  fe y, u, v, v3, uv7;      // lane 0
+  fe y, u, v, v3, uv7;      // lane 0 (EDV_SMALL_DIST_EDGES 0); y in every lane
   uint32_t t0, t1, t2;      // distributed (limb k in lane k)
+  uint32_t du, dv, dv3, duv7;  // distributed (EDV_SMALL_DIST_EDGES 1)
 };
+// limb k of a lane-uniform fe in lane k (every lane holds f; no cross-lane moves)
+__device__ __forceinline__ uint32_t dist_pick(const fe& f, uint32_t k) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) r = k == (uint32_t)i ? f.v[i] : r;
+  return r;
+}
 __device__ void r_decode_part1_lanes(RDecodeL& d, const uint32_t s[8], uint32_t lane) {
   fe z;
   fe_0(z);
+#if EDV_SMALL_DIST_EDGES
+  const uint32_t k = lane & 15;
+  const LaneTerms sq = c_lane_sq.t[lane], mu = c_lane_mul.t[lane];
+  fe_frombytes(d.y, s);  // (every lane: the same words)
+  const bool row0 = lane < 10;
+  const uint32_t yd = dist_form(k < 10 ? dist_pick(d.y, k) : 0u, lane);
+  const uint32_t y2 = dist_sq(yd, sq, lane);
+  // v = d y^2 + 1 (limb 0 of a dist_* output < 2^26: the + 1 stays in bounds)
+  const uint32_t dd = dist_form(k < 10 ? dist_pick(fe_const_d(), k) : 0u, lane);
+  d.dv = dist_mul(y2, dd, mu, lane) + dist_form(k == 0 ? 1u : 0u, lane);
+  // u = y^2 - 1 = y^2 + 2p - 1, carried: limbs of 2p are 2^27 - 38, then 2^26 - 2 / 2^27 - 2
+  const uint32_t two_p = k == 0 ? (1u << 27) - 38 : (k & 1) ? (1u << 26) - 2 : (1u << 27) - 2;
+  d.du = lane_cols_carry(row0 ? (uint64_t)y2 + two_p - (lane == 0 ? 1u : 0u) : 0ull, lane);
+  d.dv3 = dist_mul(dist_sq(d.dv, sq, lane), d.dv, mu, lane);
+  d.duv7 = dist_mul(dist_mul(dist_sq(d.dv3, sq, lane), d.dv, mu, lane), d.du, mu, lane);  // u v^7
+  const uint32_t zd = d.duv7;
+#else
   if (lane == 0) {
     fe one, x;
     fe_1(one);
@@ -1070,42 +1101,63 @@ __device__ void r_decode_part1_lanes(RDecodeL& d, const uint32_t s[8], uint32_t 
   const uint32_t k = lane & 15;
   const LaneTerms sq = c_lane_sq.t[lane], mu = c_lane_mul.t[lane];
   const uint32_t zd = dist_from_lane0(z, lane);
-  uint32_t t0 = dist_sq(zd, sq, k);
-  uint32_t t1 = dist_sqn(t0, 2, sq, k);
-  t1 = dist_mul(zd, t1, mu, k);
-  t0 = dist_mul(t0, t1, mu, k);
-  t0 = dist_sq(t0, sq, k);
-  t0 = dist_mul(t1, t0, mu, k);
-  t1 = dist_sqn(t0, 5, sq, k);
-  t0 = dist_mul(t1, t0, mu, k);
-  t1 = dist_sqn(t0, 10, sq, k);
-  t1 = dist_mul(t1, t0, mu, k);
-  uint32_t t2 = dist_sqn(t1, 20, sq, k);
-  t1 = dist_mul(t2, t1, mu, k);
-  t1 = dist_sqn(t1, 10, sq, k);
-  t0 = dist_mul(t1, t0, mu, k);
-  t1 = dist_sqn(t0, 50, sq, k);
-  t1 = dist_mul(t1, t0, mu, k);
-  d.t2 = dist_sqn(t1, 30, sq, k);
+#endif
+  uint32_t t0 = dist_sq(zd, sq, lane);
+  uint32_t t1 = dist_sqn(t0, 2, sq, lane);
+  t1 = dist_mul(zd, t1, mu, lane);
+  t0 = dist_mul(t0, t1, mu, lane);
+  t0 = dist_sq(t0, sq, lane);
+  t0 = dist_mul(t1, t0, mu, lane);
+  t1 = dist_sqn(t0, 5, sq, lane);
+  t0 = dist_mul(t1, t0, mu, lane);
+  t1 = dist_sqn(t0, 10, sq, lane);
+  t1 = dist_mul(t1, t0, mu, lane);
+  uint32_t t2 = dist_sqn(t1, 20, sq, lane);
+  t1 = dist_mul(t2, t1, mu, lane);
+  t1 = dist_sqn(t1, 10, sq, lane);
+  t0 = dist_mul(t1, t0, mu, lane);
+  t1 = dist_sqn(t0, 50, sq, lane);
+  t1 = dist_mul(t1, t0, mu, lane);
+  d.t2 = dist_sqn(t1, 30, sq, lane);
   d.t0 = t0;
   d.t1 = t1;
 }
 // every lane of the wave calls; lane 0's x and result are r_decode_part2's
 __device__ bool r_decode_part2_lanes(fe& x, RDecodeL& d, const uint32_t s[8], uint32_t lane) {
-  const uint32_t k = lane & 15;
   const LaneTerms sq = c_lane_sq.t[lane], mu = c_lane_mul.t[lane];
-  uint32_t t2 = dist_sqn(d.t2, 70, sq, k);
-  uint32_t t1 = dist_mul(t2, d.t1, mu, k);
-  t1 = dist_sqn(t1, 50, sq, k);
-  uint32_t t0 = dist_mul(t1, d.t0, mu, k);
-  t0 = dist_sqn(t0, 2, sq, k);
+  uint32_t t2 = dist_sqn(d.t2, 70, sq, lane);
+  uint32_t t1 = dist_mul(t2, d.t1, mu, lane);
+  t1 = dist_sqn(t1, 50, sq, lane);
+  uint32_t t0 = dist_mul(t1, d.t0, mu, lane);
+  t0 = dist_sqn(t0, 2, sq, lane);
+  fe vxx, chk;
+#if EDV_SMALL_DIST_EDGES
+  // x = u v^3 (u v^7)^((p-5)/8), then v x^2, on the wave; lane 0 takes x, v x^2 and u
+  uint32_t xd = dist_mul(dist_mul(dist_mul(t0, d.duv7, mu, lane), d.dv3, mu, lane), d.du, mu, lane);
+  const uint32_t vxxd = dist_mul(dist_sq(xd, sq, lane), d.dv, mu, lane);
+  fe u;
+  dist_to_fe(x, xd);  // class C, in every lane
+  dist_to_fe(vxx, vxxd);
+  dist_to_fe(u, d.du);
+  if (lane != 0) return false;
+  fe_sub(chk, vxx, u);
+  if (!fe_iszero(chk)) {
+    fe_add(chk, vxx, u);
+    if (!fe_iszero(chk)) return false;
+    fe_mul_o<kSO>(x, x, fe_const_sqrtm1());
+  }
+  if (fe_isnegative(x) != (s[7] >> 31)) {
+    fe_neg(x, x);
+    fe_carry(x);
+  }
+  return true;
+#else
   fe pw;
   dist_to_fe(pw, t0);  // (u v^7)^((p-5)/8), class C, in every lane
   if (lane != 0) return false;
   fe_mul_o<kSO>(x, pw, d.uv7);
   fe_mul_o<kSO>(x, x, d.v3);
   fe_mul_o<kSO>(x, x, d.u);   // u v^3 (u v^7)^((p-5)/8)
-  fe vxx, chk;
   fe_sq_o<kSO>(vxx, x);
   fe_mul_o<kSO>(vxx, vxx, d.v);
   fe_sub(chk, vxx, d.u);
@@ -1119,6 +1171,7 @@ __device__ bool r_decode_part2_lanes(fe& x, RDecodeL& d, const uint32_t s[8], ui
     fe_carry(x);
   }
   return true;
+#endif
 }
 
 // verify_phase_hash for the single-request kernel: SHA-512(R || A || M) with the blocks' message

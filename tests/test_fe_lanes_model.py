@@ -1,8 +1,8 @@
 """csrc/fe_lanes.h's lane-distributed GF(2^255 - 19) square and product (edv_verify_small_kernel
 and edv_resident_kernel decode R with them) modelled on the CPU lane by lane: the per-lane term
 table (make_lane_tab), the 32-bit operand scalings, the 64-bit column sums of the four rows, and
-lane_cols_carry's one-exchange carry (EDV_LANE_CARRY 1: a_k + b_{k-1} + d_{k-2}, x19 past 2^255,
-limb 0's excess into limb 1).  Every intermediate is checked against the machine width it lives
+lane_cols_carry's one-exchange carry (EDV_LANE_CARRY 1 and 2 -- ds_bpermute or DPP row moves, the
+same arithmetic: a_k + b_{k-1} + d_{k-2}, x19 past 2^255, limb 0's excess into limb 1).  Every intermediate is checked against the machine width it lives
 in, and every result against exact arithmetic mod p, over long chains that start from limbs at
 the stated output bounds -- the bound argument of fe_lanes.h, executed."""
 import random
