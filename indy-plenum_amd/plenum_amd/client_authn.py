@@ -405,9 +405,10 @@ class GpuAuthMixin:
             key = self._key_of(identifier, verkey)
             if not key:  # nacl_wrappers.py:237-238: no key -> False
                 raise InvalidSignature
-            hit = g.verdicts.get((key, sm))
+            vk = (key, sm)
+            hit = g.verdicts.get(vk)
             if hit is None:
-                hit = self._verify_prepared(_Prepared(identifier, sm[:64], sm[64:], key))
+                hit = self._verify_miss(identifier, key, sm, vk)
             else:
                 g.stats["cache_hits"] += 1
             if not hit:
@@ -648,6 +649,30 @@ class GpuAuthMixin:
             epochs[0][1] -= 1
             if epochs[0][1] <= 0:
                 epochs.popleft()
+
+    def _verify_miss(self, identifier, key, sm, vk):
+        """_verify_prepared for authenticate()'s miss of the verdict cache (the
+        cache key vk = (key, sm) already looked up): the steady state's
+        registered, built key straight to the one-request launch with sm's two
+        halves as views (no copies, no second lookup), else _verify_prepared."""
+        g = self._g
+        eng = g.engine
+        if (len(sm) >= 64 and not g.hot and not g.pending and eng is not None
+                and hasattr(eng, "verify_one_keyed") and g.max_keys > 0):
+            with _engine_lock(eng):
+                ks = self._key_store()
+                kid = ks.lookup_one(key) if ks is not None else None
+                if kid is not None:
+                    g.stats["single_verifies"] += 1
+                    mv = memoryview(sm)
+                    ok = bool(eng.verify_one_keyed(mv[:64], kid, mv[64:]))
+                    st = g.stats
+                    st["batches"] += 1
+                    st["batch_items"] += 1
+                    st["keyed_items"] += 1
+                    self._remember(None, ok, vk)
+                    return ok
+        return self._verify_prepared(_Prepared(identifier, sm[:64], sm[64:], key))
 
     def _verify_prepared(self, p):
         if not p.key:  # nacl_wrappers.py:237-238: no key -> False
