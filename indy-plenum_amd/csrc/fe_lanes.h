@@ -87,6 +87,20 @@ template <int kCtrl>
 __device__ __forceinline__ uint32_t lane_dpp(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kCtrl, 0xf, 0xf, false);
 }
+// EDV_LANE_SCALE 1: no quarter-rate v_mul_lo_u32 on the chain -- 19 x as two v_lshl_add_u32 (the
+// compiler folds shift-adds back into a multiply, hence the asm), the operands' x2 / x4 as shifts,
+// their x19 selected per lane, limb 0's excess into limb 1 by a DPP row move instead of
+// v_readlane.  Measured slower: the single-request kernel 62.4-63.6 against 50.1-51.0 us
+// (profiles/r10s); 0 (default): the v_mul_lo forms
+#ifndef EDV_LANE_SCALE
+#define EDV_LANE_SCALE 0
+#endif
+__device__ __forceinline__ uint32_t lane_mul19(uint32_t x) {
+  uint32_t t, r;
+  asm("v_lshl_add_u32 %0, %1, 4, %1" : "=v"(t) : "v"(x));
+  asm("v_lshl_add_u32 %0, %1, 1, %2" : "=v"(r) : "v"(x), "v"(t));
+  return r;
+}
 __device__ __forceinline__ uint32_t lane_cols_carry(uint64_t p, uint32_t lane) {
   const uint32_t k = lane & 15;
   uint32_t lo = (uint32_t)p, hi = (uint32_t)(p >> 32);
@@ -114,9 +128,15 @@ __device__ __forceinline__ uint32_t lane_cols_carry(uint64_t p, uint32_t lane) {
   const uint32_t src1 = k == 0 ? 9 : k - 1, src2 = k >= 2 ? k - 2 : k + 8;
   const uint32_t bb = lane_bperm(src1, b), dd = lane_bperm(src2, d);
 #endif
+#if EDV_LANE_SCALE
+  const uint32_t r = a + (k == 0 ? lane_mul19(bb) : bb) + (k <= 1 ? lane_mul19(dd) : dd);
+  const uint32_t c0 = lane_dpp<0x111>(r >> 26);  // lane 1 <- lane 0
+  const uint32_t out = k == 0 ? (r & ((1u << 26) - 1)) : k == 1 ? r + c0 : r;
+#else
   const uint32_t r = a + bb * m1 + dd * m2;
   const uint32_t c0 = (uint32_t)__builtin_amdgcn_readlane((int)(r >> 26), 0);
   const uint32_t out = k == 0 ? (r & ((1u << 26) - 1)) : k == 1 ? r + c0 : r;
+#endif
 #else
   const uint32_t w = (k & 1) ? 25 : 26, mask = (1u << w) - 1, src = k == 0 ? 9 : k - 1, m = k == 0 ? 19 : 1;
   const uint64_t c = p >> w;
@@ -139,6 +159,11 @@ __device__ __forceinline__ uint32_t dist_sq(uint32_t f, const LaneTerms& t, uint
   const uint32_t a1 = lane_bperm(t.ia[1], f) << t.sa[1], b1 = lane_bperm(t.ib[1], f);
   uint64_t p = (uint64_t)a0 * b0;
   p += (uint64_t)a1 * b1;
+#elif EDV_LANE_SCALE  // (an empty slot: ma = 0 -- its a-side operand zeroed by the select)
+  const uint32_t a0 = lane_bperm(t.ia[0], f), b0 = lane_bperm(t.ib[0], f);
+  const uint32_t a1 = lane_bperm(t.ia[1], f), b1 = lane_bperm(t.ib[1], f);
+  uint64_t p = (uint64_t)(t.ma[0] ? a0 << t.sa[0] : 0u) * (t.mb[0] == 19 ? lane_mul19(b0) : b0);
+  p += (uint64_t)(t.ma[1] ? a1 << t.sa[1] : 0u) * (t.mb[1] == 19 ? lane_mul19(b1) : b1);
 #else
   const uint32_t a0 = lane_bperm(t.ia[0], f), b0 = lane_bperm(t.ib[0], f);
   const uint32_t a1 = lane_bperm(t.ia[1], f), b1 = lane_bperm(t.ib[1], f);
@@ -160,6 +185,9 @@ __device__ __forceinline__ uint32_t dist_mul(uint32_t f, uint32_t g, const LaneT
 #if EDV_LANE_FORM
     const uint32_t a = lane_bperm(t.ia[s], f) << t.sa[s], b = lane_bperm(t.ib[s], g);
     p += (uint64_t)a * b;
+#elif EDV_LANE_SCALE
+    const uint32_t a = lane_bperm(t.ia[s], f), b = lane_bperm(t.ib[s], g);
+    p += (uint64_t)(t.ma[s] ? a << t.sa[s] : 0u) * (t.mb[s] == 19 ? lane_mul19(b) : b);
 #else
     const uint32_t a = lane_bperm(t.ia[s], f), b = lane_bperm(t.ib[s], g);
     p += (uint64_t)(a * t.ma[s]) * (b * t.mb[s]);
