@@ -1304,7 +1304,7 @@ __device__ unsigned long long g_small_prof[10];  // [8], [9]: the shader clock a
 struct SmallShared {
   uint64_t sw[kHashPass * kHashRow];  // wave 0's message schedules (verify_phase_hash_lanes)
   uint32_t h[8];
-  uint32_t xr[10], yr[10];  // R decoded (wave 2)
+  uint32_t xr[10];  // R decoded (wave 2; its y: wave 0 reads the bytes itself)
   uint32_t base[40];        // [S]B (wave 1): X, Y, Z, T
   int ok_hash, ok_r;
 };
@@ -1387,7 +1387,6 @@ __device__ __forceinline__ bool small_verify(SmallShared& sh, const uint32_t sig
 #endif
       const bool zero_signed = (sig[7] >> 31) && fe_iszero(x);
       store_fe(sh.xr, x);
-      store_fe(sh.yr, rd.y);
       sh.ok_r = (dec && is_canonical_point(sig) && !zero_signed) ? 1 : 0;
       EDV_SP(5);
     }
@@ -1411,6 +1410,7 @@ __device__ __forceinline__ bool small_verify(SmallShared& sh, const uint32_t sig
     EDV_SP(6);
   }
   ge_p2 Q;
+  bool ok_y = false;
   if (wave == 0 && lane == 0) {  // R' while wave 2 still decodes R ([S]B is in LDS since the first barrier)
     ge_p3 B;
     load_fe(B.X, sh.base);
@@ -1422,18 +1422,21 @@ __device__ __forceinline__ bool small_verify(SmallShared& sh, const uint32_t sig
     ge_p3_to_cached<kSO>(c, B);
     ge_add<kSO>(t, P, c);
     ge_p1p1_to_p2_addlike<kSO>(Q, t);  // R' = [h](-A) + [S]B, classes C
+    // Y' = y_R Z' needs only R's bytes (y_R as r_decode reads it): checked here, while wave 2 still
+    // decodes, so one product follows the last barrier, not two
+    fe yr, u, d;
+    fe_frombytes(yr, sig);
+    fe_mul_o<kSO>(u, yr, Q.Z);
+    fe_sub(d, Q.Y, u);
+    ok_y = fe_iszero(d);
   }
   __syncthreads();  // R's decode (wave 2) done
   if (wave != 0 || lane != 0) return false;
-  fe xr, yr, u, d;
+  fe xr, u, d;
   load_fe(xr, sh.xr);
-  load_fe(yr, sh.yr);
   fe_mul_o<kSO>(u, xr, Q.Z);
   fe_sub(d, Q.X, u);  // X' - x_R Z'  (L)
-  bool ok = sh.ok_hash && sh.ok_r && fe_iszero(d);
-  fe_mul_o<kSO>(u, yr, Q.Z);
-  fe_sub(d, Q.Y, u);
-  ok = ok && fe_iszero(d);
+  const bool ok = ok_y && sh.ok_hash && sh.ok_r && fe_iszero(d);
   EDV_SP(7);
 #if EDV_SMALL_PROFILE
   if (blockIdx.x == 0) g_small_prof[9] = __builtin_amdgcn_s_memtime();
