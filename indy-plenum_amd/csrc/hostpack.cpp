@@ -1947,6 +1947,9 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
     size_t ncand = 0;
     for (const WorkerIdrs& w : tabs) ncand += w.obj.size();
     const int P = ncand >= 8192 ? t : 1;  // (a small batch merges on this thread: no helper wake-ups)
+    // an identifier's partition from its hash's high half by a multiply (h % P was a 64-bit division
+    // per worker entry per partition: ~1.6 ms of a churning batch's merge); the low bits index the tables
+    const auto part_of = [P](uint64_t h) -> Py_ssize_t { return (Py_ssize_t)(((h >> 32) * (uint64_t)P) >> 32); };
     struct Part {
       IdrTable tab;
       std::vector<PyObject*> obj;
@@ -1964,7 +1967,7 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
           const WorkerIdrs& tb = tabs[(size_t)w];
           for (size_t u = 0; u < tb.obj.size(); ++u) {
             const uint64_t h = tb.hash[u];
-            if ((Py_ssize_t)(h % (uint64_t)P) != p) continue;
+            if (part_of(h) != p) continue;
             PyObject* o = tb.obj[u];
             bool fresh = false;
             // the worker's copy of the text when it is short (no cache miss on the object), else its data
@@ -2002,12 +2005,19 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
       // many distinct identifiers (a churning batch: ~30k of 250k items): their first occurrences
       // are distinct positions of the batch, so a scatter into a position table and one pass over
       // it orders them in O(n) -- the comparison sort took ~1.5 ms
-      std::vector<uint32_t> at((size_t)n, 0xffffffffu);
-      for (uint32_t c = 0; c < (uint32_t)cand.size(); ++c) at[(size_t)cand[c].first] = c;
+      // (a bitmap of the positions taken -- n / 8 bytes zeroed, not n words -- and the
+      // position -> candidate table left uninitialised: only the marked entries are read)
+      std::unique_ptr<uint32_t[]> at(new uint32_t[(size_t)n]);
+      std::vector<uint64_t> mark(((size_t)n + 63) / 64, 0);
+      for (uint32_t c = 0; c < (uint32_t)cand.size(); ++c) {
+        const size_t f = (size_t)cand[c].first;
+        at[f] = c;
+        mark[f >> 6] |= 1ull << (f & 63);
+      }
       std::vector<Cand> sorted;
       sorted.reserve(cand.size());
-      for (Py_ssize_t i = 0; i < n; ++i)
-        if (at[(size_t)i] != 0xffffffffu) sorted.push_back(cand[at[(size_t)i]]);
+      for (size_t wi = 0; wi < mark.size(); ++wi)
+        for (uint64_t m = mark[wi]; m; m &= m - 1) sorted.push_back(cand[at[(wi << 6) + (size_t)__builtin_ctzll(m)]]);
       cand.swap(sorted);
     } else {
       std::sort(cand.begin(), cand.end(), [](const Cand& a, const Cand& b) { return a.first < b.first; });
@@ -2023,7 +2033,7 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
       for (Py_ssize_t w = a; w < b; ++w) {
         const WorkerIdrs& tb = tabs[(size_t)w];
         std::vector<uint32_t>& tg = to_global[(size_t)w];
-        for (size_t u = 0; u < tg.size(); ++u) tg[u] = parts[(size_t)(tb.hash[u] % (uint64_t)P)].gid[tg[u]];
+        for (size_t u = 0; u < tg.size(); ++u) tg[u] = parts[(size_t)part_of(tb.hash[u])].gid[tg[u]];
       }
     }, 1);
     // the GIL pass (3) below adds the deferred items' identifiers to this table

@@ -537,3 +537,24 @@ def test_general_items_matches_numpy():
         general_items(np.array([5], np.uint32), np.zeros(3, np.uint8), bytes(96))
     with pytest.raises(ValueError):
         general_items(np.array([0], np.uint32), np.zeros(3, np.uint8), bytes(95))
+
+
+def test_scan_many_distinct_identifiers_first_occurrence_order():
+    """A churning batch's shape: ~15k distinct identifiers in 40k requests (the merge's hash
+    partitions on the workers, the first occurrences ordered through the position bitmap): uniq
+    is the identifiers in order of first occurrence and uidx maps every request to its own --
+    equal to the one-thread scan and to Python's dict.fromkeys order."""
+    r = random.Random(5)
+    n, distinct = 40000, 15000
+    msgs = []
+    for i in range(n):
+        k = i if i < distinct else r.randrange(distinct)
+        msgs.append({"identifier": "D%07d" % ((k * 7919) % 1000003), "reqId": i,
+                     "operation": {"type": "1", "alias": "a" * (i % 5)},
+                     "signature": b58encode(bytes(r.getrandbits(8) for _ in range(64)))})
+    r.shuffle(msgs)
+    fu, uidx, uniq, *rest = H.scan_batch_u(msgs, ["signature"], 8)
+    assert H.scan_batch_u(msgs, ["signature"], 1) == (fu, uidx, uniq, *rest)
+    assert uniq == list(dict.fromkeys(m["identifier"] for m in msgs))
+    u = struct.unpack("<%dI" % n, uidx)
+    assert all(uniq[u[i]] == msgs[i]["identifier"] for i in range(n))
