@@ -1340,30 +1340,7 @@ void run_chunks(Py_ssize_t n, int t, F&& f, Py_ssize_t chunk = kScanChunk) {
 // ~600 MB of newly mapped memory per call (page faults on first touch, unmaps
 // on free), which measured ~25 % of the scan.  The scan holds the GIL from
 // start to end, so calls never overlap.
-struct alignas(64) WorkerIdrs {  // a cache line (or more) of its own per worker
-  IdrTable slot;
-  std::vector<PyObject*> obj;
-  std::vector<uint32_t> kid;      // speculation: the key id of each of its identifiers (kmap)
-  std::vector<Py_ssize_t> first;  // the item where the worker met it first
-  std::vector<uint64_t> hash;     // IdrTable::hash of each of its identifiers (the merge's partitions)
-  std::vector<char> txt;          // the first IdrTable::kInl bytes of each (the merge compares these)
-  std::vector<uint32_t> tlen;     // and its length
-  size_t deferred = 0;            // items left for the GIL pass (3)
-#ifdef EDV_HAVE_DK
-  std::unique_ptr<ShapeCache> shapes;  // this call's remembered dict shapes (shaped_dict)
-#endif
-};
-struct MergePart {  // one hash partition of the merge of the workers' identifier tables
-  IdrTable tab;
-  std::vector<PyObject*> obj;
-  std::vector<Py_ssize_t> first;
-  std::vector<uint32_t> kid;
-  std::vector<uint32_t> gid;
-};
 struct ScanScratch {
-  std::vector<WorkerIdrs> tabs;
-  std::vector<MergePart> parts;
-  size_t tab_hint = 1024, part_hint = 64;  // the last call's largest worker table / partition
   std::vector<ScanItem> it;
   std::vector<PyObject*> idr_of;
   std::vector<ScanBuf> bufs;
@@ -1684,26 +1661,27 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
     b.sig.clear();
     b.ser.clear();
   }
-  // the workers' identifier tables, kept in the scratch with their capacity and sized from the
-  // previous call (a churning batch's ~10k identifiers per worker grew each table from 1k slots
-  // through four rehashes into freshly mapped memory, call after call)
-  std::vector<WorkerIdrs>& tabs = S.tabs;
-  tabs.resize((size_t)t);
+  struct alignas(64) WorkerIdrs {  // a cache line (or more) of its own per worker
+    IdrTable slot;
+    std::vector<PyObject*> obj;
+    std::vector<uint32_t> kid;      // speculation: the key id of each of its identifiers (kmap)
+    std::vector<Py_ssize_t> first;  // the item where the worker met it first
+    std::vector<uint64_t> hash;     // IdrTable::hash of each of its identifiers (the merge's partitions)
+    std::vector<char> txt;          // the first IdrTable::kInl bytes of each (the merge compares these)
+    std::vector<uint32_t> tlen;     // and its length
+    size_t deferred = 0;            // items left for the GIL pass (3)
+#ifdef EDV_HAVE_DK
+    std::unique_ptr<ShapeCache> shapes;  // this call's remembered dict shapes (shaped_dict)
+#endif
+  };
+  std::vector<WorkerIdrs> tabs((size_t)t);
   // remembered dict shapes (shaped_dict); EDV_SCAN_SHAPES=0: wser_dict for every request (A/B)
   const char* shape_env = getenv("EDV_SCAN_SHAPES");
   const bool shapes = g_scan_direct_env() && !(shape_env && shape_env[0] == '0');
   for (WorkerIdrs& w : tabs) {
-    // (at most the items a worker gets: a small batch after a large one zeroes a small table)
-    w.slot.reset(std::min<size_t>(std::max<size_t>(1024, S.tab_hint), (size_t)(n / t) + 64));
-    w.obj.clear();
-    w.kid.clear();
-    w.first.clear();
-    w.hash.clear();
-    w.txt.clear();
-    w.tlen.clear();
-    w.deferred = 0;
+    w.slot.reset(1024);
 #ifdef EDV_HAVE_DK
-    w.shapes.reset(shapes ? new ShapeCache : nullptr);
+    if (shapes) w.shapes.reset(new ShapeCache);
 #endif
   }
   // the signature output (n slots) is sized before the scan: in slot mode the workers write an
@@ -1972,19 +1950,19 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
     // an identifier's partition from its hash's high half by a multiply (h % P was a 64-bit division
     // per worker entry per partition: ~1.6 ms of a churning batch's merge); the low bits index the tables
     const auto part_of = [P](uint64_t h) -> Py_ssize_t { return (Py_ssize_t)(((h >> 32) * (uint64_t)P) >> 32); };
-    std::vector<MergePart>& parts = S.parts;
-    parts.resize((size_t)P);
-    const size_t part_expect = std::min<size_t>(
-        std::max<size_t>(tabs.empty() ? 64 : tabs[0].obj.size() / (size_t)P + 64, S.part_hint), ncand / (size_t)P + 64);
+    struct Part {
+      IdrTable tab;
+      std::vector<PyObject*> obj;
+      std::vector<Py_ssize_t> first;
+      std::vector<uint32_t> kid;
+      std::vector<uint32_t> gid;
+    };
+    std::vector<Part> parts((size_t)P);
     for (int w = 0; w < t; ++w) to_global[(size_t)w].resize(tabs[(size_t)w].obj.size());
     run_chunks(P, P, [&](int, Py_ssize_t a, Py_ssize_t b) {
       for (Py_ssize_t p = a; p < b; ++p) {
-        MergePart& pt = parts[(size_t)p];  // (P = 1: the one partition, serially)
-        pt.tab.reset(part_expect);
-        pt.obj.clear();
-        pt.first.clear();
-        pt.kid.clear();
-        pt.gid.clear();
+        Part& pt = parts[(size_t)p];  // (P = 1: the one partition, serially)
+        pt.tab.reset(tabs.empty() ? 64 : tabs[0].obj.size() / (size_t)P + 64);
         for (int w = 0; w < t; ++w) {
           const WorkerIdrs& tb = tabs[(size_t)w];
           for (size_t u = 0; u < tb.obj.size(); ++u) {
@@ -2019,7 +1997,7 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
     };
     std::vector<Cand> cand;
     for (int p = 0; p < P; ++p) {
-      MergePart& pt = parts[(size_t)p];
+      Part& pt = parts[(size_t)p];
       pt.gid.resize(pt.obj.size());
       for (size_t l = 0; l < pt.obj.size(); ++l) cand.push_back(Cand{pt.first[l], p, (uint32_t)l});
     }
@@ -2046,7 +2024,7 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
     }
     uniq.reserve(cand.size());
     for (const Cand& c : cand) {
-      MergePart& pt = parts[(size_t)c.p];
+      Part& pt = parts[(size_t)c.p];
       pt.gid[c.local] = (uint32_t)uniq.size();
       uniq.push_back(pt.obj[c.local]);
       if (kmap) spec_u.push_back(pt.kid[c.local]);
@@ -2065,9 +2043,6 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
                        (uint32_t)g, fresh);
     }
   }
-  S.tab_hint = S.part_hint = 0;  // the next call's table sizes
-  for (const WorkerIdrs& w : tabs) S.tab_hint = std::max(S.tab_hint, w.obj.size());
-  for (const MergePart& pt : S.parts) S.part_hint = std::max(S.part_hint, pt.obj.size());
   // (the items' worker-local ids are mapped in (4), on the workers)
   auto t_p2 = now();
   // (3) the items the workers left (non-ASCII identifiers, floats / big ints /
