@@ -1906,12 +1906,13 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
       }
       idr_of[(size_t)i] = iv;
       bool fresh = false;
-      x.uid = tab.slot.find_or_add((const char*)PyUnicode_1BYTE_DATA(iv), (size_t)PyUnicode_GET_LENGTH(iv),
-                                   (uint32_t)tab.obj.size(), fresh);
+      const uint64_t ih = IdrTable::hash((const char*)PyUnicode_1BYTE_DATA(iv), (size_t)PyUnicode_GET_LENGTH(iv));
+      x.uid = tab.slot.find_or_add_h(ih, (const char*)PyUnicode_1BYTE_DATA(iv), (size_t)PyUnicode_GET_LENGTH(iv),
+                                     (uint32_t)tab.obj.size(), fresh);
       if (fresh) {
         tab.obj.push_back(iv);
         tab.first.push_back(i);
-        tab.hash.push_back(IdrTable::hash((const char*)PyUnicode_1BYTE_DATA(iv), (size_t)PyUnicode_GET_LENGTH(iv)));
+        tab.hash.push_back(ih);  // (computed once: the table's probe and the merge's partition)
         {
           const size_t tn = (size_t)PyUnicode_GET_LENGTH(iv), at = tab.txt.size();
           tab.txt.resize(at + IdrTable::kInl);
