@@ -58,6 +58,7 @@ from copy import deepcopy
 from typing import Dict
 
 from .base58 import b58decode
+from . import exceptions as _exc
 from .exceptions import (CouldNotAuthenticate, EmptyIdentifier, EmptySignature, InsufficientCorrectSignatures,
                          InsufficientSignatures, InvalidSignature, InvalidSignatureFormat, MissingIdentifier,
                          MissingSignature, SigningException, UnknownIdentifier)
@@ -129,6 +130,21 @@ REQ_ID = 'reqId'
 VERKEY = 'verkey'
 
 
+def _invalid_signatures(nf):
+    """nf fresh InvalidSignature() instances.  With this package's own exception classes (no
+    reference plenum importable) the constructor only records identifier = reqId = None, so the
+    instances are made by BaseException.__new__ (args ()) and that one dict update -- a third of
+    the constructor's cost for a batch's ~1k forgeries; the reference's classes are constructed."""
+    if nf < 64 or _exc.REFERENCE:
+        return [InvalidSignature() for _ in range(nf)]
+    new, cls = InvalidSignature.__new__, InvalidSignature
+    attrs = {"identifier": None, "reqId": None}
+    out = [new(cls) for _ in range(nf)]
+    for e in out:
+        e.__dict__.update(attrs)
+    return out
+
+
 def _results_failing(ok, short, uidx_b, uniq):
     """_results_ok with a fresh InvalidSignature at every failing item (verdict False or a short
     signature), the exceptions made BEFORE the result list exists (hostpack.cpp results_ok: made
@@ -136,7 +152,7 @@ def _results_failing(ok, short, uidx_b, uniq):
     import numpy as np
     okb = np.frombuffer(ok, np.uint8) if not isinstance(ok, np.ndarray) else ok.view(np.uint8)
     nf = int(np.count_nonzero((okb == 0) | (np.frombuffer(short, np.uint8) != 0)))
-    fails = [InvalidSignature() for _ in range(nf)]
+    fails = _invalid_signatures(nf)
     results, failed = _results_ok(ok, short, uidx_b, uniq, fails)
     if len(failed) != nf:  # (never expected: the native pass left None at its failures)
         for i in failed:

@@ -1393,3 +1393,19 @@ def test_batch_calls_pause_and_restore_the_collector(oracle, monkeypatch):
         assert not gc.isenabled()
     finally:
         gc.enable()
+
+
+def test_fast_invalid_signatures_equal_constructed_ones():
+    """_invalid_signatures builds a batch's many InvalidSignature instances without the
+    constructor when the classes are this package's: each equals a constructed one in class, args,
+    attributes, cause and str, and each is a distinct object."""
+    from plenum_amd import client_authn as ca
+    from plenum_amd.exceptions import InvalidSignature
+    got = ca._invalid_signatures(300)
+    ref = InvalidSignature()
+    assert len({id(e) for e in got}) == 300
+    for e in got:
+        assert type(e) is InvalidSignature and e.args == ref.args and e.__dict__ == ref.__dict__
+        assert e.__cause__ is None and e.__context__ is None and str(e) == str(ref)
+        assert e.code == ref.code and e.reason == ref.reason
+    assert len(ca._invalid_signatures(3)) == 3
