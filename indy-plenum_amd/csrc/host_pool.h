@@ -89,6 +89,7 @@ class HostPool {
         t = w;  // fewer helpers: workers 0..w-1 (run_chunks' shared counter covers every item)
         break;
       }
+      if (have_aff_) (void)pthread_setaffinity_np(th_.back().native_handle(), sizeof aff_, &aff_);
       const char* pin_env = getenv("EDV_SCAN_PIN");
       if (pin_env && pin_env[0] == '1') {
         const std::vector<int> cpus = worker_cpus(w + 1);
@@ -112,6 +113,18 @@ class HostPool {
     job_ = nullptr;
     lk.unlock();
     if (err) std::rethrow_exception(err);
+  }
+  // Every helper's CPU set (best effort; EDV_SCAN_NUMA: the NUMA node the batch's objects live on)
+  void set_affinity(const cpu_set_t& set) {
+    std::unique_lock<std::mutex> busy(run_mu_);
+    std::lock_guard<std::mutex> lk(mu_);
+    for (std::thread& x : th_) (void)pthread_setaffinity_np(x.native_handle(), sizeof set, &set);
+    aff_ = set;
+    have_aff_ = true;
+  }
+  bool same_affinity(const cpu_set_t& set) {
+    std::lock_guard<std::mutex> lk(mu_);
+    return have_aff_ && CPU_EQUAL(&aff_, &set);
   }
   static HostPool& get() {
     static std::mutex m;
@@ -146,6 +159,8 @@ class HostPool {
   const std::function<void(int)>* job_ = nullptr;
   uint64_t gen_ = 0;
   int active_ = 0, pending_ = 0;
+  cpu_set_t aff_;
+  bool have_aff_ = false;
 };
 
 }  // namespace
