@@ -1340,7 +1340,9 @@ void run_chunks(Py_ssize_t n, int t, F&& f, Py_ssize_t chunk = kScanChunk) {
 // EDV_SCAN_NUMA=1 (A/B): the scan's helper threads run on the CPUs of the NUMA node that holds
 // the batch's request objects (the node of the pages of three sampled dicts, get_mempolicy), so a
 // batch built on another node than the helpers happened to run on is not walked across the
-// socket link.  The calling thread is left where it is.
+// socket link.  The calling thread is left where it is.  Measured slower on the GPU box (2 x EPYC
+// 9575F, NPS1, a 16-CPU quota over 256 CPUs): 39.0-48.5 against 49.1-50.6 M/s whole node
+// (profiles/r10y) -- off by default.
 inline int numa_node_cpus(int node, cpu_set_t& set) {
   char path[96];
   snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
