@@ -996,7 +996,7 @@ class GpuAuthMixin:
             g.msg_bytes_per_item = max(g.msg_bytes_per_item * 0.5, float(staged_bytes) / n if n else 0.0)
             # authenticate():93-99, once per identifier (on the worker pool; the keys also as one buffer)
             ukeys, uflat, uodd, all_keys = self._keys_for_flat(uniq)
-            tk = perf_counter()
+            tk = g.t_ids_of = perf_counter()
             ids = None
             general_u = None  # distinct identifiers whose key has no built table: the general path
             tr = tk
@@ -1004,6 +1004,7 @@ class GpuAuthMixin:
                 pre = None
                 if g.hot or g.pending:  # (the batch's keys pinned by id: one native lookup)
                     pre = ks.ids_of(uflat, uodd, ukeys) if g.hot else None
+                    g.t_ids_of = perf_counter()
                     v0 = ks.version
                     got = self._register_waiting(ks, ukeys, pre)
                     if got or ks.version != v0:
@@ -1175,6 +1176,7 @@ class GpuAuthMixin:
                             # verify, the verified-use counts
                             "parts_ms": {k: round(v * 1e3, 3) for k, v in (
                                 (("keys", t_keys[0] - t1), ("register", t_keys[1] - t_keys[0]),
+                                 ("ids_of", max(0.0, getattr(g, "t_ids_of", t_keys[0]) - t_keys[0])),
                                  ("ids", t2 - t_keys[1])) if t_keys else ()) + (
                                 ("gather", tg - t2), ("keyed_wait", tw - tg), ("general", tv - tw),
                                 ("count", t3 - tv))}}
