@@ -679,7 +679,7 @@ def time_node_drain(eng, reqs, idrs, vks, drains=40, per_drain=100, n_nodes=25, 
     return out
 
 
-def time_key_churn(eng, signers=100_000, n=1_000_000, batches=4, zipf=1.1, seed_offset=1 << 20, warm=2):
+def time_key_churn(eng, signers=100_000, n=1_000_000, batches=4, zipf=1.1, seed_offset=1 << 20, warm=3):
     """end_to_end.key_churn: a domain ledger's signer population through
     GpuAuthNr -- `signers` NYM owners all registered with addIdr
     (node.py:2476-2494), far more than the key store's max_keys slots, and
