@@ -151,7 +151,9 @@ def _results_failing(ok, short, uidx_b, uniq):
     after it, their allocations let the collector's young-generation passes walk the fresh list)."""
     import numpy as np
     okb = np.frombuffer(ok, np.uint8) if not isinstance(ok, np.ndarray) else ok.view(np.uint8)
-    nf = int(np.count_nonzero((okb == 0) | (np.frombuffer(short, np.uint8) != 0)))
+    # (a pass is ok 1 and short 0, i.e. ok > short on the 0/1 bytes: one comparison over the batch,
+    # not two plus an OR -- 1.6 against 0.26 ms per 1M on the CPU)
+    nf = len(okb) - int(np.count_nonzero(okb > np.frombuffer(short, np.uint8, count=len(okb))))
     fails = _invalid_signatures(nf)
     results, failed = _results_ok(ok, short, uidx_b, uniq, fails)
     if len(failed) != nf:  # (never expected: the native pass left None at its failures)
