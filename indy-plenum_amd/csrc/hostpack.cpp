@@ -1981,6 +1981,7 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
     if (copier.failed) staged_ok = false;
   }
   auto t_p1 = now();
+  auto t_m1 = t_p1, t_m2 = t_p1;  // (the merge's partition pass / ordering / remap, EDV_SCAN_PROFILE)
   // (2) the workers' identifier tables merged into the batch's, in order of
   // first occurrence in the batch (the single-thread order, whichever worker
   // took which chunk)
@@ -2042,6 +2043,7 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
         }
       }
     }, 1);
+    t_m1 = now();
     struct Cand {
       Py_ssize_t first;
       int p;
@@ -2081,6 +2083,7 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
       uniq.push_back(pt.obj[c.local]);
       if (kmap) spec_u.push_back(pt.kid[c.local]);
     }
+    t_m2 = now();
     run_chunks(t, P > 1 ? t : 1, [&](int, Py_ssize_t a, Py_ssize_t b) {  // each worker's table, side by side
       for (Py_ssize_t w = a; w < b; ++w) {
         const WorkerIdrs& tb = tabs[(size_t)w];
@@ -2204,8 +2207,11 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
     }
     if (prof) {
       auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
-      fprintf(stderr, "scan (staged): n=%zd threads=%d  workers %.0f us, merge %.0f us, bookkeeping %.0f us\n", n, t,
-              us(t_start, t_p1), us(t_p1, t_p2), us(t_p3, now()));
+      fprintf(stderr,
+              "scan (staged): n=%zd threads=%d  workers %.0f us, merge %.0f us (partitions %.0f, order %.0f, remap "
+              "%.0f), bookkeeping %.0f us\n",
+              n, t, us(t_start, t_p1), us(t_p1, t_p2), us(t_p1, t_m1), us(t_m1, t_m2), us(t_m2, t_p2),
+              us(t_p3, now()));
     }
     // speculation: the key id used per distinct identifier (uint32 bytes), or None; parts_ok: every
     // part's kernels were queued
@@ -2256,8 +2262,11 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
     }
     if (prof) {
       auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
-      fprintf(stderr, "scan: n=%zd threads=%d  workers %.0f us, merge %.0f us, under the GIL %.0f us, pack %.0f us\n",
-              n, t, us(t_start, t_p1), us(t_p1, t_p2), us(t_p2, t_p3), us(t_p3, now()));
+      fprintf(stderr,
+              "scan: n=%zd threads=%d  workers %.0f us, merge %.0f us (partitions %.0f, order %.0f, remap %.0f), under "
+              "the GIL %.0f us, pack %.0f us\n",
+              n, t, us(t_start, t_p1), us(t_p1, t_p2), us(t_p1, t_m1), us(t_m1, t_m2), us(t_m2, t_p2), us(t_p2, t_p3),
+              us(t_p3, now()));
     }
     if (unique_form) {
       PyObject* ul = PyList_New((Py_ssize_t)uniq.size());
