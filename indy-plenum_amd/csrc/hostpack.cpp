@@ -1281,27 +1281,29 @@ inline void pf(const void* p) { __builtin_prefetch(p); }
 inline void pf_lines(const void* p, int n) {
   for (int k = 0; k < n; ++k) __builtin_prefetch((const char*)p + 64 * k);
 }
+// (K scales every distance: EDV_SCAN_PF=2 or 3 prefetches two or three times as far ahead, A/B)
+template <int K = 1>
 inline void prefetch_ahead(PyObject** items, Py_ssize_t i, Py_ssize_t b) {
-  if (i + 10 < b) pf(items[i + 10]);
-  if (i + 7 < b) {
-    PyObject* o = items[i + 7];
+  if (i + 10 * K < b) pf(items[i + 10 * K]);
+  if (i + 7 * K < b) {
+    PyObject* o = items[i + 7 * K];
     if (Py_TYPE(o) == &PyDict_Type) pf_lines(((PyDictObject*)o)->ma_keys, 3);
   }
 #ifdef EDV_HAVE_DK
   Py_ssize_t n;
-  if (i + 4 < b)
-    if (const DkEntry* e = dk_entries(items[i + 4], n))
+  if (i + 4 * K < b)
+    if (const DkEntry* e = dk_entries(items[i + 4 * K], n))
       for (Py_ssize_t j = 0; j < n; ++j)
         if (e[j].v) {
           pf(e[j].k);
           pf_lines(e[j].v, 2);
         }
-  if (i + 2 < b)
-    if (const DkEntry* e = dk_entries(items[i + 2], n))
+  if (i + 2 * K < b)
+    if (const DkEntry* e = dk_entries(items[i + 2 * K], n))
       for (Py_ssize_t j = 0; j < n; ++j)
         if (e[j].v && Py_TYPE(e[j].v) == &PyDict_Type) pf_lines(((PyDictObject*)e[j].v)->ma_keys, 3);
-  if (i + 1 < b)
-    if (const DkEntry* e = dk_entries(items[i + 1], n))
+  if (i + K < b)
+    if (const DkEntry* e = dk_entries(items[i + K], n))
       for (Py_ssize_t j = 0; j < n; ++j) {
         Py_ssize_t n2;
         if (e[j].v)
@@ -1874,6 +1876,8 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
   // turns it off
   const char* pf_env = getenv("EDV_SCAN_PREFETCH");
   const bool prefetch = !(pf_env && pf_env[0] == '0');
+  const char* pfs_env = getenv("EDV_SCAN_PF");  // the distances' scale (A/B): 1 (default), 2, 3
+  const int pf_scale = pfs_env ? atoi(pfs_env) : 1;
   const char* dir_env = getenv("EDV_SCAN_DIRECT");
   g_scan_direct = !(dir_env && dir_env[0] == '0');
   // non-temporal stores for what only the DMA reads: the staged scan's slots and messages
@@ -1890,7 +1894,14 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
       x = ScanItem{};
       idr_of[(size_t)i] = nullptr;
       if (kid_out) kid_out[i] = 0xffffffffu;
-      if (prefetch) prefetch_ahead(items, i, b);
+      if (prefetch) {
+        if (pf_scale == 2)
+          prefetch_ahead<2>(items, i, b);
+        else if (pf_scale == 3)
+          prefetch_ahead<3>(items, i, b);
+        else
+          prefetch_ahead<1>(items, i, b);
+      }
       if (!PyDict_CheckExact(m)) continue;
       // one pass over the request's keys: its signing serialization (kept if the item stays on
       // the fast path) and the signature and identifier values
