@@ -2060,39 +2060,59 @@ PyObject* scan_impl_body(PyObject* args, bool unique_form, PyRefs& refs) {
       int p;
       uint32_t local;
     };
-    std::vector<Cand> cand;
-    for (int p = 0; p < P; ++p) {
-      Part& pt = parts[(size_t)p];
-      pt.gid.resize(pt.obj.size());
-      for (size_t l = 0; l < pt.obj.size(); ++l) cand.push_back(Cand{pt.first[l], p, (uint32_t)l});
-    }
-    if (cand.size() > 4096 && (Py_ssize_t)cand.size() * 16 > n) {
-      // many distinct identifiers (a churning batch: ~30k of 250k items): their first occurrences
-      // are distinct positions of the batch, so a scatter into a position table and one pass over
-      // it orders them in O(n) -- the comparison sort took ~1.5 ms
-      // (a bitmap of the positions taken -- n / 8 bytes zeroed, not n words -- and the
-      // position -> candidate table left uninitialised: only the marked entries are read)
-      std::unique_ptr<uint32_t[]> at(new uint32_t[(size_t)n]);
-      std::vector<uint64_t> mark(((size_t)n + 63) / 64, 0);
-      for (uint32_t c = 0; c < (uint32_t)cand.size(); ++c) {
-        const size_t f = (size_t)cand[c].first;
-        at[f] = c;
-        mark[f >> 6] |= 1ull << (f & 63);
-      }
-      std::vector<Cand> sorted;
-      sorted.reserve(cand.size());
-      for (size_t wi = 0; wi < mark.size(); ++wi)
-        for (uint64_t m = mark[wi]; m; m &= m - 1) sorted.push_back(cand[at[(wi << 6) + (size_t)__builtin_ctzll(m)]]);
-      cand.swap(sorted);
+    size_t ncand_u = 0;
+    for (int p = 0; p < P; ++p) ncand_u += parts[(size_t)p].obj.size();
+    if (P > 1 && ncand_u > 4096) {
+      // many distinct identifiers (a churning batch: ~30k of 250k items), ordered on the workers: the
+      // batch's positions cut into P ranges, worker r takes from every partition the identifiers
+      // first met in range r and sorts them; a prefix sum over the ranges' counts gives each its
+      // global number.  (Ordered on one thread -- a comparison sort, a position bitmap or a radix
+      // sort alike -- it took ~2 ms: the partitions' arrays were written by the other cores.)
+      uniq.resize(ncand_u);
+      if (kmap) spec_u.resize(ncand_u);
+      std::vector<std::vector<Cand>> by_range((size_t)P);
+      std::vector<size_t> base((size_t)P + 1, 0);
+      const auto range_of = [n, P](Py_ssize_t f) { return (int)((uint64_t)f * (uint64_t)P / (uint64_t)n); };
+      run_chunks(P, P, [&](int, Py_ssize_t ra, Py_ssize_t rb) {
+        for (Py_ssize_t r = ra; r < rb; ++r) {
+          std::vector<Cand>& mine = by_range[(size_t)r];
+          for (int p = 0; p < P; ++p) {
+            const Part& pt = parts[(size_t)p];
+            for (size_t l = 0; l < pt.first.size(); ++l)
+              if (range_of(pt.first[l]) == (int)r) mine.push_back(Cand{pt.first[l], p, (uint32_t)l});
+          }
+          std::sort(mine.begin(), mine.end(), [](const Cand& x, const Cand& y) { return x.first < y.first; });
+        }
+      }, 1);
+      for (int r = 0; r < P; ++r) base[(size_t)r + 1] = base[(size_t)r] + by_range[(size_t)r].size();
+      for (int p = 0; p < P; ++p) parts[(size_t)p].gid.resize(parts[(size_t)p].obj.size());
+      run_chunks(P, P, [&](int, Py_ssize_t ra, Py_ssize_t rb) {
+        for (Py_ssize_t r = ra; r < rb; ++r) {
+          size_t g = base[(size_t)r];
+          for (const Cand& c : by_range[(size_t)r]) {
+            Part& pt = parts[(size_t)c.p];
+            pt.gid[c.local] = (uint32_t)g;
+            uniq[g] = pt.obj[c.local];
+            if (kmap) spec_u[g] = pt.kid[c.local];
+            ++g;
+          }
+        }
+      }, 1);
     } else {
-      std::sort(cand.begin(), cand.end(), [](const Cand& a, const Cand& b) { return a.first < b.first; });
-    }
-    uniq.reserve(cand.size());
-    for (const Cand& c : cand) {
-      Part& pt = parts[(size_t)c.p];
-      pt.gid[c.local] = (uint32_t)uniq.size();
-      uniq.push_back(pt.obj[c.local]);
-      if (kmap) spec_u.push_back(pt.kid[c.local]);
+      std::vector<Cand> cand;
+      for (int p = 0; p < P; ++p) {
+        Part& pt = parts[(size_t)p];
+        pt.gid.resize(pt.obj.size());
+        for (size_t l = 0; l < pt.obj.size(); ++l) cand.push_back(Cand{pt.first[l], p, (uint32_t)l});
+      }
+      std::sort(cand.begin(), cand.end(), [](const Cand& x, const Cand& y) { return x.first < y.first; });
+      uniq.reserve(cand.size());
+      for (const Cand& c : cand) {
+        Part& pt = parts[(size_t)c.p];
+        pt.gid[c.local] = (uint32_t)uniq.size();
+        uniq.push_back(pt.obj[c.local]);
+        if (kmap) spec_u.push_back(pt.kid[c.local]);
+      }
     }
     t_m2 = now();
     run_chunks(t, P > 1 ? t : 1, [&](int, Py_ssize_t a, Py_ssize_t b) {  // each worker's table, side by side
